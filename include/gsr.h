@@ -1,0 +1,174 @@
+/*
+ * gsr.h — C ABI of the MI355X (gfx950) Gaussian-splatting rasterizer (libgsr.so).
+ *
+ * Drop-in boundary: this library replaces the native arithmetic behind
+ * pose-splatter's renderer plugin (src/gaussian_renderer.py):
+ *
+ *   - 3D: the gsplat extension called by GaussianRenderer3D.render
+ *         (src/gaussian_renderer.py:196-208 → gsplat.rendering.rasterization, packed=False,
+ *         classic mode).  Each entry point below replaces one gsplat stage:
+ *           gsr3d_project_fwd   ← fully_fused_projection (fwd)
+ *           gsr_bin_offsets     ← isect_tiles (counting) + isect_offset_encode
+ *           gsr_bin_sort        ← isect_tiles (key emission) + cub radix sort
+ *           gsr3d_raster_fwd    ← rasterize_to_pixels (fwd)
+ *           gsr3d_raster_bwd    ← rasterize_to_pixels (bwd)
+ *           gsr3d_project_bwd   ← fully_fused_projection (bwd) + the adapter's autograd
+ *                                  (exp / quat-normalise / clamp / sigmoid,
+ *                                   src/gaussian_renderer.py:190-193)
+ *   - 2D: the dense PyTorch compositor GaussianRenderer2D._render_vectorized
+ *         (src/gaussian_renderer.py:336-427) and its autograd backward, re-expressed as a
+ *         tiled, index-ordered compositor:  gsr2d_project_fwd / gsr_bin_* (index order) /
+ *         gsr2d_raster_fwd / gsr2d_raster_bwd / gsr2d_project_bwd.
+ *
+ * Conventions
+ *   - Plain pointers to DEVICE memory; the caller (PyTorch's caching allocator) owns all
+ *     memory.  The library allocates nothing and frees nothing.  Inputs are read-only.
+ *   - Every call enqueues on the caller's stream (a hipStream_t passed as void*); no call
+ *     synchronises the device.  The only host read the caller needs is gsr_bin_stats
+ *     (filled on the device by gsr_bin_offsets, 16 bytes) to size the intersection buffers.
+ *   - Return 0 on success; negative on failure (GSR_E*).  gsr_last_error() returns a
+ *     thread-local message for the last failure of the calling thread.  No C++ exception
+ *     crosses the ABI.
+ *   - fp32 arithmetic throughout; 32-bit indices (I < 2^31 intersections per call).
+ *
+ * Splat record (written by *_project_fwd, read by binning and rasterisation):
+ *   12 floats (48 B) per (camera c, Gaussian n), at rec[(c*N + n)*12]:
+ *     [0]=x [1]=y  screen-space mean (pixels)      [2]=opacity   [3]=depth (3D) / 0 (2D)
+ *     [4]=a [5]=b [6]=c  exponent  sigma = a*dx^2 + b*dx*dy + c*dy^2,  d = mean - pixel
+ *     [7]=0
+ *     [8..10]=rgb (activated colour)                [11]=0
+ *   rect: 2 uint32 per (c,n): {x0 | x1<<16, y0 | y1<<16}, tiles [x0,x1) x [y0,y1).
+ *
+ * Per-entry gradient partials (written by *_raster_bwd, reduced by *_project_bwd):
+ *   9 floats per sorted intersection s:  d/dx, d/dy, d/da, d/db, d/dc, d/dopacity, d/drgb[3]
+ *   (summed over the 16x16 tile's pixels) — a deterministic replacement for float atomics.
+ */
+#ifndef GSR_H
+#define GSR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSR_OK 0
+#define GSR_EINVAL -1     /* bad shape / argument                                   */
+#define GSR_ELAUNCH -2    /* HIP launch failure                                     */
+#define GSR_ECAPACITY -3  /* caller buffer / workspace too small                     */
+
+#define GSR_TILE 16
+#define GSR_RADIUS_OPACITY_AABB 0      /* gsplat >= 1.5: per-axis, opacity-aware extent */
+#define GSR_RADIUS_ISOTROPIC_3SIGMA 1  /* gsplat <= 1.4: ceil(3*sqrt(lambda_max))       */
+#define GSR_ORDER_DEPTH 0              /* 3D: per-tile list ordered by (depth, c*N+n)   */
+#define GSR_ORDER_INDEX 1              /* 2D: per-tile list ordered by parameter index  */
+
+typedef struct gsr_bin_stats {
+  int64_t n_isect;     /* total (Gaussian, tile) intersections I                     */
+  int32_t max_seg;     /* longest per-tile list                                       */
+  int32_t n_busy;      /* tiles with a non-empty list                                 */
+} gsr_bin_stats;
+
+int gsr_version(void);
+const char* gsr_last_error(void);
+
+/* ---------------------------------------------------------------- (a) projection */
+
+/* 3D projection (+ adapter activations fused).  params: [N, >=14] fp32 rows with
+ * row_stride floats (layout src/gaussian_renderer.py:183-187); viewmats [C,4,4] world->cam
+ * row-major; Ks [C,3,3].  Writes rec [C*N*12], rect [C*N*2], isect_count [C*N] and
+ * ACCUMULATES into tile_count [C*tiles] (caller zeroes it).  Culled Gaussians get count 0. */
+int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride,
+                      const float* viewmats, const float* Ks, int C, int width, int height,
+                      float near_plane, float far_plane, float radius_clip, float eps2d,
+                      int radius_mode, float* rec, uint32_t* rect, int32_t* isect_count,
+                      int32_t* tile_count, void* stream);
+
+/* 2D projection: params [N, >=9] (layout src/gaussian_renderer.py:314-318).  The tile rect
+ * covers every pixel where opacity*exp(-q) >= eps_cut (the reference is dense; eps_cut
+ * bounds the dropped mass).  Same outputs as gsr3d_project_fwd with C = 1. */
+int gsr2d_project_fwd(const float* params, int64_t N, int64_t row_stride, int width,
+                      int height, float eps_cut, float* rec, uint32_t* rect,
+                      int32_t* isect_count, int32_t* tile_count, void* stream);
+
+/* ---------------------------------------------------------------- (b) binning */
+
+/* Workspace for gsr_bin_offsets, bytes. */
+size_t gsr_bin_offsets_workspace(int64_t CN, int64_t CT);
+
+/* Exclusive scans: isect_offset [CN] (per-Gaussian emission offsets), tile_offset [CT+1],
+ * busy_tiles [CT] (indices of non-empty tiles, ascending), stats (device). */
+int gsr_bin_offsets(const int32_t* isect_count, int64_t CN, const int32_t* tile_count,
+                    int64_t CT, void* workspace, size_t workspace_bytes,
+                    int32_t* isect_offset, int32_t* tile_offset, int32_t* busy_tiles,
+                    gsr_bin_stats* stats, void* stream);
+
+/* Workspace for gsr_bin_sort, bytes (depends on the I read back from stats). */
+size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT);
+
+/* Emit (tile, key) pairs and sort each tile's list in LDS.  Outputs:
+ *   sorted_ids [I]: c*N+n per sorted entry (what the rasterizer reads),
+ *   isect_pos  [I]: for emission slot isect_offset[cn]+j (j = row-major index of the tile in
+ *                   the Gaussian's rect) the sorted position s.
+ * order: GSR_ORDER_DEPTH (3D) or GSR_ORDER_INDEX (2D).  max_seg/n_busy from stats. */
+int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_offset,
+                 const int32_t* tile_offset, const int32_t* busy_tiles, int C, int64_t N,
+                 int width, int height, int order, int64_t n_isect, int32_t max_seg,
+                 int32_t n_busy, void* workspace, size_t workspace_bytes,
+                 int32_t* sorted_ids, int32_t* isect_pos, void* stream);
+
+/* ---------------------------------------------------------------- (c) rasterisation */
+
+/* Front-to-back compositing (gsplat classic), one workgroup per 16x16 tile.
+ * bg [C,3].  Outputs rgb [C,H,W,3], alpha [C,H,W], final_T [C,H,W] (exact transmittance,
+ * kept for the backward), last [C,H,W] (index of the last contributing sorted entry, -1
+ * if none), tile_end [CT] (1 + max last over the tile, or the tile's start). */
+int gsr3d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
+                     int C, int width, int height, const float* bg, float* rgb, float* alpha,
+                     float* final_T, int32_t* last, int32_t* tile_end, void* stream);
+
+/* Backward of gsr3d_raster_fwd.  v_rgb [C,H,W,3], v_alpha [C,H,W] (contiguous).
+ * Writes partial [I*9] for every sorted entry s in [tile start, tile_end). */
+int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
+                     const int32_t* tile_end, const int32_t* busy_tiles, int32_t n_busy,
+                     int C, int width, int height, const float* bg, const float* final_T,
+                     const int32_t* last, const float* v_rgb, const float* v_alpha,
+                     float* partial, void* stream);
+
+/* 2D index-order compositor (src/gaussian_renderer.py:416-425), integer pixel centres.
+ * rgb = canvas + (1-A)*bg, alpha = A.  Same outputs as the 3D call (final_T = 1-A unused). */
+int gsr2d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
+                     int width, int height, const float* bg, float* rgb, float* alpha,
+                     int32_t* last, int32_t* tile_end, void* stream);
+
+/* Workspace for gsr2d_raster_bwd (transmittance checkpoints), bytes. */
+size_t gsr2d_raster_bwd_workspace(int64_t n_isect, int64_t CT);
+
+int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
+                     const int32_t* tile_end, const int32_t* busy_tiles, int32_t n_busy,
+                     int width, int height, const float* bg, const int32_t* last,
+                     const float* v_rgb, const float* v_alpha, void* workspace,
+                     size_t workspace_bytes, float* partial, void* stream);
+
+/* ---------------------------------------------------------------- projection backward */
+
+/* Reduce the per-entry partials of each (c,n), chain through projection and the adapter
+ * activations, sum over cameras: v_params [N,14] (fully overwritten, deterministic). */
+int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride,
+                      const float* viewmats, const float* Ks, int C, int width, int height,
+                      float eps2d, const uint32_t* rect, const int32_t* isect_offset,
+                      const int32_t* isect_count, const int32_t* isect_pos,
+                      const int32_t* tile_end, const float* partial, float* v_params,
+                      void* stream);
+
+int gsr2d_project_bwd(const float* params, int64_t N, int64_t row_stride, int width,
+                      int height, const uint32_t* rect, const int32_t* isect_offset,
+                      const int32_t* isect_count, const int32_t* isect_pos,
+                      const int32_t* tile_end, const float* partial, float* v_params,
+                      void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSR_H */

@@ -1,0 +1,335 @@
+// (b) Tile binning: per-Gaussian / per-tile exclusive scans, emission of (tile, key) pairs
+// into per-tile buckets, and a per-tile sort of the keys in LDS.
+//
+// gsplat (isect_tiles + cub DeviceRadixSort over 64-bit (camera|tile|depth) keys) is
+// restated as an MSD counting pass on the tile digit (the buckets come from the tile
+// histogram written by projection) followed by an LDS-resident bitonic sort of each
+// bucket's 64-bit (depth-bits << 32 | c*N+n) keys — the same total order a stable radix
+// sort of gsplat's keys over emission order produces (ties in depth → ascending c*N+n),
+// without a global multi-pass radix sort over HBM.  2D uses key = n (parameter order).
+#include "gsr_common.h"
+
+namespace gsr {
+
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 16;
+constexpr int kScanTile = kScanThreads * kScanItems;   // 4096 per block
+constexpr int kTopThreads = 1024;
+constexpr int kEmitThreads = 256;
+constexpr int kEmitPerBlock = 2048;
+constexpr int kHistMaxTiles = 16384;
+constexpr int kSortThreads = 512;
+constexpr int kSortLdsKeys = 16384;   // 128 KB of 64-bit keys
+
+// ---------------------------------------------------------------- per-Gaussian scan
+__global__ __launch_bounds__(kScanThreads) void k_scan_partials(const int32_t* __restrict__ x, int64_t n,
+                                                               int32_t* __restrict__ bsum) {
+  __shared__ int s_tmp[kScanThreads / 64 + 1];
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  int acc = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int64_t i = base + k;
+    if (i < n) acc += x[i];
+  }
+  int total;
+  block_exclusive_scan<kScanThreads>(acc, s_tmp, &total);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+// single block: exclusive scan of bsum[0..nb) in place
+__global__ __launch_bounds__(kTopThreads) void k_scan_top(int32_t* __restrict__ bsum, int nb) {
+  __shared__ int s_tmp[kTopThreads / 64 + 1];
+  int carry = 0;
+  for (int b0 = 0; b0 < nb; b0 += kTopThreads) {
+    const int i = b0 + threadIdx.x;
+    const int v = i < nb ? bsum[i] : 0;
+    int total;
+    const int ex = block_exclusive_scan<kTopThreads>(v, s_tmp, &total);
+    if (i < nb) bsum[i] = carry + ex;
+    carry += total;
+  }
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_apply(const int32_t* __restrict__ x, int64_t n,
+                                                            const int32_t* __restrict__ bsum,
+                                                            int32_t* __restrict__ out) {
+  __shared__ int s_tmp[kScanThreads / 64 + 1];
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  int v[kScanItems];
+  int acc = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int64_t i = base + k;
+    v[k] = i < n ? x[i] : 0;
+    acc += v[k];
+  }
+  int total;
+  int run = block_exclusive_scan<kScanThreads>(acc, s_tmp, &total) + bsum[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int64_t i = base + k;
+    if (i < n) out[i] = run;
+    run += v[k];
+  }
+}
+
+// ---------------------------------------------------------------- tile scan (single block)
+// tile_offset[0..CT], busy list (ascending), stats.
+__global__ __launch_bounds__(kTopThreads) void k_tile_scan(const int32_t* __restrict__ tile_count, int64_t CT,
+                                                          int32_t* __restrict__ tile_offset,
+                                                          int32_t* __restrict__ busy,
+                                                          gsr_bin_stats* __restrict__ stats) {
+  __shared__ int s_tmp[kTopThreads / 64 + 1];
+  __shared__ int s_max;
+  if (threadIdx.x == 0) s_max = 0;
+  __syncthreads();
+  long long carry = 0;
+  int bcarry = 0;
+  for (int64_t b0 = 0; b0 < CT; b0 += kTopThreads) {
+    const int64_t i = b0 + threadIdx.x;
+    const int v = i < CT ? tile_count[i] : 0;
+    int total;
+    const int ex = block_exclusive_scan<kTopThreads>(v, s_tmp, &total);
+    if (i < CT) tile_offset[i] = (int32_t)(carry + ex);
+    if (v > 0) atomicMax(&s_max, v);
+    int btotal;
+    const int bex = block_exclusive_scan<kTopThreads>(v > 0 ? 1 : 0, s_tmp, &btotal);
+    if (v > 0) busy[bcarry + bex] = (int32_t)i;
+    carry += total;
+    bcarry += btotal;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    tile_offset[CT] = (int32_t)carry;
+    stats->n_isect = carry;
+    stats->max_seg = s_max;
+    stats->n_busy = bcarry;
+  }
+}
+
+// ---------------------------------------------------------------- emission
+__device__ __forceinline__ uint64_t make_key(const Splat* rec, int64_t cn, int order) {
+  if (order == GSR_ORDER_DEPTH) {
+    const uint32_t d = __float_as_uint(rec[cn].p0.w);
+    return ((uint64_t)d << 32) | (uint64_t)(uint32_t)cn;
+  }
+  return (uint64_t)(uint32_t)cn;
+}
+
+__global__ __launch_bounds__(kEmitThreads) void k_emit(const Splat* __restrict__ rec, const uint2* __restrict__ rect,
+                                                      int64_t N, int tw, int th, int order, int use_lds,
+                                                      int32_t* __restrict__ cursor, uint64_t* __restrict__ keys) {
+  extern __shared__ int hist[];
+  const int c = blockIdx.y;
+  const int T = tw * th;
+  int32_t* gcur = cursor + (int64_t)c * T;
+  const int64_t n0 = (int64_t)blockIdx.x * kEmitPerBlock;
+  const int64_t n1 = min(N, n0 + kEmitPerBlock);
+  if (use_lds) {
+    for (int t = threadIdx.x; t < T; t += blockDim.x) hist[t] = 0;
+    __syncthreads();
+    for (int64_t n = n0 + threadIdx.x; n < n1; n += blockDim.x) {
+      const uint2 r = rect[(int64_t)c * N + n];
+      const int x0 = r.x & 0xffff, x1 = r.x >> 16, y0 = r.y & 0xffff, y1 = r.y >> 16;
+      for (int ty = y0; ty < y1; ++ty)
+        for (int tx = x0; tx < x1; ++tx) atomicAdd(&hist[ty * tw + tx], 1);
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < T; t += blockDim.x) {
+      const int v = hist[t];
+      if (v) hist[t] = atomicAdd(&gcur[t], v);
+    }
+    __syncthreads();
+  }
+  for (int64_t n = n0 + threadIdx.x; n < n1; n += blockDim.x) {
+    const int64_t cn = (int64_t)c * N + n;
+    const uint2 r = rect[cn];
+    const int x0 = r.x & 0xffff, x1 = r.x >> 16, y0 = r.y & 0xffff, y1 = r.y >> 16;
+    if (x1 <= x0 || y1 <= y0) continue;
+    const uint64_t key = make_key(rec, cn, order);
+    for (int ty = y0; ty < y1; ++ty)
+      for (int tx = x0; tx < x1; ++tx) {
+        const int t = ty * tw + tx;
+        const int slot = use_lds ? atomicAdd(&hist[t], 1) : atomicAdd(&gcur[t], 1);
+        keys[slot] = key;
+      }
+  }
+}
+
+// ---------------------------------------------------------------- per-tile sort
+__device__ __forceinline__ void bitonic_lds(uint64_t* s, int n2) {
+  for (int k = 2; k <= n2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int p = threadIdx.x; p < (n2 >> 1); p += blockDim.x) {
+        const int i = 2 * p - (p & (j - 1));
+        const int l = i + j;
+        const uint64_t a = s[i], b = s[l];
+        const bool asc = (i & k) == 0;
+        if ((a > b) == asc) {
+          s[i] = b;
+          s[l] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__device__ __forceinline__ int next_pow2(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+// Merge two sorted runs [a, a+na) and [b, b+nb) of unique keys into out (block-cooperative,
+// per-element rank by binary search).
+__device__ void merge_runs(const uint64_t* __restrict__ a, int na, const uint64_t* __restrict__ b, int nb,
+                           uint64_t* __restrict__ out) {
+  for (int i = threadIdx.x; i < na; i += blockDim.x) {
+    const uint64_t k = a[i];
+    int lo = 0, hi = nb;   // count of b < k
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (b[mid] < k) lo = mid + 1; else hi = mid;
+    }
+    out[i + lo] = k;
+  }
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+    const uint64_t k = b[i];
+    int lo = 0, hi = na;   // count of a <= k
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (a[mid] <= k) lo = mid + 1; else hi = mid;
+    }
+    out[i + lo] = k;
+  }
+}
+
+__global__ __launch_bounds__(kSortThreads) void k_segsort(
+    uint64_t* __restrict__ keys, uint64_t* __restrict__ tmp, const int32_t* __restrict__ tile_offset,
+    const int32_t* __restrict__ busy, const uint2* __restrict__ rect, const int32_t* __restrict__ isect_offset,
+    int tw, int th, int lds_keys, int32_t* __restrict__ sorted_ids, int32_t* __restrict__ isect_pos) {
+  extern __shared__ uint64_t s_keys[];
+  const int ct = busy[blockIdx.x];
+  const int start = tile_offset[ct];
+  const int len = tile_offset[ct + 1] - start;
+  const int T = tw * th;
+  const int t = ct % T;
+  const int ty = t / tw, tx = t - (t / tw) * tw;
+  const uint64_t* src = keys + start;
+  if (len <= lds_keys) {
+    const int n2 = next_pow2(len);
+    for (int i = threadIdx.x; i < n2; i += blockDim.x) s_keys[i] = i < len ? keys[start + i] : ~0ull;
+    __syncthreads();
+    bitonic_lds(s_keys, n2);
+  } else {
+    // Large bucket: sort runs of lds_keys in LDS, then merge runs pairwise in global memory.
+    uint64_t* bufA = keys + start;
+    uint64_t* bufB = tmp + start;
+    for (int r0 = 0; r0 < len; r0 += lds_keys) {
+      const int rl = min(lds_keys, len - r0);
+      const int n2 = next_pow2(rl);
+      for (int i = threadIdx.x; i < n2; i += blockDim.x) s_keys[i] = i < rl ? bufA[r0 + i] : ~0ull;
+      __syncthreads();
+      bitonic_lds(s_keys, n2);
+      for (int i = threadIdx.x; i < rl; i += blockDim.x) bufA[r0 + i] = s_keys[i];
+      __syncthreads();
+    }
+    for (int run = lds_keys; run < len; run <<= 1) {
+      for (int r0 = 0; r0 < len; r0 += 2 * run) {
+        const int na = min(run, len - r0);
+        const int nb = max(0, min(run, len - r0 - na));
+        merge_runs(bufA + r0, na, bufA + r0 + na, nb, bufB + r0);
+      }
+      __threadfence_block();
+      __syncthreads();
+      uint64_t* sw = bufA; bufA = bufB; bufB = sw;
+    }
+    src = bufA;
+  }
+  for (int s = threadIdx.x; s < len; s += blockDim.x) {
+    const uint64_t key = (len <= lds_keys) ? s_keys[s] : src[s];
+    const int32_t cn = (int32_t)(uint32_t)(key & 0xffffffffull);
+    sorted_ids[start + s] = cn;
+    const uint2 r = rect[cn];
+    const int x0 = r.x & 0xffff, x1 = r.x >> 16, y0 = r.y & 0xffff;
+    const int j = (ty - y0) * (x1 - x0) + (tx - x0);
+    isect_pos[isect_offset[cn] + j] = start + s;
+  }
+}
+
+}  // namespace gsr
+
+using namespace gsr;
+
+extern "C" {
+
+size_t gsr_bin_offsets_workspace(int64_t CN, int64_t CT) {
+  (void)CT;
+  const int64_t nb = (CN + kScanTile - 1) / kScanTile;
+  return (size_t)((nb + 64) * sizeof(int32_t));
+}
+
+int gsr_bin_offsets(const int32_t* isect_count, int64_t CN, const int32_t* tile_count, int64_t CT,
+                    void* workspace, size_t workspace_bytes, int32_t* isect_offset, int32_t* tile_offset,
+                    int32_t* busy_tiles, gsr_bin_stats* stats, void* stream) {
+  GSR_REQUIRE(CN >= 0 && CN < (1ll << 31), "gsr_bin_offsets: bad CN=%lld", (long long)CN);
+  GSR_REQUIRE(CT >= 1 && CT < (1ll << 31), "gsr_bin_offsets: bad CT=%lld", (long long)CT);
+  GSR_REQUIRE(workspace_bytes >= gsr_bin_offsets_workspace(CN, CT), "gsr_bin_offsets: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  int32_t* bsum = (int32_t*)workspace;
+  if (CN > 0) {
+    const int nb = ceil_div(CN, kScanTile);
+    hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(kScanThreads), 0, s, isect_count, CN, bsum);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kTopThreads), 0, s, bsum, nb);
+    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(kScanThreads), 0, s, isect_count, CN, bsum, isect_offset);
+    GSR_LAUNCH_CHECK("k_scan");
+  }
+  hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kTopThreads), 0, s, tile_count, CT, tile_offset, busy_tiles, stats);
+  GSR_LAUNCH_CHECK("k_tile_scan");
+  return GSR_OK;
+}
+
+size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT) {
+  // keys [I] + merge temp [I] (u64) + cursor [CT] (i32)
+  return (size_t)(2 * n_isect * sizeof(uint64_t) + (CT + 64) * sizeof(int32_t) + 256);
+}
+
+int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_offset, const int32_t* tile_offset,
+                 const int32_t* busy_tiles, int C, int64_t N, int width, int height, int order, int64_t n_isect,
+                 int32_t max_seg, int32_t n_busy, void* workspace, size_t workspace_bytes, int32_t* sorted_ids,
+                 int32_t* isect_pos, void* stream) {
+  GSR_REQUIRE(order == GSR_ORDER_DEPTH || order == GSR_ORDER_INDEX, "gsr_bin_sort: bad order %d", order);
+  GSR_REQUIRE(n_isect >= 0 && n_isect < (1ll << 31), "gsr_bin_sort: I=%lld out of range", (long long)n_isect);
+  GSR_REQUIRE((int64_t)C * N < (1ll << 31), "gsr_bin_sort: C*N too large for 32-bit ids");
+  const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
+  const int64_t T = (int64_t)tw * th;
+  const int64_t CT = T * C;
+  GSR_REQUIRE(workspace_bytes >= gsr_bin_sort_workspace(n_isect, CT), "gsr_bin_sort: workspace too small");
+  if (n_isect == 0 || N == 0) return GSR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  uint64_t* keys = (uint64_t*)workspace;
+  uint64_t* tmp = keys + n_isect;
+  int32_t* cursor = (int32_t*)(tmp + n_isect);
+  if (hipMemcpyAsync(cursor, tile_offset, CT * sizeof(int32_t), hipMemcpyDeviceToDevice, s) != hipSuccess) {
+    set_error("gsr_bin_sort: cursor copy failed");
+    return GSR_ELAUNCH;
+  }
+  const int use_lds = T <= kHistMaxTiles;
+  dim3 grid(ceil_div(N, kEmitPerBlock), C);
+  hipLaunchKernelGGL(k_emit, grid, dim3(kEmitThreads), use_lds ? T * sizeof(int) : 0, s, (const Splat*)rec,
+                     (const uint2*)rect, N, tw, th, order, use_lds, cursor, keys);
+  GSR_LAUNCH_CHECK("k_emit");
+  if (n_busy > 0) {
+    int lds_keys = 64;
+    while (lds_keys < max_seg && lds_keys < kSortLdsKeys) lds_keys <<= 1;
+    hipLaunchKernelGGL(k_segsort, dim3(n_busy), dim3(kSortThreads), lds_keys * sizeof(uint64_t), s, keys, tmp,
+                       tile_offset, busy_tiles, (const uint2*)rect, isect_offset, tw, th, lds_keys, sorted_ids,
+                       isect_pos);
+    GSR_LAUNCH_CHECK("k_segsort");
+  }
+  return GSR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,106 @@
+// Shared device/host helpers for libgsr (gfx950 / CDNA4, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gsr.h"
+
+namespace gsr {
+
+constexpr int kTile = GSR_TILE;          // 16x16 pixel tiles (gsplat's binning granule)
+constexpr int kTilePix = kTile * kTile;  // 256 pixels = 4 waves of 64
+constexpr int kWave = 64;
+constexpr float kAlphaThreshold = 1.f / 255.f;   // gsplat ALPHA_THRESHOLD
+constexpr float kAlphaMax = 0.999f;              // gsplat alpha clamp
+constexpr float kTMin = 1e-4f;                   // gsplat transmittance stop
+constexpr float kExtendMax = 3.33f;              // gsplat >=1.5 max sigma extent
+constexpr int kPartial = 9;                      // per-entry gradient partial width
+
+// Splat record: 3 x float4 (48 B) per (camera, Gaussian).  See include/gsr.h.
+struct __align__(16) Splat {
+  float4 p0;  // x, y, opacity, depth
+  float4 p1;  // a, b, c, 0     (sigma = a dx^2 + b dx dy + c dy^2)
+  float4 p2;  // r, g, b, 0
+};
+
+// ---------------------------------------------------------------- host-side error state
+void set_error(const char* fmt, ...);
+
+#define GSR_REQUIRE(cond, ...)            \
+  do {                                    \
+    if (!(cond)) {                        \
+      ::gsr::set_error(__VA_ARGS__);      \
+      return GSR_EINVAL;                  \
+    }                                     \
+  } while (0)
+
+#define GSR_LAUNCH_CHECK(name)                                                   \
+  do {                                                                           \
+    hipError_t e_ = hipGetLastError();                                           \
+    if (e_ != hipSuccess) {                                                      \
+      ::gsr::set_error("%s: launch failed: %s", name, hipGetErrorString(e_));   \
+      return GSR_ELAUNCH;                                                        \
+    }                                                                            \
+  } while (0)
+
+inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// ---------------------------------------------------------------- device helpers
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+
+__device__ __forceinline__ float readlane_f(float v, int lane) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
+}
+
+// Full-wave (64-lane) sum; every lane must be active.  Returns the total in all lanes.
+// quad xor-1, quad xor-2, half-row mirror, row mirror → 16-lane row sums; then 4 readlanes.
+__device__ __forceinline__ float wave_sum(float v) {
+  v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);   // row_half_mirror
+  v += dpp_mov<0x140>(v);   // row_mirror
+  return (readlane_f(v, 0) + readlane_f(v, 16)) + (readlane_f(v, 32) + readlane_f(v, 48));
+}
+
+__device__ __forceinline__ unsigned long long wave_ballot(bool p) { return __ballot(p); }
+
+// Block-wide exclusive scan of one int per thread (NT threads, multiple of 64).
+// s_tmp must hold NT/64 + 1 ints.  Returns the exclusive prefix; *total = block sum.
+template <int NT>
+__device__ __forceinline__ int block_exclusive_scan(int v, int* s_tmp, int* total) {
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_tmp[w] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int k = 0; k < NT / 64; ++k) {
+      int t = s_tmp[k];
+      s_tmp[k] = acc;
+      acc += t;
+    }
+    s_tmp[NT / 64] = acc;
+  }
+  __syncthreads();
+  int res = x - v + s_tmp[w];
+  *total = s_tmp[NT / 64];
+  __syncthreads();
+  return res;
+}
+
+__device__ __forceinline__ uint32_t pack_rect_lo(int a, int b) {
+  return (uint32_t)a | ((uint32_t)b << 16);
+}
+
+}  // namespace gsr

@@ -1,0 +1,233 @@
+// (a) Projection forward: activations + screen-space conic + tile rect + tile histogram.
+//
+// One thread per (camera, Gaussian); one workgroup covers `gpb` Gaussians of ONE camera so
+// that its tile histogram fits in LDS (tiles of one camera).  The histogram is flushed with
+// one coalesced no-return atomic per non-empty tile per workgroup (MI355X float/int atomics
+// execute at the memory side — scattered per-entry atomics would be ~17x slower).
+#include <cstdarg>
+#include <cstdio>
+
+#include "project_math.h"
+
+namespace gsr {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+constexpr int kProjThreads = 256;
+constexpr int kProjPerBlock = 2048;     // Gaussians per workgroup (8 per thread)
+constexpr int kHistMaxTiles = 16384;    // LDS histogram limit (64 KB)
+
+__device__ __forceinline__ void hist_add(int* hist, int32_t* gcount, bool use_lds, int x0, int x1,
+                                         int y0, int y1, int tw) {
+  for (int ty = y0; ty < y1; ++ty)
+    for (int tx = x0; tx < x1; ++tx) {
+      if (use_lds)
+        atomicAdd(&hist[ty * tw + tx], 1);
+      else
+        atomicAdd(&gcount[ty * tw + tx], 1);
+    }
+}
+
+__device__ __forceinline__ void hist_flush(int* hist, int32_t* gcount, int T) {
+  __syncthreads();
+  for (int t = threadIdx.x; t < T; t += blockDim.x) {
+    const int v = hist[t];
+    if (v) atomicAdd(&gcount[t], v);
+  }
+}
+
+template <int RMODE>
+__global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
+    const float* __restrict__ params, int64_t N, int64_t stride, const float* __restrict__ viewmats,
+    const float* __restrict__ Ks, int W, int H, float near_plane, float far_plane,
+    float radius_clip, float eps2d, int tw, int th, int use_lds, Splat* __restrict__ rec,
+    uint2* __restrict__ rect, int32_t* __restrict__ cnt, int32_t* __restrict__ tile_count) {
+  extern __shared__ int hist[];
+  const int c = blockIdx.y;
+  const int T = tw * th;
+  int32_t* gcount = tile_count + (int64_t)c * T;
+  if (use_lds) {
+    for (int t = threadIdx.x; t < T; t += blockDim.x) hist[t] = 0;
+    __syncthreads();
+  }
+  const Cam cam = load_cam(viewmats + c * 16, Ks + c * 9);
+  const int64_t n0 = (int64_t)blockIdx.x * kProjPerBlock;
+  const int64_t n1 = min(N, n0 + kProjPerBlock);
+  for (int64_t n = n0 + threadIdx.x; n < n1; n += blockDim.x) {
+    const int64_t cn = (int64_t)c * N + n;
+    const Act3D a = activate3d(params + n * stride);
+    Geo3D g;
+    bool ok = geo3d(a, cam, W, H, near_plane, far_plane, eps2d, g);
+    float rx = 0.f, ry = 0.f;
+    if (ok) {
+      if (RMODE == GSR_RADIUS_OPACITY_AABB) {
+        if (a.op < kAlphaThreshold) {
+          ok = false;
+        } else {
+          const float extend = fminf(kExtendMax, sqrtf(2.f * logf(a.op / kAlphaThreshold)));
+          rx = ceilf(extend * sqrtf(g.c00));
+          ry = ceilf(extend * sqrtf(g.c11));
+          if (rx <= radius_clip && ry <= radius_clip) ok = false;
+        }
+      } else {
+        const float b = 0.5f * (g.c00 + g.c11);
+        const float v1 = b + sqrtf(fmaxf(0.01f, b * b - g.det));
+        const float r = ceilf(3.f * sqrtf(v1));
+        rx = r;
+        ry = r;
+        if (r <= radius_clip) ok = false;
+      }
+    }
+    if (ok) {
+      if (g.u + rx <= 0.f || g.u - rx >= (float)W || g.v + ry <= 0.f || g.v - ry >= (float)H) ok = false;
+      if (!isfinite(g.u) || !isfinite(g.v)) ok = false;
+    }
+    int x0 = 0, x1 = 0, y0 = 0, y1 = 0;
+    if (ok) {
+      // gsplat isect_tiles: floor/ceil of (mean/16 -+ radius/16), clamped to [0, tiles]
+      const float tix = g.u / (float)kTile, tiy = g.v / (float)kTile;
+      const float trx = rx / (float)kTile, try_ = ry / (float)kTile;
+      x0 = (int)fminf(fmaxf(floorf(tix - trx), 0.f), (float)tw);
+      x1 = (int)fminf(fmaxf(ceilf(tix + trx), 0.f), (float)tw);
+      y0 = (int)fminf(fmaxf(floorf(tiy - try_), 0.f), (float)th);
+      y1 = (int)fminf(fmaxf(ceilf(tiy + try_), 0.f), (float)th);
+      if (x1 < x0) x1 = x0;
+      if (y1 < y0) y1 = y0;
+      Splat s;
+      s.p0 = make_float4(g.u, g.v, a.op, g.mc[2]);
+      s.p1 = make_float4(0.5f * g.A, g.B, 0.5f * g.C, 0.f);
+      s.p2 = make_float4(a.col[0], a.col[1], a.col[2], 0.f);
+      rec[cn] = s;
+      hist_add(hist, gcount, use_lds, x0, x1, y0, y1, tw);
+    }
+    rect[cn] = make_uint2(pack_rect_lo(x0, x1), pack_rect_lo(y0, y1));
+    cnt[cn] = (x1 - x0) * (y1 - y0);
+  }
+  if (use_lds) hist_flush(hist, gcount, T);
+}
+
+__global__ __launch_bounds__(kProjThreads) void k_project2d_fwd(
+    const float* __restrict__ params, int64_t N, int64_t stride, int W, int H, float eps_cut,
+    int tw, int th, int use_lds, Splat* __restrict__ rec, uint2* __restrict__ rect,
+    int32_t* __restrict__ cnt, int32_t* __restrict__ tile_count) {
+  extern __shared__ int hist[];
+  const int T = tw * th;
+  if (use_lds) {
+    for (int t = threadIdx.x; t < T; t += blockDim.x) hist[t] = 0;
+    __syncthreads();
+  }
+  const int64_t n0 = (int64_t)blockIdx.x * kProjPerBlock;
+  const int64_t n1 = min(N, n0 + kProjPerBlock);
+  for (int64_t n = n0 + threadIdx.x; n < n1; n += blockDim.x) {
+    const Geo2D g = geo2d(params + n * stride);
+    int x0 = 0, x1 = 0, y0 = 0, y1 = 0;
+    bool ok = g.op > eps_cut && isfinite(g.u) && isfinite(g.v);
+    if (ok) {
+      // q <= L = ln(op/eps) ellipse; its AABB half-extents: sqrt(L * (Minv)_xx), Minv =
+      // R^T diag(1/ia, 1/ib) R.  Slightly inflated so the cut never drops g >= eps_cut.
+      const float L = logf(g.op / eps_cut);
+      const float ai = 1.f / g.ia, bi = 1.f / g.ib;
+      const float c2 = g.cs * g.cs, s2 = g.sn * g.sn;
+      float hx = sqrtf(L * (ai * c2 + bi * s2)) * 1.0001f + 1e-3f;
+      float hy = sqrtf(L * (ai * s2 + bi * c2)) * 1.0001f + 1e-3f;
+      // integer pixel centres 0..W-1 (src/gaussian_renderer.py:355-358)
+      float jx0 = floorf(g.u - hx), jx1 = ceilf(g.u + hx);
+      float jy0 = floorf(g.v - hy), jy1 = ceilf(g.v + hy);
+      if (!(hx == hx)) { jx0 = 0.f; jx1 = (float)(W - 1); }   // NaN guard: whole image
+      if (!(hy == hy)) { jy0 = 0.f; jy1 = (float)(H - 1); }
+      jx0 = fmaxf(jx0, 0.f);
+      jy0 = fmaxf(jy0, 0.f);
+      jx1 = fminf(jx1, (float)(W - 1));
+      jy1 = fminf(jy1, (float)(H - 1));
+      if (jx0 > jx1 || jy0 > jy1) {
+        ok = false;
+      } else {
+        x0 = (int)jx0 / kTile;
+        x1 = (int)jx1 / kTile + 1;
+        y0 = (int)jy0 / kTile;
+        y1 = (int)jy1 / kTile + 1;
+      }
+    }
+    if (ok) {
+      Splat s;
+      s.p0 = make_float4(g.u, g.v, g.op, 0.f);
+      s.p1 = make_float4(g.a, g.b, g.c, 0.f);
+      s.p2 = make_float4(g.col[0], g.col[1], g.col[2], 0.f);
+      rec[n] = s;
+      hist_add(hist, tile_count, use_lds, x0, x1, y0, y1, tw);
+    }
+    rect[n] = make_uint2(pack_rect_lo(x0, x1), pack_rect_lo(y0, y1));
+    cnt[n] = (x1 - x0) * (y1 - y0);
+  }
+  if (use_lds) hist_flush(hist, tile_count, T);
+}
+
+}  // namespace gsr
+
+using namespace gsr;
+
+extern "C" {
+
+int gsr_version(void) { return 1; }
+
+const char* gsr_last_error(void) { return g_err; }
+
+int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride, const float* viewmats,
+                      const float* Ks, int C, int width, int height, float near_plane,
+                      float far_plane, float radius_clip, float eps2d, int radius_mode, float* rec,
+                      uint32_t* rect, int32_t* isect_count, int32_t* tile_count, void* stream) {
+  GSR_REQUIRE(N >= 0 && C >= 1 && C <= 65535, "gsr3d_project_fwd: bad N=%lld or C=%d", (long long)N, C);
+  GSR_REQUIRE(width > 0 && height > 0, "gsr3d_project_fwd: bad image %dx%d", width, height);
+  GSR_REQUIRE(row_stride >= 14, "gsr3d_project_fwd: row_stride %lld < 14", (long long)row_stride);
+  GSR_REQUIRE(radius_mode == GSR_RADIUS_OPACITY_AABB || radius_mode == GSR_RADIUS_ISOTROPIC_3SIGMA,
+              "gsr3d_project_fwd: bad radius_mode %d", radius_mode);
+  const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
+  GSR_REQUIRE(tw < 65536 && th < 65536, "gsr3d_project_fwd: image too large");
+  if (N == 0) return GSR_OK;
+  const int T = tw * th;
+  const int use_lds = T <= kHistMaxTiles;
+  const size_t lds = use_lds ? (size_t)T * sizeof(int) : 0;
+  dim3 grid(ceil_div(N, kProjPerBlock), C);
+  hipStream_t s = (hipStream_t)stream;
+  if (radius_mode == GSR_RADIUS_OPACITY_AABB)
+    hipLaunchKernelGGL(k_project3d_fwd<GSR_RADIUS_OPACITY_AABB>, grid, dim3(kProjThreads), lds, s,
+                       params, N, row_stride, viewmats, Ks, width, height, near_plane, far_plane,
+                       radius_clip, eps2d, tw, th, use_lds, (Splat*)rec, (uint2*)rect, isect_count,
+                       tile_count);
+  else
+    hipLaunchKernelGGL(k_project3d_fwd<GSR_RADIUS_ISOTROPIC_3SIGMA>, grid, dim3(kProjThreads), lds, s,
+                       params, N, row_stride, viewmats, Ks, width, height, near_plane, far_plane,
+                       radius_clip, eps2d, tw, th, use_lds, (Splat*)rec, (uint2*)rect, isect_count,
+                       tile_count);
+  GSR_LAUNCH_CHECK("k_project3d_fwd");
+  return GSR_OK;
+}
+
+int gsr2d_project_fwd(const float* params, int64_t N, int64_t row_stride, int width, int height,
+                      float eps_cut, float* rec, uint32_t* rect, int32_t* isect_count,
+                      int32_t* tile_count, void* stream) {
+  GSR_REQUIRE(N >= 0, "gsr2d_project_fwd: bad N=%lld", (long long)N);
+  GSR_REQUIRE(width > 0 && height > 0, "gsr2d_project_fwd: bad image %dx%d", width, height);
+  GSR_REQUIRE(row_stride >= 9, "gsr2d_project_fwd: row_stride %lld < 9", (long long)row_stride);
+  GSR_REQUIRE(eps_cut > 0.f && eps_cut < 1.f, "gsr2d_project_fwd: eps_cut must be in (0,1)");
+  const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
+  GSR_REQUIRE(tw < 65536 && th < 65536, "gsr2d_project_fwd: image too large");
+  if (N == 0) return GSR_OK;
+  const int T = tw * th;
+  const int use_lds = T <= kHistMaxTiles;
+  const size_t lds = use_lds ? (size_t)T * sizeof(int) : 0;
+  hipLaunchKernelGGL(k_project2d_fwd, dim3(ceil_div(N, kProjPerBlock)), dim3(kProjThreads), lds,
+                     (hipStream_t)stream, params, N, row_stride, width, height, eps_cut, tw, th,
+                     use_lds, (Splat*)rec, (uint2*)rect, isect_count, tile_count);
+  GSR_LAUNCH_CHECK("k_project2d_fwd");
+  return GSR_OK;
+}
+
+}  // extern "C"

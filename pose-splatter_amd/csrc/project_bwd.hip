@@ -1,0 +1,276 @@
+// Projection backward: per Gaussian, reduce its per-entry partials (fixed order → bitwise
+// deterministic), chain through the screen-space parameters, the projection and the
+// adapter activations, and sum over cameras.  One thread per Gaussian n.
+//
+// 3D chain (oracle/oracle3d.py restates the forward; its autograd is the parity check):
+//   record (a,b,c) = (A/2, B, C/2) of conic = inv(cov2d + eps2d I)
+//   V_cov = -Cinv V_sym Cinv,  V_sym = [[vA, vB/2],[vB/2, vC]]
+//   cov2d = J Sc J^T:  V_Sc = J^T V_cov J,  V_J = 2 V_cov J Sc
+//   J(x,y,z) with FOV-clamped tx/ty (gradient through x/y only where unclamped)
+//   mean2d = (fx x/z + cx, fy y/z + cy);  mean_c = Rv m + t;  Sc = Rv S Rv^T
+//   S = M M^T, M = R(q) diag(s):  V_M = 2 V_S M
+//   R(q) with q re-normalised (gsplat) after the adapter's q/(|q|+1e-8)
+//   scales = exp, colours clamp(0,1) (pass-through on [0,1] inclusive), opacity sigmoid.
+// 2D chain: (a,b,c)(theta, ia, ib), ia = 1/(2 sx^2 + 1e-8), sx = exp(ls).
+#include "project_math.h"
+
+namespace gsr {
+
+constexpr int kBwdThreads = 256;
+
+__device__ __forceinline__ void gather_partials(const uint2 r, int T, int tw, int64_t ct_base, const int32_t* __restrict__ pos,
+                                                int off, const int32_t* __restrict__ tile_end,
+                                                const float* __restrict__ partial, float (&acc)[kPartial]) {
+  const int x0 = r.x & 0xffff, x1 = r.x >> 16, y0 = r.y & 0xffff, y1 = r.y >> 16;
+  const int w = x1 - x0;
+  int jj = 0;
+  for (int ty = y0; ty < y1; ++ty) {
+    for (int tx = x0; tx < x0 + w; ++tx, ++jj) {
+      const int s = pos[off + jj];
+      const int t = ty * tw + tx;
+      if (s < tile_end[ct_base + t]) {
+        const float* p = partial + (int64_t)s * kPartial;
+#pragma unroll
+        for (int v = 0; v < kPartial; ++v) acc[v] += p[v];
+      }
+    }
+  }
+  (void)T;
+}
+
+__global__ __launch_bounds__(kBwdThreads) void k_project3d_bwd(
+    const float* __restrict__ params, int64_t N, int64_t stride, const float* __restrict__ viewmats,
+    const float* __restrict__ Ks, int C, int W, int H, float eps2d, int tw, int th, const uint2* __restrict__ rect,
+    const int32_t* __restrict__ isect_offset, const int32_t* __restrict__ isect_count,
+    const int32_t* __restrict__ pos, const int32_t* __restrict__ tile_end, const float* __restrict__ partial,
+    float* __restrict__ v_params) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const float* p = params + n * stride;
+  const Act3D a = activate3d(p);
+  const int T = tw * th;
+  float v_m[3] = {0.f, 0.f, 0.f};
+  float v_s[3] = {0.f, 0.f, 0.f};
+  float v_R[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) v_R[k] = 0.f;
+  float v_col[3] = {0.f, 0.f, 0.f};
+  float v_op = 0.f;
+  bool any = false;
+  Geo3D g;
+  for (int c = 0; c < C; ++c) {
+    const int64_t cn = (int64_t)c * N + n;
+    if (isect_count[cn] <= 0) continue;
+    float acc[kPartial];
+#pragma unroll
+    for (int v = 0; v < kPartial; ++v) acc[v] = 0.f;
+    gather_partials(rect[cn], T, tw, (int64_t)c * T, pos, isect_offset[cn], tile_end, partial, acc);
+    const Cam cam = load_cam(viewmats + c * 16, Ks + c * 9);
+    // recompute the forward geometry (not culled: it has intersections)
+    geo3d(a, cam, W, H, 0.f, 3.4e38f, eps2d, g);
+    any = true;
+    v_op += acc[5];
+    v_col[0] += acc[6];
+    v_col[1] += acc[7];
+    v_col[2] += acc[8];
+    // conic (A,B,C) from record (a,b,c) = (A/2, B, C/2)
+    const float vA = 0.5f * acc[2], vB = acc[3], vC = 0.5f * acc[4];
+    // V_cov = -Cinv V_sym Cinv ; Cinv = [[A,B],[B,C]]
+    const float A = g.A, B = g.B, Cc = g.C;
+    const float hb = 0.5f * vB;
+    // X = V_sym Cinv
+    const float X00 = vA * A + hb * B, X01 = vA * B + hb * Cc;
+    const float X10 = hb * A + vC * B, X11 = hb * B + vC * Cc;
+    const float G00 = -(A * X00 + B * X10);
+    const float G01 = -(A * X01 + B * X11);
+    const float G11 = -(B * X01 + Cc * X11);
+    // V_Sc = J^T G J  (J = [[J00,0,J02],[0,J11,J12]])
+    const float J00 = g.J00, J02 = g.J02, J11 = g.J11, J12 = g.J12;
+    float VSc[9];
+    {
+      // G J : 2x3
+      const float GJ00 = G00 * J00, GJ01 = G01 * J11, GJ02 = G00 * J02 + G01 * J12;
+      const float GJ10 = G01 * J00, GJ11 = G11 * J11, GJ12 = G01 * J02 + G11 * J12;
+      // J^T (GJ): 3x3, J^T rows: (J00,0), (0,J11), (J02,J12)
+      VSc[0] = J00 * GJ00;
+      VSc[1] = J00 * GJ01;
+      VSc[2] = J00 * GJ02;
+      VSc[3] = J11 * GJ10;
+      VSc[4] = J11 * GJ11;
+      VSc[5] = J11 * GJ12;
+      VSc[6] = J02 * GJ00 + J12 * GJ10;
+      VSc[7] = J02 * GJ01 + J12 * GJ11;
+      VSc[8] = J02 * GJ02 + J12 * GJ12;
+    }
+    // V_J = 2 G J Sc  (2x3), only the entries J00, J02, J11, J12 matter
+    const float* S = g.Sc;  // s00 s01 s02 s11 s12 s22
+    const float Sf[9] = {S[0], S[1], S[2], S[1], S[3], S[4], S[2], S[4], S[5]};
+    float JS[6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      JS[k] = J00 * Sf[0 * 3 + k] + J02 * Sf[2 * 3 + k];
+      JS[3 + k] = J11 * Sf[1 * 3 + k] + J12 * Sf[2 * 3 + k];
+    }
+    const float vJ00 = 2.f * (G00 * JS[0] + G01 * JS[3]);
+    const float vJ02 = 2.f * (G00 * JS[2] + G01 * JS[5]);
+    const float vJ11 = 2.f * (G01 * JS[1] + G11 * JS[4]);
+    const float vJ12 = 2.f * (G01 * JS[2] + G11 * JS[5]);
+    // mean_c gradients
+    const float x = g.mc[0], y = g.mc[1];
+    const float rz = g.rz, rz2 = rz * rz, rz3 = rz2 * rz;
+    const float fx = cam.fx, fy = cam.fy;
+    const float vu = acc[0], vv = acc[1];
+    float vmc0 = fx * rz * vu;
+    float vmc1 = fy * rz * vv;
+    float vmc2 = -(fx * x * vu + fy * y * vv) * rz2;
+    vmc2 += -fx * rz2 * vJ00 - fy * rz2 * vJ11;
+    if (g.clx) {
+      vmc0 += -fx * rz2 * vJ02;
+      vmc2 += 2.f * fx * g.tx * rz3 * vJ02;
+    } else {
+      vmc2 += fx * g.tx * rz3 * vJ02;
+    }
+    if (g.cly) {
+      vmc1 += -fy * rz2 * vJ12;
+      vmc2 += 2.f * fy * g.ty * rz3 * vJ12;
+    } else {
+      vmc2 += fy * g.ty * rz3 * vJ12;
+    }
+    const float* Rv = cam.R;
+    // v_m += Rv^T v_mc
+#pragma unroll
+    for (int k = 0; k < 3; ++k) v_m[k] += Rv[0 * 3 + k] * vmc0 + Rv[1 * 3 + k] * vmc1 + Rv[2 * 3 + k] * vmc2;
+    // V_S = Rv^T V_Sc Rv
+    float T1[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        T1[r * 3 + k] = Rv[0 * 3 + r] * VSc[0 * 3 + k] + Rv[1 * 3 + r] * VSc[1 * 3 + k] + Rv[2 * 3 + r] * VSc[2 * 3 + k];
+    float VS[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        VS[r * 3 + k] = T1[r * 3 + 0] * Rv[0 * 3 + k] + T1[r * 3 + 1] * Rv[1 * 3 + k] + T1[r * 3 + 2] * Rv[2 * 3 + k];
+    // V_M = (V_S + V_S^T) M
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        float vm = 0.f;
+#pragma unroll
+        for (int l = 0; l < 3; ++l) vm += (VS[r * 3 + l] + VS[l * 3 + r]) * g.M[l * 3 + k];
+        // M = R diag(s)
+        v_R[r * 3 + k] += vm * a.s[k];
+        v_s[k] += vm * g.Rq[r * 3 + k];
+      }
+  }
+  float* out = v_params + n * 14;
+  if (!any) {
+#pragma unroll
+    for (int k = 0; k < 14; ++k) out[k] = 0.f;
+    return;
+  }
+  // R(qn) → v_qn (normalised quaternion)
+  const float w = g.qn[0], x = g.qn[1], y = g.qn[2], z = g.qn[3];
+  const float* V = v_R;
+  float vq[4];
+  vq[0] = 2.f * (z * (V[3] - V[1]) + y * (V[2] - V[6]) + x * (V[7] - V[5]));
+  vq[1] = 2.f * (y * V[1] + z * V[2] + y * V[3] - 2.f * x * V[4] - w * V[5] + z * V[6] + w * V[7] - 2.f * x * V[8]);
+  vq[2] = 2.f * (-2.f * y * V[0] + x * V[1] + w * V[2] + x * V[3] + z * V[5] - w * V[6] + z * V[7] - 2.f * y * V[8]);
+  vq[3] = 2.f * (-2.f * z * V[0] - w * V[1] + x * V[2] + w * V[3] - 2.f * z * V[4] + y * V[5] + x * V[6] + y * V[7]);
+  // gsplat normalisation vjp: v_qa = (vq - (vq.qn) qn) / |qa|
+  const float dqn = vq[0] * w + vq[1] * x + vq[2] * y + vq[3] * z;
+  float vqa[4] = {(vq[0] - dqn * w) * g.qinv, (vq[1] - dqn * x) * g.qinv, (vq[2] - dqn * y) * g.qinv,
+                  (vq[3] - dqn * z) * g.qinv};
+  // adapter: qa = q / (r + 1e-8), r = |q|:  v_q = v_qa/(r+eps) - q (q.v_qa) / (r (r+eps)^2)
+  const float den = a.rq + 1e-8f;
+  const float qdot = a.qraw[0] * vqa[0] + a.qraw[1] * vqa[1] + a.qraw[2] * vqa[2] + a.qraw[3] * vqa[3];
+  const float coef = qdot / (a.rq * den * den);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) out[k] = v_m[k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) out[3 + k] = v_s[k] * a.s[k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) out[6 + k] = vqa[k] / den - a.qraw[k] * coef;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) out[10 + k] = (a.craw[k] >= 0.f && a.craw[k] <= 1.f) ? v_col[k] : 0.f;
+  out[13] = v_op * a.op * (1.f - a.op);
+}
+
+__global__ __launch_bounds__(kBwdThreads) void k_project2d_bwd(
+    const float* __restrict__ params, int64_t N, int64_t stride, int tw, int th, const uint2* __restrict__ rect,
+    const int32_t* __restrict__ isect_offset, const int32_t* __restrict__ isect_count,
+    const int32_t* __restrict__ pos, const int32_t* __restrict__ tile_end, const float* __restrict__ partial,
+    float* __restrict__ v_params) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float* out = v_params + n * 9;
+  if (isect_count[n] <= 0) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) out[k] = 0.f;
+    return;
+  }
+  float acc[kPartial];
+#pragma unroll
+  for (int v = 0; v < kPartial; ++v) acc[v] = 0.f;
+  gather_partials(rect[n], tw * th, tw, 0, pos, isect_offset[n], tile_end, partial, acc);
+  const Geo2D g = geo2d(params + n * stride);
+  const float va = acc[2], vb = acc[3], vc = acc[4];
+  const float C = g.cs, S = g.sn;
+  const float C2 = C * C, S2 = S * S, CS = C * S;
+  const float v_ia = va * C2 + vb * 2.f * CS + vc * S2;
+  const float v_ib = va * S2 - vb * 2.f * CS + vc * C2;
+  const float dd = g.ia - g.ib;
+  const float v_th = dd * (-2.f * CS * va + 2.f * (C2 - S2) * vb + 2.f * CS * vc);
+  // ia = 1/(2 sx^2 + 1e-8): d ia/d sx = -4 sx ia^2 ; sx = exp(ls): d sx/d ls = sx
+  const float v_lsx = v_ia * (-4.f * g.sx * g.ia * g.ia) * g.sx;
+  const float v_lsy = v_ib * (-4.f * g.sy * g.ib * g.ib) * g.sy;
+  out[0] = acc[0];
+  out[1] = acc[1];
+  out[2] = v_lsx;
+  out[3] = v_lsy;
+  out[4] = v_th;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) out[5 + k] = (g.craw[k] >= 0.f && g.craw[k] <= 1.f) ? acc[6 + k] : 0.f;
+  out[8] = acc[5] * g.op * (1.f - g.op);
+}
+
+}  // namespace gsr
+
+using namespace gsr;
+
+extern "C" {
+
+int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride, const float* viewmats, const float* Ks,
+                      int C, int width, int height, float eps2d, const uint32_t* rect, const int32_t* isect_offset,
+                      const int32_t* isect_count, const int32_t* isect_pos, const int32_t* tile_end,
+                      const float* partial, float* v_params, void* stream) {
+  GSR_REQUIRE(N >= 0 && C >= 1 && width > 0 && height > 0, "gsr3d_project_bwd: bad arguments");
+  GSR_REQUIRE(row_stride >= 14, "gsr3d_project_bwd: row_stride < 14");
+  if (N == 0) return GSR_OK;
+  const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
+  hipLaunchKernelGGL(k_project3d_bwd, dim3(ceil_div(N, kBwdThreads)), dim3(kBwdThreads), 0, (hipStream_t)stream,
+                     params, N, row_stride, viewmats, Ks, C, width, height, eps2d, tw, th, (const uint2*)rect,
+                     isect_offset, isect_count, isect_pos, tile_end, partial, v_params);
+  GSR_LAUNCH_CHECK("k_project3d_bwd");
+  return GSR_OK;
+}
+
+int gsr2d_project_bwd(const float* params, int64_t N, int64_t row_stride, int width, int height,
+                      const uint32_t* rect, const int32_t* isect_offset, const int32_t* isect_count,
+                      const int32_t* isect_pos, const int32_t* tile_end, const float* partial, float* v_params,
+                      void* stream) {
+  GSR_REQUIRE(N >= 0 && width > 0 && height > 0, "gsr2d_project_bwd: bad arguments");
+  GSR_REQUIRE(row_stride >= 9, "gsr2d_project_bwd: row_stride < 9");
+  if (N == 0) return GSR_OK;
+  const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
+  hipLaunchKernelGGL(k_project2d_bwd, dim3(ceil_div(N, kBwdThreads)), dim3(kBwdThreads), 0, (hipStream_t)stream,
+                     params, N, row_stride, tw, th, (const uint2*)rect, isect_offset, isect_count, isect_pos,
+                     tile_end, partial, v_params);
+  GSR_LAUNCH_CHECK("k_project2d_bwd");
+  return GSR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,506 @@
+// (c) Per-tile compositing, forward and backward.
+//
+// One 256-thread workgroup per 16x16 tile (4 waves of 64 pixels).  The tile's sorted list
+// is staged through LDS in batches of 256 splat records (each record gathered once per
+// tile, broadcast-read by all 4 waves); each wave leaves the inner loop as soon as all of
+// its 64 pixels are done (exec-mask early-out), the workgroup as soon as all 4 are.
+//
+// Backward gradient scatter: instead of per-Gaussian float atomics (memory-side on MI355X,
+// ~0.08 TB/s for scattered lanes), every sorted entry's gradient is summed over the tile's
+// pixels on chip (DPP wave sums + a 4-wave LDS combine) and stored ONCE, coalesced, as a
+// 9-float partial; *_project_bwd reduces each Gaussian's partials in a fixed order, so the
+// gradients are bitwise deterministic.
+#include "gsr_common.h"
+
+namespace gsr {
+
+constexpr int kRasterThreads = 256;
+
+__device__ __forceinline__ void tile_coords(int ct, int tw, int th, int& c, int& ty, int& tx) {
+  const int T = tw * th;
+  c = ct / T;
+  const int t = ct - c * T;
+  ty = t / tw;
+  tx = t - ty * tw;
+}
+
+// ---------------------------------------------------------------- 3D forward
+__global__ __launch_bounds__(kRasterThreads) void k_raster3d_fwd(
+    const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
+    int W, int H, int tw, int th, const float* __restrict__ bg, float* __restrict__ out_rgb,
+    float* __restrict__ out_alpha, float* __restrict__ out_T, int32_t* __restrict__ out_last,
+    int32_t* __restrict__ tile_end) {
+  __shared__ float4 s_p0[kRasterThreads];
+  __shared__ float4 s_p1[kRasterThreads];
+  __shared__ float4 s_p2[kRasterThreads];
+  __shared__ int s_max;
+  const int ct = blockIdx.x;
+  int c, ty, tx;
+  tile_coords(ct, tw, th, c, ty, tx);
+  const int i = ty * kTile + (threadIdx.x >> 4);
+  const int j = tx * kTile + (threadIdx.x & 15);
+  const bool inside = (i < H) && (j < W);
+  const float px = (float)j + 0.5f, py = (float)i + 0.5f;
+  const int start = tile_offset[ct], end = tile_offset[ct + 1];
+  if (threadIdx.x == 0) s_max = -1;
+  float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f;
+  int last = -1;
+  bool done = !inside;
+  for (int b0 = start; b0 < end; b0 += kRasterThreads) {
+    if (__syncthreads_count(!done) == 0) break;
+    const int e = b0 + threadIdx.x;
+    if (e < end) {
+      const Splat s = rec[ids[e]];
+      s_p0[threadIdx.x] = s.p0;
+      s_p1[threadIdx.x] = s.p1;
+      s_p2[threadIdx.x] = s.p2;
+    }
+    __syncthreads();
+    const int n = min(kRasterThreads, end - b0);
+    if (!done) {
+      for (int k = 0; k < n; ++k) {
+        const float4 p0 = s_p0[k];
+        const float4 p1 = s_p1[k];
+        const float dx = p0.x - px, dy = p0.y - py;
+        const float sigma = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
+        const float alpha = fminf(kAlphaMax, p0.z * __expf(-sigma));
+        if (sigma < 0.f || alpha < kAlphaThreshold) continue;
+        const float nT = T * (1.f - alpha);
+        if (nT <= kTMin) {
+          done = true;
+          break;
+        }
+        const float vis = alpha * T;
+        const float4 p2 = s_p2[k];
+        cr += p2.x * vis;
+        cg += p2.y * vis;
+        cb += p2.z * vis;
+        T = nT;
+        last = b0 + k;
+      }
+    }
+  }
+  if (inside) {
+    const int64_t pix = ((int64_t)c * H + i) * W + j;
+    const float* bgc = bg + c * 3;
+    out_rgb[pix * 3 + 0] = cr + T * bgc[0];
+    out_rgb[pix * 3 + 1] = cg + T * bgc[1];
+    out_rgb[pix * 3 + 2] = cb + T * bgc[2];
+    out_alpha[pix] = 1.f - T;
+    out_T[pix] = T;
+    out_last[pix] = last;
+  }
+  __syncthreads();
+  if (last >= 0) atomicMax(&s_max, last);
+  __syncthreads();
+  if (threadIdx.x == 0) tile_end[ct] = s_max >= 0 ? s_max + 1 : start;
+}
+
+// ---------------------------------------------------------------- 2D forward
+// Reference recursion (src/gaussian_renderer.py:416-425), integer pixel centres:
+//   contrib = g (1 - A);  canvas += contrib * colour;  A += contrib.
+// Once A == 1.0f exactly every later contribution is exactly 0, so stopping there is exact.
+__global__ __launch_bounds__(kRasterThreads) void k_raster2d_fwd(
+    const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
+    int W, int H, int tw, int th, const float* __restrict__ bg, float* __restrict__ out_rgb,
+    float* __restrict__ out_alpha, int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end) {
+  __shared__ float4 s_p0[kRasterThreads];
+  __shared__ float4 s_p1[kRasterThreads];
+  __shared__ float4 s_p2[kRasterThreads];
+  __shared__ int s_max;
+  const int ct = blockIdx.x;
+  int c, ty, tx;
+  tile_coords(ct, tw, th, c, ty, tx);
+  const int i = ty * kTile + (threadIdx.x >> 4);
+  const int j = tx * kTile + (threadIdx.x & 15);
+  const bool inside = (i < H) && (j < W);
+  const float px = (float)j, py = (float)i;
+  const int start = tile_offset[ct], end = tile_offset[ct + 1];
+  if (threadIdx.x == 0) s_max = -1;
+  float A = 0.f, cr = 0.f, cg = 0.f, cb = 0.f;
+  int last = -1;
+  bool done = !inside;
+  for (int b0 = start; b0 < end; b0 += kRasterThreads) {
+    if (__syncthreads_count(!done) == 0) break;
+    const int e = b0 + threadIdx.x;
+    if (e < end) {
+      const Splat s = rec[ids[e]];
+      s_p0[threadIdx.x] = s.p0;
+      s_p1[threadIdx.x] = s.p1;
+      s_p2[threadIdx.x] = s.p2;
+    }
+    __syncthreads();
+    const int n = min(kRasterThreads, end - b0);
+    if (!done) {
+      for (int k = 0; k < n; ++k) {
+        const float4 p0 = s_p0[k];
+        const float4 p1 = s_p1[k];
+        const float4 p2 = s_p2[k];
+        const float dx = p0.x - px, dy = p0.y - py;
+        const float q = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
+        const float g = p0.z * __expf(-q);
+        const float contrib = g * (1.f - A);
+        cr += contrib * p2.x;
+        cg += contrib * p2.y;
+        cb += contrib * p2.z;
+        A += contrib;
+        last = b0 + k;
+        if (A == 1.f) {
+          done = true;
+          break;
+        }
+      }
+    }
+  }
+  if (inside) {
+    const int64_t pix = ((int64_t)c * H + i) * W + j;
+    const float* bgc = bg + c * 3;
+    const float Tr = 1.f - A;
+    out_rgb[pix * 3 + 0] = cr + Tr * bgc[0];
+    out_rgb[pix * 3 + 1] = cg + Tr * bgc[1];
+    out_rgb[pix * 3 + 2] = cb + Tr * bgc[2];
+    out_alpha[pix] = A;
+    out_last[pix] = last;
+  }
+  __syncthreads();
+  if (last >= 0) atomicMax(&s_max, last);
+  __syncthreads();
+  if (threadIdx.x == 0) tile_end[ct] = s_max >= 0 ? s_max + 1 : start;
+}
+
+// ---------------------------------------------------------------- partial combine helpers
+// s_w[v][wave][k]: wave sums for entry k of the current batch.
+struct PartialLds {
+  float w[kPartial][4][kRasterThreads];
+};
+
+__device__ __forceinline__ void wave_emit(PartialLds& L, int k, bool any, float (&gv)[kPartial]) {
+  const int wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  if (any) {
+#pragma unroll
+    for (int v = 0; v < kPartial; ++v) {
+      const float s = wave_sum(gv[v]);
+      if (lane == 0) L.w[v][wv][k] = s;
+    }
+  } else if (lane == 0) {
+#pragma unroll
+    for (int v = 0; v < kPartial; ++v) L.w[v][wv][k] = 0.f;
+  }
+}
+
+__device__ __forceinline__ void block_store_partials(const PartialLds& L, int b0, int n, float* __restrict__ partial) {
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    float* dst = partial + (int64_t)(b0 + k) * kPartial;
+#pragma unroll
+    for (int v = 0; v < kPartial; ++v) dst[v] = (L.w[v][0][k] + L.w[v][1][k]) + (L.w[v][2][k] + L.w[v][3][k]);
+  }
+}
+
+// ---------------------------------------------------------------- 3D backward
+// Back-to-front from each pixel's last contributing entry; T_i recovered as T_{i+1}/(1-a_i)
+// (safe: a <= 0.999), starting from the EXACT final transmittance saved by the forward.
+//   d rgb/d c_i = a_i T_i;  d rgb/d a_i = c_i T_i - (S_i + T_f bg)/(1-a_i);  d alpha/d a_i = T_f/(1-a_i)
+//   a = o e^{-sigma} (unclamped only):  d/do = e^{-sigma},  d/dsigma = -a.
+__global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
+    const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
+    const int32_t* __restrict__ tile_end, const int32_t* __restrict__ busy, int W, int H, int tw, int th,
+    const float* __restrict__ bg, const float* __restrict__ final_T, const int32_t* __restrict__ last_in,
+    const float* __restrict__ v_rgb, const float* __restrict__ v_alpha, float* __restrict__ partial) {
+  __shared__ float4 s_p0[kRasterThreads];
+  __shared__ float4 s_p1[kRasterThreads];
+  __shared__ float4 s_p2[kRasterThreads];
+  __shared__ PartialLds L;
+  const int ct = busy[blockIdx.x];
+  int c, ty, tx;
+  tile_coords(ct, tw, th, c, ty, tx);
+  const int i = ty * kTile + (threadIdx.x >> 4);
+  const int j = tx * kTile + (threadIdx.x & 15);
+  const bool inside = (i < H) && (j < W);
+  const float px = (float)j + 0.5f, py = (float)i + 0.5f;
+  const int start = tile_offset[ct];
+  const int eff = tile_end[ct];
+  float Tf = 1.f, vr = 0.f, vg = 0.f, vb = 0.f, va = 0.f;
+  int last = -1;
+  if (inside) {
+    const int64_t pix = ((int64_t)c * H + i) * W + j;
+    Tf = final_T[pix];
+    last = last_in[pix];
+    vr = v_rgb[pix * 3 + 0];
+    vg = v_rgb[pix * 3 + 1];
+    vb = v_rgb[pix * 3 + 2];
+    va = v_alpha[pix];
+  }
+  const float* bgc = bg + c * 3;
+  const float bgdot = bgc[0] * vr + bgc[1] * vg + bgc[2] * vb;
+  float T = Tf, Sr = 0.f, Sg = 0.f, Sb = 0.f;
+  for (int bend = eff; bend > start; bend -= kRasterThreads) {
+    const int b0 = max(start, bend - kRasterThreads);
+    const int n = bend - b0;
+    __syncthreads();
+    const int e = b0 + threadIdx.x;
+    if (e < bend) {
+      const Splat s = rec[ids[e]];
+      s_p0[threadIdx.x] = s.p0;
+      s_p1[threadIdx.x] = s.p1;
+      s_p2[threadIdx.x] = s.p2;
+    }
+    __syncthreads();
+    for (int k = n - 1; k >= 0; --k) {
+      const int ek = b0 + k;
+      float gv[kPartial];
+#pragma unroll
+      for (int v = 0; v < kPartial; ++v) gv[v] = 0.f;
+      bool valid = ek <= last;
+      if (valid) {
+        const float4 p0 = s_p0[k];
+        const float4 p1 = s_p1[k];
+        const float dx = p0.x - px, dy = p0.y - py;
+        const float sigma = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
+        const float vis = __expf(-sigma);
+        const float raw = p0.z * vis;
+        const float alpha = fminf(kAlphaMax, raw);
+        valid = !(sigma < 0.f || alpha < kAlphaThreshold);
+        if (valid) {
+          const float4 p2 = s_p2[k];
+          const float ra = 1.f / (1.f - alpha);
+          T *= ra;
+          const float fac = alpha * T;
+          gv[6] = fac * vr;
+          gv[7] = fac * vg;
+          gv[8] = fac * vb;
+          const float v_al = (p2.x * T - Sr * ra) * vr + (p2.y * T - Sg * ra) * vg + (p2.z * T - Sb * ra) * vb +
+                             Tf * ra * (va - bgdot);
+          if (raw <= kAlphaMax) {
+            const float v_sig = -raw * v_al;
+            gv[2] = v_sig * dx * dx;
+            gv[3] = v_sig * dx * dy;
+            gv[4] = v_sig * dy * dy;
+            gv[0] = v_sig * (2.f * p1.x * dx + p1.y * dy);
+            gv[1] = v_sig * (p1.y * dx + 2.f * p1.z * dy);
+            gv[5] = vis * v_al;
+          }
+          Sr += p2.x * fac;
+          Sg += p2.y * fac;
+          Sb += p2.z * fac;
+        }
+      }
+      wave_emit(L, k, wave_ballot(valid) != 0, gv);
+    }
+    __syncthreads();
+    block_store_partials(L, b0, n, partial);
+  }
+}
+
+// ---------------------------------------------------------------- 2D backward
+// Adjoint of the reference recursion with lambda = dL/dA_{i+1} (no division, safe when
+// A reaches 1):
+//   dL/dg_i  = T_i (v_C . c_i + lambda_{i+1}),   T_i = 1 - A_i
+//   dL/dc_i  = g_i T_i v_C
+//   lambda_i = lambda_{i+1} (1 - g_i) - g_i (v_C . c_i),   lambda_N = v_alpha - v_rgb . bg
+// A_i comes from a forward replay: A is checkpointed every kChunk entries (workspace), and
+// each chunk is replayed into registers before its backward sweep.
+constexpr int kChunk = 32;
+
+__global__ __launch_bounds__(kRasterThreads) void k_raster2d_bwd(
+    const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
+    const int32_t* __restrict__ tile_end, const int32_t* __restrict__ busy, int W, int H, int tw, int th,
+    const float* __restrict__ bg, const int32_t* __restrict__ last_in, const float* __restrict__ v_rgb,
+    const float* __restrict__ v_alpha, float* __restrict__ ckpt, float* __restrict__ partial) {
+  __shared__ float4 s_p0[kRasterThreads];
+  __shared__ float4 s_p1[kRasterThreads];
+  __shared__ float4 s_p2[kRasterThreads];
+  __shared__ PartialLds L;
+  const int ct = busy[blockIdx.x];
+  int c, ty, tx;
+  tile_coords(ct, tw, th, c, ty, tx);
+  const int i = ty * kTile + (threadIdx.x >> 4);
+  const int j = tx * kTile + (threadIdx.x & 15);
+  const bool inside = (i < H) && (j < W);
+  const float px = (float)j, py = (float)i;
+  const int start = tile_offset[ct];
+  const int eff = tile_end[ct];
+  const int len = eff - start;
+  if (len <= 0) return;
+  float* ck = ckpt + ((int64_t)(start / kChunk) + ct) * kRasterThreads;
+  float vr = 0.f, vg = 0.f, vb = 0.f, va = 0.f;
+  int last = -1;
+  if (inside) {
+    const int64_t pix = ((int64_t)c * H + i) * W + j;
+    last = last_in[pix];
+    vr = v_rgb[pix * 3 + 0];
+    vg = v_rgb[pix * 3 + 1];
+    vb = v_rgb[pix * 3 + 2];
+    va = v_alpha[pix];
+  }
+  const float* bgc = bg + c * 3;
+  // ---- pass 1: forward replay, checkpoint A before every chunk
+  float A = 0.f;
+  for (int b0 = start; b0 < eff; b0 += kRasterThreads) {
+    __syncthreads();
+    const int e = b0 + threadIdx.x;
+    if (e < eff) {
+      const Splat s = rec[ids[e]];
+      s_p0[threadIdx.x] = s.p0;
+      s_p1[threadIdx.x] = s.p1;
+    }
+    __syncthreads();
+    const int n = min(kRasterThreads, eff - b0);
+    for (int k = 0; k < n; ++k) {
+      const int ek = b0 + k;
+      if (((ek - start) % kChunk) == 0) ck[((ek - start) / kChunk) * kRasterThreads + threadIdx.x] = A;
+      if (ek <= last) {
+        const float4 p0 = s_p0[k];
+        const float4 p1 = s_p1[k];
+        const float dx = p0.x - px, dy = p0.y - py;
+        const float q = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
+        const float g = p0.z * __expf(-q);
+        A += g * (1.f - A);
+      }
+    }
+  }
+  // ---- pass 2: backward, chunk by chunk from the end
+  float lam = va - (bgc[0] * vr + bgc[1] * vg + bgc[2] * vb);
+  const int nchunks = (len + kChunk - 1) / kChunk;
+  int loaded_b0 = -1;
+  for (int q = nchunks - 1; q >= 0; --q) {
+    const int c0 = start + q * kChunk;
+    const int cn = min(kChunk, eff - c0);
+    // stage the 256-entry batch containing this chunk (batches aligned at start + 256*m)
+    const int b0 = start + ((q * kChunk) / kRasterThreads) * kRasterThreads;
+    if (b0 != loaded_b0) {
+      __syncthreads();
+      if (loaded_b0 >= 0) block_store_partials(L, loaded_b0, min(kRasterThreads, eff - loaded_b0), partial);
+      __syncthreads();
+      const int e = b0 + threadIdx.x;
+      if (e < eff) {
+        const Splat s = rec[ids[e]];
+        s_p0[threadIdx.x] = s.p0;
+        s_p1[threadIdx.x] = s.p1;
+        s_p2[threadIdx.x] = s.p2;
+      }
+      loaded_b0 = b0;
+      __syncthreads();
+    }
+    const int kb = c0 - b0;   // chunk offset inside the batch
+    // replay this chunk's A_i into registers
+    float Ai[kChunk];
+    float a_run = ck[q * kRasterThreads + threadIdx.x];
+#pragma unroll
+    for (int k = 0; k < kChunk; ++k) {
+      Ai[k] = a_run;
+      if (k < cn && c0 + k <= last) {
+        const float4 p0 = s_p0[kb + k];
+        const float4 p1 = s_p1[kb + k];
+        const float dx = p0.x - px, dy = p0.y - py;
+        const float qq = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
+        const float g = p0.z * __expf(-qq);
+        a_run += g * (1.f - a_run);
+      }
+    }
+#pragma unroll
+    for (int k = kChunk - 1; k >= 0; --k) {
+      if (k < cn) {
+        const int ek = c0 + k;
+        float gv[kPartial];
+#pragma unroll
+        for (int v = 0; v < kPartial; ++v) gv[v] = 0.f;
+        const bool valid = ek <= last;
+        if (valid) {
+          const float4 p0 = s_p0[kb + k];
+          const float4 p1 = s_p1[kb + k];
+          const float4 p2 = s_p2[kb + k];
+          const float dx = p0.x - px, dy = p0.y - py;
+          const float qq = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
+          const float e_ = __expf(-qq);
+          const float g = p0.z * e_;
+          const float Ti = 1.f - Ai[k];
+          const float wc = vr * p2.x + vg * p2.y + vb * p2.z;
+          const float v_g = Ti * (wc + lam);
+          gv[6] = g * Ti * vr;
+          gv[7] = g * Ti * vg;
+          gv[8] = g * Ti * vb;
+          gv[5] = e_ * v_g;
+          const float v_q = -g * v_g;
+          gv[2] = v_q * dx * dx;
+          gv[3] = v_q * dx * dy;
+          gv[4] = v_q * dy * dy;
+          gv[0] = v_q * (2.f * p1.x * dx + p1.y * dy);
+          gv[1] = v_q * (p1.y * dx + 2.f * p1.z * dy);
+          lam = lam * (1.f - g) - g * wc;
+        }
+        wave_emit(L, kb + k, wave_ballot(valid) != 0, gv);
+      }
+    }
+  }
+  __syncthreads();
+  if (loaded_b0 >= 0) block_store_partials(L, loaded_b0, min(kRasterThreads, eff - loaded_b0), partial);
+}
+
+}  // namespace gsr
+
+using namespace gsr;
+
+extern "C" {
+
+int gsr3d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset, int C, int width,
+                     int height, const float* bg, float* rgb, float* alpha, float* final_T, int32_t* last,
+                     int32_t* tile_end, void* stream) {
+  GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "gsr3d_raster_fwd: bad C=%d or image %dx%d", C, width, height);
+  const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
+  const int64_t CT = (int64_t)C * tw * th;
+  GSR_REQUIRE(CT < (1ll << 31), "gsr3d_raster_fwd: too many tiles");
+  hipLaunchKernelGGL(k_raster3d_fwd, dim3((unsigned)CT), dim3(kRasterThreads), 0, (hipStream_t)stream,
+                     (const Splat*)rec, sorted_ids, tile_offset, width, height, tw, th, bg, rgb, alpha, final_T,
+                     last, tile_end);
+  GSR_LAUNCH_CHECK("k_raster3d_fwd");
+  return GSR_OK;
+}
+
+int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
+                     const int32_t* tile_end, const int32_t* busy_tiles, int32_t n_busy, int C, int width,
+                     int height, const float* bg, const float* final_T, const int32_t* last, const float* v_rgb,
+                     const float* v_alpha, float* partial, void* stream) {
+  GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "gsr3d_raster_bwd: bad C=%d or image %dx%d", C, width, height);
+  GSR_REQUIRE(n_busy >= 0, "gsr3d_raster_bwd: bad n_busy");
+  if (n_busy == 0) return GSR_OK;
+  const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
+  hipLaunchKernelGGL(k_raster3d_bwd, dim3(n_busy), dim3(kRasterThreads), 0, (hipStream_t)stream,
+                     (const Splat*)rec, sorted_ids, tile_offset, tile_end, busy_tiles, width, height, tw, th, bg,
+                     final_T, last, v_rgb, v_alpha, partial);
+  GSR_LAUNCH_CHECK("k_raster3d_bwd");
+  return GSR_OK;
+}
+
+int gsr2d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset, int width,
+                     int height, const float* bg, float* rgb, float* alpha, int32_t* last, int32_t* tile_end,
+                     void* stream) {
+  GSR_REQUIRE(width > 0 && height > 0, "gsr2d_raster_fwd: bad image %dx%d", width, height);
+  const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
+  hipLaunchKernelGGL(k_raster2d_fwd, dim3(tw * th), dim3(kRasterThreads), 0, (hipStream_t)stream,
+                     (const Splat*)rec, sorted_ids, tile_offset, width, height, tw, th, bg, rgb, alpha, last,
+                     tile_end);
+  GSR_LAUNCH_CHECK("k_raster2d_fwd");
+  return GSR_OK;
+}
+
+size_t gsr2d_raster_bwd_workspace(int64_t n_isect, int64_t CT) {
+  return (size_t)((n_isect / kChunk + CT + 2) * kRasterThreads * sizeof(float));
+}
+
+int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
+                     const int32_t* tile_end, const int32_t* busy_tiles, int32_t n_busy, int width, int height,
+                     const float* bg, const int32_t* last, const float* v_rgb, const float* v_alpha, void* workspace,
+                     size_t workspace_bytes, float* partial, void* stream) {
+  GSR_REQUIRE(width > 0 && height > 0, "gsr2d_raster_bwd: bad image %dx%d", width, height);
+  if (n_busy <= 0) return GSR_OK;
+  const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
+  (void)workspace_bytes;
+  hipLaunchKernelGGL(k_raster2d_bwd, dim3(n_busy), dim3(kRasterThreads), 0, (hipStream_t)stream,
+                     (const Splat*)rec, sorted_ids, tile_offset, tile_end, busy_tiles, width, height, tw, th, bg,
+                     last, v_rgb, v_alpha, (float*)workspace, partial);
+  GSR_LAUNCH_CHECK("k_raster2d_bwd");
+  return GSR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,153 @@
+"""Generate golden fixtures by importing the REFERENCE (build container only).
+
+Run from /tmp so nothing is written into the read-only reference tree:
+
+    cd /tmp && PYTHONDONTWRITEBYTECODE=1 python /root/repo/tests/golden/make_golden.py
+
+Outputs (committed, small .npz data files — inputs and expected outputs only):
+
+* ref2d_<case>.npz  — GaussianRenderer2D.render (src/gaussian_renderer.py:269-427):
+  params, background, rgb, alpha, and d(loss)/d(params) for fixed cotangents
+  loss = sum(rgb * v_rgb) + sum(alpha * v_alpha).
+* ref3d_adapter.npz — what GaussianRenderer3D.render (src/gaussian_renderer.py:157-211)
+  passes to gsplat's ``rasterization``: activated means/quats/scales/opacities/colors,
+  captured with a recording stub installed as ``gsplat.rendering`` BEFORE the import
+  (gsplat itself is absent from this container), plus the adapter's autograd
+  (grads of the raw [N,14] params for fixed cotangents on every captured tensor).
+
+The reference never travels to the GPU box; only these fixtures do.
+"""
+from __future__ import annotations
+
+import math
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _params2d(n, w, h, seed, scale_mu=0.4, scale_sd=0.3, spread=1.0):
+    g = torch.Generator().manual_seed(seed)
+    p = torch.empty(n, 9)
+    p[:, 0] = torch.rand(n, generator=g) * w * spread - (spread - 1) * w / 2
+    p[:, 1] = torch.rand(n, generator=g) * h * spread - (spread - 1) * h / 2
+    p[:, 2:4] = scale_mu + scale_sd * torch.randn(n, 2, generator=g)
+    p[:, 4] = (torch.rand(n, generator=g) * 2 - 1) * math.pi
+    p[:, 5:8] = torch.rand(n, 3, generator=g) * 1.4 - 0.2   # exercises clamp(0,1)
+    p[:, 8] = 2.0 * torch.randn(n, generator=g)
+    return p
+
+
+def make_2d():
+    sys.path.insert(0, REF)
+    from src.gaussian_renderer import GaussianRenderer2D  # noqa: E402  (reference import)
+
+    cases = [
+        # name, N, W, H, bg, seed, kwargs for _params2d
+        ("n1_64x48_black", 1, 64, 48, (0.0, 0.0, 0.0), 11, {}),
+        ("n2_64x48_white", 2, 64, 48, (1.0, 1.0, 1.0), 12, {}),
+        ("n40_64x48_white", 40, 64, 48, (1.0, 1.0, 1.0), 13, {"scale_mu": 1.0, "scale_sd": 0.5}),
+        ("n40_96x80_grey", 40, 96, 80, (0.3, 0.6, 0.9), 14, {"scale_mu": 1.2, "scale_sd": 0.6}),
+        ("n256_96x80_white", 256, 96, 80, (1.0, 1.0, 1.0), 15, {}),
+        ("n256_96x80_dense", 256, 96, 80, (1.0, 1.0, 1.0), 16, {"scale_mu": 1.5, "scale_sd": 0.4}),
+        ("n64_offscreen_64x48", 64, 64, 48, (0.0, 0.0, 0.0), 17, {"spread": 2.0}),
+    ]
+    for name, n, w, h, bg, seed, kw in cases:
+        r = GaussianRenderer2D(w, h, device="cpu")
+        r.set_background_color(torch.tensor(bg, dtype=torch.float32))
+        params = _params2d(n, w, h, seed, **kw).requires_grad_(True)
+        rgb, alpha = r.render(params, None, None)
+        gen = torch.Generator().manual_seed(seed + 1)
+        v_rgb = torch.randn(h, w, 3, generator=gen)
+        v_alpha = torch.randn(h, w, generator=gen)
+        ((rgb * v_rgb).sum() + (alpha * v_alpha).sum()).backward()
+        np.savez_compressed(
+            os.path.join(OUT, f"ref2d_{name}.npz"),
+            params=params.detach().numpy(), background=np.array(bg, np.float32),
+            width=w, height=h, rgb=rgb.detach().numpy(), alpha=alpha.detach().numpy(),
+            v_rgb=v_rgb.numpy(), v_alpha=v_alpha.numpy(), grad=params.grad.numpy())
+        print("2d", name, "rgb max", float(rgb.max()), "alpha max", float(alpha.max()))
+
+    # Known-answer: a single Gaussian at the pixel centre (tests/test_gaussian_renderer.py:58-87)
+    r = GaussianRenderer2D(256, 256, device="cpu")
+    p = torch.tensor([[128.0, 128.0, 1.0, 1.0, 0.0, 1.0, 0.0, 0.0, 2.0]])
+    rgb, alpha = r.render(p, None, None)
+    np.savez_compressed(os.path.join(OUT, "ref2d_kat_centre.npz"), params=p.numpy(),
+                        background=np.zeros(3, np.float32), width=256, height=256,
+                        rgb_centre=rgb[128, 128].numpy(), alpha_centre=alpha[128, 128].numpy(),
+                        alpha_corner=alpha[0, 0].numpy())
+    print("kat centre", rgb[128, 128].tolist())
+
+
+def make_3d_adapter():
+    captured = {}
+
+    def rasterization(**kw):
+        captured.update(kw)
+        c = kw["viewmats"].shape[0]
+        H, W = kw["height"], kw["width"]
+        # Return something differentiable in every captured tensor so that the adapter's
+        # own autograd (exp / normalise / clamp / sigmoid) can be recorded.
+        s = (kw["means"] * w_means).sum() + (kw["quats"] * w_quats).sum() + \
+            (kw["scales"] * w_scales).sum() + (kw["opacities"] * w_op).sum() + \
+            (kw["colors"] * w_col).sum()
+        rgb = s * torch.ones(c, H, W, 3) / (H * W * 3)
+        alpha = torch.zeros(c, H, W, 1)
+        return rgb, alpha, {}
+
+    gs = types.ModuleType("gsplat")
+    gsr = types.ModuleType("gsplat.rendering")
+    gsr.rasterization = rasterization
+    gs.rendering = gsr
+    sys.modules["gsplat"] = gs
+    sys.modules["gsplat.rendering"] = gsr
+    sys.path.insert(0, REF)
+    for k in [m for m in sys.modules if m == "src" or m.startswith("src.")]:
+        del sys.modules[k]
+    from src.gaussian_renderer import GaussianRenderer3D  # noqa: E402
+
+    n = 64
+    g = torch.Generator().manual_seed(2024)
+    w_means = torch.randn(n, 3, generator=g)
+    w_quats = torch.randn(n, 4, generator=g)
+    w_scales = torch.randn(n, 3, generator=g)
+    w_op = torch.randn(n, generator=g)
+    w_col = torch.randn(n, 3, generator=g)
+    params = torch.randn(n, 14, generator=g)
+    params[:, 3:6] = -5.0 + 0.5 * params[:, 3:6]
+    params[:, 10:13] = params[:, 10:13] * 0.8 + 0.5   # straddles the clamp bounds
+    params[5, 6:10] = 0.0                              # zero quaternion: the +1e-8 guard
+    params = params.requires_grad_(True)
+    r = GaussianRenderer3D(32, 24, device="cpu")
+    viewmat = torch.eye(4)
+    K = torch.tensor([[30.0, 0, 16], [0, 30.0, 12], [0, 0, 1]])
+    rgb, alpha = r.render(params, viewmat, K)
+    rgb.sum().backward()
+    np.savez_compressed(
+        os.path.join(OUT, "ref3d_adapter.npz"),
+        params=params.detach().numpy(),
+        means=captured["means"].detach().numpy(),
+        means_stride=np.array(captured["means"].stride()),
+        quats=captured["quats"].detach().numpy(),
+        scales=captured["scales"].detach().numpy(),
+        opacities=captured["opacities"].detach().numpy(),
+        colors=captured["colors"].detach().numpy(),
+        viewmats_shape=np.array(captured["viewmats"].shape),
+        Ks_shape=np.array(captured["Ks"].shape),
+        packed=np.array(bool(captured["packed"])),
+        backgrounds=captured["backgrounds"].detach().numpy(),
+        w_means=w_means.numpy(), w_quats=w_quats.numpy(), w_scales=w_scales.numpy(),
+        w_op=w_op.numpy(), w_col=w_col.numpy(), grad=params.grad.numpy(),
+        out_shapes=np.array([list(rgb.shape) + [0], list(alpha.shape) + [0, 0]]))
+    print("3d adapter captured keys", sorted(captured))
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(8)
+    make_2d()
+    make_3d_adapter()

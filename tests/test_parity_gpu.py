@@ -1,0 +1,322 @@
+"""HIP path (libgsr.so through the C ABI) vs the CPU oracle and the reference fixtures.
+
+Tolerances (BASELINE.json north_star: 1e-4 relative fp32):
+  * forward rgb/alpha: |a-e| <= 1e-4*|e| + 1e-6 (abs floor for near-zero background pixels)
+  * gradients: |a-e| <= 1e-4*|e| + 1e-5*max|e| (abs floor scaled to the tensor: per-pixel
+    sums are accumulated in a different order on the GPU)
+  * integer work (tile lists, offsets, intersection counts): bit-exact.
+3D discrete decisions (alpha >= 1/255 skip, T <= 1e-4 stop) can flip on fp32 ties between
+two correct implementations; the large-scene tests allow a tiny fraction of flipped pixels
+(bounded by one Gaussian's contribution) and report it.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from _util import assert_close, grad_close
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle3d():
+    from oracle import oracle3d
+    return oracle3d
+
+
+def _scene3d(N, W, H, C, seed, extent=0.11, scale_shift=0.0):
+    from gsr.scenes import gaussians3d, ring_cameras
+    p = gaussians3d(N, seed, extent=extent)
+    p[:, 3:6] += scale_shift
+    V, K = ring_cameras(C, W, H)
+    return p, V, K
+
+
+def _run_gpu3d(p, V, K, W, H, bg, cuda, v_rgb=None, v_alpha=None, radius_mode="opacity_aabb"):
+    from src.gaussian_renderer import GaussianRenderer3D
+    r = GaussianRenderer3D(W, H, device="cuda", radius_mode=radius_mode)
+    r.set_background_color(bg.to(cuda))
+    pg = p.to(cuda).requires_grad_(True)
+    rgb, alpha = r.render(pg, V.to(cuda), K.to(cuda))
+    grad = None
+    if v_rgb is not None:
+        ((rgb * v_rgb.to(cuda)).sum() + (alpha * v_alpha.to(cuda)).sum()).backward()
+        grad = pg.grad.detach().cpu()
+    return rgb.detach().cpu(), alpha.detach().cpu(), grad
+
+
+def _run_oracle3d(p, V, K, W, H, bg, v_rgb=None, v_alpha=None, radius_mode=0):
+    o = _oracle3d()
+    pc = p.clone().requires_grad_(True)
+    rgb, alpha = o.render3d(pc, V, K, W, H, bg, radius_mode=radius_mode)
+    grad = None
+    if v_rgb is not None:
+        ((rgb * v_rgb).sum() + (alpha * v_alpha).sum()).backward()
+        grad = pc.grad.detach()
+    return rgb.detach(), alpha.detach(), grad
+
+
+def _cot(C, H, W, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(C, H, W, 3, generator=g), torch.randn(C, H, W, generator=g)
+
+
+@pytest.mark.parametrize("N,W,H,C,seed,shift", [
+    (1, 32, 24, 1, 1, 2.0),
+    (12, 40, 32, 1, 2, 2.5),
+    (200, 48, 40, 2, 3, 1.0),
+    (2000, 96, 80, 3, 4, 0.0),
+])
+def test_3d_small_vs_oracle(cuda, N, W, H, C, seed, shift):
+    p, V, K = _scene3d(N, W, H, C, seed, extent=0.05, scale_shift=shift)
+    bg = torch.tensor([0.1, 0.5, 0.9])
+    vr, va = _cot(C, H, W, seed + 100)
+    rgb_g, a_g, g_g = _run_gpu3d(p, V, K, W, H, bg, cuda, vr, va)
+    rgb_o, a_o, g_o = _run_oracle3d(p, V, K, W, H, bg, vr, va)
+    assert_close(rgb_g, rgb_o, what="rgb")
+    assert_close(a_g, a_o, what="alpha")
+    grad_close(g_g, g_o, what="grad")
+
+
+def test_3d_multiview_equals_single_views(cuda):
+    W, H, C = 64, 48, 4
+    p, V, K = _scene3d(3000, W, H, C, 7)
+    bg = torch.ones(3)
+    rgb_b, a_b, _ = _run_gpu3d(p, V, K, W, H, bg, cuda)
+    for c in range(C):
+        rgb_c, a_c, _ = _run_gpu3d(p, V[c:c + 1], K[c:c + 1], W, H, bg, cuda)
+        assert torch.equal(rgb_b[c], rgb_c[0]) and torch.equal(a_b[c], a_c[0])
+
+
+def test_3d_deterministic(cuda):
+    W, H, C = 96, 80, 2
+    p, V, K = _scene3d(20000, W, H, C, 8)
+    bg = torch.ones(3)
+    vr, va = _cot(C, H, W, 9)
+    r1 = _run_gpu3d(p, V, K, W, H, bg, cuda, vr, va)
+    r2 = _run_gpu3d(p, V, K, W, H, bg, cuda, vr, va)
+    for a, b in zip(r1, r2):
+        assert torch.equal(a, b)
+
+
+def test_3d_binning_exact(cuda):
+    """Tile lists are integer work: compare bit-exactly with a CPU re-sort of the GPU's own
+    projection output (rect + depth bits), and the rects with the oracle's projection."""
+    from gsr import render as R
+    W, H, C = 192, 170, 2
+    p, V, K = _scene3d(10000, W, H, C, 11)
+    rgb, alpha, b, _ = R.debug_forward3d(p.to(cuda), V.to(cuda), K.to(cuda), torch.ones(3, device=cuda), W, H)
+    N = p.shape[0]
+    rect = b.rect.cpu().view(C * N, 2).to(torch.int64) & 0xFFFFFFFF
+    x0, x1 = rect[:, 0] & 0xFFFF, rect[:, 0] >> 16
+    y0, y1 = rect[:, 1] & 0xFFFF, rect[:, 1] >> 16
+    cnt = b.cnt.cpu().to(torch.int64)
+    assert torch.equal(cnt, (x1 - x0) * (y1 - y0))
+    depth = b.rec.cpu().view(C * N, 12)[:, 3].contiguous()
+    tw, th = (W + 15) // 16, (H + 15) // 16
+    T = tw * th
+    # expected lists: (camera, tile) then (depth bits, c*N+n)
+    keys = []
+    for cn in torch.nonzero(cnt > 0).flatten().tolist():
+        c = cn // N
+        dbits = int(np.float32(depth[cn].item()).view(np.uint32))
+        for ty in range(int(y0[cn]), int(y1[cn])):
+            for tx in range(int(x0[cn]), int(x1[cn])):
+                keys.append((c * T + ty * tw + tx, dbits, cn))
+    keys.sort()
+    exp_ids = torch.tensor([k[2] for k in keys], dtype=torch.int64)
+    exp_tiles = torch.tensor([k[0] for k in keys], dtype=torch.int64)
+    I = b.n_isect
+    assert I == len(keys)
+    assert torch.equal(b.sorted_ids.cpu()[:I].to(torch.int64), exp_ids)
+    exp_off = torch.zeros(C * T + 1, dtype=torch.int64)
+    exp_off[1:] = torch.cumsum(torch.bincount(exp_tiles, minlength=C * T), 0)
+    assert torch.equal(b.tile_off.cpu().to(torch.int64), exp_off)
+    # inverse map: pos[off[cn] + j] = sorted position
+    pos = b.pos.cpu()[:I].to(torch.int64)
+    off = b.isect_off.cpu().to(torch.int64)
+    ids = b.sorted_ids.cpu()[:I].to(torch.int64)
+    assert torch.equal(ids[pos], torch.repeat_interleave(torch.arange(C * N), cnt))
+    # projection rects vs the oracle's (float decisions: near-total agreement)
+    o = _oracle3d()
+    m, q, s, col, op = o.activations3d(p)
+    pr = o.project3d(m, q, s, op, V, K, W, H)
+    _, oids = o.isect_tiles(pr.means2d, pr.radii, pr.depths, W, H)
+    agree = float((cnt.view(C, N) == 0).eq(~pr.valid).double().mean())
+    assert agree > 0.999, agree
+    assert abs(len(oids) - I) <= max(5, I // 2000)
+
+
+def test_3d_cfg1_vs_oracle(cuda):
+    """BASELINE config 1 scene (10k Gaussians, 192x170, 1 view) fwd+bwd vs the oracle."""
+    from gsr.scenes import CONFIGS, gaussians3d, ring_cameras
+    c = CONFIGS[1]
+    p = gaussians3d(c.N, c.seed)
+    V, K = ring_cameras(c.views, c.width, c.height)
+    bg = torch.ones(3)
+    vr, va = _cot(1, c.height, c.width, 5)
+    rgb_g, a_g, g_g = _run_gpu3d(p, V, K, c.width, c.height, bg, cuda, vr, va)
+    rgb_o, a_o, g_o = _run_oracle3d(p, V, K, c.width, c.height, bg, vr, va)
+    r = assert_close(rgb_g, rgb_o, max_frac=2e-4, max_outlier=0.02, what="rgb")
+    assert_close(a_g, a_o, max_frac=2e-4, max_outlier=0.02, what="alpha")
+    grad_close(g_g, g_o, max_frac=2e-3, what="grad")
+    # PSNR of the rendering against the oracle render must agree to 0.05 dB vs any target
+    tgt = (rgb_o + 0.05 * torch.randn(rgb_o.shape, generator=torch.Generator().manual_seed(1))).clamp(0, 1)
+    psnr = lambda x: float(10 * torch.log10(1.0 / ((x - tgt) ** 2).mean()))
+    assert abs(psnr(rgb_g) - psnr(rgb_o)) < 0.05, r
+
+
+def test_3d_isotropic_radius_mode(cuda):
+    W, H = 64, 48
+    p, V, K = _scene3d(500, W, H, 1, 21, extent=0.05, scale_shift=1.0)
+    bg = torch.zeros(3)
+    vr, va = _cot(1, H, W, 22)
+    rgb_g, a_g, g_g = _run_gpu3d(p, V, K, W, H, bg, cuda, vr, va, radius_mode="isotropic_3sigma")
+    rgb_o, a_o, g_o = _run_oracle3d(p, V, K, W, H, bg, vr, va, radius_mode=1)
+    assert_close(rgb_g, rgb_o, what="rgb")
+    grad_close(g_g, g_o, what="grad")
+
+
+def test_3d_edge_cases(cuda):
+    W, H = 48, 40
+    p, V, K = _scene3d(64, W, H, 1, 31, extent=0.05, scale_shift=1.5)
+    bg = torch.tensor([0.2, 0.3, 0.4])
+    # push some behind the camera, some far off-screen, some huge, one zero-opacity-ish
+    cam_pos = -V[0, :3, :3].T @ V[0, :3, 3]
+    p[0:8, 0:3] = cam_pos * 2.0           # behind the camera
+    p[8:16, 0:3] = torch.tensor([5.0, 5.0, 5.0])
+    p[16:20, 3:6] = -1.0                  # huge (covers the image)
+    p[20:24, 13] = -8.0                   # opacity < 1/255: culled by the opacity-aware rule
+    vr, va = _cot(1, H, W, 32)
+    rgb_g, a_g, g_g = _run_gpu3d(p, V, K, W, H, bg, cuda, vr, va)
+    rgb_o, a_o, g_o = _run_oracle3d(p, V, K, W, H, bg, vr, va)
+    assert_close(rgb_g, rgb_o, what="rgb")
+    grad_close(g_g, g_o, what="grad")
+    # nothing visible at all → background, zero grads
+    q = p.clone()
+    q[:, 0:3] = cam_pos * 2.0
+    rgb_g, a_g, g_g = _run_gpu3d(q, V, K, W, H, bg, cuda, vr, va)
+    assert torch.allclose(rgb_g, bg.view(1, 1, 3).expand_as(rgb_g))
+    assert float(a_g.abs().max()) == 0.0 and float(g_g.abs().max()) == 0.0
+
+
+def test_3d_long_tile_lists(cuda):
+    """> 16384 entries in one tile list: exercises the run-sort + global merge path."""
+    W, H = 32, 32
+    N = 40000
+    p, V, K = _scene3d(N, W, H, 1, 41, extent=0.004)
+    p[:, 13] = -3.5                       # faint, so pixels terminate late
+    bg = torch.zeros(3)
+    vr, va = _cot(1, H, W, 42)
+    from gsr import render as R
+    rgb_g, a_g, g_g = _run_gpu3d(p, V, K, W, H, bg, cuda, vr, va)
+    st = R.last_stats()
+    assert st["max_seg"] > 16384, st
+    rgb_o, a_o, g_o = _run_oracle3d(p, V, K, W, H, bg, vr, va)
+    assert_close(rgb_g, rgb_o, max_frac=1e-3, max_outlier=0.02, what="rgb")
+    grad_close(g_g, g_o, max_frac=2e-3, what="grad")
+
+
+# ------------------------------------------------------------------------------------ 2D
+
+def _golden(name):
+    import os
+    d = os.path.join(os.path.dirname(__file__), "golden")
+    return np.load(os.path.join(d, f"ref2d_{name}.npz"))
+
+
+GOLDEN_2D = ["n1_64x48_black", "n2_64x48_white", "n40_64x48_white", "n40_96x80_grey",
+             "n256_96x80_white", "n256_96x80_dense", "n64_offscreen_64x48"]
+
+
+def _run_gpu2d(p, W, H, bg, cuda, v_rgb=None, v_alpha=None):
+    from src.gaussian_renderer import GaussianRenderer2D
+    r = GaussianRenderer2D(W, H, device="cuda")
+    r.set_background_color(bg.to(cuda))
+    pg = p.to(cuda).requires_grad_(True)
+    rgb, alpha = r.render(pg, None, None)
+    grad = None
+    if v_rgb is not None:
+        ((rgb * v_rgb.to(cuda)).sum() + (alpha * v_alpha.to(cuda)).sum()).backward()
+        grad = pg.grad.detach().cpu()
+    return rgb.detach().cpu(), alpha.detach().cpu(), grad
+
+
+@pytest.mark.parametrize("name", GOLDEN_2D)
+def test_2d_vs_reference_golden(cuda, name):
+    z = _golden(name)
+    W, H = int(z["width"]), int(z["height"])
+    p = torch.from_numpy(z["params"])
+    bg = torch.from_numpy(z["background"])
+    rgb, alpha, grad = _run_gpu2d(p, W, H, bg, cuda, torch.from_numpy(z["v_rgb"]), torch.from_numpy(z["v_alpha"]))
+    assert_close(rgb, torch.from_numpy(z["rgb"]), what="rgb")
+    assert_close(alpha, torch.from_numpy(z["alpha"]), what="alpha")
+    grad_close(grad, torch.from_numpy(z["grad"]), what="grad")
+
+
+def test_2d_kat_centre(cuda):
+    z = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "ref2d_kat_centre.npz"))
+    rgb, alpha, _ = _run_gpu2d(torch.from_numpy(z["params"]), 256, 256, torch.zeros(3), cuda)
+    assert abs(float(rgb[128, 128, 0]) - 0.8807970285415649) < 1e-6
+    assert float(rgb[128, 128, 1]) == 0.0 and float(rgb[128, 128, 2]) == 0.0
+    assert abs(float(alpha[0, 0]) - float(z["alpha_corner"])) < 1e-6
+
+
+def _oracle2d(p, W, H, bg, vr, va):
+    from oracle.oracle2d import render2d_dense
+    pc = p.clone().requires_grad_(True)
+    rgb, alpha = render2d_dense(pc, W, H, bg)
+    ((rgb * vr).sum() + (alpha * va).sum()).backward()
+    return rgb.detach(), alpha.detach(), pc.grad.detach()
+
+
+@pytest.mark.parametrize("N,W,H,seed,mu", [(3000, 128, 96, 51, 0.4), (1500, 64, 64, 52, 1.8)])
+def test_2d_vs_oracle_dense(cuda, N, W, H, seed, mu):
+    from gsr.scenes import gaussians2d
+    p = gaussians2d(N, W, H, seed)
+    p[:, 2:4] += mu - 0.4
+    bg = torch.ones(3)
+    g = torch.Generator().manual_seed(seed)
+    vr, va = torch.randn(H, W, 3, generator=g), torch.randn(H, W, generator=g)
+    rgb, alpha, grad = _run_gpu2d(p, W, H, bg, cuda, vr, va)
+    rgb_o, a_o, g_o = _oracle2d(p, W, H, bg, vr, va)
+    assert_close(rgb, rgb_o, what="rgb")
+    assert_close(alpha, a_o, what="alpha")
+    grad_close(grad, g_o, what="grad")
+
+
+def test_2d_saturation_and_long_lists(cuda):
+    """Opaque stacks drive A to exactly 1.0f (exact early stop + division-free backward);
+    > 2048-entry lists exercise several checkpoint chunks, > 16384 the merge sort."""
+    W, H = 32, 32
+    N = 20000
+    g = torch.Generator().manual_seed(61)
+    p = torch.empty(N, 9)
+    p[:, 0:2] = 8.0 + torch.rand(N, 2, generator=g) * 16.0
+    p[:, 2:4] = 1.0 + 0.3 * torch.randn(N, 2, generator=g)
+    p[:, 4] = torch.rand(N, generator=g) * 6.28
+    p[:, 5:8] = torch.rand(N, 3, generator=g)
+    p[:, 8] = torch.randn(N, generator=g) * 3.0
+    p[:50, 8] = 20.0                       # sigmoid == 1.0f exactly
+    bg = torch.tensor([0.0, 1.0, 0.0])
+    vr, va = torch.randn(H, W, 3, generator=g), torch.randn(H, W, generator=g)
+    rgb, alpha, grad = _run_gpu2d(p, W, H, bg, cuda, vr, va)
+    from gsr import render as R
+    assert R.last_stats()["max_seg"] > 16384
+    rgb_o, a_o, g_o = _oracle2d(p, W, H, bg, vr, va)
+    assert_close(rgb, rgb_o, what="rgb")
+    assert_close(alpha, a_o, what="alpha")
+    grad_close(grad, g_o, what="grad")
+
+
+def test_2d_deterministic(cuda):
+    from gsr.scenes import gaussians2d
+    W, H = 192, 160
+    p = gaussians2d(30000, W, H, 71)
+    g = torch.Generator().manual_seed(72)
+    vr, va = torch.randn(H, W, 3, generator=g), torch.randn(H, W, generator=g)
+    a = _run_gpu2d(p, W, H, torch.ones(3), cuda, vr, va)
+    b = _run_gpu2d(p, W, H, torch.ones(3), cuda, vr, va)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
