@@ -1,0 +1,250 @@
+#!/usr/bin/env python3
+"""Benchmark: rendered frames/s (fwd+bwd) of the MI355X rasterizer on BASELINE config 3.
+
+A "step" = one full pass of the hot path over one batch of synthetic input: projection →
+tile binning (incl. its one 16-byte host read) → raster fwd → raster bwd (fixed random
+cotangents) → projection bwd, for the 6 cameras of config 3 (3D, 200k Gaussians, 576x512)
+— the shape BASELINE.json's north-star target is quoted on.  Inputs are resident in HBM
+before the timed region.  value = views (frames) rendered fwd+bwd per second, summed over
+ranks.
+
+Multi-GPU (torchrun, one process per GPU, RCCL): every rank renders 6 cameras of its own
+(ring azimuths offset per rank) of the SAME Gaussian set and the per-rank parameter
+gradients are all-reduced (SUM) — the one real exchange of multi-view training.  Per-GPU
+work is fixed as N grows → "scaling": "weak".
+
+Also reported: the dominant kernel's roofline (algorithmic bytes per launch, SURVEY.md
+§8(d), over its HIP-event-timed average duration) and the CPU baseline (the oracle, a
+restatement of the reference semantics, timed on a bounded sample on this host).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "pose-splatter_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the CPU oracle timing")
+    ap.add_argument("--cpu-views", type=int, default=1, help="views in the bounded CPU sample")
+    ap.add_argument("--traffic-csv", default=None,
+                    help="rocprofv3 --pmc counter_collection.csv to fill roofline.traffic")
+    return ap.parse_args()
+
+
+def algorithmic_bytes(kernel: str, C: int, N: int, P: int, I: int, I_eff: int, p: int) -> float:
+    """Per-launch algorithmic bytes, SURVEY.md §8(d) per-unit figures × units per launch."""
+    if kernel.startswith("raster") and kernel.endswith("_fwd"):
+        return 40.0 * I_eff + 20.0 * P                 # read id+xy+conic+opac+colour; write rgb+alpha+last
+    if kernel.startswith("raster") and kernel.endswith("_bwd"):
+        return 24.0 * P + 40.0 * I_eff + 36.0 * C * N  # cotangents+alpha+last; list; reduced grads
+    if kernel.startswith("project") and kernel.endswith("_fwd"):
+        return C * N * (4.0 * p + 32.0)
+    if kernel.startswith("project") and kernel.endswith("_bwd"):
+        return N * (36.0 + 32.0 + 8.0 * p) * C
+    if kernel == "bin_sort":
+        return 36.0 * I
+    return 0.0
+
+
+def traffic_from_csv(path: str, kernel_substr: str):
+    """HBM bytes per launch from a rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE pass (KB units;
+    FETCH_SIZE doubled per the gfx950 correction in MI355X_MICROARCH.md §HBM)."""
+    import csv
+    fetch, write = [], []
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if kernel_substr not in row.get("Kernel_Name", ""):
+                continue
+            name, val = row.get("Counter_Name"), float(row.get("Counter_Value", 0))
+            if name == "FETCH_SIZE":
+                fetch.append(val)
+            elif name == "WRITE_SIZE":
+                write.append(val)
+    if not fetch and not write:
+        return None
+    f = 2.0 * 1024.0 * (sum(fetch) / max(len(fetch), 1))
+    w = 1024.0 * (sum(write) / max(len(write), 1))
+    return f + w
+
+
+def cpu_baseline(cfg, params, V, K, views: int):
+    """The oracle (CPU restatement of the reference semantics) on `views` of the workload."""
+    from oracle.oracle3d import render3d as oracle_render3d
+    from oracle.oracle2d import render2d_dense
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(cfg.seed + 1)
+    t0 = time.perf_counter()
+    if cfg.mode == "3d":
+        p = params.detach().cpu().clone().requires_grad_(True)
+        rgb, alpha = oracle_render3d(p, V[:views].cpu(), K[:views].cpu(), cfg.width, cfg.height, torch.ones(3))
+        vr = torch.randn(rgb.shape, generator=g)
+        va = torch.randn(alpha.shape, generator=g)
+        ((rgb * vr).sum() + (alpha * va).sum()).backward()
+        sample = f"{views} of {cfg.views} views of {cfg.name}, fwd+bwd, oracle/oracle3d.py"
+    else:
+        n = 2000
+        p = params[:n].detach().cpu().clone().requires_grad_(True)
+        rgb, alpha = render2d_dense(p, cfg.width, cfg.height, torch.ones(3))
+        ((rgb * torch.randn(rgb.shape, generator=g)).sum()).backward()
+        sample = f"first {n} of {cfg.N} Gaussians, 1 view, dense reference algorithm (linear in N)"
+    dt = time.perf_counter() - t0
+    value = views / dt if cfg.mode == "3d" else (n / cfg.N) / dt
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": value, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": sample, "seconds": round(dt, 2), "cpu": cpu}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+
+    from gsr import render as R
+    from gsr.scenes import CONFIGS, gaussians2d, gaussians3d, ring_cameras
+    cfg = CONFIGS[args.config]
+    C = cfg.views
+    P = C * cfg.width * cfg.height
+    if cfg.mode == "3d":
+        params_cpu = gaussians3d(cfg.N, cfg.seed)
+        V, K = ring_cameras(C, cfg.width, cfg.height, azimuth0=2 * 3.141592653589793 * rank / (C * world))
+        p_dim = 14
+    else:
+        params_cpu = gaussians2d(cfg.N, cfg.width, cfg.height, cfg.seed + rank)
+        V, K = ring_cameras(1, cfg.width, cfg.height)
+        p_dim = 9
+    params = params_cpu.to(dev).requires_grad_(True)
+    Vd, Kd = V.to(dev), K.to(dev)
+    bg = torch.ones(3, device=dev)
+    g = torch.Generator().manual_seed(cfg.seed + 1)
+    if cfg.mode == "3d":
+        v_rgb = torch.randn(C, cfg.height, cfg.width, 3, generator=g).to(dev)
+        v_alpha = torch.randn(C, cfg.height, cfg.width, generator=g).to(dev)
+    else:
+        v_rgb = torch.randn(cfg.height, cfg.width, 3, generator=g).to(dev)
+        v_alpha = torch.randn(cfg.height, cfg.width, generator=g).to(dev)
+
+    def step():
+        params.grad = None
+        if cfg.mode == "3d":
+            rgb, alpha = R.render3d(params, Vd, Kd, cfg.width, cfg.height, bg)
+            torch.autograd.backward([rgb, alpha], [v_rgb, v_alpha])
+        else:
+            # 2D: the reference ignores the camera, so every view of a frame is the same image
+            for _ in range(C):
+                rgb, alpha = R.render2d(params, cfg.width, cfg.height, bg)
+                torch.autograd.backward([rgb, alpha], [v_rgb, v_alpha])
+        if world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(params.grad)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    R.enable_kernel_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ktimes = R.kernel_times_ms()
+    R.enable_kernel_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+
+    st = R.last_stats()
+    I = st.get("n_isect", 0)
+    I_eff = R.effective_isect()
+    views_per_step = C * world
+    value = views_per_step * args.steps / elapsed
+    ms_per_step = 1000.0 * elapsed / args.steps
+
+    # dominant kernel (longest average duration)
+    dom = max(ktimes.items(), key=lambda kv: kv[1][0] * kv[1][1]) if ktimes else (None, (0.0, 0))
+    dom_name, (dom_ms, dom_n) = dom
+    Pd = P if cfg.mode == "3d" else cfg.width * cfg.height
+    Cd = C if cfg.mode == "3d" else 1
+    alg = algorithmic_bytes(dom_name or "", Cd, cfg.N, Pd, I, I_eff, p_dim)
+    achieved = alg / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    traffic = None
+    if args.traffic_csv and dom_name:
+        traffic = traffic_from_csv(args.traffic_csv, "k_" + dom_name)
+
+    out = {
+        "metric": "rendered frames/sec (fwd+bwd) at N_gauss x H x W",
+        "value": value,
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (SURVEY.md §8(d) distribution A, seed 1000+config)",
+        "config": {"workload": cfg.name, "N_gauss": cfg.N, "width": cfg.width, "height": cfg.height,
+                   "views_per_gpu": C, "background": "white",
+                   "parallelism": f"view-sharded x{world} + RCCL all-reduce of v_params" if world > 1 else "single GPU"},
+        "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "algorithmic_bytes": alg, "avg_ms": dom_ms, "launches": dom_n},
+        "kernels_ms": {k: round(v[0], 4) for k, v in sorted(ktimes.items())},
+        "binning": {"I": I, "I_eff": I_eff, "max_list": st.get("max_seg"), "busy_tiles": st.get("n_busy"),
+                    "tiles": st.get("tiles")},
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        cb = cpu_baseline(cfg, params_cpu, V, K, args.cpu_views)
+        out["cpu_baseline"] = cb
+        out["speedup_vs_cpu"] = value / cb["value"] if cb["value"] > 0 else None
+    else:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

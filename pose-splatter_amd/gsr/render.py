@@ -56,6 +56,41 @@ class RenderOptions3D:
 
 
 _last_stats = {}
+_timers = None   # name -> [(start_event, end_event)] while kernel timing is enabled
+
+
+def enable_kernel_timing(enabled: bool = True) -> None:
+    """Bracket each libgsr launch with CUDA(HIP) events on the current stream (bench.py)."""
+    global _timers
+    _timers = {} if enabled else None
+
+
+def kernel_times_ms() -> dict:
+    """Average duration (ms) and launch count per bracketed libgsr call (synchronises)."""
+    if not _timers:
+        return {}
+    torch.cuda.synchronize()
+    return {k: (sum(s.elapsed_time(e) for s, e in v) / len(v), len(v)) for k, v in _timers.items()}
+
+
+class _timed:
+    __slots__ = ("name", "s")
+
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        if _timers is not None:
+            self.s = torch.cuda.Event(enable_timing=True)
+            self.s.record()
+        return self
+
+    def __exit__(self, *exc):
+        if _timers is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            _timers.setdefault(self.name, []).append((self.s, e))
+        return False
 
 
 def last_stats() -> dict:
@@ -90,7 +125,8 @@ class _Bins:
         CN = self.C * self.N
         ws = torch.empty(int(L.gsr_bin_offsets_workspace(CN, self.CT)), device=self.rec.device,
                          dtype=torch.uint8)
-        check(L.gsr_bin_offsets(_ptr(self.cnt), CN, _ptr(self.tile_cnt), self.CT, _ptr(ws), ws.numel(),
+        with _timed("bin_offsets"):
+          check(L.gsr_bin_offsets(_ptr(self.cnt), CN, _ptr(self.tile_cnt), self.CT, _ptr(ws), ws.numel(),
                                 _ptr(self.isect_off), _ptr(self.tile_off), _ptr(self.busy),
                                 _ptr(self.stats_dev), stream), "gsr_bin_offsets")
         st = self.stats_dev.cpu()   # the one D2H sync of the forward
@@ -107,7 +143,8 @@ class _Bins:
         self.sorted_ids = torch.empty(max(I, 1), device=dev, dtype=torch.int32)
         self.pos = torch.empty(max(I, 1), device=dev, dtype=torch.int32)
         ws = torch.empty(int(L.gsr_bin_sort_workspace(I, self.CT)), device=dev, dtype=torch.uint8)
-        check(L.gsr_bin_sort(_ptr(self.rec), _ptr(self.rect), _ptr(self.isect_off), _ptr(self.tile_off),
+        with _timed("bin_sort"):
+          check(L.gsr_bin_sort(_ptr(self.rec), _ptr(self.rect), _ptr(self.isect_off), _ptr(self.tile_off),
                              _ptr(self.busy), self.C, self.N, self.W, self.H, order, I, self.max_seg,
                              self.n_busy, _ptr(ws), ws.numel(), _ptr(self.sorted_ids), _ptr(self.pos),
                              stream), "gsr_bin_sort")
@@ -143,7 +180,8 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
     bgc = bg.detach().to(device=dev, dtype=torch.float32).reshape(-1, 3).expand(C, 3).contiguous()
     b = _Bins(dev, C, N, width, height)
     if N > 0:
-        check(L.gsr3d_project_fwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height,
+        with _timed("project3d_fwd"):
+          check(L.gsr3d_project_fwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height,
                                   opts.near_plane, opts.far_plane, opts.radius_clip, opts.eps2d,
                                   opts.radius_mode, _ptr(b.rec), _ptr(b.rect), _ptr(b.cnt),
                                   _ptr(b.tile_cnt), stream), "gsr3d_project_fwd")
@@ -154,7 +192,8 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
     b.final_T = torch.empty(C, height, width, device=dev, dtype=torch.float32)
     b.last = torch.empty(C, height, width, device=dev, dtype=torch.int32)
     b.tile_end = torch.empty(b.CT, device=dev, dtype=torch.int32)
-    check(L.gsr3d_raster_fwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), C, width, height,
+    with _timed("raster3d_fwd"):
+      check(L.gsr3d_raster_fwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), C, width, height,
                              _ptr(bgc), _ptr(rgb), _ptr(alpha), _ptr(b.final_T), _ptr(b.last),
                              _ptr(b.tile_end), stream), "gsr3d_raster_fwd")
     _record_stats(b)
@@ -169,7 +208,8 @@ def _forward2d(params, bg, width, height, eps_cut):
     p, stride = _rows(params, 9)
     bgc = bg.detach().to(device=dev, dtype=torch.float32).reshape(1, 3).contiguous()
     b = _Bins(dev, 1, N, width, height)
-    check(L.gsr2d_project_fwd(_ptr(p), N, stride, width, height, eps_cut, _ptr(b.rec), _ptr(b.rect),
+    with _timed("project2d_fwd"):
+      check(L.gsr2d_project_fwd(_ptr(p), N, stride, width, height, eps_cut, _ptr(b.rec), _ptr(b.rect),
                               _ptr(b.cnt), _ptr(b.tile_cnt), stream), "gsr2d_project_fwd")
     b.offsets(stream)
     b.sort(_lib.ORDER_INDEX, stream)
@@ -177,7 +217,8 @@ def _forward2d(params, bg, width, height, eps_cut):
     alpha = torch.empty(height, width, device=dev, dtype=torch.float32)
     b.last = torch.empty(height, width, device=dev, dtype=torch.int32)
     b.tile_end = torch.empty(b.CT, device=dev, dtype=torch.int32)
-    check(L.gsr2d_raster_fwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), width, height, _ptr(bgc),
+    with _timed("raster2d_fwd"):
+      check(L.gsr2d_raster_fwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), width, height, _ptr(bgc),
                              _ptr(rgb), _ptr(alpha), _ptr(b.last), _ptr(b.tile_end), stream),
           "gsr2d_raster_fwd")
     _record_stats(b)
@@ -219,11 +260,13 @@ class _Render3D(torch.autograd.Function):
         v_params = torch.empty(N, 14, device=dev, dtype=torch.float32)
         if N > 0:
             partial = torch.empty(max(b.n_isect, 1) * 9, device=dev, dtype=torch.float32)
-            check(L.gsr3d_raster_bwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), _ptr(b.tile_end),
+            with _timed("raster3d_bwd"):
+              check(L.gsr3d_raster_bwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), _ptr(b.tile_end),
                                      _ptr(b.busy), b.n_busy, C, width, height, _ptr(bgc), _ptr(b.final_T),
                                      _ptr(b.last), _ptr(v_rgb), _ptr(v_alpha), _ptr(partial), stream),
                   "gsr3d_raster_bwd")
-            check(L.gsr3d_project_bwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height, opts.eps2d,
+            with _timed("project3d_bwd"):
+              check(L.gsr3d_project_bwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height, opts.eps2d,
                                       _ptr(b.rect), _ptr(b.isect_off), _ptr(b.cnt), _ptr(b.pos),
                                       _ptr(b.tile_end), _ptr(partial), _ptr(v_params), stream),
                   "gsr3d_project_bwd")
@@ -257,11 +300,13 @@ class _Render2D(torch.autograd.Function):
         if N > 0:
             partial = torch.empty(max(b.n_isect, 1) * 9, device=dev, dtype=torch.float32)
             ws = torch.empty(int(L.gsr2d_raster_bwd_workspace(b.n_isect, b.CT)), device=dev, dtype=torch.uint8)
-            check(L.gsr2d_raster_bwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), _ptr(b.tile_end),
+            with _timed("raster2d_bwd"):
+              check(L.gsr2d_raster_bwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), _ptr(b.tile_end),
                                      _ptr(b.busy), b.n_busy, width, height, _ptr(bgc), _ptr(b.last),
                                      _ptr(v_rgb), _ptr(v_alpha), _ptr(ws), ws.numel(), _ptr(partial), stream),
                   "gsr2d_raster_bwd")
-            check(L.gsr2d_project_bwd(_ptr(p), N, stride, width, height, _ptr(b.rect), _ptr(b.isect_off),
+            with _timed("project2d_bwd"):
+              check(L.gsr2d_project_bwd(_ptr(p), N, stride, width, height, _ptr(b.rect), _ptr(b.isect_off),
                                       _ptr(b.cnt), _ptr(b.pos), _ptr(b.tile_end), _ptr(partial),
                                       _ptr(v_params), stream), "gsr2d_project_bwd")
         return v_params.view(ctx.params_shape), None, None, None, None
