@@ -98,7 +98,8 @@ int gsr2d_project_fwd(const float* params, int64_t N, int64_t row_stride, int wi
 size_t gsr_bin_offsets_workspace(int64_t CN, int64_t CT);
 
 /* Exclusive scans: isect_offset [CN] (per-Gaussian emission offsets), tile_offset [CT+1],
- * busy_tiles [CT] (indices of non-empty tiles, ascending), stats (device). */
+ * busy_tiles [CT] (rasterizer visit order: the stats.n_busy non-empty tiles first, longest
+ * lists first, then the empty tiles), stats (device). */
 int gsr_bin_offsets(const int32_t* isect_count, int64_t CN, const int32_t* tile_count,
                     int64_t CT, void* workspace, size_t workspace_bytes,
                     int32_t* isect_offset, int32_t* tile_offset, int32_t* busy_tiles,
@@ -120,13 +121,14 @@ int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_of
 
 /* ---------------------------------------------------------------- (c) rasterisation */
 
-/* Front-to-back compositing (gsplat classic), one workgroup per 16x16 tile.
- * bg [C,3].  Outputs rgb [C,H,W,3], alpha [C,H,W], final_T [C,H,W] (exact transmittance,
+/* Front-to-back compositing (gsplat classic), one workgroup per 16x16 tile, visited in
+ * tile_order (the busy_tiles array of gsr_bin_offsets: all C*tiles entries).  bg [C,3].  Outputs rgb [C,H,W,3], alpha [C,H,W], final_T [C,H,W] (exact transmittance,
  * kept for the backward), last [C,H,W] (index of the last contributing sorted entry, -1
  * if none), tile_end [CT] (1 + max last over the tile, or the tile's start). */
 int gsr3d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
-                     int C, int width, int height, const float* bg, float* rgb, float* alpha,
-                     float* final_T, int32_t* last, int32_t* tile_end, void* stream);
+                     const int32_t* tile_order, int C, int width, int height, const float* bg,
+                     float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
+                     void* stream);
 
 /* Backward of gsr3d_raster_fwd.  v_rgb [C,H,W,3], v_alpha [C,H,W] (contiguous).
  * Writes partial [I*9] for every sorted entry s in [tile start, tile_end). */

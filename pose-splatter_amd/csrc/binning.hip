@@ -75,7 +75,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const int32_t* __re
 }
 
 // ---------------------------------------------------------------- tile scan (single block)
-// tile_offset[0..CT], busy list (ascending), stats.
+// tile_offset[0..CT], visit order (non-empty tiles longest-first, then empty), stats.
 __global__ __launch_bounds__(kTopThreads) void k_tile_scan(const int32_t* __restrict__ tile_count, int64_t CT,
                                                           int32_t* __restrict__ tile_offset,
                                                           int32_t* __restrict__ busy,
@@ -93,11 +93,9 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(const int32_t* __rest
     const int ex = block_exclusive_scan<kTopThreads>(v, s_tmp, &total);
     if (i < CT) tile_offset[i] = (int32_t)(carry + ex);
     if (v > 0) atomicMax(&s_max, v);
-    int btotal;
-    const int bex = block_exclusive_scan<kTopThreads>(v > 0 ? 1 : 0, s_tmp, &btotal);
-    if (v > 0) busy[bcarry + bex] = (int32_t)i;
+    const int nb = __syncthreads_count(v > 0);
     carry += total;
-    bcarry += btotal;
+    bcarry += nb;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -105,6 +103,33 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(const int32_t* __rest
     stats->n_isect = carry;
     stats->max_seg = s_max;
     stats->n_busy = bcarry;
+  }
+  // Visit order for the rasterizer: non-empty tiles first, longest lists first (log2
+  // buckets; order inside a bucket is arbitrary — it only affects scheduling), then the
+  // empty tiles.  Longest-processing-time-first keeps the heavy tiles off the tail.
+  __shared__ int s_bucket[34];
+  if (threadIdx.x < 34) s_bucket[threadIdx.x] = 0;
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < CT; i += blockDim.x) {
+    const int v = tile_count[i];
+    const int b = v > 0 ? 31 - __clz(v) : 32;
+    atomicAdd(&s_bucket[b], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int b = 31; b >= 0; --b) {
+      const int c = s_bucket[b];
+      s_bucket[b] = acc;
+      acc += c;
+    }
+    s_bucket[32] = acc;
+  }
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < CT; i += blockDim.x) {
+    const int v = tile_count[i];
+    const int b = v > 0 ? 31 - __clz(v) : 32;
+    busy[atomicAdd(&s_bucket[b], 1)] = (int32_t)i;
   }
 }
 

@@ -24,73 +24,150 @@ __device__ __forceinline__ void tile_coords(int ct, int tw, int th, int& c, int&
   tx = t - ty * tw;
 }
 
-// ---------------------------------------------------------------- 3D forward
-__global__ __launch_bounds__(kRasterThreads) void k_raster3d_fwd(
+// ---------------------------------------------------------------- per-wave culling
+// A wave owns an 8x8 sub-tile of its 16x16 tile.  An entry can only change a pixel of the
+// sub-tile if its level set {opacity*exp(-sigma) >= cut} (3D: cut = 1/255, gsplat's skip
+// threshold; 2D: eps_cut) meets the sub-tile's pixel-centre box.  The test uses that
+// ellipse's axis-aligned extent (inflated by a small margin), so it never drops an entry
+// the per-pixel test would keep: culling changes the work, not the result.
+template <bool IS2D>
+__device__ __forceinline__ bool cull_keep(const float4 p0, const float4 p1, float bx0, float bx1, float by0,
+                                          float by1, float cut) {
+  const float ratio = IS2D ? p0.z / cut : p0.z * 255.f;
+  if (!(ratio >= 1.f)) return false;
+  const float L = __logf(ratio) * 1.0001f + 1e-4f;
+  const float det = p1.x * p1.z - 0.25f * p1.y * p1.y;
+  if (!(det > 0.f)) return true;
+  const float hx = sqrtf(L * p1.z / det) * 1.001f + 0.01f;
+  const float hy = sqrtf(L * p1.x / det) * 1.001f + 0.01f;
+  return (p0.x + hx >= bx0) && (p0.x - hx <= bx1) && (p0.y + hy >= by0) && (p0.y - hy <= by1);
+}
+
+struct SubTile {
+  int c, ty, tx, wv, lane, i, j;
+  float px, py, bx0, bx1, by0, by1;
+  bool inside;
+};
+
+template <bool IS2D>
+__device__ __forceinline__ SubTile sub_tile(int ct, int tw, int th, int W, int H) {
+  SubTile t;
+  tile_coords(ct, tw, th, t.c, t.ty, t.tx);
+  t.wv = threadIdx.x >> 6;
+  t.lane = threadIdx.x & 63;
+  const int sx0 = t.tx * kTile + (t.wv & 1) * 8;
+  const int sy0 = t.ty * kTile + (t.wv >> 1) * 8;
+  t.i = sy0 + (t.lane >> 3);
+  t.j = sx0 + (t.lane & 7);
+  t.inside = (t.i < H) && (t.j < W);
+  const float off = IS2D ? 0.f : 0.5f;   // 2D: integer centres (src/gaussian_renderer.py:355-358)
+  t.px = (float)t.j + off;
+  t.py = (float)t.i + off;
+  t.bx0 = (float)sx0 + off;
+  t.bx1 = (float)(sx0 + 7) + off;
+  t.by0 = (float)sy0 + off;
+  t.by1 = (float)(sy0 + 7) + off;
+  return t;
+}
+
+// ---------------------------------------------------------------- 3D / 2D forward
+// Waves run independently (no workgroup barrier in the loop): each wave gathers the next 64
+// list entries (prefetched one batch ahead), culls them against its sub-tile, compacts the
+// survivors into its private LDS queue, and composites them branch-free.  A wave leaves as
+// soon as all of its 64 pixels are done.
+//  3D (gsplat classic):  a = min(0.999, o e^-s); skip s<0 | a<1/255; stop before T(1-a)<=1e-4
+//  2D (reference):       c = o e^-q (1-A); canvas += c rgb; A += c   (A == 1 exactly → done)
+template <bool IS2D>
+__global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
-    int W, int H, int tw, int th, const float* __restrict__ bg, float* __restrict__ out_rgb,
-    float* __restrict__ out_alpha, float* __restrict__ out_T, int32_t* __restrict__ out_last,
-    int32_t* __restrict__ tile_end) {
-  __shared__ float4 s_p0[kRasterThreads];
-  __shared__ float4 s_p1[kRasterThreads];
-  __shared__ float4 s_p2[kRasterThreads];
+    const int32_t* __restrict__ order, int W, int H, int tw, int th, float cut, const float* __restrict__ bg,
+    float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
+    int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end) {
+  __shared__ float4 s_p0[4][64];
+  __shared__ float4 s_p1[4][64];
+  __shared__ float4 s_p2[4][64];
   __shared__ int s_max;
-  const int ct = blockIdx.x;
-  int c, ty, tx;
-  tile_coords(ct, tw, th, c, ty, tx);
-  const int i = ty * kTile + (threadIdx.x >> 4);
-  const int j = tx * kTile + (threadIdx.x & 15);
-  const bool inside = (i < H) && (j < W);
-  const float px = (float)j + 0.5f, py = (float)i + 0.5f;
+  const int ct = order[blockIdx.x];
+  const SubTile st = sub_tile<IS2D>(ct, tw, th, W, H);
+  const int wv = st.wv;
   const int start = tile_offset[ct], end = tile_offset[ct + 1];
   if (threadIdx.x == 0) s_max = -1;
-  float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f;
+  __syncthreads();
+  float T = 1.f;   // 3D: transmittance;  2D: accumulated alpha A
+  if (IS2D) T = 0.f;
+  float cr = 0.f, cg = 0.f, cb = 0.f;
   int last = -1;
-  bool done = !inside;
-  for (int b0 = start; b0 < end; b0 += kRasterThreads) {
-    if (__syncthreads_count(!done) == 0) break;
-    const int e = b0 + threadIdx.x;
-    if (e < end) {
-      const Splat s = rec[ids[e]];
-      s_p0[threadIdx.x] = s.p0;
-      s_p1[threadIdx.x] = s.p1;
-      s_p2[threadIdx.x] = s.p2;
+  bool done = !st.inside;
+  int e = start + st.lane;
+  float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0;
+  bool have = e < end;
+  if (have) {
+    const Splat s = rec[ids[e]];
+    n0 = s.p0; n1 = s.p1; n2 = s.p2;
+  }
+  for (int b0 = start; b0 < end; b0 += 64) {
+    if (__ballot(!done) == 0ull) break;
+    const bool keep = have && cull_keep<IS2D>(n0, n1, st.bx0, st.bx1, st.by0, st.by1, cut);
+    const unsigned long long m = __ballot(keep);
+    const int n = __popcll(m);
+    if (keep) {
+      const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+      s_p0[wv][slot] = n0;
+      s_p1[wv][slot] = make_float4(n1.x, n1.y, n1.z, __int_as_float(b0 + st.lane));
+      s_p2[wv][slot] = n2;
     }
-    __syncthreads();
-    const int n = min(kRasterThreads, end - b0);
-    if (!done) {
-      for (int k = 0; k < n; ++k) {
-        const float4 p0 = s_p0[k];
-        const float4 p1 = s_p1[k];
-        const float dx = p0.x - px, dy = p0.y - py;
-        const float sigma = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
-        const float alpha = fminf(kAlphaMax, p0.z * __expf(-sigma));
-        if (sigma < 0.f || alpha < kAlphaThreshold) continue;
+    // prefetch the next batch while this one is composited
+    e = b0 + 64 + st.lane;
+    have = e < end;
+    if (have) {
+      const Splat s = rec[ids[e]];
+      n0 = s.p0; n1 = s.p1; n2 = s.p2;
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll 4
+    for (int k = 0; k < n; ++k) {
+      const float4 p0 = s_p0[wv][k];
+      const float4 p1 = s_p1[wv][k];
+      const float4 p2 = s_p2[wv][k];
+      const float dx = p0.x - st.px, dy = p0.y - st.py;
+      const float sg = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
+      if (!IS2D) {
+        const float alpha = fminf(kAlphaMax, p0.z * __expf(-sg));
+        const bool ok = !done && sg >= 0.f && alpha >= kAlphaThreshold;
         const float nT = T * (1.f - alpha);
-        if (nT <= kTMin) {
-          done = true;
-          break;
-        }
-        const float vis = alpha * T;
-        const float4 p2 = s_p2[k];
+        const bool stop = ok && (nT <= kTMin);
+        const bool con = ok && !stop;
+        const float vis = con ? alpha * T : 0.f;
         cr += p2.x * vis;
         cg += p2.y * vis;
         cb += p2.z * vis;
-        T = nT;
-        last = b0 + k;
+        T = con ? nT : T;
+        last = con ? __float_as_int(p1.w) : last;
+        done = done || stop;
+      } else {
+        const float g = p0.z * __expf(-sg);
+        const float contrib = done ? 0.f : g * (1.f - T);
+        cr += contrib * p2.x;
+        cg += contrib * p2.y;
+        cb += contrib * p2.z;
+        T += contrib;
+        last = done ? last : __float_as_int(p1.w);
+        done = done || (T == 1.f);
       }
     }
+    __builtin_amdgcn_wave_barrier();
   }
-  if (inside) {
-    const int64_t pix = ((int64_t)c * H + i) * W + j;
-    const float* bgc = bg + c * 3;
-    out_rgb[pix * 3 + 0] = cr + T * bgc[0];
-    out_rgb[pix * 3 + 1] = cg + T * bgc[1];
-    out_rgb[pix * 3 + 2] = cb + T * bgc[2];
-    out_alpha[pix] = 1.f - T;
-    out_T[pix] = T;
+  if (st.inside) {
+    const int64_t pix = ((int64_t)st.c * H + st.i) * W + st.j;
+    const float* bgc = bg + st.c * 3;
+    const float Tr = IS2D ? 1.f - T : T;
+    out_rgb[pix * 3 + 0] = cr + Tr * bgc[0];
+    out_rgb[pix * 3 + 1] = cg + Tr * bgc[1];
+    out_rgb[pix * 3 + 2] = cb + Tr * bgc[2];
+    out_alpha[pix] = IS2D ? T : 1.f - T;
+    if (!IS2D) out_T[pix] = T;
     out_last[pix] = last;
   }
-  __syncthreads();
   if (last >= 0) atomicMax(&s_max, last);
   __syncthreads();
   if (threadIdx.x == 0) tile_end[ct] = s_max >= 0 ? s_max + 1 : start;
@@ -202,6 +279,8 @@ __device__ __forceinline__ void block_store_partials(const PartialLds& L, int b0
 // (safe: a <= 0.999), starting from the EXACT final transmittance saved by the forward.
 //   d rgb/d c_i = a_i T_i;  d rgb/d a_i = c_i T_i - (S_i + T_f bg)/(1-a_i);  d alpha/d a_i = T_f/(1-a_i)
 //   a = o e^{-sigma} (unclamped only):  d/do = e^{-sigma},  d/dsigma = -a.
+// The tile's list is staged 256 entries at a time; each wave walks only the entries that
+// survive its sub-tile cull (the same test as the forward), back to front.
 __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ tile_end, const int32_t* __restrict__ busy, int W, int H, int tw, int th,
@@ -211,19 +290,16 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
   __shared__ float4 s_p1[kRasterThreads];
   __shared__ float4 s_p2[kRasterThreads];
   __shared__ PartialLds L;
+  __shared__ unsigned long long s_m[4][4];
   const int ct = busy[blockIdx.x];
-  int c, ty, tx;
-  tile_coords(ct, tw, th, c, ty, tx);
-  const int i = ty * kTile + (threadIdx.x >> 4);
-  const int j = tx * kTile + (threadIdx.x & 15);
-  const bool inside = (i < H) && (j < W);
-  const float px = (float)j + 0.5f, py = (float)i + 0.5f;
+  const SubTile st = sub_tile<false>(ct, tw, th, W, H);
+  const int wv = st.wv;
   const int start = tile_offset[ct];
   const int eff = tile_end[ct];
   float Tf = 1.f, vr = 0.f, vg = 0.f, vb = 0.f, va = 0.f;
   int last = -1;
-  if (inside) {
-    const int64_t pix = ((int64_t)c * H + i) * W + j;
+  if (st.inside) {
+    const int64_t pix = ((int64_t)st.c * H + st.i) * W + st.j;
     Tf = final_T[pix];
     last = last_in[pix];
     vr = v_rgb[pix * 3 + 0];
@@ -231,8 +307,13 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
     vb = v_rgb[pix * 3 + 2];
     va = v_alpha[pix];
   }
-  const float* bgc = bg + c * 3;
+  const float* bgc = bg + st.c * 3;
   const float bgdot = bgc[0] * vr + bgc[1] * vg + bgc[2] * vb;
+  const float vTa = Tf * (va - bgdot);
+  // the wave's deepest contributing entry: nothing beyond it matters for this wave
+  int wlast = last;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) wlast = max(wlast, __shfl_xor(wlast, o, 64));
   float T = Tf, Sr = 0.f, Sg = 0.f, Sb = 0.f;
   for (int bend = eff; bend > start; bend -= kRasterThreads) {
     const int b0 = max(start, bend - kRasterThreads);
@@ -246,23 +327,35 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
       s_p2[threadIdx.x] = s.p2;
     }
     __syncthreads();
-    for (int k = n - 1; k >= 0; --k) {
-      const int ek = b0 + k;
-      float gv[kPartial];
+    unsigned long long mq[4];
 #pragma unroll
-      for (int v = 0; v < kPartial; ++v) gv[v] = 0.f;
-      bool valid = ek <= last;
-      if (valid) {
+    for (int q = 0; q < 4; ++q) {
+      const int k = q * 64 + st.lane;
+      const bool keep = k < n && (b0 + k) <= wlast &&
+                        cull_keep<false>(s_p0[k], s_p1[k], st.bx0, st.bx1, st.by0, st.by1, 0.f);
+      mq[q] = __ballot(keep);
+    }
+#pragma unroll
+    for (int q = 3; q >= 0; --q) {
+      unsigned long long m = mq[q];
+      while (m) {
+        const int bit = 63 - __clzll(m);
+        m &= ~(1ull << bit);
+        const int k = q * 64 + bit;
+        const int ek = b0 + k;
+        float gv[kPartial];
+#pragma unroll
+        for (int v = 0; v < kPartial; ++v) gv[v] = 0.f;
         const float4 p0 = s_p0[k];
         const float4 p1 = s_p1[k];
-        const float dx = p0.x - px, dy = p0.y - py;
+        const float4 p2 = s_p2[k];
+        const float dx = p0.x - st.px, dy = p0.y - st.py;
         const float sigma = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
         const float vis = __expf(-sigma);
         const float raw = p0.z * vis;
         const float alpha = fminf(kAlphaMax, raw);
-        valid = !(sigma < 0.f || alpha < kAlphaThreshold);
+        const bool valid = ek <= last && !(sigma < 0.f || alpha < kAlphaThreshold);
         if (valid) {
-          const float4 p2 = s_p2[k];
           const float ra = 1.f / (1.f - alpha);
           T *= ra;
           const float fac = alpha * T;
@@ -270,7 +363,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
           gv[7] = fac * vg;
           gv[8] = fac * vb;
           const float v_al = (p2.x * T - Sr * ra) * vr + (p2.y * T - Sg * ra) * vg + (p2.z * T - Sb * ra) * vb +
-                             Tf * ra * (va - bgdot);
+                             vTa * ra;
           if (raw <= kAlphaMax) {
             const float v_sig = -raw * v_al;
             gv[2] = v_sig * dx * dx;
@@ -284,11 +377,40 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
           Sg += p2.y * fac;
           Sb += p2.z * fac;
         }
+        const bool any = __ballot(valid) != 0ull;
+        if (any) {
+#pragma unroll
+          for (int v = 0; v < kPartial; ++v) {
+            const float sum = wave_sum(gv[v]);
+            if (st.lane == 0) L.w[v][wv][k] = sum;
+          }
+        } else {
+          mq[q] &= ~(1ull << bit);   // nothing written for this entry by this wave
+        }
       }
-      wave_emit(L, k, wave_ballot(valid) != 0, gv);
+    }
+    if (st.lane == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s_m[wv][q] = mq[q];
     }
     __syncthreads();
-    block_store_partials(L, b0, n, partial);
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+      const int q = k >> 6;
+      const unsigned long long bit = 1ull << (k & 63);
+      float acc[kPartial];
+#pragma unroll
+      for (int v = 0; v < kPartial; ++v) acc[v] = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        if (s_m[w][q] & bit) {
+#pragma unroll
+          for (int v = 0; v < kPartial; ++v) acc[v] += L.w[v][w][k];
+        }
+      }
+      float* dst = partial + (int64_t)(b0 + k) * kPartial;
+#pragma unroll
+      for (int v = 0; v < kPartial; ++v) dst[v] = acc[v];
+    }
   }
 }
 
@@ -443,17 +565,17 @@ using namespace gsr;
 
 extern "C" {
 
-int gsr3d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset, int C, int width,
-                     int height, const float* bg, float* rgb, float* alpha, float* final_T, int32_t* last,
-                     int32_t* tile_end, void* stream) {
+int gsr3d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
+                     const int32_t* tile_order, int C, int width, int height, const float* bg, float* rgb,
+                     float* alpha, float* final_T, int32_t* last, int32_t* tile_end, void* stream) {
   GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "gsr3d_raster_fwd: bad C=%d or image %dx%d", C, width, height);
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   const int64_t CT = (int64_t)C * tw * th;
   GSR_REQUIRE(CT < (1ll << 31), "gsr3d_raster_fwd: too many tiles");
-  hipLaunchKernelGGL(k_raster3d_fwd, dim3((unsigned)CT), dim3(kRasterThreads), 0, (hipStream_t)stream,
-                     (const Splat*)rec, sorted_ids, tile_offset, width, height, tw, th, bg, rgb, alpha, final_T,
-                     last, tile_end);
-  GSR_LAUNCH_CHECK("k_raster3d_fwd");
+  hipLaunchKernelGGL(k_raster_fwd<false>, dim3((unsigned)CT), dim3(kRasterThreads), 0, (hipStream_t)stream,
+                     (const Splat*)rec, sorted_ids, tile_offset, tile_order, width, height, tw, th, kAlphaThreshold,
+                     bg, rgb, alpha, final_T, last, tile_end);
+  GSR_LAUNCH_CHECK("k_raster_fwd<3d>");
   return GSR_OK;
 }
 

@@ -193,7 +193,7 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
     b.last = torch.empty(C, height, width, device=dev, dtype=torch.int32)
     b.tile_end = torch.empty(b.CT, device=dev, dtype=torch.int32)
     with _timed("raster3d_fwd"):
-      check(L.gsr3d_raster_fwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), C, width, height,
+      check(L.gsr3d_raster_fwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), _ptr(b.busy), C, width, height,
                              _ptr(bgc), _ptr(rgb), _ptr(alpha), _ptr(b.final_T), _ptr(b.last),
                              _ptr(b.tile_end), stream), "gsr3d_raster_fwd")
     _record_stats(b)
