@@ -73,6 +73,10 @@ typedef struct gsr_bin_stats {
 int gsr_version(void);
 const char* gsr_last_error(void);
 
+/* Self-test of the cross-lane reduction used by the backward kernels (one 64-lane wave):
+ * out[l] = sum over lanes L of v_L[l] with v_L[i] = ((L*7 + i*13) % 97) + i/4.  out: 64 floats. */
+int gsr_selftest_reduce64(float* out, void* stream);
+
 /* ---------------------------------------------------------------- (a) projection */
 
 /* 3D projection (+ adapter activations fused).  params: [N, >=14] fp32 rows with

@@ -67,6 +67,62 @@ __device__ __forceinline__ float wave_sum(float v) {
   return (readlane_f(v, 0) + readlane_f(v, 16)) + (readlane_f(v, 32) + readlane_f(v, 48));
 }
 
+// ---------------------------------------------------------------- transposed reduction
+// reduce64(v): every lane holds 64 values; afterwards lane l holds sum over all 64 lanes of
+// v[l].  A butterfly that halves the number of live registers at every level:
+//   xor-32 and xor-16 levels: one v_permlane32_swap / v_permlane16_swap (gfx950) + one add
+//   per register pair; the four intra-row levels pair lanes with row_mirror, row_half_mirror
+//   and two quad_perms (DPP), the lane's bit choosing which register it keeps.
+// ~150 VALU ops for 64 sums, versus ~11 per sum for independent full-wave reductions.
+// NOTE: ROCm 7.2's clang returns the FIRST result register for both halves of
+// __builtin_amdgcn_permlane{32,16}_swap (the second result is mis-lowered), so the swaps are
+// issued as inline asm.  Hardware semantics (verified on MI355X, tools/diag_lanes.hip):
+//   v_permlane32_swap a, b:  a' = [a_lo32, b_lo32],  b' = [a_hi32, b_hi32]
+//   v_permlane16_swap a, b:  a' = [a_r0, b_r0, a_r2, b_r2],  b' = [a_r1, b_r1, a_r3, b_r3]
+// The s_nop 1 covers the VALU-write -> permlane-read hazard the compiler cannot see in asm.
+__device__ __forceinline__ float2 swap32(float a, float b) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  return make_float2(a, b);
+}
+__device__ __forceinline__ float2 swap16(float a, float b) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  return make_float2(a, b);
+}
+
+template <int CTRL>
+__device__ __forceinline__ float pair_level(float lo, float hi, bool upper) {
+  const float keep = upper ? hi : lo;
+  const float send = upper ? lo : hi;
+  return keep + dpp_mov<CTRL>(send);
+}
+
+__device__ __forceinline__ float reduce64(float (&v)[64]) {
+  const int lane = threadIdx.x & 63;
+  float a[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const float2 r = swap32(v[i], v[i + 32]);
+    a[i] = r.x + r.y;
+  }
+  float b[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const float2 r = swap16(a[i], a[i + 16]);
+    b[i] = r.x + r.y;
+  }
+  float c[8];
+  const bool b3 = (lane & 8) != 0, b2 = (lane & 4) != 0, b1 = (lane & 2) != 0, b0 = (lane & 1) != 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) c[i] = pair_level<0x140>(b[i], b[i + 8], b3);   // row_mirror
+  float d[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) d[i] = pair_level<0x141>(c[i], c[i + 4], b2);   // row_half_mirror
+  float e[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) e[i] = pair_level<0x4E>(d[i], d[i + 2], b1);    // quad_perm [2,3,0,1]
+  return pair_level<0xB1>(e[0], e[1], b0);                                     // quad_perm [1,0,3,2]
+}
+
 __device__ __forceinline__ unsigned long long wave_ballot(bool p) { return __ballot(p); }
 
 // Block-wide exclusive scan of one int per thread (NT threads, multiple of 64).

@@ -335,63 +335,89 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
                         cull_keep<false>(s_p0[k], s_p1[k], st.bx0, st.bx1, st.by0, st.by1, 0.f);
       mq[q] = __ballot(keep);
     }
-#pragma unroll
-    for (int q = 3; q >= 0; --q) {
-      unsigned long long m = mq[q];
-      while (m) {
-        const int bit = 63 - __clzll(m);
-        m &= ~(1ull << bit);
-        const int k = q * 64 + bit;
-        const int ek = b0 + k;
-        float gv[kPartial];
-#pragma unroll
-        for (int v = 0; v < kPartial; ++v) gv[v] = 0.f;
-        const float4 p0 = s_p0[k];
-        const float4 p1 = s_p1[k];
-        const float4 p2 = s_p2[k];
-        const float dx = p0.x - st.px, dy = p0.y - st.py;
-        const float sigma = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
-        const float vis = __expf(-sigma);
-        const float raw = p0.z * vis;
-        const float alpha = fminf(kAlphaMax, raw);
-        const bool valid = ek <= last && !(sigma < 0.f || alpha < kAlphaThreshold);
-        if (valid) {
-          const float ra = 1.f / (1.f - alpha);
-          T *= ra;
-          const float fac = alpha * T;
-          gv[6] = fac * vr;
-          gv[7] = fac * vg;
-          gv[8] = fac * vb;
-          const float v_al = (p2.x * T - Sr * ra) * vr + (p2.y * T - Sg * ra) * vg + (p2.z * T - Sb * ra) * vb +
-                             vTa * ra;
-          if (raw <= kAlphaMax) {
-            const float v_sig = -raw * v_al;
-            gv[2] = v_sig * dx * dx;
-            gv[3] = v_sig * dx * dy;
-            gv[4] = v_sig * dy * dy;
-            gv[0] = v_sig * (2.f * p1.x * dx + p1.y * dy);
-            gv[1] = v_sig * (p1.y * dx + 2.f * p1.z * dy);
-            gv[5] = vis * v_al;
-          }
-          Sr += p2.x * fac;
-          Sg += p2.y * fac;
-          Sb += p2.z * fac;
-        }
-        const bool any = __ballot(valid) != 0ull;
-        if (any) {
-#pragma unroll
-          for (int v = 0; v < kPartial; ++v) {
-            const float sum = wave_sum(gv[v]);
-            if (st.lane == 0) L.w[v][wv][k] = sum;
-          }
-        } else {
-          mq[q] &= ~(1ull << bit);   // nothing written for this entry by this wave
-        }
-      }
-    }
     if (st.lane == 0) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) s_m[wv][q] = mq[q];
+      for (int q = 0; q < 4; ++q) s_m[wv][q] = 0ull;
+    }
+    // Walk the survivors back to front; entries that touch a valid pixel are gathered in
+    // groups of 7 (63 of reduce64's 64 slots: 7 entries x 9 partials) and reduced at once.
+    int q = 3;
+    unsigned long long m = mq[3];
+    bool more = true;
+    while (more) {
+      float acc[64];
+#pragma unroll
+      for (int v = 0; v < 64; ++v) acc[v] = 0.f;
+      int kk[7];
+#pragma unroll
+      for (int g = 0; g < 7; ++g) {
+        kk[g] = -1;
+        while (more) {
+          while (m == 0ull && q > 0) {
+            --q;
+            m = mq[q];
+          }
+          if (m == 0ull) {
+            more = false;
+            break;
+          }
+          const int bit = 63 - __clzll(m);
+          m &= ~(1ull << bit);
+          const int k = q * 64 + bit;
+          const int ek = b0 + k;
+          const float4 p0 = s_p0[k];
+          const float4 p1 = s_p1[k];
+          const float4 p2 = s_p2[k];
+          const float dx = p0.x - st.px, dy = p0.y - st.py;
+          const float sigma = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
+          const float vis = __expf(-sigma);
+          const float raw = p0.z * vis;
+          const float alpha = fminf(kAlphaMax, raw);
+          const bool valid = ek <= last && !(sigma < 0.f || alpha < kAlphaThreshold);
+          float gv[kPartial];
+#pragma unroll
+          for (int v = 0; v < kPartial; ++v) gv[v] = 0.f;
+          if (valid) {
+            const float ra = 1.f / (1.f - alpha);
+            T *= ra;
+            const float fac = alpha * T;
+            gv[6] = fac * vr;
+            gv[7] = fac * vg;
+            gv[8] = fac * vb;
+            const float v_al = (p2.x * T - Sr * ra) * vr + (p2.y * T - Sg * ra) * vg + (p2.z * T - Sb * ra) * vb +
+                               vTa * ra;
+            if (raw <= kAlphaMax) {
+              const float v_sig = -raw * v_al;
+              gv[2] = v_sig * dx * dx;
+              gv[3] = v_sig * dx * dy;
+              gv[4] = v_sig * dy * dy;
+              gv[0] = v_sig * (2.f * p1.x * dx + p1.y * dy);
+              gv[1] = v_sig * (p1.y * dx + 2.f * p1.z * dy);
+              gv[5] = vis * v_al;
+            }
+            Sr += p2.x * fac;
+            Sg += p2.y * fac;
+            Sb += p2.z * fac;
+          }
+          if (__ballot(valid) != 0ull) {
+#pragma unroll
+            for (int v = 0; v < kPartial; ++v) acc[g * kPartial + v] = gv[v];
+            kk[g] = k;
+            if (st.lane == 0) s_m[wv][q] |= 1ull << bit;
+            break;
+          }
+        }
+      }
+      if (kk[0] < 0) break;
+      const float sum = reduce64(acc);
+      if (st.lane < 63) {
+        const int g = st.lane / kPartial;
+        const int v = st.lane - g * kPartial;
+        int k = kk[0];
+#pragma unroll
+        for (int g2 = 1; g2 < 7; ++g2) k = (g == g2) ? kk[g2] : k;
+        if (k >= 0) L.w[v][wv][k] = sum;
+      }
     }
     __syncthreads();
     for (int k = threadIdx.x; k < n; k += blockDim.x) {
@@ -559,11 +585,26 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster2d_bwd(
   if (loaded_b0 >= 0) block_store_partials(L, loaded_b0, min(kRasterThreads, eff - loaded_b0), partial);
 }
 
+__global__ void k_selftest_reduce64(float* out) {
+  float v[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) v[i] = (float)((threadIdx.x * 7 + i * 13) % 97) + 0.25f * (float)i;
+  out[threadIdx.x] = reduce64(v);
+}
+
 }  // namespace gsr
 
 using namespace gsr;
 
 extern "C" {
+
+// Self-test of the transposed wave reduction: out[l] = sum over lanes of v_lane[l] for the
+// pattern v_lane[i] = ((lane*7 + i*13) % 97) + i/4 (checked on the host by tests/).
+int gsr_selftest_reduce64(float* out, void* stream) {
+  hipLaunchKernelGGL(k_selftest_reduce64, dim3(1), dim3(64), 0, (hipStream_t)stream, out);
+  GSR_LAUNCH_CHECK("k_selftest_reduce64");
+  return GSR_OK;
+}
 
 int gsr3d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_order, int C, int width, int height, const float* bg, float* rgb,

@@ -20,6 +20,17 @@ from _util import assert_close, grad_close
 pytestmark = pytest.mark.gpu
 
 
+def test_selftest_reduce64(cuda):
+    """The transposed permlane/DPP butterfly reduction gives lane l the sum of value l."""
+    from gsr import _lib
+    out = torch.empty(64, device=cuda)
+    _lib.check(_lib.lib().gsr_selftest_reduce64(out.data_ptr(), torch.cuda.current_stream().cuda_stream), "selftest")
+    lanes = torch.arange(64, dtype=torch.float64)[:, None]
+    i = torch.arange(64, dtype=torch.float64)[None, :]
+    v = ((lanes * 7 + i * 13) % 97) + 0.25 * i
+    assert torch.allclose(out.cpu().double(), v.sum(0), rtol=0, atol=1e-3), out
+
+
 def _oracle3d():
     from oracle import oracle3d
     return oracle3d
