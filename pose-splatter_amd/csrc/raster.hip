@@ -35,11 +35,13 @@ __device__ __forceinline__ bool cull_keep(const float4 p0, const float4 p1, floa
                                           float by1, float cut) {
   const float ratio = IS2D ? p0.z / cut : p0.z * 255.f;
   if (!(ratio >= 1.f)) return false;
-  const float L = __logf(ratio) * 1.0001f + 1e-4f;
+  // approximate v_log / v_rcp / v_sqrt (~1 ulp) — the 0.1% + 0.01 px margin absorbs them
+  const float L = __builtin_amdgcn_logf(ratio) * 0.69320154f + 1e-4f;   // ln2 * 1.0001
   const float det = p1.x * p1.z - 0.25f * p1.y * p1.y;
   if (!(det > 0.f)) return true;
-  const float hx = sqrtf(L * p1.z / det) * 1.001f + 0.01f;
-  const float hy = sqrtf(L * p1.x / det) * 1.001f + 0.01f;
+  const float id = __builtin_amdgcn_rcpf(det);
+  const float hx = __builtin_amdgcn_sqrtf(L * p1.z * id) * 1.001f + 0.01f;
+  const float hy = __builtin_amdgcn_sqrtf(L * p1.x * id) * 1.001f + 0.01f;
   return (p0.x + hx >= bx0) && (p0.x - hx <= bx1) && (p0.y + hy >= by0) && (p0.y - hy <= by1);
 }
 
@@ -291,6 +293,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
   __shared__ float4 s_p2[kRasterThreads];
   __shared__ PartialLds L;
   __shared__ unsigned long long s_m[4][4];
+  __shared__ short s_list[4][kRasterThreads];
   const int ct = busy[blockIdx.x];
   const SubTile st = sub_tile<false>(ct, tw, th, W, H);
   const int wv = st.wv;
@@ -327,43 +330,32 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
       s_p2[threadIdx.x] = s.p2;
     }
     __syncthreads();
-    unsigned long long mq[4];
+    // cull the staged batch against this wave's sub-tile; survivors are listed back to front
+    int nsurv = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 3; q >= 0; --q) {
       const int k = q * 64 + st.lane;
       const bool keep = k < n && (b0 + k) <= wlast &&
                         cull_keep<false>(s_p0[k], s_p1[k], st.bx0, st.bx1, st.by0, st.by1, 0.f);
-      mq[q] = __ballot(keep);
+      const unsigned long long mk = __ballot(keep);
+      if (st.lane == 0) s_m[wv][q] = mk;
+      if (keep) {
+        const unsigned long long above = st.lane == 63 ? 0ull : (mk >> (st.lane + 1));
+        s_list[wv][nsurv + __popcll(above)] = (short)k;
+      }
+      nsurv += __popcll(mk);
     }
-    if (st.lane == 0) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) s_m[wv][q] = 0ull;
-    }
-    // Walk the survivors back to front; entries that touch a valid pixel are gathered in
-    // groups of 7 (63 of reduce64's 64 slots: 7 entries x 9 partials) and reduced at once.
-    int q = 3;
-    unsigned long long m = mq[3];
-    bool more = true;
-    while (more) {
+    __builtin_amdgcn_wave_barrier();
+    // Walk the survivors back to front in groups of 7 (63 of reduce64's 64 slots:
+    // 7 entries x 9 partials), reducing each group across the wave at once.
+    for (int g0 = 0; g0 < nsurv; g0 += 7) {
       float acc[64];
 #pragma unroll
       for (int v = 0; v < 64; ++v) acc[v] = 0.f;
-      int kk[7];
 #pragma unroll
       for (int g = 0; g < 7; ++g) {
-        kk[g] = -1;
-        while (more) {
-          while (m == 0ull && q > 0) {
-            --q;
-            m = mq[q];
-          }
-          if (m == 0ull) {
-            more = false;
-            break;
-          }
-          const int bit = 63 - __clzll(m);
-          m &= ~(1ull << bit);
-          const int k = q * 64 + bit;
+        if (g0 + g < nsurv) {
+          const int k = s_list[wv][g0 + g];
           const int ek = b0 + k;
           const float4 p0 = s_p0[k];
           const float4 p1 = s_p1[k];
@@ -374,50 +366,33 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
           const float raw = p0.z * vis;
           const float alpha = fminf(kAlphaMax, raw);
           const bool valid = ek <= last && !(sigma < 0.f || alpha < kAlphaThreshold);
-          float gv[kPartial];
-#pragma unroll
-          for (int v = 0; v < kPartial; ++v) gv[v] = 0.f;
           if (valid) {
-            const float ra = 1.f / (1.f - alpha);
+            const float ra = __builtin_amdgcn_rcpf(1.f - alpha);
             T *= ra;
             const float fac = alpha * T;
-            gv[6] = fac * vr;
-            gv[7] = fac * vg;
-            gv[8] = fac * vb;
-            const float v_al = (p2.x * T - Sr * ra) * vr + (p2.y * T - Sg * ra) * vg + (p2.z * T - Sb * ra) * vb +
-                               vTa * ra;
+            acc[g * kPartial + 6] = fac * vr;
+            acc[g * kPartial + 7] = fac * vg;
+            acc[g * kPartial + 8] = fac * vb;
+            const float v_al = (p2.x * T - Sr * ra) * vr + (p2.y * T - Sg * ra) * vg +
+                               (p2.z * T - Sb * ra) * vb + vTa * ra;
             if (raw <= kAlphaMax) {
               const float v_sig = -raw * v_al;
-              gv[2] = v_sig * dx * dx;
-              gv[3] = v_sig * dx * dy;
-              gv[4] = v_sig * dy * dy;
-              gv[0] = v_sig * (2.f * p1.x * dx + p1.y * dy);
-              gv[1] = v_sig * (p1.y * dx + 2.f * p1.z * dy);
-              gv[5] = vis * v_al;
+              acc[g * kPartial + 2] = v_sig * dx * dx;
+              acc[g * kPartial + 3] = v_sig * dx * dy;
+              acc[g * kPartial + 4] = v_sig * dy * dy;
+              acc[g * kPartial + 0] = v_sig * (2.f * p1.x * dx + p1.y * dy);
+              acc[g * kPartial + 1] = v_sig * (p1.y * dx + 2.f * p1.z * dy);
+              acc[g * kPartial + 5] = vis * v_al;
             }
             Sr += p2.x * fac;
             Sg += p2.y * fac;
             Sb += p2.z * fac;
           }
-          if (__ballot(valid) != 0ull) {
-#pragma unroll
-            for (int v = 0; v < kPartial; ++v) acc[g * kPartial + v] = gv[v];
-            kk[g] = k;
-            if (st.lane == 0) s_m[wv][q] |= 1ull << bit;
-            break;
-          }
         }
       }
-      if (kk[0] < 0) break;
       const float sum = reduce64(acc);
-      if (st.lane < 63) {
-        const int g = st.lane / kPartial;
-        const int v = st.lane - g * kPartial;
-        int k = kk[0];
-#pragma unroll
-        for (int g2 = 1; g2 < 7; ++g2) k = (g == g2) ? kk[g2] : k;
-        if (k >= 0) L.w[v][wv][k] = sum;
-      }
+      const int g = st.lane / kPartial;
+      if (g < 7 && g0 + g < nsurv) L.w[st.lane - g * kPartial][wv][s_list[wv][g0 + g]] = sum;
     }
     __syncthreads();
     for (int k = threadIdx.x; k < n; k += blockDim.x) {
