@@ -18,8 +18,10 @@ constexpr int kTopThreads = 1024;
 constexpr int kEmitThreads = 256;
 constexpr int kEmitPerBlock = 2048;
 constexpr int kHistMaxTiles = 16384;
-constexpr int kSortThreads = 512;
+constexpr int kSortThreads = 1024;    // 16 waves
+constexpr int kSortWaves = kSortThreads / 64;
 constexpr int kSortLdsKeys = 16384;   // 128 KB of 64-bit keys
+constexpr int kSortRounds = kSortLdsKeys / kSortThreads;   // 64-element rounds per wave
 
 // ---------------------------------------------------------------- per-Gaussian scan
 __global__ __launch_bounds__(kScanThreads) void k_scan_partials(const int32_t* __restrict__ x, int64_t n,
@@ -139,7 +141,7 @@ __device__ __forceinline__ uint64_t make_key(const Splat* rec, int64_t cn, int o
     const uint32_t d = __float_as_uint(rec[cn].p0.w);
     return ((uint64_t)d << 32) | (uint64_t)(uint32_t)cn;
   }
-  return (uint64_t)(uint32_t)cn;
+  return ((uint64_t)(uint32_t)cn << 32) | (uint64_t)(uint32_t)cn;   // 2D: sort word = index
 }
 
 __global__ __launch_bounds__(kEmitThreads) void k_emit(const Splat* __restrict__ rec, const uint2* __restrict__ rect,
@@ -183,21 +185,106 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const Splat* __restrict__
 }
 
 // ---------------------------------------------------------------- per-tile sort
-__device__ __forceinline__ void bitonic_lds(uint64_t* s, int n2) {
-  for (int k = 2; k <= n2; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int p = threadIdx.x; p < (n2 >> 1); p += blockDim.x) {
-        const int i = 2 * p - (p & (j - 1));
-        const int l = i + j;
-        const uint64_t a = s[i], b = s[l];
-        const bool asc = (i & k) == 0;
-        if ((a > b) == asc) {
-          s[i] = b;
-          s[l] = a;
+// Keys are (sort word << 32 | c*N+n); the sort word is the depth's float bits (3D, depth >
+// 0 so integer order = float order) or the index itself (2D).  Each segment is sorted in LDS
+// by a stable LSD radix sort on the sort word, 8-bit digits, skipping digit positions that
+// do not vary inside the segment; rank-within-wave comes from 8 ballots per element (exact
+// peer mask), so a pass is one read, one block scan of 16x256 counters and one scatter.
+// Ties on the sort word (equal depths) are then put in ascending c*N+n order by a bounded
+// odd-even fix-up — the order a stable radix sort of gsplat's keys over emission order gives.
+
+__device__ __forceinline__ uint32_t sort_word(uint64_t k) { return (uint32_t)(k >> 32); }
+
+// a: n <= kSortLdsKeys keys in LDS; s_hist: kSortWaves*256 + 64 ints.
+__device__ void lds_radix_sort(uint64_t* a, int n, int* s_hist) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  int* s_misc = s_hist + kSortWaves * 256;
+  if (threadIdx.x == 0) s_misc[0] = 0;
+  __syncthreads();
+  const uint32_t w0 = sort_word(a[0]);
+  uint32_t orv = 0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) orv |= sort_word(a[i]) ^ w0;
+  if (orv) atomicOr((unsigned*)&s_misc[0], orv);
+  __syncthreads();
+  const uint32_t varying = (uint32_t)s_misc[0];
+  const int per_wave = (((n + kSortWaves - 1) / kSortWaves) + 63) & ~63;
+  const int rounds = per_wave >> 6;
+  for (int shift = 0; shift < 32; shift += 8) {
+    if (((varying >> shift) & 0xFFu) == 0u) continue;
+    for (int i = lane; i < 256; i += 64) s_hist[wv * 256 + i] = 0;
+    __builtin_amdgcn_wave_barrier();
+    uint64_t el[kSortRounds];
+    int rk[kSortRounds];
+#pragma unroll
+    for (int r = 0; r < kSortRounds; ++r) {
+      if (r < rounds) {
+        const int idx = wv * per_wave + r * 64 + lane;
+        const bool valid = idx < n;
+        el[r] = valid ? a[idx] : 0ull;
+        const uint32_t d = (sort_word(el[r]) >> shift) & 0xFFu;
+        const unsigned long long vm = __ballot(valid);
+        unsigned long long peers = vm;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          const unsigned long long bb = __ballot(valid && ((d >> b) & 1u));
+          peers &= ((d >> b) & 1u) ? bb : (vm & ~bb);
+        }
+        const int rin = __popcll(peers & lt);
+        int base = 0;
+        if (valid) base = s_hist[wv * 256 + d];
+        __builtin_amdgcn_wave_barrier();
+        if (valid && rin == 0) s_hist[wv * 256 + d] = base + __popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        rk[r] = valid ? (int)((d << 23) | (uint32_t)(base + rin)) : -1;   // pos < 2^23
+      }
+    }
+    __syncthreads();
+    // digit-major, wave-minor exclusive scan of the 16 x 256 counters: 4 per thread
+    {
+      int v[4];
+      int sum = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = threadIdx.x * 4 + j;
+        v[j] = s_hist[(c & (kSortWaves - 1)) * 256 + (c >> 4)];
+        sum += v[j];
+      }
+      int total;
+      int run = block_exclusive_scan<kSortThreads>(sum, s_misc + 8, &total);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = threadIdx.x * 4 + j;
+        s_hist[(c & (kSortWaves - 1)) * 256 + (c >> 4)] = run;
+        run += v[j];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSortRounds; ++r) {
+      if (r < rounds && rk[r] >= 0) {
+        const int d = rk[r] >> 23;
+        a[s_hist[wv * 256 + d] + (rk[r] & 0x7FFFFF)] = el[r];
+      }
+    }
+    __syncthreads();
+  }
+  // equal sort words: order by the low word (c*N+n) — odd-even passes until nothing moves
+  while (true) {
+    bool moved = false;
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) {
+      for (int i = 2 * threadIdx.x + ph; i + 1 < n; i += 2 * blockDim.x) {
+        const uint64_t x = a[i], y = a[i + 1];
+        if (sort_word(x) == sort_word(y) && x > y) {
+          a[i] = y;
+          a[i + 1] = x;
+          moved = true;
         }
       }
       __syncthreads();
     }
+    if (!__syncthreads_or(moved)) break;
   }
 }
 
@@ -236,6 +323,7 @@ __global__ __launch_bounds__(kSortThreads) void k_segsort(
     const int32_t* __restrict__ busy, const uint2* __restrict__ rect, const int32_t* __restrict__ isect_offset,
     int tw, int th, int lds_keys, int32_t* __restrict__ sorted_ids, int32_t* __restrict__ isect_pos) {
   extern __shared__ uint64_t s_keys[];
+  int* s_hist = (int*)(s_keys + lds_keys);
   const int ct = busy[blockIdx.x];
   const int start = tile_offset[ct];
   const int len = tile_offset[ct + 1] - start;
@@ -244,20 +332,18 @@ __global__ __launch_bounds__(kSortThreads) void k_segsort(
   const int ty = t / tw, tx = t - (t / tw) * tw;
   const uint64_t* src = keys + start;
   if (len <= lds_keys) {
-    const int n2 = next_pow2(len);
-    for (int i = threadIdx.x; i < n2; i += blockDim.x) s_keys[i] = i < len ? keys[start + i] : ~0ull;
+    for (int i = threadIdx.x; i < len; i += blockDim.x) s_keys[i] = keys[start + i];
     __syncthreads();
-    bitonic_lds(s_keys, n2);
+    lds_radix_sort(s_keys, len, s_hist);
   } else {
     // Large bucket: sort runs of lds_keys in LDS, then merge runs pairwise in global memory.
     uint64_t* bufA = keys + start;
     uint64_t* bufB = tmp + start;
     for (int r0 = 0; r0 < len; r0 += lds_keys) {
       const int rl = min(lds_keys, len - r0);
-      const int n2 = next_pow2(rl);
-      for (int i = threadIdx.x; i < n2; i += blockDim.x) s_keys[i] = i < rl ? bufA[r0 + i] : ~0ull;
+      for (int i = threadIdx.x; i < rl; i += blockDim.x) s_keys[i] = bufA[r0 + i];
       __syncthreads();
-      bitonic_lds(s_keys, n2);
+      lds_radix_sort(s_keys, rl, s_hist);
       for (int i = threadIdx.x; i < rl; i += blockDim.x) bufA[r0 + i] = s_keys[i];
       __syncthreads();
     }
@@ -347,9 +433,10 @@ int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_of
                      (const uint2*)rect, N, tw, th, order, use_lds, cursor, keys);
   GSR_LAUNCH_CHECK("k_emit");
   if (n_busy > 0) {
-    int lds_keys = 64;
+    int lds_keys = 1024;
     while (lds_keys < max_seg && lds_keys < kSortLdsKeys) lds_keys <<= 1;
-    hipLaunchKernelGGL(k_segsort, dim3(n_busy), dim3(kSortThreads), lds_keys * sizeof(uint64_t), s, keys, tmp,
+    const size_t lds = lds_keys * sizeof(uint64_t) + (kSortWaves * 256 + 64) * sizeof(int);
+    hipLaunchKernelGGL(k_segsort, dim3(n_busy), dim3(kSortThreads), lds, s, keys, tmp,
                        tile_offset, busy_tiles, (const uint2*)rect, isect_offset, tw, th, lds_keys, sorted_ids,
                        isect_pos);
     GSR_LAUNCH_CHECK("k_segsort");
