@@ -125,11 +125,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # GSR_DIST_BACKEND=gloo + GSR_SAME_DEVICE=1 rehearse N ranks on a single GPU (box tests);
+    # the driver's scaling runs use the defaults: backend "nccl" (RCCL), one GPU per rank.
+    if os.environ.get("GSR_SAME_DEVICE") == "1":
+        local = 0
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(os.environ.get("GSR_DIST_BACKEND", "nccl"))
     dev = torch.device("cuda", local)
 
     from gsr import render as R
@@ -139,7 +143,7 @@ def main():
     P = C * cfg.width * cfg.height
     if cfg.mode == "3d":
         params_cpu = gaussians3d(cfg.N, cfg.seed)
-        V, K = ring_cameras(C, cfg.width, cfg.height, azimuth0=2 * 3.141592653589793 * rank / (C * world))
+        V, K = ring_cameras(C, cfg.width, cfg.height)
         p_dim = 14
     else:
         params_cpu = gaussians2d(cfg.N, cfg.width, cfg.height, cfg.seed + rank)
@@ -156,9 +160,24 @@ def main():
         v_rgb = torch.randn(cfg.height, cfg.width, 3, generator=g).to(dev)
         v_alpha = torch.randn(cfg.height, cfg.width, generator=g).to(dev)
 
+    if cfg.mode == "3d" and world > 1:
+        # all ranks hold the same Gaussians; this rank renders its shard of the 6*world views
+        from gsr.multiview import sharded_backward, view_shard
+        V_all, K_all = ring_cameras(C * world, cfg.width, cfg.height)
+        V_all, K_all = V_all.to(dev), K_all.to(dev)
+        assert view_shard(C * world, world, rank).stop - view_shard(C * world, world, rank).start == C
+        g2 = torch.Generator().manual_seed(cfg.seed + 2)
+        vr_all = torch.randn(C * world, cfg.height, cfg.width, 3, generator=g2).to(dev)
+        va_all = torch.randn(C * world, cfg.height, cfg.width, generator=g2).to(dev)
+
+        def render_views(p, Vs, Ks):
+            return R.render3d(p, Vs, Ks, cfg.width, cfg.height, bg)
+
     def step():
         params.grad = None
-        if cfg.mode == "3d":
+        if cfg.mode == "3d" and world > 1:
+            params.grad = sharded_backward(render_views, params, V_all, K_all, vr_all, va_all)
+        elif cfg.mode == "3d":
             rgb, alpha = R.render3d(params, Vd, Kd, cfg.width, cfg.height, bg)
             torch.autograd.backward([rgb, alpha], [v_rgb, v_alpha])
         else:
@@ -166,9 +185,9 @@ def main():
             for _ in range(C):
                 rgb, alpha = R.render2d(params, cfg.width, cfg.height, bg)
                 torch.autograd.backward([rgb, alpha], [v_rgb, v_alpha])
-        if world > 1:
-            import torch.distributed as dist
-            dist.all_reduce(params.grad)
+            if world > 1:
+                import torch.distributed as dist
+                dist.all_reduce(params.grad)
 
     for _ in range(args.warmup):
         step()

@@ -470,10 +470,10 @@ def render3d_pixelloop(params, viewmats, Ks, width, height, background, **kw):
                     dy = xy[1] - (i + 0.5)
                     sigma = 0.5 * (con[0] * dx * dx + con[2] * dy * dy) + con[1] * dx * dy
                     al = torch.clamp(opac[n] * torch.exp(-sigma), max=Ref3D.ALPHA_MAX)
-                    if float(sigma) < 0 or float(al) < Ref3D.ALPHA_THRESHOLD:
+                    if float(sigma.detach()) < 0 or float(al.detach()) < Ref3D.ALPHA_THRESHOLD:
                         continue
                     nT = T * (1 - al)
-                    if float(nT) <= Ref3D.T_MIN:
+                    if float(nT.detach()) <= Ref3D.T_MIN:
                         break
                     Cc = Cc + colors[n] * al * T
                     T = nT

@@ -1,0 +1,70 @@
+"""CPU: libgsr.so (the C ABI) loads and exports every function include/gsr.h declares.
+
+Only argument-validation paths are called here (they return before any HIP call), so no
+GPU is needed; compute calls are exercised by the -m gpu tests.
+"""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "gsr.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gsr[0-9a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_entry_points():
+    names = _declared()
+    for n in ["gsr3d_project_fwd", "gsr2d_project_fwd", "gsr_bin_offsets", "gsr_bin_sort",
+              "gsr3d_raster_fwd", "gsr3d_raster_bwd", "gsr2d_raster_fwd", "gsr2d_raster_bwd",
+              "gsr3d_project_bwd", "gsr2d_project_bwd", "gsr_last_error", "gsr_version"]:
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol():
+    from gsr import _lib
+    lib = _lib.lib()
+    for name in _declared():
+        assert hasattr(lib, name), f"{name} missing from {_lib.LIB_PATH}"
+    assert set(_declared()) == set(_lib.EXPORTS), "ctypes prototypes out of sync with gsr.h"
+    assert lib.gsr_version() >= 1
+
+
+def test_invalid_arguments_are_reported_not_launched():
+    from gsr import _lib
+    lib = _lib.lib()
+    rc = lib.gsr3d_project_fwd(None, 10, 14, None, None, 0, 64, 64, 0.01, 1e10, 0.0, 0.3, 0,
+                               None, None, None, None, None)
+    assert rc == -1 and b"bad N" in lib.gsr_last_error()
+    rc = lib.gsr3d_project_fwd(None, 10, 14, None, None, 1, 64, 64, 0.01, 1e10, 0.0, 0.3, 7,
+                               None, None, None, None, None)
+    assert rc == -1 and b"radius_mode" in lib.gsr_last_error()
+    rc = lib.gsr2d_project_fwd(None, 10, 9, 64, 64, 2.0, None, None, None, None, None)
+    assert rc == -1 and b"eps_cut" in lib.gsr_last_error()
+    rc = lib.gsr_bin_sort(None, None, None, None, None, 1, 10, 64, 64, 5, 0, 0, 0, None, 0, None, None, None)
+    assert rc == -1 and b"bad order" in lib.gsr_last_error()
+    with pytest.raises(ValueError, match="bad order"):
+        _lib.check(rc, "gsr_bin_sort")
+
+
+def test_workspace_queries():
+    from gsr import _lib
+    lib = _lib.lib()
+    assert lib.gsr_bin_offsets_workspace(10_000, 132) >= 4
+    assert lib.gsr_bin_sort_workspace(1000, 132) >= 16 * 1000
+    assert lib.gsr2d_raster_bwd_workspace(1000, 132) > 0
+
+
+def test_missing_library_fails_loudly(tmp_path, monkeypatch):
+    from gsr import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(_lib.GsrLibraryError):
+        _lib.lib()
