@@ -64,10 +64,14 @@ extern "C" {
 #define GSR_ORDER_DEPTH 0              /* 3D: per-tile list ordered by (depth, c*N+n)   */
 #define GSR_ORDER_INDEX 1              /* 2D: per-tile list ordered by parameter index  */
 
+#define GSR_CHUNK 256                  /* list entries per backward work unit (chunk)   */
+
 typedef struct gsr_bin_stats {
   int64_t n_isect;     /* total (Gaussian, tile) intersections I                     */
   int32_t max_seg;     /* longest per-tile list                                       */
   int32_t n_busy;      /* tiles with a non-empty list                                 */
+  int32_t n_chunks;    /* sum over tiles of ceil(list length / GSR_CHUNK)              */
+  int32_t reserved;
 } gsr_bin_stats;
 
 int gsr_version(void);
@@ -102,12 +106,13 @@ int gsr2d_project_fwd(const float* params, int64_t N, int64_t row_stride, int wi
 size_t gsr_bin_offsets_workspace(int64_t CN, int64_t CT);
 
 /* Exclusive scans: isect_offset [CN] (per-Gaussian emission offsets), tile_offset [CT+1],
- * busy_tiles [CT] (rasterizer visit order: the stats.n_busy non-empty tiles first, longest
- * lists first, then the empty tiles), stats (device). */
+ * chunk_base [CT+1] (first GSR_CHUNK-entry chunk of each tile's list), busy_tiles [CT]
+ * (rasterizer visit order: the stats.n_busy non-empty tiles first, longest lists first,
+ * then the empty tiles), stats (device). */
 int gsr_bin_offsets(const int32_t* isect_count, int64_t CN, const int32_t* tile_count,
                     int64_t CT, void* workspace, size_t workspace_bytes,
-                    int32_t* isect_offset, int32_t* tile_offset, int32_t* busy_tiles,
-                    gsr_bin_stats* stats, void* stream);
+                    int32_t* isect_offset, int32_t* tile_offset, int32_t* chunk_base,
+                    int32_t* busy_tiles, gsr_bin_stats* stats, void* stream);
 
 /* Workspace for gsr_bin_sort, bytes (depends on the I read back from stats). */
 size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT);
@@ -126,18 +131,25 @@ int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_of
 /* ---------------------------------------------------------------- (c) rasterisation */
 
 /* Front-to-back compositing (gsplat classic), one workgroup per 16x16 tile, visited in
- * tile_order (the busy_tiles array of gsr_bin_offsets: all C*tiles entries).  bg [C,3].  Outputs rgb [C,H,W,3], alpha [C,H,W], final_T [C,H,W] (exact transmittance,
- * kept for the backward), last [C,H,W] (index of the last contributing sorted entry, -1
- * if none), tile_end [CT] (1 + max last over the tile, or the tile's start). */
+ * tile_order (the busy_tiles array of gsr_bin_offsets: all C*tiles entries).  bg [C,3].
+ * Outputs rgb [C,H,W,3], alpha [C,H,W], final_T [C,H,W] (exact transmittance, kept for the
+ * backward), last [C,H,W] (index of the last contributing sorted entry, -1 if none),
+ * tile_end [CT] (1 + max last over the tile, or the tile's start), and for the
+ * chunk-parallel backward: chunk_state [n_chunks*256*4] ({T at the chunk's start, the
+ * chunk's own rgb sum} per pixel of the tile, for every GSR_CHUNK-entry chunk a pixel
+ * reached) and chunk_tile [n_chunks] (owning tile of each chunk). */
 int gsr3d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
-                     const int32_t* tile_order, int C, int width, int height, const float* bg,
-                     float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
+                     const int32_t* tile_order, const int32_t* chunk_base, int C, int width,
+                     int height, const float* bg, float* rgb, float* alpha, float* final_T,
+                     int32_t* last, int32_t* tile_end, float* chunk_state, int32_t* chunk_tile,
                      void* stream);
 
-/* Backward of gsr3d_raster_fwd.  v_rgb [C,H,W,3], v_alpha [C,H,W] (contiguous).
- * Writes partial [I*9] for every sorted entry s in [tile start, tile_end). */
+/* Backward of gsr3d_raster_fwd, one workgroup per (tile, chunk).  v_rgb [C,H,W,3],
+ * v_alpha [C,H,W] (contiguous).  Writes partial [I*9] for every sorted entry s in
+ * [tile start, tile_end). */
 int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
-                     const int32_t* tile_end, const int32_t* busy_tiles, int32_t n_busy,
+                     const int32_t* tile_end, const int32_t* chunk_base,
+                     const int32_t* chunk_tile, const float* chunk_state, int32_t n_chunks,
                      int C, int width, int height, const float* bg, const float* final_T,
                      const int32_t* last, const float* v_rgb, const float* v_alpha,
                      float* partial, void* stream);

@@ -15,6 +15,7 @@ constexpr int kScanThreads = 256;
 constexpr int kScanItems = 16;
 constexpr int kScanTile = kScanThreads * kScanItems;   // 4096 per block
 constexpr int kTopThreads = 1024;
+constexpr int kChunkEntries = GSR_CHUNK;   // backward work unit (list entries)
 constexpr int kEmitThreads = 256;
 constexpr int kEmitPerBlock = 2048;
 constexpr int kHistMaxTiles = 16384;
@@ -77,47 +78,38 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const int32_t* __re
 }
 
 // ---------------------------------------------------------------- tile scan (single block)
-// tile_offset[0..CT], visit order (non-empty tiles longest-first, then empty), stats.
+// One pass over contiguous per-thread ranges: tile_offset[0..CT] (list starts),
+// chunk_base[0..CT] (starts of each tile's 256-entry chunks, for the chunk-parallel backward),
+// the visit order (non-empty tiles longest-first in log2 buckets, then the empty tiles in
+// ascending order) and the stats.  Order inside a bucket only affects scheduling.
 __global__ __launch_bounds__(kTopThreads) void k_tile_scan(const int32_t* __restrict__ tile_count, int64_t CT,
                                                           int32_t* __restrict__ tile_offset,
-                                                          int32_t* __restrict__ busy,
+                                                          int32_t* __restrict__ chunk_base,
+                                                          int32_t* __restrict__ order,
                                                           gsr_bin_stats* __restrict__ stats) {
   __shared__ int s_tmp[kTopThreads / 64 + 1];
   __shared__ int s_max;
+  __shared__ int s_bucket[33];
   if (threadIdx.x == 0) s_max = 0;
+  if (threadIdx.x < 33) s_bucket[threadIdx.x] = 0;
   __syncthreads();
-  long long carry = 0;
-  int bcarry = 0;
-  for (int64_t b0 = 0; b0 < CT; b0 += kTopThreads) {
-    const int64_t i = b0 + threadIdx.x;
-    const int v = i < CT ? tile_count[i] : 0;
-    int total;
-    const int ex = block_exclusive_scan<kTopThreads>(v, s_tmp, &total);
-    if (i < CT) tile_offset[i] = (int32_t)(carry + ex);
-    if (v > 0) atomicMax(&s_max, v);
-    const int nb = __syncthreads_count(v > 0);
-    carry += total;
-    bcarry += nb;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    tile_offset[CT] = (int32_t)carry;
-    stats->n_isect = carry;
-    stats->max_seg = s_max;
-    stats->n_busy = bcarry;
-  }
-  // Visit order for the rasterizer: non-empty tiles first, longest lists first (log2
-  // buckets; order inside a bucket is arbitrary — it only affects scheduling), then the
-  // empty tiles.  Longest-processing-time-first keeps the heavy tiles off the tail.
-  __shared__ int s_bucket[34];
-  if (threadIdx.x < 34) s_bucket[threadIdx.x] = 0;
-  __syncthreads();
-  for (int64_t i = threadIdx.x; i < CT; i += blockDim.x) {
+  const int64_t ipt = (CT + kTopThreads - 1) / kTopThreads;
+  const int64_t i0 = min<int64_t>(CT, ipt * threadIdx.x), i1 = min<int64_t>(CT, i0 + ipt);
+  int sc = 0, sk = 0, se = 0, mx = 0;
+  for (int64_t i = i0; i < i1; ++i) {
     const int v = tile_count[i];
-    const int b = v > 0 ? 31 - __clz(v) : 32;
-    atomicAdd(&s_bucket[b], 1);
+    sc += v;
+    sk += (v + kChunkEntries - 1) / kChunkEntries;
+    se += v == 0;
+    mx = max(mx, v);
+    if (v > 0) atomicAdd(&s_bucket[31 - __clz(v)], 1);
   }
-  __syncthreads();
+  if (mx) atomicMax(&s_max, mx);
+  int tc, tk, te;
+  int oc = block_exclusive_scan<kTopThreads>(sc, s_tmp, &tc);
+  int ok = block_exclusive_scan<kTopThreads>(sk, s_tmp, &tk);
+  int oe = block_exclusive_scan<kTopThreads>(se, s_tmp, &te);
+  const int n_busy = (int)CT - te;
   if (threadIdx.x == 0) {
     int acc = 0;
     for (int b = 31; b >= 0; --b) {
@@ -125,13 +117,25 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(const int32_t* __rest
       s_bucket[b] = acc;
       acc += c;
     }
-    s_bucket[32] = acc;
   }
   __syncthreads();
-  for (int64_t i = threadIdx.x; i < CT; i += blockDim.x) {
+  for (int64_t i = i0; i < i1; ++i) {
     const int v = tile_count[i];
-    const int b = v > 0 ? 31 - __clz(v) : 32;
-    busy[atomicAdd(&s_bucket[b], 1)] = (int32_t)i;
+    tile_offset[i] = oc;
+    chunk_base[i] = ok;
+    oc += v;
+    ok += (v + kChunkEntries - 1) / kChunkEntries;
+    if (v > 0) order[atomicAdd(&s_bucket[31 - __clz(v)], 1)] = (int32_t)i;
+    else order[n_busy + oe++] = (int32_t)i;
+  }
+  if (threadIdx.x == 0) {
+    tile_offset[CT] = tc;
+    chunk_base[CT] = tk;
+    stats->n_isect = tc;
+    stats->max_seg = s_max;
+    stats->n_busy = n_busy;
+    stats->n_chunks = tk;
+    stats->reserved = 0;
   }
 }
 
@@ -384,7 +388,7 @@ size_t gsr_bin_offsets_workspace(int64_t CN, int64_t CT) {
 
 int gsr_bin_offsets(const int32_t* isect_count, int64_t CN, const int32_t* tile_count, int64_t CT,
                     void* workspace, size_t workspace_bytes, int32_t* isect_offset, int32_t* tile_offset,
-                    int32_t* busy_tiles, gsr_bin_stats* stats, void* stream) {
+                    int32_t* chunk_base, int32_t* busy_tiles, gsr_bin_stats* stats, void* stream) {
   GSR_REQUIRE(CN >= 0 && CN < (1ll << 31), "gsr_bin_offsets: bad CN=%lld", (long long)CN);
   GSR_REQUIRE(CT >= 1 && CT < (1ll << 31), "gsr_bin_offsets: bad CT=%lld", (long long)CT);
   GSR_REQUIRE(workspace_bytes >= gsr_bin_offsets_workspace(CN, CT), "gsr_bin_offsets: workspace too small");
@@ -397,7 +401,8 @@ int gsr_bin_offsets(const int32_t* isect_count, int64_t CN, const int32_t* tile_
     hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(kScanThreads), 0, s, isect_count, CN, bsum, isect_offset);
     GSR_LAUNCH_CHECK("k_scan");
   }
-  hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kTopThreads), 0, s, tile_count, CT, tile_offset, busy_tiles, stats);
+  hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kTopThreads), 0, s, tile_count, CT, tile_offset, chunk_base, busy_tiles,
+                     stats);
   GSR_LAUNCH_CHECK("k_tile_scan");
   return GSR_OK;
 }

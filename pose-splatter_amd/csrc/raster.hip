@@ -15,6 +15,7 @@
 namespace gsr {
 
 constexpr int kRasterThreads = 256;
+constexpr int kChunk3 = GSR_CHUNK;   // backward work unit: list entries per chunk
 
 __device__ __forceinline__ void tile_coords(int ct, int tw, int th, int& c, int& ty, int& tx) {
   const int T = tw * th;
@@ -84,7 +85,8 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ order, int W, int H, int tw, int th, float cut, const float* __restrict__ bg,
     float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
-    int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end) {
+    int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end, float4* __restrict__ ckpt,
+    const int32_t* __restrict__ chunk_base, int32_t* __restrict__ chunk_tile) {
   __shared__ float4 s_p0[4][64];
   __shared__ float4 s_p1[4][64];
   __shared__ float4 s_p2[4][64];
@@ -100,6 +102,15 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   float cr = 0.f, cg = 0.f, cb = 0.f;
   int last = -1;
   bool done = !st.inside;
+  // 3D: chunk records for the chunk-parallel backward — per pixel and per GSR_CHUNK-entry
+  // chunk k of the tile's list: {T at the chunk's start, the chunk's own colour sum}.
+  int cbase = 0, kcur = 0;
+  float Ts = 1.f, dr = 0.f, dg = 0.f, db = 0.f;
+  if (!IS2D) {
+    cbase = chunk_base[ct];
+    const int nchunk = (end - start + kChunk3 - 1) / kChunk3;
+    for (int k = threadIdx.x; k < nchunk; k += blockDim.x) chunk_tile[cbase + k] = ct;
+  }
   int e = start + st.lane;
   float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0;
   bool have = e < end;
@@ -109,6 +120,15 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   }
   for (int b0 = start; b0 < end; b0 += 64) {
     if (__ballot(!done) == 0ull) break;
+    if (!IS2D && b0 > start && ((b0 - start) % kChunk3) == 0) {   // entering chunk kcur+1
+      ckpt[(int64_t)(cbase + kcur) * kRasterThreads + threadIdx.x] = make_float4(Ts, dr, dg, db);
+      cr += dr;
+      cg += dg;
+      cb += db;
+      dr = dg = db = 0.f;
+      Ts = T;
+      ++kcur;
+    }
     const bool keep = have && cull_keep<IS2D>(n0, n1, st.bx0, st.bx1, st.by0, st.by1, cut);
     const unsigned long long m = __ballot(keep);
     const int n = __popcll(m);
@@ -140,9 +160,9 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
         const bool stop = ok && (nT <= kTMin);
         const bool con = ok && !stop;
         const float vis = con ? alpha * T : 0.f;
-        cr += p2.x * vis;
-        cg += p2.y * vis;
-        cb += p2.z * vis;
+        dr += p2.x * vis;
+        dg += p2.y * vis;
+        db += p2.z * vis;
         T = con ? nT : T;
         last = con ? __float_as_int(p1.w) : last;
         done = done || stop;
@@ -158,6 +178,12 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
       }
     }
     __builtin_amdgcn_wave_barrier();
+  }
+  if (!IS2D && end > start) {
+    ckpt[(int64_t)(cbase + kcur) * kRasterThreads + threadIdx.x] = make_float4(Ts, dr, dg, db);
+    cr += dr;
+    cg += dg;
+    cb += db;
   }
   if (st.inside) {
     const int64_t pix = ((int64_t)st.c * H + st.i) * W + st.j;
@@ -277,15 +303,21 @@ __device__ __forceinline__ void block_store_partials(const PartialLds& L, int b0
 }
 
 // ---------------------------------------------------------------- 3D backward
-// Back-to-front from each pixel's last contributing entry; T_i recovered as T_{i+1}/(1-a_i)
-// (safe: a <= 0.999), starting from the EXACT final transmittance saved by the forward.
+// Chunk-parallel: one workgroup per (tile, GSR_CHUNK-entry chunk of its list), so no pixel's
+// back-to-front walk is longer than one chunk.  The forward's chunk records give each
+// pixel's state at the chunk's END exactly: T_end = T at the start of the next chunk (or
+// the exact final T for the pixel's last chunk), and the suffix colour sum S_end = sum of the
+// later chunks' own colour sums (positive terms, no cancellation).  Inside the chunk:
+//   T_i recovered as T_{i+1}/(1-a_i) with v_rcp (a <= 0.999);
 //   d rgb/d c_i = a_i T_i;  d rgb/d a_i = c_i T_i - (S_i + T_f bg)/(1-a_i);  d alpha/d a_i = T_f/(1-a_i)
 //   a = o e^{-sigma} (unclamped only):  d/do = e^{-sigma},  d/dsigma = -a.
-// The tile's list is staged 256 entries at a time; each wave walks only the entries that
-// survive its sub-tile cull (the same test as the forward), back to front.
+// Each wave culls the chunk against its 8x8 sub-tile (same test as the forward), walks its
+// survivors back to front, reduces 7 entries x 9 gradients at once (reduce64), and a 4-wave
+// LDS combine stores one 9-float partial per sorted entry.
 __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
-    const int32_t* __restrict__ tile_end, const int32_t* __restrict__ busy, int W, int H, int tw, int th,
+    const int32_t* __restrict__ tile_end, const int32_t* __restrict__ chunk_base,
+    const int32_t* __restrict__ chunk_tile, const float4* __restrict__ ckpt, int W, int H, int tw, int th,
     const float* __restrict__ bg, const float* __restrict__ final_T, const int32_t* __restrict__ last_in,
     const float* __restrict__ v_rgb, const float* __restrict__ v_alpha, float* __restrict__ partial) {
   __shared__ float4 s_p0[kRasterThreads];
@@ -294,124 +326,134 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
   __shared__ PartialLds L;
   __shared__ unsigned long long s_m[4][4];
   __shared__ short s_list[4][kRasterThreads];
-  const int ct = busy[blockIdx.x];
-  const SubTile st = sub_tile<false>(ct, tw, th, W, H);
-  const int wv = st.wv;
+  const int ct = chunk_tile[blockIdx.x];
+  const int cbase = chunk_base[ct];
+  const int kc = blockIdx.x - cbase;
   const int start = tile_offset[ct];
   const int eff = tile_end[ct];
+  const int b0 = start + kc * kChunk3;
+  if (b0 >= eff) return;   // nothing past the tile's last contributing entry needs a partial
+  const int n = min(kChunk3, eff - b0);
+  const SubTile st = sub_tile<false>(ct, tw, th, W, H);
+  const int wv = st.wv;
   float Tf = 1.f, vr = 0.f, vg = 0.f, vb = 0.f, va = 0.f;
   int last = -1;
   if (st.inside) {
     const int64_t pix = ((int64_t)st.c * H + st.i) * W + st.j;
-    Tf = final_T[pix];
     last = last_in[pix];
-    vr = v_rgb[pix * 3 + 0];
-    vg = v_rgb[pix * 3 + 1];
-    vb = v_rgb[pix * 3 + 2];
-    va = v_alpha[pix];
+    if (last >= b0) {
+      Tf = final_T[pix];
+      vr = v_rgb[pix * 3 + 0];
+      vg = v_rgb[pix * 3 + 1];
+      vb = v_rgb[pix * 3 + 2];
+      va = v_alpha[pix];
+    }
+  }
+  // state at the end of this chunk
+  float T = Tf, Sr = 0.f, Sg = 0.f, Sb = 0.f;
+  if (last >= b0) {
+    const int kl = (last - start) / kChunk3;
+    for (int j = kc + 1; j <= kl; ++j) {
+      const float4 r = ckpt[(int64_t)(cbase + j) * kRasterThreads + threadIdx.x];
+      if (j == kc + 1) T = r.x;
+      Sr += r.y;
+      Sg += r.z;
+      Sb += r.w;
+    }
   }
   const float* bgc = bg + st.c * 3;
   const float bgdot = bgc[0] * vr + bgc[1] * vg + bgc[2] * vb;
   const float vTa = Tf * (va - bgdot);
-  // the wave's deepest contributing entry: nothing beyond it matters for this wave
   int wlast = last;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wlast = max(wlast, __shfl_xor(wlast, o, 64));
-  float T = Tf, Sr = 0.f, Sg = 0.f, Sb = 0.f;
-  for (int bend = eff; bend > start; bend -= kRasterThreads) {
-    const int b0 = max(start, bend - kRasterThreads);
-    const int n = bend - b0;
-    __syncthreads();
-    const int e = b0 + threadIdx.x;
-    if (e < bend) {
-      const Splat s = rec[ids[e]];
-      s_p0[threadIdx.x] = s.p0;
-      s_p1[threadIdx.x] = s.p1;
-      s_p2[threadIdx.x] = s.p2;
+  if (threadIdx.x < n) {
+    const Splat sp = rec[ids[b0 + threadIdx.x]];
+    s_p0[threadIdx.x] = sp.p0;
+    s_p1[threadIdx.x] = sp.p1;
+    s_p2[threadIdx.x] = sp.p2;
+  }
+  __syncthreads();
+  // cull the chunk against this wave's sub-tile; survivors are listed back to front
+  int nsurv = 0;
+#pragma unroll
+  for (int q = 3; q >= 0; --q) {
+    const int k = q * 64 + st.lane;
+    const bool keep = k < n && (b0 + k) <= wlast &&
+                      cull_keep<false>(s_p0[k], s_p1[k], st.bx0, st.bx1, st.by0, st.by1, 0.f);
+    const unsigned long long mk = __ballot(keep);
+    if (st.lane == 0) s_m[wv][q] = mk;
+    if (keep) {
+      const unsigned long long above = st.lane == 63 ? 0ull : (mk >> (st.lane + 1));
+      s_list[wv][nsurv + __popcll(above)] = (short)k;
     }
-    __syncthreads();
-    // cull the staged batch against this wave's sub-tile; survivors are listed back to front
-    int nsurv = 0;
+    nsurv += __popcll(mk);
+  }
+  __builtin_amdgcn_wave_barrier();
+  for (int g0 = 0; g0 < nsurv; g0 += 7) {
+    float acc[64];
 #pragma unroll
-    for (int q = 3; q >= 0; --q) {
-      const int k = q * 64 + st.lane;
-      const bool keep = k < n && (b0 + k) <= wlast &&
-                        cull_keep<false>(s_p0[k], s_p1[k], st.bx0, st.bx1, st.by0, st.by1, 0.f);
-      const unsigned long long mk = __ballot(keep);
-      if (st.lane == 0) s_m[wv][q] = mk;
-      if (keep) {
-        const unsigned long long above = st.lane == 63 ? 0ull : (mk >> (st.lane + 1));
-        s_list[wv][nsurv + __popcll(above)] = (short)k;
-      }
-      nsurv += __popcll(mk);
-    }
-    __builtin_amdgcn_wave_barrier();
-    // Walk the survivors back to front in groups of 7 (63 of reduce64's 64 slots:
-    // 7 entries x 9 partials), reducing each group across the wave at once.
-    for (int g0 = 0; g0 < nsurv; g0 += 7) {
-      float acc[64];
+    for (int v = 0; v < 64; ++v) acc[v] = 0.f;
 #pragma unroll
-      for (int v = 0; v < 64; ++v) acc[v] = 0.f;
-#pragma unroll
-      for (int g = 0; g < 7; ++g) {
-        if (g0 + g < nsurv) {
-          const int k = s_list[wv][g0 + g];
-          const int ek = b0 + k;
-          const float4 p0 = s_p0[k];
-          const float4 p1 = s_p1[k];
-          const float4 p2 = s_p2[k];
-          const float dx = p0.x - st.px, dy = p0.y - st.py;
-          const float sigma = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
-          const float vis = __expf(-sigma);
-          const float raw = p0.z * vis;
-          const float alpha = fminf(kAlphaMax, raw);
-          const bool valid = ek <= last && !(sigma < 0.f || alpha < kAlphaThreshold);
-          if (valid) {
-            const float ra = __builtin_amdgcn_rcpf(1.f - alpha);
-            T *= ra;
-            const float fac = alpha * T;
-            acc[g * kPartial + 6] = fac * vr;
-            acc[g * kPartial + 7] = fac * vg;
-            acc[g * kPartial + 8] = fac * vb;
-            const float v_al = (p2.x * T - Sr * ra) * vr + (p2.y * T - Sg * ra) * vg +
-                               (p2.z * T - Sb * ra) * vb + vTa * ra;
-            if (raw <= kAlphaMax) {
-              const float v_sig = -raw * v_al;
-              acc[g * kPartial + 2] = v_sig * dx * dx;
-              acc[g * kPartial + 3] = v_sig * dx * dy;
-              acc[g * kPartial + 4] = v_sig * dy * dy;
-              acc[g * kPartial + 0] = v_sig * (2.f * p1.x * dx + p1.y * dy);
-              acc[g * kPartial + 1] = v_sig * (p1.y * dx + 2.f * p1.z * dy);
-              acc[g * kPartial + 5] = vis * v_al;
-            }
-            Sr += p2.x * fac;
-            Sg += p2.y * fac;
-            Sb += p2.z * fac;
+    for (int g = 0; g < 7; ++g) {
+      if (g0 + g < nsurv) {
+        const int k = s_list[wv][g0 + g];
+        const int ek = b0 + k;
+        const float4 p0 = s_p0[k];
+        const float4 p1 = s_p1[k];
+        const float4 p2 = s_p2[k];
+        const float dx = p0.x - st.px, dy = p0.y - st.py;
+        const float sigma = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
+        const float vis = __expf(-sigma);
+        const float raw = p0.z * vis;
+        const float alpha = fminf(kAlphaMax, raw);
+        const bool valid = ek <= last && !(sigma < 0.f || alpha < kAlphaThreshold);
+        if (valid) {
+          const float ra = __builtin_amdgcn_rcpf(1.f - alpha);
+          T *= ra;
+          const float fac = alpha * T;
+          acc[g * kPartial + 6] = fac * vr;
+          acc[g * kPartial + 7] = fac * vg;
+          acc[g * kPartial + 8] = fac * vb;
+          const float v_al = (p2.x * T - Sr * ra) * vr + (p2.y * T - Sg * ra) * vg +
+                             (p2.z * T - Sb * ra) * vb + vTa * ra;
+          if (raw <= kAlphaMax) {
+            const float v_sig = -raw * v_al;
+            acc[g * kPartial + 2] = v_sig * dx * dx;
+            acc[g * kPartial + 3] = v_sig * dx * dy;
+            acc[g * kPartial + 4] = v_sig * dy * dy;
+            acc[g * kPartial + 0] = v_sig * (2.f * p1.x * dx + p1.y * dy);
+            acc[g * kPartial + 1] = v_sig * (p1.y * dx + 2.f * p1.z * dy);
+            acc[g * kPartial + 5] = vis * v_al;
           }
+          Sr += p2.x * fac;
+          Sg += p2.y * fac;
+          Sb += p2.z * fac;
         }
       }
-      const float sum = reduce64(acc);
-      const int g = st.lane / kPartial;
-      if (g < 7 && g0 + g < nsurv) L.w[st.lane - g * kPartial][wv][s_list[wv][g0 + g]] = sum;
     }
-    __syncthreads();
-    for (int k = threadIdx.x; k < n; k += blockDim.x) {
-      const int q = k >> 6;
-      const unsigned long long bit = 1ull << (k & 63);
-      float acc[kPartial];
+    const float sum = reduce64(acc);
+    const int g = st.lane / kPartial;
+    if (g < 7 && g0 + g < nsurv) L.w[st.lane - g * kPartial][wv][s_list[wv][g0 + g]] = sum;
+  }
+  __syncthreads();
+  if (threadIdx.x < n) {
+    const int k = threadIdx.x;
+    const int q = k >> 6;
+    const unsigned long long bit = 1ull << (k & 63);
+    float acc[kPartial];
 #pragma unroll
-      for (int v = 0; v < kPartial; ++v) acc[v] = 0.f;
+    for (int v = 0; v < kPartial; ++v) acc[v] = 0.f;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        if (s_m[w][q] & bit) {
+    for (int w = 0; w < 4; ++w) {
+      if (s_m[w][q] & bit) {
 #pragma unroll
-          for (int v = 0; v < kPartial; ++v) acc[v] += L.w[v][w][k];
-        }
+        for (int v = 0; v < kPartial; ++v) acc[v] += L.w[v][w][k];
       }
-      float* dst = partial + (int64_t)(b0 + k) * kPartial;
-#pragma unroll
-      for (int v = 0; v < kPartial; ++v) dst[v] = acc[v];
     }
+    float* dst = partial + (int64_t)(b0 + k) * kPartial;
+#pragma unroll
+    for (int v = 0; v < kPartial; ++v) dst[v] = acc[v];
   }
 }
 
@@ -582,30 +624,32 @@ int gsr_selftest_reduce64(float* out, void* stream) {
 }
 
 int gsr3d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
-                     const int32_t* tile_order, int C, int width, int height, const float* bg, float* rgb,
-                     float* alpha, float* final_T, int32_t* last, int32_t* tile_end, void* stream) {
+                     const int32_t* tile_order, const int32_t* chunk_base, int C, int width, int height,
+                     const float* bg, float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
+                     float* chunk_state, int32_t* chunk_tile, void* stream) {
   GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "gsr3d_raster_fwd: bad C=%d or image %dx%d", C, width, height);
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   const int64_t CT = (int64_t)C * tw * th;
   GSR_REQUIRE(CT < (1ll << 31), "gsr3d_raster_fwd: too many tiles");
   hipLaunchKernelGGL(k_raster_fwd<false>, dim3((unsigned)CT), dim3(kRasterThreads), 0, (hipStream_t)stream,
                      (const Splat*)rec, sorted_ids, tile_offset, tile_order, width, height, tw, th, kAlphaThreshold,
-                     bg, rgb, alpha, final_T, last, tile_end);
+                     bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state, chunk_base, chunk_tile);
   GSR_LAUNCH_CHECK("k_raster_fwd<3d>");
   return GSR_OK;
 }
 
 int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
-                     const int32_t* tile_end, const int32_t* busy_tiles, int32_t n_busy, int C, int width,
-                     int height, const float* bg, const float* final_T, const int32_t* last, const float* v_rgb,
-                     const float* v_alpha, float* partial, void* stream) {
+                     const int32_t* tile_end, const int32_t* chunk_base, const int32_t* chunk_tile,
+                     const float* chunk_state, int32_t n_chunks, int C, int width, int height, const float* bg,
+                     const float* final_T, const int32_t* last, const float* v_rgb, const float* v_alpha,
+                     float* partial, void* stream) {
   GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "gsr3d_raster_bwd: bad C=%d or image %dx%d", C, width, height);
-  GSR_REQUIRE(n_busy >= 0, "gsr3d_raster_bwd: bad n_busy");
-  if (n_busy == 0) return GSR_OK;
+  GSR_REQUIRE(n_chunks >= 0, "gsr3d_raster_bwd: bad n_chunks");
+  if (n_chunks == 0) return GSR_OK;
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
-  hipLaunchKernelGGL(k_raster3d_bwd, dim3(n_busy), dim3(kRasterThreads), 0, (hipStream_t)stream,
-                     (const Splat*)rec, sorted_ids, tile_offset, tile_end, busy_tiles, width, height, tw, th, bg,
-                     final_T, last, v_rgb, v_alpha, partial);
+  hipLaunchKernelGGL(k_raster3d_bwd, dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
+                     (const Splat*)rec, sorted_ids, tile_offset, tile_end, chunk_base, chunk_tile,
+                     (const float4*)chunk_state, width, height, tw, th, bg, final_T, last, v_rgb, v_alpha, partial);
   GSR_LAUNCH_CHECK("k_raster3d_bwd");
   return GSR_OK;
 }

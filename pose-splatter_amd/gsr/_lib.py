@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get(
     "GSR_LIBRARY", os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libgsr.so"))
 
 TILE = 16
+CHUNK = 256
 RADIUS_OPACITY_AABB = 0
 RADIUS_ISOTROPIC_3SIGMA = 1
 ORDER_DEPTH = 0
@@ -32,7 +33,8 @@ class GsrLibraryError(RuntimeError):
 
 
 class BinStats(ctypes.Structure):
-    _fields_ = [("n_isect", ctypes.c_int64), ("max_seg", ctypes.c_int32), ("n_busy", ctypes.c_int32)]
+    _fields_ = [("n_isect", ctypes.c_int64), ("max_seg", ctypes.c_int32), ("n_busy", ctypes.c_int32),
+                ("n_chunks", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 _P = ctypes.c_void_p
@@ -50,13 +52,14 @@ EXPORTS = {
                                          _I32, _P, _P, _P, _P, _P]),
     "gsr2d_project_fwd": (ctypes.c_int, [_P, _I64, _I64, _I32, _I32, _F, _P, _P, _P, _P, _P]),
     "gsr_bin_offsets_workspace": (_SZ, [_I64, _I64]),
-    "gsr_bin_offsets": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _SZ, _P, _P, _P, _P, _P]),
+    "gsr_bin_offsets": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _SZ, _P, _P, _P, _P, _P, _P]),
     "gsr_bin_sort_workspace": (_SZ, [_I64, _I64]),
     "gsr_bin_sort": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I32, _I64, _I32,
                                     _I32, _P, _SZ, _P, _P, _P]),
-    "gsr3d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
-    "gsr3d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P, _P, _P, _P,
-                                        _P, _P, _P]),
+    "gsr3d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P,
+                                        _P, _P]),
+    "gsr3d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P, _P, _P,
+                                        _P, _P, _P, _P]),
     "gsr2d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "gsr2d_raster_bwd_workspace": (_SZ, [_I64, _I64]),
     "gsr2d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P,

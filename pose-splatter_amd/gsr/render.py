@@ -115,7 +115,9 @@ class _Bins:
         self.isect_off = torch.empty(max(CN, 1), **i32)
         self.tile_off = torch.empty(self.CT + 1, **i32)
         self.busy = torch.empty(self.CT, **i32)
-        self.stats_dev = torch.zeros(4, **i32)   # gsr_bin_stats (16 B)
+        self.chunk_base = torch.empty(self.CT + 1, **i32)
+        self.stats_dev = torch.zeros(6, **i32)   # gsr_bin_stats (24 B)
+        self.n_chunks = 0
         self.n_isect = 0
         self.max_seg = 0
         self.n_busy = 0
@@ -127,12 +129,13 @@ class _Bins:
                          dtype=torch.uint8)
         with _timed("bin_offsets"):
           check(L.gsr_bin_offsets(_ptr(self.cnt), CN, _ptr(self.tile_cnt), self.CT, _ptr(ws), ws.numel(),
-                                _ptr(self.isect_off), _ptr(self.tile_off), _ptr(self.busy),
-                                _ptr(self.stats_dev), stream), "gsr_bin_offsets")
+                                _ptr(self.isect_off), _ptr(self.tile_off), _ptr(self.chunk_base),
+                                _ptr(self.busy), _ptr(self.stats_dev), stream), "gsr_bin_offsets")
         st = self.stats_dev.cpu()   # the one D2H sync of the forward
         self.n_isect = (int(st[0]) & 0xFFFFFFFF) | (int(st[1]) << 32)
         self.max_seg = int(st[2])
         self.n_busy = int(st[3])
+        self.n_chunks = int(st[4])
         if self.n_isect >= 2 ** 31:
             raise RuntimeError(f"gsr: {self.n_isect} intersections exceed the 32-bit index range")
 
@@ -192,10 +195,12 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
     b.final_T = torch.empty(C, height, width, device=dev, dtype=torch.float32)
     b.last = torch.empty(C, height, width, device=dev, dtype=torch.int32)
     b.tile_end = torch.empty(b.CT, device=dev, dtype=torch.int32)
+    b.chunk_state = torch.empty(max(b.n_chunks, 1) * 256 * 4, device=dev, dtype=torch.float32)
+    b.chunk_tile = torch.empty(max(b.n_chunks, 1), device=dev, dtype=torch.int32)
     with _timed("raster3d_fwd"):
-      check(L.gsr3d_raster_fwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), _ptr(b.busy), C, width, height,
-                             _ptr(bgc), _ptr(rgb), _ptr(alpha), _ptr(b.final_T), _ptr(b.last),
-                             _ptr(b.tile_end), stream), "gsr3d_raster_fwd")
+      check(L.gsr3d_raster_fwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), _ptr(b.busy), _ptr(b.chunk_base),
+                             C, width, height, _ptr(bgc), _ptr(rgb), _ptr(alpha), _ptr(b.final_T), _ptr(b.last),
+                             _ptr(b.tile_end), _ptr(b.chunk_state), _ptr(b.chunk_tile), stream), "gsr3d_raster_fwd")
     _record_stats(b)
     return rgb, alpha, b, (p, stride, V, Kc, bgc, width, height, opts)
 
@@ -262,8 +267,9 @@ class _Render3D(torch.autograd.Function):
             partial = torch.empty(max(b.n_isect, 1) * 9, device=dev, dtype=torch.float32)
             with _timed("raster3d_bwd"):
               check(L.gsr3d_raster_bwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), _ptr(b.tile_end),
-                                     _ptr(b.busy), b.n_busy, C, width, height, _ptr(bgc), _ptr(b.final_T),
-                                     _ptr(b.last), _ptr(v_rgb), _ptr(v_alpha), _ptr(partial), stream),
+                                     _ptr(b.chunk_base), _ptr(b.chunk_tile), _ptr(b.chunk_state), b.n_chunks,
+                                     C, width, height, _ptr(bgc), _ptr(b.final_T), _ptr(b.last), _ptr(v_rgb),
+                                     _ptr(v_alpha), _ptr(partial), stream),
                   "gsr3d_raster_bwd")
             with _timed("project3d_bwd"):
               check(L.gsr3d_project_bwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height, opts.eps2d,
