@@ -119,14 +119,17 @@ size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT);
 
 /* Emit (tile, key) pairs and sort each tile's list in LDS.  Outputs:
  *   sorted_ids [I]: c*N+n per sorted entry (what the rasterizer reads),
- *   isect_pos  [I]: for emission slot isect_offset[cn]+j (j = row-major index of the tile in
- *                   the Gaussian's rect) the sorted position s.
+ *   slot_of_k  [I]: for emission entry k = isect_offset[cn]+j (j = row-major index of the
+ *                   tile in the Gaussian's rect) its pre-sort slot in the tile's bucket,
+ *   pos_of_slot[I]: for every pre-sort slot its sorted position s; the sorted position of
+ *                   emission entry k is pos_of_slot[slot_of_k[k]] (used by *_project_bwd).
  * order: GSR_ORDER_DEPTH (3D) or GSR_ORDER_INDEX (2D).  max_seg/n_busy from stats. */
 int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_offset,
                  const int32_t* tile_offset, const int32_t* busy_tiles, int C, int64_t N,
                  int width, int height, int order, int64_t n_isect, int32_t max_seg,
                  int32_t n_busy, void* workspace, size_t workspace_bytes,
-                 int32_t* sorted_ids, int32_t* isect_pos, void* stream);
+                 int32_t* sorted_ids, int32_t* slot_of_k, int32_t* pos_of_slot,
+                 void* stream);
 
 /* ---------------------------------------------------------------- (c) rasterisation */
 
@@ -176,15 +179,15 @@ int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t*
 int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride,
                       const float* viewmats, const float* Ks, int C, int width, int height,
                       float eps2d, const uint32_t* rect, const int32_t* isect_offset,
-                      const int32_t* isect_count, const int32_t* isect_pos,
-                      const int32_t* tile_end, const float* partial, float* v_params,
-                      void* stream);
+                      const int32_t* isect_count, const int32_t* slot_of_k,
+                      const int32_t* pos_of_slot, const int32_t* tile_end,
+                      const float* partial, float* v_params, void* stream);
 
 int gsr2d_project_bwd(const float* params, int64_t N, int64_t row_stride, int width,
                       int height, const uint32_t* rect, const int32_t* isect_offset,
-                      const int32_t* isect_count, const int32_t* isect_pos,
-                      const int32_t* tile_end, const float* partial, float* v_params,
-                      void* stream);
+                      const int32_t* isect_count, const int32_t* slot_of_k,
+                      const int32_t* pos_of_slot, const int32_t* tile_end,
+                      const float* partial, float* v_params, void* stream);
 
 #ifdef __cplusplus
 }

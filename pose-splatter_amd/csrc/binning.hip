@@ -149,8 +149,9 @@ __device__ __forceinline__ uint64_t make_key(const Splat* rec, int64_t cn, int o
 }
 
 __global__ __launch_bounds__(kEmitThreads) void k_emit(const Splat* __restrict__ rec, const uint2* __restrict__ rect,
-                                                      int64_t N, int tw, int th, int order, int use_lds,
-                                                      int32_t* __restrict__ cursor, uint64_t* __restrict__ keys) {
+                                                      const int32_t* __restrict__ isect_offset, int64_t N, int tw,
+                                                      int th, int order, int use_lds, int32_t* __restrict__ cursor,
+                                                      uint64_t* __restrict__ keys, int32_t* __restrict__ slot_of_k) {
   extern __shared__ int hist[];
   const int c = blockIdx.y;
   const int T = tw * th;
@@ -179,28 +180,36 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const Splat* __restrict__
     const int x0 = r.x & 0xffff, x1 = r.x >> 16, y0 = r.y & 0xffff, y1 = r.y >> 16;
     if (x1 <= x0 || y1 <= y0) continue;
     const uint64_t key = make_key(rec, cn, order);
+    int32_t* sk = slot_of_k + isect_offset[cn];   // emission entries of (c,n): rect row-major
     for (int ty = y0; ty < y1; ++ty)
       for (int tx = x0; tx < x1; ++tx) {
         const int t = ty * tw + tx;
         const int slot = use_lds ? atomicAdd(&hist[t], 1) : atomicAdd(&gcur[t], 1);
         keys[slot] = key;
+        *sk++ = slot;
       }
   }
 }
 
 // ---------------------------------------------------------------- per-tile sort
-// Keys are (sort word << 32 | c*N+n); the sort word is the depth's float bits (3D, depth >
-// 0 so integer order = float order) or the index itself (2D).  Each segment is sorted in LDS
-// by a stable LSD radix sort on the sort word, 8-bit digits, skipping digit positions that
-// do not vary inside the segment; rank-within-wave comes from 8 ballots per element (exact
-// peer mask), so a pass is one read, one block scan of 16x256 counters and one scatter.
-// Ties on the sort word (equal depths) are then put in ascending c*N+n order by a bounded
-// odd-even fix-up — the order a stable radix sort of gsplat's keys over emission order gives.
+// Emitted keys are (sort word << 32 | c*N+n); the sort word is the depth's float bits (3D,
+// depth > 0 so integer order = float order) or the index itself (2D).  In LDS each element is
+// (sort word << 32 | p), p = its pre-sort position in the tile's bucket, so every lookup after
+// the sort (c*N+n, and the slot → sorted-position map used by the backward) stays inside the
+// bucket's own window of the key array (L2-resident) instead of gathering per-Gaussian data.
+// The LDS sort is a stable LSD radix sort on the sort word, 8-bit digits, skipping digit
+// positions that do not vary inside the segment; rank-within-wave comes from 8 ballots per
+// element (exact peer mask), so a pass is one read, one block scan of 16x256 counters and one
+// scatter.  Ties on the sort word (equal depths) are then put in ascending c*N+n order by a
+// bounded odd-even fix-up — the order a stable radix sort of gsplat's keys over emission
+// order gives.
 
 __device__ __forceinline__ uint32_t sort_word(uint64_t k) { return (uint32_t)(k >> 32); }
+__device__ __forceinline__ uint32_t low_word(uint64_t k) { return (uint32_t)(k & 0xffffffffull); }
 
-// a: n <= kSortLdsKeys keys in LDS; s_hist: kSortWaves*256 + 64 ints.
-__device__ void lds_radix_sort(uint64_t* a, int n, int* s_hist) {
+// a: n <= kSortLdsKeys elements (word << 32 | p) in LDS; seg: the bucket's original keys
+// (tie-break by their low word); s_hist: kSortWaves*256 + 64 ints.
+__device__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, const uint64_t* __restrict__ seg) {
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const unsigned long long lt = (1ull << lane) - 1ull;
   int* s_misc = s_hist + kSortWaves * 256;
@@ -273,14 +282,14 @@ __device__ void lds_radix_sort(uint64_t* a, int n, int* s_hist) {
     }
     __syncthreads();
   }
-  // equal sort words: order by the low word (c*N+n) — odd-even passes until nothing moves
+  // equal sort words: order by c*N+n — odd-even passes until nothing moves
   while (true) {
     bool moved = false;
 #pragma unroll
     for (int ph = 0; ph < 2; ++ph) {
       for (int i = 2 * threadIdx.x + ph; i + 1 < n; i += 2 * blockDim.x) {
         const uint64_t x = a[i], y = a[i + 1];
-        if (sort_word(x) == sort_word(y) && x > y) {
+        if (sort_word(x) == sort_word(y) && low_word(seg[low_word(x)]) > low_word(seg[low_word(y)])) {
           a[i] = y;
           a[i + 1] = x;
           moved = true;
@@ -298,10 +307,11 @@ __device__ __forceinline__ int next_pow2(int v) {
   return p;
 }
 
-// Merge two sorted runs [a, a+na) and [b, b+nb) of unique keys into out (block-cooperative,
-// per-element rank by binary search).
-__device__ void merge_runs(const uint64_t* __restrict__ a, int na, const uint64_t* __restrict__ b, int nb,
-                           uint64_t* __restrict__ out) {
+// Merge two sorted runs of unique keys (with payloads) into out (block-cooperative, per-element
+// rank by binary search in the other run).
+__device__ void merge_runs(const uint64_t* __restrict__ a, const int32_t* __restrict__ pa, int na,
+                           const uint64_t* __restrict__ b, const int32_t* __restrict__ pb, int nb,
+                           uint64_t* __restrict__ out, int32_t* __restrict__ pout) {
   for (int i = threadIdx.x; i < na; i += blockDim.x) {
     const uint64_t k = a[i];
     int lo = 0, hi = nb;   // count of b < k
@@ -310,6 +320,7 @@ __device__ void merge_runs(const uint64_t* __restrict__ a, int na, const uint64_
       if (b[mid] < k) lo = mid + 1; else hi = mid;
     }
     out[i + lo] = k;
+    pout[i + lo] = pa[i];
   }
   for (int i = threadIdx.x; i < nb; i += blockDim.x) {
     const uint64_t k = b[i];
@@ -319,58 +330,68 @@ __device__ void merge_runs(const uint64_t* __restrict__ a, int na, const uint64_
       if (a[mid] <= k) lo = mid + 1; else hi = mid;
     }
     out[i + lo] = k;
+    pout[i + lo] = pb[i];
   }
 }
 
+// Outputs: sorted_ids[s] = c*N+n of sorted entry s; pos_of_slot[pre-sort slot] = s.
 __global__ __launch_bounds__(kSortThreads) void k_segsort(
-    uint64_t* __restrict__ keys, uint64_t* __restrict__ tmp, const int32_t* __restrict__ tile_offset,
-    const int32_t* __restrict__ busy, const uint2* __restrict__ rect, const int32_t* __restrict__ isect_offset,
-    int tw, int th, int lds_keys, int32_t* __restrict__ sorted_ids, int32_t* __restrict__ isect_pos) {
+    uint64_t* __restrict__ keys, uint64_t* __restrict__ tmpk, int32_t* __restrict__ tmpp0,
+    int32_t* __restrict__ tmpp1, const int32_t* __restrict__ tile_offset, const int32_t* __restrict__ busy,
+    int lds_keys, int32_t* __restrict__ sorted_ids, int32_t* __restrict__ pos_of_slot) {
   extern __shared__ uint64_t s_keys[];
   int* s_hist = (int*)(s_keys + lds_keys);
   const int ct = busy[blockIdx.x];
   const int start = tile_offset[ct];
   const int len = tile_offset[ct + 1] - start;
-  const int T = tw * th;
-  const int t = ct % T;
-  const int ty = t / tw, tx = t - (t / tw) * tw;
-  const uint64_t* src = keys + start;
+  uint64_t* seg = keys + start;
   if (len <= lds_keys) {
-    for (int i = threadIdx.x; i < len; i += blockDim.x) s_keys[i] = keys[start + i];
+    for (int i = threadIdx.x; i < len; i += blockDim.x)
+      s_keys[i] = (seg[i] & 0xffffffff00000000ull) | (uint64_t)(uint32_t)i;
     __syncthreads();
-    lds_radix_sort(s_keys, len, s_hist);
-  } else {
-    // Large bucket: sort runs of lds_keys in LDS, then merge runs pairwise in global memory.
-    uint64_t* bufA = keys + start;
-    uint64_t* bufB = tmp + start;
-    for (int r0 = 0; r0 < len; r0 += lds_keys) {
-      const int rl = min(lds_keys, len - r0);
-      for (int i = threadIdx.x; i < rl; i += blockDim.x) s_keys[i] = bufA[r0 + i];
-      __syncthreads();
-      lds_radix_sort(s_keys, rl, s_hist);
-      for (int i = threadIdx.x; i < rl; i += blockDim.x) bufA[r0 + i] = s_keys[i];
-      __syncthreads();
+    lds_radix_sort(s_keys, len, s_hist, seg);
+    for (int s = threadIdx.x; s < len; s += blockDim.x) {
+      const uint32_t p = low_word(s_keys[s]);
+      sorted_ids[start + s] = (int32_t)low_word(seg[p]);
+      pos_of_slot[start + p] = start + s;
     }
-    for (int run = lds_keys; run < len; run <<= 1) {
-      for (int r0 = 0; r0 < len; r0 += 2 * run) {
-        const int na = min(run, len - r0);
-        const int nb = max(0, min(run, len - r0 - na));
-        merge_runs(bufA + r0, na, bufA + r0 + na, nb, bufB + r0);
-      }
-      __threadfence_block();
-      __syncthreads();
-      uint64_t* sw = bufA; bufA = bufB; bufB = sw;
+    return;
+  }
+  // Large bucket: sort runs of lds_keys in LDS (elements keep their bucket-local index p), write
+  // them back as (word | c*N+n) keys with p as payload, then merge runs pairwise in global memory.
+  uint64_t* kA = tmpk + start;
+  int32_t* pA = tmpp0 + start;
+  uint64_t* kB = seg;   // the original keys are dead once every run is converted
+  int32_t* pB = tmpp1 + start;
+  for (int r0 = 0; r0 < len; r0 += lds_keys) {
+    const int rl = min(lds_keys, len - r0);
+    for (int i = threadIdx.x; i < rl; i += blockDim.x)
+      s_keys[i] = (seg[r0 + i] & 0xffffffff00000000ull) | (uint64_t)(uint32_t)(r0 + i);
+    __syncthreads();
+    lds_radix_sort(s_keys, rl, s_hist, seg);
+    for (int i = threadIdx.x; i < rl; i += blockDim.x) {
+      const uint32_t p = low_word(s_keys[i]);
+      kA[r0 + i] = (s_keys[i] & 0xffffffff00000000ull) | (uint64_t)low_word(seg[p]);
+      pA[r0 + i] = (int32_t)p;
     }
-    src = bufA;
+    __syncthreads();
+  }
+  __threadfence_block();
+  __syncthreads();
+  for (int run = lds_keys; run < len; run <<= 1) {
+    for (int r0 = 0; r0 < len; r0 += 2 * run) {
+      const int na = min(run, len - r0);
+      const int nb = max(0, min(run, len - r0 - na));
+      merge_runs(kA + r0, pA + r0, na, kA + r0 + na, pA + r0 + na, nb, kB + r0, pB + r0);
+    }
+    __threadfence_block();
+    __syncthreads();
+    uint64_t* tk = kA; kA = kB; kB = tk;
+    int32_t* tp = pA; pA = pB; pB = tp;
   }
   for (int s = threadIdx.x; s < len; s += blockDim.x) {
-    const uint64_t key = (len <= lds_keys) ? s_keys[s] : src[s];
-    const int32_t cn = (int32_t)(uint32_t)(key & 0xffffffffull);
-    sorted_ids[start + s] = cn;
-    const uint2 r = rect[cn];
-    const int x0 = r.x & 0xffff, x1 = r.x >> 16, y0 = r.y & 0xffff;
-    const int j = (ty - y0) * (x1 - x0) + (tx - x0);
-    isect_pos[isect_offset[cn] + j] = start + s;
+    sorted_ids[start + s] = (int32_t)low_word(kA[s]);
+    pos_of_slot[start + pA[s]] = start + s;
   }
 }
 
@@ -408,14 +429,15 @@ int gsr_bin_offsets(const int32_t* isect_count, int64_t CN, const int32_t* tile_
 }
 
 size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT) {
-  // keys [I] + merge temp [I] (u64) + cursor [CT] (i32)
-  return (size_t)(2 * n_isect * sizeof(uint64_t) + (CT + 64) * sizeof(int32_t) + 256);
+  // keys [I] + merge keys [I] (u64), two merge payloads [I] (i32), cursor [CT] (i32)
+  return (size_t)(2 * n_isect * sizeof(uint64_t) + 2 * n_isect * sizeof(int32_t) + (CT + 64) * sizeof(int32_t) +
+                  256);
 }
 
 int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_offset, const int32_t* tile_offset,
                  const int32_t* busy_tiles, int C, int64_t N, int width, int height, int order, int64_t n_isect,
                  int32_t max_seg, int32_t n_busy, void* workspace, size_t workspace_bytes, int32_t* sorted_ids,
-                 int32_t* isect_pos, void* stream) {
+                 int32_t* slot_of_k, int32_t* pos_of_slot, void* stream) {
   GSR_REQUIRE(order == GSR_ORDER_DEPTH || order == GSR_ORDER_INDEX, "gsr_bin_sort: bad order %d", order);
   GSR_REQUIRE(n_isect >= 0 && n_isect < (1ll << 31), "gsr_bin_sort: I=%lld out of range", (long long)n_isect);
   GSR_REQUIRE((int64_t)C * N < (1ll << 31), "gsr_bin_sort: C*N too large for 32-bit ids");
@@ -426,8 +448,10 @@ int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_of
   if (n_isect == 0 || N == 0) return GSR_OK;
   hipStream_t s = (hipStream_t)stream;
   uint64_t* keys = (uint64_t*)workspace;
-  uint64_t* tmp = keys + n_isect;
-  int32_t* cursor = (int32_t*)(tmp + n_isect);
+  uint64_t* tmpk = keys + n_isect;
+  int32_t* tmpp0 = (int32_t*)(tmpk + n_isect);
+  int32_t* tmpp1 = tmpp0 + n_isect;
+  int32_t* cursor = tmpp1 + n_isect;
   if (hipMemcpyAsync(cursor, tile_offset, CT * sizeof(int32_t), hipMemcpyDeviceToDevice, s) != hipSuccess) {
     set_error("gsr_bin_sort: cursor copy failed");
     return GSR_ELAUNCH;
@@ -435,15 +459,14 @@ int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_of
   const int use_lds = T <= kHistMaxTiles;
   dim3 grid(ceil_div(N, kEmitPerBlock), C);
   hipLaunchKernelGGL(k_emit, grid, dim3(kEmitThreads), use_lds ? T * sizeof(int) : 0, s, (const Splat*)rec,
-                     (const uint2*)rect, N, tw, th, order, use_lds, cursor, keys);
+                     (const uint2*)rect, isect_offset, N, tw, th, order, use_lds, cursor, keys, slot_of_k);
   GSR_LAUNCH_CHECK("k_emit");
   if (n_busy > 0) {
     int lds_keys = 1024;
     while (lds_keys < max_seg && lds_keys < kSortLdsKeys) lds_keys <<= 1;
     const size_t lds = lds_keys * sizeof(uint64_t) + (kSortWaves * 256 + 64) * sizeof(int);
-    hipLaunchKernelGGL(k_segsort, dim3(n_busy), dim3(kSortThreads), lds, s, keys, tmp,
-                       tile_offset, busy_tiles, (const uint2*)rect, isect_offset, tw, th, lds_keys, sorted_ids,
-                       isect_pos);
+    hipLaunchKernelGGL(k_segsort, dim3(n_busy), dim3(kSortThreads), lds, s, keys, tmpk, tmpp0, tmpp1, tile_offset,
+                       busy_tiles, lds_keys, sorted_ids, pos_of_slot);
     GSR_LAUNCH_CHECK("k_segsort");
   }
   return GSR_OK;

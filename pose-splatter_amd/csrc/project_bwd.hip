@@ -18,15 +18,19 @@ namespace gsr {
 
 constexpr int kBwdThreads = 256;
 
-__device__ __forceinline__ void gather_partials(const uint2 r, int T, int tw, int64_t ct_base, const int32_t* __restrict__ pos,
-                                                int off, const int32_t* __restrict__ tile_end,
+// Emission entry k = isect_offset[c*N+n] + j (j: row-major tile of the rect) → pre-sort slot
+// (slot_of_k, written by the emitter) → sorted position (pos_of_slot, written by the sort).
+__device__ __forceinline__ void gather_partials(const uint2 r, int T, int tw, int64_t ct_base,
+                                                const int32_t* __restrict__ slot_of_k,
+                                                const int32_t* __restrict__ pos_of_slot, int off,
+                                                const int32_t* __restrict__ tile_end,
                                                 const float* __restrict__ partial, float (&acc)[kPartial]) {
   const int x0 = r.x & 0xffff, x1 = r.x >> 16, y0 = r.y & 0xffff, y1 = r.y >> 16;
   const int w = x1 - x0;
   int jj = 0;
   for (int ty = y0; ty < y1; ++ty) {
     for (int tx = x0; tx < x0 + w; ++tx, ++jj) {
-      const int s = pos[off + jj];
+      const int s = pos_of_slot[slot_of_k[off + jj]];
       const int t = ty * tw + tx;
       if (s < tile_end[ct_base + t]) {
         const float* p = partial + (int64_t)s * kPartial;
@@ -42,7 +46,7 @@ __global__ __launch_bounds__(kBwdThreads) void k_project3d_bwd(
     const float* __restrict__ params, int64_t N, int64_t stride, const float* __restrict__ viewmats,
     const float* __restrict__ Ks, int C, int W, int H, float eps2d, int tw, int th, const uint2* __restrict__ rect,
     const int32_t* __restrict__ isect_offset, const int32_t* __restrict__ isect_count,
-    const int32_t* __restrict__ pos, const int32_t* __restrict__ tile_end, const float* __restrict__ partial,
+    const int32_t* __restrict__ slot_of_k, const int32_t* __restrict__ pos_of_slot, const int32_t* __restrict__ tile_end, const float* __restrict__ partial,
     float* __restrict__ v_params) {
   const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
@@ -64,7 +68,8 @@ __global__ __launch_bounds__(kBwdThreads) void k_project3d_bwd(
     float acc[kPartial];
 #pragma unroll
     for (int v = 0; v < kPartial; ++v) acc[v] = 0.f;
-    gather_partials(rect[cn], T, tw, (int64_t)c * T, pos, isect_offset[cn], tile_end, partial, acc);
+    gather_partials(rect[cn], T, tw, (int64_t)c * T, slot_of_k, pos_of_slot, isect_offset[cn], tile_end, partial,
+                    acc);
     const Cam cam = load_cam(viewmats + c * 16, Ks + c * 9);
     // recompute the forward geometry (not culled: it has intersections)
     geo3d(a, cam, W, H, 0.f, 3.4e38f, eps2d, g);
@@ -202,7 +207,7 @@ __global__ __launch_bounds__(kBwdThreads) void k_project3d_bwd(
 __global__ __launch_bounds__(kBwdThreads) void k_project2d_bwd(
     const float* __restrict__ params, int64_t N, int64_t stride, int tw, int th, const uint2* __restrict__ rect,
     const int32_t* __restrict__ isect_offset, const int32_t* __restrict__ isect_count,
-    const int32_t* __restrict__ pos, const int32_t* __restrict__ tile_end, const float* __restrict__ partial,
+    const int32_t* __restrict__ slot_of_k, const int32_t* __restrict__ pos_of_slot, const int32_t* __restrict__ tile_end, const float* __restrict__ partial,
     float* __restrict__ v_params) {
   const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
@@ -215,7 +220,7 @@ __global__ __launch_bounds__(kBwdThreads) void k_project2d_bwd(
   float acc[kPartial];
 #pragma unroll
   for (int v = 0; v < kPartial; ++v) acc[v] = 0.f;
-  gather_partials(rect[n], tw * th, tw, 0, pos, isect_offset[n], tile_end, partial, acc);
+  gather_partials(rect[n], tw * th, tw, 0, slot_of_k, pos_of_slot, isect_offset[n], tile_end, partial, acc);
   const Geo2D g = geo2d(params + n * stride);
   const float va = acc[2], vb = acc[3], vc = acc[4];
   const float C = g.cs, S = g.sn;
@@ -245,29 +250,29 @@ extern "C" {
 
 int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride, const float* viewmats, const float* Ks,
                       int C, int width, int height, float eps2d, const uint32_t* rect, const int32_t* isect_offset,
-                      const int32_t* isect_count, const int32_t* isect_pos, const int32_t* tile_end,
-                      const float* partial, float* v_params, void* stream) {
+                      const int32_t* isect_count, const int32_t* slot_of_k, const int32_t* pos_of_slot,
+                      const int32_t* tile_end, const float* partial, float* v_params, void* stream) {
   GSR_REQUIRE(N >= 0 && C >= 1 && width > 0 && height > 0, "gsr3d_project_bwd: bad arguments");
   GSR_REQUIRE(row_stride >= 14, "gsr3d_project_bwd: row_stride < 14");
   if (N == 0) return GSR_OK;
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   hipLaunchKernelGGL(k_project3d_bwd, dim3(ceil_div(N, kBwdThreads)), dim3(kBwdThreads), 0, (hipStream_t)stream,
                      params, N, row_stride, viewmats, Ks, C, width, height, eps2d, tw, th, (const uint2*)rect,
-                     isect_offset, isect_count, isect_pos, tile_end, partial, v_params);
+                     isect_offset, isect_count, slot_of_k, pos_of_slot, tile_end, partial, v_params);
   GSR_LAUNCH_CHECK("k_project3d_bwd");
   return GSR_OK;
 }
 
 int gsr2d_project_bwd(const float* params, int64_t N, int64_t row_stride, int width, int height,
                       const uint32_t* rect, const int32_t* isect_offset, const int32_t* isect_count,
-                      const int32_t* isect_pos, const int32_t* tile_end, const float* partial, float* v_params,
-                      void* stream) {
+                      const int32_t* slot_of_k, const int32_t* pos_of_slot, const int32_t* tile_end,
+                      const float* partial, float* v_params, void* stream) {
   GSR_REQUIRE(N >= 0 && width > 0 && height > 0, "gsr2d_project_bwd: bad arguments");
   GSR_REQUIRE(row_stride >= 9, "gsr2d_project_bwd: row_stride < 9");
   if (N == 0) return GSR_OK;
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   hipLaunchKernelGGL(k_project2d_bwd, dim3(ceil_div(N, kBwdThreads)), dim3(kBwdThreads), 0, (hipStream_t)stream,
-                     params, N, row_stride, tw, th, (const uint2*)rect, isect_offset, isect_count, isect_pos,
+                     params, N, row_stride, tw, th, (const uint2*)rect, isect_offset, isect_count, slot_of_k, pos_of_slot,
                      tile_end, partial, v_params);
   GSR_LAUNCH_CHECK("k_project2d_bwd");
   return GSR_OK;

@@ -55,7 +55,7 @@ EXPORTS = {
     "gsr_bin_offsets": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _SZ, _P, _P, _P, _P, _P, _P]),
     "gsr_bin_sort_workspace": (_SZ, [_I64, _I64]),
     "gsr_bin_sort": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I32, _I64, _I32,
-                                    _I32, _P, _SZ, _P, _P, _P]),
+                                    _I32, _P, _SZ, _P, _P, _P, _P]),
     "gsr3d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P,
                                         _P, _P]),
     "gsr3d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P, _P, _P,
@@ -65,9 +65,9 @@ EXPORTS = {
     "gsr2d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P,
                                         _SZ, _P, _P]),
     "gsr3d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _I32, _I32, _I32, _F, _P, _P, _P,
-                                         _P, _P, _P, _P, _P]),
+                                         _P, _P, _P, _P, _P, _P]),
     "gsr2d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P, _P,
-                                         _P]),
+                                         _P, _P]),
 }
 
 _lock = threading.Lock()

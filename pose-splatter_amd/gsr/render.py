@@ -144,13 +144,14 @@ class _Bins:
         dev = self.rec.device
         I = self.n_isect
         self.sorted_ids = torch.empty(max(I, 1), device=dev, dtype=torch.int32)
-        self.pos = torch.empty(max(I, 1), device=dev, dtype=torch.int32)
+        self.slot_of_k = torch.empty(max(I, 1), device=dev, dtype=torch.int32)
+        self.pos_of_slot = torch.empty(max(I, 1), device=dev, dtype=torch.int32)
         ws = torch.empty(int(L.gsr_bin_sort_workspace(I, self.CT)), device=dev, dtype=torch.uint8)
         with _timed("bin_sort"):
           check(L.gsr_bin_sort(_ptr(self.rec), _ptr(self.rect), _ptr(self.isect_off), _ptr(self.tile_off),
                              _ptr(self.busy), self.C, self.N, self.W, self.H, order, I, self.max_seg,
-                             self.n_busy, _ptr(ws), ws.numel(), _ptr(self.sorted_ids), _ptr(self.pos),
-                             stream), "gsr_bin_sort")
+                             self.n_busy, _ptr(ws), ws.numel(), _ptr(self.sorted_ids), _ptr(self.slot_of_k),
+                             _ptr(self.pos_of_slot), stream), "gsr_bin_sort")
 
 
 def _record_stats(b: _Bins):
@@ -273,7 +274,7 @@ class _Render3D(torch.autograd.Function):
                   "gsr3d_raster_bwd")
             with _timed("project3d_bwd"):
               check(L.gsr3d_project_bwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height, opts.eps2d,
-                                      _ptr(b.rect), _ptr(b.isect_off), _ptr(b.cnt), _ptr(b.pos),
+                                      _ptr(b.rect), _ptr(b.isect_off), _ptr(b.cnt), _ptr(b.slot_of_k), _ptr(b.pos_of_slot),
                                       _ptr(b.tile_end), _ptr(partial), _ptr(v_params), stream),
                   "gsr3d_project_bwd")
         return v_params.view(ctx.params_shape), None, None, None, None, None, None
@@ -313,7 +314,7 @@ class _Render2D(torch.autograd.Function):
                   "gsr2d_raster_bwd")
             with _timed("project2d_bwd"):
               check(L.gsr2d_project_bwd(_ptr(p), N, stride, width, height, _ptr(b.rect), _ptr(b.isect_off),
-                                      _ptr(b.cnt), _ptr(b.pos), _ptr(b.tile_end), _ptr(partial),
+                                      _ptr(b.cnt), _ptr(b.slot_of_k), _ptr(b.pos_of_slot), _ptr(b.tile_end), _ptr(partial),
                                       _ptr(v_params), stream), "gsr2d_project_bwd")
         return v_params.view(ctx.params_shape), None, None, None, None
 

@@ -144,11 +144,23 @@ def test_3d_binning_exact(cuda):
     exp_off = torch.zeros(C * T + 1, dtype=torch.int64)
     exp_off[1:] = torch.cumsum(torch.bincount(exp_tiles, minlength=C * T), 0)
     assert torch.equal(b.tile_off.cpu().to(torch.int64), exp_off)
-    # inverse map: pos[off[cn] + j] = sorted position
-    pos = b.pos.cpu()[:I].to(torch.int64)
-    off = b.isect_off.cpu().to(torch.int64)
+    # inverse map: emission entry k → pre-sort slot → sorted position (both permutations)
+    sk = b.slot_of_k.cpu()[:I].to(torch.int64)
+    ps = b.pos_of_slot.cpu()[:I].to(torch.int64)
+    assert torch.equal(torch.sort(sk).values, torch.arange(I))
+    assert torch.equal(torch.sort(ps).values, torch.arange(I))
+    pos = ps[sk]
     ids = b.sorted_ids.cpu()[:I].to(torch.int64)
     assert torch.equal(ids[pos], torch.repeat_interleave(torch.arange(C * N), cnt))
+    # entry j of a Gaussian's rect lands in that (camera, tile)'s bucket (row-major j)
+    tiles_of_pos = torch.searchsorted(exp_off, pos, right=True) - 1
+    exp_k_tiles = []
+    for cn in torch.nonzero(cnt > 0).flatten().tolist():
+        c = cn // N
+        for ty in range(int(y0[cn]), int(y1[cn])):
+            for tx in range(int(x0[cn]), int(x1[cn])):
+                exp_k_tiles.append(c * T + ty * tw + tx)
+    assert torch.equal(tiles_of_pos, torch.tensor(exp_k_tiles, dtype=torch.int64))
     # projection rects vs the oracle's (float decisions: near-total agreement)
     o = _oracle3d()
     m, q, s, col, op = o.activations3d(p)
