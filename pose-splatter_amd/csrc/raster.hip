@@ -320,12 +320,15 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
     const int32_t* __restrict__ chunk_tile, const float4* __restrict__ ckpt, int W, int H, int tw, int th,
     const float* __restrict__ bg, const float* __restrict__ final_T, const int32_t* __restrict__ last_in,
     const float* __restrict__ v_rgb, const float* __restrict__ v_alpha, float* __restrict__ partial) {
-  __shared__ float4 s_p0[kRasterThreads];
-  __shared__ float4 s_p1[kRasterThreads];
-  __shared__ float4 s_p2[kRasterThreads];
+  // slot kNull: a zero-opacity record (never valid) that pads survivor groups to 7
+  constexpr int kNull = kChunk3;
+  constexpr int kGroup = 7;
+  __shared__ float4 s_p0[kChunk3 + 1];
+  __shared__ float4 s_p1[kChunk3 + 1];
+  __shared__ float4 s_p2[kChunk3 + 1];
   __shared__ PartialLds L;
   __shared__ unsigned long long s_m[4][4];
-  __shared__ short s_list[4][kRasterThreads];
+  __shared__ short s_list[4][kChunk3 + kGroup];
   const int ct = chunk_tile[blockIdx.x];
   const int cbase = chunk_base[ct];
   const int kc = blockIdx.x - cbase;
@@ -373,6 +376,12 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
     s_p1[threadIdx.x] = sp.p1;
     s_p2[threadIdx.x] = sp.p2;
   }
+  if (threadIdx.x == 0) {
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    s_p0[kNull] = z;
+    s_p1[kNull] = z;
+    s_p2[kNull] = z;
+  }
   __syncthreads();
   // cull the chunk against this wave's sub-tile; survivors are listed back to front
   int nsurv = 0;
@@ -389,52 +398,47 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
     }
     nsurv += __popcll(mk);
   }
+  if (st.lane < kGroup) s_list[wv][nsurv + st.lane] = (short)kNull;
   __builtin_amdgcn_wave_barrier();
-  for (int g0 = 0; g0 < nsurv; g0 += 7) {
+  // Branch-free groups of 7 survivors: an invalid (entry, pixel) pair contributes zeros and
+  // leaves T and S unchanged (ra = 1, fac = 0), so every group is straight-line code.
+  for (int g0 = 0; g0 < nsurv; g0 += kGroup) {
     float acc[64];
+    acc[63] = 0.f;
 #pragma unroll
-    for (int v = 0; v < 64; ++v) acc[v] = 0.f;
-#pragma unroll
-    for (int g = 0; g < 7; ++g) {
-      if (g0 + g < nsurv) {
-        const int k = s_list[wv][g0 + g];
-        const int ek = b0 + k;
-        const float4 p0 = s_p0[k];
-        const float4 p1 = s_p1[k];
-        const float4 p2 = s_p2[k];
-        const float dx = p0.x - st.px, dy = p0.y - st.py;
-        const float sigma = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
-        const float vis = __expf(-sigma);
-        const float raw = p0.z * vis;
-        const float alpha = fminf(kAlphaMax, raw);
-        const bool valid = ek <= last && !(sigma < 0.f || alpha < kAlphaThreshold);
-        if (valid) {
-          const float ra = __builtin_amdgcn_rcpf(1.f - alpha);
-          T *= ra;
-          const float fac = alpha * T;
-          acc[g * kPartial + 6] = fac * vr;
-          acc[g * kPartial + 7] = fac * vg;
-          acc[g * kPartial + 8] = fac * vb;
-          const float v_al = (p2.x * T - Sr * ra) * vr + (p2.y * T - Sg * ra) * vg +
-                             (p2.z * T - Sb * ra) * vb + vTa * ra;
-          if (raw <= kAlphaMax) {
-            const float v_sig = -raw * v_al;
-            acc[g * kPartial + 2] = v_sig * dx * dx;
-            acc[g * kPartial + 3] = v_sig * dx * dy;
-            acc[g * kPartial + 4] = v_sig * dy * dy;
-            acc[g * kPartial + 0] = v_sig * (2.f * p1.x * dx + p1.y * dy);
-            acc[g * kPartial + 1] = v_sig * (p1.y * dx + 2.f * p1.z * dy);
-            acc[g * kPartial + 5] = vis * v_al;
-          }
-          Sr += p2.x * fac;
-          Sg += p2.y * fac;
-          Sb += p2.z * fac;
-        }
-      }
+    for (int g = 0; g < kGroup; ++g) {
+      const int k = s_list[wv][g0 + g];
+      const float4 p0 = s_p0[k];
+      const float4 p1 = s_p1[k];
+      const float4 p2 = s_p2[k];
+      const float dx = p0.x - st.px, dy = p0.y - st.py;
+      const float sigma = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
+      const float vis = __expf(-sigma);
+      const float raw = p0.z * vis;
+      const float alpha = fminf(kAlphaMax, raw);
+      const bool valid = (b0 + k) <= last && sigma >= 0.f && alpha >= kAlphaThreshold;
+      const float ra = valid ? __builtin_amdgcn_rcpf(1.f - alpha) : 1.f;
+      T *= ra;
+      const float fac = valid ? alpha * T : 0.f;
+      acc[g * kPartial + 6] = fac * vr;
+      acc[g * kPartial + 7] = fac * vg;
+      acc[g * kPartial + 8] = fac * vb;
+      const float v_al = (p2.x * T - Sr * ra) * vr + (p2.y * T - Sg * ra) * vg + (p2.z * T - Sb * ra) * vb + vTa * ra;
+      const bool unclamped = valid && raw <= kAlphaMax;
+      const float v_sig = unclamped ? -raw * v_al : 0.f;
+      acc[g * kPartial + 2] = v_sig * dx * dx;
+      acc[g * kPartial + 3] = v_sig * dx * dy;
+      acc[g * kPartial + 4] = v_sig * dy * dy;
+      acc[g * kPartial + 0] = v_sig * (2.f * p1.x * dx + p1.y * dy);
+      acc[g * kPartial + 1] = v_sig * (p1.y * dx + 2.f * p1.z * dy);
+      acc[g * kPartial + 5] = unclamped ? vis * v_al : 0.f;
+      Sr += p2.x * fac;
+      Sg += p2.y * fac;
+      Sb += p2.z * fac;
     }
     const float sum = reduce64(acc);
     const int g = st.lane / kPartial;
-    if (g < 7 && g0 + g < nsurv) L.w[st.lane - g * kPartial][wv][s_list[wv][g0 + g]] = sum;
+    if (g < kGroup && g0 + g < nsurv) L.w[st.lane - g * kPartial][wv][s_list[wv][g0 + g]] = sum;
   }
   __syncthreads();
   if (threadIdx.x < n) {
