@@ -25,7 +25,7 @@
  *     memory.  The library allocates nothing and frees nothing.  Inputs are read-only.
  *   - Every call enqueues on the caller's stream (a hipStream_t passed as void*); no call
  *     synchronises the device.  The only host read the caller needs is gsr_bin_stats
- *     (filled on the device by gsr_bin_offsets, 16 bytes) to size the intersection buffers.
+ *     (filled on the device by gsr_bin_offsets; the first 24 bytes) to size the intersection buffers.
  *   - Return 0 on success; negative on failure (GSR_E*).  gsr_last_error() returns a
  *     thread-local message for the last failure of the calling thread.  No C++ exception
  *     crosses the ABI.
@@ -71,8 +71,9 @@ typedef struct gsr_bin_stats {
   int32_t max_seg;     /* longest per-tile list                                       */
   int32_t n_busy;      /* tiles with a non-empty list                                 */
   int32_t n_chunks;    /* sum over tiles of ceil(list length / GSR_CHUNK)              */
-  int32_t reserved;
-} gsr_bin_stats;
+  int32_t n_active;    /* chunks the 3D backward visits (appended by gsr3d_raster_fwd)   */
+  int32_t reserved[2];
+} gsr_bin_stats;       /* 32 bytes; counters zeroed by gsr_bin_offsets                  */
 
 int gsr_version(void);
 const char* gsr_last_error(void);
@@ -133,26 +134,31 @@ int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_of
 
 /* ---------------------------------------------------------------- (c) rasterisation */
 
-/* Front-to-back compositing (gsplat classic), one workgroup per 16x16 tile, visited in
- * tile_order (the busy_tiles array of gsr_bin_offsets: all C*tiles entries).  bg [C,3].
+/* Front-to-back compositing (gsplat classic).  One workgroup per non-empty 16x16 tile,
+ * visited in tile_order (the busy_tiles array of gsr_bin_offsets: non-empty tiles
+ * longest-first, then the empty ones); n_busy = stats.n_busy as read back by the host.
+ * Empty tiles get the background (written by extra fill workgroups).  bg [C,3].
  * Outputs rgb [C,H,W,3], alpha [C,H,W], final_T [C,H,W] (exact transmittance, kept for the
  * backward), last [C,H,W] (index of the last contributing sorted entry, -1 if none),
  * tile_end [CT] (1 + max last over the tile, or the tile's start), and for the
- * chunk-parallel backward: chunk_state [n_chunks*256*4] ({T at the chunk's start, the
- * chunk's own rgb sum} per pixel of the tile, for every GSR_CHUNK-entry chunk a pixel
- * reached) and chunk_tile [n_chunks] (owning tile of each chunk). */
+ * chunk-parallel backward: chunk_state [n_chunks*256*4] ({T at the chunk's end, the rgb
+ * sum of all later chunks} per pixel of the tile, for every GSR_CHUNK-entry chunk the tile's
+ * walk reached), chunk_tile [n_chunks] (owning tile of each chunk) and chunk_list
+ * [n_chunks] (the chunks before each tile's tile_end, in no particular order; their count
+ * is added to stats->n_active).  stats: the device gsr_bin_stats of gsr_bin_offsets. */
 int gsr3d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_order, const int32_t* chunk_base, int C, int width,
-                     int height, const float* bg, float* rgb, float* alpha, float* final_T,
-                     int32_t* last, int32_t* tile_end, float* chunk_state, int32_t* chunk_tile,
-                     void* stream);
+                     int height, const float* bg, int32_t n_busy, gsr_bin_stats* stats,
+                     float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
+                     float* chunk_state, int32_t* chunk_tile, int32_t* chunk_list, void* stream);
 
-/* Backward of gsr3d_raster_fwd, one workgroup per (tile, chunk).  v_rgb [C,H,W,3],
- * v_alpha [C,H,W] (contiguous).  Writes partial [I*9] for every sorted entry s in
- * [tile start, tile_end). */
+/* Backward of gsr3d_raster_fwd: workgroup b takes chunk_list[b] for b < stats->n_active
+ * (n_chunks bounds the grid).  v_rgb [C,H,W,3], v_alpha [C,H,W] (contiguous).  Writes
+ * partial [I*9] for every sorted entry s in [tile start, tile_end). */
 int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_end, const int32_t* chunk_base,
-                     const int32_t* chunk_tile, const float* chunk_state, int32_t n_chunks,
+                     const int32_t* chunk_tile, const float* chunk_state,
+                     const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
                      int C, int width, int height, const float* bg, const float* final_T,
                      const int32_t* last, const float* v_rgb, const float* v_alpha,
                      float* partial, void* stream);

@@ -135,7 +135,9 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(const int32_t* __rest
     stats->max_seg = s_max;
     stats->n_busy = n_busy;
     stats->n_chunks = tk;
-    stats->reserved = 0;
+    stats->n_active = 0;
+    stats->reserved[0] = 0;
+    stats->reserved[1] = 0;
   }
 }
 

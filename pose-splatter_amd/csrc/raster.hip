@@ -14,8 +14,22 @@
 
 namespace gsr {
 
+#ifdef GSR_EXP_COUNT
+// work counters for timing analysis builds only (tools/count_work.py)
+__device__ unsigned long long g_cnt[16];
+#define GSR_CNT_ADD(i, v) atomicAdd(&g_cnt[i], (unsigned long long)(v))
+#define GSR_CNT_MAX(i, v) atomicMax(&g_cnt[i], (unsigned long long)(v))
+#define GSR_CLOCK() clock64()
+#else
+#define GSR_CNT_ADD(i, v)
+#define GSR_CNT_MAX(i, v)
+#define GSR_CLOCK() 0ll
+#endif
+
 constexpr int kRasterThreads = 256;
 constexpr int kChunk3 = GSR_CHUNK;   // backward work unit: list entries per chunk
+constexpr int kFillBlocks = 1024;    // workgroups that fill the empty tiles
+
 
 __device__ __forceinline__ void tile_coords(int ct, int tw, int th, int& c, int& ty, int& tx) {
   const int T = tw * th;
@@ -73,6 +87,33 @@ __device__ __forceinline__ SubTile sub_tile(int ct, int tw, int th, int W, int H
   return t;
 }
 
+// ---------------------------------------------------------------- empty tiles
+// Tiles with an empty list only need the background.  The forward launches them as extra
+// workgroups (blockIdx >= n_busy) that stride over order[n_busy..CT): cheap stores that
+// run beside the busy tiles instead of one short-lived workgroup per empty tile.
+template <bool IS2D>
+__device__ void fill_empty(const int32_t* __restrict__ order, const int32_t* __restrict__ tile_offset, int n_busy,
+                           int64_t CT, int W, int H, int tw, int th, const float* __restrict__ bg,
+                           float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
+                           int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end) {
+  const int G = gridDim.x - n_busy;
+  for (int64_t t = n_busy + (blockIdx.x - n_busy); t < CT; t += G) {
+    const int ct = order[t];
+    const SubTile st = sub_tile<IS2D>(ct, tw, th, W, H);
+    if (st.inside) {
+      const int64_t pix = ((int64_t)st.c * H + st.i) * W + st.j;
+      const float* bgc = bg + st.c * 3;
+      out_rgb[pix * 3 + 0] = bgc[0];
+      out_rgb[pix * 3 + 1] = bgc[1];
+      out_rgb[pix * 3 + 2] = bgc[2];
+      out_alpha[pix] = 0.f;
+      if (!IS2D) out_T[pix] = 1.f;
+      out_last[pix] = -1;
+    }
+    if (threadIdx.x == 0) tile_end[ct] = tile_offset[ct];
+  }
+}
+
 // ---------------------------------------------------------------- 3D / 2D forward
 // Waves run independently (no workgroup barrier in the loop): each wave gathers the next 64
 // list entries (prefetched one batch ahead), culls them against its sub-tile, compacts the
@@ -86,11 +127,17 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     const int32_t* __restrict__ order, int W, int H, int tw, int th, float cut, const float* __restrict__ bg,
     float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
     int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end, float4* __restrict__ ckpt,
-    const int32_t* __restrict__ chunk_base, int32_t* __restrict__ chunk_tile) {
+    const int32_t* __restrict__ chunk_base, int32_t* __restrict__ chunk_tile, int n_busy, int64_t CT,
+    gsr_bin_stats* __restrict__ stats, int32_t* __restrict__ chunk_list) {
   __shared__ float4 s_p0[4][64];
   __shared__ float4 s_p1[4][64];
   __shared__ float4 s_p2[4][64];
-  __shared__ int s_max;
+  __shared__ int s_max, s_pos, s_nact;
+  if ((int)blockIdx.x >= n_busy) {
+    fill_empty<IS2D>(order, tile_offset, n_busy, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T, out_last,
+                     tile_end);
+    return;
+  }
   const int ct = order[blockIdx.x];
   const SubTile st = sub_tile<IS2D>(ct, tw, th, W, H);
   const int wv = st.wv;
@@ -111,15 +158,34 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     const int nchunk = (end - start + kChunk3 - 1) / kChunk3;
     for (int k = threadIdx.x; k < nchunk; k += blockDim.x) chunk_tile[cbase + k] = ct;
   }
-  int e = start + st.lane;
-  float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0;
-  bool have = e < end;
-  if (have) {
-    const Splat s = rec[ids[e]];
-    n0 = s.p0; n1 = s.p1; n2 = s.p2;
+  // Software pipeline over 64-entry batches: while batch b is culled and composited, the
+  // records of b+1 and b+2 and the list ids of b+3 are in flight.  Two record buffers (X, Y)
+  // and two id registers alternate roles in a 2-way unrolled loop, so no loaded value is
+  // ever copied (a copy would wait for its load).  Loads are unconditional (index clamped to
+  // the list's last entry, validity from the position) and each step issues the ids of b+3
+  // BEFORE the records of b+2, so waiting for an id never waits for younger record loads.
+  const int e_last = max(end - 1, start);
+  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 x0 = zero4, x1 = zero4, x2 = zero4, y0 = zero4, y1 = zero4, y2 = zero4;
+  int idp = 0, idq = 0;
+  if (end > start) {
+    const int ida = ids[min(start + st.lane, e_last)];
+    const int idb = ids[min(start + 64 + st.lane, e_last)];
+    const Splat sa = rec[ida];
+    idp = ids[min(start + 128 + st.lane, e_last)];
+    const Splat sb = rec[idb];
+    x0 = sa.p0; x1 = sa.p1; x2 = sa.p2;
+    y0 = sb.p0; y1 = sb.p1; y2 = sb.p2;
   }
-  for (int b0 = start; b0 < end; b0 += 64) {
-    if (__ballot(!done) == 0ull) break;
+  [[maybe_unused]] int cnt_b = 0, cnt_s = 0;
+  [[maybe_unused]] long long clk_cull = 0, clk_comp = 0;
+  [[maybe_unused]] const long long clk_start = GSR_CLOCK();
+  // one batch: cull + compact c (batch b0), refill c with batch b0+128 (id_use), load the
+  // ids of batch b0+192 into id_new, composite.  false = every pixel of the wave is done.
+  auto step = [&](int b0, float4& c0, float4& c1, float4& c2, int id_use, int& id_new) -> bool {
+    if (__ballot(!done) == 0ull) return false;
+    [[maybe_unused]] const long long t0 = GSR_CLOCK();
+    ++cnt_b;
     if (!IS2D && b0 > start && ((b0 - start) % kChunk3) == 0) {   // entering chunk kcur+1
       ckpt[(int64_t)(cbase + kcur) * kRasterThreads + threadIdx.x] = make_float4(Ts, dr, dg, db);
       cr += dr;
@@ -129,23 +195,21 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
       Ts = T;
       ++kcur;
     }
-    const bool keep = have && cull_keep<IS2D>(n0, n1, st.bx0, st.bx1, st.by0, st.by1, cut);
+    const bool keep = (b0 + st.lane < end) && cull_keep<IS2D>(c0, c1, st.bx0, st.bx1, st.by0, st.by1, cut);
     const unsigned long long m = __ballot(keep);
     const int n = __popcll(m);
+    cnt_s += n;
     if (keep) {
       const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-      s_p0[wv][slot] = n0;
-      s_p1[wv][slot] = make_float4(n1.x, n1.y, n1.z, __int_as_float(b0 + st.lane));
-      s_p2[wv][slot] = n2;
+      s_p0[wv][slot] = c0;
+      s_p1[wv][slot] = make_float4(c1.x, c1.y, c1.z, __int_as_float(b0 + st.lane));
+      s_p2[wv][slot] = c2;
     }
-    // prefetch the next batch while this one is composited
-    e = b0 + 64 + st.lane;
-    have = e < end;
-    if (have) {
-      const Splat s = rec[ids[e]];
-      n0 = s.p0; n1 = s.p1; n2 = s.p2;
-    }
+    id_new = ids[min(b0 + 192 + st.lane, e_last)];
+    const Splat sc = rec[id_use];
+    c0 = sc.p0; c1 = sc.p1; c2 = sc.p2;
     __builtin_amdgcn_wave_barrier();
+    [[maybe_unused]] const long long t1 = GSR_CLOCK();
 #pragma unroll 4
     for (int k = 0; k < n; ++k) {
       const float4 p0 = s_p0[wv][k];
@@ -178,12 +242,49 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
       }
     }
     __builtin_amdgcn_wave_barrier();
+    [[maybe_unused]] const long long t2 = GSR_CLOCK();
+    clk_cull += t1 - t0;
+    clk_comp += t2 - t1;
+    return true;
+  };
+  for (int b0 = start; b0 < end; b0 += 128) {
+    if (!step(b0, x0, x1, x2, idp, idq)) break;
+    if (b0 + 64 >= end || !step(b0 + 64, y0, y1, y2, idq, idp)) break;
+  }
+  if (st.lane == 0) {
+    GSR_CNT_ADD(0, cnt_b);
+    GSR_CNT_MAX(1, cnt_b);
+    GSR_CNT_ADD(2, cnt_s);
+    GSR_CNT_ADD(3, clk_cull);
+    GSR_CNT_ADD(4, clk_comp);
+    GSR_CNT_ADD(5, GSR_CLOCK() - clk_start);
+    GSR_CNT_MAX(6, GSR_CLOCK() - clk_start);
   }
   if (!IS2D && end > start) {
-    ckpt[(int64_t)(cbase + kcur) * kRasterThreads + threadIdx.x] = make_float4(Ts, dr, dg, db);
     cr += dr;
     cg += dg;
     cb += db;
+    // Turn this pixel's chunk records {T at chunk start, chunk colour sum} into what the
+    // backward needs at each chunk's END: {T_end, suffix colour sum of the later chunks}
+    // (positive terms, summed back to front).  Records are re-read 8 at a time.
+    float4* ck = ckpt + (int64_t)cbase * kRasterThreads + threadIdx.x;
+    ck[(int64_t)kcur * kRasterThreads] = make_float4(T, 0.f, 0.f, 0.f);
+    float Tn = Ts, sr = dr, sg = dg, sb = db;
+    for (int k0 = kcur - 1; k0 >= 0; k0 -= 8) {
+      float4 r[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k0 - u >= 0) r[u] = ck[(int64_t)(k0 - u) * kRasterThreads];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k0 - u >= 0) {
+          ck[(int64_t)(k0 - u) * kRasterThreads] = make_float4(Tn, sr, sg, sb);
+          Tn = r[u].x;
+          sr += r[u].y;
+          sg += r[u].z;
+          sb += r[u].w;
+        }
+    }
   }
   if (st.inside) {
     const int64_t pix = ((int64_t)st.c * H + st.i) * W + st.j;
@@ -198,7 +299,16 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   }
   if (last >= 0) atomicMax(&s_max, last);
   __syncthreads();
-  if (threadIdx.x == 0) tile_end[ct] = s_max >= 0 ? s_max + 1 : start;
+  if (threadIdx.x == 0) {
+    const int te = s_max >= 0 ? s_max + 1 : start;
+    tile_end[ct] = te;
+    // 3D: register the chunks before tile_end with the backward's work list
+    const int nact = IS2D ? 0 : (te - start + kChunk3 - 1) / kChunk3;
+    s_nact = nact;
+    s_pos = nact > 0 ? atomicAdd(&stats->n_active, nact) : 0;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < s_nact; k += blockDim.x) chunk_list[s_pos + k] = cbase + k;
 }
 
 // ---------------------------------------------------------------- 2D forward
@@ -303,11 +413,11 @@ __device__ __forceinline__ void block_store_partials(const PartialLds& L, int b0
 }
 
 // ---------------------------------------------------------------- 3D backward
-// Chunk-parallel: one workgroup per (tile, GSR_CHUNK-entry chunk of its list), so no pixel's
-// back-to-front walk is longer than one chunk.  The forward's chunk records give each
-// pixel's state at the chunk's END exactly: T_end = T at the start of the next chunk (or
-// the exact final T for the pixel's last chunk), and the suffix colour sum S_end = sum of the
-// later chunks' own colour sums (positive terms, no cancellation).  Inside the chunk:
+// Chunk-parallel: one workgroup per (tile, GSR_CHUNK-entry chunk of its list), so no
+// pixel's back-to-front walk is longer than one chunk.  Workgroup b takes entry b of the
+// forward's chunk list (only chunks before their tile's tile_end).  The forward's chunk records give each pixel's state at the chunk's END exactly:
+// T_end (the T the forward had there) and the suffix colour sum S_end = sum of the later
+// chunks' own colour sums (positive terms, no cancellation).  Inside the chunk:
 //   T_i recovered as T_{i+1}/(1-a_i) with v_rcp (a <= 0.999);
 //   d rgb/d c_i = a_i T_i;  d rgb/d a_i = c_i T_i - (S_i + T_f bg)/(1-a_i);  d alpha/d a_i = T_f/(1-a_i)
 //   a = o e^{-sigma} (unclamped only):  d/do = e^{-sigma},  d/dsigma = -a.
@@ -319,24 +429,29 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
     const int32_t* __restrict__ tile_end, const int32_t* __restrict__ chunk_base,
     const int32_t* __restrict__ chunk_tile, const float4* __restrict__ ckpt, int W, int H, int tw, int th,
     const float* __restrict__ bg, const float* __restrict__ final_T, const int32_t* __restrict__ last_in,
-    const float* __restrict__ v_rgb, const float* __restrict__ v_alpha, float* __restrict__ partial) {
+    const float* __restrict__ v_rgb, const float* __restrict__ v_alpha, float* __restrict__ partial,
+    const int32_t* __restrict__ chunk_list, gsr_bin_stats* __restrict__ stats) {
   // slot kNull: a zero-opacity record (never valid) that pads survivor groups to 7
   constexpr int kNull = kChunk3;
   constexpr int kGroup = 7;
   __shared__ float4 s_p0[kChunk3 + 1];
   __shared__ float4 s_p1[kChunk3 + 1];
   __shared__ float4 s_p2[kChunk3 + 1];
-  __shared__ PartialLds L;
-  __shared__ unsigned long long s_m[4][4];
+  // gradient sums per entry: waves {0,1} add into pair slot 0, waves {2,3} into slot 1.  Two
+  // float adds onto 0 commute exactly, so the LDS atomics keep the result deterministic.
+  __shared__ float L[kPartial][2][kChunk3];
   __shared__ short s_list[4][kChunk3 + kGroup];
-  const int ct = chunk_tile[blockIdx.x];
+  // one workgroup per grid slot; slots past the forward's active-chunk count exit at once
+  if ((int)blockIdx.x >= stats->n_active) return;
+  [[maybe_unused]] const long long clk_start = GSR_CLOCK();
+  const int chunk = chunk_list[blockIdx.x];
+  const int ct = chunk_tile[chunk];
   const int cbase = chunk_base[ct];
-  const int kc = blockIdx.x - cbase;
+  const int kc = chunk - cbase;
   const int start = tile_offset[ct];
   const int eff = tile_end[ct];
   const int b0 = start + kc * kChunk3;
-  if (b0 >= eff) return;   // nothing past the tile's last contributing entry needs a partial
-  const int n = min(kChunk3, eff - b0);
+  const int n = min(kChunk3, eff - b0);   // >= 1: the list holds chunks before tile_end only
   const SubTile st = sub_tile<false>(ct, tw, th, W, H);
   const int wv = st.wv;
   float Tf = 1.f, vr = 0.f, vg = 0.f, vb = 0.f, va = 0.f;
@@ -352,17 +467,14 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
       va = v_alpha[pix];
     }
   }
-  // state at the end of this chunk
+  // state at the end of this chunk: {T_end, suffix colour sum} (forward epilogue)
   float T = Tf, Sr = 0.f, Sg = 0.f, Sb = 0.f;
   if (last >= b0) {
-    const int kl = (last - start) / kChunk3;
-    for (int j = kc + 1; j <= kl; ++j) {
-      const float4 r = ckpt[(int64_t)(cbase + j) * kRasterThreads + threadIdx.x];
-      if (j == kc + 1) T = r.x;
-      Sr += r.y;
-      Sg += r.z;
-      Sb += r.w;
-    }
+    const float4 r = ckpt[(int64_t)(cbase + kc) * kRasterThreads + threadIdx.x];
+    T = r.x;
+    Sr = r.y;
+    Sg = r.z;
+    Sb = r.w;
   }
   const float* bgc = bg + st.c * 3;
   const float bgdot = bgc[0] * vr + bgc[1] * vg + bgc[2] * vb;
@@ -376,6 +488,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
     s_p1[threadIdx.x] = sp.p1;
     s_p2[threadIdx.x] = sp.p2;
   }
+  for (int i = threadIdx.x; i < kPartial * 2 * kChunk3; i += kRasterThreads) (&L[0][0][0])[i] = 0.f;
   if (threadIdx.x == 0) {
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
     s_p0[kNull] = z;
@@ -391,12 +504,18 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
     const bool keep = k < n && (b0 + k) <= wlast &&
                       cull_keep<false>(s_p0[k], s_p1[k], st.bx0, st.bx1, st.by0, st.by1, 0.f);
     const unsigned long long mk = __ballot(keep);
-    if (st.lane == 0) s_m[wv][q] = mk;
     if (keep) {
       const unsigned long long above = st.lane == 63 ? 0ull : (mk >> (st.lane + 1));
       s_list[wv][nsurv + __popcll(above)] = (short)k;
     }
     nsurv += __popcll(mk);
+  }
+  [[maybe_unused]] const long long clk_loop = GSR_CLOCK();
+  if (st.lane == 0) {
+    GSR_CNT_ADD(8, nsurv);
+    GSR_CNT_ADD(9, (nsurv + 6) / 7);
+    GSR_CNT_ADD(10, clk_loop - clk_start);
+    if (wv == 0) GSR_CNT_ADD(13, 1);
   }
   if (st.lane < kGroup) s_list[wv][nsurv + st.lane] = (short)kNull;
   __builtin_amdgcn_wave_barrier();
@@ -438,26 +557,22 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
     }
     const float sum = reduce64(acc);
     const int g = st.lane / kPartial;
-    if (g < kGroup && g0 + g < nsurv) L.w[st.lane - g * kPartial][wv][s_list[wv][g0 + g]] = sum;
+    if (g < kGroup && g0 + g < nsurv)
+      __hip_atomic_fetch_add(&L[st.lane - g * kPartial][wv >> 1][s_list[wv][g0 + g]], sum, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
   }
+  [[maybe_unused]] const long long clk_loop_end = GSR_CLOCK();
   __syncthreads();
+  if (st.lane == 0) {
+    GSR_CNT_ADD(11, clk_loop_end - clk_loop);
+    GSR_CNT_ADD(12, GSR_CLOCK() - clk_loop_end);
+    GSR_CNT_MAX(14, GSR_CLOCK() - clk_start);
+  }
   if (threadIdx.x < n) {
     const int k = threadIdx.x;
-    const int q = k >> 6;
-    const unsigned long long bit = 1ull << (k & 63);
-    float acc[kPartial];
-#pragma unroll
-    for (int v = 0; v < kPartial; ++v) acc[v] = 0.f;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      if (s_m[w][q] & bit) {
-#pragma unroll
-        for (int v = 0; v < kPartial; ++v) acc[v] += L.w[v][w][k];
-      }
-    }
     float* dst = partial + (int64_t)(b0 + k) * kPartial;
 #pragma unroll
-    for (int v = 0; v < kPartial; ++v) dst[v] = acc[v];
+    for (int v = 0; v < kPartial; ++v) dst[v] = L[v][0][k] + L[v][1][k];
   }
 }
 
@@ -619,6 +734,18 @@ using namespace gsr;
 
 extern "C" {
 
+#ifdef GSR_EXP_COUNT
+int gsr_debug_counters(unsigned long long* out, int reset) {
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(gsr::g_cnt), sizeof(gsr::g_cnt));
+  if (reset) {
+    unsigned long long z[16] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(gsr::g_cnt), z, sizeof(z));
+  }
+  return 0;
+}
+#endif
+
 // Self-test of the transposed wave reduction: out[l] = sum over lanes of v_lane[l] for the
 // pattern v_lane[i] = ((lane*7 + i*13) % 97) + i/4 (checked on the host by tests/).
 int gsr_selftest_reduce64(float* out, void* stream) {
@@ -629,31 +756,37 @@ int gsr_selftest_reduce64(float* out, void* stream) {
 
 int gsr3d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_order, const int32_t* chunk_base, int C, int width, int height,
-                     const float* bg, float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
-                     float* chunk_state, int32_t* chunk_tile, void* stream) {
+                     const float* bg, int32_t n_busy, gsr_bin_stats* stats, float* rgb, float* alpha,
+                     float* final_T, int32_t* last, int32_t* tile_end, float* chunk_state, int32_t* chunk_tile,
+                     int32_t* chunk_list, void* stream) {
   GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "gsr3d_raster_fwd: bad C=%d or image %dx%d", C, width, height);
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   const int64_t CT = (int64_t)C * tw * th;
   GSR_REQUIRE(CT < (1ll << 31), "gsr3d_raster_fwd: too many tiles");
-  hipLaunchKernelGGL(k_raster_fwd<false>, dim3((unsigned)CT), dim3(kRasterThreads), 0, (hipStream_t)stream,
-                     (const Splat*)rec, sorted_ids, tile_offset, tile_order, width, height, tw, th, kAlphaThreshold,
-                     bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state, chunk_base, chunk_tile);
+  GSR_REQUIRE(n_busy >= 0 && n_busy <= CT, "gsr3d_raster_fwd: n_busy=%d out of [0, %lld]", n_busy, (long long)CT);
+  const int64_t n_fill = std::min<int64_t>(CT - n_busy, kFillBlocks);
+  hipLaunchKernelGGL(k_raster_fwd<false>, dim3((unsigned)(n_busy + n_fill)), dim3(kRasterThreads), 0,
+                     (hipStream_t)stream, (const Splat*)rec, sorted_ids, tile_offset, tile_order, width, height, tw,
+                     th, kAlphaThreshold, bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state, chunk_base,
+                     chunk_tile, (int)n_busy, CT, stats, chunk_list);
   GSR_LAUNCH_CHECK("k_raster_fwd<3d>");
   return GSR_OK;
 }
 
 int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_end, const int32_t* chunk_base, const int32_t* chunk_tile,
-                     const float* chunk_state, int32_t n_chunks, int C, int width, int height, const float* bg,
-                     const float* final_T, const int32_t* last, const float* v_rgb, const float* v_alpha,
-                     float* partial, void* stream) {
+                     const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
+                     int C, int width, int height, const float* bg, const float* final_T, const int32_t* last,
+                     const float* v_rgb, const float* v_alpha, float* partial, void* stream) {
   GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "gsr3d_raster_bwd: bad C=%d or image %dx%d", C, width, height);
   GSR_REQUIRE(n_chunks >= 0, "gsr3d_raster_bwd: bad n_chunks");
   if (n_chunks == 0) return GSR_OK;
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
+  // n_chunks bounds the forward's active-chunk count (stats->n_active, device-side)
   hipLaunchKernelGGL(k_raster3d_bwd, dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
                      (const Splat*)rec, sorted_ids, tile_offset, tile_end, chunk_base, chunk_tile,
-                     (const float4*)chunk_state, width, height, tw, th, bg, final_T, last, v_rgb, v_alpha, partial);
+                     (const float4*)chunk_state, width, height, tw, th, bg, final_T, last, v_rgb, v_alpha, partial,
+                     chunk_list, stats);
   GSR_LAUNCH_CHECK("k_raster3d_bwd");
   return GSR_OK;
 }

@@ -34,7 +34,8 @@ class GsrLibraryError(RuntimeError):
 
 class BinStats(ctypes.Structure):
     _fields_ = [("n_isect", ctypes.c_int64), ("max_seg", ctypes.c_int32), ("n_busy", ctypes.c_int32),
-                ("n_chunks", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("n_chunks", ctypes.c_int32), ("n_active", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 2)]
 
 
 _P = ctypes.c_void_p
@@ -56,10 +57,10 @@ EXPORTS = {
     "gsr_bin_sort_workspace": (_SZ, [_I64, _I64]),
     "gsr_bin_sort": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I32, _I64, _I32,
                                     _I32, _P, _SZ, _P, _P, _P, _P]),
-    "gsr3d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P,
-                                        _P, _P]),
-    "gsr3d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P, _P, _P,
-                                        _P, _P, _P, _P]),
+    "gsr3d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _I32, _P, _P, _P, _P,
+                                        _P, _P, _P, _P, _P, _P]),
+    "gsr3d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P,
+                                        _P, _P, _P, _P, _P, _P]),
     "gsr2d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "gsr2d_raster_bwd_workspace": (_SZ, [_I64, _I64]),
     "gsr2d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P,

@@ -116,7 +116,7 @@ class _Bins:
         self.tile_off = torch.empty(self.CT + 1, **i32)
         self.busy = torch.empty(self.CT, **i32)
         self.chunk_base = torch.empty(self.CT + 1, **i32)
-        self.stats_dev = torch.zeros(6, **i32)   # gsr_bin_stats (24 B)
+        self.stats_dev = torch.zeros(8, **i32)   # gsr_bin_stats (32 B)
         self.n_chunks = 0
         self.n_isect = 0
         self.max_seg = 0
@@ -198,10 +198,12 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
     b.tile_end = torch.empty(b.CT, device=dev, dtype=torch.int32)
     b.chunk_state = torch.empty(max(b.n_chunks, 1) * 256 * 4, device=dev, dtype=torch.float32)
     b.chunk_tile = torch.empty(max(b.n_chunks, 1), device=dev, dtype=torch.int32)
+    b.chunk_list = torch.empty(max(b.n_chunks, 1), device=dev, dtype=torch.int32)
     with _timed("raster3d_fwd"):
       check(L.gsr3d_raster_fwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), _ptr(b.busy), _ptr(b.chunk_base),
-                             C, width, height, _ptr(bgc), _ptr(rgb), _ptr(alpha), _ptr(b.final_T), _ptr(b.last),
-                             _ptr(b.tile_end), _ptr(b.chunk_state), _ptr(b.chunk_tile), stream), "gsr3d_raster_fwd")
+                             C, width, height, _ptr(bgc), b.n_busy, _ptr(b.stats_dev), _ptr(rgb), _ptr(alpha),
+                             _ptr(b.final_T), _ptr(b.last), _ptr(b.tile_end), _ptr(b.chunk_state),
+                             _ptr(b.chunk_tile), _ptr(b.chunk_list), stream), "gsr3d_raster_fwd")
     _record_stats(b)
     return rgb, alpha, b, (p, stride, V, Kc, bgc, width, height, opts)
 
@@ -268,7 +270,8 @@ class _Render3D(torch.autograd.Function):
             partial = torch.empty(max(b.n_isect, 1) * 9, device=dev, dtype=torch.float32)
             with _timed("raster3d_bwd"):
               check(L.gsr3d_raster_bwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), _ptr(b.tile_end),
-                                     _ptr(b.chunk_base), _ptr(b.chunk_tile), _ptr(b.chunk_state), b.n_chunks,
+                                     _ptr(b.chunk_base), _ptr(b.chunk_tile), _ptr(b.chunk_state),
+                                     _ptr(b.chunk_list), _ptr(b.stats_dev), b.n_chunks,
                                      C, width, height, _ptr(bgc), _ptr(b.final_T), _ptr(b.last), _ptr(v_rgb),
                                      _ptr(v_alpha), _ptr(partial), stream),
                   "gsr3d_raster_bwd")

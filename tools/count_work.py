@@ -1,0 +1,42 @@
+"""Work counters of the raster kernels (needs a -DGSR_EXP_COUNT build via GSR_LIBRARY).
+
+Prints, for one fwd+bwd of a bench config: forward batches traversed per wave (sum, max),
+forward survivors, backward survivors / 7-groups / max per wave / active chunk blocks.
+"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "pose-splatter_amd"))
+import torch  # noqa: E402
+from gsr import render as R  # noqa: E402
+from gsr._lib import lib  # noqa: E402
+from gsr.scenes import CONFIGS, gaussians3d, ring_cameras  # noqa: E402
+
+cfg = CONFIGS[int(sys.argv[1]) if len(sys.argv) > 1 else 3]
+dev = torch.device("cuda:0")
+p = gaussians3d(cfg.N, cfg.seed).to(dev).requires_grad_(True)
+V, K = ring_cameras(cfg.views, cfg.width, cfg.height)
+V, K = V.to(dev), K.to(dev)
+bg = torch.ones(3, device=dev)
+L = lib()
+f = L.gsr_debug_counters
+f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+out = (ctypes.c_ulonglong * 16)()
+rgb, alpha = R.render3d(p, V, K, cfg.width, cfg.height, bg)
+(rgb.sum() + alpha.sum()).backward()
+f(out, 1)
+R.enable_kernel_timing(True)
+rgb, alpha = R.render3d(p, V, K, cfg.width, cfg.height, bg)
+(rgb.sum() + alpha.sum()).backward()
+f(out, 1)
+print({k: round(v[0], 4) for k, v in R.kernel_times_ms().items()})
+names = ["fwd_batches", "fwd_max_batches_per_wave", "fwd_survivors", "fwd_cycles_cull+issue",
+         "fwd_cycles_composite", "fwd_cycles_wave_total", "fwd_cycles_wave_max", "-",
+         "bwd_survivors", "bwd_groups", "bwd_cycles_prologue", "bwd_cycles_groups", "bwd_cycles_epilogue",
+         "bwd_active_blocks", "bwd_cycles_wave_max", "-"]
+for n, v in zip(names, out):
+    print(f"{n:28s} {v}")
+st = R.last_stats()
+print({k: v for k, v in st.items() if not k.startswith("_")})
