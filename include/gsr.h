@@ -40,8 +40,11 @@
  *   rect: 2 uint32 per (c,n): {x0 | x1<<16, y0 | y1<<16}, tiles [x0,x1) x [y0,y1).
  *
  * Per-entry gradient partials (written by *_raster_bwd, reduced by *_project_bwd):
- *   9 floats per sorted intersection s:  d/dx, d/dy, d/da, d/db, d/dc, d/dopacity, d/drgb[3]
- *   (summed over the 16x16 tile's pixels) — a deterministic replacement for float atomics.
+ *   one row of GSR_PARTIAL_STRIDE floats per intersection, in EMISSION order (row
+ *   k = isect_offset[c*N+n] + j, j = row-major index of the tile in the Gaussian's rect):
+ *   d/dx, d/dy, d/da, d/db, d/dc, d/dopacity, d/drgb[3], 0, 0, 0 (summed over the 16x16
+ *   tile's pixels) — a deterministic replacement for float atomics.  Only entries before
+ *   their tile's cut (see tile_cut) are written; the others are never read.
  */
 #ifndef GSR_H
 #define GSR_H
@@ -65,6 +68,7 @@ extern "C" {
 #define GSR_ORDER_INDEX 1              /* 2D: per-tile list ordered by parameter index  */
 
 #define GSR_CHUNK 256                  /* list entries per backward work unit (chunk)   */
+#define GSR_PARTIAL_STRIDE 12          /* floats per partial row (9 used, 16 B aligned) */
 
 typedef struct gsr_bin_stats {
   int64_t n_isect;     /* total (Gaussian, tile) intersections I                     */
@@ -120,17 +124,16 @@ size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT);
 
 /* Emit (tile, key) pairs and sort each tile's list in LDS.  Outputs:
  *   sorted_ids [I]: c*N+n per sorted entry (what the rasterizer reads),
- *   slot_of_k  [I]: for emission entry k = isect_offset[cn]+j (j = row-major index of the
- *                   tile in the Gaussian's rect) its pre-sort slot in the tile's bucket,
- *   pos_of_slot[I]: for every pre-sort slot its sorted position s; the sorted position of
- *                   emission entry k is pos_of_slot[slot_of_k[k]] (used by *_project_bwd).
- * order: GSR_ORDER_DEPTH (3D) or GSR_ORDER_INDEX (2D).  max_seg/n_busy from stats. */
+ *   k_of_s     [I]: the emission entry k = isect_offset[cn]+j of each sorted entry (j =
+ *                   row-major index of the tile in the Gaussian's rect): where the raster
+ *                   backward stores that entry's partial row.
+ * Sort key per entry: (sort word << 32) | c*N+n, sort word = depth float bits (3D, order
+ * GSR_ORDER_DEPTH) or c*N+n (2D, GSR_ORDER_INDEX).  max_seg/n_busy from stats. */
 int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_offset,
                  const int32_t* tile_offset, const int32_t* busy_tiles, int C, int64_t N,
                  int width, int height, int order, int64_t n_isect, int32_t max_seg,
                  int32_t n_busy, void* workspace, size_t workspace_bytes,
-                 int32_t* sorted_ids, int32_t* slot_of_k, int32_t* pos_of_slot,
-                 void* stream);
+                 int32_t* sorted_ids, int32_t* k_of_s, void* stream);
 
 /* ---------------------------------------------------------------- (c) rasterisation */
 
@@ -140,7 +143,9 @@ int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_of
  * Empty tiles get the background (written by extra fill workgroups).  bg [C,3].
  * Outputs rgb [C,H,W,3], alpha [C,H,W], final_T [C,H,W] (exact transmittance, kept for the
  * backward), last [C,H,W] (index of the last contributing sorted entry, -1 if none),
- * tile_end [CT] (1 + max last over the tile, or the tile's start), and for the
+ * tile_end [CT] (1 + max last over the tile, or the tile's start), tile_cut [CT] (sort key
+ * of the tile's entry at tile_end, ~0 if none: an entry has a partial row iff its key is
+ * below its tile's cut), and for the
  * chunk-parallel backward: chunk_state [n_chunks*256*4] ({T at the chunk's end, the rgb
  * sum of all later chunks} per pixel of the tile, for every GSR_CHUNK-entry chunk the tile's
  * walk reached), chunk_tile [n_chunks] (owning tile of each chunk) and chunk_list
@@ -150,24 +155,25 @@ int gsr3d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t*
                      const int32_t* tile_order, const int32_t* chunk_base, int C, int width,
                      int height, const float* bg, int32_t n_busy, gsr_bin_stats* stats,
                      float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
-                     float* chunk_state, int32_t* chunk_tile, int32_t* chunk_list, void* stream);
+                     uint64_t* tile_cut, float* chunk_state, int32_t* chunk_tile,
+                     int32_t* chunk_list, void* stream);
 
 /* Backward of gsr3d_raster_fwd: workgroup b takes chunk_list[b] for b < stats->n_active
- * (n_chunks bounds the grid).  v_rgb [C,H,W,3], v_alpha [C,H,W] (contiguous).  Writes
- * partial [I*9] for every sorted entry s in [tile start, tile_end). */
+ * (n_chunks bounds the grid).  v_rgb [C,H,W,3], v_alpha [C,H,W] (contiguous).  Writes the
+ * partial row k_of_s[s] of every sorted entry s in [tile start, tile_end). */
 int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_end, const int32_t* chunk_base,
                      const int32_t* chunk_tile, const float* chunk_state,
                      const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
                      int C, int width, int height, const float* bg, const float* final_T,
                      const int32_t* last, const float* v_rgb, const float* v_alpha,
-                     float* partial, void* stream);
+                     const int32_t* k_of_s, float* partial, void* stream);
 
 /* 2D index-order compositor (src/gaussian_renderer.py:416-425), integer pixel centres.
  * rgb = canvas + (1-A)*bg, alpha = A.  Same outputs as the 3D call (final_T = 1-A unused). */
 int gsr2d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                      int width, int height, const float* bg, float* rgb, float* alpha,
-                     int32_t* last, int32_t* tile_end, void* stream);
+                     int32_t* last, int32_t* tile_end, uint64_t* tile_cut, void* stream);
 
 /* Workspace for gsr2d_raster_bwd (transmittance checkpoints), bytes. */
 size_t gsr2d_raster_bwd_workspace(int64_t n_isect, int64_t CT);
@@ -176,23 +182,23 @@ int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t*
                      const int32_t* tile_end, const int32_t* busy_tiles, int32_t n_busy,
                      int width, int height, const float* bg, const int32_t* last,
                      const float* v_rgb, const float* v_alpha, void* workspace,
-                     size_t workspace_bytes, float* partial, void* stream);
+                     size_t workspace_bytes, const int32_t* k_of_s, float* partial, void* stream);
 
 /* ---------------------------------------------------------------- projection backward */
 
-/* Reduce the per-entry partials of each (c,n), chain through projection and the adapter
- * activations, sum over cameras: v_params [N,14] (fully overwritten, deterministic). */
+/* Reduce the partial rows of each (c,n) (those below their tile's cut, in row order),
+ * chain through projection and the adapter activations, sum over cameras: v_params [N,14]
+ * (fully overwritten, deterministic).  rec: the forward's splat records (for sort keys). */
 int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride,
                       const float* viewmats, const float* Ks, int C, int width, int height,
-                      float eps2d, const uint32_t* rect, const int32_t* isect_offset,
-                      const int32_t* isect_count, const int32_t* slot_of_k,
-                      const int32_t* pos_of_slot, const int32_t* tile_end,
-                      const float* partial, float* v_params, void* stream);
+                      float eps2d, const float* rec, const uint32_t* rect,
+                      const int32_t* isect_offset, const int32_t* isect_count,
+                      const uint64_t* tile_cut, const float* partial, float* v_params,
+                      void* stream);
 
 int gsr2d_project_bwd(const float* params, int64_t N, int64_t row_stride, int width,
                       int height, const uint32_t* rect, const int32_t* isect_offset,
-                      const int32_t* isect_count, const int32_t* slot_of_k,
-                      const int32_t* pos_of_slot, const int32_t* tile_end,
+                      const int32_t* isect_count, const uint64_t* tile_cut,
                       const float* partial, float* v_params, void* stream);
 
 #ifdef __cplusplus

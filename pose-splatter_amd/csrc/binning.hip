@@ -142,18 +142,10 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(const int32_t* __rest
 }
 
 // ---------------------------------------------------------------- emission
-__device__ __forceinline__ uint64_t make_key(const Splat* rec, int64_t cn, int order) {
-  if (order == GSR_ORDER_DEPTH) {
-    const uint32_t d = __float_as_uint(rec[cn].p0.w);
-    return ((uint64_t)d << 32) | (uint64_t)(uint32_t)cn;
-  }
-  return ((uint64_t)(uint32_t)cn << 32) | (uint64_t)(uint32_t)cn;   // 2D: sort word = index
-}
-
 __global__ __launch_bounds__(kEmitThreads) void k_emit(const Splat* __restrict__ rec, const uint2* __restrict__ rect,
                                                       const int32_t* __restrict__ isect_offset, int64_t N, int tw,
                                                       int th, int order, int use_lds, int32_t* __restrict__ cursor,
-                                                      uint64_t* __restrict__ keys, int32_t* __restrict__ slot_of_k) {
+                                                      uint64_t* __restrict__ keys, int32_t* __restrict__ k_of_slot) {
   extern __shared__ int hist[];
   const int c = blockIdx.y;
   const int T = tw * th;
@@ -181,14 +173,14 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const Splat* __restrict__
     const uint2 r = rect[cn];
     const int x0 = r.x & 0xffff, x1 = r.x >> 16, y0 = r.y & 0xffff, y1 = r.y >> 16;
     if (x1 <= x0 || y1 <= y0) continue;
-    const uint64_t key = make_key(rec, cn, order);
-    int32_t* sk = slot_of_k + isect_offset[cn];   // emission entries of (c,n): rect row-major
+    const uint64_t key = sort_key(rec, cn, order);
+    int k = isect_offset[cn];   // emission entries of (c,n): k = offset + rect row-major index
     for (int ty = y0; ty < y1; ++ty)
       for (int tx = x0; tx < x1; ++tx) {
         const int t = ty * tw + tx;
         const int slot = use_lds ? atomicAdd(&hist[t], 1) : atomicAdd(&gcur[t], 1);
         keys[slot] = key;
-        *sk++ = slot;
+        k_of_slot[slot] = k++;
       }
   }
 }
@@ -336,11 +328,12 @@ __device__ void merge_runs(const uint64_t* __restrict__ a, const int32_t* __rest
   }
 }
 
-// Outputs: sorted_ids[s] = c*N+n of sorted entry s; pos_of_slot[pre-sort slot] = s.
+// Outputs: sorted_ids[s] = c*N+n of sorted entry s; k_of_s[s] = its emission entry index.
 __global__ __launch_bounds__(kSortThreads) void k_segsort(
     uint64_t* __restrict__ keys, uint64_t* __restrict__ tmpk, int32_t* __restrict__ tmpp0,
     int32_t* __restrict__ tmpp1, const int32_t* __restrict__ tile_offset, const int32_t* __restrict__ busy,
-    int lds_keys, int32_t* __restrict__ sorted_ids, int32_t* __restrict__ pos_of_slot) {
+    const int32_t* __restrict__ k_of_slot, int lds_keys, int32_t* __restrict__ sorted_ids,
+    int32_t* __restrict__ k_of_s) {
   extern __shared__ uint64_t s_keys[];
   int* s_hist = (int*)(s_keys + lds_keys);
   const int ct = busy[blockIdx.x];
@@ -355,7 +348,7 @@ __global__ __launch_bounds__(kSortThreads) void k_segsort(
     for (int s = threadIdx.x; s < len; s += blockDim.x) {
       const uint32_t p = low_word(s_keys[s]);
       sorted_ids[start + s] = (int32_t)low_word(seg[p]);
-      pos_of_slot[start + p] = start + s;
+      k_of_s[start + s] = k_of_slot[start + p];
     }
     return;
   }
@@ -393,7 +386,7 @@ __global__ __launch_bounds__(kSortThreads) void k_segsort(
   }
   for (int s = threadIdx.x; s < len; s += blockDim.x) {
     sorted_ids[start + s] = (int32_t)low_word(kA[s]);
-    pos_of_slot[start + pA[s]] = start + s;
+    k_of_s[start + s] = k_of_slot[start + pA[s]];
   }
 }
 
@@ -431,15 +424,15 @@ int gsr_bin_offsets(const int32_t* isect_count, int64_t CN, const int32_t* tile_
 }
 
 size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT) {
-  // keys [I] + merge keys [I] (u64), two merge payloads [I] (i32), cursor [CT] (i32)
-  return (size_t)(2 * n_isect * sizeof(uint64_t) + 2 * n_isect * sizeof(int32_t) + (CT + 64) * sizeof(int32_t) +
+  // keys [I] + merge keys [I] (u64), two merge payloads [I] + k_of_slot [I] (i32), cursor [CT]
+  return (size_t)(2 * n_isect * sizeof(uint64_t) + 3 * n_isect * sizeof(int32_t) + (CT + 64) * sizeof(int32_t) +
                   256);
 }
 
 int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_offset, const int32_t* tile_offset,
                  const int32_t* busy_tiles, int C, int64_t N, int width, int height, int order, int64_t n_isect,
                  int32_t max_seg, int32_t n_busy, void* workspace, size_t workspace_bytes, int32_t* sorted_ids,
-                 int32_t* slot_of_k, int32_t* pos_of_slot, void* stream) {
+                 int32_t* k_of_s, void* stream) {
   GSR_REQUIRE(order == GSR_ORDER_DEPTH || order == GSR_ORDER_INDEX, "gsr_bin_sort: bad order %d", order);
   GSR_REQUIRE(n_isect >= 0 && n_isect < (1ll << 31), "gsr_bin_sort: I=%lld out of range", (long long)n_isect);
   GSR_REQUIRE((int64_t)C * N < (1ll << 31), "gsr_bin_sort: C*N too large for 32-bit ids");
@@ -453,7 +446,8 @@ int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_of
   uint64_t* tmpk = keys + n_isect;
   int32_t* tmpp0 = (int32_t*)(tmpk + n_isect);
   int32_t* tmpp1 = tmpp0 + n_isect;
-  int32_t* cursor = tmpp1 + n_isect;
+  int32_t* k_of_slot = tmpp1 + n_isect;
+  int32_t* cursor = k_of_slot + n_isect;
   if (hipMemcpyAsync(cursor, tile_offset, CT * sizeof(int32_t), hipMemcpyDeviceToDevice, s) != hipSuccess) {
     set_error("gsr_bin_sort: cursor copy failed");
     return GSR_ELAUNCH;
@@ -461,14 +455,14 @@ int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_of
   const int use_lds = T <= kHistMaxTiles;
   dim3 grid(ceil_div(N, kEmitPerBlock), C);
   hipLaunchKernelGGL(k_emit, grid, dim3(kEmitThreads), use_lds ? T * sizeof(int) : 0, s, (const Splat*)rec,
-                     (const uint2*)rect, isect_offset, N, tw, th, order, use_lds, cursor, keys, slot_of_k);
+                     (const uint2*)rect, isect_offset, N, tw, th, order, use_lds, cursor, keys, k_of_slot);
   GSR_LAUNCH_CHECK("k_emit");
   if (n_busy > 0) {
     int lds_keys = 1024;
     while (lds_keys < max_seg && lds_keys < kSortLdsKeys) lds_keys <<= 1;
     const size_t lds = lds_keys * sizeof(uint64_t) + (kSortWaves * 256 + 64) * sizeof(int);
     hipLaunchKernelGGL(k_segsort, dim3(n_busy), dim3(kSortThreads), lds, s, keys, tmpk, tmpp0, tmpp1, tile_offset,
-                       busy_tiles, lds_keys, sorted_ids, pos_of_slot);
+                       busy_tiles, k_of_slot, lds_keys, sorted_ids, k_of_s);
     GSR_LAUNCH_CHECK("k_segsort");
   }
   return GSR_OK;

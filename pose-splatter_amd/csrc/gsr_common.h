@@ -16,6 +16,7 @@ constexpr float kAlphaMax = 0.999f;              // gsplat alpha clamp
 constexpr float kTMin = 1e-4f;                   // gsplat transmittance stop
 constexpr float kExtendMax = 3.33f;              // gsplat >=1.5 max sigma extent
 constexpr int kPartial = 9;                      // per-entry gradient partial width
+constexpr int kPartialStride = GSR_PARTIAL_STRIDE;   // floats per partial row (3 x float4)
 
 // Splat record: 3 x float4 (48 B) per (camera, Gaussian).  See include/gsr.h.
 struct __align__(16) Splat {
@@ -23,6 +24,14 @@ struct __align__(16) Splat {
   float4 p1;  // a, b, c, 0     (sigma = a dx^2 + b dx dy + c dy^2)
   float4 p2;  // r, g, b, 0
 };
+
+// Sort key of (c,n)'s entries: (sort word << 32) | c*N+n.  3D sort word = the depth's float
+// bits (depth > 0: integer order = float order); 2D = the index itself.  Keys are unique
+// inside a tile, so "sorted position < tile_end" <=> "key < key of the entry at tile_end".
+__device__ __forceinline__ uint64_t sort_key(const Splat* rec, int64_t cn, int order) {
+  const uint32_t w = order == GSR_ORDER_DEPTH ? __float_as_uint(rec[cn].p0.w) : (uint32_t)cn;
+  return ((uint64_t)w << 32) | (uint64_t)(uint32_t)cn;
+}
 
 // ---------------------------------------------------------------- host-side error state
 void set_error(const char* fmt, ...);

@@ -18,35 +18,32 @@ namespace gsr {
 
 constexpr int kBwdThreads = 256;
 
-// Emission entry k = isect_offset[c*N+n] + j (j: row-major tile of the rect) → pre-sort slot
-// (slot_of_k, written by the emitter) → sorted position (pos_of_slot, written by the sort).
-__device__ __forceinline__ void gather_partials(const uint2 r, int T, int tw, int64_t ct_base,
-                                                const int32_t* __restrict__ slot_of_k,
-                                                const int32_t* __restrict__ pos_of_slot, int off,
-                                                const int32_t* __restrict__ tile_end,
+// Sum the partial rows of one (c,n): entry j (row-major tile of its rect) has row
+// isect_offset[c*N+n] + j (emission order); it was written by the raster backward iff the
+// entry precedes its tile's cut (key < tile_cut[tile]), otherwise it contributes nothing.
+__device__ __forceinline__ void gather_partials(const uint2 r, int tw, int64_t ct_base, uint64_t key, int off,
+                                                const uint64_t* __restrict__ tile_cut,
                                                 const float* __restrict__ partial, float (&acc)[kPartial]) {
   const int x0 = r.x & 0xffff, x1 = r.x >> 16, y0 = r.y & 0xffff, y1 = r.y >> 16;
-  const int w = x1 - x0;
-  int jj = 0;
+  const float4* row = reinterpret_cast<const float4*>(partial + (int64_t)off * kPartialStride);
   for (int ty = y0; ty < y1; ++ty) {
-    for (int tx = x0; tx < x0 + w; ++tx, ++jj) {
-      const int s = pos_of_slot[slot_of_k[off + jj]];
-      const int t = ty * tw + tx;
-      if (s < tile_end[ct_base + t]) {
-        const float* p = partial + (int64_t)s * kPartial;
-#pragma unroll
-        for (int v = 0; v < kPartial; ++v) acc[v] += p[v];
+    for (int tx = x0; tx < x1; ++tx, row += 3) {
+      if (key < tile_cut[ct_base + ty * tw + tx]) {
+        const float4 a = row[0], b = row[1];
+        const float c = row[2].x;
+        acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+        acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+        acc[8] += c;
       }
     }
   }
-  (void)T;
 }
 
 __global__ __launch_bounds__(kBwdThreads) void k_project3d_bwd(
     const float* __restrict__ params, int64_t N, int64_t stride, const float* __restrict__ viewmats,
     const float* __restrict__ Ks, int C, int W, int H, float eps2d, int tw, int th, const uint2* __restrict__ rect,
     const int32_t* __restrict__ isect_offset, const int32_t* __restrict__ isect_count,
-    const int32_t* __restrict__ slot_of_k, const int32_t* __restrict__ pos_of_slot, const int32_t* __restrict__ tile_end, const float* __restrict__ partial,
+    const Splat* __restrict__ rec, const uint64_t* __restrict__ tile_cut, const float* __restrict__ partial,
     float* __restrict__ v_params) {
   const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
@@ -68,8 +65,8 @@ __global__ __launch_bounds__(kBwdThreads) void k_project3d_bwd(
     float acc[kPartial];
 #pragma unroll
     for (int v = 0; v < kPartial; ++v) acc[v] = 0.f;
-    gather_partials(rect[cn], T, tw, (int64_t)c * T, slot_of_k, pos_of_slot, isect_offset[cn], tile_end, partial,
-                    acc);
+    gather_partials(rect[cn], tw, (int64_t)c * T, sort_key(rec, cn, GSR_ORDER_DEPTH), isect_offset[cn], tile_cut,
+                    partial, acc);
     const Cam cam = load_cam(viewmats + c * 16, Ks + c * 9);
     // recompute the forward geometry (not culled: it has intersections)
     geo3d(a, cam, W, H, 0.f, 3.4e38f, eps2d, g);
@@ -207,8 +204,7 @@ __global__ __launch_bounds__(kBwdThreads) void k_project3d_bwd(
 __global__ __launch_bounds__(kBwdThreads) void k_project2d_bwd(
     const float* __restrict__ params, int64_t N, int64_t stride, int tw, int th, const uint2* __restrict__ rect,
     const int32_t* __restrict__ isect_offset, const int32_t* __restrict__ isect_count,
-    const int32_t* __restrict__ slot_of_k, const int32_t* __restrict__ pos_of_slot, const int32_t* __restrict__ tile_end, const float* __restrict__ partial,
-    float* __restrict__ v_params) {
+    const uint64_t* __restrict__ tile_cut, const float* __restrict__ partial, float* __restrict__ v_params) {
   const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
   float* out = v_params + n * 9;
@@ -220,7 +216,9 @@ __global__ __launch_bounds__(kBwdThreads) void k_project2d_bwd(
   float acc[kPartial];
 #pragma unroll
   for (int v = 0; v < kPartial; ++v) acc[v] = 0.f;
-  gather_partials(rect[n], tw * th, tw, 0, slot_of_k, pos_of_slot, isect_offset[n], tile_end, partial, acc);
+  const uint64_t key = ((uint64_t)(uint32_t)n << 32) | (uint64_t)(uint32_t)n;   // sort_key, index order
+  gather_partials(rect[n], tw, 0, key, isect_offset[n], tile_cut, partial, acc);
+  (void)th;
   const Geo2D g = geo2d(params + n * stride);
   const float va = acc[2], vb = acc[3], vc = acc[4];
   const float C = g.cs, S = g.sn;
@@ -249,31 +247,30 @@ using namespace gsr;
 extern "C" {
 
 int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride, const float* viewmats, const float* Ks,
-                      int C, int width, int height, float eps2d, const uint32_t* rect, const int32_t* isect_offset,
-                      const int32_t* isect_count, const int32_t* slot_of_k, const int32_t* pos_of_slot,
-                      const int32_t* tile_end, const float* partial, float* v_params, void* stream) {
+                      int C, int width, int height, float eps2d, const float* rec, const uint32_t* rect,
+                      const int32_t* isect_offset, const int32_t* isect_count, const uint64_t* tile_cut,
+                      const float* partial, float* v_params, void* stream) {
   GSR_REQUIRE(N >= 0 && C >= 1 && width > 0 && height > 0, "gsr3d_project_bwd: bad arguments");
   GSR_REQUIRE(row_stride >= 14, "gsr3d_project_bwd: row_stride < 14");
   if (N == 0) return GSR_OK;
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   hipLaunchKernelGGL(k_project3d_bwd, dim3(ceil_div(N, kBwdThreads)), dim3(kBwdThreads), 0, (hipStream_t)stream,
                      params, N, row_stride, viewmats, Ks, C, width, height, eps2d, tw, th, (const uint2*)rect,
-                     isect_offset, isect_count, slot_of_k, pos_of_slot, tile_end, partial, v_params);
+                     isect_offset, isect_count, (const Splat*)rec, tile_cut, partial, v_params);
   GSR_LAUNCH_CHECK("k_project3d_bwd");
   return GSR_OK;
 }
 
 int gsr2d_project_bwd(const float* params, int64_t N, int64_t row_stride, int width, int height,
                       const uint32_t* rect, const int32_t* isect_offset, const int32_t* isect_count,
-                      const int32_t* slot_of_k, const int32_t* pos_of_slot, const int32_t* tile_end,
-                      const float* partial, float* v_params, void* stream) {
+                      const uint64_t* tile_cut, const float* partial, float* v_params, void* stream) {
   GSR_REQUIRE(N >= 0 && width > 0 && height > 0, "gsr2d_project_bwd: bad arguments");
   GSR_REQUIRE(row_stride >= 9, "gsr2d_project_bwd: row_stride < 9");
   if (N == 0) return GSR_OK;
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   hipLaunchKernelGGL(k_project2d_bwd, dim3(ceil_div(N, kBwdThreads)), dim3(kBwdThreads), 0, (hipStream_t)stream,
-                     params, N, row_stride, tw, th, (const uint2*)rect, isect_offset, isect_count, slot_of_k, pos_of_slot,
-                     tile_end, partial, v_params);
+                     params, N, row_stride, tw, th, (const uint2*)rect, isect_offset, isect_count, tile_cut, partial,
+                     v_params);
   GSR_LAUNCH_CHECK("k_project2d_bwd");
   return GSR_OK;
 }

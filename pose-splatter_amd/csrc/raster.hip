@@ -95,7 +95,8 @@ template <bool IS2D>
 __device__ void fill_empty(const int32_t* __restrict__ order, const int32_t* __restrict__ tile_offset, int n_busy,
                            int64_t CT, int W, int H, int tw, int th, const float* __restrict__ bg,
                            float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
-                           int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end) {
+                           int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end,
+                           uint64_t* __restrict__ tile_cut) {
   const int G = gridDim.x - n_busy;
   for (int64_t t = n_busy + (blockIdx.x - n_busy); t < CT; t += G) {
     const int ct = order[t];
@@ -110,7 +111,10 @@ __device__ void fill_empty(const int32_t* __restrict__ order, const int32_t* __r
       if (!IS2D) out_T[pix] = 1.f;
       out_last[pix] = -1;
     }
-    if (threadIdx.x == 0) tile_end[ct] = tile_offset[ct];
+    if (threadIdx.x == 0) {
+      tile_end[ct] = tile_offset[ct];
+      tile_cut[ct] = ~0ull;
+    }
   }
 }
 
@@ -128,14 +132,14 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
     int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end, float4* __restrict__ ckpt,
     const int32_t* __restrict__ chunk_base, int32_t* __restrict__ chunk_tile, int n_busy, int64_t CT,
-    gsr_bin_stats* __restrict__ stats, int32_t* __restrict__ chunk_list) {
+    gsr_bin_stats* __restrict__ stats, int32_t* __restrict__ chunk_list, uint64_t* __restrict__ tile_cut) {
   __shared__ float4 s_p0[4][64];
   __shared__ float4 s_p1[4][64];
   __shared__ float4 s_p2[4][64];
   __shared__ int s_max, s_pos, s_nact;
   if ((int)blockIdx.x >= n_busy) {
     fill_empty<IS2D>(order, tile_offset, n_busy, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T, out_last,
-                     tile_end);
+                     tile_end, tile_cut);
     return;
   }
   const int ct = order[blockIdx.x];
@@ -302,6 +306,8 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   if (threadIdx.x == 0) {
     const int te = s_max >= 0 ? s_max + 1 : start;
     tile_end[ct] = te;
+    // key of the first entry past tile_end (its partial is never written)
+    tile_cut[ct] = te < end ? sort_key(rec, ids[te], IS2D ? GSR_ORDER_INDEX : GSR_ORDER_DEPTH) : ~0ull;
     // 3D: register the chunks before tile_end with the backward's work list
     const int nact = IS2D ? 0 : (te - start + kChunk3 - 1) / kChunk3;
     s_nact = nact;
@@ -318,7 +324,8 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
 __global__ __launch_bounds__(kRasterThreads) void k_raster2d_fwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
     int W, int H, int tw, int th, const float* __restrict__ bg, float* __restrict__ out_rgb,
-    float* __restrict__ out_alpha, int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end) {
+    float* __restrict__ out_alpha, int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end,
+    uint64_t* __restrict__ tile_cut) {
   __shared__ float4 s_p0[kRasterThreads];
   __shared__ float4 s_p1[kRasterThreads];
   __shared__ float4 s_p2[kRasterThreads];
@@ -380,7 +387,11 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster2d_fwd(
   __syncthreads();
   if (last >= 0) atomicMax(&s_max, last);
   __syncthreads();
-  if (threadIdx.x == 0) tile_end[ct] = s_max >= 0 ? s_max + 1 : start;
+  if (threadIdx.x == 0) {
+    const int te = s_max >= 0 ? s_max + 1 : start;
+    tile_end[ct] = te;
+    tile_cut[ct] = te < end ? sort_key(rec, ids[te], GSR_ORDER_INDEX) : ~0ull;
+  }
 }
 
 // ---------------------------------------------------------------- partial combine helpers
@@ -404,11 +415,23 @@ __device__ __forceinline__ void wave_emit(PartialLds& L, int k, bool any, float 
   }
 }
 
-__device__ __forceinline__ void block_store_partials(const PartialLds& L, int b0, int n, float* __restrict__ partial) {
+// Partial rows are stored in EMISSION order (row k_of_s[s] for sorted entry s), 12 floats
+// (3 x float4) per row, so *_project_bwd reads each Gaussian's rows contiguously.
+__device__ __forceinline__ void store_partial_row(float* __restrict__ partial, int k, const float (&v)[kPartial]) {
+  float4* dst = reinterpret_cast<float4*>(partial + (int64_t)k * kPartialStride);
+  dst[0] = make_float4(v[0], v[1], v[2], v[3]);
+  dst[1] = make_float4(v[4], v[5], v[6], v[7]);
+  dst[2] = make_float4(v[8], 0.f, 0.f, 0.f);
+}
+
+__device__ __forceinline__ void block_store_partials(const PartialLds& L, int b0, int n,
+                                                     const int32_t* __restrict__ k_of_s,
+                                                     float* __restrict__ partial) {
   for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    float* dst = partial + (int64_t)(b0 + k) * kPartial;
+    float v[kPartial];
 #pragma unroll
-    for (int v = 0; v < kPartial; ++v) dst[v] = (L.w[v][0][k] + L.w[v][1][k]) + (L.w[v][2][k] + L.w[v][3][k]);
+    for (int q = 0; q < kPartial; ++q) v[q] = (L.w[q][0][k] + L.w[q][1][k]) + (L.w[q][2][k] + L.w[q][3][k]);
+    store_partial_row(partial, k_of_s[b0 + k], v);
   }
 }
 
@@ -430,7 +453,8 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
     const int32_t* __restrict__ chunk_tile, const float4* __restrict__ ckpt, int W, int H, int tw, int th,
     const float* __restrict__ bg, const float* __restrict__ final_T, const int32_t* __restrict__ last_in,
     const float* __restrict__ v_rgb, const float* __restrict__ v_alpha, float* __restrict__ partial,
-    const int32_t* __restrict__ chunk_list, gsr_bin_stats* __restrict__ stats) {
+    const int32_t* __restrict__ chunk_list, gsr_bin_stats* __restrict__ stats,
+    const int32_t* __restrict__ k_of_s) {
   // slot kNull: a zero-opacity record (never valid) that pads survivor groups to 7
   constexpr int kNull = kChunk3;
   constexpr int kGroup = 7;
@@ -570,9 +594,10 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
   }
   if (threadIdx.x < n) {
     const int k = threadIdx.x;
-    float* dst = partial + (int64_t)(b0 + k) * kPartial;
+    float v[kPartial];
 #pragma unroll
-    for (int v = 0; v < kPartial; ++v) dst[v] = L[v][0][k] + L[v][1][k];
+    for (int q = 0; q < kPartial; ++q) v[q] = L[q][0][k] + L[q][1][k];
+    store_partial_row(partial, k_of_s[b0 + k], v);
   }
 }
 
@@ -590,7 +615,8 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster2d_bwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ tile_end, const int32_t* __restrict__ busy, int W, int H, int tw, int th,
     const float* __restrict__ bg, const int32_t* __restrict__ last_in, const float* __restrict__ v_rgb,
-    const float* __restrict__ v_alpha, float* __restrict__ ckpt, float* __restrict__ partial) {
+    const float* __restrict__ v_alpha, float* __restrict__ ckpt, const int32_t* __restrict__ k_of_s,
+    float* __restrict__ partial) {
   __shared__ float4 s_p0[kRasterThreads];
   __shared__ float4 s_p1[kRasterThreads];
   __shared__ float4 s_p2[kRasterThreads];
@@ -654,7 +680,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster2d_bwd(
     const int b0 = start + ((q * kChunk) / kRasterThreads) * kRasterThreads;
     if (b0 != loaded_b0) {
       __syncthreads();
-      if (loaded_b0 >= 0) block_store_partials(L, loaded_b0, min(kRasterThreads, eff - loaded_b0), partial);
+      if (loaded_b0 >= 0) block_store_partials(L, loaded_b0, min(kRasterThreads, eff - loaded_b0), k_of_s, partial);
       __syncthreads();
       const int e = b0 + threadIdx.x;
       if (e < eff) {
@@ -718,7 +744,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster2d_bwd(
     }
   }
   __syncthreads();
-  if (loaded_b0 >= 0) block_store_partials(L, loaded_b0, min(kRasterThreads, eff - loaded_b0), partial);
+  if (loaded_b0 >= 0) block_store_partials(L, loaded_b0, min(kRasterThreads, eff - loaded_b0), k_of_s, partial);
 }
 
 __global__ void k_selftest_reduce64(float* out) {
@@ -757,8 +783,8 @@ int gsr_selftest_reduce64(float* out, void* stream) {
 int gsr3d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_order, const int32_t* chunk_base, int C, int width, int height,
                      const float* bg, int32_t n_busy, gsr_bin_stats* stats, float* rgb, float* alpha,
-                     float* final_T, int32_t* last, int32_t* tile_end, float* chunk_state, int32_t* chunk_tile,
-                     int32_t* chunk_list, void* stream) {
+                     float* final_T, int32_t* last, int32_t* tile_end, uint64_t* tile_cut, float* chunk_state,
+                     int32_t* chunk_tile, int32_t* chunk_list, void* stream) {
   GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "gsr3d_raster_fwd: bad C=%d or image %dx%d", C, width, height);
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   const int64_t CT = (int64_t)C * tw * th;
@@ -768,7 +794,7 @@ int gsr3d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t*
   hipLaunchKernelGGL(k_raster_fwd<false>, dim3((unsigned)(n_busy + n_fill)), dim3(kRasterThreads), 0,
                      (hipStream_t)stream, (const Splat*)rec, sorted_ids, tile_offset, tile_order, width, height, tw,
                      th, kAlphaThreshold, bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state, chunk_base,
-                     chunk_tile, (int)n_busy, CT, stats, chunk_list);
+                     chunk_tile, (int)n_busy, CT, stats, chunk_list, tile_cut);
   GSR_LAUNCH_CHECK("k_raster_fwd<3d>");
   return GSR_OK;
 }
@@ -777,7 +803,8 @@ int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t*
                      const int32_t* tile_end, const int32_t* chunk_base, const int32_t* chunk_tile,
                      const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
                      int C, int width, int height, const float* bg, const float* final_T, const int32_t* last,
-                     const float* v_rgb, const float* v_alpha, float* partial, void* stream) {
+                     const float* v_rgb, const float* v_alpha, const int32_t* k_of_s, float* partial,
+                     void* stream) {
   GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "gsr3d_raster_bwd: bad C=%d or image %dx%d", C, width, height);
   GSR_REQUIRE(n_chunks >= 0, "gsr3d_raster_bwd: bad n_chunks");
   if (n_chunks == 0) return GSR_OK;
@@ -786,19 +813,19 @@ int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t*
   hipLaunchKernelGGL(k_raster3d_bwd, dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
                      (const Splat*)rec, sorted_ids, tile_offset, tile_end, chunk_base, chunk_tile,
                      (const float4*)chunk_state, width, height, tw, th, bg, final_T, last, v_rgb, v_alpha, partial,
-                     chunk_list, stats);
+                     chunk_list, stats, k_of_s);
   GSR_LAUNCH_CHECK("k_raster3d_bwd");
   return GSR_OK;
 }
 
 int gsr2d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset, int width,
                      int height, const float* bg, float* rgb, float* alpha, int32_t* last, int32_t* tile_end,
-                     void* stream) {
+                     uint64_t* tile_cut, void* stream) {
   GSR_REQUIRE(width > 0 && height > 0, "gsr2d_raster_fwd: bad image %dx%d", width, height);
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   hipLaunchKernelGGL(k_raster2d_fwd, dim3(tw * th), dim3(kRasterThreads), 0, (hipStream_t)stream,
                      (const Splat*)rec, sorted_ids, tile_offset, width, height, tw, th, bg, rgb, alpha, last,
-                     tile_end);
+                     tile_end, tile_cut);
   GSR_LAUNCH_CHECK("k_raster2d_fwd");
   return GSR_OK;
 }
@@ -810,14 +837,15 @@ size_t gsr2d_raster_bwd_workspace(int64_t n_isect, int64_t CT) {
 int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_end, const int32_t* busy_tiles, int32_t n_busy, int width, int height,
                      const float* bg, const int32_t* last, const float* v_rgb, const float* v_alpha, void* workspace,
-                     size_t workspace_bytes, float* partial, void* stream) {
+                     size_t workspace_bytes, const int32_t* k_of_s, float* partial, void* stream) {
   GSR_REQUIRE(width > 0 && height > 0, "gsr2d_raster_bwd: bad image %dx%d", width, height);
   if (n_busy <= 0) return GSR_OK;
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
-  (void)workspace_bytes;
+  GSR_REQUIRE(workspace != nullptr && workspace_bytes >= gsr2d_raster_bwd_workspace(0, (int64_t)tw * th),
+              "gsr2d_raster_bwd: workspace too small");
   hipLaunchKernelGGL(k_raster2d_bwd, dim3(n_busy), dim3(kRasterThreads), 0, (hipStream_t)stream,
                      (const Splat*)rec, sorted_ids, tile_offset, tile_end, busy_tiles, width, height, tw, th, bg,
-                     last, v_rgb, v_alpha, (float*)workspace, partial);
+                     last, v_rgb, v_alpha, (float*)workspace, k_of_s, partial);
   GSR_LAUNCH_CHECK("k_raster2d_bwd");
   return GSR_OK;
 }

@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get(
     "GSR_LIBRARY", os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libgsr.so"))
 
 TILE = 16
+PARTIAL_STRIDE = 12
 CHUNK = 256
 RADIUS_OPACITY_AABB = 0
 RADIUS_ISOTROPIC_3SIGMA = 1
@@ -56,19 +57,18 @@ EXPORTS = {
     "gsr_bin_offsets": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _SZ, _P, _P, _P, _P, _P, _P]),
     "gsr_bin_sort_workspace": (_SZ, [_I64, _I64]),
     "gsr_bin_sort": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I32, _I64, _I32,
-                                    _I32, _P, _SZ, _P, _P, _P, _P]),
+                                    _I32, _P, _SZ, _P, _P, _P]),
     "gsr3d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _I32, _P, _P, _P, _P,
-                                        _P, _P, _P, _P, _P, _P]),
+                                        _P, _P, _P, _P, _P, _P, _P]),
     "gsr3d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P,
-                                        _P, _P, _P, _P, _P, _P]),
-    "gsr2d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P]),
+                                        _P, _P, _P, _P, _P, _P, _P]),
+    "gsr2d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
     "gsr2d_raster_bwd_workspace": (_SZ, [_I64, _I64]),
     "gsr2d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P,
-                                        _SZ, _P, _P]),
+                                        _SZ, _P, _P, _P]),
     "gsr3d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _I32, _I32, _I32, _F, _P, _P, _P,
-                                         _P, _P, _P, _P, _P, _P]),
-    "gsr2d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P, _P,
-                                         _P, _P]),
+                                         _P, _P, _P, _P, _P]),
+    "gsr2d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
 }
 
 _lock = threading.Lock()

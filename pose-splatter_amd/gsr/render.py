@@ -144,14 +144,13 @@ class _Bins:
         dev = self.rec.device
         I = self.n_isect
         self.sorted_ids = torch.empty(max(I, 1), device=dev, dtype=torch.int32)
-        self.slot_of_k = torch.empty(max(I, 1), device=dev, dtype=torch.int32)
-        self.pos_of_slot = torch.empty(max(I, 1), device=dev, dtype=torch.int32)
+        self.k_of_s = torch.empty(max(I, 1), device=dev, dtype=torch.int32)
         ws = torch.empty(int(L.gsr_bin_sort_workspace(I, self.CT)), device=dev, dtype=torch.uint8)
         with _timed("bin_sort"):
           check(L.gsr_bin_sort(_ptr(self.rec), _ptr(self.rect), _ptr(self.isect_off), _ptr(self.tile_off),
                              _ptr(self.busy), self.C, self.N, self.W, self.H, order, I, self.max_seg,
-                             self.n_busy, _ptr(ws), ws.numel(), _ptr(self.sorted_ids), _ptr(self.slot_of_k),
-                             _ptr(self.pos_of_slot), stream), "gsr_bin_sort")
+                             self.n_busy, _ptr(ws), ws.numel(), _ptr(self.sorted_ids), _ptr(self.k_of_s),
+                             stream), "gsr_bin_sort")
 
 
 def _record_stats(b: _Bins):
@@ -196,13 +195,14 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
     b.final_T = torch.empty(C, height, width, device=dev, dtype=torch.float32)
     b.last = torch.empty(C, height, width, device=dev, dtype=torch.int32)
     b.tile_end = torch.empty(b.CT, device=dev, dtype=torch.int32)
+    b.tile_cut = torch.empty(b.CT, device=dev, dtype=torch.int64)
     b.chunk_state = torch.empty(max(b.n_chunks, 1) * 256 * 4, device=dev, dtype=torch.float32)
     b.chunk_tile = torch.empty(max(b.n_chunks, 1), device=dev, dtype=torch.int32)
     b.chunk_list = torch.empty(max(b.n_chunks, 1), device=dev, dtype=torch.int32)
     with _timed("raster3d_fwd"):
       check(L.gsr3d_raster_fwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), _ptr(b.busy), _ptr(b.chunk_base),
                              C, width, height, _ptr(bgc), b.n_busy, _ptr(b.stats_dev), _ptr(rgb), _ptr(alpha),
-                             _ptr(b.final_T), _ptr(b.last), _ptr(b.tile_end), _ptr(b.chunk_state),
+                             _ptr(b.final_T), _ptr(b.last), _ptr(b.tile_end), _ptr(b.tile_cut), _ptr(b.chunk_state),
                              _ptr(b.chunk_tile), _ptr(b.chunk_list), stream), "gsr3d_raster_fwd")
     _record_stats(b)
     return rgb, alpha, b, (p, stride, V, Kc, bgc, width, height, opts)
@@ -225,9 +225,10 @@ def _forward2d(params, bg, width, height, eps_cut):
     alpha = torch.empty(height, width, device=dev, dtype=torch.float32)
     b.last = torch.empty(height, width, device=dev, dtype=torch.int32)
     b.tile_end = torch.empty(b.CT, device=dev, dtype=torch.int32)
+    b.tile_cut = torch.empty(b.CT, device=dev, dtype=torch.int64)
     with _timed("raster2d_fwd"):
       check(L.gsr2d_raster_fwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), width, height, _ptr(bgc),
-                             _ptr(rgb), _ptr(alpha), _ptr(b.last), _ptr(b.tile_end), stream),
+                             _ptr(rgb), _ptr(alpha), _ptr(b.last), _ptr(b.tile_end), _ptr(b.tile_cut), stream),
           "gsr2d_raster_fwd")
     _record_stats(b)
     return rgb, alpha, b, (p, stride, bgc, width, height)
@@ -267,18 +268,18 @@ class _Render3D(torch.autograd.Function):
         v_alpha = v_alpha.float().contiguous()
         v_params = torch.empty(N, 14, device=dev, dtype=torch.float32)
         if N > 0:
-            partial = torch.empty(max(b.n_isect, 1) * 9, device=dev, dtype=torch.float32)
+            partial = torch.empty(max(b.n_isect, 1) * _lib.PARTIAL_STRIDE, device=dev, dtype=torch.float32)
             with _timed("raster3d_bwd"):
               check(L.gsr3d_raster_bwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), _ptr(b.tile_end),
                                      _ptr(b.chunk_base), _ptr(b.chunk_tile), _ptr(b.chunk_state),
                                      _ptr(b.chunk_list), _ptr(b.stats_dev), b.n_chunks,
                                      C, width, height, _ptr(bgc), _ptr(b.final_T), _ptr(b.last), _ptr(v_rgb),
-                                     _ptr(v_alpha), _ptr(partial), stream),
+                                     _ptr(v_alpha), _ptr(b.k_of_s), _ptr(partial), stream),
                   "gsr3d_raster_bwd")
             with _timed("project3d_bwd"):
               check(L.gsr3d_project_bwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height, opts.eps2d,
-                                      _ptr(b.rect), _ptr(b.isect_off), _ptr(b.cnt), _ptr(b.slot_of_k), _ptr(b.pos_of_slot),
-                                      _ptr(b.tile_end), _ptr(partial), _ptr(v_params), stream),
+                                      _ptr(b.rec), _ptr(b.rect), _ptr(b.isect_off), _ptr(b.cnt), _ptr(b.tile_cut),
+                                      _ptr(partial), _ptr(v_params), stream),
                   "gsr3d_project_bwd")
         return v_params.view(ctx.params_shape), None, None, None, None, None, None
 
@@ -308,16 +309,17 @@ class _Render2D(torch.autograd.Function):
         v_alpha = v_alpha.float().contiguous()
         v_params = torch.empty(N, 9, device=dev, dtype=torch.float32)
         if N > 0:
-            partial = torch.empty(max(b.n_isect, 1) * 9, device=dev, dtype=torch.float32)
+            partial = torch.empty(max(b.n_isect, 1) * _lib.PARTIAL_STRIDE, device=dev, dtype=torch.float32)
             ws = torch.empty(int(L.gsr2d_raster_bwd_workspace(b.n_isect, b.CT)), device=dev, dtype=torch.uint8)
             with _timed("raster2d_bwd"):
               check(L.gsr2d_raster_bwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), _ptr(b.tile_end),
                                      _ptr(b.busy), b.n_busy, width, height, _ptr(bgc), _ptr(b.last),
-                                     _ptr(v_rgb), _ptr(v_alpha), _ptr(ws), ws.numel(), _ptr(partial), stream),
+                                     _ptr(v_rgb), _ptr(v_alpha), _ptr(ws), ws.numel(), _ptr(b.k_of_s), _ptr(partial),
+                                     stream),
                   "gsr2d_raster_bwd")
             with _timed("project2d_bwd"):
               check(L.gsr2d_project_bwd(_ptr(p), N, stride, width, height, _ptr(b.rect), _ptr(b.isect_off),
-                                      _ptr(b.cnt), _ptr(b.slot_of_k), _ptr(b.pos_of_slot), _ptr(b.tile_end), _ptr(partial),
+                                      _ptr(b.cnt), _ptr(b.tile_cut), _ptr(partial),
                                       _ptr(v_params), stream), "gsr2d_project_bwd")
         return v_params.view(ctx.params_shape), None, None, None, None
 

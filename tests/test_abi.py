@@ -48,8 +48,7 @@ def test_invalid_arguments_are_reported_not_launched():
     assert rc == -1 and b"radius_mode" in lib.gsr_last_error()
     rc = lib.gsr2d_project_fwd(None, 10, 9, 64, 64, 2.0, None, None, None, None, None)
     assert rc == -1 and b"eps_cut" in lib.gsr_last_error()
-    rc = lib.gsr_bin_sort(None, None, None, None, None, 1, 10, 64, 64, 5, 0, 0, 0, None, 0, None, None, None,
-                          None)
+    rc = lib.gsr_bin_sort(None, None, None, None, None, 1, 10, 64, 64, 5, 0, 0, 0, None, 0, None, None, None)
     assert rc == -1 and b"bad order" in lib.gsr_last_error()
     with pytest.raises(ValueError, match="bad order"):
         _lib.check(rc, "gsr_bin_sort")
@@ -69,3 +68,17 @@ def test_missing_library_fails_loudly(tmp_path, monkeypatch):
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(_lib.GsrLibraryError):
         _lib.lib()
+
+
+def test_binding_prototypes_match_header():
+    """Every ctypes prototype in gsr/_lib.py has the header's parameter count."""
+    import re
+    from gsr import _lib
+    hdr = open(os.path.join(ROOT, "include", "gsr.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    decls = dict(re.findall(r"\b(gsr\w+)\s*\(([^;{]*?)\)\s*;", hdr, flags=re.S))
+    assert set(_lib.EXPORTS) <= set(decls), set(_lib.EXPORTS) - set(decls)
+    for name, (_, args) in _lib.EXPORTS.items():
+        params = decls[name].strip()
+        n = 0 if params in ("", "void") else params.count(",") + 1
+        assert n == len(args), (name, n, len(args))

@@ -144,15 +144,14 @@ def test_3d_binning_exact(cuda):
     exp_off = torch.zeros(C * T + 1, dtype=torch.int64)
     exp_off[1:] = torch.cumsum(torch.bincount(exp_tiles, minlength=C * T), 0)
     assert torch.equal(b.tile_off.cpu().to(torch.int64), exp_off)
-    # inverse map: emission entry k → pre-sort slot → sorted position (both permutations)
-    sk = b.slot_of_k.cpu()[:I].to(torch.int64)
-    ps = b.pos_of_slot.cpu()[:I].to(torch.int64)
-    assert torch.equal(torch.sort(sk).values, torch.arange(I))
-    assert torch.equal(torch.sort(ps).values, torch.arange(I))
-    pos = ps[sk]
+    # k_of_s: the emission entry of each sorted entry (a permutation); emission entry
+    # k = isect_offset[cn] + j belongs to Gaussian cn and to tile j (row-major) of its rect
+    ks = b.k_of_s.cpu()[:I].to(torch.int64)
+    assert torch.equal(torch.sort(ks).values, torch.arange(I))
+    pos = torch.empty(I, dtype=torch.int64)
+    pos[ks] = torch.arange(I)
     ids = b.sorted_ids.cpu()[:I].to(torch.int64)
     assert torch.equal(ids[pos], torch.repeat_interleave(torch.arange(C * N), cnt))
-    # entry j of a Gaussian's rect lands in that (camera, tile)'s bucket (row-major j)
     tiles_of_pos = torch.searchsorted(exp_off, pos, right=True) - 1
     exp_k_tiles = []
     for cn in torch.nonzero(cnt > 0).flatten().tolist():
