@@ -28,6 +28,14 @@ __device__ __forceinline__ void gather_partials(const uint2 r, int tw, int64_t c
   const float4* row = reinterpret_cast<const float4*>(partial + (int64_t)off * kPartialStride);
   for (int ty = y0; ty < y1; ++ty) {
     for (int tx = x0; tx < x1; ++tx, row += 3) {
+#ifdef GSR_PB_SPEC
+      const float4 a = row[0], b = row[1];
+      const float c = row[2].x;
+      const bool on = key < tile_cut[ct_base + ty * tw + tx];
+      acc[0] += on ? a.x : 0.f; acc[1] += on ? a.y : 0.f; acc[2] += on ? a.z : 0.f; acc[3] += on ? a.w : 0.f;
+      acc[4] += on ? b.x : 0.f; acc[5] += on ? b.y : 0.f; acc[6] += on ? b.z : 0.f; acc[7] += on ? b.w : 0.f;
+      acc[8] += on ? c : 0.f;
+#else
       if (key < tile_cut[ct_base + ty * tw + tx]) {
         const float4 a = row[0], b = row[1];
         const float c = row[2].x;
@@ -35,147 +43,197 @@ __device__ __forceinline__ void gather_partials(const uint2 r, int tw, int64_t c
         acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
         acc[8] += c;
       }
+#endif
     }
   }
 }
 
-__global__ __launch_bounds__(kBwdThreads) void k_project3d_bwd(
+// (camera, Gaussian)-parallel: a workgroup owns G Gaussians and CPB = min(C, 256) camera
+// slots (thread = slot * G + g; slot s handles cameras s, s+CPB, ...).  Each thread gathers
+// its (c,n) partial rows and chains them to the camera's contribution {v_mean, V_M (the
+// gradient of M = R diag(s)), v_colour, v_opacity}; the slots are then summed in LDS in
+// fixed order (deterministic) and one thread per Gaussian applies the camera-independent
+// chain (rotation / scale / quaternion normalisation / adapter activations).
+constexpr int kContrib = 16;   // v_m[3], V_M[9], v_col[3], v_op
+
+#ifdef GSR_PB_OCC
+#define GSR_PB_ATTR __attribute__((amdgpu_waves_per_eu(GSR_PB_OCC)))
+#else
+#define GSR_PB_ATTR
+#endif
+__global__ __launch_bounds__(kBwdThreads) GSR_PB_ATTR void k_project3d_bwd(
     const float* __restrict__ params, int64_t N, int64_t stride, const float* __restrict__ viewmats,
     const float* __restrict__ Ks, int C, int W, int H, float eps2d, int tw, int th, const uint2* __restrict__ rect,
     const int32_t* __restrict__ isect_offset, const int32_t* __restrict__ isect_count,
     const Splat* __restrict__ rec, const uint64_t* __restrict__ tile_cut, const float* __restrict__ partial,
-    float* __restrict__ v_params) {
-  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  const float* p = params + n * stride;
-  const Act3D a = activate3d(p);
+    int CPB, int G, float* __restrict__ v_params) {
+  __shared__ float s_con[kBwdThreads][kContrib + 1];
+  __shared__ int s_any[kBwdThreads];
+  const int g_loc = threadIdx.x % G;
+  const int slot = threadIdx.x / G;
+  const int64_t n = (int64_t)blockIdx.x * G + g_loc;
+  const bool active = slot < CPB && n < N;
   const int T = tw * th;
   float v_m[3] = {0.f, 0.f, 0.f};
-  float v_s[3] = {0.f, 0.f, 0.f};
-  float v_R[9];
+  float v_M[9];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) v_R[k] = 0.f;
+  for (int k = 0; k < 9; ++k) v_M[k] = 0.f;
   float v_col[3] = {0.f, 0.f, 0.f};
   float v_op = 0.f;
-  bool any = false;
-  Geo3D g;
-  for (int c = 0; c < C; ++c) {
-    const int64_t cn = (int64_t)c * N + n;
-    if (isect_count[cn] <= 0) continue;
-    float acc[kPartial];
+  int any = 0;
+  if (active) {
+    const Act3D a = activate3d(params + n * stride);
+    Geo3D g;
+    for (int c = slot; c < C; c += CPB) {
+      const int64_t cn = (int64_t)c * N + n;
+      if (isect_count[cn] <= 0) continue;
+      float acc[kPartial];
 #pragma unroll
-    for (int v = 0; v < kPartial; ++v) acc[v] = 0.f;
-    gather_partials(rect[cn], tw, (int64_t)c * T, sort_key(rec, cn, GSR_ORDER_DEPTH), isect_offset[cn], tile_cut,
-                    partial, acc);
-    const Cam cam = load_cam(viewmats + c * 16, Ks + c * 9);
-    // recompute the forward geometry (not culled: it has intersections)
-    geo3d(a, cam, W, H, 0.f, 3.4e38f, eps2d, g);
-    any = true;
-    v_op += acc[5];
-    v_col[0] += acc[6];
-    v_col[1] += acc[7];
-    v_col[2] += acc[8];
-    // conic (A,B,C) from record (a,b,c) = (A/2, B, C/2)
-    const float vA = 0.5f * acc[2], vB = acc[3], vC = 0.5f * acc[4];
-    // V_cov = -Cinv V_sym Cinv ; Cinv = [[A,B],[B,C]]
-    const float A = g.A, B = g.B, Cc = g.C;
-    const float hb = 0.5f * vB;
-    // X = V_sym Cinv
-    const float X00 = vA * A + hb * B, X01 = vA * B + hb * Cc;
-    const float X10 = hb * A + vC * B, X11 = hb * B + vC * Cc;
-    const float G00 = -(A * X00 + B * X10);
-    const float G01 = -(A * X01 + B * X11);
-    const float G11 = -(B * X01 + Cc * X11);
-    // V_Sc = J^T G J  (J = [[J00,0,J02],[0,J11,J12]])
-    const float J00 = g.J00, J02 = g.J02, J11 = g.J11, J12 = g.J12;
-    float VSc[9];
-    {
-      // G J : 2x3
-      const float GJ00 = G00 * J00, GJ01 = G01 * J11, GJ02 = G00 * J02 + G01 * J12;
-      const float GJ10 = G01 * J00, GJ11 = G11 * J11, GJ12 = G01 * J02 + G11 * J12;
-      // J^T (GJ): 3x3, J^T rows: (J00,0), (0,J11), (J02,J12)
-      VSc[0] = J00 * GJ00;
-      VSc[1] = J00 * GJ01;
-      VSc[2] = J00 * GJ02;
-      VSc[3] = J11 * GJ10;
-      VSc[4] = J11 * GJ11;
-      VSc[5] = J11 * GJ12;
-      VSc[6] = J02 * GJ00 + J12 * GJ10;
-      VSc[7] = J02 * GJ01 + J12 * GJ11;
-      VSc[8] = J02 * GJ02 + J12 * GJ12;
-    }
-    // V_J = 2 G J Sc  (2x3), only the entries J00, J02, J11, J12 matter
-    const float* S = g.Sc;  // s00 s01 s02 s11 s12 s22
-    const float Sf[9] = {S[0], S[1], S[2], S[1], S[3], S[4], S[2], S[4], S[5]};
-    float JS[6];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      JS[k] = J00 * Sf[0 * 3 + k] + J02 * Sf[2 * 3 + k];
-      JS[3 + k] = J11 * Sf[1 * 3 + k] + J12 * Sf[2 * 3 + k];
-    }
-    const float vJ00 = 2.f * (G00 * JS[0] + G01 * JS[3]);
-    const float vJ02 = 2.f * (G00 * JS[2] + G01 * JS[5]);
-    const float vJ11 = 2.f * (G01 * JS[1] + G11 * JS[4]);
-    const float vJ12 = 2.f * (G01 * JS[2] + G11 * JS[5]);
-    // mean_c gradients
-    const float x = g.mc[0], y = g.mc[1];
-    const float rz = g.rz, rz2 = rz * rz, rz3 = rz2 * rz;
-    const float fx = cam.fx, fy = cam.fy;
-    const float vu = acc[0], vv = acc[1];
-    float vmc0 = fx * rz * vu;
-    float vmc1 = fy * rz * vv;
-    float vmc2 = -(fx * x * vu + fy * y * vv) * rz2;
-    vmc2 += -fx * rz2 * vJ00 - fy * rz2 * vJ11;
-    if (g.clx) {
-      vmc0 += -fx * rz2 * vJ02;
-      vmc2 += 2.f * fx * g.tx * rz3 * vJ02;
-    } else {
-      vmc2 += fx * g.tx * rz3 * vJ02;
-    }
-    if (g.cly) {
-      vmc1 += -fy * rz2 * vJ12;
-      vmc2 += 2.f * fy * g.ty * rz3 * vJ12;
-    } else {
-      vmc2 += fy * g.ty * rz3 * vJ12;
-    }
-    const float* Rv = cam.R;
-    // v_m += Rv^T v_mc
-#pragma unroll
-    for (int k = 0; k < 3; ++k) v_m[k] += Rv[0 * 3 + k] * vmc0 + Rv[1 * 3 + k] * vmc1 + Rv[2 * 3 + k] * vmc2;
-    // V_S = Rv^T V_Sc Rv
-    float T1[9];
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-      for (int k = 0; k < 3; ++k)
-        T1[r * 3 + k] = Rv[0 * 3 + r] * VSc[0 * 3 + k] + Rv[1 * 3 + r] * VSc[1 * 3 + k] + Rv[2 * 3 + r] * VSc[2 * 3 + k];
-    float VS[9];
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-      for (int k = 0; k < 3; ++k)
-        VS[r * 3 + k] = T1[r * 3 + 0] * Rv[0 * 3 + k] + T1[r * 3 + 1] * Rv[1 * 3 + k] + T1[r * 3 + 2] * Rv[2 * 3 + k];
-    // V_M = (V_S + V_S^T) M
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
+      for (int v = 0; v < kPartial; ++v) acc[v] = 0.f;
+      gather_partials(rect[cn], tw, (int64_t)c * T, sort_key(rec, cn, GSR_ORDER_DEPTH), isect_offset[cn],
+                      tile_cut, partial, acc);
+      const Cam cam = load_cam(viewmats + c * 16, Ks + c * 9);
+      // recompute the forward geometry (not culled: it has intersections)
+      geo3d(a, cam, W, H, 0.f, 3.4e38f, eps2d, g);
+      any = 1;
+      v_op += acc[5];
+      v_col[0] += acc[6];
+      v_col[1] += acc[7];
+      v_col[2] += acc[8];
+      // conic (A,B,C) from record (a,b,c) = (A/2, B, C/2)
+      const float vA = 0.5f * acc[2], vB = acc[3], vC = 0.5f * acc[4];
+      // V_cov = -Cinv V_sym Cinv ; Cinv = [[A,B],[B,C]]
+      const float A = g.A, B = g.B, Cc = g.C;
+      const float hb = 0.5f * vB;
+      // X = V_sym Cinv
+      const float X00 = vA * A + hb * B, X01 = vA * B + hb * Cc;
+      const float X10 = hb * A + vC * B, X11 = hb * B + vC * Cc;
+      const float G00 = -(A * X00 + B * X10);
+      const float G01 = -(A * X01 + B * X11);
+      const float G11 = -(B * X01 + Cc * X11);
+      // V_Sc = J^T G J  (J = [[J00,0,J02],[0,J11,J12]])
+      const float J00 = g.J00, J02 = g.J02, J11 = g.J11, J12 = g.J12;
+      float VSc[9];
+      {
+        // G J : 2x3
+        const float GJ00 = G00 * J00, GJ01 = G01 * J11, GJ02 = G00 * J02 + G01 * J12;
+        const float GJ10 = G01 * J00, GJ11 = G11 * J11, GJ12 = G01 * J02 + G11 * J12;
+        // J^T (GJ): 3x3, J^T rows: (J00,0), (0,J11), (J02,J12)
+        VSc[0] = J00 * GJ00;
+        VSc[1] = J00 * GJ01;
+        VSc[2] = J00 * GJ02;
+        VSc[3] = J11 * GJ10;
+        VSc[4] = J11 * GJ11;
+        VSc[5] = J11 * GJ12;
+        VSc[6] = J02 * GJ00 + J12 * GJ10;
+        VSc[7] = J02 * GJ01 + J12 * GJ11;
+        VSc[8] = J02 * GJ02 + J12 * GJ12;
+      }
+      // V_J = 2 G J Sc  (2x3), only the entries J00, J02, J11, J12 matter
+      const float* S = g.Sc;  // s00 s01 s02 s11 s12 s22
+      const float Sf[9] = {S[0], S[1], S[2], S[1], S[3], S[4], S[2], S[4], S[5]};
+      float JS[6];
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        float vm = 0.f;
-#pragma unroll
-        for (int l = 0; l < 3; ++l) vm += (VS[r * 3 + l] + VS[l * 3 + r]) * g.M[l * 3 + k];
-        // M = R diag(s)
-        v_R[r * 3 + k] += vm * a.s[k];
-        v_s[k] += vm * g.Rq[r * 3 + k];
+        JS[k] = J00 * Sf[0 * 3 + k] + J02 * Sf[2 * 3 + k];
+        JS[3 + k] = J11 * Sf[1 * 3 + k] + J12 * Sf[2 * 3 + k];
       }
+      const float vJ00 = 2.f * (G00 * JS[0] + G01 * JS[3]);
+      const float vJ02 = 2.f * (G00 * JS[2] + G01 * JS[5]);
+      const float vJ11 = 2.f * (G01 * JS[1] + G11 * JS[4]);
+      const float vJ12 = 2.f * (G01 * JS[2] + G11 * JS[5]);
+      // mean_c gradients
+      const float x = g.mc[0], y = g.mc[1];
+      const float rz = g.rz, rz2 = rz * rz, rz3 = rz2 * rz;
+      const float fx = cam.fx, fy = cam.fy;
+      const float vu = acc[0], vv = acc[1];
+      float vmc0 = fx * rz * vu;
+      float vmc1 = fy * rz * vv;
+      float vmc2 = -(fx * x * vu + fy * y * vv) * rz2;
+      vmc2 += -fx * rz2 * vJ00 - fy * rz2 * vJ11;
+      if (g.clx) {
+        vmc0 += -fx * rz2 * vJ02;
+        vmc2 += 2.f * fx * g.tx * rz3 * vJ02;
+      } else {
+        vmc2 += fx * g.tx * rz3 * vJ02;
+      }
+      if (g.cly) {
+        vmc1 += -fy * rz2 * vJ12;
+        vmc2 += 2.f * fy * g.ty * rz3 * vJ12;
+      } else {
+        vmc2 += fy * g.ty * rz3 * vJ12;
+      }
+      const float* Rv = cam.R;
+      // v_m += Rv^T v_mc
+#pragma unroll
+      for (int k = 0; k < 3; ++k) v_m[k] += Rv[0 * 3 + k] * vmc0 + Rv[1 * 3 + k] * vmc1 + Rv[2 * 3 + k] * vmc2;
+      // V_S = Rv^T V_Sc Rv
+      float T1[9];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          T1[r * 3 + k] = Rv[0 * 3 + r] * VSc[0 * 3 + k] + Rv[1 * 3 + r] * VSc[1 * 3 + k] + Rv[2 * 3 + r] * VSc[2 * 3 + k];
+      float VS[9];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          VS[r * 3 + k] = T1[r * 3 + 0] * Rv[0 * 3 + k] + T1[r * 3 + 1] * Rv[1 * 3 + k] + T1[r * 3 + 2] * Rv[2 * 3 + k];
+      // V_M = (V_S + V_S^T) M   (M = R diag(s); converted to v_R, v_s after the camera sum)
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          float vm = 0.f;
+#pragma unroll
+          for (int l = 0; l < 3; ++l) vm += (VS[r * 3 + l] + VS[l * 3 + r]) * g.M[l * 3 + k];
+          v_M[r * 3 + k] += vm;
+        }
+    }
   }
+  {
+    float* d = s_con[threadIdx.x];
+    d[0] = v_m[0]; d[1] = v_m[1]; d[2] = v_m[2];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) d[3 + k] = v_M[k];
+    d[12] = v_col[0]; d[13] = v_col[1]; d[14] = v_col[2];
+    d[15] = v_op;
+    s_any[threadIdx.x] = any;
+  }
+  __syncthreads();
+  if (slot != 0 || n >= N) return;
+  any = 0;
+  for (int sl = 1; sl < CPB; ++sl) {
+    const float* d = s_con[sl * G + g_loc];
+    v_m[0] += d[0]; v_m[1] += d[1]; v_m[2] += d[2];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) v_M[k] += d[3 + k];
+    v_col[0] += d[12]; v_col[1] += d[13]; v_col[2] += d[14];
+    v_op += d[15];
+    any |= s_any[sl * G + g_loc];
+  }
+  any |= s_any[threadIdx.x];
   float* out = v_params + n * 14;
   if (!any) {
 #pragma unroll
     for (int k = 0; k < 14; ++k) out[k] = 0.f;
     return;
   }
+  const Act3D a = activate3d(params + n * stride);
+  // M = R diag(s):  v_R = V_M diag(s),  v_s = sum_r V_M[r][k] R[r][k]
+  float Rq[9], qn[4], qinv;
+  quat_rotmat(a.q, Rq, qn, &qinv);
+  float v_R[9], v_s[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      v_R[r * 3 + k] = v_M[r * 3 + k] * a.s[k];
+      v_s[k] += v_M[r * 3 + k] * Rq[r * 3 + k];
+    }
   // R(qn) → v_qn (normalised quaternion)
-  const float w = g.qn[0], x = g.qn[1], y = g.qn[2], z = g.qn[3];
+  const float w = qn[0], x = qn[1], y = qn[2], z = qn[3];
   const float* V = v_R;
   float vq[4];
   vq[0] = 2.f * (z * (V[3] - V[1]) + y * (V[2] - V[6]) + x * (V[7] - V[5]));
@@ -184,8 +242,8 @@ __global__ __launch_bounds__(kBwdThreads) void k_project3d_bwd(
   vq[3] = 2.f * (-2.f * z * V[0] - w * V[1] + x * V[2] + w * V[3] - 2.f * z * V[4] + y * V[5] + x * V[6] + y * V[7]);
   // gsplat normalisation vjp: v_qa = (vq - (vq.qn) qn) / |qa|
   const float dqn = vq[0] * w + vq[1] * x + vq[2] * y + vq[3] * z;
-  float vqa[4] = {(vq[0] - dqn * w) * g.qinv, (vq[1] - dqn * x) * g.qinv, (vq[2] - dqn * y) * g.qinv,
-                  (vq[3] - dqn * z) * g.qinv};
+  float vqa[4] = {(vq[0] - dqn * w) * qinv, (vq[1] - dqn * x) * qinv, (vq[2] - dqn * y) * qinv,
+                  (vq[3] - dqn * z) * qinv};
   // adapter: qa = q / (r + 1e-8), r = |q|:  v_q = v_qa/(r+eps) - q (q.v_qa) / (r (r+eps)^2)
   const float den = a.rq + 1e-8f;
   const float qdot = a.qraw[0] * vqa[0] + a.qraw[1] * vqa[1] + a.qraw[2] * vqa[2] + a.qraw[3] * vqa[3];
@@ -254,9 +312,11 @@ int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride, const 
   GSR_REQUIRE(row_stride >= 14, "gsr3d_project_bwd: row_stride < 14");
   if (N == 0) return GSR_OK;
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
-  hipLaunchKernelGGL(k_project3d_bwd, dim3(ceil_div(N, kBwdThreads)), dim3(kBwdThreads), 0, (hipStream_t)stream,
-                     params, N, row_stride, viewmats, Ks, C, width, height, eps2d, tw, th, (const uint2*)rect,
-                     isect_offset, isect_count, (const Splat*)rec, tile_cut, partial, v_params);
+  const int CPB = C < kBwdThreads ? C : kBwdThreads;   // camera slots per Gaussian
+  const int G = kBwdThreads / CPB;                       // Gaussians per workgroup
+  hipLaunchKernelGGL(k_project3d_bwd, dim3(ceil_div(N, G)), dim3(kBwdThreads), 0, (hipStream_t)stream, params, N,
+                     row_stride, viewmats, Ks, C, width, height, eps2d, tw, th, (const uint2*)rect, isect_offset,
+                     isect_count, (const Splat*)rec, tile_cut, partial, CPB, G, v_params);
   GSR_LAUNCH_CHECK("k_project3d_bwd");
   return GSR_OK;
 }

@@ -42,22 +42,29 @@ __device__ __forceinline__ void tile_coords(int ct, int tw, int th, int& c, int&
 // ---------------------------------------------------------------- per-wave culling
 // A wave owns an 8x8 sub-tile of its 16x16 tile.  An entry can only change a pixel of the
 // sub-tile if its level set {opacity*exp(-sigma) >= cut} (3D: cut = 1/255, gsplat's skip
-// threshold; 2D: eps_cut) meets the sub-tile's pixel-centre box.  The test uses that
-// ellipse's axis-aligned extent (inflated by a small margin), so it never drops an entry
-// the per-pixel test would keep: culling changes the work, not the result.
+// threshold; 2D: eps_cut) meets the sub-tile's pixel-centre box B, i.e. iff
+// min over B of sigma <= L = ln(opacity/cut).  That minimum is computed exactly: sigma is a
+// convex quadratic with its minimum at the mean, so when the mean lies outside B the
+// minimiser lies on an edge of B facing the mean, and along an edge the best point is the
+// clamped 1-D optimum.  With dx fixed to the mean's nearest x in B, the best dy is
+// clamp(-b dx / 2c); likewise for y; the smaller of the two values is the box minimum (the
+// non-facing "edge" evaluates a segment inside B, never below the true minimum).  A small
+// relative margin absorbs rounding, so culling changes the work, never the result.
 template <bool IS2D>
 __device__ __forceinline__ bool cull_keep(const float4 p0, const float4 p1, float bx0, float bx1, float by0,
                                           float by1, float cut) {
   const float ratio = IS2D ? p0.z / cut : p0.z * 255.f;
   if (!(ratio >= 1.f)) return false;
-  // approximate v_log / v_rcp / v_sqrt (~1 ulp) — the 0.1% + 0.01 px margin absorbs them
-  const float L = __builtin_amdgcn_logf(ratio) * 0.69320154f + 1e-4f;   // ln2 * 1.0001
-  const float det = p1.x * p1.z - 0.25f * p1.y * p1.y;
-  if (!(det > 0.f)) return true;
-  const float id = __builtin_amdgcn_rcpf(det);
-  const float hx = __builtin_amdgcn_sqrtf(L * p1.z * id) * 1.001f + 0.01f;
-  const float hy = __builtin_amdgcn_sqrtf(L * p1.x * id) * 1.001f + 0.01f;
-  return (p0.x + hx >= bx0) && (p0.x - hx <= bx1) && (p0.y + hy >= by0) && (p0.y - hy <= by1);
+  const float a = p1.x, b = p1.y, c = p1.z;
+  if (!(a > 0.f && c > 0.f && 4.f * a * c > b * b)) return true;   // not positive definite: keep
+  const float L = __builtin_amdgcn_logf(ratio) * 0.69314718f;      // v_log is log2
+  const float dxe = p0.x - fminf(fmaxf(p0.x, bx0), bx1);
+  const float dye = p0.y - fminf(fmaxf(p0.y, by0), by1);
+  const float dy1 = fminf(fmaxf(-b * dxe * __builtin_amdgcn_rcpf(2.f * c), p0.y - by1), p0.y - by0);
+  const float dx2 = fminf(fmaxf(-b * dye * __builtin_amdgcn_rcpf(2.f * a), p0.x - bx1), p0.x - bx0);
+  const float s1 = a * dxe * dxe + b * dxe * dy1 + c * dy1 * dy1;
+  const float s2 = a * dx2 * dx2 + b * dx2 * dye + c * dye * dye;
+  return fminf(s1, s2) <= L * 1.001f + 1e-3f;
 }
 
 struct SubTile {
