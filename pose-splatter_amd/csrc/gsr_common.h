@@ -59,7 +59,7 @@ inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 template <int CTRL>
 __device__ __forceinline__ float dpp_mov(float v) {
   return __builtin_bit_cast(
-      float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
 }
 
 __device__ __forceinline__ float readlane_f(float v, int lane) {
@@ -88,37 +88,47 @@ __device__ __forceinline__ float wave_sum(float v) {
 // issued as inline asm.  Hardware semantics (verified on MI355X, tools/diag_lanes.hip):
 //   v_permlane32_swap a, b:  a' = [a_lo32, b_lo32],  b' = [a_hi32, b_hi32]
 //   v_permlane16_swap a, b:  a' = [a_r0, b_r0, a_r2, b_r2],  b' = [a_r1, b_r1, a_r3, b_r3]
-// The s_nop 1 covers the VALU-write -> permlane-read hazard the compiler cannot see in asm.
-__device__ __forceinline__ float2 swap32(float a, float b) {
-  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-  return make_float2(a, b);
+// The swaps of one level are issued 8 pairs per asm block behind ONE s_nop 1, which covers
+// the VALU-write -> permlane-read hazard the compiler cannot see in asm (the swaps inside a
+// block read only registers no other swap of the block writes).
+#define GSR_SWAP8(OP)                                                                          \
+  asm(OP " %0, %8\n\t" OP " %1, %9\n\t" OP " %2, %10\n\t" OP " %3, %11\n\t" OP " %4, %12\n\t" \
+      OP " %5, %13\n\t" OP " %6, %14\n\t" OP " %7, %15"                                        \
+      : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]), "+v"(lo[3]), "+v"(lo[4]), "+v"(lo[5]), "+v"(lo[6]),   \
+        "+v"(lo[7]), "+v"(hi[0]), "+v"(hi[1]), "+v"(hi[2]), "+v"(hi[3]), "+v"(hi[4]), "+v"(hi[5]),   \
+        "+v"(hi[6]), "+v"(hi[7]))
+__device__ __forceinline__ void swap32x8(float* lo, float* hi) {
+  asm("s_nop 1");
+  GSR_SWAP8("v_permlane32_swap_b32");
 }
-__device__ __forceinline__ float2 swap16(float a, float b) {
-  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-  return make_float2(a, b);
+__device__ __forceinline__ void swap16x8(float* lo, float* hi) {
+  asm("s_nop 1");
+  GSR_SWAP8("v_permlane16_swap_b32");
 }
+#undef GSR_SWAP8
 
+// Intra-row level: a lane in the upper half (of the row / half-row / quad pair) keeps the
+// `hi` register, one in the lower half keeps `lo`; each adds its partner's copy of the same
+// register (DPP), so out = upper ? hi + dpp(hi) : lo + dpp(lo).
 template <int CTRL>
 __device__ __forceinline__ float pair_level(float lo, float hi, bool upper) {
-  const float keep = upper ? hi : lo;
-  const float send = upper ? lo : hi;
-  return keep + dpp_mov<CTRL>(send);
+  const float l = lo + dpp_mov<CTRL>(lo);
+  const float h = hi + dpp_mov<CTRL>(hi);
+  return upper ? h : l;
 }
 
 __device__ __forceinline__ float reduce64(float (&v)[64]) {
   const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) swap32x8(&v[8 * g], &v[32 + 8 * g]);
   float a[32];
 #pragma unroll
-  for (int i = 0; i < 32; ++i) {
-    const float2 r = swap32(v[i], v[i + 32]);
-    a[i] = r.x + r.y;
-  }
+  for (int i = 0; i < 32; ++i) a[i] = v[i] + v[i + 32];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) swap16x8(&a[8 * g], &a[16 + 8 * g]);
   float b[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const float2 r = swap16(a[i], a[i + 16]);
-    b[i] = r.x + r.y;
-  }
+  for (int i = 0; i < 16; ++i) b[i] = a[i] + a[i + 16];
   float c[8];
   const bool b3 = (lane & 8) != 0, b2 = (lane & 4) != 0, b1 = (lane & 2) != 0, b0 = (lane & 1) != 0;
 #pragma unroll
