@@ -91,7 +91,7 @@ int gsr_selftest_reduce64(float* out, void* stream);
 /* 3D projection (+ adapter activations fused).  params: [N, >=14] fp32 rows with
  * row_stride floats (layout src/gaussian_renderer.py:183-187); viewmats [C,4,4] world->cam
  * row-major; Ks [C,3,3].  Writes rec [C*N*12], rect [C*N*2], isect_count [C*N] and
- * ACCUMULATES into tile_count [C*tiles] (caller zeroes it).  Culled Gaussians get count 0. */
+ * writes tile_count [C*tiles] (zeroed, then accumulated).  Culled Gaussians get count 0. */
 int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride,
                       const float* viewmats, const float* Ks, int C, int width, int height,
                       float near_plane, float far_plane, float radius_clip, float eps2d,
@@ -122,7 +122,8 @@ int gsr_bin_offsets(const int32_t* isect_count, int64_t CN, const int32_t* tile_
 /* Workspace for gsr_bin_sort, bytes (depends on the I read back from stats). */
 size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT);
 
-/* Emit (tile, key) pairs and sort each tile's list in LDS.  Outputs:
+/* Emit (tile, key) pairs and sort each tile's list in LDS.  tile_count (the projection's
+ * per-tile counts) is consumed: it is counted down to zero while slots are claimed.  Outputs:
  *   sorted_ids [I]: c*N+n per sorted entry (what the rasterizer reads),
  *   k_of_s     [I]: the emission entry k = isect_offset[cn]+j of each sorted entry (j =
  *                   row-major index of the tile in the Gaussian's rect): where the raster
@@ -130,7 +131,8 @@ size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT);
  * Sort key per entry: (sort word << 32) | c*N+n, sort word = depth float bits (3D, order
  * GSR_ORDER_DEPTH) or c*N+n (2D, GSR_ORDER_INDEX).  max_seg/n_busy from stats. */
 int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_offset,
-                 const int32_t* tile_offset, const int32_t* busy_tiles, int C, int64_t N,
+                 const int32_t* tile_offset, int32_t* tile_count,
+                 const int32_t* busy_tiles, int C, int64_t N,
                  int width, int height, int order, int64_t n_isect, int32_t max_seg,
                  int32_t n_busy, void* workspace, size_t workspace_bytes,
                  int32_t* sorted_ids, int32_t* k_of_s, void* stream);

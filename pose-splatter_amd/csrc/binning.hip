@@ -144,12 +144,17 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(const int32_t* __rest
 // ---------------------------------------------------------------- emission
 __global__ __launch_bounds__(kEmitThreads) void k_emit(const Splat* __restrict__ rec, const uint2* __restrict__ rect,
                                                       const int32_t* __restrict__ isect_offset, int64_t N, int tw,
-                                                      int th, int order, int use_lds, int32_t* __restrict__ cursor,
-                                                      uint64_t* __restrict__ keys, int32_t* __restrict__ k_of_slot) {
+                                                      int th, int order, int use_lds,
+                                                      const int32_t* __restrict__ tile_offset,
+                                                      int32_t* __restrict__ tile_count, uint64_t* __restrict__ keys,
+                                                      int32_t* __restrict__ k_of_slot) {
+  // Slots are claimed by counting each tile's count down to zero (slot = tile start +
+  // remaining count - 1): no separate cursor array, and tile_count is left zeroed.
   extern __shared__ int hist[];
   const int c = blockIdx.y;
   const int T = tw * th;
-  int32_t* gcur = cursor + (int64_t)c * T;
+  int32_t* gcnt = tile_count + (int64_t)c * T;
+  const int32_t* toff = tile_offset + (int64_t)c * T;
   const int64_t n0 = (int64_t)blockIdx.x * kEmitPerBlock;
   const int64_t n1 = min(N, n0 + kEmitPerBlock);
   if (use_lds) {
@@ -164,7 +169,7 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const Splat* __restrict__
     __syncthreads();
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
       const int v = hist[t];
-      if (v) hist[t] = atomicAdd(&gcur[t], v);
+      if (v) hist[t] = toff[t] + atomicSub(&gcnt[t], v) - v;
     }
     __syncthreads();
   }
@@ -178,7 +183,7 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const Splat* __restrict__
     for (int ty = y0; ty < y1; ++ty)
       for (int tx = x0; tx < x1; ++tx) {
         const int t = ty * tw + tx;
-        const int slot = use_lds ? atomicAdd(&hist[t], 1) : atomicAdd(&gcur[t], 1);
+        const int slot = use_lds ? atomicAdd(&hist[t], 1) : toff[t] + atomicSub(&gcnt[t], 1) - 1;
         keys[slot] = key;
         k_of_slot[slot] = k++;
       }
@@ -424,13 +429,13 @@ int gsr_bin_offsets(const int32_t* isect_count, int64_t CN, const int32_t* tile_
 }
 
 size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT) {
-  // keys [I] + merge keys [I] (u64), two merge payloads [I] + k_of_slot [I] (i32), cursor [CT]
-  return (size_t)(2 * n_isect * sizeof(uint64_t) + 3 * n_isect * sizeof(int32_t) + (CT + 64) * sizeof(int32_t) +
-                  256);
+  // keys [I] + merge keys [I] (u64), two merge payloads [I] + k_of_slot [I] (i32)
+  (void)CT;
+  return (size_t)(2 * n_isect * sizeof(uint64_t) + 3 * n_isect * sizeof(int32_t) + 256);
 }
 
 int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_offset, const int32_t* tile_offset,
-                 const int32_t* busy_tiles, int C, int64_t N, int width, int height, int order, int64_t n_isect,
+                 int32_t* tile_count, const int32_t* busy_tiles, int C, int64_t N, int width, int height, int order, int64_t n_isect,
                  int32_t max_seg, int32_t n_busy, void* workspace, size_t workspace_bytes, int32_t* sorted_ids,
                  int32_t* k_of_s, void* stream) {
   GSR_REQUIRE(order == GSR_ORDER_DEPTH || order == GSR_ORDER_INDEX, "gsr_bin_sort: bad order %d", order);
@@ -447,15 +452,11 @@ int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_of
   int32_t* tmpp0 = (int32_t*)(tmpk + n_isect);
   int32_t* tmpp1 = tmpp0 + n_isect;
   int32_t* k_of_slot = tmpp1 + n_isect;
-  int32_t* cursor = k_of_slot + n_isect;
-  if (hipMemcpyAsync(cursor, tile_offset, CT * sizeof(int32_t), hipMemcpyDeviceToDevice, s) != hipSuccess) {
-    set_error("gsr_bin_sort: cursor copy failed");
-    return GSR_ELAUNCH;
-  }
   const int use_lds = T <= kHistMaxTiles;
   dim3 grid(ceil_div(N, kEmitPerBlock), C);
   hipLaunchKernelGGL(k_emit, grid, dim3(kEmitThreads), use_lds ? T * sizeof(int) : 0, s, (const Splat*)rec,
-                     (const uint2*)rect, isect_offset, N, tw, th, order, use_lds, cursor, keys, k_of_slot);
+                     (const uint2*)rect, isect_offset, N, tw, th, order, use_lds, tile_offset, tile_count, keys,
+                     k_of_slot);
   GSR_LAUNCH_CHECK("k_emit");
   if (n_busy > 0) {
     int lds_keys = 1024;

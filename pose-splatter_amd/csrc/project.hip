@@ -190,6 +190,10 @@ int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride, const 
               "gsr3d_project_fwd: bad radius_mode %d", radius_mode);
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   GSR_REQUIRE(tw < 65536 && th < 65536, "gsr3d_project_fwd: image too large");
+  if (hipMemsetAsync(tile_count, 0, (size_t)C * tw * th * sizeof(int32_t), (hipStream_t)stream) != hipSuccess) {
+    set_error("gsr3d_project_fwd: tile_count memset failed");
+    return GSR_ELAUNCH;
+  }
   if (N == 0) return GSR_OK;
   const int T = tw * th;
   const int use_lds = T <= kHistMaxTiles;
@@ -219,6 +223,10 @@ int gsr2d_project_fwd(const float* params, int64_t N, int64_t row_stride, int wi
   GSR_REQUIRE(eps_cut > 0.f && eps_cut < 1.f, "gsr2d_project_fwd: eps_cut must be in (0,1)");
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   GSR_REQUIRE(tw < 65536 && th < 65536, "gsr2d_project_fwd: image too large");
+  if (hipMemsetAsync(tile_count, 0, (size_t)tw * th * sizeof(int32_t), (hipStream_t)stream) != hipSuccess) {
+    set_error("gsr2d_project_fwd: tile_count memset failed");
+    return GSR_ELAUNCH;
+  }
   if (N == 0) return GSR_OK;
   const int T = tw * th;
   const int use_lds = T <= kHistMaxTiles;

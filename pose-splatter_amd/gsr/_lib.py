@@ -56,7 +56,7 @@ EXPORTS = {
     "gsr_bin_offsets_workspace": (_SZ, [_I64, _I64]),
     "gsr_bin_offsets": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _SZ, _P, _P, _P, _P, _P, _P]),
     "gsr_bin_sort_workspace": (_SZ, [_I64, _I64]),
-    "gsr_bin_sort": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I32, _I64, _I32,
+    "gsr_bin_sort": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I32, _I64, _I32,
                                     _I32, _P, _SZ, _P, _P, _P]),
     "gsr3d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _I32, _P, _P, _P, _P,
                                         _P, _P, _P, _P, _P, _P, _P]),

@@ -4,8 +4,9 @@
 parameters (the same tensor ``GaussianRenderer.render`` receives,
 src/gaussian_renderer.py:157-211 and :269-334).  All device memory comes from PyTorch's
 caching allocator; every libgsr call is enqueued on ``torch.cuda.current_stream()``.
-The one host synchronisation per forward is the 16-byte ``gsr_bin_stats`` read that
-sizes the intersection buffers (gsplat reads its intersection count the same way).
+The one host synchronisation per forward is the ``gsr_bin_stats`` read (into pinned host
+memory) that sizes the intersection buffers (gsplat reads its intersection count the same
+way).  Intermediates live in two arenas per forward (see ``_Arena``).
 """
 from __future__ import annotations
 
@@ -57,12 +58,16 @@ class RenderOptions3D:
 
 _last_stats = {}
 _timers = None   # name -> [(start_event, end_event)] while kernel timing is enabled
+_timed_only = None
 
 
-def enable_kernel_timing(enabled: bool = True) -> None:
-    """Bracket each libgsr launch with CUDA(HIP) events on the current stream (bench.py)."""
-    global _timers
+def enable_kernel_timing(enabled: bool = True, only=None) -> None:
+    """Bracket libgsr launches with CUDA(HIP) events on the current stream (bench.py).
+    ``only``: a set of call names to time (default: all).  Every event record is a packet
+    on the stream, so time only what is needed inside a measured region."""
+    global _timers, _timed_only
     _timers = {} if enabled else None
+    _timed_only = set(only) if only else None
 
 
 def kernel_times_ms() -> dict:
@@ -78,15 +83,16 @@ class _timed:
 
     def __init__(self, name):
         self.name = name
+        self.s = None
 
     def __enter__(self):
-        if _timers is not None:
+        if _timers is not None and (_timed_only is None or self.name in _timed_only):
             self.s = torch.cuda.Event(enable_timing=True)
             self.s.record()
         return self
 
     def __exit__(self, *exc):
-        if _timers is not None:
+        if self.s is not None:
             e = torch.cuda.Event(enable_timing=True)
             e.record()
             _timers.setdefault(self.name, []).append((self.s, e))
@@ -98,76 +104,165 @@ def last_stats() -> dict:
     return dict(_last_stats)
 
 
+class _Arena:
+    """One device allocation carved into 256-byte-aligned sub-buffers.
+
+    The hot path only needs raw pointers (``ptr``), so a forward costs one caching-allocator
+    call per arena instead of one per buffer; typed tensor views are built on demand."""
+
+    def __init__(self, device, spec: dict):
+        self.off = {}
+        total = 0
+        for name, nbytes in spec.items():
+            self.off[name] = (total, int(nbytes))
+            total += (int(nbytes) + 255) // 256 * 256
+        self.buf = torch.empty(max(total, 256), device=device, dtype=torch.uint8)
+        base = self.buf.data_ptr()
+        self.ptr = {name: base + o for name, (o, _) in self.off.items()}
+
+    def view(self, name, dtype, count=None):
+        o, n = self.off[name]
+        t = self.buf[o:o + n].view(dtype)
+        return t if count is None else t[:count]
+
+
+_I32, _I64, _F32 = torch.int32, torch.int64, torch.float32
+# tensor views exposed for tests / debugging: name -> (arena attribute, dtype)
+_VIEWS = {"rec": ("pre", _F32), "rect": ("pre", _I32), "cnt": ("pre", _I32), "tile_cnt": ("pre", _I32),
+          "isect_off": ("pre", _I32), "tile_off": ("pre", _I32), "busy": ("pre", _I32),
+          "chunk_base": ("pre", _I32), "stats_dev": ("pre", _I32),
+          "sorted_ids": ("post", _I32), "k_of_s": ("post", _I32), "final_T": ("post", _F32),
+          "last": ("post", _I32), "tile_end": ("post", _I32), "tile_cut": ("post", _I64),
+          "chunk_state": ("post", _F32), "chunk_tile": ("post", _I32), "chunk_list": ("post", _I32)}
+
+_pinned = {}
+_size_hint = {}   # (device, C, N, W, H) -> (I, n_chunks) of the last forward of that shape
+_bg_cache = {}
+
+
+def _pinned_stats(device) -> torch.Tensor:
+    t = _pinned.get(device)
+    if t is None:
+        t = _pinned[device] = torch.empty(8, dtype=torch.int32, pin_memory=True)
+    return t
+
+
 class _Bins:
-    """Per-call intermediates shared by forward and backward (all device tensors)."""
+    """Per-call intermediates shared by forward and backward: two arenas, one sized before
+    the stats readback (per-Gaussian and per-tile buffers) and one after it (per-intersection
+    buffers)."""
 
     def __init__(self, device, C, N, width, height):
+        self.device = device
         self.C, self.N, self.W, self.H = C, N, width, height
         self.tw = (width + _TILE - 1) // _TILE
         self.th = (height + _TILE - 1) // _TILE
         self.CT = C * self.tw * self.th
-        CN = C * N
-        i32 = dict(device=device, dtype=torch.int32)
-        self.rec = torch.empty(max(CN, 1) * 12, device=device, dtype=torch.float32)
-        self.rect = torch.empty(max(CN, 1) * 2, **i32)
-        self.cnt = torch.empty(max(CN, 1), **i32)
-        self.tile_cnt = torch.zeros(self.CT, **i32)
-        self.isect_off = torch.empty(max(CN, 1), **i32)
-        self.tile_off = torch.empty(self.CT + 1, **i32)
-        self.busy = torch.empty(self.CT, **i32)
-        self.chunk_base = torch.empty(self.CT + 1, **i32)
-        self.stats_dev = torch.zeros(8, **i32)   # gsr_bin_stats (32 B)
-        self.n_chunks = 0
-        self.n_isect = 0
-        self.max_seg = 0
-        self.n_busy = 0
+        CN = max(C * N, 1)
+        L = lib()
+        self.pre = _Arena(device, {
+            "rec": CN * 48, "rect": CN * 8, "cnt": CN * 4, "tile_cnt": self.CT * 4, "isect_off": CN * 4,
+            "tile_off": (self.CT + 1) * 4, "busy": self.CT * 4, "chunk_base": (self.CT + 1) * 4,
+            "stats_dev": 32, "offsets_ws": int(L.gsr_bin_offsets_workspace(C * N, self.CT))})
+        self.p = dict(self.pre.ptr)
+        self.post = None
+        self.n_chunks = self.n_isect = self.max_seg = self.n_busy = 0
+        self.key = (str(device), C, N, width, height)
+
+    def guess_post(self, with_chunks: bool):
+        """Before the stats readback: size the per-intersection arena from the last call with
+        the same shapes (plus 25 %), so its allocation overlaps the GPU's projection/scan."""
+        hint = _size_hint.get(self.key)
+        if hint is not None:
+            self.alloc_post(with_chunks, int(hint[0] * 1.25) + 1024, int(hint[1] * 1.25) + 16)
+
+    def __getattr__(self, name):
+        # typed views of arena buffers (not used on the hot path)
+        if name in _VIEWS:
+            where, dt = _VIEWS[name]
+            arena = self.__dict__.get(where)
+            if arena is not None:
+                return arena.view(name, dt)
+        raise AttributeError(name)
 
     def offsets(self, stream):
         L = lib()
+        p = self.p
         CN = self.C * self.N
-        ws = torch.empty(int(L.gsr_bin_offsets_workspace(CN, self.CT)), device=self.rec.device,
-                         dtype=torch.uint8)
         with _timed("bin_offsets"):
-          check(L.gsr_bin_offsets(_ptr(self.cnt), CN, _ptr(self.tile_cnt), self.CT, _ptr(ws), ws.numel(),
-                                _ptr(self.isect_off), _ptr(self.tile_off), _ptr(self.chunk_base),
-                                _ptr(self.busy), _ptr(self.stats_dev), stream), "gsr_bin_offsets")
-        st = self.stats_dev.cpu()   # the one D2H sync of the forward
-        self.n_isect = (int(st[0]) & 0xFFFFFFFF) | (int(st[1]) << 32)
-        self.max_seg = int(st[2])
-        self.n_busy = int(st[3])
-        self.n_chunks = int(st[4])
+          check(L.gsr_bin_offsets(p["cnt"], CN, p["tile_cnt"], self.CT, p["offsets_ws"],
+                                self.pre.off["offsets_ws"][1], p["isect_off"], p["tile_off"],
+                                p["chunk_base"], p["busy"], p["stats_dev"], stream), "gsr_bin_offsets")
+        host = _pinned_stats(self.device)
+        host.copy_(self.pre.view("stats_dev", _I32), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        while not ev.query():   # the one host sync of the forward (spin: lowest wake-up latency)
+            pass
+        st = host.tolist()
+        self.n_isect = (st[0] & 0xFFFFFFFF) | (st[1] << 32)
+        self.max_seg, self.n_busy, self.n_chunks = st[2], st[3], st[4]
         if self.n_isect >= 2 ** 31:
             raise RuntimeError(f"gsr: {self.n_isect} intersections exceed the 32-bit index range")
 
+    def alloc_post(self, with_chunks: bool, n_isect: int, n_chunks: int):
+        L = lib()
+        I = max(n_isect, 1)
+        P = self.C * self.W * self.H
+        K = max(n_chunks, 1) if with_chunks else 1
+        self.post = _Arena(self.device, {
+            "sorted_ids": I * 4, "k_of_s": I * 4, "sort_ws": int(L.gsr_bin_sort_workspace(I, self.CT)),
+            "final_T": P * 4, "last": P * 4, "tile_end": self.CT * 4, "tile_cut": self.CT * 8,
+            "chunk_state": K * 256 * 16, "chunk_tile": K * 4, "chunk_list": K * 4})
+        self.post_cap = (I, K)
+        self.p.update(self.post.ptr)
+
+    def ensure_post(self, with_chunks: bool):
+        """After the stats readback: keep the speculatively sized arena if it is big enough."""
+        I, K = self.post_cap if self.post is not None else (0, 0)
+        if self.n_isect > I or (with_chunks and self.n_chunks > K):
+            self.alloc_post(with_chunks, int(self.n_isect * 1.25), int(self.n_chunks * 1.25))
+        _size_hint[self.key] = (self.n_isect, self.n_chunks)
+
     def sort(self, order, stream):
         L = lib()
-        dev = self.rec.device
-        I = self.n_isect
-        self.sorted_ids = torch.empty(max(I, 1), device=dev, dtype=torch.int32)
-        self.k_of_s = torch.empty(max(I, 1), device=dev, dtype=torch.int32)
-        ws = torch.empty(int(L.gsr_bin_sort_workspace(I, self.CT)), device=dev, dtype=torch.uint8)
+        p = self.p
         with _timed("bin_sort"):
-          check(L.gsr_bin_sort(_ptr(self.rec), _ptr(self.rect), _ptr(self.isect_off), _ptr(self.tile_off),
-                             _ptr(self.busy), self.C, self.N, self.W, self.H, order, I, self.max_seg,
-                             self.n_busy, _ptr(ws), ws.numel(), _ptr(self.sorted_ids), _ptr(self.k_of_s),
-                             stream), "gsr_bin_sort")
+          check(L.gsr_bin_sort(p["rec"], p["rect"], p["isect_off"], p["tile_off"], p["tile_cnt"], p["busy"],
+                             self.C, self.N,
+                             self.W, self.H, order, self.n_isect, self.max_seg, self.n_busy, p["sort_ws"],
+                             self.post.off["sort_ws"][1], p["sorted_ids"], p["k_of_s"], stream), "gsr_bin_sort")
 
 
 def _record_stats(b: _Bins):
     _last_stats.clear()
     _last_stats.update(n_isect=b.n_isect, max_seg=b.max_seg, n_busy=b.n_busy, tiles=b.CT)
-    _last_stats["_tile_end"] = b.tile_end
-    _last_stats["_tile_off"] = b.tile_off
+    _last_stats["_bins"] = b
 
 
 def effective_isect(stats: dict | None = None) -> int:
     """I_eff = sum over tiles of (tile_end - start): list entries the raster actually read."""
     s = _last_stats if stats is None else stats
-    if "_tile_end" not in s:
+    if "_bins" not in s:
         return 0
-    te = s["_tile_end"].to(torch.int64)
-    st = s["_tile_off"][:-1].to(torch.int64)
+    te = s["_bins"].tile_end.to(torch.int64)
+    st = s["_bins"].tile_off[:-1].to(torch.int64)
     return int((te - st).clamp(min=0).sum())
+
+
+def _background(bg: torch.Tensor, C: int, dev) -> torch.Tensor:
+    """bg [3] or [C,3] -> contiguous float32 [C,3] on dev (expanded copies are cached per
+    source tensor version, so a fixed background costs no kernel per call)."""
+    b = bg.detach()
+    if b.device == dev and b.dtype == torch.float32 and b.is_contiguous() and b.numel() == 3 * C:
+        return b.reshape(C, 3)
+    key = (b.data_ptr(), b._version, tuple(b.shape), C, str(dev))
+    hit = _bg_cache.get(key)
+    if hit is None:
+        if len(_bg_cache) > 64:
+            _bg_cache.clear()
+        hit = _bg_cache[key] = b.to(device=dev, dtype=torch.float32).reshape(-1, 3).expand(C, 3).contiguous()
+    return hit
 
 
 def _forward3d(params, viewmats, Ks, bg, width, height, opts):
@@ -180,30 +275,25 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
     p, stride = _rows(params, 14)
     V = viewmats.detach().to(device=dev, dtype=torch.float32).contiguous()
     Kc = Ks.detach().to(device=dev, dtype=torch.float32).contiguous()
-    bgc = bg.detach().to(device=dev, dtype=torch.float32).reshape(-1, 3).expand(C, 3).contiguous()
+    bgc = _background(bg, C, dev)
     b = _Bins(dev, C, N, width, height)
-    if N > 0:
-        with _timed("project3d_fwd"):
-          check(L.gsr3d_project_fwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height,
-                                  opts.near_plane, opts.far_plane, opts.radius_clip, opts.eps2d,
-                                  opts.radius_mode, _ptr(b.rec), _ptr(b.rect), _ptr(b.cnt),
-                                  _ptr(b.tile_cnt), stream), "gsr3d_project_fwd")
+    q = b.p
+    with _timed("project3d_fwd"):
+      check(L.gsr3d_project_fwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height,
+                              opts.near_plane, opts.far_plane, opts.radius_clip, opts.eps2d,
+                              opts.radius_mode, q["rec"], q["rect"], q["cnt"], q["tile_cnt"], stream),
+          "gsr3d_project_fwd")
+    b.guess_post(with_chunks=True)
     b.offsets(stream)
+    b.ensure_post(with_chunks=True)
     b.sort(_lib.ORDER_DEPTH, stream)
     rgb = torch.empty(C, height, width, 3, device=dev, dtype=torch.float32)
     alpha = torch.empty(C, height, width, device=dev, dtype=torch.float32)
-    b.final_T = torch.empty(C, height, width, device=dev, dtype=torch.float32)
-    b.last = torch.empty(C, height, width, device=dev, dtype=torch.int32)
-    b.tile_end = torch.empty(b.CT, device=dev, dtype=torch.int32)
-    b.tile_cut = torch.empty(b.CT, device=dev, dtype=torch.int64)
-    b.chunk_state = torch.empty(max(b.n_chunks, 1) * 256 * 4, device=dev, dtype=torch.float32)
-    b.chunk_tile = torch.empty(max(b.n_chunks, 1), device=dev, dtype=torch.int32)
-    b.chunk_list = torch.empty(max(b.n_chunks, 1), device=dev, dtype=torch.int32)
     with _timed("raster3d_fwd"):
-      check(L.gsr3d_raster_fwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), _ptr(b.busy), _ptr(b.chunk_base),
-                             C, width, height, _ptr(bgc), b.n_busy, _ptr(b.stats_dev), _ptr(rgb), _ptr(alpha),
-                             _ptr(b.final_T), _ptr(b.last), _ptr(b.tile_end), _ptr(b.tile_cut), _ptr(b.chunk_state),
-                             _ptr(b.chunk_tile), _ptr(b.chunk_list), stream), "gsr3d_raster_fwd")
+      check(L.gsr3d_raster_fwd(q["rec"], q["sorted_ids"], q["tile_off"], q["busy"], q["chunk_base"],
+                             C, width, height, _ptr(bgc), b.n_busy, q["stats_dev"], _ptr(rgb), _ptr(alpha),
+                             q["final_T"], q["last"], q["tile_end"], q["tile_cut"], q["chunk_state"],
+                             q["chunk_tile"], q["chunk_list"], stream), "gsr3d_raster_fwd")
     _record_stats(b)
     return rgb, alpha, b, (p, stride, V, Kc, bgc, width, height, opts)
 
@@ -214,21 +304,21 @@ def _forward2d(params, bg, width, height, eps_cut):
     stream = _stream(dev)
     N = params.shape[0]
     p, stride = _rows(params, 9)
-    bgc = bg.detach().to(device=dev, dtype=torch.float32).reshape(1, 3).contiguous()
+    bgc = _background(bg, 1, dev)
     b = _Bins(dev, 1, N, width, height)
+    q = b.p
     with _timed("project2d_fwd"):
-      check(L.gsr2d_project_fwd(_ptr(p), N, stride, width, height, eps_cut, _ptr(b.rec), _ptr(b.rect),
-                              _ptr(b.cnt), _ptr(b.tile_cnt), stream), "gsr2d_project_fwd")
+      check(L.gsr2d_project_fwd(_ptr(p), N, stride, width, height, eps_cut, q["rec"], q["rect"],
+                              q["cnt"], q["tile_cnt"], stream), "gsr2d_project_fwd")
+    b.guess_post(with_chunks=False)
     b.offsets(stream)
+    b.ensure_post(with_chunks=False)
     b.sort(_lib.ORDER_INDEX, stream)
     rgb = torch.empty(height, width, 3, device=dev, dtype=torch.float32)
     alpha = torch.empty(height, width, device=dev, dtype=torch.float32)
-    b.last = torch.empty(height, width, device=dev, dtype=torch.int32)
-    b.tile_end = torch.empty(b.CT, device=dev, dtype=torch.int32)
-    b.tile_cut = torch.empty(b.CT, device=dev, dtype=torch.int64)
     with _timed("raster2d_fwd"):
-      check(L.gsr2d_raster_fwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), width, height, _ptr(bgc),
-                             _ptr(rgb), _ptr(alpha), _ptr(b.last), _ptr(b.tile_end), _ptr(b.tile_cut), stream),
+      check(L.gsr2d_raster_fwd(q["rec"], q["sorted_ids"], q["tile_off"], width, height, _ptr(bgc),
+                             _ptr(rgb), _ptr(alpha), q["last"], q["tile_end"], q["tile_cut"], stream),
           "gsr2d_raster_fwd")
     _record_stats(b)
     return rgb, alpha, b, (p, stride, bgc, width, height)
@@ -269,16 +359,16 @@ class _Render3D(torch.autograd.Function):
         v_params = torch.empty(N, 14, device=dev, dtype=torch.float32)
         if N > 0:
             partial = torch.empty(max(b.n_isect, 1) * _lib.PARTIAL_STRIDE, device=dev, dtype=torch.float32)
+            q = b.p
             with _timed("raster3d_bwd"):
-              check(L.gsr3d_raster_bwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), _ptr(b.tile_end),
-                                     _ptr(b.chunk_base), _ptr(b.chunk_tile), _ptr(b.chunk_state),
-                                     _ptr(b.chunk_list), _ptr(b.stats_dev), b.n_chunks,
-                                     C, width, height, _ptr(bgc), _ptr(b.final_T), _ptr(b.last), _ptr(v_rgb),
-                                     _ptr(v_alpha), _ptr(b.k_of_s), _ptr(partial), stream),
+              check(L.gsr3d_raster_bwd(q["rec"], q["sorted_ids"], q["tile_off"], q["tile_end"], q["chunk_base"],
+                                     q["chunk_tile"], q["chunk_state"], q["chunk_list"], q["stats_dev"],
+                                     b.n_chunks, C, width, height, _ptr(bgc), q["final_T"], q["last"],
+                                     _ptr(v_rgb), _ptr(v_alpha), q["k_of_s"], _ptr(partial), stream),
                   "gsr3d_raster_bwd")
             with _timed("project3d_bwd"):
               check(L.gsr3d_project_bwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height, opts.eps2d,
-                                      _ptr(b.rec), _ptr(b.rect), _ptr(b.isect_off), _ptr(b.cnt), _ptr(b.tile_cut),
+                                      q["rec"], q["rect"], q["isect_off"], q["cnt"], q["tile_cut"],
                                       _ptr(partial), _ptr(v_params), stream),
                   "gsr3d_project_bwd")
         return v_params.view(ctx.params_shape), None, None, None, None, None, None
@@ -311,16 +401,16 @@ class _Render2D(torch.autograd.Function):
         if N > 0:
             partial = torch.empty(max(b.n_isect, 1) * _lib.PARTIAL_STRIDE, device=dev, dtype=torch.float32)
             ws = torch.empty(int(L.gsr2d_raster_bwd_workspace(b.n_isect, b.CT)), device=dev, dtype=torch.uint8)
+            q = b.p
             with _timed("raster2d_bwd"):
-              check(L.gsr2d_raster_bwd(_ptr(b.rec), _ptr(b.sorted_ids), _ptr(b.tile_off), _ptr(b.tile_end),
-                                     _ptr(b.busy), b.n_busy, width, height, _ptr(bgc), _ptr(b.last),
-                                     _ptr(v_rgb), _ptr(v_alpha), _ptr(ws), ws.numel(), _ptr(b.k_of_s), _ptr(partial),
-                                     stream),
+              check(L.gsr2d_raster_bwd(q["rec"], q["sorted_ids"], q["tile_off"], q["tile_end"], q["busy"],
+                                     b.n_busy, width, height, _ptr(bgc), q["last"], _ptr(v_rgb), _ptr(v_alpha),
+                                     _ptr(ws), ws.numel(), q["k_of_s"], _ptr(partial), stream),
                   "gsr2d_raster_bwd")
             with _timed("project2d_bwd"):
-              check(L.gsr2d_project_bwd(_ptr(p), N, stride, width, height, _ptr(b.rect), _ptr(b.isect_off),
-                                      _ptr(b.cnt), _ptr(b.tile_cut), _ptr(partial),
-                                      _ptr(v_params), stream), "gsr2d_project_bwd")
+              check(L.gsr2d_project_bwd(_ptr(p), N, stride, width, height, q["rect"], q["isect_off"],
+                                      q["cnt"], q["tile_cut"], _ptr(partial), _ptr(v_params), stream),
+                  "gsr2d_project_bwd")
         return v_params.view(ctx.params_shape), None, None, None, None
 
 
