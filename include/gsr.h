@@ -86,6 +86,10 @@ const char* gsr_last_error(void);
  * out[l] = sum over lanes L of v_L[l] with v_L[i] = ((L*7 + i*13) % 97) + i/4.  out: 64 floats. */
 int gsr_selftest_reduce64(float* out, void* stream);
 
+/* Self-test of the lane-ordered LDS atomics the tile sort's ranking relies on: writes the
+ * number of violations (0 expected) to the device int *violations. */
+int gsr_selftest_lds_order(int32_t* violations, void* stream);
+
 /* ---------------------------------------------------------------- (a) projection */
 
 /* 3D projection (+ adapter activations fused).  params: [N, >=14] fp32 rows with

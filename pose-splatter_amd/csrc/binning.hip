@@ -11,6 +11,17 @@
 
 namespace gsr {
 
+#ifdef GSR_EXP_COUNT
+__device__ unsigned long long g_cnt_bin[16];
+#define GSR_BCNT_ADD(i, v) atomicAdd(&g_cnt_bin[i], (unsigned long long)(v))
+#define GSR_BCNT_MAX(i, v) atomicMax(&g_cnt_bin[i], (unsigned long long)(v))
+#define GSR_BCLOCK() clock64()
+#else
+#define GSR_BCNT_ADD(i, v)
+#define GSR_BCNT_MAX(i, v)
+#define GSR_BCLOCK() 0ll
+#endif
+
 constexpr int kScanThreads = 256;
 constexpr int kScanItems = 16;
 constexpr int kScanTile = kScanThreads * kScanItems;   // 4096 per block
@@ -197,9 +208,9 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const Splat* __restrict__
 // the sort (c*N+n, and the slot → sorted-position map used by the backward) stays inside the
 // bucket's own window of the key array (L2-resident) instead of gathering per-Gaussian data.
 // The LDS sort is a stable LSD radix sort on the sort word, 8-bit digits, skipping digit
-// positions that do not vary inside the segment; rank-within-wave comes from 8 ballots per
-// element (exact peer mask), so a pass is one read, one block scan of 16x256 counters and one
-// scatter.  Ties on the sort word (equal depths) are then put in ascending c*N+n order by a
+// positions that do not vary inside the segment; the rank within the wave comes from one
+// returning LDS atomic per key (lane-ordered), so a pass is one read, one block scan of
+// 16x256 counters and one scatter.  Ties on the sort word (equal depths) are then put in ascending c*N+n order by a
 // bounded odd-even fix-up — the order a stable radix sort of gsplat's keys over emission
 // order gives.
 
@@ -210,7 +221,6 @@ __device__ __forceinline__ uint32_t low_word(uint64_t k) { return (uint32_t)(k &
 // (tie-break by their low word); s_hist: kSortWaves*256 + 64 ints.
 __device__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, const uint64_t* __restrict__ seg) {
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const unsigned long long lt = (1ull << lane) - 1ull;
   int* s_misc = s_hist + kSortWaves * 256;
   if (threadIdx.x == 0) s_misc[0] = 0;
   __syncthreads();
@@ -228,6 +238,10 @@ __device__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, const uint64_t* 
     __builtin_amdgcn_wave_barrier();
     uint64_t el[kSortRounds];
     int rk[kSortRounds];
+    // Stable rank inside the wave's digit bucket from ONE returning LDS atomic per key: the
+    // LDS serialises same-address atomics of one wave instruction in lane order (measured on
+    // MI355X; gsr_selftest_lds_order checks it), and rounds run in order, so the returned
+    // count is the key's position among the wave's equal digits.
 #pragma unroll
     for (int r = 0; r < kSortRounds; ++r) {
       if (r < rounds) {
@@ -235,20 +249,7 @@ __device__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, const uint64_t* 
         const bool valid = idx < n;
         el[r] = valid ? a[idx] : 0ull;
         const uint32_t d = (sort_word(el[r]) >> shift) & 0xFFu;
-        const unsigned long long vm = __ballot(valid);
-        unsigned long long peers = vm;
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-          const unsigned long long bb = __ballot(valid && ((d >> b) & 1u));
-          peers &= ((d >> b) & 1u) ? bb : (vm & ~bb);
-        }
-        const int rin = __popcll(peers & lt);
-        int base = 0;
-        if (valid) base = s_hist[wv * 256 + d];
-        __builtin_amdgcn_wave_barrier();
-        if (valid && rin == 0) s_hist[wv * 256 + d] = base + __popcll(peers);
-        __builtin_amdgcn_wave_barrier();
-        rk[r] = valid ? (int)((d << 23) | (uint32_t)(base + rin)) : -1;   // pos < 2^23
+        rk[r] = valid ? (int)((d << 23) | (uint32_t)atomicAdd(&s_hist[wv * 256 + d], 1)) : -1;   // pos < 2^23
       }
     }
     __syncthreads();
@@ -281,8 +282,11 @@ __device__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, const uint64_t* 
     }
     __syncthreads();
   }
+  [[maybe_unused]] const long long t_fix = GSR_BCLOCK();
+  [[maybe_unused]] int fix_iters = 0;
   // equal sort words: order by c*N+n — odd-even passes until nothing moves
   while (true) {
+    ++fix_iters;
     bool moved = false;
 #pragma unroll
     for (int ph = 0; ph < 2; ++ph) {
@@ -297,6 +301,11 @@ __device__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, const uint64_t* 
       __syncthreads();
     }
     if (!__syncthreads_or(moved)) break;
+  }
+  if (threadIdx.x == 0) {
+    GSR_BCNT_ADD(5, GSR_BCLOCK() - t_fix);
+    GSR_BCNT_ADD(6, fix_iters);
+    GSR_BCNT_MAX(7, fix_iters);
   }
 }
 
@@ -346,14 +355,24 @@ __global__ __launch_bounds__(kSortThreads) void k_segsort(
   const int len = tile_offset[ct + 1] - start;
   uint64_t* seg = keys + start;
   if (len <= lds_keys) {
+    [[maybe_unused]] const long long t0 = GSR_BCLOCK();
     for (int i = threadIdx.x; i < len; i += blockDim.x)
       s_keys[i] = (seg[i] & 0xffffffff00000000ull) | (uint64_t)(uint32_t)i;
     __syncthreads();
+    [[maybe_unused]] const long long t1 = GSR_BCLOCK();
     lds_radix_sort(s_keys, len, s_hist, seg);
+    [[maybe_unused]] const long long t2 = GSR_BCLOCK();
     for (int s = threadIdx.x; s < len; s += blockDim.x) {
       const uint32_t p = low_word(s_keys[s]);
       sorted_ids[start + s] = (int32_t)low_word(seg[p]);
       k_of_s[start + s] = k_of_slot[start + p];
+    }
+    if (threadIdx.x == 0) {
+      GSR_BCNT_ADD(0, t1 - t0);
+      GSR_BCNT_ADD(1, t2 - t1);
+      GSR_BCNT_ADD(2, GSR_BCLOCK() - t2);
+      GSR_BCNT_MAX(3, GSR_BCLOCK() - t0);
+      GSR_BCNT_ADD(4, 1);
     }
     return;
   }
@@ -393,6 +412,28 @@ __global__ __launch_bounds__(kSortThreads) void k_segsort(
     sorted_ids[start + s] = (int32_t)low_word(kA[s]);
     k_of_s[start + s] = k_of_slot[start + pA[s]];
   }
+}
+
+__global__ void k_selftest_lds_order(int32_t* violations) {
+  __shared__ int hist[4][256];
+  __shared__ int got[256];
+  __shared__ int dig[256];
+  __shared__ int bad;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < 4 * 256; i += blockDim.x) (&hist[0][0])[i] = 0;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  for (int r = 0; r < 48; ++r) {
+    // all-equal, few-distinct and spread digit patterns
+    const int d = r % 3 == 0 ? 7 : (r % 3 == 1 ? ((lane * 7 + r) >> 4) & 3 : (lane * 37 + r * 11) & 255);
+    dig[threadIdx.x] = d;
+    got[threadIdx.x] = atomicAdd(&hist[wv][d], 1);
+    __syncthreads();
+    for (int b = lane + 1; b < 64; ++b)
+      if (dig[wv * 64 + b] == d && !(got[wv * 64 + b] > got[threadIdx.x])) atomicAdd(&bad, 1);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *violations = bad;
 }
 
 }  // namespace gsr
@@ -468,5 +509,27 @@ int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_of
   }
   return GSR_OK;
 }
+
+// Self-test of the property the sort's ranking relies on: returning LDS atomics of one wave
+// instruction to the same address are applied in lane order.  out[64*R] gets each lane's
+// returned count for R rounds of digits d(lane, r); returns GSR_OK and writes the number of
+// out-of-order pairs to *violations (device int).
+int gsr_selftest_lds_order(int32_t* violations, void* stream) {
+  hipLaunchKernelGGL(k_selftest_lds_order, dim3(1), dim3(256), 0, (hipStream_t)stream, violations);
+  GSR_LAUNCH_CHECK("k_selftest_lds_order");
+  return GSR_OK;
+}
+
+#ifdef GSR_EXP_COUNT
+int gsr_debug_counters_bin(unsigned long long* out, int reset) {
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(gsr::g_cnt_bin), sizeof(gsr::g_cnt_bin));
+  if (reset) {
+    unsigned long long z[16] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(gsr::g_cnt_bin), z, sizeof(z));
+  }
+  return 0;
+}
+#endif
 
 }  // extern "C"

@@ -31,6 +31,16 @@ def test_selftest_reduce64(cuda):
     assert torch.allclose(out.cpu().double(), v.sum(0), rtol=0, atol=1e-3), out
 
 
+def test_selftest_lds_order(cuda):
+    """The tile sort ranks keys with returning LDS atomics, relying on same-address atomics of
+    one wave instruction being applied in lane order."""
+    from gsr import _lib
+    out = torch.full((1,), -1, device=cuda, dtype=torch.int32)
+    _lib.check(_lib.lib().gsr_selftest_lds_order(out.data_ptr(), torch.cuda.current_stream().cuda_stream),
+               "selftest")
+    assert int(out.item()) == 0
+
+
 def _oracle3d():
     from oracle import oracle3d
     return oracle3d

@@ -24,19 +24,27 @@ L = lib()
 f = L.gsr_debug_counters
 f.argtypes = [ctypes.c_void_p, ctypes.c_int]
 out = (ctypes.c_ulonglong * 16)()
+fb = L.gsr_debug_counters_bin
+fb.argtypes = [ctypes.c_void_p, ctypes.c_int]
+outb = (ctypes.c_ulonglong * 16)()
 rgb, alpha = R.render3d(p, V, K, cfg.width, cfg.height, bg)
 (rgb.sum() + alpha.sum()).backward()
 f(out, 1)
+fb(outb, 1)
 R.enable_kernel_timing(True)
 rgb, alpha = R.render3d(p, V, K, cfg.width, cfg.height, bg)
 (rgb.sum() + alpha.sum()).backward()
 f(out, 1)
+fb(outb, 1)
 print({k: round(v[0], 4) for k, v in R.kernel_times_ms().items()})
 names = ["fwd_batches", "fwd_max_batches_per_wave", "fwd_survivors", "fwd_cycles_cull+issue",
          "fwd_cycles_composite", "fwd_cycles_wave_total", "fwd_cycles_wave_max", "-",
          "bwd_survivors", "bwd_groups", "bwd_cycles_prologue", "bwd_cycles_groups", "bwd_cycles_epilogue",
          "bwd_active_blocks", "bwd_cycles_wave_max", "-"]
 for n, v in zip(names, out):
+    print(f"{n:28s} {v}")
+for n, v in zip(["sort_cycles_load", "sort_cycles_radix", "sort_cycles_out", "sort_cycles_block_max",
+                 "sort_blocks_lds", "sort_cycles_fixup", "sort_fix_iters", "sort_fix_iters_max"], outb):
     print(f"{n:28s} {v}")
 st = R.last_stats()
 print({k: v for k, v in st.items() if not k.startswith("_")})
