@@ -219,7 +219,7 @@ __device__ __forceinline__ uint32_t low_word(uint64_t k) { return (uint32_t)(k &
 
 // a: n <= kSortLdsKeys elements (word << 32 | p) in LDS; seg: the bucket's original keys
 // (tie-break by their low word); s_hist: kSortWaves*256 + 64 ints.
-__device__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, const uint64_t* __restrict__ seg) {
+__device__ __forceinline__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, const uint64_t* __restrict__ seg) {
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int* s_misc = s_hist + kSortWaves * 256;
   if (threadIdx.x == 0) s_misc[0] = 0;
@@ -317,7 +317,7 @@ __device__ __forceinline__ int next_pow2(int v) {
 
 // Merge two sorted runs of unique keys (with payloads) into out (block-cooperative, per-element
 // rank by binary search in the other run).
-__device__ void merge_runs(const uint64_t* __restrict__ a, const int32_t* __restrict__ pa, int na,
+__device__ __forceinline__ void merge_runs(const uint64_t* __restrict__ a, const int32_t* __restrict__ pa, int na,
                            const uint64_t* __restrict__ b, const int32_t* __restrict__ pb, int nb,
                            uint64_t* __restrict__ out, int32_t* __restrict__ pout) {
   for (int i = threadIdx.x; i < na; i += blockDim.x) {
