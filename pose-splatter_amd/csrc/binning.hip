@@ -27,8 +27,14 @@ constexpr int kScanItems = 16;
 constexpr int kScanTile = kScanThreads * kScanItems;   // 4096 per block
 constexpr int kTopThreads = 1024;
 constexpr int kChunkEntries = GSR_CHUNK;   // backward work unit (list entries)
-constexpr int kEmitThreads = 256;
-constexpr int kEmitPerBlock = 2048;
+#ifndef GSR_EMIT_THREADS
+#define GSR_EMIT_THREADS 512
+#endif
+#ifndef GSR_EMIT_PER_BLOCK
+#define GSR_EMIT_PER_BLOCK 1024
+#endif
+constexpr int kEmitThreads = GSR_EMIT_THREADS;
+constexpr int kEmitPerBlock = GSR_EMIT_PER_BLOCK;
 constexpr int kHistMaxTiles = 16384;
 constexpr int kSortThreads = 1024;    // 16 waves
 constexpr int kSortWaves = kSortThreads / 64;
