@@ -96,16 +96,16 @@ __device__ __forceinline__ SubTile sub_tile(int ct, int tw, int th, int W, int H
 
 // ---------------------------------------------------------------- empty tiles
 // Tiles with an empty list only need the background.  The forward launches them as extra
-// workgroups (blockIdx >= n_busy) that stride over order[n_busy..CT): cheap stores that
+// workgroups (after the busy tiles' ones) that stride over order[n_busy..CT): cheap stores that
 // run beside the busy tiles instead of one short-lived workgroup per empty tile.
 template <bool IS2D>
 __device__ void fill_empty(const int32_t* __restrict__ order, const int32_t* __restrict__ tile_offset, int n_busy,
-                           int64_t CT, int W, int H, int tw, int th, const float* __restrict__ bg,
+                           int busy_blocks, int64_t CT, int W, int H, int tw, int th, const float* __restrict__ bg,
                            float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
                            int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end,
                            uint64_t* __restrict__ tile_cut) {
-  const int G = gridDim.x - n_busy;
-  for (int64_t t = n_busy + (blockIdx.x - n_busy); t < CT; t += G) {
+  const int G = gridDim.x - busy_blocks;
+  for (int64_t t = n_busy + (blockIdx.x - busy_blocks); t < CT; t += G) {
     const int ct = order[t];
     const SubTile st = sub_tile<IS2D>(ct, tw, th, W, H);
     if (st.inside) {
@@ -125,65 +125,103 @@ __device__ void fill_empty(const int32_t* __restrict__ order, const int32_t* __r
   }
 }
 
-// ---------------------------------------------------------------- 3D / 2D forward
-// Waves run independently (no workgroup barrier in the loop): each wave gathers the next 64
-// list entries (prefetched one batch ahead), culls them against its sub-tile, compacts the
-// survivors into its private LDS queue, and composites them branch-free.  A wave leaves as
-// soon as all of its 64 pixels are done.
-//  3D (gsplat classic):  a = min(0.999, o e^-s); skip s<0 | a<1/255; stop before T(1-a)<=1e-4
-//  2D (reference):       c = o e^-q (1-A); canvas += c rgb; A += c   (A == 1 exactly → done)
-template <bool IS2D>
-__global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
+// ---------------------------------------------------------------- 3D forward
+// Work unit: a 4x4-pixel sub-tile per wave, FOUR lanes per pixel.  A tile's list is walked by
+// 16 independent waves (4 workgroups of 4 waves, one per 8x8 quadrant); each wave gathers
+// 64-entry batches (software-pipelined), culls them against its 4x4 pixel-centre box,
+// compacts the survivors into a private LDS queue and composites them four at a time: lane
+// (pixel p, slot q) evaluates survivor 4t+q for pixel p, and the quad (the 4 lanes of a
+// pixel, a DPP quad) combines the four in list order:
+//   x_q = 1 - a_q (1 for skipped entries),  T_q = T * prod_{i<q} x_i   (quad prefix product)
+//   the first q with T * prod_{i<=q} x_i <= 1e-4 stops the pixel (that entry and the later
+//   ones are not composited), the others add c_q a_q T_q,  T <- T * prod_{i<stop} x_i.
+// That is gsplat's sequential recursion with the product regrouped in fours (fp32 rounding
+// only).  The serial chain per wave is a quarter of the list walk, and the finer cull box
+// cuts the evaluated (pixel, entry) pairs.
+constexpr int kQuadPrefix1 = 0x90;   // quad_perm [0,0,1,2]: lane q reads lane max(q-1,0)
+constexpr int kQuadPrefix2 = 0x40;   // quad_perm [0,0,0,1]: lane q reads lane max(q-2,0)
+constexpr int kQuadXor1 = 0xB1;      // quad_perm [1,0,3,2]
+constexpr int kQuadXor2 = 0x4E;      // quad_perm [2,3,0,1]
+
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
+}
+__device__ __forceinline__ float quad_sum(float v) {
+  v += dpp_mov<kQuadXor1>(v);
+  return v + dpp_mov<kQuadXor2>(v);
+}
+__device__ __forceinline__ float quad_min(float v) {
+  v = fminf(v, dpp_mov<kQuadXor1>(v));
+  return fminf(v, dpp_mov<kQuadXor2>(v));
+}
+__device__ __forceinline__ int quad_min_i(int v) {
+  v = min(v, dpp_i<kQuadXor1>(v));
+  return min(v, dpp_i<kQuadXor2>(v));
+}
+__device__ __forceinline__ int quad_max_i(int v) {
+  v = max(v, dpp_i<kQuadXor1>(v));
+  return max(v, dpp_i<kQuadXor2>(v));
+}
+// thread index of tile pixel (il, jl) in the backward's layout (4 waves of 8x8)
+__device__ __forceinline__ int bwd_pixel_slot(int il, int jl) {
+  return ((il >> 3) << 7) | ((jl >> 3) << 6) | ((il & 7) << 3) | (jl & 7);
+}
+
+__global__ __launch_bounds__(kRasterThreads) void k_raster3d_fwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
-    const int32_t* __restrict__ order, int W, int H, int tw, int th, float cut, const float* __restrict__ bg,
+    const int32_t* __restrict__ order, int W, int H, int tw, int th, const float* __restrict__ bg,
     float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
     int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end, float4* __restrict__ ckpt,
     const int32_t* __restrict__ chunk_base, int32_t* __restrict__ chunk_tile, int n_busy, int64_t CT,
-    gsr_bin_stats* __restrict__ stats, int32_t* __restrict__ chunk_list, uint64_t* __restrict__ tile_cut) {
+    uint64_t* __restrict__ tile_cut) {
   __shared__ float4 s_p0[4][64];
   __shared__ float4 s_p1[4][64];
   __shared__ float4 s_p2[4][64];
-  __shared__ int s_max, s_pos, s_nact;
-  if ((int)blockIdx.x >= n_busy) {
-    fill_empty<IS2D>(order, tile_offset, n_busy, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T, out_last,
-                     tile_end, tile_cut);
+  __shared__ int s_max;
+  if ((int)blockIdx.x >= 4 * n_busy) {
+    fill_empty<false>(order, tile_offset, n_busy, 4 * n_busy, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
+                      out_last, tile_end, tile_cut);
     return;
   }
-  const int ct = order[blockIdx.x];
-  const SubTile st = sub_tile<IS2D>(ct, tw, th, W, H);
-  const int wv = st.wv;
+  const int ct = order[blockIdx.x >> 2];
+  const int quad = blockIdx.x & 3;
+  int c, ty, tx;
+  tile_coords(ct, tw, th, c, ty, tx);
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int q = lane & 3, p = lane >> 2;
+  const int ox = ((quad & 1) << 3) + ((wv & 1) << 2), oy = ((quad >> 1) << 3) + ((wv >> 1) << 2);
+  const int il = oy + (p >> 2), jl = ox + (p & 3);
+  const int i = ty * kTile + il, j = tx * kTile + jl;
+  const bool inside = i < H && j < W;
+  const float px = (float)j + 0.5f, py = (float)i + 0.5f;
+  const float bx0 = (float)(tx * kTile + ox) + 0.5f, bx1 = bx0 + 3.f;
+  const float by0 = (float)(ty * kTile + oy) + 0.5f, by1 = by0 + 3.f;
   const int start = tile_offset[ct], end = tile_offset[ct + 1];
   if (threadIdx.x == 0) s_max = -1;
   __syncthreads();
-  float T = 1.f;   // 3D: transmittance;  2D: accumulated alpha A
-  if (IS2D) T = 0.f;
-  float cr = 0.f, cg = 0.f, cb = 0.f;
+  float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f;
   int last = -1;
-  bool done = !st.inside;
-  // 3D: chunk records for the chunk-parallel backward — per pixel and per GSR_CHUNK-entry
-  // chunk k of the tile's list: {T at the chunk's start, the chunk's own colour sum}.
-  int cbase = 0, kcur = 0;
-  float Ts = 1.f, dr = 0.f, dg = 0.f, db = 0.f;
-  if (!IS2D) {
-    cbase = chunk_base[ct];
+  bool done = !inside;
+  // chunk records for the chunk-parallel backward (per pixel, per GSR_CHUNK-entry chunk)
+  const int cbase = chunk_base[ct];
+  int kcur = 0;
+  float Ts = 1.f, dr = 0.f, dg = 0.f, db = 0.f;   // dr..: this lane's share of the chunk's colour
+  if (quad == 0) {
     const int nchunk = (end - start + kChunk3 - 1) / kChunk3;
     for (int k = threadIdx.x; k < nchunk; k += blockDim.x) chunk_tile[cbase + k] = ct;
   }
-  // Software pipeline over 64-entry batches: while batch b is culled and composited, the
-  // records of b+1 and b+2 and the list ids of b+3 are in flight.  Two record buffers (X, Y)
-  // and two id registers alternate roles in a 2-way unrolled loop, so no loaded value is
-  // ever copied (a copy would wait for its load).  Loads are unconditional (index clamped to
-  // the list's last entry, validity from the position) and each step issues the ids of b+3
-  // BEFORE the records of b+2, so waiting for an id never waits for younger record loads.
+  // software pipeline over 64-entry batches (records of b+1, b+2 and ids of b+3 in flight;
+  // see the notes of the 2-way unrolled loop below)
   const int e_last = max(end - 1, start);
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 x0 = zero4, x1 = zero4, x2 = zero4, y0 = zero4, y1 = zero4, y2 = zero4;
   int idp = 0, idq = 0;
   if (end > start) {
-    const int ida = ids[min(start + st.lane, e_last)];
-    const int idb = ids[min(start + 64 + st.lane, e_last)];
+    const int ida = ids[min(start + lane, e_last)];
+    const int idb = ids[min(start + 64 + lane, e_last)];
     const Splat sa = rec[ida];
-    idp = ids[min(start + 128 + st.lane, e_last)];
+    idp = ids[min(start + 128 + lane, e_last)];
     const Splat sb = rec[idb];
     x0 = sa.p0; x1 = sa.p1; x2 = sa.p2;
     y0 = sb.p0; y1 = sb.p1; y2 = sb.p2;
@@ -191,66 +229,68 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   [[maybe_unused]] int cnt_b = 0, cnt_s = 0;
   [[maybe_unused]] long long clk_cull = 0, clk_comp = 0;
   [[maybe_unused]] const long long clk_start = GSR_CLOCK();
-  // one batch: cull + compact c (batch b0), refill c with batch b0+128 (id_use), load the
-  // ids of batch b0+192 into id_new, composite.  false = every pixel of the wave is done.
+  // One batch: cull + compact c (batch b0), refill c with batch b0+128 (id_use), load the ids
+  // of batch b0+192 into id_new (issued BEFORE the record loads, so waiting for an id never
+  // waits for younger record loads), composite.  false = every pixel of the wave is done.
   auto step = [&](int b0, float4& c0, float4& c1, float4& c2, int id_use, int& id_new) -> bool {
     if (__ballot(!done) == 0ull) return false;
     [[maybe_unused]] const long long t0 = GSR_CLOCK();
     ++cnt_b;
-    if (!IS2D && b0 > start && ((b0 - start) % kChunk3) == 0) {   // entering chunk kcur+1
-      ckpt[(int64_t)(cbase + kcur) * kRasterThreads + threadIdx.x] = make_float4(Ts, dr, dg, db);
-      cr += dr;
-      cg += dg;
-      cb += db;
+    if (b0 > start && ((b0 - start) % kChunk3) == 0) {   // entering chunk kcur+1
+      const float Dr = quad_sum(dr), Dg = quad_sum(dg), Db = quad_sum(db);
+      if (q == 0) ckpt[(int64_t)(cbase + kcur) * kRasterThreads + bwd_pixel_slot(il, jl)] = make_float4(Ts, Dr, Dg, Db);
+      cr += Dr;
+      cg += Dg;
+      cb += Db;
       dr = dg = db = 0.f;
       Ts = T;
       ++kcur;
     }
-    const bool keep = (b0 + st.lane < end) && cull_keep<IS2D>(c0, c1, st.bx0, st.bx1, st.by0, st.by1, cut);
+    const bool keep = (b0 + lane < end) && cull_keep<false>(c0, c1, bx0, bx1, by0, by1, 0.f);
     const unsigned long long m = __ballot(keep);
     const int n = __popcll(m);
     cnt_s += n;
     if (keep) {
       const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
       s_p0[wv][slot] = c0;
-      s_p1[wv][slot] = make_float4(c1.x, c1.y, c1.z, __int_as_float(b0 + st.lane));
+      s_p1[wv][slot] = make_float4(c1.x, c1.y, c1.z, __int_as_float(b0 + lane));
       s_p2[wv][slot] = c2;
     }
-    id_new = ids[min(b0 + 192 + st.lane, e_last)];
+    id_new = ids[min(b0 + 192 + lane, e_last)];
     const Splat sc = rec[id_use];
     c0 = sc.p0; c1 = sc.p1; c2 = sc.p2;
     __builtin_amdgcn_wave_barrier();
     [[maybe_unused]] const long long t1 = GSR_CLOCK();
-#pragma unroll 4
-    for (int k = 0; k < n; ++k) {
-      const float4 p0 = s_p0[wv][k];
-      const float4 p1 = s_p1[wv][k];
-      const float4 p2 = s_p2[wv][k];
-      const float dx = p0.x - st.px, dy = p0.y - st.py;
+    for (int k0 = 0; k0 < n; k0 += 4) {
+      const int k = k0 + q;
+      const int kk = k < n ? k : n - 1;
+      const float4 p0 = s_p0[wv][kk];
+      const float4 p1 = s_p1[wv][kk];
+      const float4 p2 = s_p2[wv][kk];
+      const float dx = p0.x - px, dy = p0.y - py;
       const float sg = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
-      if (!IS2D) {
-        const float alpha = fminf(kAlphaMax, p0.z * __expf(-sg));
-        const bool ok = !done && sg >= 0.f && alpha >= kAlphaThreshold;
-        const float nT = T * (1.f - alpha);
-        const bool stop = ok && (nT <= kTMin);
-        const bool con = ok && !stop;
-        const float vis = con ? alpha * T : 0.f;
-        dr += p2.x * vis;
-        dg += p2.y * vis;
-        db += p2.z * vis;
-        T = con ? nT : T;
-        last = con ? __float_as_int(p1.w) : last;
-        done = done || stop;
-      } else {
-        const float g = p0.z * __expf(-sg);
-        const float contrib = done ? 0.f : g * (1.f - T);
-        cr += contrib * p2.x;
-        cg += contrib * p2.y;
-        cb += contrib * p2.z;
-        T += contrib;
-        last = done ? last : __float_as_int(p1.w);
-        done = done || (T == 1.f);
-      }
+      const float alpha = fminf(kAlphaMax, p0.z * __expf(-sg));
+      const bool valid = k < n && !done && sg >= 0.f && alpha >= kAlphaThreshold;
+      const float xq = valid ? 1.f - alpha : 1.f;
+      // quad prefix products of x (inclusive Q, exclusive P).  The DPP moves run in every
+      // lane (a DPP read of a lane that is switched off returns 0); only the selects depend
+      // on the slot.
+      const float d1 = dpp_mov<kQuadPrefix1>(xq);
+      const float q1 = xq * (q >= 1 ? d1 : 1.f);
+      const float d2 = dpp_mov<kQuadPrefix2>(q1);
+      const float Qi = q1 * (q >= 2 ? d2 : 1.f);      // prod_{i<=q} x_i
+      const float d3 = dpp_mov<kQuadPrefix1>(Qi);
+      const float Pe = q >= 1 ? d3 : 1.f;             // prod_{i<q} x_i
+      const float nT = T * Qi;
+      const int fs = quad_min_i(valid && nT <= kTMin ? q : 4);   // first stopping slot
+      const bool con = valid && q < fs;
+      const float vis = con ? alpha * (T * Pe) : 0.f;
+      dr += p2.x * vis;
+      dg += p2.y * vis;
+      db += p2.z * vis;
+      last = con ? __float_as_int(p1.w) : last;
+      T = quad_min(q < fs ? nT : T);
+      done = done || fs < 4;
     }
     __builtin_amdgcn_wave_barrier();
     [[maybe_unused]] const long long t2 = GSR_CLOCK();
@@ -262,7 +302,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     if (!step(b0, x0, x1, x2, idp, idq)) break;
     if (b0 + 64 >= end || !step(b0 + 64, y0, y1, y2, idq, idp)) break;
   }
-  if (st.lane == 0) {
+  if (lane == 0) {
     GSR_CNT_ADD(0, cnt_b);
     GSR_CNT_MAX(1, cnt_b);
     GSR_CNT_ADD(2, cnt_s);
@@ -271,16 +311,18 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     GSR_CNT_ADD(5, GSR_CLOCK() - clk_start);
     GSR_CNT_MAX(6, GSR_CLOCK() - clk_start);
   }
-  if (!IS2D && end > start) {
-    cr += dr;
-    cg += dg;
-    cb += db;
+  const float Dr = quad_sum(dr), Dg = quad_sum(dg), Db = quad_sum(db);
+  cr += Dr;
+  cg += Dg;
+  cb += Db;
+  last = quad_max_i(last);
+  if (q == 0 && end > start) {
     // Turn this pixel's chunk records {T at chunk start, chunk colour sum} into what the
     // backward needs at each chunk's END: {T_end, suffix colour sum of the later chunks}
     // (positive terms, summed back to front).  Records are re-read 8 at a time.
-    float4* ck = ckpt + (int64_t)cbase * kRasterThreads + threadIdx.x;
+    float4* ck = ckpt + (int64_t)cbase * kRasterThreads + bwd_pixel_slot(il, jl);
     ck[(int64_t)kcur * kRasterThreads] = make_float4(T, 0.f, 0.f, 0.f);
-    float Tn = Ts, sr = dr, sg = dg, sb = db;
+    float Tn = Ts, sr = Dr, sg = Dg, sb = Db;
     for (int k0 = kcur - 1; k0 >= 0; k0 -= 8) {
       float4 r[8];
 #pragma unroll
@@ -297,31 +339,42 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
         }
     }
   }
-  if (st.inside) {
-    const int64_t pix = ((int64_t)st.c * H + st.i) * W + st.j;
-    const float* bgc = bg + st.c * 3;
-    const float Tr = IS2D ? 1.f - T : T;
-    out_rgb[pix * 3 + 0] = cr + Tr * bgc[0];
-    out_rgb[pix * 3 + 1] = cg + Tr * bgc[1];
-    out_rgb[pix * 3 + 2] = cb + Tr * bgc[2];
-    out_alpha[pix] = IS2D ? T : 1.f - T;
-    if (!IS2D) out_T[pix] = T;
+  if (q == 0 && inside) {
+    const int64_t pix = ((int64_t)c * H + i) * W + j;
+    const float* bgc = bg + c * 3;
+    out_rgb[pix * 3 + 0] = cr + T * bgc[0];
+    out_rgb[pix * 3 + 1] = cg + T * bgc[1];
+    out_rgb[pix * 3 + 2] = cb + T * bgc[2];
+    out_alpha[pix] = 1.f - T;
+    out_T[pix] = T;
     out_last[pix] = last;
   }
-  if (last >= 0) atomicMax(&s_max, last);
+  if (q == 0 && last >= 0) atomicMax(&s_max, last);
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const int te = s_max >= 0 ? s_max + 1 : start;
-    tile_end[ct] = te;
-    // key of the first entry past tile_end (its partial is never written)
-    tile_cut[ct] = te < end ? sort_key(rec, ids[te], IS2D ? GSR_ORDER_INDEX : GSR_ORDER_DEPTH) : ~0ull;
-    // 3D: register the chunks before tile_end with the backward's work list
-    const int nact = IS2D ? 0 : (te - start + kChunk3 - 1) / kChunk3;
-    s_nact = nact;
-    s_pos = nact > 0 ? atomicAdd(&stats->n_active, nact) : 0;
+  if (threadIdx.x == 0 && s_max >= 0) atomicMax(&tile_end[ct], s_max);   // finalised below
+}
+
+// Per busy tile: tile_end = 1 + max last over the tile's four quadrant workgroups (or the
+// tile's start), the cut key, and the tile's active chunks appended to the backward's list.
+__global__ __launch_bounds__(kRasterThreads) void k_raster3d_finalize(
+    const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
+    const int32_t* __restrict__ order, int n_busy, const int32_t* __restrict__ chunk_base,
+    int32_t* __restrict__ tile_end, uint64_t* __restrict__ tile_cut, gsr_bin_stats* __restrict__ stats,
+    int32_t* __restrict__ chunk_list) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n_busy) return;
+  const int ct = order[b];
+  const int start = tile_offset[ct], end = tile_offset[ct + 1];
+  const int m = tile_end[ct];
+  const int te = m >= 0 ? m + 1 : start;
+  tile_end[ct] = te;
+  tile_cut[ct] = te < end ? sort_key(rec, ids[te], GSR_ORDER_DEPTH) : ~0ull;
+  const int nact = (te - start + kChunk3 - 1) / kChunk3;
+  if (nact > 0) {
+    const int pos = atomicAdd(&stats->n_active, nact);
+    const int cbase = chunk_base[ct];
+    for (int k = 0; k < nact; ++k) chunk_list[pos + k] = cbase + k;
   }
-  __syncthreads();
-  for (int k = threadIdx.x; k < s_nact; k += blockDim.x) chunk_list[s_pos + k] = cbase + k;
 }
 
 // ---------------------------------------------------------------- 2D forward
@@ -798,11 +851,23 @@ int gsr3d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t*
   GSR_REQUIRE(CT < (1ll << 31), "gsr3d_raster_fwd: too many tiles");
   GSR_REQUIRE(n_busy >= 0 && n_busy <= CT, "gsr3d_raster_fwd: n_busy=%d out of [0, %lld]", n_busy, (long long)CT);
   const int64_t n_fill = std::min<int64_t>(CT - n_busy, kFillBlocks);
-  hipLaunchKernelGGL(k_raster_fwd<false>, dim3((unsigned)(n_busy + n_fill)), dim3(kRasterThreads), 0,
-                     (hipStream_t)stream, (const Splat*)rec, sorted_ids, tile_offset, tile_order, width, height, tw,
-                     th, kAlphaThreshold, bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state, chunk_base,
-                     chunk_tile, (int)n_busy, CT, stats, chunk_list, tile_cut);
-  GSR_LAUNCH_CHECK("k_raster_fwd<3d>");
+  hipStream_t s = (hipStream_t)stream;
+  // tile_end collects max(last) of the quadrant workgroups (atomicMax from -1)
+  if (hipMemsetAsync(tile_end, 0xFF, CT * sizeof(int32_t), s) != hipSuccess) {
+    set_error("gsr3d_raster_fwd: tile_end memset failed");
+    return GSR_ELAUNCH;
+  }
+  hipLaunchKernelGGL(k_raster3d_fwd, dim3((unsigned)(4 * (int64_t)n_busy + n_fill)), dim3(kRasterThreads), 0, s,
+                     (const Splat*)rec, sorted_ids, tile_offset, tile_order, width, height, tw, th, bg, rgb, alpha,
+                     final_T, last, tile_end, (float4*)chunk_state, chunk_base, chunk_tile, (int)n_busy, CT,
+                     tile_cut);
+  GSR_LAUNCH_CHECK("k_raster3d_fwd");
+  if (n_busy > 0) {
+    hipLaunchKernelGGL(k_raster3d_finalize, dim3(ceil_div(n_busy, kRasterThreads)), dim3(kRasterThreads), 0, s,
+                       (const Splat*)rec, sorted_ids, tile_offset, tile_order, (int)n_busy, chunk_base, tile_end,
+                       tile_cut, stats, chunk_list);
+  }
+  GSR_LAUNCH_CHECK("k_raster3d_finalize");
   return GSR_OK;
 }
 
