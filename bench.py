@@ -33,6 +33,8 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# PMC counter run of the same bench command (FETCH_SIZE and WRITE_SIZE passes), committed
+DEFAULT_TRAFFIC_CSV = os.path.join(ROOT, "profiles", "r01_pmc_counters.csv")
 
 
 def parse():
@@ -43,8 +45,9 @@ def parse():
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the CPU oracle timing")
     ap.add_argument("--cpu-views", type=int, default=1, help="views in the bounded CPU sample")
-    ap.add_argument("--traffic-csv", default=None,
-                    help="rocprofv3 --pmc counter_collection.csv to fill roofline.traffic")
+    ap.add_argument("--traffic-csv", default=DEFAULT_TRAFFIC_CSV,
+                    help="rocprofv3 --pmc counter_collection.csv to fill roofline.traffic "
+                         "(default: the committed profiles/ counter run, if present)")
     return ap.parse_args()
 
 
@@ -61,6 +64,11 @@ def algorithmic_bytes(kernel: str, C: int, N: int, P: int, I: int, I_eff: int, p
     if kernel == "bin_sort":
         return 36.0 * I
     return 0.0
+
+
+def step_bytes(C: int, N: int, P_view: int, I: int, I_eff: int, p: int) -> float:
+    """Whole fwd+bwd step, SURVEY.md §8(d): C·N·(12p+136) + 36·I + 80·I_eff + 44·C·P."""
+    return C * N * (12.0 * p + 136.0) + 36.0 * I + 80.0 * I_eff + 44.0 * C * P_view
 
 
 def traffic_from_csv(path: str, kernel_substr: str):
@@ -236,8 +244,9 @@ def main():
     alg = algorithmic_bytes(dom_name or "", Cd, cfg.N, Pd, I, I_eff, p_dim)
     achieved = alg / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     traffic = None
-    if args.traffic_csv and dom_name:
+    if args.traffic_csv and dom_name and os.path.exists(args.traffic_csv):
         traffic = traffic_from_csv(args.traffic_csv, "k_" + dom_name)
+    sb = step_bytes(Cd, cfg.N, cfg.width * cfg.height, I, I_eff, p_dim) * (1 if cfg.mode == "3d" else C)
 
     out = {
         "metric": "rendered frames/sec (fwd+bwd) at N_gauss x H x W",
@@ -259,6 +268,11 @@ def main():
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes": alg, "avg_ms": dom_ms, "launches": dom_n},
         "kernels_ms": {k: round(v[0], 4) for k, v in sorted(breakdown.items())},
+        "sets_per_s": value / C,
+        "pair_evals_per_s": 2.0 * 256.0 * I_eff * (1 if cfg.mode == "3d" else C) * world / (ms_per_step * 1e-3),
+        "step_roofline": {"algorithmic_bytes": sb, "achieved": sb / (ms_per_step * 1e-3) / 1e9,
+                          "unit": "GB/s", "frac": sb / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                          "formula": "SURVEY.md 8(d): C*N*(12p+136) + 36*I + 80*I_eff + 44*C*P per rank"},
         "binning": {"I": I, "I_eff": I_eff, "max_list": st.get("max_seg"), "busy_tiles": st.get("n_busy"),
                     "tiles": st.get("tiles")},
     }

@@ -163,6 +163,9 @@ __device__ __forceinline__ int quad_max_i(int v) {
   v = max(v, dpp_i<kQuadXor1>(v));
   return max(v, dpp_i<kQuadXor2>(v));
 }
+// workgroups for the busy tiles: 4 per tile, rounded up to whole groups of 8 tiles (32 ids)
+__host__ __device__ __forceinline__ int busy_grid(int n_busy) { return 32 * ((n_busy + 7) / 8); }
+
 // thread index of tile pixel (il, jl) in the backward's layout (4 waves of 8x8)
 __device__ __forceinline__ int bwd_pixel_slot(int il, int jl) {
   return ((il >> 3) << 7) | ((jl >> 3) << 6) | ((il & 7) << 3) | (jl & 7);
@@ -179,13 +182,19 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_fwd(
   __shared__ float4 s_p1[4][64];
   __shared__ float4 s_p2[4][64];
   __shared__ int s_max;
-  if ((int)blockIdx.x >= 4 * n_busy) {
-    fill_empty<false>(order, tile_offset, n_busy, 4 * n_busy, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
+  const int busy_blocks = busy_grid(n_busy);
+  if ((int)blockIdx.x >= busy_blocks) {
+    fill_empty<false>(order, tile_offset, n_busy, busy_blocks, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
                       out_last, tile_end, tile_cut);
     return;
   }
-  const int ct = order[blockIdx.x >> 2];
-  const int quad = blockIdx.x & 3;
+  // XCD-aware mapping: workgroups are dealt to the 8 XCDs round-robin by id, so the four
+  // quadrant workgroups of a tile get ids 32k + 8*quad + x (same id mod 8): they share one
+  // XCD's L2 for the tile's records.  Busy tile u = 8k + x, in longest-first order.
+  const int u = ((int)blockIdx.x >> 5) * 8 + ((int)blockIdx.x & 7);
+  const int quad = ((int)blockIdx.x >> 3) & 3;
+  if (u >= n_busy) return;
+  const int ct = order[u];
   int c, ty, tx;
   tile_coords(ct, tw, th, c, ty, tx);
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -857,7 +866,7 @@ int gsr3d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t*
     set_error("gsr3d_raster_fwd: tile_end memset failed");
     return GSR_ELAUNCH;
   }
-  hipLaunchKernelGGL(k_raster3d_fwd, dim3((unsigned)(4 * (int64_t)n_busy + n_fill)), dim3(kRasterThreads), 0, s,
+  hipLaunchKernelGGL(k_raster3d_fwd, dim3((unsigned)(busy_grid(n_busy) + n_fill)), dim3(kRasterThreads), 0, s,
                      (const Splat*)rec, sorted_ids, tile_offset, tile_order, width, height, tw, th, bg, rgb, alpha,
                      final_T, last, tile_end, (float4*)chunk_state, chunk_base, chunk_tile, (int)n_busy, CT,
                      tile_cut);
