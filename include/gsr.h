@@ -33,10 +33,12 @@
  *
  * Splat record (written by *_project_fwd, read by binning and rasterisation):
  *   12 floats (48 B) per (camera c, Gaussian n), at rec[(c*N + n)*12]:
- *     [0]=x [1]=y  screen-space mean (pixels)      [2]=opacity   [3]=depth (3D) / 0 (2D)
+ *     [0]=x [1]=y  screen-space mean (pixels)      [2]=opacity   [3]=ln(255*opacity) (3D)
  *     [4]=a [5]=b [6]=c  exponent  sigma = a*dx^2 + b*dx*dy + c*dy^2,  d = mean - pixel
- *     [7]=0
- *     [8..10]=rgb (activated colour)                [11]=0
+ *     [7]=-b/(2c) (3D)
+ *     [8..10]=rgb (activated colour)                [11]=-b/(2a) (3D)
+ *   ([3], [7], [11] are the per-Gaussian constants of the rasterizer's sub-tile cull; 0 in 2D.)
+ *   depth: 1 float per (c,n) (3D camera-space z; the sort key's high word).
  *   rect: 2 uint32 per (c,n): {x0 | x1<<16, y0 | y1<<16}, tiles [x0,x1) x [y0,y1).
  *
  * Per-entry gradient partials (written by *_raster_bwd, reduced by *_project_bwd):
@@ -94,12 +96,12 @@ int gsr_selftest_lds_order(int32_t* violations, void* stream);
 
 /* 3D projection (+ adapter activations fused).  params: [N, >=14] fp32 rows with
  * row_stride floats (layout src/gaussian_renderer.py:183-187); viewmats [C,4,4] world->cam
- * row-major; Ks [C,3,3].  Writes rec [C*N*12], rect [C*N*2], isect_count [C*N] and
+ * row-major; Ks [C,3,3].  Writes rec [C*N*12], depth [C*N], rect [C*N*2], isect_count [C*N] and
  * writes tile_count [C*tiles] (zeroed, then accumulated).  Culled Gaussians get count 0. */
 int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride,
                       const float* viewmats, const float* Ks, int C, int width, int height,
                       float near_plane, float far_plane, float radius_clip, float eps2d,
-                      int radius_mode, float* rec, uint32_t* rect, int32_t* isect_count,
+                      int radius_mode, float* rec, float* depth, uint32_t* rect, int32_t* isect_count,
                       int32_t* tile_count, void* stream);
 
 /* 2D projection: params [N, >=9] (layout src/gaussian_renderer.py:314-318).  The tile rect
@@ -126,7 +128,8 @@ int gsr_bin_offsets(const int32_t* isect_count, int64_t CN, const int32_t* tile_
 /* Workspace for gsr_bin_sort, bytes (depends on the I read back from stats). */
 size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT);
 
-/* Emit (tile, key) pairs and sort each tile's list in LDS.  tile_count (the projection's
+/* Emit (tile, key) pairs and sort each tile's list in LDS.  depth: gsr3d_project_fwd's
+ * depth array (GSR_ORDER_DEPTH; may be null for GSR_ORDER_INDEX).  tile_count (the projection's
  * per-tile counts) is consumed: it is counted down to zero while slots are claimed.  Outputs:
  *   sorted_ids [I]: c*N+n per sorted entry (what the rasterizer reads),
  *   k_of_s     [I]: the emission entry k = isect_offset[cn]+j of each sorted entry (j =
@@ -134,7 +137,7 @@ size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT);
  *                   backward stores that entry's partial row.
  * Sort key per entry: (sort word << 32) | c*N+n, sort word = depth float bits (3D, order
  * GSR_ORDER_DEPTH) or c*N+n (2D, GSR_ORDER_INDEX).  max_seg/n_busy from stats. */
-int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_offset,
+int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_offset,
                  const int32_t* tile_offset, int32_t* tile_count,
                  const int32_t* busy_tiles, int C, int64_t N,
                  int width, int height, int order, int64_t n_isect, int32_t max_seg,
@@ -157,7 +160,7 @@ int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_of
  * walk reached), chunk_tile [n_chunks] (owning tile of each chunk) and chunk_list
  * [n_chunks] (the chunks before each tile's tile_end, in no particular order; their count
  * is added to stats->n_active).  stats: the device gsr_bin_stats of gsr_bin_offsets. */
-int gsr3d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
+int gsr3d_raster_fwd(const float* rec, const float* depth, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_order, const int32_t* chunk_base, int C, int width,
                      int height, const float* bg, int32_t n_busy, gsr_bin_stats* stats,
                      float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
@@ -194,10 +197,10 @@ int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t*
 
 /* Reduce the partial rows of each (c,n) (those below their tile's cut, in row order),
  * chain through projection and the adapter activations, sum over cameras: v_params [N,14]
- * (fully overwritten, deterministic).  rec: the forward's splat records (for sort keys). */
+ * (fully overwritten, deterministic).  depth: the projection's depth array (sort keys). */
 int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride,
                       const float* viewmats, const float* Ks, int C, int width, int height,
-                      float eps2d, const float* rec, const uint32_t* rect,
+                      float eps2d, const float* depth, const uint32_t* rect,
                       const int32_t* isect_offset, const int32_t* isect_count,
                       const uint64_t* tile_cut, const float* partial, float* v_params,
                       void* stream);

@@ -159,7 +159,7 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(const int32_t* __rest
 }
 
 // ---------------------------------------------------------------- emission
-__global__ __launch_bounds__(kEmitThreads) void k_emit(const Splat* __restrict__ rec, const uint2* __restrict__ rect,
+__global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__ depth, const uint2* __restrict__ rect,
                                                       const int32_t* __restrict__ isect_offset, int64_t N, int tw,
                                                       int th, int order, int use_lds,
                                                       const int32_t* __restrict__ tile_offset,
@@ -195,7 +195,7 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const Splat* __restrict__
     const uint2 r = rect[cn];
     const int x0 = r.x & 0xffff, x1 = r.x >> 16, y0 = r.y & 0xffff, y1 = r.y >> 16;
     if (x1 <= x0 || y1 <= y0) continue;
-    const uint64_t key = sort_key(rec, cn, order);
+    const uint64_t key = sort_key(depth, cn, order);
     int k = isect_offset[cn];   // emission entries of (c,n): k = offset + rect row-major index
     for (int ty = y0; ty < y1; ++ty)
       for (int tx = x0; tx < x1; ++tx) {
@@ -481,7 +481,7 @@ size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT) {
   return (size_t)(2 * n_isect * sizeof(uint64_t) + 3 * n_isect * sizeof(int32_t) + 256);
 }
 
-int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_offset, const int32_t* tile_offset,
+int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_offset, const int32_t* tile_offset,
                  int32_t* tile_count, const int32_t* busy_tiles, int C, int64_t N, int width, int height, int order, int64_t n_isect,
                  int32_t max_seg, int32_t n_busy, void* workspace, size_t workspace_bytes, int32_t* sorted_ids,
                  int32_t* k_of_s, void* stream) {
@@ -501,7 +501,8 @@ int gsr_bin_sort(const float* rec, const uint32_t* rect, const int32_t* isect_of
   int32_t* k_of_slot = tmpp1 + n_isect;
   const int use_lds = T <= kHistMaxTiles;
   dim3 grid(ceil_div(N, kEmitPerBlock), C);
-  hipLaunchKernelGGL(k_emit, grid, dim3(kEmitThreads), use_lds ? T * sizeof(int) : 0, s, (const Splat*)rec,
+  GSR_REQUIRE(order == GSR_ORDER_INDEX || depth != nullptr, "gsr_bin_sort: depth order needs the depth array");
+  hipLaunchKernelGGL(k_emit, grid, dim3(kEmitThreads), use_lds ? T * sizeof(int) : 0, s, depth,
                      (const uint2*)rect, isect_offset, N, tw, th, order, use_lds, tile_offset, tile_count, keys,
                      k_of_slot);
   GSR_LAUNCH_CHECK("k_emit");

@@ -26,10 +26,11 @@ struct __align__(16) Splat {
 };
 
 // Sort key of (c,n)'s entries: (sort word << 32) | c*N+n.  3D sort word = the depth's float
-// bits (depth > 0: integer order = float order); 2D = the index itself.  Keys are unique
-// inside a tile, so "sorted position < tile_end" <=> "key < key of the entry at tile_end".
-__device__ __forceinline__ uint64_t sort_key(const Splat* rec, int64_t cn, int order) {
-  const uint32_t w = order == GSR_ORDER_DEPTH ? __float_as_uint(rec[cn].p0.w) : (uint32_t)cn;
+// bits (depth > 0: integer order = float order; depth [C*N] from gsr3d_project_fwd); 2D = the
+// index itself (depth unused, may be null).  Keys are unique inside a tile, so "sorted
+// position < tile_end" <=> "key < key of the entry at tile_end".
+__device__ __forceinline__ uint64_t sort_key(const float* depth, int64_t cn, int order) {
+  const uint32_t w = order == GSR_ORDER_DEPTH ? __float_as_uint(depth[cn]) : (uint32_t)cn;
   return ((uint64_t)w << 32) | (uint64_t)(uint32_t)cn;
 }
 

@@ -48,7 +48,8 @@ __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
     const float* __restrict__ params, int64_t N, int64_t stride, const float* __restrict__ viewmats,
     const float* __restrict__ Ks, int W, int H, float near_plane, float far_plane,
     float radius_clip, float eps2d, int tw, int th, int use_lds, Splat* __restrict__ rec,
-    uint2* __restrict__ rect, int32_t* __restrict__ cnt, int32_t* __restrict__ tile_count) {
+    float* __restrict__ depth, uint2* __restrict__ rect, int32_t* __restrict__ cnt,
+    int32_t* __restrict__ tile_count) {
   extern __shared__ int hist[];
   const int c = blockIdx.y;
   const int T = tw * th;
@@ -100,11 +101,14 @@ __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
       y1 = (int)fminf(fmaxf(ceilf(tiy + try_), 0.f), (float)th);
       if (x1 < x0) x1 = x0;
       if (y1 < y0) y1 = y0;
+      // record: the compositing inputs plus the per-Gaussian constants of the exact sub-tile
+      // cull (raster.hip cull_keep): L = ln(opacity * 255) and the edge slopes -B/C, -B/A
       Splat s;
-      s.p0 = make_float4(g.u, g.v, a.op, g.mc[2]);
-      s.p1 = make_float4(0.5f * g.A, g.B, 0.5f * g.C, 0.f);
-      s.p2 = make_float4(a.col[0], a.col[1], a.col[2], 0.f);
+      s.p0 = make_float4(g.u, g.v, a.op, logf(a.op * 255.f));
+      s.p1 = make_float4(0.5f * g.A, g.B, 0.5f * g.C, -g.B / g.C);
+      s.p2 = make_float4(a.col[0], a.col[1], a.col[2], -g.B / g.A);
       rec[cn] = s;
+      depth[cn] = g.mc[2];
       hist_add(hist, gcount, use_lds, x0, x1, y0, y1, tw);
     }
     rect[cn] = make_uint2(pack_rect_lo(x0, x1), pack_rect_lo(y0, y1));
@@ -182,7 +186,7 @@ const char* gsr_last_error(void) { return g_err; }
 int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride, const float* viewmats,
                       const float* Ks, int C, int width, int height, float near_plane,
                       float far_plane, float radius_clip, float eps2d, int radius_mode, float* rec,
-                      uint32_t* rect, int32_t* isect_count, int32_t* tile_count, void* stream) {
+                      float* depth, uint32_t* rect, int32_t* isect_count, int32_t* tile_count, void* stream) {
   GSR_REQUIRE(N >= 0 && C >= 1 && C <= 65535, "gsr3d_project_fwd: bad N=%lld or C=%d", (long long)N, C);
   GSR_REQUIRE(width > 0 && height > 0, "gsr3d_project_fwd: bad image %dx%d", width, height);
   GSR_REQUIRE(row_stride >= 14, "gsr3d_project_fwd: row_stride %lld < 14", (long long)row_stride);
@@ -203,12 +207,12 @@ int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride, const 
   if (radius_mode == GSR_RADIUS_OPACITY_AABB)
     hipLaunchKernelGGL(k_project3d_fwd<GSR_RADIUS_OPACITY_AABB>, grid, dim3(kProjThreads), lds, s,
                        params, N, row_stride, viewmats, Ks, width, height, near_plane, far_plane,
-                       radius_clip, eps2d, tw, th, use_lds, (Splat*)rec, (uint2*)rect, isect_count,
+                       radius_clip, eps2d, tw, th, use_lds, (Splat*)rec, depth, (uint2*)rect, isect_count,
                        tile_count);
   else
     hipLaunchKernelGGL(k_project3d_fwd<GSR_RADIUS_ISOTROPIC_3SIGMA>, grid, dim3(kProjThreads), lds, s,
                        params, N, row_stride, viewmats, Ks, width, height, near_plane, far_plane,
-                       radius_clip, eps2d, tw, th, use_lds, (Splat*)rec, (uint2*)rect, isect_count,
+                       radius_clip, eps2d, tw, th, use_lds, (Splat*)rec, depth, (uint2*)rect, isect_count,
                        tile_count);
   GSR_LAUNCH_CHECK("k_project3d_fwd");
   return GSR_OK;

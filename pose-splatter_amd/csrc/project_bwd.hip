@@ -65,7 +65,7 @@ __global__ __launch_bounds__(kBwdThreads) GSR_PB_ATTR void k_project3d_bwd(
     const float* __restrict__ params, int64_t N, int64_t stride, const float* __restrict__ viewmats,
     const float* __restrict__ Ks, int C, int W, int H, float eps2d, int tw, int th, const uint2* __restrict__ rect,
     const int32_t* __restrict__ isect_offset, const int32_t* __restrict__ isect_count,
-    const Splat* __restrict__ rec, const uint64_t* __restrict__ tile_cut, const float* __restrict__ partial,
+    const float* __restrict__ depth, const uint64_t* __restrict__ tile_cut, const float* __restrict__ partial,
     int CPB, int G, float* __restrict__ v_params) {
   __shared__ float s_con[kBwdThreads][kContrib + 1];
   __shared__ int s_any[kBwdThreads];
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(kBwdThreads) GSR_PB_ATTR void k_project3d_bwd(
       float acc[kPartial];
 #pragma unroll
       for (int v = 0; v < kPartial; ++v) acc[v] = 0.f;
-      gather_partials(rect[cn], tw, (int64_t)c * T, sort_key(rec, cn, GSR_ORDER_DEPTH), isect_offset[cn],
+      gather_partials(rect[cn], tw, (int64_t)c * T, sort_key(depth, cn, GSR_ORDER_DEPTH), isect_offset[cn],
                       tile_cut, partial, acc);
       const Cam cam = load_cam(viewmats + c * 16, Ks + c * 9);
       // recompute the forward geometry (not culled: it has intersections)
@@ -305,7 +305,7 @@ using namespace gsr;
 extern "C" {
 
 int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride, const float* viewmats, const float* Ks,
-                      int C, int width, int height, float eps2d, const float* rec, const uint32_t* rect,
+                      int C, int width, int height, float eps2d, const float* depth, const uint32_t* rect,
                       const int32_t* isect_offset, const int32_t* isect_count, const uint64_t* tile_cut,
                       const float* partial, float* v_params, void* stream) {
   GSR_REQUIRE(N >= 0 && C >= 1 && width > 0 && height > 0, "gsr3d_project_bwd: bad arguments");
@@ -316,7 +316,7 @@ int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride, const 
   const int G = kBwdThreads / CPB;                       // Gaussians per workgroup
   hipLaunchKernelGGL(k_project3d_bwd, dim3(ceil_div(N, G)), dim3(kBwdThreads), 0, (hipStream_t)stream, params, N,
                      row_stride, viewmats, Ks, C, width, height, eps2d, tw, th, (const uint2*)rect, isect_offset,
-                     isect_count, (const Splat*)rec, tile_cut, partial, CPB, G, v_params);
+                     isect_count, depth, tile_cut, partial, CPB, G, v_params);
   GSR_LAUNCH_CHECK("k_project3d_bwd");
   return GSR_OK;
 }

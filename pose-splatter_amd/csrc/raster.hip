@@ -20,6 +20,7 @@ __device__ unsigned long long g_cnt[16];
 #define GSR_CNT_ADD(i, v) atomicAdd(&g_cnt[i], (unsigned long long)(v))
 #define GSR_CNT_MAX(i, v) atomicMax(&g_cnt[i], (unsigned long long)(v))
 #define GSR_CLOCK() clock64()
+__device__ unsigned long long g_blk[32768][3];   // per forward workgroup: start, end (s_memrealtime), list length
 #else
 #define GSR_CNT_ADD(i, v)
 #define GSR_CNT_MAX(i, v)
@@ -29,6 +30,7 @@ __device__ unsigned long long g_cnt[16];
 constexpr int kRasterThreads = 256;
 constexpr int kChunk3 = GSR_CHUNK;   // backward work unit: list entries per chunk
 constexpr int kFillBlocks = 1024;    // workgroups that fill the empty tiles
+constexpr int kFwdLdsPad = 28000;    // 12.3 KB static + pad: 4 forward workgroups per CU (160 KB)
 
 
 __device__ __forceinline__ void tile_coords(int ct, int tw, int th, int& c, int& ty, int& tx) {
@@ -49,19 +51,21 @@ __device__ __forceinline__ void tile_coords(int ct, int tw, int th, int& c, int&
 // clamped 1-D optimum.  With dx fixed to the mean's nearest x in B, the best dy is
 // clamp(-b dx / 2c); likewise for y; the smaller of the two values is the box minimum (the
 // non-facing "edge" evaluates a segment inside B, never below the true minimum).  A small
-// relative margin absorbs rounding, so culling changes the work, never the result.
+// relative margin absorbs rounding, so culling changes the work, never the result.  The
+// per-Gaussian constants (L and the two edge slopes) come precomputed in the record's .w
+// slots (gsr3d_project_fwd), so the test has no transcendental.
 template <bool IS2D>
-__device__ __forceinline__ bool cull_keep(const float4 p0, const float4 p1, float bx0, float bx1, float by0,
-                                          float by1, float cut) {
-  const float ratio = IS2D ? p0.z / cut : p0.z * 255.f;
-  if (!(ratio >= 1.f)) return false;
+__device__ __forceinline__ bool cull_keep(const float4 p0, const float4 p1, const float4 p2, float bx0, float bx1,
+                                          float by0, float by1) {
+  static_assert(!IS2D, "the cull constants are written by the 3D projection only");
+  const float L = p0.w;   // ln(opacity * 255): < 0 never reaches the 1/255 skip threshold
+  if (!(L >= 0.f)) return false;
   const float a = p1.x, b = p1.y, c = p1.z;
   if (!(a > 0.f && c > 0.f && 4.f * a * c > b * b)) return true;   // not positive definite: keep
-  const float L = __builtin_amdgcn_logf(ratio) * 0.69314718f;      // v_log is log2
   const float dxe = p0.x - fminf(fmaxf(p0.x, bx0), bx1);
   const float dye = p0.y - fminf(fmaxf(p0.y, by0), by1);
-  const float dy1 = fminf(fmaxf(-b * dxe * __builtin_amdgcn_rcpf(2.f * c), p0.y - by1), p0.y - by0);
-  const float dx2 = fminf(fmaxf(-b * dye * __builtin_amdgcn_rcpf(2.f * a), p0.x - bx1), p0.x - bx0);
+  const float dy1 = fminf(fmaxf(p1.w * dxe, p0.y - by1), p0.y - by0);   // p1.w = -b / 2c
+  const float dx2 = fminf(fmaxf(p2.w * dye, p0.x - bx1), p0.x - bx0);   // p2.w = -b / 2a
   const float s1 = a * dxe * dxe + b * dxe * dy1 + c * dy1 * dy1;
   const float s2 = a * dx2 * dx2 + b * dx2 * dye + c * dye * dye;
   return fminf(s1, s2) <= L * 1.001f + 1e-3f;
@@ -191,6 +195,9 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_fwd(
   // XCD-aware mapping: workgroups are dealt to the 8 XCDs round-robin by id, so the four
   // quadrant workgroups of a tile get ids 32k + 8*quad + x (same id mod 8): they share one
   // XCD's L2 for the tile's records.  Busy tile u = 8k + x, in longest-first order.
+#ifdef GSR_EXP_COUNT
+  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   const int u = ((int)blockIdx.x >> 5) * 8 + ((int)blockIdx.x & 7);
   const int quad = ((int)blockIdx.x >> 3) & 3;
   if (u >= n_busy) return;
@@ -255,7 +262,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_fwd(
       Ts = T;
       ++kcur;
     }
-    const bool keep = (b0 + lane < end) && cull_keep<false>(c0, c1, bx0, bx1, by0, by1, 0.f);
+    const bool keep = (b0 + lane < end) && cull_keep<false>(c0, c1, c2, bx0, bx1, by0, by1);
     const unsigned long long m = __ballot(keep);
     const int n = __popcll(m);
     cnt_s += n;
@@ -361,12 +368,19 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_fwd(
   if (q == 0 && last >= 0) atomicMax(&s_max, last);
   __syncthreads();
   if (threadIdx.x == 0 && s_max >= 0) atomicMax(&tile_end[ct], s_max);   // finalised below
+#ifdef GSR_EXP_COUNT
+  if (threadIdx.x == 0 && blockIdx.x < 32768) {
+    g_blk[blockIdx.x][0] = rt0;
+    g_blk[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+    g_blk[blockIdx.x][2] = (unsigned long long)(end - start);
+  }
+#endif
 }
 
 // Per busy tile: tile_end = 1 + max last over the tile's four quadrant workgroups (or the
 // tile's start), the cut key, and the tile's active chunks appended to the backward's list.
 __global__ __launch_bounds__(kRasterThreads) void k_raster3d_finalize(
-    const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
+    const float* __restrict__ depth, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ order, int n_busy, const int32_t* __restrict__ chunk_base,
     int32_t* __restrict__ tile_end, uint64_t* __restrict__ tile_cut, gsr_bin_stats* __restrict__ stats,
     int32_t* __restrict__ chunk_list) {
@@ -377,7 +391,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_finalize(
   const int m = tile_end[ct];
   const int te = m >= 0 ? m + 1 : start;
   tile_end[ct] = te;
-  tile_cut[ct] = te < end ? sort_key(rec, ids[te], GSR_ORDER_DEPTH) : ~0ull;
+  tile_cut[ct] = te < end ? sort_key(depth, ids[te], GSR_ORDER_DEPTH) : ~0ull;
   const int nact = (te - start + kChunk3 - 1) / kChunk3;
   if (nact > 0) {
     const int pos = atomicAdd(&stats->n_active, nact);
@@ -459,7 +473,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster2d_fwd(
   if (threadIdx.x == 0) {
     const int te = s_max >= 0 ? s_max + 1 : start;
     tile_end[ct] = te;
-    tile_cut[ct] = te < end ? sort_key(rec, ids[te], GSR_ORDER_INDEX) : ~0ull;
+    tile_cut[ct] = te < end ? sort_key(nullptr, ids[te], GSR_ORDER_INDEX) : ~0ull;
   }
 }
 
@@ -595,7 +609,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
   for (int q = 3; q >= 0; --q) {
     const int k = q * 64 + st.lane;
     const bool keep = k < n && (b0 + k) <= wlast &&
-                      cull_keep<false>(s_p0[k], s_p1[k], st.bx0, st.bx1, st.by0, st.by1, 0.f);
+                      cull_keep<false>(s_p0[k], s_p1[k], s_p2[k], st.bx0, st.bx1, st.by0, st.by1);
     const unsigned long long mk = __ballot(keep);
     if (keep) {
       const unsigned long long above = st.lane == 63 ? 0ull : (mk >> (st.lane + 1));
@@ -830,6 +844,10 @@ using namespace gsr;
 extern "C" {
 
 #ifdef GSR_EXP_COUNT
+int gsr_debug_blocks(unsigned long long* out) {
+  (void)hipDeviceSynchronize();
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gsr::g_blk), sizeof(gsr::g_blk)) == hipSuccess ? 0 : -2;
+}
 int gsr_debug_counters(unsigned long long* out, int reset) {
   (void)hipDeviceSynchronize();
   (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(gsr::g_cnt), sizeof(gsr::g_cnt));
@@ -849,7 +867,7 @@ int gsr_selftest_reduce64(float* out, void* stream) {
   return GSR_OK;
 }
 
-int gsr3d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
+int gsr3d_raster_fwd(const float* rec, const float* depth, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_order, const int32_t* chunk_base, int C, int width, int height,
                      const float* bg, int32_t n_busy, gsr_bin_stats* stats, float* rgb, float* alpha,
                      float* final_T, int32_t* last, int32_t* tile_end, uint64_t* tile_cut, float* chunk_state,
@@ -866,14 +884,16 @@ int gsr3d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t*
     set_error("gsr3d_raster_fwd: tile_end memset failed");
     return GSR_ELAUNCH;
   }
-  hipLaunchKernelGGL(k_raster3d_fwd, dim3((unsigned)(busy_grid(n_busy) + n_fill)), dim3(kRasterThreads), 0, s,
+  // Dynamic-LDS padding caps the forward at 4 workgroups per CU (measured: 4 and 5 per CU
+  // beat 6, whose extra tiles in flight spill each XCD's L2; 3 starves the CU).
+  hipLaunchKernelGGL(k_raster3d_fwd, dim3((unsigned)(busy_grid(n_busy) + n_fill)), dim3(kRasterThreads), kFwdLdsPad, s,
                      (const Splat*)rec, sorted_ids, tile_offset, tile_order, width, height, tw, th, bg, rgb, alpha,
                      final_T, last, tile_end, (float4*)chunk_state, chunk_base, chunk_tile, (int)n_busy, CT,
                      tile_cut);
   GSR_LAUNCH_CHECK("k_raster3d_fwd");
   if (n_busy > 0) {
     hipLaunchKernelGGL(k_raster3d_finalize, dim3(ceil_div(n_busy, kRasterThreads)), dim3(kRasterThreads), 0, s,
-                       (const Splat*)rec, sorted_ids, tile_offset, tile_order, (int)n_busy, chunk_base, tile_end,
+                       depth, sorted_ids, tile_offset, tile_order, (int)n_busy, chunk_base, tile_end,
                        tile_cut, stats, chunk_list);
   }
   GSR_LAUNCH_CHECK("k_raster3d_finalize");

@@ -128,7 +128,7 @@ class _Arena:
 
 _I32, _I64, _F32 = torch.int32, torch.int64, torch.float32
 # tensor views exposed for tests / debugging: name -> (arena attribute, dtype)
-_VIEWS = {"rec": ("pre", _F32), "rect": ("pre", _I32), "cnt": ("pre", _I32), "tile_cnt": ("pre", _I32),
+_VIEWS = {"rec": ("pre", _F32), "depth": ("pre", _F32), "rect": ("pre", _I32), "cnt": ("pre", _I32), "tile_cnt": ("pre", _I32),
           "isect_off": ("pre", _I32), "tile_off": ("pre", _I32), "busy": ("pre", _I32),
           "chunk_base": ("pre", _I32), "stats_dev": ("pre", _I32),
           "sorted_ids": ("post", _I32), "k_of_s": ("post", _I32), "final_T": ("post", _F32),
@@ -161,7 +161,7 @@ class _Bins:
         CN = max(C * N, 1)
         L = lib()
         self.pre = _Arena(device, {
-            "rec": CN * 48, "rect": CN * 8, "cnt": CN * 4, "tile_cnt": self.CT * 4, "isect_off": CN * 4,
+            "rec": CN * 48, "depth": CN * 4, "rect": CN * 8, "cnt": CN * 4, "tile_cnt": self.CT * 4, "isect_off": CN * 4,
             "tile_off": (self.CT + 1) * 4, "busy": self.CT * 4, "chunk_base": (self.CT + 1) * 4,
             "stats_dev": 32, "offsets_ws": int(L.gsr_bin_offsets_workspace(C * N, self.CT))})
         self.p = dict(self.pre.ptr)
@@ -228,7 +228,7 @@ class _Bins:
         L = lib()
         p = self.p
         with _timed("bin_sort"):
-          check(L.gsr_bin_sort(p["rec"], p["rect"], p["isect_off"], p["tile_off"], p["tile_cnt"], p["busy"],
+          check(L.gsr_bin_sort(p["depth"] if order == _lib.ORDER_DEPTH else None, p["rect"], p["isect_off"], p["tile_off"], p["tile_cnt"], p["busy"],
                              self.C, self.N,
                              self.W, self.H, order, self.n_isect, self.max_seg, self.n_busy, p["sort_ws"],
                              self.post.off["sort_ws"][1], p["sorted_ids"], p["k_of_s"], stream), "gsr_bin_sort")
@@ -281,7 +281,7 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
     with _timed("project3d_fwd"):
       check(L.gsr3d_project_fwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height,
                               opts.near_plane, opts.far_plane, opts.radius_clip, opts.eps2d,
-                              opts.radius_mode, q["rec"], q["rect"], q["cnt"], q["tile_cnt"], stream),
+                              opts.radius_mode, q["rec"], q["depth"], q["rect"], q["cnt"], q["tile_cnt"], stream),
           "gsr3d_project_fwd")
     b.guess_post(with_chunks=True)
     b.offsets(stream)
@@ -290,7 +290,7 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
     rgb = torch.empty(C, height, width, 3, device=dev, dtype=torch.float32)
     alpha = torch.empty(C, height, width, device=dev, dtype=torch.float32)
     with _timed("raster3d_fwd"):
-      check(L.gsr3d_raster_fwd(q["rec"], q["sorted_ids"], q["tile_off"], q["busy"], q["chunk_base"],
+      check(L.gsr3d_raster_fwd(q["rec"], q["depth"], q["sorted_ids"], q["tile_off"], q["busy"], q["chunk_base"],
                              C, width, height, _ptr(bgc), b.n_busy, q["stats_dev"], _ptr(rgb), _ptr(alpha),
                              q["final_T"], q["last"], q["tile_end"], q["tile_cut"], q["chunk_state"],
                              q["chunk_tile"], q["chunk_list"], stream), "gsr3d_raster_fwd")
@@ -368,7 +368,7 @@ class _Render3D(torch.autograd.Function):
                   "gsr3d_raster_bwd")
             with _timed("project3d_bwd"):
               check(L.gsr3d_project_bwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height, opts.eps2d,
-                                      q["rec"], q["rect"], q["isect_off"], q["cnt"], q["tile_cut"],
+                                      q["depth"], q["rect"], q["isect_off"], q["cnt"], q["tile_cut"],
                                       _ptr(partial), _ptr(v_params), stream),
                   "gsr3d_project_bwd")
         return v_params.view(ctx.params_shape), None, None, None, None, None, None

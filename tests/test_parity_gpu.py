@@ -134,7 +134,7 @@ def test_3d_binning_exact(cuda):
     y0, y1 = rect[:, 1] & 0xFFFF, rect[:, 1] >> 16
     cnt = b.cnt.cpu().to(torch.int64)
     assert torch.equal(cnt, (x1 - x0) * (y1 - y0))
-    depth = b.rec.cpu().view(C * N, 12)[:, 3].contiguous()
+    depth = b.depth.cpu()[:C * N].contiguous()
     tw, th = (W + 15) // 16, (H + 15) // 16
     T = tw * th
     # expected lists: (camera, tile) then (depth bits, c*N+n)

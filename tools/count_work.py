@@ -48,3 +48,23 @@ for n, v in zip(["sort_cycles_load", "sort_cycles_radix", "sort_cycles_out", "so
     print(f"{n:28s} {v}")
 st = R.last_stats()
 print({k: v for k, v in st.items() if not k.startswith("_")})
+
+# per-workgroup timeline of the last forward (s_memrealtime ticks, 100 MHz)
+fbk = L.gsr_debug_blocks
+fbk.argtypes = [ctypes.c_void_p]
+import numpy as np
+blk = np.zeros((32768, 3), dtype=np.uint64)
+fbk(blk.ctypes.data)
+nb = 32 * ((st["n_busy"] + 7) // 8)
+b = blk[:nb].astype(np.int64)
+b = b[b[:, 1] > 0]
+t0 = b[:, 0].min()
+s, e, ln = (b[:, 0] - t0) / 100.0, (b[:, 1] - t0) / 100.0, b[:, 2]   # microseconds
+print("busy blocks", len(b), "span (first start .. last end) us", round(e.max() - s.min(), 1))
+for k in np.argsort(-e)[:8]:
+    print(f"  len {ln[k]:6d} start {s[k]:7.1f} end {e[k]:7.1f} dur {e[k]-s[k]:7.1f}")
+for lo, hi in [(0, 512), (512, 2048), (2048, 4096), (4096, 8192), (8192, 1 << 30)]:
+    m = (ln >= lo) & (ln < hi)
+    if m.any():
+        print(f"  len [{lo},{hi}): n={m.sum():4d} mean dur {np.mean(e[m]-s[m]):7.1f} max dur {np.max(e[m]-s[m]):7.1f} "
+              f"mean start {np.mean(s[m]):6.1f} max end {np.max(e[m]):6.1f}")
