@@ -28,14 +28,6 @@ __device__ __forceinline__ void gather_partials(const uint2 r, int tw, int64_t c
   const float4* row = reinterpret_cast<const float4*>(partial + (int64_t)off * kPartialStride);
   for (int ty = y0; ty < y1; ++ty) {
     for (int tx = x0; tx < x1; ++tx, row += 3) {
-#ifdef GSR_PB_SPEC
-      const float4 a = row[0], b = row[1];
-      const float c = row[2].x;
-      const bool on = key < tile_cut[ct_base + ty * tw + tx];
-      acc[0] += on ? a.x : 0.f; acc[1] += on ? a.y : 0.f; acc[2] += on ? a.z : 0.f; acc[3] += on ? a.w : 0.f;
-      acc[4] += on ? b.x : 0.f; acc[5] += on ? b.y : 0.f; acc[6] += on ? b.z : 0.f; acc[7] += on ? b.w : 0.f;
-      acc[8] += on ? c : 0.f;
-#else
       if (key < tile_cut[ct_base + ty * tw + tx]) {
         const float4 a = row[0], b = row[1];
         const float c = row[2].x;
@@ -43,7 +35,6 @@ __device__ __forceinline__ void gather_partials(const uint2 r, int tw, int64_t c
         acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
         acc[8] += c;
       }
-#endif
     }
   }
 }
@@ -56,12 +47,7 @@ __device__ __forceinline__ void gather_partials(const uint2 r, int tw, int64_t c
 // chain (rotation / scale / quaternion normalisation / adapter activations).
 constexpr int kContrib = 16;   // v_m[3], V_M[9], v_col[3], v_op
 
-#ifdef GSR_PB_OCC
-#define GSR_PB_ATTR __attribute__((amdgpu_waves_per_eu(GSR_PB_OCC)))
-#else
-#define GSR_PB_ATTR
-#endif
-__global__ __launch_bounds__(kBwdThreads) GSR_PB_ATTR void k_project3d_bwd(
+__global__ __launch_bounds__(kBwdThreads) void k_project3d_bwd(
     const float* __restrict__ params, int64_t N, int64_t stride, const float* __restrict__ viewmats,
     const float* __restrict__ Ks, int C, int W, int H, float eps2d, int tw, int th, const uint2* __restrict__ rect,
     const int32_t* __restrict__ isect_offset, const int32_t* __restrict__ isect_count,
