@@ -68,6 +68,8 @@ extern "C" {
 #define GSR_RADIUS_ISOTROPIC_3SIGMA 1  /* gsplat <= 1.4: ceil(3*sqrt(lambda_max))       */
 #define GSR_ORDER_DEPTH 0              /* 3D: per-tile list ordered by (depth, c*N+n)   */
 #define GSR_ORDER_INDEX 1              /* 2D: per-tile list ordered by parameter index  */
+#define GSR_INPUT_ADAPTER 0            /* 3D rows: raw pose-splatter params (adapter)   */
+#define GSR_INPUT_GSPLAT 1             /* 3D rows: activated gsplat rasterization() inputs */
 
 #define GSR_CHUNK 256                  /* list entries per backward work unit (chunk)   */
 #define GSR_PARTIAL_STRIDE 12          /* floats per partial row (9 used, 16 B aligned) */
@@ -95,14 +97,17 @@ int gsr_selftest_lds_order(int32_t* violations, void* stream);
 /* ---------------------------------------------------------------- (a) projection */
 
 /* 3D projection (+ adapter activations fused).  params: [N, >=14] fp32 rows with
- * row_stride floats (layout src/gaussian_renderer.py:183-187); viewmats [C,4,4] world->cam
+ * row_stride floats (layout src/gaussian_renderer.py:183-187: mean 0:3, scale 3:6, quat
+ * 6:10, colour 10:13, opacity 13).  input_mode GSR_INPUT_ADAPTER: raw values through the
+ * adapter's activations; GSR_INPUT_GSPLAT: activated values as gsplat's rasterization()
+ * takes them (no exp/sigmoid/clamp; the quaternion is only renormalised).  viewmats [C,4,4] world->cam
  * row-major; Ks [C,3,3].  Writes rec [C*N*12], depth [C*N], rect [C*N*2], isect_count [C*N] and
  * writes tile_count [C*tiles] (zeroed, then accumulated).  Culled Gaussians get count 0. */
 int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride,
                       const float* viewmats, const float* Ks, int C, int width, int height,
                       float near_plane, float far_plane, float radius_clip, float eps2d,
-                      int radius_mode, float* rec, float* depth, uint32_t* rect, int32_t* isect_count,
-                      int32_t* tile_count, void* stream);
+                      int radius_mode, int input_mode, float* rec, float* depth, uint32_t* rect,
+                      int32_t* isect_count, int32_t* tile_count, void* stream);
 
 /* 2D projection: params [N, >=9] (layout src/gaussian_renderer.py:314-318).  The tile rect
  * covers every pixel where opacity*exp(-q) >= eps_cut (the reference is dense; eps_cut
@@ -200,7 +205,7 @@ int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t*
  * (fully overwritten, deterministic).  depth: the projection's depth array (sort keys). */
 int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride,
                       const float* viewmats, const float* Ks, int C, int width, int height,
-                      float eps2d, const float* depth, const uint32_t* rect,
+                      float eps2d, int input_mode, const float* depth, const uint32_t* rect,
                       const int32_t* isect_offset, const int32_t* isect_count,
                       const uint64_t* tile_cut, const float* partial, float* v_params,
                       void* stream);

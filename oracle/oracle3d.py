@@ -411,23 +411,30 @@ class _Raster3D(torch.autograd.Function):
 
 def render3d(params, viewmats, Ks, width, height, background, *,
              radius_mode=Ref3D.RADIUS_OPACITY_AABB, near=Ref3D.NEAR, far=Ref3D.FAR,
-             radius_clip=Ref3D.RADIUS_CLIP, eps2d=Ref3D.EPS2D, return_meta=False):
+             radius_clip=Ref3D.RADIUS_CLIP, eps2d=Ref3D.EPS2D, return_meta=False, activated=False):
     """Full oracle of GaussianRenderer3D.render for C cameras: rgb [C,H,W,3], alpha [C,H,W].
 
-    Differentiable w.r.t. ``params`` ([N,14]); viewmats [C,4,4], Ks [C,3,3], background [3].
+    Differentiable w.r.t. ``params`` ([N,14]); viewmats [C,4,4], Ks [C,3,3], background [3]
+    or per-camera [C,3].  ``activated=True`` restates a direct gsplat ``rasterization`` call
+    (src/model.py:339-365): the rows already hold scales, opacities and colours, and the
+    quaternion is only renormalised inside the rotation (quat_to_rotmat).
     """
     if params.shape[1] != 14:
         raise ValueError(f"Expected 14 parameters per Gaussian, got {params.shape[1]}")
     dt = params.dtype
     C = viewmats.shape[0]
-    means, quats, scales, colors, opac = activations3d(params)
+    if activated:
+        means, scales, quats = params[:, 0:3], params[:, 3:6], params[:, 6:10]
+        colors, opac = params[:, 10:13], params[:, 13]
+    else:
+        means, quats, scales, colors, opac = activations3d(params)
     proj = project3d(means, quats, scales, opac, viewmats, Ks, width, height, near=near, far=far,
                      radius_clip=radius_clip, eps2d=eps2d, radius_mode=radius_mode)
     offsets, ids = isect_tiles(proj.means2d, proj.radii, proj.depths, width, height)
     N = params.shape[0]
     colors_c = colors[None].expand(C, N, 3)
     opac_c = opac[None].expand(C, N)
-    bg = background.to(dt).view(1, 3).expand(C, 3).contiguous()
+    bg = background.to(dt).reshape(-1, 3).expand(C, 3).contiguous()
     rgb, alpha, last = _Raster3D.apply(proj.means2d, proj.conics, colors_c, opac_c, bg,
                                        offsets, ids, width, height)
     if return_meta:

@@ -47,7 +47,7 @@ template <int RMODE>
 __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
     const float* __restrict__ params, int64_t N, int64_t stride, const float* __restrict__ viewmats,
     const float* __restrict__ Ks, int W, int H, float near_plane, float far_plane,
-    float radius_clip, float eps2d, int tw, int th, int use_lds, Splat* __restrict__ rec,
+    float radius_clip, float eps2d, int input_mode, int tw, int th, int use_lds, Splat* __restrict__ rec,
     float* __restrict__ depth, uint2* __restrict__ rect, int32_t* __restrict__ cnt,
     int32_t* __restrict__ tile_count) {
   extern __shared__ int hist[];
@@ -63,7 +63,7 @@ __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
   const int64_t n1 = min(N, n0 + kProjPerBlock);
   for (int64_t n = n0 + threadIdx.x; n < n1; n += blockDim.x) {
     const int64_t cn = (int64_t)c * N + n;
-    const Act3D a = activate3d(params + n * stride);
+    const Act3D a = activate3d(params + n * stride, input_mode);
     Geo3D g;
     bool ok = geo3d(a, cam, W, H, near_plane, far_plane, eps2d, g);
     float rx = 0.f, ry = 0.f;
@@ -185,13 +185,16 @@ const char* gsr_last_error(void) { return g_err; }
 
 int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride, const float* viewmats,
                       const float* Ks, int C, int width, int height, float near_plane,
-                      float far_plane, float radius_clip, float eps2d, int radius_mode, float* rec,
-                      float* depth, uint32_t* rect, int32_t* isect_count, int32_t* tile_count, void* stream) {
+                      float far_plane, float radius_clip, float eps2d, int radius_mode, int input_mode,
+                      float* rec, float* depth, uint32_t* rect, int32_t* isect_count, int32_t* tile_count,
+                      void* stream) {
   GSR_REQUIRE(N >= 0 && C >= 1 && C <= 65535, "gsr3d_project_fwd: bad N=%lld or C=%d", (long long)N, C);
   GSR_REQUIRE(width > 0 && height > 0, "gsr3d_project_fwd: bad image %dx%d", width, height);
   GSR_REQUIRE(row_stride >= 14, "gsr3d_project_fwd: row_stride %lld < 14", (long long)row_stride);
   GSR_REQUIRE(radius_mode == GSR_RADIUS_OPACITY_AABB || radius_mode == GSR_RADIUS_ISOTROPIC_3SIGMA,
               "gsr3d_project_fwd: bad radius_mode %d", radius_mode);
+  GSR_REQUIRE(input_mode == GSR_INPUT_ADAPTER || input_mode == GSR_INPUT_GSPLAT,
+              "gsr3d_project_fwd: bad input_mode %d", input_mode);
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   GSR_REQUIRE(tw < 65536 && th < 65536, "gsr3d_project_fwd: image too large");
   if (hipMemsetAsync(tile_count, 0, (size_t)C * tw * th * sizeof(int32_t), (hipStream_t)stream) != hipSuccess) {
@@ -207,12 +210,12 @@ int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride, const 
   if (radius_mode == GSR_RADIUS_OPACITY_AABB)
     hipLaunchKernelGGL(k_project3d_fwd<GSR_RADIUS_OPACITY_AABB>, grid, dim3(kProjThreads), lds, s,
                        params, N, row_stride, viewmats, Ks, width, height, near_plane, far_plane,
-                       radius_clip, eps2d, tw, th, use_lds, (Splat*)rec, depth, (uint2*)rect, isect_count,
+                       radius_clip, eps2d, input_mode, tw, th, use_lds, (Splat*)rec, depth, (uint2*)rect, isect_count,
                        tile_count);
   else
     hipLaunchKernelGGL(k_project3d_fwd<GSR_RADIUS_ISOTROPIC_3SIGMA>, grid, dim3(kProjThreads), lds, s,
                        params, N, row_stride, viewmats, Ks, width, height, near_plane, far_plane,
-                       radius_clip, eps2d, tw, th, use_lds, (Splat*)rec, depth, (uint2*)rect, isect_count,
+                       radius_clip, eps2d, input_mode, tw, th, use_lds, (Splat*)rec, depth, (uint2*)rect, isect_count,
                        tile_count);
   GSR_LAUNCH_CHECK("k_project3d_fwd");
   return GSR_OK;

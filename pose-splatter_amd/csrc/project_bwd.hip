@@ -49,7 +49,8 @@ constexpr int kContrib = 16;   // v_m[3], V_M[9], v_col[3], v_op
 
 __global__ __launch_bounds__(kBwdThreads) void k_project3d_bwd(
     const float* __restrict__ params, int64_t N, int64_t stride, const float* __restrict__ viewmats,
-    const float* __restrict__ Ks, int C, int W, int H, float eps2d, int tw, int th, const uint2* __restrict__ rect,
+    const float* __restrict__ Ks, int C, int W, int H, float eps2d, int input_mode, int tw, int th,
+    const uint2* __restrict__ rect,
     const int32_t* __restrict__ isect_offset, const int32_t* __restrict__ isect_count,
     const float* __restrict__ depth, const uint64_t* __restrict__ tile_cut, const float* __restrict__ partial,
     int CPB, int G, float* __restrict__ v_params) {
@@ -68,7 +69,7 @@ __global__ __launch_bounds__(kBwdThreads) void k_project3d_bwd(
   float v_op = 0.f;
   int any = 0;
   if (active) {
-    const Act3D a = activate3d(params + n * stride);
+    const Act3D a = activate3d(params + n * stride, input_mode);
     Geo3D g;
     for (int c = slot; c < C; c += CPB) {
       const int64_t cn = (int64_t)c * N + n;
@@ -206,7 +207,7 @@ __global__ __launch_bounds__(kBwdThreads) void k_project3d_bwd(
     for (int k = 0; k < 14; ++k) out[k] = 0.f;
     return;
   }
-  const Act3D a = activate3d(params + n * stride);
+  const Act3D a = activate3d(params + n * stride, input_mode);
   // M = R diag(s):  v_R = V_M diag(s),  v_s = sum_r V_M[r][k] R[r][k]
   float Rq[9], qn[4], qinv;
   quat_rotmat(a.q, Rq, qn, &qinv);
@@ -230,12 +231,22 @@ __global__ __launch_bounds__(kBwdThreads) void k_project3d_bwd(
   const float dqn = vq[0] * w + vq[1] * x + vq[2] * y + vq[3] * z;
   float vqa[4] = {(vq[0] - dqn * w) * qinv, (vq[1] - dqn * x) * qinv, (vq[2] - dqn * y) * qinv,
                   (vq[3] - dqn * z) * qinv};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) out[k] = v_m[k];
+  if (input_mode == GSR_INPUT_GSPLAT) {   // gradients w.r.t. the activated gsplat inputs
+#pragma unroll
+    for (int k = 0; k < 3; ++k) out[3 + k] = v_s[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) out[6 + k] = vqa[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) out[10 + k] = v_col[k];
+    out[13] = v_op;
+    return;
+  }
   // adapter: qa = q / (r + 1e-8), r = |q|:  v_q = v_qa/(r+eps) - q (q.v_qa) / (r (r+eps)^2)
   const float den = a.rq + 1e-8f;
   const float qdot = a.qraw[0] * vqa[0] + a.qraw[1] * vqa[1] + a.qraw[2] * vqa[2] + a.qraw[3] * vqa[3];
   const float coef = qdot / (a.rq * den * den);
-#pragma unroll
-  for (int k = 0; k < 3; ++k) out[k] = v_m[k];
 #pragma unroll
   for (int k = 0; k < 3; ++k) out[3 + k] = v_s[k] * a.s[k];
 #pragma unroll
@@ -291,18 +302,21 @@ using namespace gsr;
 extern "C" {
 
 int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride, const float* viewmats, const float* Ks,
-                      int C, int width, int height, float eps2d, const float* depth, const uint32_t* rect,
+                      int C, int width, int height, float eps2d, int input_mode, const float* depth,
+                      const uint32_t* rect,
                       const int32_t* isect_offset, const int32_t* isect_count, const uint64_t* tile_cut,
                       const float* partial, float* v_params, void* stream) {
   GSR_REQUIRE(N >= 0 && C >= 1 && width > 0 && height > 0, "gsr3d_project_bwd: bad arguments");
   GSR_REQUIRE(row_stride >= 14, "gsr3d_project_bwd: row_stride < 14");
+  GSR_REQUIRE(input_mode == GSR_INPUT_ADAPTER || input_mode == GSR_INPUT_GSPLAT,
+              "gsr3d_project_bwd: bad input_mode %d", input_mode);
   if (N == 0) return GSR_OK;
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   const int CPB = C < kBwdThreads ? C : kBwdThreads;   // camera slots per Gaussian
   const int G = kBwdThreads / CPB;                       // Gaussians per workgroup
   hipLaunchKernelGGL(k_project3d_bwd, dim3(ceil_div(N, G)), dim3(kBwdThreads), 0, (hipStream_t)stream, params, N,
-                     row_stride, viewmats, Ks, C, width, height, eps2d, tw, th, (const uint2*)rect, isect_offset,
-                     isect_count, depth, tile_cut, partial, CPB, G, v_params);
+                     row_stride, viewmats, Ks, C, width, height, eps2d, input_mode, tw, th, (const uint2*)rect,
+                     isect_offset, isect_count, depth, tile_cut, partial, CPB, G, v_params);
   GSR_LAUNCH_CHECK("k_project3d_bwd");
   return GSR_OK;
 }

@@ -42,12 +42,17 @@ struct Act3D {
   float op;     // sigmoid(logit)
 };
 
-__device__ __forceinline__ Act3D activate3d(const float* __restrict__ p) {
+// mode GSR_INPUT_ADAPTER: raw pose-splatter params (exp / q/(|q|+1e-8) / clamp / sigmoid,
+// src/gaussian_renderer.py:183-194).  GSR_INPUT_GSPLAT: gsplat rasterization() inputs, already
+// activated (scales, opacities and colours as given; the quaternion only gets gsplat's own
+// renormalisation in quat_rotmat).  Same row layout in both modes.
+__device__ __forceinline__ Act3D activate3d(const float* __restrict__ p, int mode) {
   Act3D a;
+  const bool raw = mode == GSR_INPUT_ADAPTER;
 #pragma unroll
   for (int k = 0; k < 3; ++k) a.m[k] = p[k];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) a.s[k] = expf(p[3 + k]);
+  for (int k = 0; k < 3; ++k) a.s[k] = raw ? expf(p[3 + k]) : p[3 + k];
   float qq = 0.f;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -55,15 +60,15 @@ __device__ __forceinline__ Act3D activate3d(const float* __restrict__ p) {
     qq += a.qraw[k] * a.qraw[k];
   }
   a.rq = sqrtf(qq);
-  const float den = a.rq + 1e-8f;
+  const float den = raw ? a.rq + 1e-8f : 1.f;
 #pragma unroll
   for (int k = 0; k < 4; ++k) a.q[k] = a.qraw[k] / den;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     a.craw[k] = p[10 + k];
-    a.col[k] = fminf(fmaxf(a.craw[k], 0.f), 1.f);
+    a.col[k] = raw ? fminf(fmaxf(a.craw[k], 0.f), 1.f) : a.craw[k];
   }
-  a.op = 1.f / (1.f + expf(-p[13]));
+  a.op = raw ? 1.f / (1.f + expf(-p[13])) : p[13];
   return a;
 }
 

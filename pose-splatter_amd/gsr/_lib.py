@@ -23,6 +23,8 @@ RADIUS_OPACITY_AABB = 0
 RADIUS_ISOTROPIC_3SIGMA = 1
 ORDER_DEPTH = 0
 ORDER_INDEX = 1
+INPUT_ADAPTER = 0
+INPUT_GSPLAT = 1
 
 GSR_EINVAL = -1
 GSR_ELAUNCH = -2
@@ -52,7 +54,7 @@ EXPORTS = {
     "gsr_selftest_reduce64": (ctypes.c_int, [_P, _P]),
     "gsr_selftest_lds_order": (ctypes.c_int, [_P, _P]),
     "gsr3d_project_fwd": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _I32, _I32, _I32, _F, _F, _F, _F,
-                                         _I32, _P, _P, _P, _P, _P, _P]),
+                                         _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "gsr2d_project_fwd": (ctypes.c_int, [_P, _I64, _I64, _I32, _I32, _F, _P, _P, _P, _P, _P]),
     "gsr_bin_offsets_workspace": (_SZ, [_I64, _I64]),
     "gsr_bin_offsets": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _SZ, _P, _P, _P, _P, _P, _P]),
@@ -67,8 +69,8 @@ EXPORTS = {
     "gsr2d_raster_bwd_workspace": (_SZ, [_I64, _I64]),
     "gsr2d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P,
                                         _SZ, _P, _P, _P]),
-    "gsr3d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _I32, _I32, _I32, _F, _P, _P, _P,
-                                         _P, _P, _P, _P, _P]),
+    "gsr3d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _I32, _I32, _I32, _F, _I32, _P, _P,
+                                         _P, _P, _P, _P, _P, _P]),
     "gsr2d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
 }
 

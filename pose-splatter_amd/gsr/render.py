@@ -54,6 +54,7 @@ class RenderOptions3D:
     radius_clip: float = 0.0
     eps2d: float = 0.3
     radius_mode: int = _lib.RADIUS_OPACITY_AABB
+    input_mode: int = _lib.INPUT_ADAPTER   # INPUT_GSPLAT: rows hold activated gsplat inputs
 
 
 _last_stats = {}
@@ -252,7 +253,9 @@ def effective_isect(stats: dict | None = None) -> int:
 
 def _background(bg: torch.Tensor, C: int, dev) -> torch.Tensor:
     """bg [3] or [C,3] -> contiguous float32 [C,3] on dev (expanded copies are cached per
-    source tensor version, so a fixed background costs no kernel per call)."""
+    source tensor version, so a fixed background costs no kernel per call).  The cache entry
+    holds the source tensor, so its address cannot be recycled by a different background
+    while the entry is alive."""
     b = bg.detach()
     if b.device == dev and b.dtype == torch.float32 and b.is_contiguous() and b.numel() == 3 * C:
         return b.reshape(C, 3)
@@ -261,8 +264,8 @@ def _background(bg: torch.Tensor, C: int, dev) -> torch.Tensor:
     if hit is None:
         if len(_bg_cache) > 64:
             _bg_cache.clear()
-        hit = _bg_cache[key] = b.to(device=dev, dtype=torch.float32).reshape(-1, 3).expand(C, 3).contiguous()
-    return hit
+        hit = _bg_cache[key] = (b, b.to(device=dev, dtype=torch.float32).reshape(-1, 3).expand(C, 3).contiguous())
+    return hit[1]
 
 
 def _forward3d(params, viewmats, Ks, bg, width, height, opts):
@@ -281,7 +284,7 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
     with _timed("project3d_fwd"):
       check(L.gsr3d_project_fwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height,
                               opts.near_plane, opts.far_plane, opts.radius_clip, opts.eps2d,
-                              opts.radius_mode, q["rec"], q["depth"], q["rect"], q["cnt"], q["tile_cnt"], stream),
+                              opts.radius_mode, opts.input_mode, q["rec"], q["depth"], q["rect"], q["cnt"], q["tile_cnt"], stream),
           "gsr3d_project_fwd")
     b.guess_post(with_chunks=True)
     b.offsets(stream)
@@ -368,6 +371,7 @@ class _Render3D(torch.autograd.Function):
                   "gsr3d_raster_bwd")
             with _timed("project3d_bwd"):
               check(L.gsr3d_project_bwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height, opts.eps2d,
+                                      opts.input_mode,
                                       q["depth"], q["rect"], q["isect_off"], q["cnt"], q["tile_cut"],
                                       _ptr(partial), _ptr(v_params), stream),
                   "gsr3d_project_bwd")

@@ -102,3 +102,16 @@ def test_view_shard_covers_all_views():
             assert got == list(range(C))
             sizes = [len(range(C)[view_shard(C, world, r)]) for r in range(world)]
             assert max(sizes) - min(sizes) <= 1
+
+
+def test_background_cache_never_returns_stale_colour():
+    """A freed background whose address is reused by a new tensor must not hit the cache."""
+    from gsr.render import _background
+    for _ in range(50):
+        b1 = torch.tensor([0.1, 0.5, 0.9])
+        assert torch.equal(_background(b1, 2, torch.device("cpu")), b1.expand(2, 3))
+        del b1
+        b2 = torch.ones(3)
+        assert torch.equal(_background(b2, 2, torch.device("cpu")), torch.ones(2, 3))
+        b2.mul_(0.5)                                   # in-place edit bumps the version
+        assert torch.equal(_background(b2, 2, torch.device("cpu")), torch.full((2, 3), 0.5))

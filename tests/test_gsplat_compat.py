@@ -1,0 +1,100 @@
+"""The gsplat `rasterization(**kw)` entry point: the direct gsplat calls
+in src/model.py:339-365 and src/plots.py:41-60 served by libgsr with activated inputs.
+
+CPU: argument validation (unsupported modes raise, no CPU compute path).
+GPU: forward and gradients w.r.t. every input against the oracle restatement
+(oracle3d.render3d(activated=True)), tolerance 1e-4 relative (north_star)."""
+import pytest
+import torch
+
+from _util import assert_close, grad_close
+
+
+def _inputs(N, C, W, H, seed, device="cpu"):
+    from gsr.scenes import gaussians3d, ring_cameras
+    p = gaussians3d(N, seed, extent=0.06)
+    g = torch.Generator().manual_seed(seed + 1)
+    means = p[:, 0:3].clone()
+    scales = torch.exp(p[:, 3:6] + 1.0)
+    quats = p[:, 6:10] * 3.0                     # un-normalised: gsplat renormalises
+    colors = torch.rand(N, 3, generator=g) * 1.2 - 0.1   # not clamped by gsplat
+    opac = torch.sigmoid(p[:, 13])
+    V, K = ring_cameras(C, W, H)
+    return [t.to(device) for t in (means, quats, scales, opac, colors)], V.to(device), K.to(device)
+
+
+def test_rejects_unsupported_modes():
+    from gsr.gsplat_compat import rasterization
+    (m, q, s, o, c), V, K = _inputs(4, 1, 32, 32, 1)
+    bad = [dict(sh_degree=3), dict(render_mode="RGB+D"), dict(rasterize_mode="antialiased"),
+           dict(tile_size=8), dict(camera_model="fisheye"), dict(distributed=True)]
+    for kw in bad:
+        with pytest.raises(NotImplementedError):
+            rasterization(m, q, s, o, c, V, K, 32, 32, **kw)
+
+
+def test_no_cpu_path():
+    from gsr.gsplat_compat import rasterization
+    (m, q, s, o, c), V, K = _inputs(4, 1, 32, 32, 1)
+    with pytest.raises(RuntimeError, match="CUDA|HIP|device"):
+        rasterization(m, q, s, o, c, V, K, 32, 32)
+
+
+def test_module_alias():
+    import gsr.gsplat_compat as gc
+    mod = gc.gsplat_module()
+    assert mod.rendering is gc and mod.rasterization is gc.rasterization
+
+
+def _oracle(m, q, s, o, c, V, K, W, H, bg, radius_clip, vr, va):
+    from oracle import oracle3d
+    leaves = [t.detach().clone().double().requires_grad_(True) for t in (m, q, s, o, c)]
+    rows = torch.cat([leaves[0], leaves[2], leaves[1], leaves[4], leaves[3][:, None]], 1)
+    rgb, alpha = oracle3d.render3d(rows, V.double(), K.double(), W, H, bg.double(),
+                                   radius_clip=radius_clip, activated=True)
+    ((rgb * vr.double()).sum() + (alpha * va.double()).sum()).backward()
+    return rgb.detach(), alpha.detach(), [t.grad for t in leaves]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,C,W,H,seed,radius_clip,with_bg", [
+    (300, 2, 64, 48, 3, 0.0, False),
+    (3000, 3, 96, 80, 4, 2.0, True),
+])
+def test_vs_oracle(cuda, N, C, W, H, seed, radius_clip, with_bg):
+    from gsr.gsplat_compat import rasterization
+    (m, q, s, o, c), V, K = _inputs(N, C, W, H, seed)
+    bg = torch.rand(C, 3, generator=torch.Generator().manual_seed(seed)) if with_bg else torch.zeros(C, 3)
+    g = torch.Generator().manual_seed(seed + 7)
+    vr, va = torch.randn(C, H, W, 3, generator=g), torch.randn(C, H, W, 1, generator=g)
+    leaves = [t.to(cuda).requires_grad_(True) for t in (m, q, s, o, c)]
+    rgb, alpha, meta = rasterization(*leaves, V.to(cuda), K.to(cuda), W, H, radius_clip=radius_clip,
+                                     packed=False, absgrad=True, sh_degree=None,
+                                     backgrounds=bg.to(cuda) if with_bg else None)
+    assert rgb.shape == (C, H, W, 3) and alpha.shape == (C, H, W, 1)
+    ((rgb * vr.to(cuda)).sum() + (alpha * va.to(cuda)).sum()).backward()
+    rgb_o, a_o, g_o = _oracle(m, q, s, o, c, V, K, W, H, bg, radius_clip, vr, va[..., 0])
+    assert_close(rgb.detach().cpu(), rgb_o, what="rgb")
+    assert_close(alpha.detach().cpu()[..., 0], a_o, what="alpha")
+    for name, t, e in zip(("means", "quats", "scales", "opacities", "colors"), leaves, g_o):
+        grad_close(t.grad.cpu(), e, what=f"v_{name}", max_frac=1e-3)
+
+
+@pytest.mark.gpu
+def test_matches_adapter_path(cuda):
+    """rasterization(activated) == GaussianRenderer3D.render(raw) on the same scene."""
+    from gsr.gsplat_compat import rasterization
+    from gsr.scenes import gaussians3d, ring_cameras
+    from src.gaussian_renderer import GaussianRenderer3D
+    W, H, C = 80, 64, 2
+    p = gaussians3d(2000, 11, extent=0.06)
+    V, K = ring_cameras(C, W, H)
+    r = GaussianRenderer3D(W, H, device="cuda")
+    r.set_background_color(torch.zeros(3, device=cuda))
+    rgb_a, a_a = r.render(p.to(cuda), V.to(cuda), K.to(cuda))
+    q = p[:, 6:10] / (p[:, 6:10].norm(dim=-1, keepdim=True) + 1e-8)
+    rgb_s, a_s, _ = rasterization(p[:, 0:3].to(cuda), q.to(cuda), torch.exp(p[:, 3:6]).to(cuda),
+                                  torch.sigmoid(p[:, 13]).to(cuda), p[:, 10:13].clamp(0, 1).to(cuda),
+                                  V.to(cuda), K.to(cuda), W, H)
+    assert_close(rgb_s, rgb_a, what="rgb")
+    assert_close(a_s[..., 0], a_a, what="alpha")
