@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the CPU oracle timing")
     ap.add_argument("--cpu-views", type=int, default=1, help="views in the bounded CPU sample")
+    ap.add_argument("--loss", default="none", choices=["none", "fused", "torch"],
+                    help="3D, 1 GPU: time render + the reference IoU/L1 training loss "
+                         "(train_script.py:128-133) fused into the kernels, or as plain torch ops")
     ap.add_argument("--traffic-csv", default=DEFAULT_TRAFFIC_CSV,
                     help="rocprofv3 --pmc counter_collection.csv to fill roofline.traffic "
                          "(default: the committed profiles/ counter run, if present)")
@@ -181,9 +184,27 @@ def main():
         def render_views(p, Vs, Ks):
             return R.render3d(p, Vs, Ks, cfg.width, cfg.height, bg)
 
+    if args.loss != "none":
+        if cfg.mode != "3d" or world > 1:
+            raise SystemExit("--loss: 3D configs on one GPU only")
+        from gsr.loss import render3d_iou_l1
+        g3 = torch.Generator().manual_seed(cfg.seed + 3)
+        timg = torch.rand(C, 3, cfg.height, cfg.width, generator=g3).to(dev)
+        tmask = (torch.rand(C, cfg.height, cfg.width, generator=g3) < 0.3).float().to(dev)
+
     def step():
         params.grad = None
-        if cfg.mode == "3d" and world > 1:
+        if args.loss == "fused":
+            li, lm, rgb, alpha = render3d_iou_l1(params, Vd, Kd, cfg.width, cfg.height, bg, timg, tmask, 1.0)
+            (li + lm).backward()
+        elif args.loss == "torch":
+            rgb, alpha = R.render3d(params, Vd, Kd, cfg.width, cfg.height, bg)
+            inter = (alpha * tmask).sum(dim=(-2, -1))
+            union = (alpha + tmask - alpha * tmask).sum(dim=(-2, -1))
+            li = 1 - ((inter + 1e-6) / (union + 1e-6)).mean()
+            lm = torch.abs(timg - rgb.permute(0, 3, 1, 2)).sum() / tmask.sum()
+            (li + lm).backward()
+        elif cfg.mode == "3d" and world > 1:
             params.grad = sharded_backward(render_views, params, V_all, K_all, vr_all, va_all)
         elif cfg.mode == "3d":
             rgb, alpha = R.render3d(params, Vd, Kd, cfg.width, cfg.height, bg)
@@ -262,7 +283,7 @@ def main():
         "dtype": "f32",
         "data": "synthetic (SURVEY.md §8(d) distribution A, seed 1000+config)",
         "config": {"workload": cfg.name, "N_gauss": cfg.N, "width": cfg.width, "height": cfg.height,
-                   "views_per_gpu": C, "background": "white",
+                   "views_per_gpu": C, "background": "white", "loss": args.loss,
                    "parallelism": f"view-sharded x{world} + RCCL all-reduce of v_params" if world > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

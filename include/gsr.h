@@ -215,6 +215,44 @@ int gsr2d_project_bwd(const float* params, int64_t N, int64_t row_stride, int wi
                       const int32_t* isect_count, const uint64_t* tile_cut,
                       const float* partial, float* v_params, void* stream);
 
+/* ---- Loss-fused backward ------------------------------------------
+ * The reference training step (scripts/training/train_script.py:30-36, 128-133) takes
+ *   iou_loss = 1 - mean_c[(I_c + 1e-6) / (U_c + 1e-6)],  I_c = sum a m,  U_c = sum (a + m - a m)
+ *   img_loss = img_lambda * sum |target - rgb| / sum m
+ * of the rendered views (a = alpha [C,H,W], rgb [C,H,W,3]) against target_img [C,3,H,W]
+ * (planar, the loader's layout) and target_mask [C,H,W].  gsr_loss_iou_l1_fwd evaluates both
+ * in one pass (deterministic fixed-order reduction) and gsr3d_raster_bwd_loss generates the
+ * per-pixel cotangents of  g_iou * iou_loss + g_img * img_loss (+ optional extra cotangents,
+ * e.g. an SSIM term's) inside the raster backward, so no v_rgb / v_alpha image is written. */
+size_t gsr_loss_workspace(int C, int width, int height);
+
+/* sums [(C+1)*4]: per view {I_c, U_c, sum m, sum |t-rgb|}, row C = {0, 0, total m, total L1};
+ * iou_loss, img_loss: one float each.  ws: gsr_loss_workspace bytes. */
+int gsr_loss_iou_l1_fwd(const float* rgb, const float* alpha, const float* target_img,
+                        const float* target_mask, int C, int width, int height, float img_lambda,
+                        void* ws, size_t ws_bytes, float* sums, float* iou_loss, float* img_loss,
+                        void* stream);
+
+typedef struct gsr_loss_terms {
+  const float* rgb;            /* [C,H,W,3] forward output */
+  const float* target_img;     /* [C,3,H,W] */
+  const float* target_mask;    /* [C,H,W] */
+  const float* sums;           /* [(C+1)*4] from gsr_loss_iou_l1_fwd */
+  const float* grad_out;       /* [2] = {g_iou, g_img}: d(total)/d(iou_loss), d(total)/d(img_loss) */
+  const float* v_rgb_extra;    /* optional [C,H,W,3] added to the fused cotangent (NULL: none) */
+  const float* v_alpha_extra;  /* optional [C,H,W] */
+  float img_lambda;
+  int32_t reserved;
+} gsr_loss_terms;
+
+/* gsr3d_raster_bwd with the cotangents generated from `loss` instead of read from images. */
+int gsr3d_raster_bwd_loss(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
+                          const int32_t* tile_end, const int32_t* chunk_base, const int32_t* chunk_tile,
+                          const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats,
+                          int32_t n_chunks, int C, int width, int height, const float* bg,
+                          const float* final_T, const int32_t* last, const gsr_loss_terms* loss,
+                          const int32_t* k_of_s, float* partial, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -518,6 +518,36 @@ __device__ __forceinline__ void block_store_partials(const PartialLds& L, int b0
   }
 }
 
+// Cotangent of  g_iou * iou_loss + g_img * img_loss  (+ extra cotangents) at one pixel
+// (scripts/training/train_script.py:30-36, 128-130), from the sums of gsr_loss_iou_l1_fwd:
+//   d iou_loss / d a = -(1/C) [ m / (U+e) - (I+e) / (U+e)^2 (1 - m) ]       (e = 1e-6)
+//   d img_loss / d rgb_k = img_lambda / M * sign(rgb_k - t_k)                 (sign(0) = 0)
+// the same association torch's autograd uses for the unfused expressions.
+__device__ __forceinline__ void loss_cotangent(const gsr_loss_terms& lt, int C, int c, int64_t pix, int64_t pv,
+                                               int64_t HW, float& vr, float& vg, float& vb, float& va) {
+  const float g_iou = lt.grad_out[0], g_img = lt.grad_out[1];
+  const float Ie = lt.sums[4 * c + 0] + 1e-6f, Ue = lt.sums[4 * c + 1] + 1e-6f;
+  const float M = lt.sums[4 * C + 2];
+  const float m = lt.target_mask[pix];
+  const float d_iou_dI = 1.f / Ue;
+  const float d_iou_dU = -Ie / (Ue * Ue);
+  const float g = -g_iou / (float)C;
+  va = g * (d_iou_dI * m + d_iou_dU * (1.f - m));
+  const float s = g_img * lt.img_lambda / M;
+  const float* t = lt.target_img + (int64_t)c * 3 * HW + pv;
+  const float* r = lt.rgb + pix * 3;
+  const float d0 = r[0] - t[0], d1 = r[1] - t[HW], d2 = r[2] - t[2 * HW];
+  vr = s * (float)((d0 > 0.f) - (d0 < 0.f));
+  vg = s * (float)((d1 > 0.f) - (d1 < 0.f));
+  vb = s * (float)((d2 > 0.f) - (d2 < 0.f));
+  if (lt.v_rgb_extra) {
+    vr += lt.v_rgb_extra[pix * 3 + 0];
+    vg += lt.v_rgb_extra[pix * 3 + 1];
+    vb += lt.v_rgb_extra[pix * 3 + 2];
+  }
+  if (lt.v_alpha_extra) va += lt.v_alpha_extra[pix];
+}
+
 // ---------------------------------------------------------------- 3D backward
 // Chunk-parallel: one workgroup per (tile, GSR_CHUNK-entry chunk of its list), so no
 // pixel's back-to-front walk is longer than one chunk.  Workgroup b takes entry b of the
@@ -530,6 +560,10 @@ __device__ __forceinline__ void block_store_partials(const PartialLds& L, int b0
 // Each wave culls the chunk against its 8x8 sub-tile (same test as the forward), walks its
 // survivors back to front, reduces 7 entries x 9 gradients at once (reduce64), and a 4-wave
 // LDS combine stores one 9-float partial per sorted entry.
+//
+// LOSS: the pixel cotangents are not read from v_rgb / v_alpha images but generated from the
+// training loss (loss_cotangent below, gsr3d_raster_bwd_loss).
+template <bool LOSS>
 __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ tile_end, const int32_t* __restrict__ chunk_base,
@@ -537,7 +571,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
     const float* __restrict__ bg, const float* __restrict__ final_T, const int32_t* __restrict__ last_in,
     const float* __restrict__ v_rgb, const float* __restrict__ v_alpha, float* __restrict__ partial,
     const int32_t* __restrict__ chunk_list, gsr_bin_stats* __restrict__ stats,
-    const int32_t* __restrict__ k_of_s) {
+    const int32_t* __restrict__ k_of_s, const gsr_loss_terms lt, int C) {
   // slot kNull: a zero-opacity record (never valid) that pads survivor groups to 7
   constexpr int kNull = kChunk3;
   constexpr int kGroup = 7;
@@ -568,10 +602,14 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
     last = last_in[pix];
     if (last >= b0) {
       Tf = final_T[pix];
-      vr = v_rgb[pix * 3 + 0];
-      vg = v_rgb[pix * 3 + 1];
-      vb = v_rgb[pix * 3 + 2];
-      va = v_alpha[pix];
+      if constexpr (LOSS) {
+        loss_cotangent(lt, C, st.c, pix, (int64_t)st.i * W + st.j, (int64_t)W * H, vr, vg, vb, va);
+      } else {
+        vr = v_rgb[pix * 3 + 0];
+        vg = v_rgb[pix * 3 + 1];
+        vb = v_rgb[pix * 3 + 2];
+        va = v_alpha[pix];
+      }
     }
   }
   // state at the end of this chunk: {T_end, suffix colour sum} (forward epilogue)
@@ -911,11 +949,33 @@ int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t*
   if (n_chunks == 0) return GSR_OK;
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   // n_chunks bounds the forward's active-chunk count (stats->n_active, device-side)
-  hipLaunchKernelGGL(k_raster3d_bwd, dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
+  const gsr_loss_terms none{};
+  hipLaunchKernelGGL(k_raster3d_bwd<false>, dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
                      (const Splat*)rec, sorted_ids, tile_offset, tile_end, chunk_base, chunk_tile,
                      (const float4*)chunk_state, width, height, tw, th, bg, final_T, last, v_rgb, v_alpha, partial,
-                     chunk_list, stats, k_of_s);
+                     chunk_list, stats, k_of_s, none, C);
   GSR_LAUNCH_CHECK("k_raster3d_bwd");
+  return GSR_OK;
+}
+
+int gsr3d_raster_bwd_loss(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
+                          const int32_t* tile_end, const int32_t* chunk_base, const int32_t* chunk_tile,
+                          const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats,
+                          int32_t n_chunks, int C, int width, int height, const float* bg, const float* final_T,
+                          const int32_t* last, const gsr_loss_terms* loss, const int32_t* k_of_s, float* partial,
+                          void* stream) {
+  GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "gsr3d_raster_bwd_loss: bad C=%d or image %dx%d", C, width,
+              height);
+  GSR_REQUIRE(n_chunks >= 0, "gsr3d_raster_bwd_loss: bad n_chunks");
+  GSR_REQUIRE(loss != nullptr && loss->rgb && loss->target_img && loss->target_mask && loss->sums && loss->grad_out,
+              "gsr3d_raster_bwd_loss: incomplete loss terms");
+  if (n_chunks == 0) return GSR_OK;
+  const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
+  hipLaunchKernelGGL(k_raster3d_bwd<true>, dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
+                     (const Splat*)rec, sorted_ids, tile_offset, tile_end, chunk_base, chunk_tile,
+                     (const float4*)chunk_state, width, height, tw, th, bg, final_T, last, nullptr, nullptr,
+                     partial, chunk_list, stats, k_of_s, *loss, C);
+  GSR_LAUNCH_CHECK("k_raster3d_bwd_loss");
   return GSR_OK;
 }
 

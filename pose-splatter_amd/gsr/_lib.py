@@ -10,7 +10,7 @@ import ctypes
 import os
 import threading
 
-__all__ = ["LIB_PATH", "GsrLibraryError", "lib", "check", "BinStats", "EXPORTS",
+__all__ = ["LIB_PATH", "GsrLibraryError", "lib", "check", "BinStats", "LossTerms", "EXPORTS",
            "RADIUS_OPACITY_AABB", "RADIUS_ISOTROPIC_3SIGMA", "ORDER_DEPTH", "ORDER_INDEX", "TILE"]
 
 LIB_PATH = os.environ.get(
@@ -39,6 +39,13 @@ class BinStats(ctypes.Structure):
     _fields_ = [("n_isect", ctypes.c_int64), ("max_seg", ctypes.c_int32), ("n_busy", ctypes.c_int32),
                 ("n_chunks", ctypes.c_int32), ("n_active", ctypes.c_int32),
                 ("reserved", ctypes.c_int32 * 2)]
+
+
+class LossTerms(ctypes.Structure):
+    """gsr_loss_terms (include/gsr.h): device pointers + img_lambda for gsr3d_raster_bwd_loss."""
+    _fields_ = [("rgb", ctypes.c_void_p), ("target_img", ctypes.c_void_p), ("target_mask", ctypes.c_void_p),
+                ("sums", ctypes.c_void_p), ("grad_out", ctypes.c_void_p), ("v_rgb_extra", ctypes.c_void_p),
+                ("v_alpha_extra", ctypes.c_void_p), ("img_lambda", ctypes.c_float), ("reserved", ctypes.c_int32)]
 
 
 _P = ctypes.c_void_p
@@ -72,6 +79,10 @@ EXPORTS = {
     "gsr3d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _I32, _I32, _I32, _F, _I32, _P, _P,
                                          _P, _P, _P, _P, _P, _P]),
     "gsr2d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
+    "gsr_loss_workspace": (_SZ, [_I32, _I32, _I32]),
+    "gsr_loss_iou_l1_fwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _SZ, _P, _P, _P, _P]),
+    "gsr3d_raster_bwd_loss": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P,
+                                             _P, _P, ctypes.POINTER(LossTerms), _P, _P, _P]),
 }
 
 _lock = threading.Lock()

@@ -347,35 +347,46 @@ class _Render3D(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, v_rgb, v_alpha):
-        L = lib()
         b = ctx.b
-        p, stride, V, Kc, bgc, width, height, opts = ctx.meta
-        dev = p.device
-        stream = _stream(dev)
-        C, N = b.C, b.N
+        _, _, _, _, bgc, width, height, _ = ctx.meta
+        C, dev = b.C, b.device
         if v_rgb is None:
             v_rgb = torch.zeros(C, height, width, 3, device=dev)
         if v_alpha is None:
             v_alpha = torch.zeros(C, height, width, device=dev)
         v_rgb = v_rgb.float().contiguous()
         v_alpha = v_alpha.float().contiguous()
-        v_params = torch.empty(N, 14, device=dev, dtype=torch.float32)
-        if N > 0:
-            partial = torch.empty(max(b.n_isect, 1) * _lib.PARTIAL_STRIDE, device=dev, dtype=torch.float32)
-            q = b.p
-            with _timed("raster3d_bwd"):
-              check(L.gsr3d_raster_bwd(q["rec"], q["sorted_ids"], q["tile_off"], q["tile_end"], q["chunk_base"],
+
+        def raster(L, q, partial, stream):
+            check(L.gsr3d_raster_bwd(q["rec"], q["sorted_ids"], q["tile_off"], q["tile_end"], q["chunk_base"],
                                      q["chunk_tile"], q["chunk_state"], q["chunk_list"], q["stats_dev"],
                                      b.n_chunks, C, width, height, _ptr(bgc), q["final_T"], q["last"],
                                      _ptr(v_rgb), _ptr(v_alpha), q["k_of_s"], _ptr(partial), stream),
                   "gsr3d_raster_bwd")
-            with _timed("project3d_bwd"):
-              check(L.gsr3d_project_bwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height, opts.eps2d,
-                                      opts.input_mode,
-                                      q["depth"], q["rect"], q["isect_off"], q["cnt"], q["tile_cut"],
-                                      _ptr(partial), _ptr(v_params), stream),
-                  "gsr3d_project_bwd")
+        v_params = backward3d(b, ctx.meta, raster)
         return v_params.view(ctx.params_shape), None, None, None, None, None, None
+
+
+def backward3d(b, meta, raster) -> torch.Tensor:
+    """Raster backward (``raster(L, q, partial, stream)`` issues the raster call that writes
+    the partial rows) followed by the projection backward: v_params [N,14]."""
+    L = lib()
+    p, stride, V, Kc, bgc, width, height, opts = meta
+    stream = _stream(p.device)
+    C, N = b.C, b.N
+    v_params = torch.empty(N, 14, device=p.device, dtype=torch.float32)
+    if N > 0:
+        partial = torch.empty(max(b.n_isect, 1) * _lib.PARTIAL_STRIDE, device=p.device, dtype=torch.float32)
+        q = b.p
+        with _timed("raster3d_bwd"):
+            raster(L, q, partial, stream)
+        with _timed("project3d_bwd"):
+          check(L.gsr3d_project_bwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height, opts.eps2d,
+                                    opts.input_mode,
+                                    q["depth"], q["rect"], q["isect_off"], q["cnt"], q["tile_cut"],
+                                    _ptr(partial), _ptr(v_params), stream),
+                "gsr3d_project_bwd")
+    return v_params
 
 
 class _Render2D(torch.autograd.Function):

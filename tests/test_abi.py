@@ -82,3 +82,40 @@ def test_binding_prototypes_match_header():
         params = decls[name].strip()
         n = 0 if params in ("", "void") else params.count(",") + 1
         assert n == len(args), (name, n, len(args))
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """ctypes mirrors of gsr_bin_stats / gsr_loss_terms have the C compiler's size and offsets."""
+    import shutil
+    import subprocess
+    from gsr import _lib
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    src = tmp_path / "layout.c"
+    structs = {"gsr_bin_stats": _lib.BinStats, "gsr_loss_terms": _lib.LossTerms}
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "gsr.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines += ["return 0;", "}"]
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run([cc, "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                         text=True).stdout.splitlines())
+    for cname, py in structs.items():
+        assert int(got[f"{cname} size"]) == ctypes.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert int(got[f"{cname} {f}"]) == getattr(py, f).offset, (cname, f)
+
+
+def test_loss_entry_points_validate():
+    from gsr import _lib
+    lib = _lib.lib()
+    assert lib.gsr_loss_workspace(6, 576, 512) >= 6 * 16
+    rc = lib.gsr_loss_iou_l1_fwd(None, None, None, None, 0, 64, 64, 1.0, None, 0, None, None, None, None)
+    assert rc == -1 and b"bad C" in lib.gsr_last_error()
+    rc = lib.gsr3d_raster_bwd_loss(*([None] * 9), 1, 1, 64, 64, None, None, None, None, None, None, None)
+    assert rc == -1 and b"loss terms" in lib.gsr_last_error()
