@@ -253,6 +253,44 @@ int gsr3d_raster_bwd_loss(const float* rec, const int32_t* sorted_ids, const int
                           const float* final_T, const int32_t* last, const gsr_loss_terms* loss,
                           const int32_t* k_of_s, float* partial, void* stream);
 
+/* ---- Parameter head + pose transform ----------------------------
+ * Replace the post-MLP part of PoseSplatter.get_gaussian_params_from_volume_unified
+ * (src/model.py:185-254) and apply_pose_transform_3d (src/model.py:258-298, with the
+ * quaternion helpers at :378-421, whose float64 eigh runs here as in-register Jacobi). */
+
+size_t gsr_head_select_workspace(int64_t M);
+
+/* Mask-threshold search + ordered selection (src/model.py:185-197) over v0 = volume[0] [M]:
+ * mt starts at mask_threshold, rises by delta while more than max_n voxels pass
+ * sigmoid(v0 - mt) > prob_threshold, then falls while fewer than min_n pass (at most
+ * max_iter steps in total).  Writes *mt_out (float64), info[0] = final count, info[1] =
+ * steps taken, info[2] = 1 if max_iter was hit, and idx[0..count) = the passing voxel
+ * indices in increasing order (idx needs M entries of room).  No host synchronisation. */
+int gsr_head_select(const float* v0, int64_t M, double mask_threshold, float prob_threshold, double delta,
+                    int32_t min_n, int32_t max_n, int32_t max_iter, void* ws, size_t ws_bytes, int32_t* info,
+                    double* mt_out, int64_t* idx, void* stream);
+
+/* net [N, >=14] (row stride net_stride): the MLP output (quats, scales, opacity, colours,
+ * delta_means); v0 [N] = volume[0] at the selected voxels; grid [N,3] their grid points;
+ * scale: device pointer to the model's scalar log-scale offset.  out [N,14] in the renderer
+ * layout (means, log_scales, quats, colours, logit opacity); pose = 1 also applies the pose
+ * transform for the rotation angle (host) and translation p3d[3] (device pointer). */
+int gsr_head3d_fwd(const float* net, int64_t N, int64_t net_stride, const float* v0, const float* grid,
+                   const float* scale, float mt, float prob_threshold, float clip_lo, float clip_hi,
+                   float voxel_size, int pose, double angle, const float* p3d, float* out, void* stream);
+
+/* g_out [N,14] -> g_net [N,14] (column 7, the discarded opacity, gets 0) and g_v0 [N].
+ * The gradient of the scale offset is the sum of g_out[:,3:6] (left to the caller). */
+int gsr_head3d_bwd(const float* net, int64_t N, int64_t net_stride, const float* v0, const float* grid,
+                   float mt, float prob_threshold, float clip_lo, float clip_hi, float voxel_size, int pose,
+                   double angle, const float* g_out, float* g_net, float* g_v0, void* stream);
+
+/* apply_pose_transform_3d alone on renderer-layout rows [N, >=14]; out / g_params [N,14]. */
+int gsr_pose3d_fwd(const float* params, int64_t N, int64_t row_stride, double angle, const float* p3d,
+                   float* out, void* stream);
+int gsr_pose3d_bwd(const float* params, int64_t N, int64_t row_stride, double angle, const float* g_out,
+                   float* g_params, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

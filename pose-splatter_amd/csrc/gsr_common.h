@@ -55,6 +55,7 @@ void set_error(const char* fmt, ...);
   } while (0)
 
 inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+inline int64_t ceil_div64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // ---------------------------------------------------------------- device helpers
 template <int CTRL>

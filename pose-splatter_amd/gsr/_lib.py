@@ -52,6 +52,7 @@ _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
 _I64 = ctypes.c_int64
 _F = ctypes.c_float
+_D = ctypes.c_double
 _SZ = ctypes.c_size_t
 
 # name -> (restype, argtypes); must list every function declared in include/gsr.h
@@ -83,6 +84,12 @@ EXPORTS = {
     "gsr_loss_iou_l1_fwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _SZ, _P, _P, _P, _P]),
     "gsr3d_raster_bwd_loss": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P,
                                              _P, _P, ctypes.POINTER(LossTerms), _P, _P, _P]),
+    "gsr_head_select_workspace": (_SZ, [_I64]),
+    "gsr_head_select": (ctypes.c_int, [_P, _I64, _D, _F, _D, _I32, _I32, _I32, _P, _SZ, _P, _P, _P, _P]),
+    "gsr_head3d_fwd": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _P, _F, _F, _F, _F, _F, _I32, _D, _P, _P, _P]),
+    "gsr_head3d_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _F, _F, _F, _F, _F, _I32, _D, _P, _P, _P, _P]),
+    "gsr_pose3d_fwd": (ctypes.c_int, [_P, _I64, _I64, _D, _P, _P, _P]),
+    "gsr_pose3d_bwd": (ctypes.c_int, [_P, _I64, _I64, _D, _P, _P, _P]),
 }
 
 _lock = threading.Lock()

@@ -1,0 +1,208 @@
+"""Parameter head + pose transform: gsr.head against the oracle
+restatement of src/model.py:185-298, 378-421 (oracle/head.py).  Selection is compared
+exactly (indices and the float64 threshold); parameters and gradients within 1e-4 relative
+(north_star; the eigenvector path runs in float64 on both sides and is cast to float32)."""
+import math
+
+import pytest
+import torch
+
+from _util import assert_close, grad_close
+
+
+def test_oracle_identity_quaternion_kat():
+    """q = (1,0,0,0), angle 0: the reference matrix is the identity and the quaternion returns."""
+    from oracle.head import pose_transform_3d
+    p = torch.zeros(1, 14)
+    p[0, 6] = 1.0
+    out = pose_transform_3d(p, 0.0, torch.zeros(3))
+    assert torch.allclose(out[0, 6:10], torch.tensor([1.0, 0.0, 0.0, 0.0]), atol=1e-7)
+
+
+def test_oracle_matrix_is_the_reference_one():
+    """[1][1] = 1 + q00 - q00 and [1][0] = q12 - q30 (src/model.py:391-394), not a rotation."""
+    from oracle.head import quaternion_matrix_ref
+    q = torch.tensor([[0.5, 0.5, 0.5, 0.5]])
+    M = quaternion_matrix_ref(q)[0].double()
+    assert abs(float(M[1, 1]) - 1.0) < 1e-7
+    assert abs(float(M[1, 0]) - float(M[0, 1])) < 1e-7
+    assert not torch.allclose(M[:3, :3] @ M[:3, :3].T, torch.eye(3, dtype=torch.float64), atol=1e-3)
+
+
+def test_api_validation_cpu():
+    from gsr.head import gaussian_params_3d, pose_transform_3d, select_gaussians
+    with pytest.raises(RuntimeError):
+        select_gaussians(torch.zeros(100))
+    with pytest.raises(RuntimeError):
+        pose_transform_3d(torch.zeros(4, 14), 0.1, [0, 0, 0])
+    with pytest.raises(RuntimeError):
+        gaussian_params_3d(torch.zeros(4, 14), torch.zeros(4), torch.zeros(1), torch.zeros(4, 3), 0.25)
+
+
+def _sign_fix(out, ref):
+    """q and -q are one rotation; the reference's w >= 0 convention is decided by rounding
+    noise when |w| ~ 0.  Rows with |w| < 1e-5 take the sign closest to the oracle and are
+    excluded from gradient checks (their gradient flips with the sign).  Returns
+    (out_fixed, ambiguous_rows)."""
+    amb = ref[:, 6].abs() < 1e-5
+    out = out.clone()
+    flip = amb & ((out[:, 6:10] + ref[:, 6:10]).abs().sum(1) < (out[:, 6:10] - ref[:, 6:10]).abs().sum(1))
+    out[flip, 6:10] = -out[flip, 6:10]
+    return out, amb
+
+
+def _inputs(N, seed):
+    g = torch.Generator().manual_seed(seed)
+    net = torch.randn(N, 14, generator=g)
+    v0 = torch.randn(N, generator=g) * 2.0 + 1.5
+    grid = (torch.rand(N, 3, generator=g) - 0.5) * 0.18
+    return net, v0, grid
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,min_n,max_n,seed", [(32768, 1000, 4000, 1), (64 ** 3, 1024, 16000, 2),
+                                                 (20000, 9000, 12000, 3), (5000, 10, 20, 4)])
+def test_select_matches_reference_loops(cuda, M, min_n, max_n, seed):
+    from gsr.head import select_gaussians
+    from oracle.head import select_mask
+    g = torch.Generator().manual_seed(seed)
+    v0 = torch.randn(M, generator=g) * 1.5 - 0.5
+    torch.manual_seed(123)
+    mask, mt_o, _ = select_mask(v0, 0.25, 0.25, 0.05, min_n, max_n)
+    torch.manual_seed(123)
+    idx, mt = select_gaussians(v0.to(cuda), 0.25, 0.25, 0.05, min_n, max_n)
+    assert mt == mt_o
+    assert torch.equal(idx.cpu(), torch.nonzero(mask, as_tuple=True)[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pose", [False, True])
+def test_head3d_vs_oracle(cuda, pose):
+    from gsr.head import gaussian_params_3d
+    from oracle.head import head3d, pose_transform_3d
+    N, mt, pt, vs = 3000, 0.3, 0.25, 0.18 / 64
+    net, v0, grid = _inputs(N, 5)
+    scale = torch.tensor([-5.5])
+    angle, p3 = (0.7, torch.tensor([0.01, -0.02, 0.03])) if pose else (None, None)
+    cot = torch.randn(N, 14, generator=torch.Generator().manual_seed(6))
+    # GPU
+    leaves = [t.to(cuda).requires_grad_(True) for t in (net, v0, scale)]
+    out = gaussian_params_3d(leaves[0], leaves[1], leaves[2], grid.to(cuda), mt, pt, (0.0, 0.99), vs,
+                             angle, p3.to(cuda) if pose else None)
+    (out * cot.to(cuda)).sum().backward()
+    # oracle (probs from the same logits, as src/model.py:188 / :224)
+    lo = [t.clone().requires_grad_(True) for t in (net, v0, scale)]
+    ref = head3d(lo[0], torch.sigmoid(lo[1] - mt), lo[2], grid, pt, (0.0, 0.99), vs)
+    if pose:
+        ref = pose_transform_3d(ref, angle, p3)
+    (ref * cot).sum().backward()
+    o, amb = _sign_fix(out.detach().cpu(), ref.detach())
+    assert_close(o, ref.detach(), rtol=1e-4, atol=1e-6, what="params")
+    keep = ~amb
+    for name, a, e in zip(("net", "v0", "scale"), leaves, lo):
+        if name == "scale":
+            continue                                  # a sum over all rows, checked below
+        grad_close(a.grad.cpu()[keep], e.grad[keep], what=f"grad {name}", max_frac=1e-3)
+    grad_close(leaves[2].grad.cpu(), lo[2].grad, what="grad scale")
+
+
+@pytest.mark.gpu
+def test_pose_transform_vs_oracle(cuda):
+    from gsr.head import pose_transform_3d
+    from oracle.head import pose_transform_3d as ref_pose
+    N = 5000
+    g = torch.Generator().manual_seed(7)
+    p = torch.randn(N, 14, generator=g)
+    # identity, a case through the reference's off-rotation entries, the near-zero branch,
+    # and a w < 0 sign flip.  (A top eigenvalue of multiplicity > 1, e.g. q = (0,1,0,0),
+    # leaves the eigenvector to the solver's choice in the reference too: not compared.)
+    p[:4, 6:10] = torch.tensor([[1.0, 0, 0, 0], [0, 0.6, 0.8, 0], [1e-9, 0, 0, 0], [-0.5, 0.5, -0.5, 0.5]])
+    cot = torch.randn(N, 14, generator=g)
+    for angle in (0.0, 1.1, -2.5, math.pi):
+        pg = p.to(cuda).requires_grad_(True)
+        out = pose_transform_3d(pg, angle, torch.tensor([0.1, 0.2, -0.3], device=cuda))
+        (out * cot.to(cuda)).sum().backward()
+        pc = p.clone().requires_grad_(True)
+        ref = ref_pose(pc, angle, torch.tensor([0.1, 0.2, -0.3]))
+        (ref * cot).sum().backward()
+        o, amb = _sign_fix(out.detach().cpu(), ref.detach())
+        assert int(amb.sum()) < 10
+        assert_close(o, ref.detach(), rtol=1e-4, atol=1e-6, what=f"pose angle={angle}")
+        grad_close(pg.grad.cpu()[~amb], pc.grad[~amb], what=f"pose grad angle={angle}", max_frac=1e-3)
+
+
+@pytest.mark.gpu
+def test_params_from_volume_end_to_end(cuda):
+    """Selection + MLP + head + pose (src/model.py:151-156) against the oracle sequence."""
+    from gsr.head import params_from_volume_3d
+    from oracle.head import head3d, pose_transform_3d, select_mask
+    torch.manual_seed(0)
+    c, M = 8, 40 ** 3
+    mlp = torch.nn.Sequential(torch.nn.Linear(c, 128), torch.nn.ReLU(), torch.nn.Linear(128, 14))
+    vol = torch.randn(c, M, generator=torch.Generator().manual_seed(8))
+    grid = (torch.rand(M, 3, generator=torch.Generator().manual_seed(9)) - 0.5) * 0.18
+    scale = torch.tensor([-5.5])
+    kw = dict(mask_threshold=0.25, prob_threshold=0.25, mask_threshold_delta=0.05, min_n=1024, max_n=16000,
+              color_clip=(0.0, 0.99), voxel_size=0.18 / 40)
+    vg = vol.to(cuda).requires_grad_(True)
+    sg = scale.to(cuda).requires_grad_(True)
+    mlp_g = __import__("copy").deepcopy(mlp).to(cuda)
+    out = params_from_volume_3d(vg, mlp_g, grid.to(cuda), sg, angle=0.4, p_3d=torch.tensor([0.0, 0.1, 0.0]), **kw)
+    cot = torch.randn(out.shape, generator=torch.Generator().manual_seed(10))
+    (out * cot.to(cuda)).sum().backward()
+    vc = vol.clone().requires_grad_(True)
+    sc = scale.clone().requires_grad_(True)
+    mask, mt, probs = select_mask(vc[0].detach(), 0.25, 0.25, 0.05, 1024, 16000)
+    probs = torch.sigmoid(vc[0] - mt)
+    ref = head3d(mlp(vc[:, mask].T), probs[mask], sc, grid[mask], 0.25, (0.0, 0.99), 0.18 / 40)
+    ref = pose_transform_3d(ref, 0.4, torch.tensor([0.0, 0.1, 0.0]))
+    (ref * cot).sum().backward()
+    assert out.shape == ref.shape
+    o, amb = _sign_fix(out.detach().cpu(), ref.detach())
+    assert_close(o, ref.detach(), rtol=1e-4, atol=1e-5, what="params")
+    grad_close(vg.grad.cpu(), vc.grad, what="grad volume", max_frac=1e-3)
+    grad_close(sg.grad.cpu(), sc.grad, what="grad scale")
+
+
+@pytest.mark.gpu
+def test_fused_head_timing_vs_torch_restatement(cuda, capsys):
+    """Times selection + head + pose, fwd+bwd, at the model's scale (64^3 voxels, max_n 16000):
+    libgsr vs the reference's torch sequence (oracle/head.py run on the GPU).  Informational
+    (printed), and the fused path must not be slower."""
+    import time
+    from gsr.head import params_from_volume_3d
+    from oracle.head import head3d, pose_transform_3d, select_mask
+    torch.manual_seed(0)
+    c, M = 8, 64 ** 3
+    mlp = torch.nn.Sequential(torch.nn.Linear(c, 128), torch.nn.ReLU(), torch.nn.Linear(128, 14)).to(cuda)
+    vol = torch.randn(c, M, device=cuda).requires_grad_(True)
+    grid = (torch.rand(M, 3, device=cuda) - 0.5) * 0.18
+    scale = torch.tensor([-5.5], device=cuda).requires_grad_(True)
+    p3 = torch.tensor([0.0, 0.1, 0.0], device=cuda)
+    kw = dict(mask_threshold=0.25, prob_threshold=0.25, mask_threshold_delta=0.05, min_n=1024, max_n=16000,
+              color_clip=(0.0, 0.99), voxel_size=0.18 / 64)
+
+    def fused():
+        out = params_from_volume_3d(vol, mlp, grid, scale, angle=0.4, p_3d=p3, **kw)
+        out.sum().backward()
+
+    def reference():
+        mask, mt, _ = select_mask(vol[0].detach(), 0.25, 0.25, 0.05, 1024, 16000)
+        probs = torch.sigmoid(vol[0] - mt)
+        ref = head3d(mlp(vol[:, mask].T), probs[mask], scale, grid[mask], 0.25, (0.0, 0.99), 0.18 / 64)
+        pose_transform_3d(ref, 0.4, p3).sum().backward()
+
+    def timeit(fn, reps=10):
+        fn()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / reps * 1e3
+
+    t_fused, t_ref = timeit(fused), timeit(reference)
+    with capsys.disabled():
+        print(f"\n[head] selection+MLP+head+pose fwd+bwd, 64^3 voxels: fused {t_fused:.3f} ms, "
+              f"torch restatement {t_ref:.3f} ms ({t_ref / t_fused:.1f}x)")
+    assert t_fused < t_ref
