@@ -45,6 +45,10 @@ def parse():
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the CPU oracle timing")
     ap.add_argument("--cpu-views", type=int, default=1, help="views in the bounded CPU sample")
+    ap.add_argument("--shard", default="views", choices=["views", "bands"],
+                    help="N>1, 3D: 'views' = every rank renders its own 6 views (weak scaling); "
+                         "'bands' = the ranks split the tile rows of ONE 6-view job (strong scaling, "
+                         "bands balanced by the per-row list lengths of a warm-up render)")
     ap.add_argument("--loss", default="none", choices=["none", "fused", "torch"],
                     help="3D, 1 GPU: time render + the reference IoU/L1 training loss "
                          "(train_script.py:128-133) fused into the kernels, or as plain torch ops")
@@ -171,7 +175,19 @@ def main():
         v_rgb = torch.randn(cfg.height, cfg.width, 3, generator=g).to(dev)
         v_alpha = torch.randn(cfg.height, cfg.width, generator=g).to(dev)
 
-    if cfg.mode == "3d" and world > 1:
+    bands = args.shard == "bands" and cfg.mode == "3d" and world > 1
+    if bands:
+        # one 6-view job split by tile rows; bands balanced by a full warm-up render's row work
+        from gsr.multiview import band_shard, row_work, sharded_backward_bands
+        th, tw = (cfg.height + 15) // 16, (cfg.width + 15) // 16
+        with torch.no_grad():
+            R.render3d(params, Vd, Kd, cfg.width, cfg.height, bg)
+        weights = row_work(R.tile_work(), C, th, tw)
+        my_band = band_shard(th, world, rank, weights)
+
+        def render_band(p, Vs, Ks, band):
+            return R.render3d(p, Vs, Ks, cfg.width, cfg.height, bg, R.RenderOptions3D(band=band))
+    elif cfg.mode == "3d" and world > 1:
         # all ranks hold the same Gaussians; this rank renders its shard of the 6*world views
         from gsr.multiview import sharded_backward, view_shard
         V_all, K_all = ring_cameras(C * world, cfg.width, cfg.height)
@@ -204,6 +220,8 @@ def main():
             li = 1 - ((inter + 1e-6) / (union + 1e-6)).mean()
             lm = torch.abs(timg - rgb.permute(0, 3, 1, 2)).sum() / tmask.sum()
             (li + lm).backward()
+        elif bands:
+            params.grad = sharded_backward_bands(render_band, params, Vd, Kd, v_rgb, v_alpha, th, weights)
         elif cfg.mode == "3d" and world > 1:
             params.grad = sharded_backward(render_views, params, V_all, K_all, vr_all, va_all)
         elif cfg.mode == "3d":
@@ -251,10 +269,28 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
 
+    allreduce_ms = None
+    if world > 1:
+        # the step's one collective, timed on its own: all_reduce(SUM) of the fp32 v_params
+        buf = torch.zeros(cfg.N, p_dim, device=dev)
+        for _ in range(3):
+            dist.all_reduce(buf)
+        torch.cuda.synchronize()
+        dist.barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            dist.all_reduce(buf)
+        e1.record()
+        torch.cuda.synchronize()
+        t = torch.tensor([e0.elapsed_time(e1) / 10], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        allreduce_ms = float(t)
+
     st = R.last_stats()
     I = st.get("n_isect", 0)
     I_eff = R.effective_isect()
-    views_per_step = C * world
+    views_per_step = C if bands else C * world
     value = views_per_step * args.steps / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
 
@@ -278,17 +314,20 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if bands else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (SURVEY.md §8(d) distribution A, seed 1000+config)",
         "config": {"workload": cfg.name, "N_gauss": cfg.N, "width": cfg.width, "height": cfg.height,
                    "views_per_gpu": C, "background": "white", "loss": args.loss,
-                   "parallelism": f"view-sharded x{world} + RCCL all-reduce of v_params" if world > 1 else "single GPU"},
+                   "parallelism": (f"tile-row bands x{world} (band {my_band[0]}-{my_band[1]} on rank 0) + RCCL "
+                                   f"all-reduce of v_params" if bands else
+                                   f"view-sharded x{world} + RCCL all-reduce of v_params" if world > 1 else "single GPU")},
         "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes": alg, "avg_ms": dom_ms, "launches": dom_n},
         "kernels_ms": {k: round(v[0], 4) for k, v in sorted(breakdown.items())},
+        "allreduce_ms": allreduce_ms,
         "sets_per_s": value / C,
         "pair_evals_per_s": 2.0 * 256.0 * I_eff * (1 if cfg.mode == "3d" else C) * world / (ms_per_step * 1e-3),
         "step_roofline": {"algorithmic_bytes": sb, "achieved": sb / (ms_per_step * 1e-3) / 1e9,

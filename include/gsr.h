@@ -102,12 +102,15 @@ int gsr_selftest_lds_order(int32_t* violations, void* stream);
  * adapter's activations; GSR_INPUT_GSPLAT: activated values as gsplat's rasterization()
  * takes them (no exp/sigmoid/clamp; the quaternion is only renormalised).  viewmats [C,4,4] world->cam
  * row-major; Ks [C,3,3].  Writes rec [C*N*12], depth [C*N], rect [C*N*2], isect_count [C*N] and
- * writes tile_count [C*tiles] (zeroed, then accumulated).  Culled Gaussians get count 0. */
+ * writes tile_count [C*tiles] (zeroed, then accumulated).  Culled Gaussians get count 0.
+ * [band_y0, band_y1): the tile rows this call bins (band_y1 = -1: all rows).  Multi-GPU band
+ * sharding gives each rank a band; tiles outside it stay empty (background)
+ * and their entries contribute nothing, so the ranks' gradients sum to the full gradient. */
 int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride,
                       const float* viewmats, const float* Ks, int C, int width, int height,
                       float near_plane, float far_plane, float radius_clip, float eps2d,
-                      int radius_mode, int input_mode, float* rec, float* depth, uint32_t* rect,
-                      int32_t* isect_count, int32_t* tile_count, void* stream);
+                      int radius_mode, int input_mode, int band_y0, int band_y1, float* rec, float* depth,
+                      uint32_t* rect, int32_t* isect_count, int32_t* tile_count, void* stream);
 
 /* 2D projection: params [N, >=9] (layout src/gaussian_renderer.py:314-318).  The tile rect
  * covers every pixel where opacity*exp(-q) >= eps_cut (the reference is dense; eps_cut
@@ -290,6 +293,18 @@ int gsr_pose3d_fwd(const float* params, int64_t N, int64_t row_stride, double an
                    float* out, void* stream);
 int gsr_pose3d_bwd(const float* params, int64_t N, int64_t row_stride, double angle, const float* g_out,
                    float* g_params, void* stream);
+
+/* ---- Shape carving -----------------------------------------------
+ * ShapeCarver.forward (src/shape_carver.py:330-366, adaptive=False): the [4, n_voxels]
+ * volume (mask occupancy, then rgb) from C masks [C,1,H,W] and images [C,3,H,W], with the
+ * scatter-min visibility of ray_cast_visibility_torch (:132-204) done as 64-bit atomicMin.
+ * grid [n_voxels,3] = the model's un-posed grid points; center [3] (device) and angle pose
+ * it (get_grid_points :369-374); Ks [C,3,3] and Es [C,4,4] are HOST arrays (fixed model
+ * cameras).  Ties in the per-pixel minimum distance go to the lower voxel index. */
+size_t gsr_carve_workspace(int64_t n_voxels, int C, int height);
+int gsr_carve_volume(const float* grid, int64_t n_voxels, const float* center, double angle, const float* Ks,
+                     const float* Es, int C, const float* mask, const float* rgb, int height, int width,
+                     float fill, float nonvisible_weight, void* ws, size_t ws_bytes, float* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -166,11 +166,13 @@ def project3d(means, quats, scales, opac, viewmats, Ks, width, height,
     return Projection(mean2d, conics, z.detach(), radii, valid)
 
 
-def isect_tiles(means2d, radii, depths, width, height, tile=Ref3D.TILE, depth_order=True):
+def isect_tiles(means2d, radii, depths, width, height, tile=Ref3D.TILE, depth_order=True, band=None):
     """SURVEY.md Appendix A.2.  Returns (tile_offsets [C*T+1] int64, ids [I] int64).
 
     ids are flatten ids c*N+n; list order within a tile is (depth float bits, c*N+n) when
-    ``depth_order`` (3D), else parameter index order (2D).
+    ``depth_order`` (3D), else parameter index order (2D).  ``band`` = (y0, y1) tile rows
+    restricts binning to those rows (the build's multi-GPU band sharding, not a reference
+    feature; the full-image result restricted to the band is unchanged).
     """
     C, N = depths.shape
     tw = (width + tile - 1) // tile
@@ -188,6 +190,9 @@ def isect_tiles(means2d, radii, depths, width, height, tile=Ref3D.TILE, depth_or
         x1 = torch.clamp(torch.ceil(tile_x + trx), min=0, max=tw).to(torch.int64)
         y0 = torch.clamp(torch.floor(tile_y - try_), min=0, max=th).to(torch.int64)
         y1 = torch.clamp(torch.ceil(tile_y + try_), min=0, max=th).to(torch.int64)
+        if band is not None:
+            y0 = y0.clamp(min=band[0])
+            y1 = y1.clamp(max=band[1])
         live = (radii[..., 0] > 0) | (radii[..., 1] > 0)
         wcnt = torch.where(live, (x1 - x0).clamp(min=0), torch.zeros_like(x0))
         hcnt = torch.where(live, (y1 - y0).clamp(min=0), torch.zeros_like(y0))
@@ -411,7 +416,7 @@ class _Raster3D(torch.autograd.Function):
 
 def render3d(params, viewmats, Ks, width, height, background, *,
              radius_mode=Ref3D.RADIUS_OPACITY_AABB, near=Ref3D.NEAR, far=Ref3D.FAR,
-             radius_clip=Ref3D.RADIUS_CLIP, eps2d=Ref3D.EPS2D, return_meta=False, activated=False):
+             radius_clip=Ref3D.RADIUS_CLIP, eps2d=Ref3D.EPS2D, return_meta=False, activated=False, band=None):
     """Full oracle of GaussianRenderer3D.render for C cameras: rgb [C,H,W,3], alpha [C,H,W].
 
     Differentiable w.r.t. ``params`` ([N,14]); viewmats [C,4,4], Ks [C,3,3], background [3]
@@ -430,7 +435,7 @@ def render3d(params, viewmats, Ks, width, height, background, *,
         means, quats, scales, colors, opac = activations3d(params)
     proj = project3d(means, quats, scales, opac, viewmats, Ks, width, height, near=near, far=far,
                      radius_clip=radius_clip, eps2d=eps2d, radius_mode=radius_mode)
-    offsets, ids = isect_tiles(proj.means2d, proj.radii, proj.depths, width, height)
+    offsets, ids = isect_tiles(proj.means2d, proj.radii, proj.depths, width, height, band=band)
     N = params.shape[0]
     colors_c = colors[None].expand(C, N, 3)
     opac_c = opac[None].expand(C, N)

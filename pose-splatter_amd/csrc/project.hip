@@ -47,8 +47,8 @@ template <int RMODE>
 __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
     const float* __restrict__ params, int64_t N, int64_t stride, const float* __restrict__ viewmats,
     const float* __restrict__ Ks, int W, int H, float near_plane, float far_plane,
-    float radius_clip, float eps2d, int input_mode, int tw, int th, int use_lds, Splat* __restrict__ rec,
-    float* __restrict__ depth, uint2* __restrict__ rect, int32_t* __restrict__ cnt,
+    float radius_clip, float eps2d, int input_mode, int tw, int th, int band_y0, int band_y1, int use_lds,
+    Splat* __restrict__ rec, float* __restrict__ depth, uint2* __restrict__ rect, int32_t* __restrict__ cnt,
     int32_t* __restrict__ tile_count) {
   extern __shared__ int hist[];
   const int c = blockIdx.y;
@@ -99,6 +99,9 @@ __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
       x1 = (int)fminf(fmaxf(ceilf(tix + trx), 0.f), (float)tw);
       y0 = (int)fminf(fmaxf(floorf(tiy - try_), 0.f), (float)th);
       y1 = (int)fminf(fmaxf(ceilf(tiy + try_), 0.f), (float)th);
+      // tile-row band of this rank (multi-GPU band sharding; the full image by default)
+      y0 = max(y0, band_y0);
+      y1 = min(y1, band_y1);
       if (x1 < x0) x1 = x0;
       if (y1 < y0) y1 = y0;
       // record: the compositing inputs plus the per-Gaussian constants of the exact sub-tile
@@ -186,8 +189,8 @@ const char* gsr_last_error(void) { return g_err; }
 int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride, const float* viewmats,
                       const float* Ks, int C, int width, int height, float near_plane,
                       float far_plane, float radius_clip, float eps2d, int radius_mode, int input_mode,
-                      float* rec, float* depth, uint32_t* rect, int32_t* isect_count, int32_t* tile_count,
-                      void* stream) {
+                      int band_y0, int band_y1, float* rec, float* depth, uint32_t* rect, int32_t* isect_count,
+                      int32_t* tile_count, void* stream) {
   GSR_REQUIRE(N >= 0 && C >= 1 && C <= 65535, "gsr3d_project_fwd: bad N=%lld or C=%d", (long long)N, C);
   GSR_REQUIRE(width > 0 && height > 0, "gsr3d_project_fwd: bad image %dx%d", width, height);
   GSR_REQUIRE(row_stride >= 14, "gsr3d_project_fwd: row_stride %lld < 14", (long long)row_stride);
@@ -197,6 +200,9 @@ int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride, const 
               "gsr3d_project_fwd: bad input_mode %d", input_mode);
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   GSR_REQUIRE(tw < 65536 && th < 65536, "gsr3d_project_fwd: image too large");
+  if (band_y1 < 0) band_y1 = th;
+  GSR_REQUIRE(band_y0 >= 0 && band_y0 <= band_y1 && band_y1 <= th, "gsr3d_project_fwd: bad band [%d,%d) of %d tile rows",
+              band_y0, band_y1, th);
   if (hipMemsetAsync(tile_count, 0, (size_t)C * tw * th * sizeof(int32_t), (hipStream_t)stream) != hipSuccess) {
     set_error("gsr3d_project_fwd: tile_count memset failed");
     return GSR_ELAUNCH;
@@ -210,13 +216,13 @@ int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride, const 
   if (radius_mode == GSR_RADIUS_OPACITY_AABB)
     hipLaunchKernelGGL(k_project3d_fwd<GSR_RADIUS_OPACITY_AABB>, grid, dim3(kProjThreads), lds, s,
                        params, N, row_stride, viewmats, Ks, width, height, near_plane, far_plane,
-                       radius_clip, eps2d, input_mode, tw, th, use_lds, (Splat*)rec, depth, (uint2*)rect, isect_count,
-                       tile_count);
+                       radius_clip, eps2d, input_mode, tw, th, band_y0, band_y1, use_lds, (Splat*)rec, depth,
+                       (uint2*)rect, isect_count, tile_count);
   else
     hipLaunchKernelGGL(k_project3d_fwd<GSR_RADIUS_ISOTROPIC_3SIGMA>, grid, dim3(kProjThreads), lds, s,
                        params, N, row_stride, viewmats, Ks, width, height, near_plane, far_plane,
-                       radius_clip, eps2d, input_mode, tw, th, use_lds, (Splat*)rec, depth, (uint2*)rect, isect_count,
-                       tile_count);
+                       radius_clip, eps2d, input_mode, tw, th, band_y0, band_y1, use_lds, (Splat*)rec, depth,
+                       (uint2*)rect, isect_count, tile_count);
   GSR_LAUNCH_CHECK("k_project3d_fwd");
   return GSR_OK;
 }

@@ -55,6 +55,7 @@ class RenderOptions3D:
     eps2d: float = 0.3
     radius_mode: int = _lib.RADIUS_OPACITY_AABB
     input_mode: int = _lib.INPUT_ADAPTER   # INPUT_GSPLAT: rows hold activated gsplat inputs
+    band: tuple = (0, -1)                  # tile rows [y0, y1) binned (multi-GPU band sharding)
 
 
 _last_stats = {}
@@ -251,6 +252,17 @@ def effective_isect(stats: dict | None = None) -> int:
     return int((te - st).clamp(min=0).sum())
 
 
+def tile_work(stats: dict | None = None) -> torch.Tensor:
+    """Per-tile list entries the last forward's raster read (tile_end - start), [C*T] int64 —
+    the work weights for multi-GPU band balancing (gsr.multiview.band_shard)."""
+    s = _last_stats if stats is None else stats
+    if "_bins" not in s:
+        raise RuntimeError("tile_work: no forward has run")
+    te = s["_bins"].tile_end.to(torch.int64)
+    st = s["_bins"].tile_off[:-1].to(torch.int64)
+    return (te - st).clamp(min=0)
+
+
 def _background(bg: torch.Tensor, C: int, dev) -> torch.Tensor:
     """bg [3] or [C,3] -> contiguous float32 [C,3] on dev (expanded copies are cached per
     source tensor version, so a fixed background costs no kernel per call).  The cache entry
@@ -284,7 +296,8 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
     with _timed("project3d_fwd"):
       check(L.gsr3d_project_fwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height,
                               opts.near_plane, opts.far_plane, opts.radius_clip, opts.eps2d,
-                              opts.radius_mode, opts.input_mode, q["rec"], q["depth"], q["rect"], q["cnt"], q["tile_cnt"], stream),
+                              opts.radius_mode, opts.input_mode, opts.band[0], opts.band[1], q["rec"], q["depth"],
+                              q["rect"], q["cnt"], q["tile_cnt"], stream),
           "gsr3d_project_fwd")
     b.guess_post(with_chunks=True)
     b.offsets(stream)

@@ -37,7 +37,12 @@ def _render(p, V, K):
     return render3d(p, V, K, 40, 32, torch.ones(3))
 
 
-def _worker(rank, world, port, out):
+def _render_band(p, V, K, band):
+    from oracle.oracle3d import render3d
+    return render3d(p, V, K, 40, 32, torch.ones(3), band=band)
+
+
+def _worker(rank, world, port, out, mode="views"):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "pose-splatter_amd")]
@@ -45,9 +50,12 @@ def _worker(rank, world, port, out):
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(2)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from gsr.multiview import sharded_backward
+    from gsr.multiview import sharded_backward, sharded_backward_bands
     p, V, K, vr, va = _scene()
-    grad = sharded_backward(_render, p, V, K, vr, va)
+    if mode == "views":
+        grad = sharded_backward(_render, p, V, K, vr, va)
+    else:
+        grad = sharded_backward_bands(_render_band, p, V, K, vr, va, rows=2, weights=[3.0, 1.0])
     out[rank] = grad
     dist.destroy_process_group()
 
@@ -63,3 +71,49 @@ def test_view_sharded_allreduce_matches_single_process(world):
     for r in range(world):
         assert torch.allclose(out[r], ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max())), r
     assert torch.equal(out[0], out[1])
+
+
+def test_band_shard_partition():
+    from gsr.multiview import band_shard
+    for rows, world in [(32, 8), (5, 8), (36, 3), (1, 2)]:
+        bands = [band_shard(rows, world, r) for r in range(world)]
+        assert bands[0][0] == 0 and bands[-1][1] == rows
+        assert all(bands[i][1] == bands[i + 1][0] for i in range(world - 1))
+    w = [1.0] * 10 + [9.0] * 2 + [1.0] * 20          # one heavy pair of rows
+    bands = [band_shard(32, 4, r, w) for r in range(4)]
+    assert bands[0][0] == 0 and bands[-1][1] == 32
+    assert all(bands[i][1] == bands[i + 1][0] for i in range(3))
+    loads = [sum(w[a:b]) for a, b in bands]
+    assert max(loads) <= sum(w) / 4 + max(w)
+
+
+def test_band_render_equals_full_render_in_band():
+    """Oracle: binning only a band of tile rows leaves those rows' pixels unchanged, and the
+    band gradients sum to the full gradient."""
+    from oracle.oracle3d import render3d
+    p, V, K, vr, va = _scene()
+    full_rgb, full_a = render3d(p, V, K, 40, 32, torch.ones(3))
+    grads = []
+    for band in [(0, 1), (1, 2)]:
+        pc = p.clone().requires_grad_(True)
+        rgb, a = render3d(pc, V, K, 40, 32, torch.ones(3), band=band)
+        rows = slice(16 * band[0], min(32, 16 * band[1]))
+        assert torch.equal(rgb[:, rows], full_rgb[:, rows]) and torch.equal(a[:, rows], full_a[:, rows])
+        # cotangents outside the band meet no Gaussians there
+        torch.autograd.backward([rgb, a], [vr, va])
+        grads.append(pc.grad)
+    pf = p.clone().requires_grad_(True)
+    torch.autograd.backward(list(render3d(pf, V, K, 40, 32, torch.ones(3))), [vr, va])
+    assert torch.allclose(grads[0] + grads[1], pf.grad, rtol=1e-5, atol=1e-6 * float(pf.grad.abs().max()))
+
+
+@pytest.mark.parametrize("world", [2])
+def test_band_sharded_allreduce_matches_single_process(world):
+    from gsr.multiview import sharded_backward
+    p, V, K, vr, va = _scene()
+    ref = sharded_backward(_render, p, V, K, vr, va)
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out, "bands"), nprocs=world, join=True)
+    for r in range(world):
+        assert torch.allclose(out[r], ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max())), r

@@ -352,3 +352,30 @@ def test_2d_deterministic(cuda):
     b = _run_gpu2d(p, W, H, torch.ones(3), cuda, vr, va)
     for x, y in zip(a, b):
         assert torch.equal(x, y)
+
+
+@pytest.mark.gpu
+def test_3d_band_sharding(cuda):
+    """Multi-GPU band sharding on one device: each band's rows are bitwise
+    the full render's rows, and the band gradients sum to the full gradient."""
+    from gsr.render import RenderOptions3D, render3d
+    from gsr.multiview import band_shard
+    W, H, C = 96, 80, 3
+    p, V, K = _scene3d(20000, W, H, C, 21)
+    bg = torch.ones(3, device=cuda)
+    vr, va = _cot(C, H, W, 22)
+    vr, va = vr.to(cuda), va.to(cuda)
+    pf = p.to(cuda).requires_grad_(True)
+    rgb_f, a_f = render3d(pf, V.to(cuda), K.to(cuda), W, H, bg)
+    torch.autograd.backward([rgb_f, a_f], [vr, va])
+    th = (H + 15) // 16
+    total = torch.zeros_like(pf)
+    for r in range(3):
+        band = band_shard(th, 3, r)
+        pb = p.to(cuda).requires_grad_(True)
+        rgb, a = render3d(pb, V.to(cuda), K.to(cuda), W, H, bg, RenderOptions3D(band=band))
+        rows = slice(16 * band[0], min(H, 16 * band[1]))
+        assert torch.equal(rgb[:, rows], rgb_f[:, rows]) and torch.equal(a[:, rows], a_f[:, rows])
+        torch.autograd.backward([rgb, a], [vr, va])
+        total += pb.grad
+    grad_close(total.cpu(), pf.grad.cpu(), what="band-summed grad")
