@@ -624,6 +624,8 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
   const float* bgc = bg + st.c * 3;
   const float bgdot = bgc[0] * vr + bgc[1] * vg + bgc[2] * vb;
   const float vTa = Tf * (va - bgdot);
+  // the suffix colour enters only through its dot product with the pixel's colour cotangent
+  float Sv = Sr * vr + Sg * vg + Sb * vb;
   int wlast = last;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wlast = max(wlast, __shfl_xor(wlast, o, 64));
@@ -687,18 +689,20 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
       acc[g * kPartial + 6] = fac * vr;
       acc[g * kPartial + 7] = fac * vg;
       acc[g * kPartial + 8] = fac * vb;
-      const float v_al = (p2.x * T - Sr * ra) * vr + (p2.y * T - Sg * ra) * vg + (p2.z * T - Sb * ra) * vb + vTa * ra;
+      const float cv = p2.x * vr + p2.y * vg + p2.z * vb;
+      const float v_al = T * cv + ra * (vTa - Sv);
       const bool unclamped = valid && raw <= kAlphaMax;
       const float v_sig = unclamped ? -raw * v_al : 0.f;
-      acc[g * kPartial + 2] = v_sig * dx * dx;
-      acc[g * kPartial + 3] = v_sig * dx * dy;
-      acc[g * kPartial + 4] = v_sig * dy * dy;
-      acc[g * kPartial + 0] = v_sig * (2.f * p1.x * dx + p1.y * dy);
-      acc[g * kPartial + 1] = v_sig * (p1.y * dx + 2.f * p1.z * dy);
+      // moments of v_sig: (dx, dy) here; the mean gradient (2a dx + b dy, b dx + 2c dy) is
+      // formed from their sums per entry after the reduction
+      const float tx = v_sig * dx, ty = v_sig * dy;
+      acc[g * kPartial + 0] = tx;
+      acc[g * kPartial + 1] = ty;
+      acc[g * kPartial + 2] = tx * dx;
+      acc[g * kPartial + 3] = tx * dy;
+      acc[g * kPartial + 4] = ty * dy;
       acc[g * kPartial + 5] = unclamped ? vis * v_al : 0.f;
-      Sr += p2.x * fac;
-      Sg += p2.y * fac;
-      Sb += p2.z * fac;
+      Sv += fac * cv;
     }
     const float sum = reduce64(acc);
     const int g = st.lane / kPartial;
@@ -718,6 +722,10 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
     float v[kPartial];
 #pragma unroll
     for (int q = 0; q < kPartial; ++q) v[q] = L[q][0][k] + L[q][1][k];
+    const float4 p1 = s_p1[k];
+    const float mx = v[0], my = v[1];
+    v[0] = 2.f * p1.x * mx + p1.y * my;
+    v[1] = p1.y * mx + 2.f * p1.z * my;
     store_partial_row(partial, k_of_s[b0 + k], v);
   }
 }
