@@ -701,7 +701,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
       acc[g * kPartial + 2] = tx * dx;
       acc[g * kPartial + 3] = tx * dy;
       acc[g * kPartial + 4] = ty * dy;
-      acc[g * kPartial + 5] = unclamped ? vis * v_al : 0.f;
+      acc[g * kPartial + 5] = v_sig;   // v_opacity = vis v_al = -v_sig / o (formed per entry below)
       Sv += fac * cv;
     }
     const float sum = reduce64(acc);
@@ -726,6 +726,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
     const float mx = v[0], my = v[1];
     v[0] = 2.f * p1.x * mx + p1.y * my;
     v[1] = p1.y * mx + 2.f * p1.z * my;
+    v[5] = -v[5] / s_p0[k].z;
     store_partial_row(partial, k_of_s[b0 + k], v);
   }
 }
