@@ -25,10 +25,25 @@ __device__ __forceinline__ void gather_partials(const uint2 r, int tw, int64_t c
                                                 const uint64_t* __restrict__ tile_cut,
                                                 const float* __restrict__ partial, float (&acc)[kPartial]) {
   const int x0 = r.x & 0xffff, x1 = r.x >> 16, y0 = r.y & 0xffff, y1 = r.y >> 16;
-  const float4* row = reinterpret_cast<const float4*>(partial + (int64_t)off * kPartialStride);
-  for (int ty = y0; ty < y1; ++ty) {
-    for (int tx = x0; tx < x1; ++tx, row += 3) {
-      if (key < tile_cut[ct_base + ty * tw + tx]) {
+  const int cnt = (x1 - x0) * (y1 - y0);
+  const float4* rows = reinterpret_cast<const float4*>(partial + (int64_t)off * kPartialStride);
+  // four tiles per round: their cut keys first, then the rows that exist (two dependent
+  // memory round trips per four tiles instead of two per tile)
+  int tx = x0, ty = y0;   // tile of entry j0 (row-major over the rect)
+  for (int j0 = 0; j0 < cnt; j0 += 4) {
+    bool has[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      has[u] = j0 + u < cnt && key < tile_cut[ct_base + ty * tw + tx];
+      if (++tx == x1) {
+        tx = x0;
+        ++ty;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (has[u]) {
+        const float4* row = rows + 3 * (j0 + u);
         const float4 a = row[0], b = row[1];
         const float c = row[2].x;
         acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
@@ -47,7 +62,10 @@ __device__ __forceinline__ void gather_partials(const uint2 r, int tw, int64_t c
 // chain (rotation / scale / quaternion normalisation / adapter activations).
 constexpr int kContrib = 16;   // v_m[3], V_M[9], v_col[3], v_op
 
-__global__ __launch_bounds__(kBwdThreads) void k_project3d_bwd(
+#ifndef GSR_PBWD_MINB
+#define GSR_PBWD_MINB 1
+#endif
+__global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
     const float* __restrict__ params, int64_t N, int64_t stride, const float* __restrict__ viewmats,
     const float* __restrict__ Ks, int C, int W, int H, float eps2d, int input_mode, int tw, int th,
     const uint2* __restrict__ rect,
@@ -73,12 +91,16 @@ __global__ __launch_bounds__(kBwdThreads) void k_project3d_bwd(
     Geo3D g;
     for (int c = slot; c < C; c += CPB) {
       const int64_t cn = (int64_t)c * N + n;
-      if (isect_count[cn] <= 0) continue;
+      // the (c,n) scalars load together (no dependent round trip before the rect / key)
+      const int cnt = isect_count[cn];
+      const uint2 rc = rect[cn];
+      const int off = isect_offset[cn];
+      const uint64_t key = sort_key(depth, cn, GSR_ORDER_DEPTH);
+      if (cnt <= 0) continue;
       float acc[kPartial];
 #pragma unroll
       for (int v = 0; v < kPartial; ++v) acc[v] = 0.f;
-      gather_partials(rect[cn], tw, (int64_t)c * T, sort_key(depth, cn, GSR_ORDER_DEPTH), isect_offset[cn],
-                      tile_cut, partial, acc);
+      gather_partials(rc, tw, (int64_t)c * T, key, off, tile_cut, partial, acc);
       const Cam cam = load_cam(viewmats + c * 16, Ks + c * 9);
       // recompute the forward geometry (not culled: it has intersections)
       geo3d(a, cam, W, H, 0.f, 3.4e38f, eps2d, g);
