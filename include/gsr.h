@@ -186,20 +186,28 @@ int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t*
                      const int32_t* last, const float* v_rgb, const float* v_alpha,
                      const int32_t* k_of_s, float* partial, void* stream);
 
-/* 2D index-order compositor (src/gaussian_renderer.py:416-425), integer pixel centres.
- * rgb = canvas + (1-A)*bg, alpha = A.  Same outputs as the 3D call (final_T = 1-A unused). */
+/* 2D index-order compositor (src/gaussian_renderer.py:416-425), integer pixel centres, on
+ * the 3D kernels' structure (C = 1, index-order keys, the forward's chunk records feed a
+ * chunk-parallel backward).  rgb = canvas + (1-A)*bg, alpha = A.  Arithmetic in
+ * transmittance form; a pixel stops after the entry that takes T to <= 2^-25 (the
+ * reference's A == 1.0f).  Pairs with alpha < eps_cut (the binning's extent cut) are left
+ * out.  final_T [H,W,2] = (T_final, T before the pixel's last composited entry). */
 int gsr2d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
-                     int width, int height, const float* bg, float* rgb, float* alpha,
-                     int32_t* last, int32_t* tile_end, uint64_t* tile_cut, void* stream);
+                     const int32_t* tile_order, const int32_t* chunk_base, int width, int height,
+                     float eps_cut, const float* bg, int32_t n_busy, gsr_bin_stats* stats,
+                     float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
+                     uint64_t* tile_cut, float* chunk_state, int32_t* chunk_tile,
+                     int32_t* chunk_list, void* stream);
 
-/* Workspace for gsr2d_raster_bwd (transmittance checkpoints), bytes. */
-size_t gsr2d_raster_bwd_workspace(int64_t n_isect, int64_t CT);
-
+/* Backward of gsr2d_raster_fwd (the reference's autograd of the recursion), same contract
+ * as gsr3d_raster_bwd with C = 1. */
 int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
-                     const int32_t* tile_end, const int32_t* busy_tiles, int32_t n_busy,
-                     int width, int height, const float* bg, const int32_t* last,
-                     const float* v_rgb, const float* v_alpha, void* workspace,
-                     size_t workspace_bytes, const int32_t* k_of_s, float* partial, void* stream);
+                     const int32_t* tile_end, const int32_t* chunk_base,
+                     const int32_t* chunk_tile, const float* chunk_state,
+                     const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
+                     int width, int height, float eps_cut, const float* bg,
+                     const float* final_T, const int32_t* last, const float* v_rgb,
+                     const float* v_alpha, const int32_t* k_of_s, float* partial, void* stream);
 
 /* ---------------------------------------------------------------- projection backward */
 

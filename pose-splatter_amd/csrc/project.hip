@@ -164,9 +164,11 @@ __global__ __launch_bounds__(kProjThreads) void k_project2d_fwd(
     }
     if (ok) {
       Splat s;
-      s.p0 = make_float4(g.u, g.v, g.op, 0.f);
-      s.p1 = make_float4(g.a, g.b, g.c, 0.f);
-      s.p2 = make_float4(g.col[0], g.col[1], g.col[2], 0.f);
+      // the raster's sub-tile cull constants (raster.hip cull_keep): L = ln(op / eps_cut)
+      // (the level set this extent bounds) and the edge slopes -b/2c, -b/2a
+      s.p0 = make_float4(g.u, g.v, g.op, logf(g.op / eps_cut));
+      s.p1 = make_float4(g.a, g.b, g.c, -g.b / (2.f * g.c));
+      s.p2 = make_float4(g.col[0], g.col[1], g.col[2], -g.b / (2.f * g.a));
       rec[n] = s;
       hist_add(hist, tile_count, use_lds, x0, x1, y0, y1, tw);
     }

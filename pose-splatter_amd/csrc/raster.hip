@@ -57,8 +57,8 @@ __device__ __forceinline__ void tile_coords(int ct, int tw, int th, int& c, int&
 template <bool IS2D>
 __device__ __forceinline__ bool cull_keep(const float4 p0, const float4 p1, const float4 p2, float bx0, float bx1,
                                           float by0, float by1) {
-  static_assert(!IS2D, "the cull constants are written by the 3D projection only");
-  const float L = p0.w;   // ln(opacity * 255): < 0 never reaches the 1/255 skip threshold
+  (void)IS2D;   // 3D: L = ln(opacity * 255); 2D: L = ln(opacity / eps_cut)
+  const float L = p0.w;   // < 0: the Gaussian never reaches the cut anywhere
   if (!(L >= 0.f)) return false;
   const float a = p1.x, b = p1.y, c = p1.z;
   if (!(a > 0.f && c > 0.f && 4.f * a * c > b * b)) return true;   // not positive definite: keep
@@ -119,7 +119,10 @@ __device__ void fill_empty(const int32_t* __restrict__ order, const int32_t* __r
       out_rgb[pix * 3 + 1] = bgc[1];
       out_rgb[pix * 3 + 2] = bgc[2];
       out_alpha[pix] = 0.f;
-      if (!IS2D) out_T[pix] = 1.f;
+      if (IS2D)
+        reinterpret_cast<float2*>(out_T)[pix] = make_float2(1.f, 1.f);
+      else
+        out_T[pix] = 1.f;
       out_last[pix] = -1;
     }
     if (threadIdx.x == 0) {
@@ -175,21 +178,34 @@ __device__ __forceinline__ int bwd_pixel_slot(int il, int jl) {
   return ((il >> 3) << 7) | ((jl >> 3) << 6) | ((il & 7) << 3) | (jl & 7);
 }
 
-__global__ __launch_bounds__(kRasterThreads) void k_raster3d_fwd(
+//
+// 2D (IS2D, the reference's index-order compositor, src/gaussian_renderer.py:416-425) runs
+// the same kernel with the reference's arithmetic in transmittance form: integer pixel
+// centres, alpha = o exp(-q) with no clamp and no skip threshold (entries with alpha below
+// eps_cut -- the binning's extent cut -- are the only ones left out, as in every sub-tile
+// the binning drops), and the saturation stop of the reference (A reaches 1.0f, after which
+// every contribution is exactly 0) becomes "stop AFTER the entry that takes T to <= 2^-25"
+// (the half-ulp of 1.0f below which A = 1 - T rounds to 1).  final_T holds (T_final,
+// T before the last composited entry) per pixel: the backward's division-free start at a
+// pixel's last entry (its 1 - alpha may be exactly 0 when opacity == 1.0f).
+constexpr float kT2DMin = 2.98023224e-8f;   // 2^-25
+
+template <bool IS2D>
+__global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ order, int W, int H, int tw, int th, const float* __restrict__ bg,
     float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
     int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end, float4* __restrict__ ckpt,
     const int32_t* __restrict__ chunk_base, int32_t* __restrict__ chunk_tile, int n_busy, int64_t CT,
-    uint64_t* __restrict__ tile_cut) {
+    uint64_t* __restrict__ tile_cut, float cut2d) {
   __shared__ float4 s_p0[4][64];
   __shared__ float4 s_p1[4][64];
   __shared__ float4 s_p2[4][64];
   __shared__ int s_max;
   const int busy_blocks = busy_grid(n_busy);
   if ((int)blockIdx.x >= busy_blocks) {
-    fill_empty<false>(order, tile_offset, n_busy, busy_blocks, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
-                      out_last, tile_end, tile_cut);
+    fill_empty<IS2D>(order, tile_offset, n_busy, busy_blocks, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
+                     out_last, tile_end, tile_cut);
     return;
   }
   // XCD-aware mapping: workgroups are dealt to the 8 XCDs round-robin by id, so the four
@@ -210,13 +226,15 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_fwd(
   const int il = oy + (p >> 2), jl = ox + (p & 3);
   const int i = ty * kTile + il, j = tx * kTile + jl;
   const bool inside = i < H && j < W;
-  const float px = (float)j + 0.5f, py = (float)i + 0.5f;
-  const float bx0 = (float)(tx * kTile + ox) + 0.5f, bx1 = bx0 + 3.f;
-  const float by0 = (float)(ty * kTile + oy) + 0.5f, by1 = by0 + 3.f;
+  const float off = IS2D ? 0.f : 0.5f;   // 2D: integer centres (src/gaussian_renderer.py:355-358)
+  const float px = (float)j + off, py = (float)i + off;
+  const float bx0 = (float)(tx * kTile + ox) + off, bx1 = bx0 + 3.f;
+  const float by0 = (float)(ty * kTile + oy) + off, by1 = by0 + 3.f;
   const int start = tile_offset[ct], end = tile_offset[ct + 1];
   if (threadIdx.x == 0) s_max = -1;
   __syncthreads();
   float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f;
+  float Tl = 1.f;   // 2D: T before this lane's latest composited entry
   int last = -1;
   bool done = !inside;
   // chunk records for the chunk-parallel backward (per pixel, per GSR_CHUNK-entry chunk)
@@ -262,7 +280,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_fwd(
       Ts = T;
       ++kcur;
     }
-    const bool keep = (b0 + lane < end) && cull_keep<false>(c0, c1, c2, bx0, bx1, by0, by1);
+    const bool keep = (b0 + lane < end) && cull_keep<IS2D>(c0, c1, c2, bx0, bx1, by0, by1);
     const unsigned long long m = __ballot(keep);
     const int n = __popcll(m);
     cnt_s += n;
@@ -285,8 +303,10 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_fwd(
       const float4 p2 = s_p2[wv][kk];
       const float dx = p0.x - px, dy = p0.y - py;
       const float sg = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
-      const float alpha = fminf(kAlphaMax, p0.z * __expf(-sg));
-      const bool valid = k < n && !done && sg >= 0.f && alpha >= kAlphaThreshold;
+      const float raw = p0.z * __expf(-sg);
+      const float alpha = IS2D ? raw : fminf(kAlphaMax, raw);
+      const bool valid = IS2D ? (k < n && !done && alpha >= cut2d)
+                              : (k < n && !done && sg >= 0.f && alpha >= kAlphaThreshold);
       const float xq = valid ? 1.f - alpha : 1.f;
       // quad prefix products of x (inclusive Q, exclusive P).  The DPP moves run in every
       // lane (a DPP read of a lane that is switched off returns 0); only the selects depend
@@ -298,14 +318,18 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_fwd(
       const float d3 = dpp_mov<kQuadPrefix1>(Qi);
       const float Pe = q >= 1 ? d3 : 1.f;             // prod_{i<q} x_i
       const float nT = T * Qi;
-      const int fs = quad_min_i(valid && nT <= kTMin ? q : 4);   // first stopping slot
-      const bool con = valid && q < fs;
-      const float vis = con ? alpha * (T * Pe) : 0.f;
+      // first stopping slot: 3D stops BEFORE the entry that takes T to <= 1e-4, 2D after
+      // the one that takes it to <= 2^-25 (the reference's A == 1.0f)
+      const int fs = quad_min_i(valid && nT <= (IS2D ? kT2DMin : kTMin) ? q : 4);
+      const bool con = valid && (IS2D ? q <= fs : q < fs);
+      const float Tq = T * Pe;
+      const float vis = con ? alpha * Tq : 0.f;
       dr += p2.x * vis;
       dg += p2.y * vis;
       db += p2.z * vis;
       last = con ? __float_as_int(p1.w) : last;
-      T = quad_min(q < fs ? nT : T);
+      if (IS2D) Tl = con ? Tq : Tl;
+      T = quad_min((IS2D ? q <= fs : q < fs) ? nT : T);
       done = done || fs < 4;
     }
     __builtin_amdgcn_wave_barrier();
@@ -331,7 +355,19 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_fwd(
   cr += Dr;
   cg += Dg;
   cb += Db;
-  last = quad_max_i(last);
+  if (IS2D) {
+    // quad arg-max of last, carrying the T before that entry
+    int ol = dpp_i<kQuadXor1>(last);
+    float oT = dpp_mov<kQuadXor1>(Tl);
+    Tl = ol > last ? oT : Tl;
+    last = max(last, ol);
+    ol = dpp_i<kQuadXor2>(last);
+    oT = dpp_mov<kQuadXor2>(Tl);
+    Tl = ol > last ? oT : Tl;
+    last = max(last, ol);
+  } else {
+    last = quad_max_i(last);
+  }
   if (q == 0 && end > start) {
     // Turn this pixel's chunk records {T at chunk start, chunk colour sum} into what the
     // backward needs at each chunk's END: {T_end, suffix colour sum of the later chunks}
@@ -362,7 +398,10 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_fwd(
     out_rgb[pix * 3 + 1] = cg + T * bgc[1];
     out_rgb[pix * 3 + 2] = cb + T * bgc[2];
     out_alpha[pix] = 1.f - T;
-    out_T[pix] = T;
+    if (IS2D)
+      reinterpret_cast<float2*>(out_T)[pix] = make_float2(T, Tl);
+    else
+      out_T[pix] = T;
     out_last[pix] = last;
   }
   if (q == 0 && last >= 0) atomicMax(&s_max, last);
@@ -383,7 +422,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_finalize(
     const float* __restrict__ depth, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ order, int n_busy, const int32_t* __restrict__ chunk_base,
     int32_t* __restrict__ tile_end, uint64_t* __restrict__ tile_cut, gsr_bin_stats* __restrict__ stats,
-    int32_t* __restrict__ chunk_list) {
+    int32_t* __restrict__ chunk_list, int key_order) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= n_busy) return;
   const int ct = order[b];
@@ -391,110 +430,12 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_finalize(
   const int m = tile_end[ct];
   const int te = m >= 0 ? m + 1 : start;
   tile_end[ct] = te;
-  tile_cut[ct] = te < end ? sort_key(depth, ids[te], GSR_ORDER_DEPTH) : ~0ull;
+  tile_cut[ct] = te < end ? sort_key(depth, ids[te], key_order) : ~0ull;
   const int nact = (te - start + kChunk3 - 1) / kChunk3;
   if (nact > 0) {
     const int pos = atomicAdd(&stats->n_active, nact);
     const int cbase = chunk_base[ct];
     for (int k = 0; k < nact; ++k) chunk_list[pos + k] = cbase + k;
-  }
-}
-
-// ---------------------------------------------------------------- 2D forward
-// Reference recursion (src/gaussian_renderer.py:416-425), integer pixel centres:
-//   contrib = g (1 - A);  canvas += contrib * colour;  A += contrib.
-// Once A == 1.0f exactly every later contribution is exactly 0, so stopping there is exact.
-__global__ __launch_bounds__(kRasterThreads) void k_raster2d_fwd(
-    const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
-    int W, int H, int tw, int th, const float* __restrict__ bg, float* __restrict__ out_rgb,
-    float* __restrict__ out_alpha, int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end,
-    uint64_t* __restrict__ tile_cut) {
-  __shared__ float4 s_p0[kRasterThreads];
-  __shared__ float4 s_p1[kRasterThreads];
-  __shared__ float4 s_p2[kRasterThreads];
-  __shared__ int s_max;
-  const int ct = blockIdx.x;
-  int c, ty, tx;
-  tile_coords(ct, tw, th, c, ty, tx);
-  const int i = ty * kTile + (threadIdx.x >> 4);
-  const int j = tx * kTile + (threadIdx.x & 15);
-  const bool inside = (i < H) && (j < W);
-  const float px = (float)j, py = (float)i;
-  const int start = tile_offset[ct], end = tile_offset[ct + 1];
-  if (threadIdx.x == 0) s_max = -1;
-  float A = 0.f, cr = 0.f, cg = 0.f, cb = 0.f;
-  int last = -1;
-  bool done = !inside;
-  for (int b0 = start; b0 < end; b0 += kRasterThreads) {
-    if (__syncthreads_count(!done) == 0) break;
-    const int e = b0 + threadIdx.x;
-    if (e < end) {
-      const Splat s = rec[ids[e]];
-      s_p0[threadIdx.x] = s.p0;
-      s_p1[threadIdx.x] = s.p1;
-      s_p2[threadIdx.x] = s.p2;
-    }
-    __syncthreads();
-    const int n = min(kRasterThreads, end - b0);
-    if (!done) {
-      for (int k = 0; k < n; ++k) {
-        const float4 p0 = s_p0[k];
-        const float4 p1 = s_p1[k];
-        const float4 p2 = s_p2[k];
-        const float dx = p0.x - px, dy = p0.y - py;
-        const float q = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
-        const float g = p0.z * __expf(-q);
-        const float contrib = g * (1.f - A);
-        cr += contrib * p2.x;
-        cg += contrib * p2.y;
-        cb += contrib * p2.z;
-        A += contrib;
-        last = b0 + k;
-        if (A == 1.f) {
-          done = true;
-          break;
-        }
-      }
-    }
-  }
-  if (inside) {
-    const int64_t pix = ((int64_t)c * H + i) * W + j;
-    const float* bgc = bg + c * 3;
-    const float Tr = 1.f - A;
-    out_rgb[pix * 3 + 0] = cr + Tr * bgc[0];
-    out_rgb[pix * 3 + 1] = cg + Tr * bgc[1];
-    out_rgb[pix * 3 + 2] = cb + Tr * bgc[2];
-    out_alpha[pix] = A;
-    out_last[pix] = last;
-  }
-  __syncthreads();
-  if (last >= 0) atomicMax(&s_max, last);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int te = s_max >= 0 ? s_max + 1 : start;
-    tile_end[ct] = te;
-    tile_cut[ct] = te < end ? sort_key(nullptr, ids[te], GSR_ORDER_INDEX) : ~0ull;
-  }
-}
-
-// ---------------------------------------------------------------- partial combine helpers
-// s_w[v][wave][k]: wave sums for entry k of the current batch.
-struct PartialLds {
-  float w[kPartial][4][kRasterThreads];
-};
-
-__device__ __forceinline__ void wave_emit(PartialLds& L, int k, bool any, float (&gv)[kPartial]) {
-  const int wv = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63;
-  if (any) {
-#pragma unroll
-    for (int v = 0; v < kPartial; ++v) {
-      const float s = wave_sum(gv[v]);
-      if (lane == 0) L.w[v][wv][k] = s;
-    }
-  } else if (lane == 0) {
-#pragma unroll
-    for (int v = 0; v < kPartial; ++v) L.w[v][wv][k] = 0.f;
   }
 }
 
@@ -505,17 +446,6 @@ __device__ __forceinline__ void store_partial_row(float* __restrict__ partial, i
   dst[0] = make_float4(v[0], v[1], v[2], v[3]);
   dst[1] = make_float4(v[4], v[5], v[6], v[7]);
   dst[2] = make_float4(v[8], 0.f, 0.f, 0.f);
-}
-
-__device__ __forceinline__ void block_store_partials(const PartialLds& L, int b0, int n,
-                                                     const int32_t* __restrict__ k_of_s,
-                                                     float* __restrict__ partial) {
-  for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    float v[kPartial];
-#pragma unroll
-    for (int q = 0; q < kPartial; ++q) v[q] = (L.w[q][0][k] + L.w[q][1][k]) + (L.w[q][2][k] + L.w[q][3][k]);
-    store_partial_row(partial, k_of_s[b0 + k], v);
-  }
 }
 
 // Cotangent of  g_iou * iou_loss + g_img * img_loss  (+ extra cotangents) at one pixel
@@ -563,15 +493,24 @@ __device__ __forceinline__ void loss_cotangent(const gsr_loss_terms& lt, int C, 
 //
 // LOSS: the pixel cotangents are not read from v_rgb / v_alpha images but generated from the
 // training loss (loss_cotangent below, gsr3d_raster_bwd_loss).
-template <bool LOSS>
-__global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
+//
+// IS2D: the same walk in "mu" form, mu_{i+1} = (value of everything after entry i) / T_{i+1}:
+//   d/d a_i = T_i (c_i.v - mu_{i+1}),   mu_i = a_i c_i.v + (1 - a_i) mu_{i+1},
+//   mu after a pixel's last entry = v.bg - v_alpha;  at a chunk end e before it,
+//   mu_e = (S_e.v + T_f mu_last) / T_e  (T_e > 2^-25: the pixel had not saturated there).
+// T_i = T_{i+1} / (1 - a_i) as in 3D, except at the pixel's last entry, whose T comes from
+// the forward (final_T .y) -- the one entry whose 1 - a may be exactly 0.  No clamp: every
+// valid pair feeds the sigma / opacity gradients.
+template <bool LOSS, bool IS2D>
+__global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ tile_end, const int32_t* __restrict__ chunk_base,
     const int32_t* __restrict__ chunk_tile, const float4* __restrict__ ckpt, int W, int H, int tw, int th,
     const float* __restrict__ bg, const float* __restrict__ final_T, const int32_t* __restrict__ last_in,
     const float* __restrict__ v_rgb, const float* __restrict__ v_alpha, float* __restrict__ partial,
     const int32_t* __restrict__ chunk_list, gsr_bin_stats* __restrict__ stats,
-    const int32_t* __restrict__ k_of_s, const gsr_loss_terms lt, int C) {
+    const int32_t* __restrict__ k_of_s, const gsr_loss_terms lt, int C, float cut2d) {
+  static_assert(!(LOSS && IS2D), "the fused loss is the 3D training loss");
   // slot kNull: a zero-opacity record (never valid) that pads survivor groups to 7
   constexpr int kNull = kChunk3;
   constexpr int kGroup = 7;
@@ -593,15 +532,21 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
   const int eff = tile_end[ct];
   const int b0 = start + kc * kChunk3;
   const int n = min(kChunk3, eff - b0);   // >= 1: the list holds chunks before tile_end only
-  const SubTile st = sub_tile<false>(ct, tw, th, W, H);
+  const SubTile st = sub_tile<IS2D>(ct, tw, th, W, H);
   const int wv = st.wv;
-  float Tf = 1.f, vr = 0.f, vg = 0.f, vb = 0.f, va = 0.f;
+  float Tf = 1.f, Tl = 1.f, vr = 0.f, vg = 0.f, vb = 0.f, va = 0.f;
   int last = -1;
   if (st.inside) {
     const int64_t pix = ((int64_t)st.c * H + st.i) * W + st.j;
     last = last_in[pix];
     if (last >= b0) {
-      Tf = final_T[pix];
+      if constexpr (IS2D) {
+        const float2 t2 = reinterpret_cast<const float2*>(final_T)[pix];
+        Tf = t2.x;
+        Tl = t2.y;
+      } else {
+        Tf = final_T[pix];
+      }
       if constexpr (LOSS) {
         loss_cotangent(lt, C, st.c, pix, (int64_t)st.i * W + st.j, (int64_t)W * H, vr, vg, vb, va);
       } else {
@@ -626,6 +571,11 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
   const float vTa = Tf * (va - bgdot);
   // the suffix colour enters only through its dot product with the pixel's colour cotangent
   float Sv = Sr * vr + Sg * vg + Sb * vb;
+  float mu = 0.f;   // 2D
+  if constexpr (IS2D) {
+    const float mu_last = bgdot - va;
+    mu = last < b0 + kChunk3 ? mu_last : (Sv + Tf * mu_last) / T;
+  }
   int wlast = last;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wlast = max(wlast, __shfl_xor(wlast, o, 64));
@@ -649,7 +599,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
   for (int q = 3; q >= 0; --q) {
     const int k = q * 64 + st.lane;
     const bool keep = k < n && (b0 + k) <= wlast &&
-                      cull_keep<false>(s_p0[k], s_p1[k], s_p2[k], st.bx0, st.bx1, st.by0, st.by1);
+                      cull_keep<IS2D>(s_p0[k], s_p1[k], s_p2[k], st.bx0, st.bx1, st.by0, st.by1);
     const unsigned long long mk = __ballot(keep);
     if (keep) {
       const unsigned long long above = st.lane == 63 ? 0ull : (mk >> (st.lane + 1));
@@ -681,18 +631,29 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
       const float sigma = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
       const float vis = __expf(-sigma);
       const float raw = p0.z * vis;
-      const float alpha = fminf(kAlphaMax, raw);
-      const bool valid = (b0 + k) <= last && sigma >= 0.f && alpha >= kAlphaThreshold;
+      const float alpha = IS2D ? raw : fminf(kAlphaMax, raw);
+      const bool valid = IS2D ? (b0 + k) <= last && alpha >= cut2d
+                              : (b0 + k) <= last && sigma >= 0.f && alpha >= kAlphaThreshold;
       const float ra = valid ? __builtin_amdgcn_rcpf(1.f - alpha) : 1.f;
-      T *= ra;
+      if (IS2D)
+        T = valid && (b0 + k) == last ? Tl : T * ra;
+      else
+        T *= ra;
       const float fac = valid ? alpha * T : 0.f;
       acc[g * kPartial + 6] = fac * vr;
       acc[g * kPartial + 7] = fac * vg;
       acc[g * kPartial + 8] = fac * vb;
       const float cv = p2.x * vr + p2.y * vg + p2.z * vb;
-      const float v_al = T * cv + ra * (vTa - Sv);
-      const bool unclamped = valid && raw <= kAlphaMax;
-      const float v_sig = unclamped ? -raw * v_al : 0.f;
+      float v_sig;
+      if constexpr (IS2D) {
+        const float dmu = cv - mu;
+        v_sig = valid ? -raw * (T * dmu) : 0.f;
+        mu = valid ? mu + alpha * dmu : mu;
+      } else {
+        const float v_al = T * cv + ra * (vTa - Sv);
+        const bool unclamped = valid && raw <= kAlphaMax;
+        v_sig = unclamped ? -raw * v_al : 0.f;
+      }
       // moments of v_sig: (dx, dy) here; the mean gradient (2a dx + b dy, b dx + 2c dy) is
       // formed from their sums per entry after the reduction
       const float tx = v_sig * dx, ty = v_sig * dy;
@@ -702,7 +663,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
       acc[g * kPartial + 3] = tx * dy;
       acc[g * kPartial + 4] = ty * dy;
       acc[g * kPartial + 5] = v_sig;   // v_opacity = vis v_al = -v_sig / o (formed per entry below)
-      Sv += fac * cv;
+      if (!IS2D) Sv += fac * cv;
     }
     const float sum = reduce64(acc);
     const int g = st.lane / kPartial;
@@ -729,152 +690,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster3d_bwd(
     v[5] = -v[5] / s_p0[k].z;
     store_partial_row(partial, k_of_s[b0 + k], v);
   }
-}
-
-// ---------------------------------------------------------------- 2D backward
-// Adjoint of the reference recursion with lambda = dL/dA_{i+1} (no division, safe when
-// A reaches 1):
-//   dL/dg_i  = T_i (v_C . c_i + lambda_{i+1}),   T_i = 1 - A_i
-//   dL/dc_i  = g_i T_i v_C
-//   lambda_i = lambda_{i+1} (1 - g_i) - g_i (v_C . c_i),   lambda_N = v_alpha - v_rgb . bg
-// A_i comes from a forward replay: A is checkpointed every kChunk entries (workspace), and
-// each chunk is replayed into registers before its backward sweep.
-constexpr int kChunk = 32;
-
-__global__ __launch_bounds__(kRasterThreads) void k_raster2d_bwd(
-    const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
-    const int32_t* __restrict__ tile_end, const int32_t* __restrict__ busy, int W, int H, int tw, int th,
-    const float* __restrict__ bg, const int32_t* __restrict__ last_in, const float* __restrict__ v_rgb,
-    const float* __restrict__ v_alpha, float* __restrict__ ckpt, const int32_t* __restrict__ k_of_s,
-    float* __restrict__ partial) {
-  __shared__ float4 s_p0[kRasterThreads];
-  __shared__ float4 s_p1[kRasterThreads];
-  __shared__ float4 s_p2[kRasterThreads];
-  __shared__ PartialLds L;
-  const int ct = busy[blockIdx.x];
-  int c, ty, tx;
-  tile_coords(ct, tw, th, c, ty, tx);
-  const int i = ty * kTile + (threadIdx.x >> 4);
-  const int j = tx * kTile + (threadIdx.x & 15);
-  const bool inside = (i < H) && (j < W);
-  const float px = (float)j, py = (float)i;
-  const int start = tile_offset[ct];
-  const int eff = tile_end[ct];
-  const int len = eff - start;
-  if (len <= 0) return;
-  float* ck = ckpt + ((int64_t)(start / kChunk) + ct) * kRasterThreads;
-  float vr = 0.f, vg = 0.f, vb = 0.f, va = 0.f;
-  int last = -1;
-  if (inside) {
-    const int64_t pix = ((int64_t)c * H + i) * W + j;
-    last = last_in[pix];
-    vr = v_rgb[pix * 3 + 0];
-    vg = v_rgb[pix * 3 + 1];
-    vb = v_rgb[pix * 3 + 2];
-    va = v_alpha[pix];
-  }
-  const float* bgc = bg + c * 3;
-  // ---- pass 1: forward replay, checkpoint A before every chunk
-  float A = 0.f;
-  for (int b0 = start; b0 < eff; b0 += kRasterThreads) {
-    __syncthreads();
-    const int e = b0 + threadIdx.x;
-    if (e < eff) {
-      const Splat s = rec[ids[e]];
-      s_p0[threadIdx.x] = s.p0;
-      s_p1[threadIdx.x] = s.p1;
-    }
-    __syncthreads();
-    const int n = min(kRasterThreads, eff - b0);
-    for (int k = 0; k < n; ++k) {
-      const int ek = b0 + k;
-      if (((ek - start) % kChunk) == 0) ck[((ek - start) / kChunk) * kRasterThreads + threadIdx.x] = A;
-      if (ek <= last) {
-        const float4 p0 = s_p0[k];
-        const float4 p1 = s_p1[k];
-        const float dx = p0.x - px, dy = p0.y - py;
-        const float q = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
-        const float g = p0.z * __expf(-q);
-        A += g * (1.f - A);
-      }
-    }
-  }
-  // ---- pass 2: backward, chunk by chunk from the end
-  float lam = va - (bgc[0] * vr + bgc[1] * vg + bgc[2] * vb);
-  const int nchunks = (len + kChunk - 1) / kChunk;
-  int loaded_b0 = -1;
-  for (int q = nchunks - 1; q >= 0; --q) {
-    const int c0 = start + q * kChunk;
-    const int cn = min(kChunk, eff - c0);
-    // stage the 256-entry batch containing this chunk (batches aligned at start + 256*m)
-    const int b0 = start + ((q * kChunk) / kRasterThreads) * kRasterThreads;
-    if (b0 != loaded_b0) {
-      __syncthreads();
-      if (loaded_b0 >= 0) block_store_partials(L, loaded_b0, min(kRasterThreads, eff - loaded_b0), k_of_s, partial);
-      __syncthreads();
-      const int e = b0 + threadIdx.x;
-      if (e < eff) {
-        const Splat s = rec[ids[e]];
-        s_p0[threadIdx.x] = s.p0;
-        s_p1[threadIdx.x] = s.p1;
-        s_p2[threadIdx.x] = s.p2;
-      }
-      loaded_b0 = b0;
-      __syncthreads();
-    }
-    const int kb = c0 - b0;   // chunk offset inside the batch
-    // replay this chunk's A_i into registers
-    float Ai[kChunk];
-    float a_run = ck[q * kRasterThreads + threadIdx.x];
-#pragma unroll
-    for (int k = 0; k < kChunk; ++k) {
-      Ai[k] = a_run;
-      if (k < cn && c0 + k <= last) {
-        const float4 p0 = s_p0[kb + k];
-        const float4 p1 = s_p1[kb + k];
-        const float dx = p0.x - px, dy = p0.y - py;
-        const float qq = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
-        const float g = p0.z * __expf(-qq);
-        a_run += g * (1.f - a_run);
-      }
-    }
-#pragma unroll
-    for (int k = kChunk - 1; k >= 0; --k) {
-      if (k < cn) {
-        const int ek = c0 + k;
-        float gv[kPartial];
-#pragma unroll
-        for (int v = 0; v < kPartial; ++v) gv[v] = 0.f;
-        const bool valid = ek <= last;
-        if (valid) {
-          const float4 p0 = s_p0[kb + k];
-          const float4 p1 = s_p1[kb + k];
-          const float4 p2 = s_p2[kb + k];
-          const float dx = p0.x - px, dy = p0.y - py;
-          const float qq = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
-          const float e_ = __expf(-qq);
-          const float g = p0.z * e_;
-          const float Ti = 1.f - Ai[k];
-          const float wc = vr * p2.x + vg * p2.y + vb * p2.z;
-          const float v_g = Ti * (wc + lam);
-          gv[6] = g * Ti * vr;
-          gv[7] = g * Ti * vg;
-          gv[8] = g * Ti * vb;
-          gv[5] = e_ * v_g;
-          const float v_q = -g * v_g;
-          gv[2] = v_q * dx * dx;
-          gv[3] = v_q * dx * dy;
-          gv[4] = v_q * dy * dy;
-          gv[0] = v_q * (2.f * p1.x * dx + p1.y * dy);
-          gv[1] = v_q * (p1.y * dx + 2.f * p1.z * dy);
-          lam = lam * (1.f - g) - g * wc;
-        }
-        wave_emit(L, kb + k, wave_ballot(valid) != 0, gv);
-      }
-    }
-  }
-  __syncthreads();
-  if (loaded_b0 >= 0) block_store_partials(L, loaded_b0, min(kRasterThreads, eff - loaded_b0), k_of_s, partial);
 }
 
 __global__ void k_selftest_reduce64(float* out) {
@@ -914,37 +729,78 @@ int gsr_selftest_reduce64(float* out, void* stream) {
   return GSR_OK;
 }
 
+}  // extern "C"
+
+namespace gsr {
+
+// Shared by the 3D and 2D entry points (2D: C = 1, index-order keys, final_T [H,W,2]).
+template <bool IS2D>
+static int raster_fwd(const char* who, const float* rec, const float* depth, const int32_t* sorted_ids,
+                      const int32_t* tile_offset, const int32_t* tile_order, const int32_t* chunk_base, int C,
+                      int width, int height, float cut2d, const float* bg, int32_t n_busy, gsr_bin_stats* stats,
+                      float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
+                      uint64_t* tile_cut, float* chunk_state, int32_t* chunk_tile, int32_t* chunk_list,
+                      void* stream) {
+  GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "%s: bad C=%d or image %dx%d", who, C, width, height);
+  const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
+  const int64_t CT = (int64_t)C * tw * th;
+  GSR_REQUIRE(CT < (1ll << 31), "%s: too many tiles", who);
+  GSR_REQUIRE(n_busy >= 0 && n_busy <= CT, "%s: n_busy=%d out of [0, %lld]", who, n_busy, (long long)CT);
+  const int64_t n_fill = std::min<int64_t>(CT - n_busy, kFillBlocks);
+  hipStream_t s = (hipStream_t)stream;
+  // tile_end collects max(last) of the quadrant workgroups (atomicMax from -1)
+  if (hipMemsetAsync(tile_end, 0xFF, CT * sizeof(int32_t), s) != hipSuccess) {
+    set_error("%s: tile_end memset failed", who);
+    return GSR_ELAUNCH;
+  }
+  // Dynamic-LDS padding caps the forward at 4 workgroups per CU (measured: 4 and 5 per CU
+  // beat 6, whose extra tiles in flight spill each XCD's L2; 3 starves the CU).
+  hipLaunchKernelGGL(k_raster_fwd<IS2D>, dim3((unsigned)(busy_grid(n_busy) + n_fill)), dim3(kRasterThreads),
+                     kFwdLdsPad, s, (const Splat*)rec, sorted_ids, tile_offset, tile_order, width, height, tw, th,
+                     bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state, chunk_base, chunk_tile,
+                     (int)n_busy, CT, tile_cut, cut2d);
+  GSR_LAUNCH_CHECK(who);
+  if (n_busy > 0) {
+    hipLaunchKernelGGL(k_raster3d_finalize, dim3(ceil_div(n_busy, kRasterThreads)), dim3(kRasterThreads), 0, s,
+                       depth, sorted_ids, tile_offset, tile_order, (int)n_busy, chunk_base, tile_end,
+                       tile_cut, stats, chunk_list, IS2D ? GSR_ORDER_INDEX : GSR_ORDER_DEPTH);
+  }
+  GSR_LAUNCH_CHECK("k_raster3d_finalize");
+  return GSR_OK;
+}
+
+template <bool LOSS, bool IS2D>
+static int raster_bwd(const char* who, const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
+                      const int32_t* tile_end, const int32_t* chunk_base, const int32_t* chunk_tile,
+                      const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
+                      int C, int width, int height, float cut2d, const float* bg, const float* final_T,
+                      const int32_t* last, const float* v_rgb, const float* v_alpha, const gsr_loss_terms& lt,
+                      const int32_t* k_of_s, float* partial, void* stream) {
+  GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "%s: bad C=%d or image %dx%d", who, C, width, height);
+  GSR_REQUIRE(n_chunks >= 0, "%s: bad n_chunks", who);
+  if (n_chunks == 0) return GSR_OK;
+  const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
+  // n_chunks bounds the forward's active-chunk count (stats->n_active, device-side)
+  hipLaunchKernelGGL((k_raster_bwd<LOSS, IS2D>), dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
+                     (const Splat*)rec, sorted_ids, tile_offset, tile_end, chunk_base, chunk_tile,
+                     (const float4*)chunk_state, width, height, tw, th, bg, final_T, last, v_rgb, v_alpha, partial,
+                     chunk_list, stats, k_of_s, lt, C, cut2d);
+  GSR_LAUNCH_CHECK(who);
+  return GSR_OK;
+}
+
+}  // namespace gsr
+
+extern "C" {
+
 int gsr3d_raster_fwd(const float* rec, const float* depth, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_order, const int32_t* chunk_base, int C, int width, int height,
                      const float* bg, int32_t n_busy, gsr_bin_stats* stats, float* rgb, float* alpha,
                      float* final_T, int32_t* last, int32_t* tile_end, uint64_t* tile_cut, float* chunk_state,
                      int32_t* chunk_tile, int32_t* chunk_list, void* stream) {
-  GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "gsr3d_raster_fwd: bad C=%d or image %dx%d", C, width, height);
-  const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
-  const int64_t CT = (int64_t)C * tw * th;
-  GSR_REQUIRE(CT < (1ll << 31), "gsr3d_raster_fwd: too many tiles");
-  GSR_REQUIRE(n_busy >= 0 && n_busy <= CT, "gsr3d_raster_fwd: n_busy=%d out of [0, %lld]", n_busy, (long long)CT);
-  const int64_t n_fill = std::min<int64_t>(CT - n_busy, kFillBlocks);
-  hipStream_t s = (hipStream_t)stream;
-  // tile_end collects max(last) of the quadrant workgroups (atomicMax from -1)
-  if (hipMemsetAsync(tile_end, 0xFF, CT * sizeof(int32_t), s) != hipSuccess) {
-    set_error("gsr3d_raster_fwd: tile_end memset failed");
-    return GSR_ELAUNCH;
-  }
-  // Dynamic-LDS padding caps the forward at 4 workgroups per CU (measured: 4 and 5 per CU
-  // beat 6, whose extra tiles in flight spill each XCD's L2; 3 starves the CU).
-  hipLaunchKernelGGL(k_raster3d_fwd, dim3((unsigned)(busy_grid(n_busy) + n_fill)), dim3(kRasterThreads), kFwdLdsPad, s,
-                     (const Splat*)rec, sorted_ids, tile_offset, tile_order, width, height, tw, th, bg, rgb, alpha,
-                     final_T, last, tile_end, (float4*)chunk_state, chunk_base, chunk_tile, (int)n_busy, CT,
-                     tile_cut);
-  GSR_LAUNCH_CHECK("k_raster3d_fwd");
-  if (n_busy > 0) {
-    hipLaunchKernelGGL(k_raster3d_finalize, dim3(ceil_div(n_busy, kRasterThreads)), dim3(kRasterThreads), 0, s,
-                       depth, sorted_ids, tile_offset, tile_order, (int)n_busy, chunk_base, tile_end,
-                       tile_cut, stats, chunk_list);
-  }
-  GSR_LAUNCH_CHECK("k_raster3d_finalize");
-  return GSR_OK;
+  return raster_fwd<false>("gsr3d_raster_fwd", rec, depth, sorted_ids, tile_offset, tile_order, chunk_base, C, width,
+                           height, 0.f, bg, n_busy, stats, rgb, alpha, final_T, last, tile_end, tile_cut,
+                           chunk_state, chunk_tile, chunk_list, stream);
 }
 
 int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
@@ -953,18 +809,10 @@ int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t*
                      int C, int width, int height, const float* bg, const float* final_T, const int32_t* last,
                      const float* v_rgb, const float* v_alpha, const int32_t* k_of_s, float* partial,
                      void* stream) {
-  GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "gsr3d_raster_bwd: bad C=%d or image %dx%d", C, width, height);
-  GSR_REQUIRE(n_chunks >= 0, "gsr3d_raster_bwd: bad n_chunks");
-  if (n_chunks == 0) return GSR_OK;
-  const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
-  // n_chunks bounds the forward's active-chunk count (stats->n_active, device-side)
   const gsr_loss_terms none{};
-  hipLaunchKernelGGL(k_raster3d_bwd<false>, dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
-                     (const Splat*)rec, sorted_ids, tile_offset, tile_end, chunk_base, chunk_tile,
-                     (const float4*)chunk_state, width, height, tw, th, bg, final_T, last, v_rgb, v_alpha, partial,
-                     chunk_list, stats, k_of_s, none, C);
-  GSR_LAUNCH_CHECK("k_raster3d_bwd");
-  return GSR_OK;
+  return raster_bwd<false, false>("gsr3d_raster_bwd", rec, sorted_ids, tile_offset, tile_end, chunk_base,
+                                  chunk_tile, chunk_state, chunk_list, stats, n_chunks, C, width, height, 0.f, bg,
+                                  final_T, last, v_rgb, v_alpha, none, k_of_s, partial, stream);
 }
 
 int gsr3d_raster_bwd_loss(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
@@ -973,51 +821,35 @@ int gsr3d_raster_bwd_loss(const float* rec, const int32_t* sorted_ids, const int
                           int32_t n_chunks, int C, int width, int height, const float* bg, const float* final_T,
                           const int32_t* last, const gsr_loss_terms* loss, const int32_t* k_of_s, float* partial,
                           void* stream) {
-  GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "gsr3d_raster_bwd_loss: bad C=%d or image %dx%d", C, width,
-              height);
-  GSR_REQUIRE(n_chunks >= 0, "gsr3d_raster_bwd_loss: bad n_chunks");
   GSR_REQUIRE(loss != nullptr && loss->rgb && loss->target_img && loss->target_mask && loss->sums && loss->grad_out,
               "gsr3d_raster_bwd_loss: incomplete loss terms");
-  if (n_chunks == 0) return GSR_OK;
-  const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
-  hipLaunchKernelGGL(k_raster3d_bwd<true>, dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
-                     (const Splat*)rec, sorted_ids, tile_offset, tile_end, chunk_base, chunk_tile,
-                     (const float4*)chunk_state, width, height, tw, th, bg, final_T, last, nullptr, nullptr,
-                     partial, chunk_list, stats, k_of_s, *loss, C);
-  GSR_LAUNCH_CHECK("k_raster3d_bwd_loss");
-  return GSR_OK;
+  return raster_bwd<true, false>("gsr3d_raster_bwd_loss", rec, sorted_ids, tile_offset, tile_end, chunk_base,
+                                 chunk_tile, chunk_state, chunk_list, stats, n_chunks, C, width, height, 0.f, bg,
+                                 final_T, last, nullptr, nullptr, *loss, k_of_s, partial, stream);
 }
 
-int gsr2d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset, int width,
-                     int height, const float* bg, float* rgb, float* alpha, int32_t* last, int32_t* tile_end,
-                     uint64_t* tile_cut, void* stream) {
-  GSR_REQUIRE(width > 0 && height > 0, "gsr2d_raster_fwd: bad image %dx%d", width, height);
-  const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
-  hipLaunchKernelGGL(k_raster2d_fwd, dim3(tw * th), dim3(kRasterThreads), 0, (hipStream_t)stream,
-                     (const Splat*)rec, sorted_ids, tile_offset, width, height, tw, th, bg, rgb, alpha, last,
-                     tile_end, tile_cut);
-  GSR_LAUNCH_CHECK("k_raster2d_fwd");
-  return GSR_OK;
-}
-
-size_t gsr2d_raster_bwd_workspace(int64_t n_isect, int64_t CT) {
-  return (size_t)((n_isect / kChunk + CT + 2) * kRasterThreads * sizeof(float));
+int gsr2d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
+                     const int32_t* tile_order, const int32_t* chunk_base, int width, int height, float eps_cut,
+                     const float* bg, int32_t n_busy, gsr_bin_stats* stats, float* rgb, float* alpha,
+                     float* final_T, int32_t* last, int32_t* tile_end, uint64_t* tile_cut, float* chunk_state,
+                     int32_t* chunk_tile, int32_t* chunk_list, void* stream) {
+  GSR_REQUIRE(eps_cut > 0.f && eps_cut < 1.f, "gsr2d_raster_fwd: eps_cut must be in (0,1)");
+  return raster_fwd<true>("gsr2d_raster_fwd", rec, nullptr, sorted_ids, tile_offset, tile_order, chunk_base, 1, width,
+                          height, eps_cut, bg, n_busy, stats, rgb, alpha, final_T, last, tile_end, tile_cut,
+                          chunk_state, chunk_tile, chunk_list, stream);
 }
 
 int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
-                     const int32_t* tile_end, const int32_t* busy_tiles, int32_t n_busy, int width, int height,
-                     const float* bg, const int32_t* last, const float* v_rgb, const float* v_alpha, void* workspace,
-                     size_t workspace_bytes, const int32_t* k_of_s, float* partial, void* stream) {
-  GSR_REQUIRE(width > 0 && height > 0, "gsr2d_raster_bwd: bad image %dx%d", width, height);
-  if (n_busy <= 0) return GSR_OK;
-  const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
-  GSR_REQUIRE(workspace != nullptr && workspace_bytes >= gsr2d_raster_bwd_workspace(0, (int64_t)tw * th),
-              "gsr2d_raster_bwd: workspace too small");
-  hipLaunchKernelGGL(k_raster2d_bwd, dim3(n_busy), dim3(kRasterThreads), 0, (hipStream_t)stream,
-                     (const Splat*)rec, sorted_ids, tile_offset, tile_end, busy_tiles, width, height, tw, th, bg,
-                     last, v_rgb, v_alpha, (float*)workspace, k_of_s, partial);
-  GSR_LAUNCH_CHECK("k_raster2d_bwd");
-  return GSR_OK;
+                     const int32_t* tile_end, const int32_t* chunk_base, const int32_t* chunk_tile,
+                     const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
+                     int width, int height, float eps_cut, const float* bg, const float* final_T,
+                     const int32_t* last, const float* v_rgb, const float* v_alpha, const int32_t* k_of_s,
+                     float* partial, void* stream) {
+  GSR_REQUIRE(eps_cut > 0.f && eps_cut < 1.f, "gsr2d_raster_bwd: eps_cut must be in (0,1)");
+  const gsr_loss_terms none{};
+  return raster_bwd<false, true>("gsr2d_raster_bwd", rec, sorted_ids, tile_offset, tile_end, chunk_base,
+                                 chunk_tile, chunk_state, chunk_list, stats, n_chunks, 1, width, height, eps_cut, bg,
+                                 final_T, last, v_rgb, v_alpha, none, k_of_s, partial, stream);
 }
 
 }  // extern "C"

@@ -73,10 +73,10 @@ EXPORTS = {
                                         _P, _P, _P, _P, _P, _P, _P, _P]),
     "gsr3d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P,
                                         _P, _P, _P, _P, _P, _P, _P]),
-    "gsr2d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
-    "gsr2d_raster_bwd_workspace": (_SZ, [_I64, _I64]),
-    "gsr2d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P,
-                                        _SZ, _P, _P, _P]),
+    "gsr2d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _F, _P, _I32, _P, _P, _P, _P, _P,
+                                        _P, _P, _P, _P, _P, _P]),
+    "gsr2d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _P,
+                                        _P, _P, _P, _P, _P, _P]),
     "gsr3d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _I32, _I32, _I32, _F, _I32, _P, _P,
                                          _P, _P, _P, _P, _P, _P]),
     "gsr2d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),

@@ -214,7 +214,7 @@ class _Bins:
         K = max(n_chunks, 1) if with_chunks else 1
         self.post = _Arena(self.device, {
             "sorted_ids": I * 4, "k_of_s": I * 4, "sort_ws": int(L.gsr_bin_sort_workspace(I, self.CT)),
-            "final_T": P * 4, "last": P * 4, "tile_end": self.CT * 4, "tile_cut": self.CT * 8,
+            "final_T": P * 8, "last": P * 4, "tile_end": self.CT * 4, "tile_cut": self.CT * 8,
             "chunk_state": K * 256 * 16, "chunk_tile": K * 4, "chunk_list": K * 4})
         self.post_cap = (I, K)
         self.p.update(self.post.ptr)
@@ -326,18 +326,19 @@ def _forward2d(params, bg, width, height, eps_cut):
     with _timed("project2d_fwd"):
       check(L.gsr2d_project_fwd(_ptr(p), N, stride, width, height, eps_cut, q["rec"], q["rect"],
                               q["cnt"], q["tile_cnt"], stream), "gsr2d_project_fwd")
-    b.guess_post(with_chunks=False)
+    b.guess_post(with_chunks=True)
     b.offsets(stream)
-    b.ensure_post(with_chunks=False)
+    b.ensure_post(with_chunks=True)
     b.sort(_lib.ORDER_INDEX, stream)
     rgb = torch.empty(height, width, 3, device=dev, dtype=torch.float32)
     alpha = torch.empty(height, width, device=dev, dtype=torch.float32)
     with _timed("raster2d_fwd"):
-      check(L.gsr2d_raster_fwd(q["rec"], q["sorted_ids"], q["tile_off"], width, height, _ptr(bgc),
-                             _ptr(rgb), _ptr(alpha), q["last"], q["tile_end"], q["tile_cut"], stream),
-          "gsr2d_raster_fwd")
+      check(L.gsr2d_raster_fwd(q["rec"], q["sorted_ids"], q["tile_off"], q["busy"], q["chunk_base"], width, height,
+                             eps_cut, _ptr(bgc), b.n_busy, q["stats_dev"], _ptr(rgb), _ptr(alpha), q["final_T"],
+                             q["last"], q["tile_end"], q["tile_cut"], q["chunk_state"], q["chunk_tile"],
+                             q["chunk_list"], stream), "gsr2d_raster_fwd")
     _record_stats(b)
-    return rgb, alpha, b, (p, stride, bgc, width, height)
+    return rgb, alpha, b, (p, stride, bgc, width, height, eps_cut)
 
 
 def debug_forward3d(params, viewmats, Ks, bg, width, height, opts=None):
@@ -415,7 +416,7 @@ class _Render2D(torch.autograd.Function):
     def backward(ctx, v_rgb, v_alpha):
         L = lib()
         b = ctx.b
-        p, stride, bgc, width, height = ctx.meta
+        p, stride, bgc, width, height, eps_cut = ctx.meta
         dev = p.device
         stream = _stream(dev)
         N = b.N
@@ -428,12 +429,12 @@ class _Render2D(torch.autograd.Function):
         v_params = torch.empty(N, 9, device=dev, dtype=torch.float32)
         if N > 0:
             partial = torch.empty(max(b.n_isect, 1) * _lib.PARTIAL_STRIDE, device=dev, dtype=torch.float32)
-            ws = torch.empty(int(L.gsr2d_raster_bwd_workspace(b.n_isect, b.CT)), device=dev, dtype=torch.uint8)
             q = b.p
             with _timed("raster2d_bwd"):
-              check(L.gsr2d_raster_bwd(q["rec"], q["sorted_ids"], q["tile_off"], q["tile_end"], q["busy"],
-                                     b.n_busy, width, height, _ptr(bgc), q["last"], _ptr(v_rgb), _ptr(v_alpha),
-                                     _ptr(ws), ws.numel(), q["k_of_s"], _ptr(partial), stream),
+              check(L.gsr2d_raster_bwd(q["rec"], q["sorted_ids"], q["tile_off"], q["tile_end"], q["chunk_base"],
+                                     q["chunk_tile"], q["chunk_state"], q["chunk_list"], q["stats_dev"],
+                                     b.n_chunks, width, height, eps_cut, _ptr(bgc), q["final_T"], q["last"],
+                                     _ptr(v_rgb), _ptr(v_alpha), q["k_of_s"], _ptr(partial), stream),
                   "gsr2d_raster_bwd")
             with _timed("project2d_bwd"):
               check(L.gsr2d_project_bwd(_ptr(p), N, stride, width, height, q["rect"], q["isect_off"],

@@ -65,7 +65,6 @@ def test_workspace_queries():
     lib = _lib.lib()
     assert lib.gsr_bin_offsets_workspace(10_000, 132) >= 4
     assert lib.gsr_bin_sort_workspace(1000, 132) >= 16 * 1000
-    assert lib.gsr2d_raster_bwd_workspace(1000, 132) > 0
 
 
 def test_missing_library_fails_loudly(tmp_path, monkeypatch):
