@@ -73,8 +73,11 @@ def algorithmic_bytes(kernel: str, C: int, N: int, P: int, I: int, I_eff: int, p
     return 0.0
 
 
-def step_bytes(C: int, N: int, P_view: int, I: int, I_eff: int, p: int) -> float:
-    """Whole fwd+bwd step, SURVEY.md §8(d): C·N·(12p+136) + 36·I + 80·I_eff + 44·C·P."""
+def step_bytes(C: int, N: int, P_view: int, I: int, I_eff: int, p: int, backward: bool = True) -> float:
+    """Whole step, SURVEY.md §8(d): fwd+bwd C·N·(12p+136) + 36·I + 80·I_eff + 44·C·P;
+    fwd-only C·N·(4p+32) + 36·I + 40·I_eff + 20·C·P."""
+    if not backward:
+        return C * N * (4.0 * p + 32.0) + 36.0 * I + 40.0 * I_eff + 20.0 * C * P_view
     return C * N * (12.0 * p + 136.0) + 36.0 * I + 80.0 * I_eff + 44.0 * C * P_view
 
 
@@ -108,12 +111,14 @@ def cpu_baseline(cfg, params, V, K, views: int):
     g = torch.Generator().manual_seed(cfg.seed + 1)
     t0 = time.perf_counter()
     if cfg.mode == "3d":
-        p = params.detach().cpu().clone().requires_grad_(True)
+        p = params.detach().cpu().clone().requires_grad_(cfg.backward)
         rgb, alpha = oracle_render3d(p, V[:views].cpu(), K[:views].cpu(), cfg.width, cfg.height, torch.ones(3))
-        vr = torch.randn(rgb.shape, generator=g)
-        va = torch.randn(alpha.shape, generator=g)
-        ((rgb * vr).sum() + (alpha * va).sum()).backward()
-        sample = f"{views} of {cfg.views} views of {cfg.name}, fwd+bwd, oracle/oracle3d.py"
+        if cfg.backward:
+            vr = torch.randn(rgb.shape, generator=g)
+            va = torch.randn(alpha.shape, generator=g)
+            ((rgb * vr).sum() + (alpha * va).sum()).backward()
+        sample = (f"{views} of {cfg.views} views of {cfg.name}, "
+                  f"{'fwd+bwd' if cfg.backward else 'fwd'}, oracle/oracle3d.py")
     else:
         n = 2000
         p = params[:n].detach().cpu().clone().requires_grad_(True)
@@ -224,6 +229,9 @@ def main():
             params.grad = sharded_backward_bands(render_band, params, Vd, Kd, v_rgb, v_alpha, th, weights)
         elif cfg.mode == "3d" and world > 1:
             params.grad = sharded_backward(render_views, params, V_all, K_all, vr_all, va_all)
+        elif cfg.mode == "3d" and not cfg.backward:
+            with torch.no_grad():   # config 2 is forward-only
+                R.render3d(params, Vd, Kd, cfg.width, cfg.height, bg)
         elif cfg.mode == "3d":
             rgb, alpha = R.render3d(params, Vd, Kd, cfg.width, cfg.height, bg)
             torch.autograd.backward([rgb, alpha], [v_rgb, v_alpha])
@@ -303,10 +311,10 @@ def main():
     traffic = None
     if args.traffic_csv and dom_name and os.path.exists(args.traffic_csv):
         traffic = traffic_from_csv(args.traffic_csv, "k_" + dom_name)
-    sb = step_bytes(Cd, cfg.N, cfg.width * cfg.height, I, I_eff, p_dim) * (1 if cfg.mode == "3d" else C)
+    sb = step_bytes(Cd, cfg.N, cfg.width * cfg.height, I, I_eff, p_dim, cfg.backward) * (1 if cfg.mode == "3d" else C)
 
     out = {
-        "metric": "rendered frames/sec (fwd+bwd) at N_gauss x H x W",
+        "metric": "rendered frames/sec (%s) at N_gauss x H x W" % ("fwd+bwd" if cfg.backward else "fwd"),
         "value": value,
         "unit": "frames/s",
         "n_gpus": world,
@@ -332,7 +340,8 @@ def main():
         "pair_evals_per_s": 2.0 * 256.0 * I_eff * (1 if cfg.mode == "3d" else C) * world / (ms_per_step * 1e-3),
         "step_roofline": {"algorithmic_bytes": sb, "achieved": sb / (ms_per_step * 1e-3) / 1e9,
                           "unit": "GB/s", "frac": sb / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                          "formula": "SURVEY.md 8(d): C*N*(12p+136) + 36*I + 80*I_eff + 44*C*P per rank"},
+                          "formula": ("SURVEY.md 8(d): C*N*(12p+136) + 36*I + 80*I_eff + 44*C*P per rank" if cfg.backward
+                                      else "SURVEY.md 8(d) fwd-only: C*N*(4p+32) + 36*I + 40*I_eff + 20*C*P per rank")},
         "binning": {"I": I, "I_eff": I_eff, "max_list": st.get("max_seg"), "busy_tiles": st.get("n_busy"),
                     "tiles": st.get("tiles")},
     }
