@@ -101,8 +101,12 @@ int gsr_selftest_lds_order(int32_t* violations, void* stream);
  * 6:10, colour 10:13, opacity 13).  input_mode GSR_INPUT_ADAPTER: raw values through the
  * adapter's activations; GSR_INPUT_GSPLAT: activated values as gsplat's rasterization()
  * takes them (no exp/sigmoid/clamp; the quaternion is only renormalised).  viewmats [C,4,4] world->cam
- * row-major; Ks [C,3,3].  Writes rec [C*N*12], depth [C*N], rect [C*N*2], isect_count [C*N] and
- * writes tile_count [C*tiles] (zeroed, then accumulated).  Culled Gaussians get count 0.
+ * row-major; Ks [C,3,3].  Writes rec [C*N*12], depth [C*N], rect [C*N*2], isect_count [C*N],
+ * isect_offset [C*N] (the first emission entry of each (c,n): every workgroup claims one
+ * contiguous range for its items with one atomic, so the (c,n) ranges tile [0, I) in
+ * workgroup arrival order -- consumers only address rows through isect_offset) and
+ * tile_count [C*tiles + 1] (zeroed, then accumulated; element C*tiles ends as I, the
+ * emission counter).  Culled Gaussians get count 0.
  * [band_y0, band_y1): the tile rows this call bins (band_y1 = -1: all rows).  Multi-GPU band
  * sharding gives each rank a band; tiles outside it stay empty (background)
  * and their entries contribute nothing, so the ranks' gradients sum to the full gradient. */
@@ -110,28 +114,26 @@ int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride,
                       const float* viewmats, const float* Ks, int C, int width, int height,
                       float near_plane, float far_plane, float radius_clip, float eps2d,
                       int radius_mode, int input_mode, int band_y0, int band_y1, float* rec, float* depth,
-                      uint32_t* rect, int32_t* isect_count, int32_t* tile_count, void* stream);
+                      uint32_t* rect, int32_t* isect_count, int32_t* isect_offset, int32_t* tile_count,
+                      void* stream);
 
 /* 2D projection: params [N, >=9] (layout src/gaussian_renderer.py:314-318).  The tile rect
  * covers every pixel where opacity*exp(-q) >= eps_cut (the reference is dense; eps_cut
  * bounds the dropped mass).  Same outputs as gsr3d_project_fwd with C = 1. */
 int gsr2d_project_fwd(const float* params, int64_t N, int64_t row_stride, int width,
                       int height, float eps_cut, float* rec, uint32_t* rect,
-                      int32_t* isect_count, int32_t* tile_count, void* stream);
+                      int32_t* isect_count, int32_t* isect_offset, int32_t* tile_count, void* stream);
 
 /* ---------------------------------------------------------------- (b) binning */
 
-/* Workspace for gsr_bin_offsets, bytes. */
-size_t gsr_bin_offsets_workspace(int64_t CN, int64_t CT);
-
-/* Exclusive scans: isect_offset [CN] (per-Gaussian emission offsets), tile_offset [CT+1],
- * chunk_base [CT+1] (first GSR_CHUNK-entry chunk of each tile's list), busy_tiles [CT]
- * (rasterizer visit order: the stats.n_busy non-empty tiles first, longest lists first,
- * then the empty tiles), stats (device). */
-int gsr_bin_offsets(const int32_t* isect_count, int64_t CN, const int32_t* tile_count,
-                    int64_t CT, void* workspace, size_t workspace_bytes,
-                    int32_t* isect_offset, int32_t* tile_offset, int32_t* chunk_base,
-                    int32_t* busy_tiles, gsr_bin_stats* stats, void* stream);
+/* One workgroup over the tile histogram: tile_offset [CT+1] (exclusive scan), chunk_base
+ * [CT+1] (first GSR_CHUNK-entry chunk of each tile's list), busy_tiles [CT] (rasterizer visit
+ * order: the stats.n_busy non-empty tiles first, longest lists first, then the empty tiles),
+ * tile_end [CT] (set to -1: the raster forward's atomicMax target), tile_cut [CT] (zeroed;
+ * the raster forward writes the cut keys) and stats (device). */
+int gsr_bin_offsets(const int32_t* tile_count, int64_t CT, int32_t* tile_offset,
+                    int32_t* chunk_base, int32_t* busy_tiles, int32_t* tile_end,
+                    uint64_t* tile_cut, gsr_bin_stats* stats, void* stream);
 
 /* Workspace for gsr_bin_sort, bytes (depends on the I read back from stats). */
 size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT);

@@ -22,9 +22,6 @@ __device__ unsigned long long g_cnt_bin[16];
 #define GSR_BCLOCK() 0ll
 #endif
 
-constexpr int kScanThreads = 256;
-constexpr int kScanItems = 16;
-constexpr int kScanTile = kScanThreads * kScanItems;   // 4096 per block
 constexpr int kTopThreads = 1024;
 constexpr int kChunkEntries = GSR_CHUNK;   // backward work unit (list entries)
 #ifndef GSR_EMIT_THREADS
@@ -41,68 +38,18 @@ constexpr int kSortWaves = kSortThreads / 64;
 constexpr int kSortLdsKeys = 16384;   // 128 KB of 64-bit keys
 constexpr int kSortRounds = kSortLdsKeys / kSortThreads;   // 64-element rounds per wave
 
-// ---------------------------------------------------------------- per-Gaussian scan
-__global__ __launch_bounds__(kScanThreads) void k_scan_partials(const int32_t* __restrict__ x, int64_t n,
-                                                               int32_t* __restrict__ bsum) {
-  __shared__ int s_tmp[kScanThreads / 64 + 1];
-  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
-  int acc = 0;
-#pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
-    const int64_t i = base + k;
-    if (i < n) acc += x[i];
-  }
-  int total;
-  block_exclusive_scan<kScanThreads>(acc, s_tmp, &total);
-  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
-}
-
-// single block: exclusive scan of bsum[0..nb) in place
-__global__ __launch_bounds__(kTopThreads) void k_scan_top(int32_t* __restrict__ bsum, int nb) {
-  __shared__ int s_tmp[kTopThreads / 64 + 1];
-  int carry = 0;
-  for (int b0 = 0; b0 < nb; b0 += kTopThreads) {
-    const int i = b0 + threadIdx.x;
-    const int v = i < nb ? bsum[i] : 0;
-    int total;
-    const int ex = block_exclusive_scan<kTopThreads>(v, s_tmp, &total);
-    if (i < nb) bsum[i] = carry + ex;
-    carry += total;
-  }
-}
-
-__global__ __launch_bounds__(kScanThreads) void k_scan_apply(const int32_t* __restrict__ x, int64_t n,
-                                                            const int32_t* __restrict__ bsum,
-                                                            int32_t* __restrict__ out) {
-  __shared__ int s_tmp[kScanThreads / 64 + 1];
-  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
-  int v[kScanItems];
-  int acc = 0;
-#pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
-    const int64_t i = base + k;
-    v[k] = i < n ? x[i] : 0;
-    acc += v[k];
-  }
-  int total;
-  int run = block_exclusive_scan<kScanThreads>(acc, s_tmp, &total) + bsum[blockIdx.x];
-#pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
-    const int64_t i = base + k;
-    if (i < n) out[i] = run;
-    run += v[k];
-  }
-}
-
 // ---------------------------------------------------------------- tile scan (single block)
 // One pass over contiguous per-thread ranges: tile_offset[0..CT] (list starts),
 // chunk_base[0..CT] (starts of each tile's 256-entry chunks, for the chunk-parallel backward),
 // the visit order (non-empty tiles longest-first in log2 buckets, then the empty tiles in
-// ascending order) and the stats.  Order inside a bucket only affects scheduling.
+// ascending order) and the stats.  Order inside a bucket only affects scheduling.  Also
+// initialises tile_end to -1 (the raster forward's atomicMax target) and zeroes tile_cut.
 __global__ __launch_bounds__(kTopThreads) void k_tile_scan(const int32_t* __restrict__ tile_count, int64_t CT,
                                                           int32_t* __restrict__ tile_offset,
                                                           int32_t* __restrict__ chunk_base,
                                                           int32_t* __restrict__ order,
+                                                          int32_t* __restrict__ tile_end,
+                                                          uint64_t* __restrict__ tile_cut,
                                                           gsr_bin_stats* __restrict__ stats) {
   __shared__ int s_tmp[kTopThreads / 64 + 1];
   __shared__ int s_max;
@@ -140,6 +87,8 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(const int32_t* __rest
     const int v = tile_count[i];
     tile_offset[i] = oc;
     chunk_base[i] = ok;
+    tile_end[i] = -1;
+    tile_cut[i] = 0ull;
     oc += v;
     ok += (v + kChunkEntries - 1) / kChunkEntries;
     if (v > 0) order[atomicAdd(&s_bucket[31 - __clz(v)], 1)] = (int32_t)i;
@@ -448,29 +397,12 @@ using namespace gsr;
 
 extern "C" {
 
-size_t gsr_bin_offsets_workspace(int64_t CN, int64_t CT) {
-  (void)CT;
-  const int64_t nb = (CN + kScanTile - 1) / kScanTile;
-  return (size_t)((nb + 64) * sizeof(int32_t));
-}
-
-int gsr_bin_offsets(const int32_t* isect_count, int64_t CN, const int32_t* tile_count, int64_t CT,
-                    void* workspace, size_t workspace_bytes, int32_t* isect_offset, int32_t* tile_offset,
-                    int32_t* chunk_base, int32_t* busy_tiles, gsr_bin_stats* stats, void* stream) {
-  GSR_REQUIRE(CN >= 0 && CN < (1ll << 31), "gsr_bin_offsets: bad CN=%lld", (long long)CN);
+int gsr_bin_offsets(const int32_t* tile_count, int64_t CT, int32_t* tile_offset, int32_t* chunk_base,
+                    int32_t* busy_tiles, int32_t* tile_end, uint64_t* tile_cut, gsr_bin_stats* stats,
+                    void* stream) {
   GSR_REQUIRE(CT >= 1 && CT < (1ll << 31), "gsr_bin_offsets: bad CT=%lld", (long long)CT);
-  GSR_REQUIRE(workspace_bytes >= gsr_bin_offsets_workspace(CN, CT), "gsr_bin_offsets: workspace too small");
-  hipStream_t s = (hipStream_t)stream;
-  int32_t* bsum = (int32_t*)workspace;
-  if (CN > 0) {
-    const int nb = ceil_div(CN, kScanTile);
-    hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(kScanThreads), 0, s, isect_count, CN, bsum);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kTopThreads), 0, s, bsum, nb);
-    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(kScanThreads), 0, s, isect_count, CN, bsum, isect_offset);
-    GSR_LAUNCH_CHECK("k_scan");
-  }
-  hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kTopThreads), 0, s, tile_count, CT, tile_offset, chunk_base, busy_tiles,
-                     stats);
+  hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kTopThreads), 0, (hipStream_t)stream, tile_count, CT, tile_offset,
+                     chunk_base, busy_tiles, tile_end, tile_cut, stats);
   GSR_LAUNCH_CHECK("k_tile_scan");
   return GSR_OK;
 }

@@ -43,14 +43,48 @@ __device__ __forceinline__ void hist_flush(int* hist, int32_t* gcount, int T) {
   }
 }
 
+// Emission offsets without a separate scan pass: the workgroup's (c,n) items [cn0, cn0+m)
+// claim ONE contiguous range of emission entries with a single atomic on a zeroed counter,
+// and are laid out in index order inside it.  Ranges of different workgroups land in
+// arrival order; that only moves where partial rows live -- every consumer addresses them
+// through isect_offset, the tile sort orders entries by key, and each Gaussian's rows are
+// summed in rect order -- so results stay bitwise deterministic.  s_cnt: the items' counts.
+constexpr int kProjItems = kProjPerBlock / kProjThreads;
+__device__ __forceinline__ void alloc_offsets(const int* s_cnt, int m, int64_t cn0, int32_t* __restrict__ counter,
+                                              int32_t* __restrict__ isect_offset) {
+  __shared__ int s_tmp[kProjThreads / 64 + 1];
+  __shared__ int s_base;
+  __syncthreads();
+  int v[kProjItems];
+  int acc = 0;
+#pragma unroll
+  for (int j = 0; j < kProjItems; ++j) {
+    const int i = threadIdx.x * kProjItems + j;
+    v[j] = i < m ? s_cnt[i] : 0;
+    acc += v[j];
+  }
+  int total;
+  int run = block_exclusive_scan<kProjThreads>(acc, s_tmp, &total);
+  if (threadIdx.x == 0) s_base = total > 0 ? atomicAdd(counter, total) : 0;
+  __syncthreads();
+  run += s_base;
+#pragma unroll
+  for (int j = 0; j < kProjItems; ++j) {
+    const int i = threadIdx.x * kProjItems + j;
+    if (i < m) isect_offset[cn0 + i] = run;
+    run += v[j];
+  }
+}
+
 template <int RMODE>
 __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
     const float* __restrict__ params, int64_t N, int64_t stride, const float* __restrict__ viewmats,
     const float* __restrict__ Ks, int W, int H, float near_plane, float far_plane,
     float radius_clip, float eps2d, int input_mode, int tw, int th, int band_y0, int band_y1, int use_lds,
     Splat* __restrict__ rec, float* __restrict__ depth, uint2* __restrict__ rect, int32_t* __restrict__ cnt,
-    int32_t* __restrict__ tile_count) {
+    int32_t* __restrict__ tile_count, int32_t* __restrict__ counter, int32_t* __restrict__ isect_offset) {
   extern __shared__ int hist[];
+  __shared__ int s_cnt[kProjPerBlock];
   const int c = blockIdx.y;
   const int T = tw * th;
   int32_t* gcount = tile_count + (int64_t)c * T;
@@ -115,16 +149,19 @@ __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
       hist_add(hist, gcount, use_lds, x0, x1, y0, y1, tw);
     }
     rect[cn] = make_uint2(pack_rect_lo(x0, x1), pack_rect_lo(y0, y1));
-    cnt[cn] = (x1 - x0) * (y1 - y0);
+    cnt[cn] = s_cnt[n - n0] = (x1 - x0) * (y1 - y0);
   }
   if (use_lds) hist_flush(hist, gcount, T);
+  alloc_offsets(s_cnt, (int)(n1 - n0), (int64_t)c * N + n0, counter, isect_offset);
 }
 
 __global__ __launch_bounds__(kProjThreads) void k_project2d_fwd(
     const float* __restrict__ params, int64_t N, int64_t stride, int W, int H, float eps_cut,
     int tw, int th, int use_lds, Splat* __restrict__ rec, uint2* __restrict__ rect,
-    int32_t* __restrict__ cnt, int32_t* __restrict__ tile_count) {
+    int32_t* __restrict__ cnt, int32_t* __restrict__ tile_count, int32_t* __restrict__ counter,
+    int32_t* __restrict__ isect_offset) {
   extern __shared__ int hist[];
+  __shared__ int s_cnt[kProjPerBlock];
   const int T = tw * th;
   if (use_lds) {
     for (int t = threadIdx.x; t < T; t += blockDim.x) hist[t] = 0;
@@ -173,9 +210,10 @@ __global__ __launch_bounds__(kProjThreads) void k_project2d_fwd(
       hist_add(hist, tile_count, use_lds, x0, x1, y0, y1, tw);
     }
     rect[n] = make_uint2(pack_rect_lo(x0, x1), pack_rect_lo(y0, y1));
-    cnt[n] = (x1 - x0) * (y1 - y0);
+    cnt[n] = s_cnt[n - n0] = (x1 - x0) * (y1 - y0);
   }
   if (use_lds) hist_flush(hist, tile_count, T);
+  alloc_offsets(s_cnt, (int)(n1 - n0), n0, counter, isect_offset);
 }
 
 }  // namespace gsr
@@ -192,7 +230,7 @@ int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride, const 
                       const float* Ks, int C, int width, int height, float near_plane,
                       float far_plane, float radius_clip, float eps2d, int radius_mode, int input_mode,
                       int band_y0, int band_y1, float* rec, float* depth, uint32_t* rect, int32_t* isect_count,
-                      int32_t* tile_count, void* stream) {
+                      int32_t* isect_offset, int32_t* tile_count, void* stream) {
   GSR_REQUIRE(N >= 0 && C >= 1 && C <= 65535, "gsr3d_project_fwd: bad N=%lld or C=%d", (long long)N, C);
   GSR_REQUIRE(width > 0 && height > 0, "gsr3d_project_fwd: bad image %dx%d", width, height);
   GSR_REQUIRE(row_stride >= 14, "gsr3d_project_fwd: row_stride %lld < 14", (long long)row_stride);
@@ -205,7 +243,8 @@ int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride, const 
   if (band_y1 < 0) band_y1 = th;
   GSR_REQUIRE(band_y0 >= 0 && band_y0 <= band_y1 && band_y1 <= th, "gsr3d_project_fwd: bad band [%d,%d) of %d tile rows",
               band_y0, band_y1, th);
-  if (hipMemsetAsync(tile_count, 0, (size_t)C * tw * th * sizeof(int32_t), (hipStream_t)stream) != hipSuccess) {
+  // tile histogram [C*T] and the emission counter (element C*T) in one memset
+  if (hipMemsetAsync(tile_count, 0, ((size_t)C * tw * th + 1) * sizeof(int32_t), (hipStream_t)stream) != hipSuccess) {
     set_error("gsr3d_project_fwd: tile_count memset failed");
     return GSR_ELAUNCH;
   }
@@ -219,26 +258,26 @@ int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride, const 
     hipLaunchKernelGGL(k_project3d_fwd<GSR_RADIUS_OPACITY_AABB>, grid, dim3(kProjThreads), lds, s,
                        params, N, row_stride, viewmats, Ks, width, height, near_plane, far_plane,
                        radius_clip, eps2d, input_mode, tw, th, band_y0, band_y1, use_lds, (Splat*)rec, depth,
-                       (uint2*)rect, isect_count, tile_count);
+                       (uint2*)rect, isect_count, tile_count, tile_count + (int64_t)C * T, isect_offset);
   else
     hipLaunchKernelGGL(k_project3d_fwd<GSR_RADIUS_ISOTROPIC_3SIGMA>, grid, dim3(kProjThreads), lds, s,
                        params, N, row_stride, viewmats, Ks, width, height, near_plane, far_plane,
                        radius_clip, eps2d, input_mode, tw, th, band_y0, band_y1, use_lds, (Splat*)rec, depth,
-                       (uint2*)rect, isect_count, tile_count);
+                       (uint2*)rect, isect_count, tile_count, tile_count + (int64_t)C * T, isect_offset);
   GSR_LAUNCH_CHECK("k_project3d_fwd");
   return GSR_OK;
 }
 
 int gsr2d_project_fwd(const float* params, int64_t N, int64_t row_stride, int width, int height,
                       float eps_cut, float* rec, uint32_t* rect, int32_t* isect_count,
-                      int32_t* tile_count, void* stream) {
+                      int32_t* isect_offset, int32_t* tile_count, void* stream) {
   GSR_REQUIRE(N >= 0, "gsr2d_project_fwd: bad N=%lld", (long long)N);
   GSR_REQUIRE(width > 0 && height > 0, "gsr2d_project_fwd: bad image %dx%d", width, height);
   GSR_REQUIRE(row_stride >= 9, "gsr2d_project_fwd: row_stride %lld < 9", (long long)row_stride);
   GSR_REQUIRE(eps_cut > 0.f && eps_cut < 1.f, "gsr2d_project_fwd: eps_cut must be in (0,1)");
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   GSR_REQUIRE(tw < 65536 && th < 65536, "gsr2d_project_fwd: image too large");
-  if (hipMemsetAsync(tile_count, 0, (size_t)tw * th * sizeof(int32_t), (hipStream_t)stream) != hipSuccess) {
+  if (hipMemsetAsync(tile_count, 0, ((size_t)tw * th + 1) * sizeof(int32_t), (hipStream_t)stream) != hipSuccess) {
     set_error("gsr2d_project_fwd: tile_count memset failed");
     return GSR_ELAUNCH;
   }
@@ -248,7 +287,7 @@ int gsr2d_project_fwd(const float* params, int64_t N, int64_t row_stride, int wi
   const size_t lds = use_lds ? (size_t)T * sizeof(int) : 0;
   hipLaunchKernelGGL(k_project2d_fwd, dim3(ceil_div(N, kProjPerBlock)), dim3(kProjThreads), lds,
                      (hipStream_t)stream, params, N, row_stride, width, height, eps_cut, tw, th,
-                     use_lds, (Splat*)rec, (uint2*)rect, isect_count, tile_count);
+                     use_lds, (Splat*)rec, (uint2*)rect, isect_count, tile_count, tile_count + T, isect_offset);
   GSR_LAUNCH_CHECK("k_project2d_fwd");
   return GSR_OK;
 }

@@ -20,11 +20,14 @@ __device__ unsigned long long g_cnt[16];
 #define GSR_CNT_ADD(i, v) atomicAdd(&g_cnt[i], (unsigned long long)(v))
 #define GSR_CNT_MAX(i, v) atomicMax(&g_cnt[i], (unsigned long long)(v))
 #define GSR_CLOCK() clock64()
-__device__ unsigned long long g_blk[32768][3];   // per forward workgroup: start, end (s_memrealtime), list length
 #else
 #define GSR_CNT_ADD(i, v)
 #define GSR_CNT_MAX(i, v)
 #define GSR_CLOCK() 0ll
+#endif
+#if defined(GSR_EXP_COUNT) || defined(GSR_EXP_TIMELINE)
+#define GSR_TIMELINE 1
+__device__ unsigned long long g_blk[32768][3];   // per forward workgroup: start, end (s_memrealtime), list length
 #endif
 
 constexpr int kRasterThreads = 256;
@@ -211,7 +214,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   // XCD-aware mapping: workgroups are dealt to the 8 XCDs round-robin by id, so the four
   // quadrant workgroups of a tile get ids 32k + 8*quad + x (same id mod 8): they share one
   // XCD's L2 for the tile's records.  Busy tile u = 8k + x, in longest-first order.
-#ifdef GSR_EXP_COUNT
+#ifdef GSR_TIMELINE
   const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
   const int u = ((int)blockIdx.x >> 5) * 8 + ((int)blockIdx.x & 7);
@@ -406,8 +409,8 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   }
   if (q == 0 && last >= 0) atomicMax(&s_max, last);
   __syncthreads();
-  if (threadIdx.x == 0 && s_max >= 0) atomicMax(&tile_end[ct], s_max);   // finalised below
-#ifdef GSR_EXP_COUNT
+  if (threadIdx.x == 0 && s_max >= 0) atomicMax(&tile_end[ct], s_max);   // finalised by k_raster_finalize
+#ifdef GSR_TIMELINE
   if (threadIdx.x == 0 && blockIdx.x < 32768) {
     g_blk[blockIdx.x][0] = rt0;
     g_blk[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
@@ -418,7 +421,10 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
 
 // Per busy tile: tile_end = 1 + max last over the tile's four quadrant workgroups (or the
 // tile's start), the cut key, and the tile's active chunks appended to the backward's list.
-__global__ __launch_bounds__(kRasterThreads) void k_raster3d_finalize(
+// (A separate launch: finishing it inside the forward by the last-arriving quadrant
+// workgroup needs device-scope release fences, which write back the XCD's L2 on gfx950 --
+// measured 2x slower forward.)
+__global__ __launch_bounds__(kRasterThreads) void k_raster_finalize(
     const float* __restrict__ depth, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ order, int n_busy, const int32_t* __restrict__ chunk_base,
     int32_t* __restrict__ tile_end, uint64_t* __restrict__ tile_cut, gsr_bin_stats* __restrict__ stats,
@@ -623,7 +629,11 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
     acc[63] = 0.f;
 #pragma unroll
     for (int g = 0; g < kGroup; ++g) {
+#ifdef GSR_EXP_NOLIST
+      const int k = (g0 + g) & 255;   // timing experiment: no list indirection
+#else
       const int k = s_list[wv][g0 + g];
+#endif
       const float4 p0 = s_p0[k];
       const float4 p1 = s_p1[k];
       const float4 p2 = s_p2[k];
@@ -665,7 +675,13 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
       acc[g * kPartial + 5] = v_sig;   // v_opacity = vis v_al = -v_sig / o (formed per entry below)
       if (!IS2D) Sv += fac * cv;
     }
+#ifdef GSR_EXP_NORED
+    float sum = 0.f;   // timing experiment: no cross-lane reduction
+#pragma unroll
+    for (int i = 0; i < 64; ++i) sum += (i & 1) ? acc[i] : -acc[i];
+#else
     const float sum = reduce64(acc);
+#endif
     const int g = st.lane / kPartial;
     if (g < kGroup && g0 + g < nsurv)
       __hip_atomic_fetch_add(&L[st.lane - g * kPartial][wv >> 1][s_list[wv][g0 + g]], sum, __ATOMIC_RELAXED,
@@ -705,11 +721,13 @@ using namespace gsr;
 
 extern "C" {
 
-#ifdef GSR_EXP_COUNT
+#ifdef GSR_TIMELINE
 int gsr_debug_blocks(unsigned long long* out) {
   (void)hipDeviceSynchronize();
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(gsr::g_blk), sizeof(gsr::g_blk)) == hipSuccess ? 0 : -2;
 }
+#endif
+#ifdef GSR_EXP_COUNT
 int gsr_debug_counters(unsigned long long* out, int reset) {
   (void)hipDeviceSynchronize();
   (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(gsr::g_cnt), sizeof(gsr::g_cnt));
@@ -748,11 +766,8 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
   GSR_REQUIRE(n_busy >= 0 && n_busy <= CT, "%s: n_busy=%d out of [0, %lld]", who, n_busy, (long long)CT);
   const int64_t n_fill = std::min<int64_t>(CT - n_busy, kFillBlocks);
   hipStream_t s = (hipStream_t)stream;
-  // tile_end collects max(last) of the quadrant workgroups (atomicMax from -1)
-  if (hipMemsetAsync(tile_end, 0xFF, CT * sizeof(int32_t), s) != hipSuccess) {
-    set_error("%s: tile_end memset failed", who);
-    return GSR_ELAUNCH;
-  }
+  // tile_end collects max(last) of the quadrant workgroups (atomicMax from the -1 that
+  // gsr_bin_offsets wrote)
   // Dynamic-LDS padding caps the forward at 4 workgroups per CU (measured: 4 and 5 per CU
   // beat 6, whose extra tiles in flight spill each XCD's L2; 3 starves the CU).
   hipLaunchKernelGGL(k_raster_fwd<IS2D>, dim3((unsigned)(busy_grid(n_busy) + n_fill)), dim3(kRasterThreads),
@@ -761,11 +776,11 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
                      (int)n_busy, CT, tile_cut, cut2d);
   GSR_LAUNCH_CHECK(who);
   if (n_busy > 0) {
-    hipLaunchKernelGGL(k_raster3d_finalize, dim3(ceil_div(n_busy, kRasterThreads)), dim3(kRasterThreads), 0, s,
+    hipLaunchKernelGGL(k_raster_finalize, dim3(ceil_div(n_busy, kRasterThreads)), dim3(kRasterThreads), 0, s,
                        depth, sorted_ids, tile_offset, tile_order, (int)n_busy, chunk_base, tile_end,
                        tile_cut, stats, chunk_list, IS2D ? GSR_ORDER_INDEX : GSR_ORDER_DEPTH);
   }
-  GSR_LAUNCH_CHECK("k_raster3d_finalize");
+  GSR_LAUNCH_CHECK("k_raster_finalize");
   return GSR_OK;
 }
 

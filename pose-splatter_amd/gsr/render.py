@@ -134,7 +134,7 @@ _VIEWS = {"rec": ("pre", _F32), "depth": ("pre", _F32), "rect": ("pre", _I32), "
           "isect_off": ("pre", _I32), "tile_off": ("pre", _I32), "busy": ("pre", _I32),
           "chunk_base": ("pre", _I32), "stats_dev": ("pre", _I32),
           "sorted_ids": ("post", _I32), "k_of_s": ("post", _I32), "final_T": ("post", _F32),
-          "last": ("post", _I32), "tile_end": ("post", _I32), "tile_cut": ("post", _I64),
+          "last": ("post", _I32), "tile_end": ("pre", _I32), "tile_cut": ("pre", _I64),
           "chunk_state": ("post", _F32), "chunk_tile": ("post", _I32), "chunk_list": ("post", _I32)}
 
 _pinned = {}
@@ -161,11 +161,11 @@ class _Bins:
         self.th = (height + _TILE - 1) // _TILE
         self.CT = C * self.tw * self.th
         CN = max(C * N, 1)
-        L = lib()
         self.pre = _Arena(device, {
-            "rec": CN * 48, "depth": CN * 4, "rect": CN * 8, "cnt": CN * 4, "tile_cnt": self.CT * 4, "isect_off": CN * 4,
-            "tile_off": (self.CT + 1) * 4, "busy": self.CT * 4, "chunk_base": (self.CT + 1) * 4,
-            "stats_dev": 32, "offsets_ws": int(L.gsr_bin_offsets_workspace(C * N, self.CT))})
+            "rec": CN * 48, "depth": CN * 4, "rect": CN * 8, "cnt": CN * 4, "tile_cnt": (self.CT + 1) * 4,
+            "isect_off": CN * 4, "tile_off": (self.CT + 1) * 4, "busy": self.CT * 4,
+            "chunk_base": (self.CT + 1) * 4, "tile_end": self.CT * 4, "tile_cut": self.CT * 8,
+            "stats_dev": 32})
         self.p = dict(self.pre.ptr)
         self.post = None
         self.n_chunks = self.n_isect = self.max_seg = self.n_busy = 0
@@ -190,11 +190,9 @@ class _Bins:
     def offsets(self, stream):
         L = lib()
         p = self.p
-        CN = self.C * self.N
         with _timed("bin_offsets"):
-          check(L.gsr_bin_offsets(p["cnt"], CN, p["tile_cnt"], self.CT, p["offsets_ws"],
-                                self.pre.off["offsets_ws"][1], p["isect_off"], p["tile_off"],
-                                p["chunk_base"], p["busy"], p["stats_dev"], stream), "gsr_bin_offsets")
+          check(L.gsr_bin_offsets(p["tile_cnt"], self.CT, p["tile_off"], p["chunk_base"], p["busy"], p["tile_end"],
+                                p["tile_cut"], p["stats_dev"], stream), "gsr_bin_offsets")
         host = _pinned_stats(self.device)
         host.copy_(self.pre.view("stats_dev", _I32), non_blocking=True)
         ev = torch.cuda.Event()
@@ -214,7 +212,7 @@ class _Bins:
         K = max(n_chunks, 1) if with_chunks else 1
         self.post = _Arena(self.device, {
             "sorted_ids": I * 4, "k_of_s": I * 4, "sort_ws": int(L.gsr_bin_sort_workspace(I, self.CT)),
-            "final_T": P * 8, "last": P * 4, "tile_end": self.CT * 4, "tile_cut": self.CT * 8,
+            "final_T": P * 8, "last": P * 4,
             "chunk_state": K * 256 * 16, "chunk_tile": K * 4, "chunk_list": K * 4})
         self.post_cap = (I, K)
         self.p.update(self.post.ptr)
@@ -297,7 +295,7 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
       check(L.gsr3d_project_fwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height,
                               opts.near_plane, opts.far_plane, opts.radius_clip, opts.eps2d,
                               opts.radius_mode, opts.input_mode, opts.band[0], opts.band[1], q["rec"], q["depth"],
-                              q["rect"], q["cnt"], q["tile_cnt"], stream),
+                              q["rect"], q["cnt"], q["isect_off"], q["tile_cnt"], stream),
           "gsr3d_project_fwd")
     b.guess_post(with_chunks=True)
     b.offsets(stream)
@@ -325,7 +323,7 @@ def _forward2d(params, bg, width, height, eps_cut):
     q = b.p
     with _timed("project2d_fwd"):
       check(L.gsr2d_project_fwd(_ptr(p), N, stride, width, height, eps_cut, q["rec"], q["rect"],
-                              q["cnt"], q["tile_cnt"], stream), "gsr2d_project_fwd")
+                              q["cnt"], q["isect_off"], q["tile_cnt"], stream), "gsr2d_project_fwd")
     b.guess_post(with_chunks=True)
     b.offsets(stream)
     b.ensure_post(with_chunks=True)

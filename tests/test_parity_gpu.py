@@ -154,22 +154,23 @@ def test_3d_binning_exact(cuda):
     exp_off = torch.zeros(C * T + 1, dtype=torch.int64)
     exp_off[1:] = torch.cumsum(torch.bincount(exp_tiles, minlength=C * T), 0)
     assert torch.equal(b.tile_off.cpu().to(torch.int64), exp_off)
-    # k_of_s: the emission entry of each sorted entry (a permutation); emission entry
+    # k_of_s: the emission entry of each sorted entry (a permutation).  The (c,n) ranges
+    # [isect_offset, +count) tile [0, I) (workgroup arrival order), and emission entry
     # k = isect_offset[cn] + j belongs to Gaussian cn and to tile j (row-major) of its rect
     ks = b.k_of_s.cpu()[:I].to(torch.int64)
     assert torch.equal(torch.sort(ks).values, torch.arange(I))
-    pos = torch.empty(I, dtype=torch.int64)
-    pos[ks] = torch.arange(I)
+    off = b.isect_off.cpu()[:C * N].to(torch.int64)
+    nz = cnt > 0
+    o_s, perm = torch.sort(off[nz])
+    c_s = cnt[nz][perm]
+    assert int(o_s[0]) == 0 and torch.equal(o_s[1:], torch.cumsum(c_s, 0)[:-1]) and int(c_s.sum()) == I
     ids = b.sorted_ids.cpu()[:I].to(torch.int64)
-    assert torch.equal(ids[pos], torch.repeat_interleave(torch.arange(C * N), cnt))
-    tiles_of_pos = torch.searchsorted(exp_off, pos, right=True) - 1
-    exp_k_tiles = []
-    for cn in torch.nonzero(cnt > 0).flatten().tolist():
-        c = cn // N
-        for ty in range(int(y0[cn]), int(y1[cn])):
-            for tx in range(int(x0[cn]), int(x1[cn])):
-                exp_k_tiles.append(c * T + ty * tw + tx)
-    assert torch.equal(tiles_of_pos, torch.tensor(exp_k_tiles, dtype=torch.int64))
+    j = ks - off[ids]
+    assert bool(((j >= 0) & (j < cnt[ids])).all())
+    w = (x1 - x0)[ids]
+    tile_of_j = (ids // N) * T + (y0[ids] + j // w) * tw + (x0[ids] + j % w)
+    tiles_of_s = torch.searchsorted(exp_off, torch.arange(I), right=True) - 1
+    assert torch.equal(tile_of_j, tiles_of_s)
     # projection rects vs the oracle's (float decisions: near-total agreement)
     o = _oracle3d()
     m, q, s, col, op = o.activations3d(p)
