@@ -80,7 +80,8 @@ typedef struct gsr_bin_stats {
   int32_t n_busy;      /* tiles with a non-empty list                                 */
   int32_t n_chunks;    /* sum over tiles of ceil(list length / GSR_CHUNK)              */
   int32_t n_active;    /* chunks the 3D backward visits (appended by gsr3d_raster_fwd)   */
-  int32_t reserved[2];
+  int32_t n_sort_big;  /* tiles with lists >= 8192 entries (the first of the busy order)   */
+  int32_t n_sort_mid;  /* tiles with 4096..8191 entries (the next ones)                    */
 } gsr_bin_stats;       /* 32 bytes; counters zeroed by gsr_bin_offsets                  */
 
 int gsr_version(void);
@@ -146,13 +147,14 @@ size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT);
  *                   row-major index of the tile in the Gaussian's rect): where the raster
  *                   backward stores that entry's partial row.
  * Sort key per entry: (sort word << 32) | c*N+n, sort word = depth float bits (3D, order
- * GSR_ORDER_DEPTH) or c*N+n (2D, GSR_ORDER_INDEX).  max_seg/n_busy from stats. */
+ * GSR_ORDER_DEPTH) or c*N+n (2D, GSR_ORDER_INDEX).  max_seg, n_busy and the sort classes
+ * n_sort_big / n_sort_mid (workgroup shapes by list length) come from stats. */
 int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_offset,
                  const int32_t* tile_offset, int32_t* tile_count,
                  const int32_t* busy_tiles, int C, int64_t N,
                  int width, int height, int order, int64_t n_isect, int32_t max_seg,
-                 int32_t n_busy, void* workspace, size_t workspace_bytes,
-                 int32_t* sorted_ids, int32_t* k_of_s, void* stream);
+                 int32_t n_busy, int32_t n_sort_big, int32_t n_sort_mid, void* workspace,
+                 size_t workspace_bytes, int32_t* sorted_ids, int32_t* k_of_s, void* stream);
 
 /* ---------------------------------------------------------------- (c) rasterisation */
 

@@ -23,6 +23,7 @@ __device__ unsigned long long g_cnt_bin[16];
 #endif
 
 constexpr int kTopThreads = 1024;
+constexpr int kScanLdsTiles = 32768;   // tile scan: counts staged in LDS up to 128 KB
 constexpr int kChunkEntries = GSR_CHUNK;   // backward work unit (list entries)
 #ifndef GSR_EMIT_THREADS
 #define GSR_EMIT_THREADS 512
@@ -33,17 +34,34 @@ constexpr int kChunkEntries = GSR_CHUNK;   // backward work unit (list entries)
 constexpr int kEmitThreads = GSR_EMIT_THREADS;
 constexpr int kEmitPerBlock = GSR_EMIT_PER_BLOCK;
 constexpr int kHistMaxTiles = 16384;
+// Tile sorts come in two workgroup shapes: 1024 threads with LDS keys up to 16384 (128 KB;
+// longer lists merge runs), or -- when every list is shorter than 4096 (the tile scan's class
+// counts) -- 256 threads with 4096 keys (32 KB: four workgroups per CU, a quarter of the
+// counters).
 constexpr int kSortThreads = 1024;    // 16 waves
-constexpr int kSortWaves = kSortThreads / 64;
+constexpr int kSortThreadsSmall = 256;
 constexpr int kSortLdsKeys = 16384;   // 128 KB of 64-bit keys
-constexpr int kSortRounds = kSortLdsKeys / kSortThreads;   // 64-element rounds per wave
+constexpr int kSortRounds = 16;       // 64-element rounds per wave (LDS keys = 16 x threads)
+constexpr int kSortSmallKeys = 4096;
 
 // ---------------------------------------------------------------- tile scan (single block)
-// One pass over contiguous per-thread ranges: tile_offset[0..CT] (list starts),
-// chunk_base[0..CT] (starts of each tile's 256-entry chunks, for the chunk-parallel backward),
-// the visit order (non-empty tiles longest-first in log2 buckets, then the empty tiles in
-// ascending order) and the stats.  Order inside a bucket only affects scheduling.  Also
-// initialises tile_end to -1 (the raster forward's atomicMax target) and zeroes tile_cut.
+// tile_offset[0..CT] (list starts), chunk_base[0..CT] (starts of each tile's 256-entry chunks,
+// for the chunk-parallel backward), the visit order (non-empty tiles longest-first in log2
+// buckets, then the empty tiles in ascending order) and the stats.  Order inside a bucket only
+// affects scheduling.  Also initialises tile_end to -1 (the raster forward's atomicMax
+// target) and zeroes tile_cut.  Each wave owns a contiguous range of tiles and walks it in
+// 64-tile rounds (coalesced loads and stores, in-wave scans); the counts are staged in LDS
+// when they fit.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(v, o, 64);
+    if (lane >= o) v += y;
+  }
+  return v;
+}
+
 __global__ __launch_bounds__(kTopThreads) void k_tile_scan(const int32_t* __restrict__ tile_count, int64_t CT,
                                                           int32_t* __restrict__ tile_offset,
                                                           int32_t* __restrict__ chunk_base,
@@ -51,50 +69,69 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(const int32_t* __rest
                                                           int32_t* __restrict__ tile_end,
                                                           uint64_t* __restrict__ tile_cut,
                                                           gsr_bin_stats* __restrict__ stats) {
-  __shared__ int s_tmp[kTopThreads / 64 + 1];
+  constexpr int NW = kTopThreads / 64;
+  __shared__ int s_w[3][NW];
   __shared__ int s_max;
   __shared__ int s_bucket[33];
+  __shared__ int s_n_busy;
+  extern __shared__ int s_cnt[];   // the counts, staged with coalesced loads (CT <= kScanLdsTiles)
+  const bool staged = CT <= kScanLdsTiles;
+  if (staged)
+    for (int64_t i = threadIdx.x; i < CT; i += kTopThreads) s_cnt[i] = tile_count[i];
+  const int32_t* cnt = staged ? s_cnt : tile_count;
   if (threadIdx.x == 0) s_max = 0;
   if (threadIdx.x < 33) s_bucket[threadIdx.x] = 0;
   __syncthreads();
-  const int64_t ipt = (CT + kTopThreads - 1) / kTopThreads;
-  const int64_t i0 = min<int64_t>(CT, ipt * threadIdx.x), i1 = min<int64_t>(CT, i0 + ipt);
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t R = ((CT + NW - 1) / NW + 63) & ~int64_t(63);
+  const int64_t i0 = min<int64_t>(CT, R * wv), i1 = min<int64_t>(CT, i0 + R);
+  // pass 1: per-wave totals, log2-length buckets, longest list
   int sc = 0, sk = 0, se = 0, mx = 0;
-  for (int64_t i = i0; i < i1; ++i) {
-    const int v = tile_count[i];
+  for (int64_t i = i0 + lane; i < i1; i += 64) {
+    const int v = cnt[i];
     sc += v;
     sk += (v + kChunkEntries - 1) / kChunkEntries;
     se += v == 0;
     mx = max(mx, v);
     if (v > 0) atomicAdd(&s_bucket[31 - __clz(v)], 1);
   }
-  if (mx) atomicMax(&s_max, mx);
-  int tc, tk, te;
-  int oc = block_exclusive_scan<kTopThreads>(sc, s_tmp, &tc);
-  int ok = block_exclusive_scan<kTopThreads>(sk, s_tmp, &tk);
-  int oe = block_exclusive_scan<kTopThreads>(se, s_tmp, &te);
-  const int n_busy = (int)CT - te;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    sc += __shfl_xor(sc, o, 64);
+    sk += __shfl_xor(sk, o, 64);
+    se += __shfl_xor(se, o, 64);
+    mx = max(mx, __shfl_xor(mx, o, 64));
+  }
+  if (lane == 0) {
+    s_w[0][wv] = sc;
+    s_w[1][wv] = sk;
+    s_w[2][wv] = se;
+    atomicMax(&s_max, mx);
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
+    int tc = 0, tk = 0, te = 0;
+    for (int w = 0; w < NW; ++w) {
+      const int a = s_w[0][w], b = s_w[1][w], c = s_w[2][w];
+      s_w[0][w] = tc;
+      s_w[1][w] = tk;
+      s_w[2][w] = te;
+      tc += a;
+      tk += b;
+      te += c;
+    }
+    const int n_busy = (int)CT - te;
+    s_n_busy = n_busy;
     int acc = 0;
     for (int b = 31; b >= 0; --b) {
       const int c = s_bucket[b];
+      if (b == 12) {   // sort classes: lists >= 8192 (buckets >= 13) and 4096..8191 (bucket 12)
+        stats->n_sort_big = acc;
+        stats->n_sort_mid = c;
+      }
       s_bucket[b] = acc;
       acc += c;
     }
-  }
-  __syncthreads();
-  for (int64_t i = i0; i < i1; ++i) {
-    const int v = tile_count[i];
-    tile_offset[i] = oc;
-    chunk_base[i] = ok;
-    tile_end[i] = -1;
-    tile_cut[i] = 0ull;
-    oc += v;
-    ok += (v + kChunkEntries - 1) / kChunkEntries;
-    if (v > 0) order[atomicAdd(&s_bucket[31 - __clz(v)], 1)] = (int32_t)i;
-    else order[n_busy + oe++] = (int32_t)i;
-  }
-  if (threadIdx.x == 0) {
     tile_offset[CT] = tc;
     chunk_base[CT] = tk;
     stats->n_isect = tc;
@@ -102,8 +139,33 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(const int32_t* __rest
     stats->n_busy = n_busy;
     stats->n_chunks = tk;
     stats->n_active = 0;
-    stats->reserved[0] = 0;
-    stats->reserved[1] = 0;
+  }
+  __syncthreads();
+  // pass 2: 64-tile rounds per wave
+  int cc = s_w[0][wv], ck = s_w[1][wv], ce = s_w[2][wv];
+  const int n_busy = s_n_busy;
+  for (int64_t base = i0; base < i1; base += 64) {
+    const int64_t i = base + lane;
+    const bool in = i < i1;
+    const int v = in ? cnt[i] : 0;
+    const int kc = (v + kChunkEntries - 1) / kChunkEntries;
+    const int iv = wave_incl_scan(v), ik = wave_incl_scan(kc);
+    const unsigned long long empty = __ballot(in && v == 0);
+    if (in) {
+      tile_offset[i] = cc + iv - v;
+      chunk_base[i] = ck + ik - kc;
+      tile_end[i] = -1;
+      tile_cut[i] = 0ull;
+      if (v > 0) {
+        order[atomicAdd(&s_bucket[31 - __clz(v)], 1)] = (int32_t)i;
+      } else {
+        const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(empty >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)empty, 0));
+        order[n_busy + ce + r] = (int32_t)i;
+      }
+    }
+    cc += __shfl(iv, 63, 64);
+    ck += __shfl(ik, 63, 64);
+    ce += __popcll(empty);
   }
 }
 
@@ -172,9 +234,13 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__
 __device__ __forceinline__ uint32_t sort_word(uint64_t k) { return (uint32_t)(k >> 32); }
 __device__ __forceinline__ uint32_t low_word(uint64_t k) { return (uint32_t)(k & 0xffffffffull); }
 
-// a: n <= kSortLdsKeys elements (word << 32 | p) in LDS; seg: the bucket's original keys
-// (tie-break by their low word); s_hist: kSortWaves*256 + 64 ints.
+// a: n <= 16*NT elements (word << 32 | p) in LDS; seg: the bucket's original keys
+// (tie-break by their low word); s_hist: (NT/64)*256 + 64 ints.
+template <int NT>
 __device__ __forceinline__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, const uint64_t* __restrict__ seg) {
+  constexpr int kSortWaves = NT / 64;
+  constexpr int kWaveBits = kSortWaves == 16 ? 4 : 2;
+  static_assert(kSortWaves == 16 || kSortWaves == 4, "16 or 4 waves");
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int* s_misc = s_hist + kSortWaves * 256;
   if (threadIdx.x == 0) s_misc[0] = 0;
@@ -215,15 +281,15 @@ __device__ __forceinline__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, 
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int c = threadIdx.x * 4 + j;
-        v[j] = s_hist[(c & (kSortWaves - 1)) * 256 + (c >> 4)];
+        v[j] = s_hist[(c & (kSortWaves - 1)) * 256 + (c >> kWaveBits)];
         sum += v[j];
       }
       int total;
-      int run = block_exclusive_scan<kSortThreads>(sum, s_misc + 8, &total);
+      int run = block_exclusive_scan<NT>(sum, s_misc + 8, &total);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int c = threadIdx.x * 4 + j;
-        s_hist[(c & (kSortWaves - 1)) * 256 + (c >> 4)] = run;
+        s_hist[(c & (kSortWaves - 1)) * 256 + (c >> kWaveBits)] = run;
         run += v[j];
       }
     }
@@ -298,7 +364,8 @@ __device__ __forceinline__ void merge_runs(const uint64_t* __restrict__ a, const
 }
 
 // Outputs: sorted_ids[s] = c*N+n of sorted entry s; k_of_s[s] = its emission entry index.
-__global__ __launch_bounds__(kSortThreads) void k_segsort(
+template <int NT>
+__global__ __launch_bounds__(NT) void k_segsort(
     uint64_t* __restrict__ keys, uint64_t* __restrict__ tmpk, int32_t* __restrict__ tmpp0,
     int32_t* __restrict__ tmpp1, const int32_t* __restrict__ tile_offset, const int32_t* __restrict__ busy,
     const int32_t* __restrict__ k_of_slot, int lds_keys, int32_t* __restrict__ sorted_ids,
@@ -315,7 +382,7 @@ __global__ __launch_bounds__(kSortThreads) void k_segsort(
       s_keys[i] = (seg[i] & 0xffffffff00000000ull) | (uint64_t)(uint32_t)i;
     __syncthreads();
     [[maybe_unused]] const long long t1 = GSR_BCLOCK();
-    lds_radix_sort(s_keys, len, s_hist, seg);
+    lds_radix_sort<NT>(s_keys, len, s_hist, seg);
     [[maybe_unused]] const long long t2 = GSR_BCLOCK();
     for (int s = threadIdx.x; s < len; s += blockDim.x) {
       const uint32_t p = low_word(s_keys[s]);
@@ -342,7 +409,7 @@ __global__ __launch_bounds__(kSortThreads) void k_segsort(
     for (int i = threadIdx.x; i < rl; i += blockDim.x)
       s_keys[i] = (seg[r0 + i] & 0xffffffff00000000ull) | (uint64_t)(uint32_t)(r0 + i);
     __syncthreads();
-    lds_radix_sort(s_keys, rl, s_hist, seg);
+    lds_radix_sort<NT>(s_keys, rl, s_hist, seg);
     for (int i = threadIdx.x; i < rl; i += blockDim.x) {
       const uint32_t p = low_word(s_keys[i]);
       kA[r0 + i] = (s_keys[i] & 0xffffffff00000000ull) | (uint64_t)low_word(seg[p]);
@@ -401,7 +468,8 @@ int gsr_bin_offsets(const int32_t* tile_count, int64_t CT, int32_t* tile_offset,
                     int32_t* busy_tiles, int32_t* tile_end, uint64_t* tile_cut, gsr_bin_stats* stats,
                     void* stream) {
   GSR_REQUIRE(CT >= 1 && CT < (1ll << 31), "gsr_bin_offsets: bad CT=%lld", (long long)CT);
-  hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kTopThreads), 0, (hipStream_t)stream, tile_count, CT, tile_offset,
+  const size_t lds = CT <= kScanLdsTiles ? (size_t)CT * sizeof(int) : 0;
+  hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kTopThreads), lds, (hipStream_t)stream, tile_count, CT, tile_offset,
                      chunk_base, busy_tiles, tile_end, tile_cut, stats);
   GSR_LAUNCH_CHECK("k_tile_scan");
   return GSR_OK;
@@ -415,8 +483,8 @@ size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT) {
 
 int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_offset, const int32_t* tile_offset,
                  int32_t* tile_count, const int32_t* busy_tiles, int C, int64_t N, int width, int height, int order, int64_t n_isect,
-                 int32_t max_seg, int32_t n_busy, void* workspace, size_t workspace_bytes, int32_t* sorted_ids,
-                 int32_t* k_of_s, void* stream) {
+                 int32_t max_seg, int32_t n_busy, int32_t n_big, int32_t n_mid, void* workspace,
+                 size_t workspace_bytes, int32_t* sorted_ids, int32_t* k_of_s, void* stream) {
   GSR_REQUIRE(order == GSR_ORDER_DEPTH || order == GSR_ORDER_INDEX, "gsr_bin_sort: bad order %d", order);
   GSR_REQUIRE(n_isect >= 0 && n_isect < (1ll << 31), "gsr_bin_sort: I=%lld out of range", (long long)n_isect);
   GSR_REQUIRE((int64_t)C * N < (1ll << 31), "gsr_bin_sort: C*N too large for 32-bit ids");
@@ -438,14 +506,23 @@ int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_
                      (const uint2*)rect, isect_offset, N, tw, th, order, use_lds, tile_offset, tile_count, keys,
                      k_of_slot);
   GSR_LAUNCH_CHECK("k_emit");
-  if (n_busy > 0) {
+  GSR_REQUIRE(n_big >= 0 && n_mid >= 0 && n_big + n_mid <= n_busy, "gsr_bin_sort: bad sort classes %d/%d of %d",
+              n_big, n_mid, n_busy);
+  auto hist_bytes = [](int nt) { return (size_t)((nt / 64) * 256 + 64) * sizeof(int); };
+  // ONE launch: separate launches per class serialise (measured slower whenever long lists
+  // exist); the small shape only when every list is short (e.g. the 2D configs)
+  if (n_big + n_mid > 0) {
     int lds_keys = 1024;
     while (lds_keys < max_seg && lds_keys < kSortLdsKeys) lds_keys <<= 1;
-    const size_t lds = lds_keys * sizeof(uint64_t) + (kSortWaves * 256 + 64) * sizeof(int);
-    hipLaunchKernelGGL(k_segsort, dim3(n_busy), dim3(kSortThreads), lds, s, keys, tmpk, tmpp0, tmpp1, tile_offset,
-                       busy_tiles, k_of_slot, lds_keys, sorted_ids, k_of_s);
-    GSR_LAUNCH_CHECK("k_segsort");
+    hipLaunchKernelGGL(k_segsort<kSortThreads>, dim3(n_busy), dim3(kSortThreads),
+                       lds_keys * sizeof(uint64_t) + hist_bytes(kSortThreads), s, keys, tmpk, tmpp0, tmpp1,
+                       tile_offset, busy_tiles, k_of_slot, lds_keys, sorted_ids, k_of_s);
+  } else if (n_busy > 0) {
+    hipLaunchKernelGGL(k_segsort<kSortThreadsSmall>, dim3(n_busy), dim3(kSortThreadsSmall),
+                       kSortSmallKeys * sizeof(uint64_t) + hist_bytes(kSortThreadsSmall), s, keys, tmpk, tmpp0,
+                       tmpp1, tile_offset, busy_tiles, k_of_slot, kSortSmallKeys, sorted_ids, k_of_s);
   }
+  GSR_LAUNCH_CHECK("k_segsort");
   return GSR_OK;
 }
 

@@ -38,7 +38,7 @@ class GsrLibraryError(RuntimeError):
 class BinStats(ctypes.Structure):
     _fields_ = [("n_isect", ctypes.c_int64), ("max_seg", ctypes.c_int32), ("n_busy", ctypes.c_int32),
                 ("n_chunks", ctypes.c_int32), ("n_active", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 2)]
+                ("n_sort_big", ctypes.c_int32), ("n_sort_mid", ctypes.c_int32)]
 
 
 class LossTerms(ctypes.Structure):
@@ -67,7 +67,7 @@ EXPORTS = {
     "gsr_bin_offsets": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P, _P, _P]),
     "gsr_bin_sort_workspace": (_SZ, [_I64, _I64]),
     "gsr_bin_sort": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I32, _I64, _I32,
-                                    _I32, _P, _SZ, _P, _P, _P]),
+                                    _I32, _I32, _I32, _P, _SZ, _P, _P, _P]),
     "gsr3d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _I32, _P, _P, _P,
                                         _P, _P, _P, _P, _P, _P, _P, _P]),
     "gsr3d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P,

@@ -202,6 +202,7 @@ class _Bins:
         st = host.tolist()
         self.n_isect = (st[0] & 0xFFFFFFFF) | (st[1] << 32)
         self.max_seg, self.n_busy, self.n_chunks = st[2], st[3], st[4]
+        self.n_sort_big, self.n_sort_mid = st[6], st[7]
         if self.n_isect >= 2 ** 31:
             raise RuntimeError(f"gsr: {self.n_isect} intersections exceed the 32-bit index range")
 
@@ -230,7 +231,8 @@ class _Bins:
         with _timed("bin_sort"):
           check(L.gsr_bin_sort(p["depth"] if order == _lib.ORDER_DEPTH else None, p["rect"], p["isect_off"], p["tile_off"], p["tile_cnt"], p["busy"],
                              self.C, self.N,
-                             self.W, self.H, order, self.n_isect, self.max_seg, self.n_busy, p["sort_ws"],
+                             self.W, self.H, order, self.n_isect, self.max_seg, self.n_busy, self.n_sort_big,
+                             self.n_sort_mid, p["sort_ws"],
                              self.post.off["sort_ws"][1], p["sorted_ids"], p["k_of_s"], stream), "gsr_bin_sort")
 
 
