@@ -28,11 +28,10 @@ constexpr int kChunkEntries = GSR_CHUNK;   // backward work unit (list entries)
 #ifndef GSR_EMIT_THREADS
 #define GSR_EMIT_THREADS 512
 #endif
-#ifndef GSR_EMIT_PER_BLOCK
-#define GSR_EMIT_PER_BLOCK 1024
-#endif
 constexpr int kEmitThreads = GSR_EMIT_THREADS;
-constexpr int kEmitPerBlock = GSR_EMIT_PER_BLOCK;
+// Gaussians per emit workgroup.  (Larger workgroups claim fewer per-(workgroup, tile) slot
+// ranges with global atomics, but measured slower at config 5: 438 -> 545 us.)
+constexpr int kEmitPerBlock = 1024;
 constexpr int kHistMaxTiles = 16384;
 // Tile sorts come in two workgroup shapes: 1024 threads with LDS keys up to 16384 (128 KB;
 // longer lists merge runs), or -- when every list is shorter than 4096 (the tile scan's class
@@ -175,7 +174,7 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__
                                                       int th, int order, int use_lds,
                                                       const int32_t* __restrict__ tile_offset,
                                                       int32_t* __restrict__ tile_count, uint64_t* __restrict__ keys,
-                                                      int32_t* __restrict__ k_of_slot) {
+                                                      int32_t* __restrict__ k_of_slot, int per_block) {
   // Slots are claimed by counting each tile's count down to zero (slot = tile start +
   // remaining count - 1): no separate cursor array, and tile_count is left zeroed.
   extern __shared__ int hist[];
@@ -183,8 +182,8 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__
   const int T = tw * th;
   int32_t* gcnt = tile_count + (int64_t)c * T;
   const int32_t* toff = tile_offset + (int64_t)c * T;
-  const int64_t n0 = (int64_t)blockIdx.x * kEmitPerBlock;
-  const int64_t n1 = min(N, n0 + kEmitPerBlock);
+  const int64_t n0 = (int64_t)blockIdx.x * per_block;
+  const int64_t n1 = min(N, n0 + per_block);
   if (use_lds) {
     for (int t = threadIdx.x; t < T; t += blockDim.x) hist[t] = 0;
     __syncthreads();
@@ -398,8 +397,77 @@ __global__ __launch_bounds__(NT) void k_segsort(
     }
     return;
   }
-  // Large bucket: sort runs of lds_keys in LDS (elements keep their bucket-local index p), write
-  // them back as (word | c*N+n) keys with p as payload, then merge runs pairwise in global memory.
+  // Long list (> lds_keys): MSD partition by the top 8 varying bits of the sort word into
+  // 256 digit buckets (through tmpk, as (word << 32 | p)), then LDS-sort groups of consecutive
+  // buckets that fit -- each group holds a contiguous key range, so the sorted groups
+  // concatenate to the sorted list.  One more pass over the list instead of global merges.
+  {
+    __shared__ int s_dstart[257];
+    __shared__ int s_dcur[256];
+    __shared__ unsigned s_or;
+    __shared__ int s_maxb;
+    if (threadIdx.x == 0) {
+      s_or = 0u;
+      s_maxb = 0;
+    }
+    for (int d = threadIdx.x; d < 256; d += blockDim.x) s_dcur[d] = 0;
+    __syncthreads();
+    const uint32_t w0 = sort_word(seg[0]);
+    uint32_t orv = 0;
+    for (int i = threadIdx.x; i < len; i += blockDim.x) orv |= sort_word(seg[i]) ^ w0;
+    if (orv) atomicOr(&s_or, orv);
+    __syncthreads();
+    const uint32_t varying = s_or;
+    const int sh = varying ? max(31 - __clz(varying) - 7, 0) : 0;
+    for (int i = threadIdx.x; i < len; i += blockDim.x) atomicAdd(&s_dcur[(sort_word(seg[i]) >> sh) & 0xFFu], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int acc = 0, mb = 0;
+      for (int d = 0; d < 256; ++d) {
+        const int c = s_dcur[d];
+        s_dstart[d] = acc;
+        s_dcur[d] = acc;
+        acc += c;
+        mb = max(mb, c);
+      }
+      s_dstart[256] = acc;
+      s_maxb = mb;
+    }
+    __syncthreads();
+    if (s_maxb <= lds_keys) {
+      uint64_t* part = tmpk + start;
+      for (int i = threadIdx.x; i < len; i += blockDim.x) {
+        const uint64_t k = seg[i];
+        const int pos = atomicAdd(&s_dcur[(sort_word(k) >> sh) & 0xFFu], 1);
+        part[pos] = (k & 0xffffffff00000000ull) | (uint64_t)(uint32_t)i;
+      }
+      __threadfence_block();
+      __syncthreads();
+      int d0 = 0;
+      while (d0 < 256) {
+        const int g0 = s_dstart[d0];
+        int d1 = d0 + 1;
+        while (d1 < 256 && s_dstart[d1 + 1] - g0 <= lds_keys) ++d1;
+        const int n = s_dstart[d1] - g0;
+        if (n > 0) {
+          for (int i = threadIdx.x; i < n; i += blockDim.x) s_keys[i] = part[g0 + i];
+          __syncthreads();
+          lds_radix_sort<NT>(s_keys, n, s_hist, seg);
+          for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const uint32_t pp = low_word(s_keys[i]);
+            sorted_ids[start + g0 + i] = (int32_t)low_word(seg[pp]);
+            k_of_s[start + g0 + i] = k_of_slot[start + pp];
+          }
+          __syncthreads();
+        }
+        d0 = d1;
+      }
+      return;
+    }
+  }
+  // a digit bucket still exceeds LDS (depths packed into < 2^-8 of their range): sort runs of
+  // lds_keys in LDS (elements keep their bucket-local index p), write them back as
+  // (word | c*N+n) keys with p as payload, then merge runs pairwise in global memory.
   uint64_t* kA = tmpk + start;
   int32_t* pA = tmpp0 + start;
   uint64_t* kB = seg;   // the original keys are dead once every run is converted
@@ -500,11 +568,12 @@ int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_
   int32_t* tmpp1 = tmpp0 + n_isect;
   int32_t* k_of_slot = tmpp1 + n_isect;
   const int use_lds = T <= kHistMaxTiles;
-  dim3 grid(ceil_div(N, kEmitPerBlock), C);
+  const int per_block = kEmitPerBlock;
+  dim3 grid(ceil_div(N, per_block), C);
   GSR_REQUIRE(order == GSR_ORDER_INDEX || depth != nullptr, "gsr_bin_sort: depth order needs the depth array");
   hipLaunchKernelGGL(k_emit, grid, dim3(kEmitThreads), use_lds ? T * sizeof(int) : 0, s, depth,
                      (const uint2*)rect, isect_offset, N, tw, th, order, use_lds, tile_offset, tile_count, keys,
-                     k_of_slot);
+                     k_of_slot, per_block);
   GSR_LAUNCH_CHECK("k_emit");
   GSR_REQUIRE(n_big >= 0 && n_mid >= 0 && n_big + n_mid <= n_busy, "gsr_bin_sort: bad sort classes %d/%d of %d",
               n_big, n_mid, n_busy);
