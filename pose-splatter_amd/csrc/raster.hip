@@ -34,6 +34,10 @@ constexpr int kRasterThreads = 256;
 constexpr int kChunk3 = GSR_CHUNK;   // backward work unit: list entries per chunk
 constexpr int kFillBlocks = 1024;    // workgroups that fill the empty tiles
 constexpr int kFwdLdsPad = 28000;    // 12.3 KB static + pad: 4 forward workgroups per CU (160 KB)
+#ifndef GSR_FWD_PAD_2D
+#define GSR_FWD_PAD_2D 0   // 2D: every tile busy, no L2 locality to protect (6 per CU by VGPRs: measured 10% faster)
+#endif
+constexpr int kFwdLdsPad2D = GSR_FWD_PAD_2D;
 
 
 __device__ __forceinline__ void tile_coords(int ct, int tw, int th, int& c, int& ty, int& tx) {
@@ -673,6 +677,9 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
       acc[g * kPartial + 3] = tx * dy;
       acc[g * kPartial + 4] = ty * dy;
       acc[g * kPartial + 5] = v_sig;   // v_opacity = vis v_al = -v_sig / o (formed per entry below)
+#ifdef GSR_EXP_B128
+      acc[63] += (p0.w + p1.w) + p2.w;   // timing experiment: .w used -> ds_read_b128
+#endif
       if (!IS2D) Sv += fac * cv;
     }
 #ifdef GSR_EXP_NORED
@@ -771,7 +778,8 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
   // Dynamic-LDS padding caps the forward at 4 workgroups per CU (measured: 4 and 5 per CU
   // beat 6, whose extra tiles in flight spill each XCD's L2; 3 starves the CU).
   hipLaunchKernelGGL(k_raster_fwd<IS2D>, dim3((unsigned)(busy_grid(n_busy) + n_fill)), dim3(kRasterThreads),
-                     kFwdLdsPad, s, (const Splat*)rec, sorted_ids, tile_offset, tile_order, width, height, tw, th,
+                     IS2D ? kFwdLdsPad2D : kFwdLdsPad, s, (const Splat*)rec, sorted_ids, tile_offset, tile_order,
+                     width, height, tw, th,
                      bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state, chunk_base, chunk_tile,
                      (int)n_busy, CT, tile_cut, cut2d);
   GSR_LAUNCH_CHECK(who);
