@@ -33,7 +33,10 @@ __device__ unsigned long long g_blk[32768][3];   // per forward workgroup: start
 constexpr int kRasterThreads = 256;
 constexpr int kChunk3 = GSR_CHUNK;   // backward work unit: list entries per chunk
 constexpr int kFillBlocks = 1024;    // workgroups that fill the empty tiles
-constexpr int kFwdLdsPad = 28000;    // 12.3 KB static + pad: 4 forward workgroups per CU (160 KB)
+#ifndef GSR_FWD_PAD_3D
+#define GSR_FWD_PAD_3D 28000
+#endif
+constexpr int kFwdLdsPad = GSR_FWD_PAD_3D;   // 12.3 KB static + pad: 4 forward workgroups per CU (160 KB)
 #ifndef GSR_FWD_PAD_2D
 #define GSR_FWD_PAD_2D 0   // 2D: every tile busy, no L2 locality to protect (6 per CU by VGPRs: measured 10% faster)
 #endif
@@ -677,9 +680,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
       acc[g * kPartial + 3] = tx * dy;
       acc[g * kPartial + 4] = ty * dy;
       acc[g * kPartial + 5] = v_sig;   // v_opacity = vis v_al = -v_sig / o (formed per entry below)
-#ifdef GSR_EXP_B128
-      acc[63] += (p0.w + p1.w) + p2.w;   // timing experiment: .w used -> ds_read_b128
-#endif
       if (!IS2D) Sv += fac * cv;
     }
 #ifdef GSR_EXP_NORED
