@@ -81,6 +81,12 @@ def step_bytes(C: int, N: int, P_view: int, I: int, I_eff: int, p: int, backward
     return C * N * (12.0 * p + 136.0) + 36.0 * I + 80.0 * I_eff + 44.0 * C * P_view
 
 
+# libgsr call name (render.py timing brackets) -> substring of its dominant kernel's symbol
+KERNEL_SYMBOL = {"raster3d_bwd": "k_raster_bwd<false, false>", "raster3d_fwd": "k_raster_fwd<false>",
+                 "raster2d_bwd": "k_raster_bwd<false, true>", "raster2d_fwd": "k_raster_fwd<true>",
+                 "bin_sort": "k_segsort"}
+
+
 def traffic_from_csv(path: str, kernel_substr: str):
     """HBM bytes per launch from a rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE pass (KB units;
     FETCH_SIZE doubled per the gfx950 correction in MI355X_MICROARCH.md §HBM)."""
@@ -310,7 +316,7 @@ def main():
     achieved = alg / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     traffic = None
     if args.traffic_csv and dom_name and os.path.exists(args.traffic_csv):
-        traffic = traffic_from_csv(args.traffic_csv, "k_" + dom_name)
+        traffic = traffic_from_csv(args.traffic_csv, KERNEL_SYMBOL.get(dom_name, "k_" + dom_name))
     sb = step_bytes(Cd, cfg.N, cfg.width * cfg.height, I, I_eff, p_dim, cfg.backward) * (1 if cfg.mode == "3d" else C)
 
     out = {
