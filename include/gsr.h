@@ -33,11 +33,12 @@
  *
  * Splat record (written by *_project_fwd, read by binning and rasterisation):
  *   12 floats (48 B) per (camera c, Gaussian n), at rec[(c*N + n)*12]:
- *     [0]=x [1]=y  screen-space mean (pixels)      [2]=opacity   [3]=ln(255*opacity) (3D)
+ *     [0]=x [1]=y  screen-space mean (pixels)      [2]=opacity   [3]=L
  *     [4]=a [5]=b [6]=c  exponent  sigma = a*dx^2 + b*dx*dy + c*dy^2,  d = mean - pixel
- *     [7]=-b/(2c) (3D)
- *     [8..10]=rgb (activated colour)                [11]=-b/(2a) (3D)
- *   ([3], [7], [11] are the per-Gaussian constants of the rasterizer's sub-tile cull; 0 in 2D.)
+ *     [7]=-b/(2c)
+ *     [8..10]=rgb (activated colour)                [11]=-b/(2a)
+ *   ([3], [7], [11] are the per-Gaussian constants of the rasterizer's sub-tile cull:
+ *    L = ln(255*opacity) in 3D (gsplat's 1/255 skip), ln(opacity/eps_cut) in 2D.)
  *   depth: 1 float per (c,n) (3D camera-space z; the sort key's high word).
  *   rect: 2 uint32 per (c,n): {x0 | x1<<16, y0 | y1<<16}, tiles [x0,x1) x [y0,y1).
  *

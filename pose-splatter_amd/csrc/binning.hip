@@ -1,12 +1,13 @@
-// (b) Tile binning: per-Gaussian / per-tile exclusive scans, emission of (tile, key) pairs
-// into per-tile buckets, and a per-tile sort of the keys in LDS.
+// (b) Tile binning: the per-tile scan, emission of (tile, key) pairs into per-tile buckets,
+// and a per-tile sort of the keys in LDS.  (The per-Gaussian emission offsets are claimed by
+// the projection's workgroups, project.hip alloc_offsets.)
 //
 // gsplat (isect_tiles + cub DeviceRadixSort over 64-bit (camera|tile|depth) keys) is
 // restated as an MSD counting pass on the tile digit (the buckets come from the tile
-// histogram written by projection) followed by an LDS-resident bitonic sort of each
-// bucket's 64-bit (depth-bits << 32 | c*N+n) keys — the same total order a stable radix
-// sort of gsplat's keys over emission order produces (ties in depth → ascending c*N+n),
-// without a global multi-pass radix sort over HBM.  2D uses key = n (parameter order).
+// histogram written by projection) followed by an LDS-resident LSD radix sort of each
+// bucket's (depth-bits << 32 | c*N+n) keys — the same total order a stable radix sort of
+// gsplat's keys over emission order produces (ties in depth → ascending c*N+n), without a
+// global multi-pass radix sort over HBM.  2D uses key = n (parameter order).
 #include "gsr_common.h"
 
 namespace gsr {
