@@ -72,7 +72,9 @@ extern "C" {
 #define GSR_INPUT_ADAPTER 0            /* 3D rows: raw pose-splatter params (adapter)   */
 #define GSR_INPUT_GSPLAT 1             /* 3D rows: activated gsplat rasterization() inputs */
 
-#define GSR_CHUNK 256                  /* list entries per backward work unit (chunk)   */
+#ifndef GSR_CHUNK
+#define GSR_CHUNK 128                  /* list entries per backward work unit (chunk; 128: measured best of 64/128/192/256) */
+#endif
 #define GSR_PARTIAL_STRIDE 12          /* floats per partial row (9 used, 16 B aligned) */
 
 typedef struct gsr_bin_stats {

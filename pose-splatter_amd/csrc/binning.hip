@@ -45,7 +45,7 @@ constexpr int kSortRounds = 16;       // 64-element rounds per wave (LDS keys = 
 constexpr int kSortSmallKeys = 4096;
 
 // ---------------------------------------------------------------- tile scan (single block)
-// tile_offset[0..CT] (list starts), chunk_base[0..CT] (starts of each tile's 256-entry chunks,
+// tile_offset[0..CT] (list starts), chunk_base[0..CT] (starts of each tile's GSR_CHUNK-entry chunks,
 // for the chunk-parallel backward), the visit order (non-empty tiles longest-first in log2
 // buckets, then the empty tiles in ascending order) and the stats.  Order inside a bucket only
 // affects scheduling.  Also initialises tile_end to -1 (the raster forward's atomicMax

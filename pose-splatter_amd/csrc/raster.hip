@@ -378,21 +378,50 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   } else {
     last = quad_max_i(last);
   }
-  if (q == 0 && end > start) {
+  if (end > start) {
     // Turn this pixel's chunk records {T at chunk start, chunk colour sum} into what the
     // backward needs at each chunk's END: {T_end, suffix colour sum of the later chunks}
-    // (positive terms, summed back to front).  Records are re-read 8 at a time.
+    // (positive terms, summed back to front).  The pixel's four quad lanes split the chunks
+    // into four contiguous ranges: each sums its range's colour, a quad suffix of the range
+    // sums gives each range's starting suffix, then each rewrites its range back to front
+    // (records re-read 8 at a time).  A quarter of the serial chain of one lane.
     float4* ck = ckpt + (int64_t)cbase * kRasterThreads + bwd_pixel_slot(il, jl);
-    ck[(int64_t)kcur * kRasterThreads] = make_float4(T, 0.f, 0.f, 0.f);
-    float Tn = Ts, sr = Dr, sg = Dg, sb = Db;
-    for (int k0 = kcur - 1; k0 >= 0; k0 -= 8) {
+    if (q == 0) ck[(int64_t)kcur * kRasterThreads] = make_float4(T, 0.f, 0.f, 0.f);
+    const int per = (kcur + 3) >> 2;
+    const int r0 = min(kcur, q * per), r1 = min(kcur, r0 + per);
+    float Rr = 0.f, Rg = 0.f, Rb = 0.f, F = 0.f;
+    for (int k0 = r0; k0 < r1; k0 += 8) {
       float4 r[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u)
-        if (k0 - u >= 0) r[u] = ck[(int64_t)(k0 - u) * kRasterThreads];
+        if (k0 + u < r1) r[u] = ck[(int64_t)(k0 + u) * kRasterThreads];
 #pragma unroll
       for (int u = 0; u < 8; ++u)
-        if (k0 - u >= 0) {
+        if (k0 + u < r1) {
+          if (k0 + u == r0) F = r[u].x;
+          Rr += r[u].y;
+          Rg += r[u].z;
+          Rb += r[u].w;
+        }
+    }
+    // suffix of the later ranges (lanes q+1..3) plus the current chunk's own colour
+    const float R1r = dpp_mov<0x55>(Rr), R1g = dpp_mov<0x55>(Rg), R1b = dpp_mov<0x55>(Rb);
+    const float R2r = dpp_mov<0xAA>(Rr), R2g = dpp_mov<0xAA>(Rg), R2b = dpp_mov<0xAA>(Rb);
+    const float R3r = dpp_mov<0xFF>(Rr), R3g = dpp_mov<0xFF>(Rg), R3b = dpp_mov<0xFF>(Rb);
+    const float Fn = dpp_mov<0xF9>(F);   // quad_perm [1,2,3,3]: F of the next range
+    float sr = Dr, sg = Dg, sb = Db;
+    if (q < 3) { sr += R3r; sg += R3g; sb += R3b; }
+    if (q < 2) { sr += R2r; sg += R2g; sb += R2b; }
+    if (q < 1) { sr += R1r; sg += R1g; sb += R1b; }
+    float Tn = r1 < kcur ? Fn : Ts;
+    for (int k0 = r1 - 1; k0 >= r0; k0 -= 8) {
+      float4 r[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k0 - u >= r0) r[u] = ck[(int64_t)(k0 - u) * kRasterThreads];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k0 - u >= r0) {
           ck[(int64_t)(k0 - u) * kRasterThreads] = make_float4(Tn, sr, sg, sb);
           Tn = r[u].x;
           sr += r[u].y;

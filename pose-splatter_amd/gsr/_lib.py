@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get(
 
 TILE = 16
 PARTIAL_STRIDE = 12
-CHUNK = 256
+CHUNK = 128
 RADIUS_OPACITY_AABB = 0
 RADIUS_ISOTROPIC_3SIGMA = 1
 ORDER_DEPTH = 0
