@@ -38,9 +38,12 @@ constexpr int kHistMaxTiles = 16384;
 // longer lists merge runs), or -- when every list is shorter than 4096 (the tile scan's class
 // counts) -- 256 threads with 4096 keys (32 KB: four workgroups per CU, a quarter of the
 // counters).
-constexpr int kSortThreads = 1024;    // 16 waves
+#ifndef GSR_SORT_THREADS
+#define GSR_SORT_THREADS 1024
+#endif
+constexpr int kSortThreads = GSR_SORT_THREADS;    // 16 waves
 constexpr int kSortThreadsSmall = 256;
-constexpr int kSortLdsKeys = 16384;   // 128 KB of 64-bit keys
+constexpr int kSortLdsKeys = 16 * kSortThreads;   // 128 KB of 64-bit keys at 1024 threads
 constexpr int kSortRounds = 16;       // 64-element rounds per wave (LDS keys = 16 x threads)
 constexpr int kSortSmallKeys = 4096;
 
@@ -239,8 +242,8 @@ __device__ __forceinline__ uint32_t low_word(uint64_t k) { return (uint32_t)(k &
 template <int NT>
 __device__ __forceinline__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, const uint64_t* __restrict__ seg) {
   constexpr int kSortWaves = NT / 64;
-  constexpr int kWaveBits = kSortWaves == 16 ? 4 : 2;
-  static_assert(kSortWaves == 16 || kSortWaves == 4, "16 or 4 waves");
+  constexpr int kWaveBits = kSortWaves == 16 ? 4 : (kSortWaves == 8 ? 3 : 2);
+  static_assert(kSortWaves == 16 || kSortWaves == 8 || kSortWaves == 4, "16, 8 or 4 waves");
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int* s_misc = s_hist + kSortWaves * 256;
   if (threadIdx.x == 0) s_misc[0] = 0;

@@ -34,9 +34,9 @@ constexpr int kRasterThreads = 256;
 constexpr int kChunk3 = GSR_CHUNK;   // backward work unit: list entries per chunk
 constexpr int kFillBlocks = 1024;    // workgroups that fill the empty tiles
 #ifndef GSR_FWD_PAD_3D
-#define GSR_FWD_PAD_3D 28000
+#define GSR_FWD_PAD_3D 0   // 3D shared rounds (~28 KB LDS): 5 per CU measured best (4 per CU: +10 us)
 #endif
-constexpr int kFwdLdsPad = GSR_FWD_PAD_3D;   // 12.3 KB static + pad: 4 forward workgroups per CU (160 KB)
+constexpr int kFwdLdsPad = GSR_FWD_PAD_3D;
 #ifndef GSR_FWD_PAD_2D
 #define GSR_FWD_PAD_2D 0   // 2D: every tile busy, no L2 locality to protect (6 per CU by VGPRs: measured 10% faster)
 #endif
@@ -143,10 +143,12 @@ __device__ void fill_empty(const int32_t* __restrict__ order, const int32_t* __r
 }
 
 // ---------------------------------------------------------------- 3D forward
-// Work unit: a 4x4-pixel sub-tile per wave, FOUR lanes per pixel.  A tile's list is walked by
-// 16 independent waves (4 workgroups of 4 waves, one per 8x8 quadrant); each wave gathers
-// 64-entry batches (software-pipelined), culls them against its 4x4 pixel-centre box,
-// compacts the survivors into a private LDS queue and composites them four at a time: lane
+// Work unit: a 4x4-pixel sub-tile per wave, FOUR lanes per pixel, 4 workgroups of 4 waves per
+// tile (one per 8x8 quadrant).  3D: the quadrant's waves share 256-entry rounds -- each entry
+// is gathered and culled against the 8x8 quadrant once, into a double-buffered LDS queue, and
+// each wave then culls that queue against its 4x4 box (one barrier per round).  2D (every
+// tile long and busy): each wave walks the list alone in 64-entry batches.  Either way the
+// survivors of a wave's box are composited four at a time: lane
 // (pixel p, slot q) evaluates survivor 4t+q for pixel p, and the quad (the 4 lanes of a
 // pixel, a DPP quad) combines the four in list order:
 //   x_q = 1 - a_q (1 for skipped entries),  T_q = T * prod_{i<q} x_i   (quad prefix product)
@@ -208,9 +210,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end, float4* __restrict__ ckpt,
     const int32_t* __restrict__ chunk_base, int32_t* __restrict__ chunk_tile, int n_busy, int64_t CT,
     uint64_t* __restrict__ tile_cut, float cut2d) {
-  __shared__ float4 s_p0[4][64];
-  __shared__ float4 s_p1[4][64];
-  __shared__ float4 s_p2[4][64];
   __shared__ int s_max;
   const int busy_blocks = busy_grid(n_busy);
   if ((int)blockIdx.x >= busy_blocks) {
@@ -255,6 +254,124 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     const int nchunk = (end - start + kChunk3 - 1) / kChunk3;
     for (int k = threadIdx.x; k < nchunk; k += blockDim.x) chunk_tile[cbase + k] = ct;
   }
+  [[maybe_unused]] int cnt_b = 0, cnt_s = 0;
+  [[maybe_unused]] long long clk_cull = 0, clk_comp = 0;
+  [[maybe_unused]] const long long clk_start = GSR_CLOCK();
+  if constexpr (!IS2D) {
+  __shared__ float4 s_q0[2][256];
+  __shared__ float4 s_q1[2][256];
+  __shared__ float4 s_q2[2][256];
+  __shared__ int s_qe[2][256];
+  __shared__ int s_qn[2][4];
+  __shared__ unsigned char s_l[4][128];
+  // 3D -- shared rounds: the quadrant workgroup walks the list in 256-entry rounds; wave w gathers
+  // entries 64w..64w+63 of the round (one round ahead), culls them against the 8x8 quadrant
+  // and writes its survivors to segment w of a double-buffered LDS queue; after ONE barrier
+  // per round every wave culls the queue against its 4x4 box (two halves = two 128-entry
+  // chunks) and composites its survivors as below.  Each entry is gathered and 8x8-culled
+  // once per quadrant instead of once per wave.
+  static_assert(kChunk3 % 128 == 0, "a round half is one 128-entry chunk");
+  const int e_last = max(end - 1, start);
+  const float qx0 = (float)(tx * kTile + ((quad & 1) << 3)) + off, qx1 = qx0 + 7.f;
+  const float qy0 = (float)(ty * kTile + ((quad >> 1) << 3)) + off, qy1 = qy0 + 7.f;
+  float4 c0 = make_float4(0.f, 0.f, 0.f, 0.f), c1 = c0, c2 = c0;
+  int idn = 0;
+  if (end > start) {
+    const int id0 = ids[min(start + 64 * wv + lane, e_last)];
+    idn = ids[min(start + 256 + 64 * wv + lane, e_last)];
+    const Splat s0 = rec[id0];
+    c0 = s0.p0; c1 = s0.p1; c2 = s0.p2;
+  }
+  int buf = 0;
+  for (int rb = start; rb < end; rb += 256, buf ^= 1) {
+    {
+      const int e = rb + 64 * wv + lane;
+      const bool keep = e < end && cull_keep<IS2D>(c0, c1, c2, qx0, qx1, qy0, qy1);
+      const unsigned long long m = __ballot(keep);
+      if (keep) {
+        const int slot = 64 * wv +
+                         __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+        s_q0[buf][slot] = c0;
+        s_q1[buf][slot] = c1;
+        s_q2[buf][slot] = c2;
+        s_qe[buf][slot] = e;
+      }
+      if (lane == 0) s_qn[buf][wv] = __popcll(m);
+      const int id_use = idn;
+      idn = ids[min(rb + 512 + 64 * wv + lane, e_last)];
+      const Splat sn = rec[id_use];
+      c0 = sn.p0; c1 = sn.p1; c2 = sn.p2;
+    }
+    if (__syncthreads_count(!done) == 0) break;
+    for (int h = 0; h < 2; ++h) {
+      const int hb = rb + 128 * h;
+      if (hb >= end || __ballot(!done) == 0ull) break;
+      ++cnt_b;
+      if (hb > start && ((hb - start) % kChunk3) == 0) {   // entering chunk kcur+1
+        const float Dr = quad_sum(dr), Dg = quad_sum(dg), Db = quad_sum(db);
+        if (q == 0) ckpt[(int64_t)(cbase + kcur) * kRasterThreads + bwd_pixel_slot(il, jl)] = make_float4(Ts, Dr, Dg, Db);
+        cr += Dr;
+        cg += Dg;
+        cb += Db;
+        dr = dg = db = 0.f;
+        Ts = T;
+        ++kcur;
+      }
+      const int na = s_qn[buf][2 * h], nh = na + s_qn[buf][2 * h + 1];
+      int n = 0;
+      for (int r0 = 0; r0 < nh; r0 += 64) {
+        const int ii = r0 + lane;
+        const int idx = ii < na ? 128 * h + ii : 128 * h + 64 + (ii - na);
+        const bool keep = ii < nh && cull_keep<IS2D>(s_q0[buf][idx], s_q1[buf][idx], s_q2[buf][idx], bx0, bx1, by0, by1);
+        const unsigned long long m = __ballot(keep);
+        if (keep)
+          s_l[wv][n + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] =
+              (unsigned char)idx;
+        n += __popcll(m);
+      }
+      cnt_s += n;
+      __builtin_amdgcn_wave_barrier();
+      for (int k0 = 0; k0 < n; k0 += 4) {
+        const int k = k0 + q;
+        const int idx = s_l[wv][k < n ? k : n - 1];
+        const float4 p0 = s_q0[buf][idx];
+        const float4 p1 = s_q1[buf][idx];
+        const float4 p2 = s_q2[buf][idx];
+        const float dx = p0.x - px, dy = p0.y - py;
+        const float sg = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
+        const float raw = p0.z * __expf(-sg);
+        const float alpha = IS2D ? raw : fminf(kAlphaMax, raw);
+        const bool valid = IS2D ? (k < n && !done && alpha >= cut2d)
+                                : (k < n && !done && sg >= 0.f && alpha >= kAlphaThreshold);
+        const float xq = valid ? 1.f - alpha : 1.f;
+        const float d1 = dpp_mov<kQuadPrefix1>(xq);
+        const float q1 = xq * (q >= 1 ? d1 : 1.f);
+        const float d2 = dpp_mov<kQuadPrefix2>(q1);
+        const float Qi = q1 * (q >= 2 ? d2 : 1.f);
+        const float d3 = dpp_mov<kQuadPrefix1>(Qi);
+        const float Pe = q >= 1 ? d3 : 1.f;
+        const float nT = T * Qi;
+        const int fs = quad_min_i(valid && nT <= (IS2D ? kT2DMin : kTMin) ? q : 4);
+        const bool con = valid && (IS2D ? q <= fs : q < fs);
+        const float Tq = T * Pe;
+        const float vis = con ? alpha * Tq : 0.f;
+        dr += p2.x * vis;
+        dg += p2.y * vis;
+        db += p2.z * vis;
+        last = con ? s_qe[buf][idx] : last;
+        if (IS2D) Tl = con ? Tq : Tl;
+        T = quad_min((IS2D ? q <= fs : q < fs) ? nT : T);
+        done = done || fs < 4;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  } else {
+  // 2D (every tile busy and long; the per-wave walk measured faster there): each wave walks
+  // the list on its own in 64-entry batches.
+  __shared__ float4 s_p0[4][64];
+  __shared__ float4 s_p1[4][64];
+  __shared__ float4 s_p2[4][64];
   // software pipeline over 64-entry batches (records of b+1, b+2 and ids of b+3 in flight;
   // see the notes of the 2-way unrolled loop below)
   const int e_last = max(end - 1, start);
@@ -270,9 +387,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     x0 = sa.p0; x1 = sa.p1; x2 = sa.p2;
     y0 = sb.p0; y1 = sb.p1; y2 = sb.p2;
   }
-  [[maybe_unused]] int cnt_b = 0, cnt_s = 0;
-  [[maybe_unused]] long long clk_cull = 0, clk_comp = 0;
-  [[maybe_unused]] const long long clk_start = GSR_CLOCK();
   // One batch: cull + compact c (batch b0), refill c with batch b0+128 (id_use), load the ids
   // of batch b0+192 into id_new (issued BEFORE the record loads, so waiting for an id never
   // waits for younger record loads), composite.  false = every pixel of the wave is done.
@@ -351,6 +465,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   for (int b0 = start; b0 < end; b0 += 128) {
     if (!step(b0, x0, x1, x2, idp, idq)) break;
     if (b0 + 64 >= end || !step(b0 + 64, y0, y1, y2, idq, idp)) break;
+  }
   }
   if (lane == 0) {
     GSR_CNT_ADD(0, cnt_b);
