@@ -43,8 +43,14 @@ constexpr int kHistMaxTiles = 16384;
 #endif
 constexpr int kSortThreads = GSR_SORT_THREADS;    // 16 waves
 constexpr int kSortThreadsSmall = 256;
-constexpr int kSortLdsKeys = 16 * kSortThreads;   // 128 KB of 64-bit keys at 1024 threads
-constexpr int kSortRounds = 16;       // 64-element rounds per wave (LDS keys = 16 x threads)
+#ifndef GSR_SORT_ROUNDS
+#define GSR_SORT_ROUNDS 16
+#endif
+#ifndef GSR_SORT_LDS_KEYS
+#define GSR_SORT_LDS_KEYS (GSR_SORT_ROUNDS * GSR_SORT_THREADS)
+#endif
+constexpr int kSortLdsKeys = GSR_SORT_LDS_KEYS;   // 128 KB of 64-bit keys at 1024 threads
+constexpr int kSortRounds = GSR_SORT_ROUNDS;      // 64-element rounds per wave (LDS keys <= rounds x threads)
 constexpr int kSortSmallKeys = 4096;
 
 // ---------------------------------------------------------------- tile scan (single block)
@@ -587,6 +593,7 @@ int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_
   if (n_big + n_mid > 0) {
     int lds_keys = 1024;
     while (lds_keys < max_seg && lds_keys < kSortLdsKeys) lds_keys <<= 1;
+    lds_keys = min(lds_keys, kSortLdsKeys);
     hipLaunchKernelGGL(k_segsort<kSortThreads>, dim3(n_busy), dim3(kSortThreads),
                        lds_keys * sizeof(uint64_t) + hist_bytes(kSortThreads), s, keys, tmpk, tmpp0, tmpp1,
                        tile_offset, busy_tiles, k_of_slot, lds_keys, sorted_ids, k_of_s);
