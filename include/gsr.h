@@ -110,7 +110,10 @@ int gsr_selftest_lds_order(int32_t* violations, void* stream);
  * contiguous range for its items with one atomic, so the (c,n) ranges tile [0, I) in
  * workgroup arrival order -- consumers only address rows through isect_offset) and
  * tile_count [C*tiles + 1] (zeroed, then accumulated; element C*tiles ends as I, the
- * emission counter).  Culled Gaussians get count 0.
+ * emission counter).  tile_count_zeroed != 0: the caller guarantees tile_count is already
+ * all zero -- gsr_bin_offsets resets the counter element and gsr_bin_sort counts the tiles
+ * back down, so a buffer that went through project -> offsets -> sort needs no memset.
+ * Culled Gaussians get count 0.
  * [band_y0, band_y1): the tile rows this call bins (band_y1 = -1: all rows).  Multi-GPU band
  * sharding gives each rank a band; tiles outside it stay empty (background)
  * and their entries contribute nothing, so the ranks' gradients sum to the full gradient. */
@@ -119,14 +122,15 @@ int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride,
                       float near_plane, float far_plane, float radius_clip, float eps2d,
                       int radius_mode, int input_mode, int band_y0, int band_y1, float* rec, float* depth,
                       uint32_t* rect, int32_t* isect_count, int32_t* isect_offset, int32_t* tile_count,
-                      void* stream);
+                      int tile_count_zeroed, void* stream);
 
 /* 2D projection: params [N, >=9] (layout src/gaussian_renderer.py:314-318).  The tile rect
  * covers every pixel where opacity*exp(-q) >= eps_cut (the reference is dense; eps_cut
  * bounds the dropped mass).  Same outputs as gsr3d_project_fwd with C = 1. */
 int gsr2d_project_fwd(const float* params, int64_t N, int64_t row_stride, int width,
                       int height, float eps_cut, float* rec, uint32_t* rect,
-                      int32_t* isect_count, int32_t* isect_offset, int32_t* tile_count, void* stream);
+                      int32_t* isect_count, int32_t* isect_offset, int32_t* tile_count,
+                      int tile_count_zeroed, void* stream);
 
 /* ---------------------------------------------------------------- (b) binning */
 
@@ -134,8 +138,9 @@ int gsr2d_project_fwd(const float* params, int64_t N, int64_t row_stride, int wi
  * [CT+1] (first GSR_CHUNK-entry chunk of each tile's list), busy_tiles [CT] (rasterizer visit
  * order: the stats.n_busy non-empty tiles first, longest lists first, then the empty tiles),
  * tile_end [CT] (set to -1: the raster forward's atomicMax target), tile_cut [CT] (zeroed;
- * the raster forward writes the cut keys) and stats (device). */
-int gsr_bin_offsets(const int32_t* tile_count, int64_t CT, int32_t* tile_offset,
+ * the raster forward writes the cut keys) and stats (device).  Resets the emission counter
+ * tile_count[CT] to 0 (the per-tile counts are consumed by gsr_bin_sort). */
+int gsr_bin_offsets(int32_t* tile_count, int64_t CT, int32_t* tile_offset,
                     int32_t* chunk_base, int32_t* busy_tiles, int32_t* tile_end,
                     uint64_t* tile_cut, gsr_bin_stats* stats, void* stream);
 
@@ -173,8 +178,9 @@ int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_
  * chunk-parallel backward: chunk_state [n_chunks*256*4] ({T at the chunk's end, the rgb
  * sum of all later chunks} per pixel of the tile, for every GSR_CHUNK-entry chunk the tile's
  * walk reached), chunk_tile [n_chunks] (owning tile of each chunk) and chunk_list
- * [n_chunks] (the chunks before each tile's tile_end, in no particular order; their count
- * is added to stats->n_active).  stats: the device gsr_bin_stats of gsr_bin_offsets. */
+ * [n_chunks][4] (a descriptor {first sorted entry, entry count, chunk_state row, tile} for
+ * each chunk before its tile's tile_end, in no particular order; their count is added to
+ * stats->n_active).  stats: the device gsr_bin_stats of gsr_bin_offsets. */
 int gsr3d_raster_fwd(const float* rec, const float* depth, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_order, const int32_t* chunk_base, int C, int width,
                      int height, const float* bg, int32_t n_busy, gsr_bin_stats* stats,

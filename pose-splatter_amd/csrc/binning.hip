@@ -71,7 +71,7 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
   return v;
 }
 
-__global__ __launch_bounds__(kTopThreads) void k_tile_scan(const int32_t* __restrict__ tile_count, int64_t CT,
+__global__ __launch_bounds__(kTopThreads) void k_tile_scan(int32_t* __restrict__ tile_count, int64_t CT,
                                                           int32_t* __restrict__ tile_offset,
                                                           int32_t* __restrict__ chunk_base,
                                                           int32_t* __restrict__ order,
@@ -88,7 +88,10 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(const int32_t* __rest
   if (staged)
     for (int64_t i = threadIdx.x; i < CT; i += kTopThreads) s_cnt[i] = tile_count[i];
   const int32_t* cnt = staged ? s_cnt : tile_count;
-  if (threadIdx.x == 0) s_max = 0;
+  if (threadIdx.x == 0) {
+    s_max = 0;
+    tile_count[CT] = 0;   // the projection's emission counter: consumed, reset for the next call
+  }
   if (threadIdx.x < 33) s_bucket[threadIdx.x] = 0;
   __syncthreads();
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -206,6 +209,9 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__
     __syncthreads();
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
       const int v = hist[t];
+#ifdef GSR_EXP_DBLATOM
+      if (v) atomicAdd(&gcnt[t], v & 0x40000000);   // timing experiment: a second atomic
+#endif
       if (v) hist[t] = toff[t] + atomicSub(&gcnt[t], v) - v;
     }
     __syncthreads();
@@ -542,7 +548,7 @@ using namespace gsr;
 
 extern "C" {
 
-int gsr_bin_offsets(const int32_t* tile_count, int64_t CT, int32_t* tile_offset, int32_t* chunk_base,
+int gsr_bin_offsets(int32_t* tile_count, int64_t CT, int32_t* tile_offset, int32_t* chunk_base,
                     int32_t* busy_tiles, int32_t* tile_end, uint64_t* tile_cut, gsr_bin_stats* stats,
                     void* stream) {
   GSR_REQUIRE(CT >= 1 && CT < (1ll << 31), "gsr_bin_offsets: bad CT=%lld", (long long)CT);

@@ -279,7 +279,11 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   if (end > start) {
     const int id0 = ids[min(start + 64 * wv + lane, e_last)];
     idn = ids[min(start + 256 + 64 * wv + lane, e_last)];
+#ifdef GSR_EXP_CONTIG
+    const Splat s0 = rec[min(start + 64 * wv + lane, e_last) >> 2]; (void)id0;
+#else
     const Splat s0 = rec[id0];
+#endif
     c0 = s0.p0; c1 = s0.p1; c2 = s0.p2;
   }
   int buf = 0;
@@ -299,7 +303,11 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
       if (lane == 0) s_qn[buf][wv] = __popcll(m);
       const int id_use = idn;
       idn = ids[min(rb + 512 + 64 * wv + lane, e_last)];
+#ifdef GSR_EXP_CONTIG
+      const Splat sn = rec[min(rb + 256 + 64 * wv + lane, e_last) >> 2]; (void)id_use;
+#else
       const Splat sn = rec[id_use];
+#endif
       c0 = sn.p0; c1 = sn.p1; c2 = sn.p2;
     }
     if (__syncthreads_count(!done) == 0) break;
@@ -592,7 +600,11 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_finalize(
   if (nact > 0) {
     const int pos = atomicAdd(&stats->n_active, nact);
     const int cbase = chunk_base[ct];
-    for (int k = 0; k < nact; ++k) chunk_list[pos + k] = cbase + k;
+    int4* desc = reinterpret_cast<int4*>(chunk_list);
+    for (int k = 0; k < nact; ++k) {
+      const int b0 = start + k * kChunk3;
+      desc[pos + k] = make_int4(b0, min(kChunk3, te - b0), cbase + k, ct);
+    }
   }
 }
 
@@ -679,16 +691,12 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
   __shared__ float L[kPartial][2][kChunk3];
   __shared__ short s_list[4][kChunk3 + kGroup];
   // one workgroup per grid slot; slots past the forward's active-chunk count exit at once
+  // the chunk's descriptor {first entry, entries (>= 1), chunk record row, tile} -- one load
+  // (read before the bound check: the list has a slot for every grid slot)
+  const int4 cd = reinterpret_cast<const int4*>(chunk_list)[blockIdx.x];
   if ((int)blockIdx.x >= stats->n_active) return;
   [[maybe_unused]] const long long clk_start = GSR_CLOCK();
-  const int chunk = chunk_list[blockIdx.x];
-  const int ct = chunk_tile[chunk];
-  const int cbase = chunk_base[ct];
-  const int kc = chunk - cbase;
-  const int start = tile_offset[ct];
-  const int eff = tile_end[ct];
-  const int b0 = start + kc * kChunk3;
-  const int n = min(kChunk3, eff - b0);   // >= 1: the list holds chunks before tile_end only
+  const int b0 = cd.x, n = cd.y, chunk = cd.z, ct = cd.w;
   const SubTile st = sub_tile<IS2D>(ct, tw, th, W, H);
   const int wv = st.wv;
   float Tf = 1.f, Tl = 1.f, vr = 0.f, vg = 0.f, vb = 0.f, va = 0.f;
@@ -717,7 +725,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
   // state at the end of this chunk: {T_end, suffix colour sum} (forward epilogue)
   float T = Tf, Sr = 0.f, Sg = 0.f, Sb = 0.f;
   if (last >= b0) {
-    const float4 r = ckpt[(int64_t)(cbase + kc) * kRasterThreads + threadIdx.x];
+    const float4 r = ckpt[(int64_t)chunk * kRasterThreads + threadIdx.x];
     T = r.x;
     Sr = r.y;
     Sg = r.z;
@@ -737,7 +745,11 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wlast = max(wlast, __shfl_xor(wlast, o, 64));
   if (threadIdx.x < n) {
+#ifdef GSR_EXP_CONTIG
+    const Splat sp = rec[(b0 + threadIdx.x) >> 2];
+#else
     const Splat sp = rec[ids[b0 + threadIdx.x]];
+#endif
     s_p0[threadIdx.x] = sp.p0;
     s_p1[threadIdx.x] = sp.p1;
     s_p2[threadIdx.x] = sp.p2;

@@ -62,8 +62,8 @@ EXPORTS = {
     "gsr_selftest_reduce64": (ctypes.c_int, [_P, _P]),
     "gsr_selftest_lds_order": (ctypes.c_int, [_P, _P]),
     "gsr3d_project_fwd": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _I32, _I32, _I32, _F, _F, _F, _F,
-                                         _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
-    "gsr2d_project_fwd": (ctypes.c_int, [_P, _I64, _I64, _I32, _I32, _F, _P, _P, _P, _P, _P, _P]),
+                                         _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _I32, _P]),
+    "gsr2d_project_fwd": (ctypes.c_int, [_P, _I64, _I64, _I32, _I32, _F, _P, _P, _P, _P, _P, _I32, _P]),
     "gsr_bin_offsets": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P, _P, _P]),
     "gsr_bin_sort_workspace": (_SZ, [_I64, _I64]),
     "gsr_bin_sort": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I32, _I64, _I32,

@@ -130,7 +130,7 @@ class _Arena:
 
 _I32, _I64, _F32 = torch.int32, torch.int64, torch.float32
 # tensor views exposed for tests / debugging: name -> (arena attribute, dtype)
-_VIEWS = {"rec": ("pre", _F32), "depth": ("pre", _F32), "rect": ("pre", _I32), "cnt": ("pre", _I32), "tile_cnt": ("pre", _I32),
+_VIEWS = {"rec": ("pre", _F32), "depth": ("pre", _F32), "rect": ("pre", _I32), "cnt": ("pre", _I32),
           "isect_off": ("pre", _I32), "tile_off": ("pre", _I32), "busy": ("pre", _I32),
           "chunk_base": ("pre", _I32), "stats_dev": ("pre", _I32),
           "sorted_ids": ("post", _I32), "k_of_s": ("post", _I32), "final_T": ("post", _F32),
@@ -149,6 +149,22 @@ def _pinned_stats(device) -> torch.Tensor:
     return t
 
 
+# Per (device, tile count): the projection's tile histogram + emission counter, shared by
+# successive calls.  project -> offsets -> sort leaves it all zero (the emit counts each tile
+# down, the offsets kernel resets the counter), so the next projection skips its memset; a
+# call that stops in between leaves the flag False and the next one clears it.  Calls on one
+# device are stream-ordered (one library stream per device), so no two pipelines overlap.
+_tc_cache = {}
+
+
+def _tile_counts(device, CT: int) -> list:
+    key = (str(device), CT)
+    e = _tc_cache.get(key)
+    if e is None:
+        e = _tc_cache[key] = [torch.empty(CT + 1, device=device, dtype=torch.int32), False]
+    return e
+
+
 class _Bins:
     """Per-call intermediates shared by forward and backward: two arenas, one sized before
     the stats readback (per-Gaussian and per-tile buffers) and one after it (per-intersection
@@ -162,14 +178,21 @@ class _Bins:
         self.CT = C * self.tw * self.th
         CN = max(C * N, 1)
         self.pre = _Arena(device, {
-            "rec": CN * 48, "depth": CN * 4, "rect": CN * 8, "cnt": CN * 4, "tile_cnt": (self.CT + 1) * 4,
+            "rec": CN * 48, "depth": CN * 4, "rect": CN * 8, "cnt": CN * 4,
             "isect_off": CN * 4, "tile_off": (self.CT + 1) * 4, "busy": self.CT * 4,
             "chunk_base": (self.CT + 1) * 4, "tile_end": self.CT * 4, "tile_cut": self.CT * 8,
             "stats_dev": 32})
         self.p = dict(self.pre.ptr)
+        self.tc = _tile_counts(device, self.CT)
+        self.p["tile_cnt"] = self.tc[0].data_ptr()
         self.post = None
         self.n_chunks = self.n_isect = self.max_seg = self.n_busy = 0
         self.key = (str(device), C, N, width, height)
+
+    def take_tile_counts(self) -> int:
+        """For the projection call: 1 if the shared tile_count buffer is known to be zero."""
+        z, self.tc[1] = self.tc[1], False
+        return int(z)
 
     def guess_post(self, with_chunks: bool):
         """Before the stats readback: size the per-intersection arena from the last call with
@@ -214,7 +237,7 @@ class _Bins:
         self.post = _Arena(self.device, {
             "sorted_ids": I * 4, "k_of_s": I * 4, "sort_ws": int(L.gsr_bin_sort_workspace(I, self.CT)),
             "final_T": P * 8, "last": P * 4,
-            "chunk_state": K * 256 * 16, "chunk_tile": K * 4, "chunk_list": K * 4})
+            "chunk_state": K * 256 * 16, "chunk_tile": K * 4, "chunk_list": K * 16})
         self.post_cap = (I, K)
         self.p.update(self.post.ptr)
 
@@ -234,6 +257,7 @@ class _Bins:
                              self.W, self.H, order, self.n_isect, self.max_seg, self.n_busy, self.n_sort_big,
                              self.n_sort_mid, p["sort_ws"],
                              self.post.off["sort_ws"][1], p["sorted_ids"], p["k_of_s"], stream), "gsr_bin_sort")
+        self.tc[1] = True   # offsets reset the counter, the emit counted every tile back to 0
 
 
 def _record_stats(b: _Bins):
@@ -297,7 +321,7 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
       check(L.gsr3d_project_fwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height,
                               opts.near_plane, opts.far_plane, opts.radius_clip, opts.eps2d,
                               opts.radius_mode, opts.input_mode, opts.band[0], opts.band[1], q["rec"], q["depth"],
-                              q["rect"], q["cnt"], q["isect_off"], q["tile_cnt"], stream),
+                              q["rect"], q["cnt"], q["isect_off"], q["tile_cnt"], b.take_tile_counts(), stream),
           "gsr3d_project_fwd")
     b.guess_post(with_chunks=True)
     b.offsets(stream)
@@ -325,7 +349,8 @@ def _forward2d(params, bg, width, height, eps_cut):
     q = b.p
     with _timed("project2d_fwd"):
       check(L.gsr2d_project_fwd(_ptr(p), N, stride, width, height, eps_cut, q["rec"], q["rect"],
-                              q["cnt"], q["isect_off"], q["tile_cnt"], stream), "gsr2d_project_fwd")
+                              q["cnt"], q["isect_off"], q["tile_cnt"], b.take_tile_counts(), stream),
+          "gsr2d_project_fwd")
     b.guess_post(with_chunks=True)
     b.offsets(stream)
     b.ensure_post(with_chunks=True)

@@ -41,18 +41,18 @@ def test_invalid_arguments_are_reported_not_launched():
     from gsr import _lib
     lib = _lib.lib()
     rc = lib.gsr3d_project_fwd(None, 10, 14, None, None, 0, 64, 64, 0.01, 1e10, 0.0, 0.3, 0, 0, 0, -1,
-                               None, None, None, None, None, None, None)
+                               None, None, None, None, None, None, 0, None)
     assert rc == -1 and b"bad N" in lib.gsr_last_error()
     rc = lib.gsr3d_project_fwd(None, 10, 14, None, None, 1, 64, 64, 0.01, 1e10, 0.0, 0.3, 7, 0, 0, -1,
-                               None, None, None, None, None, None, None)
+                               None, None, None, None, None, None, 0, None)
     assert rc == -1 and b"radius_mode" in lib.gsr_last_error()
     rc = lib.gsr3d_project_fwd(None, 10, 14, None, None, 1, 64, 64, 0.01, 1e10, 0.0, 0.3, 0, 0, 2, 1,
-                               None, None, None, None, None, None, None)
+                               None, None, None, None, None, None, 0, None)
     assert rc == -1 and b"bad band" in lib.gsr_last_error()
     rc = lib.gsr3d_project_fwd(None, 10, 14, None, None, 1, 64, 64, 0.01, 1e10, 0.0, 0.3, 7, 0, 0, -1,
-                               None, None, None, None, None, None, None)
+                               None, None, None, None, None, None, 0, None)
     assert rc == -1 and b"radius_mode" in lib.gsr_last_error()
-    rc = lib.gsr2d_project_fwd(None, 10, 9, 64, 64, 2.0, None, None, None, None, None, None)
+    rc = lib.gsr2d_project_fwd(None, 10, 9, 64, 64, 2.0, None, None, None, None, None, 0, None)
     assert rc == -1 and b"eps_cut" in lib.gsr_last_error()
     rc = lib.gsr_bin_sort(None, None, None, None, None, None, 1, 10, 64, 64, 5, 0, 0, 0, 0, 0, None, 0, None, None,
                           None)

@@ -1,6 +1,7 @@
 #!/bin/bash
 # On the GPU box: bench the default library and each build_var/libgsr_*.so (kernel times).
 set -e
+shopt -s nullglob
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 timeout -k 10 120 python bench.py --cpu-baseline 0 --steps 10 > gpurun_out/var_base.json

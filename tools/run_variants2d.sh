@@ -1,6 +1,7 @@
 #!/bin/bash
 # On the GPU box: config-4 (2D) bench of the default library and each build_var/libgsr_*.so.
 set -e
+shopt -s nullglob
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 timeout -k 10 120 python bench.py --config 4 --cpu-baseline 0 --steps 5 > gpurun_out/var2_base.json
