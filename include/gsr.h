@@ -177,23 +177,20 @@ int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_
  * below its tile's cut), and for the
  * chunk-parallel backward: chunk_state [n_chunks*256*4] ({T at the chunk's end, the rgb
  * sum of all later chunks} per pixel of the tile, for every GSR_CHUNK-entry chunk the tile's
- * walk reached), chunk_tile [n_chunks] (owning tile of each chunk) and chunk_list
- * [n_chunks][4] (a descriptor {first sorted entry, entry count, chunk_state row, tile} for
+ * walk reached) and chunk_list [n_chunks][4] (a descriptor {first sorted entry, entry count, chunk_state row, tile} for
  * each chunk before its tile's tile_end, in no particular order; their count is added to
  * stats->n_active).  stats: the device gsr_bin_stats of gsr_bin_offsets. */
 int gsr3d_raster_fwd(const float* rec, const float* depth, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_order, const int32_t* chunk_base, int C, int width,
                      int height, const float* bg, int32_t n_busy, gsr_bin_stats* stats,
                      float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
-                     uint64_t* tile_cut, float* chunk_state, int32_t* chunk_tile,
-                     int32_t* chunk_list, void* stream);
+                     uint64_t* tile_cut, float* chunk_state, int32_t* chunk_list, void* stream);
 
 /* Backward of gsr3d_raster_fwd: workgroup b takes chunk_list[b] for b < stats->n_active
  * (n_chunks bounds the grid).  v_rgb [C,H,W,3], v_alpha [C,H,W] (contiguous).  Writes the
  * partial row k_of_s[s] of every sorted entry s in [tile start, tile_end). */
 int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
-                     const int32_t* tile_end, const int32_t* chunk_base,
-                     const int32_t* chunk_tile, const float* chunk_state,
+                     const int32_t* tile_end, const int32_t* chunk_base, const float* chunk_state,
                      const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
                      int C, int width, int height, const float* bg, const float* final_T,
                      const int32_t* last, const float* v_rgb, const float* v_alpha,
@@ -209,14 +206,12 @@ int gsr2d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t*
                      const int32_t* tile_order, const int32_t* chunk_base, int width, int height,
                      float eps_cut, const float* bg, int32_t n_busy, gsr_bin_stats* stats,
                      float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
-                     uint64_t* tile_cut, float* chunk_state, int32_t* chunk_tile,
-                     int32_t* chunk_list, void* stream);
+                     uint64_t* tile_cut, float* chunk_state, int32_t* chunk_list, void* stream);
 
 /* Backward of gsr2d_raster_fwd (the reference's autograd of the recursion), same contract
  * as gsr3d_raster_bwd with C = 1. */
 int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
-                     const int32_t* tile_end, const int32_t* chunk_base,
-                     const int32_t* chunk_tile, const float* chunk_state,
+                     const int32_t* tile_end, const int32_t* chunk_base, const float* chunk_state,
                      const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
                      int width, int height, float eps_cut, const float* bg,
                      const float* final_T, const int32_t* last, const float* v_rgb,
@@ -271,7 +266,7 @@ typedef struct gsr_loss_terms {
 
 /* gsr3d_raster_bwd with the cotangents generated from `loss` instead of read from images. */
 int gsr3d_raster_bwd_loss(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
-                          const int32_t* tile_end, const int32_t* chunk_base, const int32_t* chunk_tile,
+                          const int32_t* tile_end, const int32_t* chunk_base,
                           const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats,
                           int32_t n_chunks, int C, int width, int height, const float* bg,
                           const float* final_T, const int32_t* last, const gsr_loss_terms* loss,

@@ -208,7 +208,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     const int32_t* __restrict__ order, int W, int H, int tw, int th, const float* __restrict__ bg,
     float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
     int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end, float4* __restrict__ ckpt,
-    const int32_t* __restrict__ chunk_base, int32_t* __restrict__ chunk_tile, int n_busy, int64_t CT,
+    const int32_t* __restrict__ chunk_base, int n_busy, int64_t CT,
     uint64_t* __restrict__ tile_cut, float cut2d) {
   __shared__ int s_max;
   const int busy_blocks = busy_grid(n_busy);
@@ -250,10 +250,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   const int cbase = chunk_base[ct];
   int kcur = 0;
   float Ts = 1.f, dr = 0.f, dg = 0.f, db = 0.f;   // dr..: this lane's share of the chunk's colour
-  if (quad == 0) {
-    const int nchunk = (end - start + kChunk3 - 1) / kChunk3;
-    for (int k = threadIdx.x; k < nchunk; k += blockDim.x) chunk_tile[cbase + k] = ct;
-  }
   [[maybe_unused]] int cnt_b = 0, cnt_s = 0;
   [[maybe_unused]] long long clk_cull = 0, clk_comp = 0;
   [[maybe_unused]] const long long clk_start = GSR_CLOCK();
@@ -674,7 +670,7 @@ template <bool LOSS, bool IS2D>
 __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ tile_end, const int32_t* __restrict__ chunk_base,
-    const int32_t* __restrict__ chunk_tile, const float4* __restrict__ ckpt, int W, int H, int tw, int th,
+    const float4* __restrict__ ckpt, int W, int H, int tw, int th,
     const float* __restrict__ bg, const float* __restrict__ final_T, const int32_t* __restrict__ last_in,
     const float* __restrict__ v_rgb, const float* __restrict__ v_alpha, float* __restrict__ partial,
     const int32_t* __restrict__ chunk_list, gsr_bin_stats* __restrict__ stats,
@@ -920,7 +916,7 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
                       const int32_t* tile_offset, const int32_t* tile_order, const int32_t* chunk_base, int C,
                       int width, int height, float cut2d, const float* bg, int32_t n_busy, gsr_bin_stats* stats,
                       float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
-                      uint64_t* tile_cut, float* chunk_state, int32_t* chunk_tile, int32_t* chunk_list,
+                      uint64_t* tile_cut, float* chunk_state, int32_t* chunk_list,
                       void* stream) {
   GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "%s: bad C=%d or image %dx%d", who, C, width, height);
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
@@ -936,7 +932,7 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
   hipLaunchKernelGGL(k_raster_fwd<IS2D>, dim3((unsigned)(busy_grid(n_busy) + n_fill)), dim3(kRasterThreads),
                      IS2D ? kFwdLdsPad2D : kFwdLdsPad, s, (const Splat*)rec, sorted_ids, tile_offset, tile_order,
                      width, height, tw, th,
-                     bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state, chunk_base, chunk_tile,
+                     bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state, chunk_base,
                      (int)n_busy, CT, tile_cut, cut2d);
   GSR_LAUNCH_CHECK(who);
   if (n_busy > 0) {
@@ -950,7 +946,7 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
 
 template <bool LOSS, bool IS2D>
 static int raster_bwd(const char* who, const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
-                      const int32_t* tile_end, const int32_t* chunk_base, const int32_t* chunk_tile,
+                      const int32_t* tile_end, const int32_t* chunk_base,
                       const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
                       int C, int width, int height, float cut2d, const float* bg, const float* final_T,
                       const int32_t* last, const float* v_rgb, const float* v_alpha, const gsr_loss_terms& lt,
@@ -961,7 +957,7 @@ static int raster_bwd(const char* who, const float* rec, const int32_t* sorted_i
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   // n_chunks bounds the forward's active-chunk count (stats->n_active, device-side)
   hipLaunchKernelGGL((k_raster_bwd<LOSS, IS2D>), dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
-                     (const Splat*)rec, sorted_ids, tile_offset, tile_end, chunk_base, chunk_tile,
+                     (const Splat*)rec, sorted_ids, tile_offset, tile_end, chunk_base,
                      (const float4*)chunk_state, width, height, tw, th, bg, final_T, last, v_rgb, v_alpha, partial,
                      chunk_list, stats, k_of_s, lt, C, cut2d);
   GSR_LAUNCH_CHECK(who);
@@ -976,26 +972,26 @@ int gsr3d_raster_fwd(const float* rec, const float* depth, const int32_t* sorted
                      const int32_t* tile_order, const int32_t* chunk_base, int C, int width, int height,
                      const float* bg, int32_t n_busy, gsr_bin_stats* stats, float* rgb, float* alpha,
                      float* final_T, int32_t* last, int32_t* tile_end, uint64_t* tile_cut, float* chunk_state,
-                     int32_t* chunk_tile, int32_t* chunk_list, void* stream) {
+                     int32_t* chunk_list, void* stream) {
   return raster_fwd<false>("gsr3d_raster_fwd", rec, depth, sorted_ids, tile_offset, tile_order, chunk_base, C, width,
                            height, 0.f, bg, n_busy, stats, rgb, alpha, final_T, last, tile_end, tile_cut,
-                           chunk_state, chunk_tile, chunk_list, stream);
+                           chunk_state, chunk_list, stream);
 }
 
 int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
-                     const int32_t* tile_end, const int32_t* chunk_base, const int32_t* chunk_tile,
+                     const int32_t* tile_end, const int32_t* chunk_base,
                      const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
                      int C, int width, int height, const float* bg, const float* final_T, const int32_t* last,
                      const float* v_rgb, const float* v_alpha, const int32_t* k_of_s, float* partial,
                      void* stream) {
   const gsr_loss_terms none{};
   return raster_bwd<false, false>("gsr3d_raster_bwd", rec, sorted_ids, tile_offset, tile_end, chunk_base,
-                                  chunk_tile, chunk_state, chunk_list, stats, n_chunks, C, width, height, 0.f, bg,
+                                  chunk_state, chunk_list, stats, n_chunks, C, width, height, 0.f, bg,
                                   final_T, last, v_rgb, v_alpha, none, k_of_s, partial, stream);
 }
 
 int gsr3d_raster_bwd_loss(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
-                          const int32_t* tile_end, const int32_t* chunk_base, const int32_t* chunk_tile,
+                          const int32_t* tile_end, const int32_t* chunk_base,
                           const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats,
                           int32_t n_chunks, int C, int width, int height, const float* bg, const float* final_T,
                           const int32_t* last, const gsr_loss_terms* loss, const int32_t* k_of_s, float* partial,
@@ -1003,7 +999,7 @@ int gsr3d_raster_bwd_loss(const float* rec, const int32_t* sorted_ids, const int
   GSR_REQUIRE(loss != nullptr && loss->rgb && loss->target_img && loss->target_mask && loss->sums && loss->grad_out,
               "gsr3d_raster_bwd_loss: incomplete loss terms");
   return raster_bwd<true, false>("gsr3d_raster_bwd_loss", rec, sorted_ids, tile_offset, tile_end, chunk_base,
-                                 chunk_tile, chunk_state, chunk_list, stats, n_chunks, C, width, height, 0.f, bg,
+                                 chunk_state, chunk_list, stats, n_chunks, C, width, height, 0.f, bg,
                                  final_T, last, nullptr, nullptr, *loss, k_of_s, partial, stream);
 }
 
@@ -1011,15 +1007,15 @@ int gsr2d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t*
                      const int32_t* tile_order, const int32_t* chunk_base, int width, int height, float eps_cut,
                      const float* bg, int32_t n_busy, gsr_bin_stats* stats, float* rgb, float* alpha,
                      float* final_T, int32_t* last, int32_t* tile_end, uint64_t* tile_cut, float* chunk_state,
-                     int32_t* chunk_tile, int32_t* chunk_list, void* stream) {
+                     int32_t* chunk_list, void* stream) {
   GSR_REQUIRE(eps_cut > 0.f && eps_cut < 1.f, "gsr2d_raster_fwd: eps_cut must be in (0,1)");
   return raster_fwd<true>("gsr2d_raster_fwd", rec, nullptr, sorted_ids, tile_offset, tile_order, chunk_base, 1, width,
                           height, eps_cut, bg, n_busy, stats, rgb, alpha, final_T, last, tile_end, tile_cut,
-                          chunk_state, chunk_tile, chunk_list, stream);
+                          chunk_state, chunk_list, stream);
 }
 
 int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
-                     const int32_t* tile_end, const int32_t* chunk_base, const int32_t* chunk_tile,
+                     const int32_t* tile_end, const int32_t* chunk_base,
                      const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
                      int width, int height, float eps_cut, const float* bg, const float* final_T,
                      const int32_t* last, const float* v_rgb, const float* v_alpha, const int32_t* k_of_s,
@@ -1027,7 +1023,7 @@ int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t*
   GSR_REQUIRE(eps_cut > 0.f && eps_cut < 1.f, "gsr2d_raster_bwd: eps_cut must be in (0,1)");
   const gsr_loss_terms none{};
   return raster_bwd<false, true>("gsr2d_raster_bwd", rec, sorted_ids, tile_offset, tile_end, chunk_base,
-                                 chunk_tile, chunk_state, chunk_list, stats, n_chunks, 1, width, height, eps_cut, bg,
+                                 chunk_state, chunk_list, stats, n_chunks, 1, width, height, eps_cut, bg,
                                  final_T, last, v_rgb, v_alpha, none, k_of_s, partial, stream);
 }
 

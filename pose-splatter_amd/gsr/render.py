@@ -135,7 +135,7 @@ _VIEWS = {"rec": ("pre", _F32), "depth": ("pre", _F32), "rect": ("pre", _I32), "
           "chunk_base": ("pre", _I32), "stats_dev": ("pre", _I32),
           "sorted_ids": ("post", _I32), "k_of_s": ("post", _I32), "final_T": ("post", _F32),
           "last": ("post", _I32), "tile_end": ("pre", _I32), "tile_cut": ("pre", _I64),
-          "chunk_state": ("post", _F32), "chunk_tile": ("post", _I32), "chunk_list": ("post", _I32)}
+          "chunk_state": ("post", _F32), "chunk_list": ("post", _I32)}
 
 _pinned = {}
 _size_hint = {}   # (device, C, N, W, H) -> (I, n_chunks) of the last forward of that shape
@@ -237,7 +237,7 @@ class _Bins:
         self.post = _Arena(self.device, {
             "sorted_ids": I * 4, "k_of_s": I * 4, "sort_ws": int(L.gsr_bin_sort_workspace(I, self.CT)),
             "final_T": P * 8, "last": P * 4,
-            "chunk_state": K * 256 * 16, "chunk_tile": K * 4, "chunk_list": K * 16})
+            "chunk_state": K * 256 * 16, "chunk_list": K * 16})
         self.post_cap = (I, K)
         self.p.update(self.post.ptr)
 
@@ -333,7 +333,7 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
       check(L.gsr3d_raster_fwd(q["rec"], q["depth"], q["sorted_ids"], q["tile_off"], q["busy"], q["chunk_base"],
                              C, width, height, _ptr(bgc), b.n_busy, q["stats_dev"], _ptr(rgb), _ptr(alpha),
                              q["final_T"], q["last"], q["tile_end"], q["tile_cut"], q["chunk_state"],
-                             q["chunk_tile"], q["chunk_list"], stream), "gsr3d_raster_fwd")
+                             q["chunk_list"], stream), "gsr3d_raster_fwd")
     _record_stats(b)
     return rgb, alpha, b, (p, stride, V, Kc, bgc, width, height, opts)
 
@@ -360,7 +360,7 @@ def _forward2d(params, bg, width, height, eps_cut):
     with _timed("raster2d_fwd"):
       check(L.gsr2d_raster_fwd(q["rec"], q["sorted_ids"], q["tile_off"], q["busy"], q["chunk_base"], width, height,
                              eps_cut, _ptr(bgc), b.n_busy, q["stats_dev"], _ptr(rgb), _ptr(alpha), q["final_T"],
-                             q["last"], q["tile_end"], q["tile_cut"], q["chunk_state"], q["chunk_tile"],
+                             q["last"], q["tile_end"], q["tile_cut"], q["chunk_state"],
                              q["chunk_list"], stream), "gsr2d_raster_fwd")
     _record_stats(b)
     return rgb, alpha, b, (p, stride, bgc, width, height, eps_cut)
@@ -398,7 +398,7 @@ class _Render3D(torch.autograd.Function):
 
         def raster(L, q, partial, stream):
             check(L.gsr3d_raster_bwd(q["rec"], q["sorted_ids"], q["tile_off"], q["tile_end"], q["chunk_base"],
-                                     q["chunk_tile"], q["chunk_state"], q["chunk_list"], q["stats_dev"],
+                                     q["chunk_state"], q["chunk_list"], q["stats_dev"],
                                      b.n_chunks, C, width, height, _ptr(bgc), q["final_T"], q["last"],
                                      _ptr(v_rgb), _ptr(v_alpha), q["k_of_s"], _ptr(partial), stream),
                   "gsr3d_raster_bwd")
@@ -457,7 +457,7 @@ class _Render2D(torch.autograd.Function):
             q = b.p
             with _timed("raster2d_bwd"):
               check(L.gsr2d_raster_bwd(q["rec"], q["sorted_ids"], q["tile_off"], q["tile_end"], q["chunk_base"],
-                                     q["chunk_tile"], q["chunk_state"], q["chunk_list"], q["stats_dev"],
+                                     q["chunk_state"], q["chunk_list"], q["stats_dev"],
                                      b.n_chunks, width, height, eps_cut, _ptr(bgc), q["final_T"], q["last"],
                                      _ptr(v_rgb), _ptr(v_alpha), q["k_of_s"], _ptr(partial), stream),
                   "gsr2d_raster_bwd")
