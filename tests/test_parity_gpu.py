@@ -124,9 +124,36 @@ def test_3d_deterministic(cuda):
 def test_3d_binning_exact(cuda):
     """Tile lists are integer work: compare bit-exactly with a CPU re-sort of the GPU's own
     projection output (rect + depth bits), and the rects with the oracle's projection."""
-    from gsr import render as R
     W, H, C = 192, 170, 2
     p, V, K = _scene3d(10000, W, H, C, 11)
+    b = _check_binning_exact(p, V, K, W, H, C, cuda)
+    N = p.shape[0]
+    cnt = b.cnt.cpu().to(torch.int64)
+    I = b.n_isect
+    # projection rects vs the oracle's (float decisions: near-total agreement)
+    o = _oracle3d()
+    m, q, s, col, op = o.activations3d(p)
+    pr = o.project3d(m, q, s, op, V, K, W, H)
+    _, oids = o.isect_tiles(pr.means2d, pr.radii, pr.depths, W, H)
+    agree = float((cnt.view(C, N) == 0).eq(~pr.valid).double().mean())
+    assert agree > 0.999, agree
+    assert abs(len(oids) - I) <= max(5, I // 2000)
+
+
+@pytest.mark.parametrize("N,W,H,extent,dup", [(12000, 48, 40, 0.02, 1), (12000, 48, 40, 0.02, 2),
+                                             (24000, 32, 32, 0.004, 2), (24000, 32, 32, 0.004, 3000)])
+def test_3d_binning_exact_long_lists(cuda, N, W, H, extent, dup):
+    """Lists of thousands of entries (the sample-partitioned group sort) and runs of `dup`
+    Gaussians sharing one mean (equal depths: ties in c*N+n order, across group borders)."""
+    p, V, K = _scene3d(N, W, H, 1, 23, extent=extent)
+    src = (torch.arange(N) // dup) * dup
+    p[:, 0:3] = p[src, 0:3]
+    b = _check_binning_exact(p, V, K, W, H, 1, cuda)
+    assert b.max_seg > 2048, b.max_seg
+
+
+def _check_binning_exact(p, V, K, W, H, C, cuda):
+    from gsr import render as R
     rgb, alpha, b, _ = R.debug_forward3d(p.to(cuda), V.to(cuda), K.to(cuda), torch.ones(3, device=cuda), W, H)
     N = p.shape[0]
     rect = b.rect.cpu().view(C * N, 2).to(torch.int64) & 0xFFFFFFFF
@@ -171,14 +198,7 @@ def test_3d_binning_exact(cuda):
     tile_of_j = (ids // N) * T + (y0[ids] + j // w) * tw + (x0[ids] + j % w)
     tiles_of_s = torch.searchsorted(exp_off, torch.arange(I), right=True) - 1
     assert torch.equal(tile_of_j, tiles_of_s)
-    # projection rects vs the oracle's (float decisions: near-total agreement)
-    o = _oracle3d()
-    m, q, s, col, op = o.activations3d(p)
-    pr = o.project3d(m, q, s, op, V, K, W, H)
-    _, oids = o.isect_tiles(pr.means2d, pr.radii, pr.depths, W, H)
-    agree = float((cnt.view(C, N) == 0).eq(~pr.valid).double().mean())
-    assert agree > 0.999, agree
-    assert abs(len(oids) - I) <= max(5, I // 2000)
+    return b
 
 
 def test_3d_cfg1_vs_oracle(cuda):
