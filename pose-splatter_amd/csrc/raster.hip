@@ -275,11 +275,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   if (end > start) {
     const int id0 = ids[min(start + 64 * wv + lane, e_last)];
     idn = ids[min(start + 256 + 64 * wv + lane, e_last)];
-#ifdef GSR_EXP_CONTIG
-    const Splat s0 = rec[min(start + 64 * wv + lane, e_last) >> 2]; (void)id0;
-#else
     const Splat s0 = rec[id0];
-#endif
     c0 = s0.p0; c1 = s0.p1; c2 = s0.p2;
   }
   int buf = 0;
@@ -299,11 +295,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
       if (lane == 0) s_qn[buf][wv] = __popcll(m);
       const int id_use = idn;
       idn = ids[min(rb + 512 + 64 * wv + lane, e_last)];
-#ifdef GSR_EXP_CONTIG
-      const Splat sn = rec[min(rb + 256 + 64 * wv + lane, e_last) >> 2]; (void)id_use;
-#else
       const Splat sn = rec[id_use];
-#endif
       c0 = sn.p0; c1 = sn.p1; c2 = sn.p2;
     }
     if (__syncthreads_count(!done) == 0) break;
@@ -741,11 +733,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wlast = max(wlast, __shfl_xor(wlast, o, 64));
   if (threadIdx.x < n) {
-#ifdef GSR_EXP_CONTIG
-    const Splat sp = rec[(b0 + threadIdx.x) >> 2];
-#else
     const Splat sp = rec[ids[b0 + threadIdx.x]];
-#endif
     s_p0[threadIdx.x] = sp.p0;
     s_p1[threadIdx.x] = sp.p1;
     s_p2[threadIdx.x] = sp.p2;
