@@ -2,6 +2,7 @@
 # On the GPU box: HBM traffic counters of the bench kernels, one rocprofv3 pass per counter
 # (FETCH_SIZE needs 3 TCC slots, WRITE_SIZE 2: they cannot share a pass), merged into one CSV
 # that bench.py reads for roofline.traffic.  Usage: tools/pmc_traffic.sh OUT.csv [bench args]
+# (OUT.csv under gpurun_out/ comes back from the GPU box; copy it to profiles/r01_pmc_counters.csv)
 set -e
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
