@@ -147,6 +147,17 @@ int gsr_bin_offsets(int32_t* tile_count, int64_t CT, int32_t* tile_offset,
 /* Workspace for gsr_bin_sort, bytes (depends on the I read back from stats). */
 size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT);
 
+/* Emit the (tile, key) pairs into the workspace (the first step of gsr_bin_sort), callable
+ * BEFORE the host has read stats back: the workspace layout depends only on
+ * workspace_bytes, and if this call's I (stats->n_isect, device) exceeds what the
+ * workspace holds, the kernel does nothing -- the caller then sizes a workspace from the
+ * read-back I and calls gsr_bin_sort with emitted = 0.  tile_count is consumed (counted
+ * down to zero) by an emit that ran. */
+int gsr_bin_emit(const float* depth, const uint32_t* rect, const int32_t* isect_offset,
+                 const int32_t* tile_offset, int32_t* tile_count, int C, int64_t N, int width,
+                 int height, int order, const gsr_bin_stats* stats, void* workspace,
+                 size_t workspace_bytes, void* stream);
+
 /* Emit (tile, key) pairs and sort each tile's list in LDS.  depth: gsr3d_project_fwd's
  * depth array (GSR_ORDER_DEPTH; may be null for GSR_ORDER_INDEX).  tile_count (the projection's
  * per-tile counts) is consumed: it is counted down to zero while slots are claimed.  Outputs:
@@ -156,12 +167,15 @@ size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT);
  *                   backward stores that entry's partial row.
  * Sort key per entry: (sort word << 32) | c*N+n, sort word = depth float bits (3D, order
  * GSR_ORDER_DEPTH) or c*N+n (2D, GSR_ORDER_INDEX).  max_seg, n_busy and the sort classes
- * n_sort_big / n_sort_mid (workgroup shapes by list length) come from stats. */
+ * n_sort_big / n_sort_mid (workgroup shapes by list length) come from stats (host copy).
+ * emitted != 0: gsr_bin_emit already ran on this workspace (same workspace_bytes) and I fit;
+ * otherwise the emit runs here.  stats: the device gsr_bin_stats. */
 int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_offset,
                  const int32_t* tile_offset, int32_t* tile_count,
                  const int32_t* busy_tiles, int C, int64_t N,
                  int width, int height, int order, int64_t n_isect, int32_t max_seg,
-                 int32_t n_busy, int32_t n_sort_big, int32_t n_sort_mid, void* workspace,
+                 int32_t n_busy, int32_t n_sort_big, int32_t n_sort_mid, int emitted,
+                 const gsr_bin_stats* stats, void* workspace,
                  size_t workspace_bytes, int32_t* sorted_ids, int32_t* k_of_s, void* stream);
 
 /* ---------------------------------------------------------------- (c) rasterisation */

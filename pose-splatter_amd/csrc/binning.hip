@@ -187,7 +187,11 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__
                                                       int th, int order, int use_lds,
                                                       const int32_t* __restrict__ tile_offset,
                                                       int32_t* __restrict__ tile_count, uint64_t* __restrict__ keys,
-                                                      int32_t* __restrict__ k_of_slot, int per_block) {
+                                                      int32_t* __restrict__ k_of_slot, int per_block,
+                                                      const gsr_bin_stats* __restrict__ stats, int64_t cap) {
+  // launched before the host has read I back (gsr_bin_emit): a workspace too small for this
+  // call's I makes every workgroup leave at once, and the host emits again with a larger one
+  if (stats->n_isect > cap) return;
   // Slots are claimed by counting each tile's count down to zero (slot = tile start +
   // remaining count - 1): no separate cursor array, and tile_count is left zeroed.
   extern __shared__ int hist[];
@@ -565,10 +569,56 @@ size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT) {
   return (size_t)(2 * n_isect * sizeof(uint64_t) + 3 * n_isect * sizeof(int32_t) + 256);
 }
 
+// The workspace layout is a function of its size only (capacity cap = entries it holds), so
+// gsr_bin_emit (before the host knows I) and gsr_bin_sort agree on it.
+static int64_t ws_cap(size_t workspace_bytes) {
+  return workspace_bytes > 256 ? (int64_t)((workspace_bytes - 256) / (2 * sizeof(uint64_t) + 3 * sizeof(int32_t))) : 0;
+}
+
+struct SortWs {
+  uint64_t* keys;
+  uint64_t* tmpk;
+  int32_t* tmpp0;
+  int32_t* tmpp1;
+  int32_t* k_of_slot;
+};
+
+static SortWs sort_ws(void* workspace, int64_t cap) {
+  SortWs w;
+  w.keys = (uint64_t*)workspace;
+  w.tmpk = w.keys + cap;
+  w.tmpp0 = (int32_t*)(w.tmpk + cap);
+  w.tmpp1 = w.tmpp0 + cap;
+  w.k_of_slot = w.tmpp1 + cap;
+  return w;
+}
+
+int gsr_bin_emit(const float* depth, const uint32_t* rect, const int32_t* isect_offset, const int32_t* tile_offset,
+                 int32_t* tile_count, int C, int64_t N, int width, int height, int order,
+                 const gsr_bin_stats* stats, void* workspace, size_t workspace_bytes, void* stream) {
+  GSR_REQUIRE(order == GSR_ORDER_DEPTH || order == GSR_ORDER_INDEX, "gsr_bin_emit: bad order %d", order);
+  GSR_REQUIRE(order == GSR_ORDER_INDEX || depth != nullptr, "gsr_bin_emit: depth order needs the depth array");
+  GSR_REQUIRE(C >= 1 && N >= 0 && (int64_t)C * N < (1ll << 31), "gsr_bin_emit: bad C=%d or N=%lld", C,
+              (long long)N);
+  GSR_REQUIRE(width > 0 && height > 0, "gsr_bin_emit: bad image %dx%d", width, height);
+  if (N == 0) return GSR_OK;
+  const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
+  const int64_t T = (int64_t)tw * th;
+  const int64_t cap = ws_cap(workspace_bytes);
+  const SortWs w = sort_ws(workspace, cap);
+  const int use_lds = T <= kHistMaxTiles;
+  dim3 grid(ceil_div(N, kEmitPerBlock), C);
+  hipLaunchKernelGGL(k_emit, grid, dim3(kEmitThreads), use_lds ? T * sizeof(int) : 0, (hipStream_t)stream, depth,
+                     (const uint2*)rect, isect_offset, N, tw, th, order, use_lds, tile_offset, tile_count, w.keys,
+                     w.k_of_slot, kEmitPerBlock, stats, cap);
+  GSR_LAUNCH_CHECK("k_emit");
+  return GSR_OK;
+}
+
 int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_offset, const int32_t* tile_offset,
                  int32_t* tile_count, const int32_t* busy_tiles, int C, int64_t N, int width, int height, int order, int64_t n_isect,
-                 int32_t max_seg, int32_t n_busy, int32_t n_big, int32_t n_mid, void* workspace,
-                 size_t workspace_bytes, int32_t* sorted_ids, int32_t* k_of_s, void* stream) {
+                 int32_t max_seg, int32_t n_busy, int32_t n_big, int32_t n_mid, int emitted, const gsr_bin_stats* stats,
+                 void* workspace, size_t workspace_bytes, int32_t* sorted_ids, int32_t* k_of_s, void* stream) {
   GSR_REQUIRE(order == GSR_ORDER_DEPTH || order == GSR_ORDER_INDEX, "gsr_bin_sort: bad order %d", order);
   GSR_REQUIRE(n_isect >= 0 && n_isect < (1ll << 31), "gsr_bin_sort: I=%lld out of range", (long long)n_isect);
   GSR_REQUIRE((int64_t)C * N < (1ll << 31), "gsr_bin_sort: C*N too large for 32-bit ids");
@@ -578,19 +628,17 @@ int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_
   GSR_REQUIRE(workspace_bytes >= gsr_bin_sort_workspace(n_isect, CT), "gsr_bin_sort: workspace too small");
   if (n_isect == 0 || N == 0) return GSR_OK;
   hipStream_t s = (hipStream_t)stream;
-  uint64_t* keys = (uint64_t*)workspace;
-  uint64_t* tmpk = keys + n_isect;
-  int32_t* tmpp0 = (int32_t*)(tmpk + n_isect);
-  int32_t* tmpp1 = tmpp0 + n_isect;
-  int32_t* k_of_slot = tmpp1 + n_isect;
-  const int use_lds = T <= kHistMaxTiles;
-  const int per_block = kEmitPerBlock;
-  dim3 grid(ceil_div(N, per_block), C);
-  GSR_REQUIRE(order == GSR_ORDER_INDEX || depth != nullptr, "gsr_bin_sort: depth order needs the depth array");
-  hipLaunchKernelGGL(k_emit, grid, dim3(kEmitThreads), use_lds ? T * sizeof(int) : 0, s, depth,
-                     (const uint2*)rect, isect_offset, N, tw, th, order, use_lds, tile_offset, tile_count, keys,
-                     k_of_slot, per_block);
-  GSR_LAUNCH_CHECK("k_emit");
+  const SortWs w = sort_ws(workspace, ws_cap(workspace_bytes));
+  uint64_t* keys = w.keys;
+  uint64_t* tmpk = w.tmpk;
+  int32_t* tmpp0 = w.tmpp0;
+  int32_t* tmpp1 = w.tmpp1;
+  int32_t* k_of_slot = w.k_of_slot;
+  if (!emitted) {
+    const int rc = gsr_bin_emit(depth, rect, isect_offset, tile_offset, tile_count, C, N, width, height, order, stats,
+                                workspace, workspace_bytes, stream);
+    if (rc != GSR_OK) return rc;
+  }
   GSR_REQUIRE(n_big >= 0 && n_mid >= 0 && n_big + n_mid <= n_busy, "gsr_bin_sort: bad sort classes %d/%d of %d",
               n_big, n_mid, n_busy);
   auto hist_bytes = [](int nt) { return (size_t)((nt / 64) * 256 + 64) * sizeof(int); };

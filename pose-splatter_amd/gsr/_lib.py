@@ -66,8 +66,9 @@ EXPORTS = {
     "gsr2d_project_fwd": (ctypes.c_int, [_P, _I64, _I64, _I32, _I32, _F, _P, _P, _P, _P, _P, _I32, _P]),
     "gsr_bin_offsets": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P, _P, _P]),
     "gsr_bin_sort_workspace": (_SZ, [_I64, _I64]),
+    "gsr_bin_emit": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I32, _P, _P, _SZ, _P]),
     "gsr_bin_sort": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I32, _I64, _I32,
-                                    _I32, _I32, _I32, _P, _SZ, _P, _P, _P]),
+                                    _I32, _I32, _I32, _I32, _P, _P, _SZ, _P, _P, _P]),
     "gsr3d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _I32, _P, _P, _P,
                                         _P, _P, _P, _P, _P, _P, _P]),
     "gsr3d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P,

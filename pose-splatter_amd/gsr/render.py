@@ -133,9 +133,9 @@ _I32, _I64, _F32 = torch.int32, torch.int64, torch.float32
 _VIEWS = {"rec": ("pre", _F32), "depth": ("pre", _F32), "rect": ("pre", _I32), "cnt": ("pre", _I32),
           "isect_off": ("pre", _I32), "tile_off": ("pre", _I32), "busy": ("pre", _I32),
           "chunk_base": ("pre", _I32), "stats_dev": ("pre", _I32),
-          "sorted_ids": ("post", _I32), "k_of_s": ("post", _I32), "final_T": ("post", _F32),
-          "last": ("post", _I32), "tile_end": ("pre", _I32), "tile_cut": ("pre", _I64),
-          "chunk_state": ("post", _F32), "chunk_list": ("post", _I32)}
+          "sorted_ids": ("post", _I32), "k_of_s": ("post", _I32), "final_T": ("pre", _F32),
+          "last": ("pre", _I32), "tile_end": ("pre", _I32), "tile_cut": ("pre", _I64),
+          "chunk_state": ("chunks", _F32), "chunk_list": ("chunks", _I32)}
 
 _pinned = {}
 _size_hint = {}   # (device, C, N, W, H) -> (I, n_chunks) of the last forward of that shape
@@ -181,11 +181,13 @@ class _Bins:
             "rec": CN * 48, "depth": CN * 4, "rect": CN * 8, "cnt": CN * 4,
             "isect_off": CN * 4, "tile_off": (self.CT + 1) * 4, "busy": self.CT * 4,
             "chunk_base": (self.CT + 1) * 4, "tile_end": self.CT * 4, "tile_cut": self.CT * 8,
-            "stats_dev": 32})
+            "stats_dev": 32, "final_T": C * width * height * 8, "last": C * width * height * 4})
         self.p = dict(self.pre.ptr)
         self.tc = _tile_counts(device, self.CT)
         self.p["tile_cnt"] = self.tc[0].data_ptr()
-        self.post = None
+        self.post = self.chunks = None
+        self.post_cap = self.chunk_cap = 0
+        self.emitted = False
         self.n_chunks = self.n_isect = self.max_seg = self.n_busy = 0
         self.key = (str(device), C, N, width, height)
 
@@ -195,11 +197,14 @@ class _Bins:
         return int(z)
 
     def guess_post(self, with_chunks: bool):
-        """Before the stats readback: size the per-intersection arena from the last call with
-        the same shapes (plus 25 %), so its allocation overlaps the GPU's projection/scan."""
+        """Before the stats readback: size the per-intersection and per-chunk arenas from the
+        last call with the same shapes (plus 25 %), so their allocation overlaps the GPU's
+        projection/scan and the emit can be enqueued before the readback (emit_early)."""
         hint = _size_hint.get(self.key)
         if hint is not None:
-            self.alloc_post(with_chunks, int(hint[0] * 1.25) + 1024, int(hint[1] * 1.25) + 16)
+            self.alloc_post(int(hint[0] * 1.25) + 1024)
+            if with_chunks:
+                self.alloc_chunks(int(hint[1] * 1.25) + 16)
 
     def __getattr__(self, name):
         # typed views of arena buffers (not used on the hot path)
@@ -211,41 +216,69 @@ class _Bins:
         raise AttributeError(name)
 
     def offsets(self, stream):
+        """Tile scan, then the one host sync of the forward: the 32-byte stats readback."""
+        self.offsets_launch(stream)
+        self.offsets_wait()
+
+    def offsets_launch(self, stream):
         L = lib()
         p = self.p
         with _timed("bin_offsets"):
           check(L.gsr_bin_offsets(p["tile_cnt"], self.CT, p["tile_off"], p["chunk_base"], p["busy"], p["tile_end"],
                                 p["tile_cut"], p["stats_dev"], stream), "gsr_bin_offsets")
-        host = _pinned_stats(self.device)
-        host.copy_(self.pre.view("stats_dev", _I32), non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
+        self._host = _pinned_stats(self.device)
+        self._host.copy_(self.pre.view("stats_dev", _I32), non_blocking=True)
+        self._ev = torch.cuda.Event()
+        self._ev.record()
+
+    def emit_early(self, order, stream):
+        """Enqueue the emit into the speculative arena before the readback: the GPU runs it
+        while the host waits; if this call's I does not fit, the kernel does nothing and
+        sort() emits again into an arena sized from the readback."""
+        if self.post is None:
+            return
+        L = lib()
+        p = self.p
+        check(L.gsr_bin_emit(p["depth"] if order == _lib.ORDER_DEPTH else None, p["rect"], p["isect_off"],
+                             p["tile_off"], p["tile_cnt"], self.C, self.N, self.W, self.H, order, p["stats_dev"],
+                             p["sort_ws"], self.post.off["sort_ws"][1], stream), "gsr_bin_emit")
+        self.emitted = True
+
+    def offsets_wait(self):
+        ev = self._ev
         while not ev.query():   # the one host sync of the forward (spin: lowest wake-up latency)
             pass
-        st = host.tolist()
+        st = self._host.tolist()
         self.n_isect = (st[0] & 0xFFFFFFFF) | (st[1] << 32)
         self.max_seg, self.n_busy, self.n_chunks = st[2], st[3], st[4]
         self.n_sort_big, self.n_sort_mid = st[6], st[7]
         if self.n_isect >= 2 ** 31:
             raise RuntimeError(f"gsr: {self.n_isect} intersections exceed the 32-bit index range")
 
-    def alloc_post(self, with_chunks: bool, n_isect: int, n_chunks: int):
+    def alloc_post(self, n_isect: int):
         L = lib()
         I = max(n_isect, 1)
-        P = self.C * self.W * self.H
-        K = max(n_chunks, 1) if with_chunks else 1
         self.post = _Arena(self.device, {
-            "sorted_ids": I * 4, "k_of_s": I * 4, "sort_ws": int(L.gsr_bin_sort_workspace(I, self.CT)),
-            "final_T": P * 8, "last": P * 4,
-            "chunk_state": K * 256 * 16, "chunk_list": K * 16})
-        self.post_cap = (I, K)
+            "sorted_ids": I * 4, "k_of_s": I * 4, "sort_ws": int(L.gsr_bin_sort_workspace(I, self.CT))})
+        self.post_cap = I
         self.p.update(self.post.ptr)
 
+    def alloc_chunks(self, n_chunks: int):
+        K = max(n_chunks, 1)
+        self.chunks = _Arena(self.device, {"chunk_state": K * 256 * 16, "chunk_list": K * 16})
+        self.chunk_cap = K
+        self.p.update(self.chunks.ptr)
+
     def ensure_post(self, with_chunks: bool):
-        """After the stats readback: keep the speculatively sized arena if it is big enough."""
-        I, K = self.post_cap if self.post is not None else (0, 0)
-        if self.n_isect > I or (with_chunks and self.n_chunks > K):
-            self.alloc_post(with_chunks, int(self.n_isect * 1.25), int(self.n_chunks * 1.25))
+        """After the stats readback: keep the speculatively sized arenas if they are big enough
+        (an emit_early into a too-small arena did nothing; sort() then emits)."""
+        if self.post is None or self.n_isect > self.post_cap:
+            self.alloc_post(int(self.n_isect * 1.25))
+            self.emitted = False
+        if with_chunks and (self.chunks is None or self.n_chunks > self.chunk_cap):
+            self.alloc_chunks(int(self.n_chunks * 1.25))
+        elif self.chunks is None:
+            self.alloc_chunks(1)
         _size_hint[self.key] = (self.n_isect, self.n_chunks)
 
     def sort(self, order, stream):
@@ -255,7 +288,7 @@ class _Bins:
           check(L.gsr_bin_sort(p["depth"] if order == _lib.ORDER_DEPTH else None, p["rect"], p["isect_off"], p["tile_off"], p["tile_cnt"], p["busy"],
                              self.C, self.N,
                              self.W, self.H, order, self.n_isect, self.max_seg, self.n_busy, self.n_sort_big,
-                             self.n_sort_mid, p["sort_ws"],
+                             self.n_sort_mid, int(self.emitted), p["stats_dev"], p["sort_ws"],
                              self.post.off["sort_ws"][1], p["sorted_ids"], p["k_of_s"], stream), "gsr_bin_sort")
         self.tc[1] = True   # offsets reset the counter, the emit counted every tile back to 0
 
@@ -324,7 +357,9 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
                               q["rect"], q["cnt"], q["isect_off"], q["tile_cnt"], b.take_tile_counts(), stream),
           "gsr3d_project_fwd")
     b.guess_post(with_chunks=True)
-    b.offsets(stream)
+    b.offsets_launch(stream)
+    b.emit_early(_lib.ORDER_DEPTH, stream)
+    b.offsets_wait()
     b.ensure_post(with_chunks=True)
     b.sort(_lib.ORDER_DEPTH, stream)
     rgb = torch.empty(C, height, width, 3, device=dev, dtype=torch.float32)
@@ -352,7 +387,9 @@ def _forward2d(params, bg, width, height, eps_cut):
                               q["cnt"], q["isect_off"], q["tile_cnt"], b.take_tile_counts(), stream),
           "gsr2d_project_fwd")
     b.guess_post(with_chunks=True)
-    b.offsets(stream)
+    b.offsets_launch(stream)
+    b.emit_early(_lib.ORDER_INDEX, stream)
+    b.offsets_wait()
     b.ensure_post(with_chunks=True)
     b.sort(_lib.ORDER_INDEX, stream)
     rgb = torch.empty(height, width, 3, device=dev, dtype=torch.float32)

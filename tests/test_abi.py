@@ -54,7 +54,7 @@ def test_invalid_arguments_are_reported_not_launched():
     assert rc == -1 and b"radius_mode" in lib.gsr_last_error()
     rc = lib.gsr2d_project_fwd(None, 10, 9, 64, 64, 2.0, None, None, None, None, None, 0, None)
     assert rc == -1 and b"eps_cut" in lib.gsr_last_error()
-    rc = lib.gsr_bin_sort(None, None, None, None, None, None, 1, 10, 64, 64, 5, 0, 0, 0, 0, 0, None, 0, None, None,
+    rc = lib.gsr_bin_sort(None, None, None, None, None, None, 1, 10, 64, 64, 5, 0, 0, 0, 0, 0, 0, None, None, 0, None, None,
                           None)
     assert rc == -1 and b"bad order" in lib.gsr_last_error()
     with pytest.raises(ValueError, match="bad order"):

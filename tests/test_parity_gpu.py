@@ -254,6 +254,28 @@ def test_3d_edge_cases(cuda):
     assert float(a_g.abs().max()) == 0.0 and float(g_g.abs().max()) == 0.0
 
 
+def test_3d_speculative_arena_regrow(cuda):
+    """The emit is enqueued before the stats readback into an arena sized from the previous
+    call of the same shapes; when this call's I does not fit, that emit must do nothing and
+    the sort emits again: results equal a render with no size hint at all."""
+    from gsr import render as R
+    W, H, C = 96, 80, 2
+    small, V, K = _scene3d(3000, W, H, C, 61, scale_shift=-2.0)
+    big, _, _ = _scene3d(3000, W, H, C, 61, scale_shift=1.0)
+    bg = torch.ones(3)
+    vr, va = _cot(C, H, W, 62)
+    R._size_hint.clear()
+    _run_gpu3d(small, V, K, W, H, bg, cuda, vr, va)
+    i_small = R.last_stats()["n_isect"]
+    rgb1, a1, g1 = _run_gpu3d(big, V, K, W, H, bg, cuda, vr, va)
+    assert R.last_stats()["n_isect"] > 1.25 * i_small + 1024   # beyond the speculative arena
+    R._size_hint.clear()
+    rgb2, a2, g2 = _run_gpu3d(big, V, K, W, H, bg, cuda, vr, va)
+    assert torch.equal(rgb1, rgb2) and torch.equal(a1, a2) and torch.equal(g1, g2)
+    rgb3, a3, g3 = _run_gpu3d(big, V, K, W, H, bg, cuda, vr, va)   # hint now fits: early emit
+    assert torch.equal(rgb1, rgb3) and torch.equal(a1, a3) and torch.equal(g1, g3)
+
+
 def test_3d_long_tile_lists(cuda):
     """> 16384 entries in one tile list: exercises the run-sort + global merge path."""
     W, H = 32, 32
