@@ -1,36 +1,60 @@
-"""Host-side latency of the forward's readback path (GPU box): the wait for the stats,
-the host time from the wait to the sort call, and the sort call itself."""
-import os, sys, time
-sys.path.insert(0, "pose-splatter_amd")
-import torch
-from gsr import render as R
-from gsr.scenes import CONFIGS, gaussians3d, ring_cameras
-cfg = CONFIGS[3]
+"""Host-side timeline of one fwd+bwd step (GPU box): host time (us) of each library call
+relative to the end of the forward's stats readback, medians over steps.  If the host
+reaches a launch later than the GPU finishes the previous kernel, the GPU idles."""
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "pose-splatter_amd"))
+import torch  # noqa: E402
+from gsr import render as R  # noqa: E402
+from gsr._lib import lib  # noqa: E402
+from gsr.scenes import CONFIGS, gaussians3d, ring_cameras  # noqa: E402
+
+cfg = CONFIGS[int(sys.argv[1]) if len(sys.argv) > 1 else 3]
 dev = torch.device("cuda:0")
 p = gaussians3d(cfg.N, cfg.seed).to(dev).requires_grad_(True)
 V, K = ring_cameras(cfg.views, cfg.width, cfg.height)
 V, K = V.to(dev), K.to(dev)
 bg = torch.ones(3, device=dev)
-T = {}
-orig_off, orig_sort = R._Bins.offsets_wait, R._Bins.sort
-def off(self):
-    T.setdefault("off_enter", []).append(time.perf_counter_ns())
-    orig_off(self)
-    T.setdefault("off_exit", []).append(time.perf_counter_ns())
-def sort(self, o, s):
-    T.setdefault("sort_enter", []).append(time.perf_counter_ns())
-    orig_sort(self, o, s)
-    T.setdefault("sort_exit", []).append(time.perf_counter_ns())
-R._Bins.offsets_wait, R._Bins.sort = off, sort
+marks = []
+L = lib()
+for name in ["gsr3d_project_fwd", "gsr_bin_offsets", "gsr_bin_emit", "gsr_bin_sort", "gsr3d_raster_fwd",
+             "gsr3d_raster_bwd", "gsr3d_project_bwd"]:
+    f = getattr(L, name)
+
+    def wrap(*a, _f=f, _n=name):
+        marks.append((_n, time.perf_counter_ns()))
+        return _f(*a)
+    setattr(L, name, wrap)
+orig_wait = R._Bins.offsets_wait
+
+
+def wait(self):
+    marks.append(("wait_begin", time.perf_counter_ns()))
+    orig_wait(self)
+    marks.append(("wait_end", time.perf_counter_ns()))
+
+
+R._Bins.offsets_wait = wait
 vr = torch.randn(cfg.views, cfg.height, cfg.width, 3, device=dev)
 va = torch.randn(cfg.views, cfg.height, cfg.width, device=dev)
-for i in range(30):
+steps = []
+for i in range(40):
+    marks.clear()
+    params_grad = None
+    p.grad = None
     rgb, alpha = R.render3d(p, V, K, cfg.width, cfg.height, bg)
     torch.autograd.backward([rgb, alpha], [vr, va])
+    marks.append(("step_end", time.perf_counter_ns()))
+    steps.append(list(marks))
 torch.cuda.synchronize()
-import statistics
-n = len(T["off_exit"])
-d1 = [(T["sort_enter"][i] - T["off_exit"][i]) / 1e3 for i in range(10, n)]
-d2 = [(T["sort_exit"][i] - T["sort_enter"][i]) / 1e3 for i in range(10, n)]
-d3 = [(T["off_exit"][i] - T["off_enter"][i]) / 1e3 for i in range(10, n)]
-print("readback wait us", statistics.median(d3), "off_exit->sort_enter us", statistics.median(d1), "sort call us", statistics.median(d2))
+ref = "wait_end"
+names = [n for n, _ in steps[-1]]
+for n in names:
+    vals = []
+    for s in steps[10:]:
+        d = dict(s)
+        vals.append((d[n] - d[ref]) / 1e3)
+    print(f"{n:22s} {statistics.median(vals):9.1f} us")
