@@ -1,0 +1,167 @@
+"""BASELINE.json's full sizes on the GPU (configs 3, 4 and 5), where the small-case oracle
+tests of test_parity_gpu.py cannot reach.
+
+* config 3 (3D, 200k, 576x512, 6 views): one whole view fwd+bwd against the CPU oracle
+  (oracle/oracle3d.py, ~10 s on 16 host threads), same tolerances as config 1 in
+  test_parity_gpu.py plus the 0.05 dB PSNR bar of BASELINE.json's north_star.
+* config 5 (3D, 2M, 1152x1024, 6 views): the oracle restricted to three central tile rows
+  (oracle3d.isect_tiles' ``band``; the rest of the image is the same computation at other
+  tiles), fwd in those rows and the gradient of a cotangent supported on them.
+* both: the tile lists bit-exact against an independent stable sort (torch.sort on the
+  device) of the (camera*tiles + tile, depth bits) keys the GPU's own projection implies
+  (2.6 M and 25 M entries), and size-independent properties: bitwise determinism, batch view
+  c == the single-view render of camera c, and linearity of the backward in the cotangent
+  (a power-of-two scale commutes exactly with every fp32 operation of the backward).
+* config 4 (2D, 500k, 576x512): determinism and cotangent linearity (the dense reference
+  compositor is O(N x pixels) on the CPU, so its parity is covered by the small golden and
+  oracle cases).
+"""
+import pytest
+import torch
+
+from _util import assert_close, grad_close
+
+pytestmark = pytest.mark.gpu
+
+
+def _scene(idx):
+    from gsr.scenes import CONFIGS, gaussians3d, ring_cameras
+    c = CONFIGS[idx]
+    return c, gaussians3d(c.N, c.seed), *ring_cameras(c.views, c.width, c.height)
+
+
+def _cot(C, H, W, seed, dev):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(C, H, W, 3, generator=g).to(dev), torch.randn(C, H, W, generator=g).to(dev)
+
+
+def _gpu3d(p, V, K, W, H, dev, v_rgb=None, v_alpha=None):
+    from gsr import render as R
+    pg = p.to(dev).requires_grad_(v_rgb is not None)
+    rgb, alpha = R.render3d(pg, V.to(dev), K.to(dev), W, H, torch.ones(3, device=dev))
+    grad = None
+    if v_rgb is not None:
+        torch.autograd.backward([rgb, alpha], [v_rgb, v_alpha])
+        grad = pg.grad.detach()
+    return rgb.detach(), alpha.detach(), grad
+
+
+def _check_lists_vs_torch_sort(p, V, K, W, H, C, dev):
+    """Tile lists (ids + offsets) == a stable device sort of the keys implied by the GPU's own
+    rects and depths (emission order = flatten id c*N+n, so ties keep that order)."""
+    from gsr import render as R
+    _, _, b, _ = R.debug_forward3d(p.to(dev), V.to(dev), K.to(dev), torch.ones(3, device=dev), W, H)
+    N = p.shape[0]
+    tw, th = (W + 15) // 16, (H + 15) // 16
+    T = tw * th
+    rect = b.rect.view(C * N, 2).to(torch.int64) & 0xFFFFFFFF
+    x0, x1 = rect[:, 0] & 0xFFFF, rect[:, 0] >> 16
+    y0, y1 = rect[:, 1] & 0xFFFF, rect[:, 1] >> 16
+    cnt = b.cnt[:C * N].to(torch.int64)
+    assert torch.equal(cnt, (x1 - x0) * (y1 - y0))
+    I = int(cnt.sum())
+    assert I == b.n_isect
+    owner = torch.repeat_interleave(torch.arange(C * N, device=dev), cnt)
+    local = torch.arange(I, device=dev) - (torch.cumsum(cnt, 0) - cnt)[owner]
+    w = (x1 - x0)[owner]
+    tile = (owner // N) * T + (y0[owner] + local // w) * tw + (x0[owner] + local % w)
+    dbits = b.depth[:C * N].contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    order = torch.sort((tile << 32) | dbits[owner], stable=True).indices
+    assert torch.equal(b.sorted_ids[:I].to(torch.int64), owner[order])
+    off = torch.zeros(C * T + 1, dtype=torch.int64, device=dev)
+    off[1:] = torch.cumsum(torch.bincount(tile, minlength=C * T), 0)
+    assert torch.equal(b.tile_off.to(torch.int64), off)
+    ks = b.k_of_s[:I].to(torch.int64)
+    assert torch.equal(torch.sort(ks).values, torch.arange(I, device=dev))
+    return I, int(b.max_seg)
+
+
+def _properties3d(c, p, V, K, dev):
+    W, H, C = c.width, c.height, c.views
+    vr, va = _cot(C, H, W, 77, dev)
+    r1 = _gpu3d(p, V, K, W, H, dev, vr, va)
+    r2 = _gpu3d(p, V, K, W, H, dev, vr, va)
+    for a, b in zip(r1, r2):
+        assert torch.equal(a, b), "not deterministic"
+    r4 = _gpu3d(p, V, K, W, H, dev, 4.0 * vr, 4.0 * va)
+    assert torch.equal(r4[2], 4.0 * r1[2]), "backward not linear in the cotangent"
+    for v in (0, C - 1):
+        rgb, alpha, _ = _gpu3d(p, V[v:v + 1], K[v:v + 1], W, H, dev)
+        assert torch.equal(rgb[0], r1[0][v]) and torch.equal(alpha[0], r1[1][v]), v
+    return r1
+
+
+def test_cfg3_view_vs_oracle(cuda):
+    from oracle.oracle3d import render3d
+    c, p, V, K = _scene(3)
+    W, H = c.width, c.height
+    vr, va = _cot(1, H, W, 5, "cpu")
+    rgb_g, a_g, g_g = _gpu3d(p, V[:1], K[:1], W, H, cuda, vr.to(cuda), va.to(cuda))
+    po = p.clone().requires_grad_(True)
+    rgb_o, a_o, = render3d(po, V[:1], K[:1], W, H, torch.ones(3))
+    torch.autograd.backward([rgb_o, a_o], [vr, va])
+    r = assert_close(rgb_g.cpu(), rgb_o.detach(), max_frac=2e-4, max_outlier=0.02, what="rgb")
+    assert_close(a_g.cpu(), a_o.detach(), max_frac=2e-4, max_outlier=0.02, what="alpha")
+    grad_close(g_g.cpu(), po.grad, max_frac=2e-3, what="grad")
+    tgt = (rgb_o.detach() + 0.05 * torch.randn(rgb_o.shape, generator=torch.Generator().manual_seed(1))).clamp(0, 1)
+    psnr = lambda x: float(10 * torch.log10(1.0 / ((x - tgt) ** 2).mean()))
+    assert abs(psnr(rgb_g.cpu()) - psnr(rgb_o.detach())) < 0.05, r
+
+
+def test_cfg3_lists_and_properties(cuda):
+    c, p, V, K = _scene(3)
+    I, max_seg = _check_lists_vs_torch_sort(p, V, K, c.width, c.height, c.views, cuda)
+    assert I > 2_000_000 and max_seg > 8192, (I, max_seg)   # long lists: the partitioned sort
+    _properties3d(c, p, V, K, cuda)
+
+
+def test_cfg5_band_vs_oracle(cuda):
+    """Three central tile rows of view 0 at 2M Gaussians / 1152x1024 against the oracle."""
+    from oracle.oracle3d import render3d
+    c, p, V, K = _scene(5)
+    W, H = c.width, c.height
+    row = (H // 16) // 2 - 1
+    y0, y1 = 16 * row, 16 * row + 48
+    vr, va = _cot(1, H, W, 6, "cpu")
+    band = torch.zeros(1, H, W)
+    band[:, y0:y1] = 1.0
+    vr, va = vr * band[..., None], va * band
+    rgb_g, a_g, g_g = _gpu3d(p, V[:1], K[:1], W, H, cuda, vr.to(cuda), va.to(cuda))
+    po = p.clone().requires_grad_(True)
+    rgb_o, a_o = render3d(po, V[:1], K[:1], W, H, torch.ones(3), band=(row, row + 3))
+    torch.autograd.backward([rgb_o, a_o], [vr, va])
+    assert_close(rgb_g.cpu()[:, y0:y1], rgb_o.detach()[:, y0:y1], max_frac=2e-4, max_outlier=0.02, what="rgb")
+    assert_close(a_g.cpu()[:, y0:y1], a_o.detach()[:, y0:y1], max_frac=2e-4, max_outlier=0.02, what="alpha")
+    grad_close(g_g.cpu(), po.grad, max_frac=2e-3, what="grad")
+    assert float(po.grad.abs().max()) > 0
+
+
+def test_cfg5_lists_and_properties(cuda):
+    c, p, V, K = _scene(5)
+    I, max_seg = _check_lists_vs_torch_sort(p, V, K, c.width, c.height, c.views, cuda)
+    assert I > 20_000_000 and max_seg > 16384, (I, max_seg)
+    _properties3d(c, p, V, K, cuda)
+
+
+def test_cfg4_2d_properties(cuda):
+    from gsr import render as R
+    from gsr.scenes import CONFIGS, gaussians2d
+    c = CONFIGS[4]
+    W, H = c.width, c.height
+    p = gaussians2d(c.N, W, H, c.seed).to(cuda)
+    g = torch.Generator().manual_seed(9)
+    vr = torch.randn(H, W, 3, generator=g).to(cuda)
+    va = torch.randn(H, W, generator=g).to(cuda)
+    bg = torch.ones(3, device=cuda)
+
+    def run(s):
+        pg = p.clone().requires_grad_(True)
+        rgb, alpha = R.render2d(pg, W, H, bg)
+        torch.autograd.backward([rgb, alpha], [s * vr, s * va])
+        return rgb.detach(), alpha.detach(), pg.grad.detach()
+
+    r1, r2, r4 = run(1.0), run(1.0), run(4.0)
+    for a, b in zip(r1, r2):
+        assert torch.equal(a, b), "not deterministic"
+    assert torch.equal(r4[2], 4.0 * r1[2])
+    assert float(r1[1].max()) > 0.5 and float(r1[2].abs().max()) > 0
