@@ -35,6 +35,9 @@ import torch  # noqa: E402
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # PMC counter run of the same bench command (FETCH_SIZE and WRITE_SIZE passes), committed
 DEFAULT_TRAFFIC_CSV = os.path.join(ROOT, "profiles", "r01_pmc_counters.csv")
+# SQ counter passes (tools/pmc_sq.sh) for the dominant kernel's VALU occupancy
+DEFAULT_SQ_CSVS = [os.path.join(ROOT, "profiles", f"r01_v16_pmc_sq_p{i}.csv") for i in (1, 2)]
+N_SIMDS = 256 * 4   # MI355X: 256 CUs x 4 SIMDs
 
 
 def parse():
@@ -106,6 +109,30 @@ def traffic_from_csv(path: str, kernel_substr: str):
     f = 2.0 * 1024.0 * (sum(fetch) / max(len(fetch), 1))
     w = 1024.0 * (sum(write) / max(len(write), 1))
     return f + w
+
+
+def valu_from_csv(paths, kernel_substr: str):
+    """VALU occupancy of one kernel from rocprofv3 SQ passes: SQ_ACTIVE_INST_VALU (quad-cycles,
+    summed over SIMDs) x 4 over N_SIMDS x the kernel's cycles (GRBM_GUI_ACTIVE / 8 XCDs), and
+    the issue-slot fraction SQ_INSTS_VALU x 4 cycles (a full-rate wave64 fp32 op on a 16-lane
+    SIMD) over the same SIMD-cycles.  None when the passes are missing."""
+    import csv
+    acc = {}
+    for path in paths:
+        if not os.path.exists(path):
+            return None
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if kernel_substr in row.get("Kernel_Name", ""):
+                    acc.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+    need = ("SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE")
+    if not all(k in acc for k in need):
+        return None
+    mean = {k: sum(v) / len(v) for k, v in acc.items()}
+    simd_cycles = N_SIMDS * mean["GRBM_GUI_ACTIVE"] / 8.0
+    return {"active_frac": 4.0 * mean["SQ_ACTIVE_INST_VALU"] / simd_cycles,
+            "issue_frac": 4.0 * mean["SQ_INSTS_VALU"] / simd_cycles,
+            "insts_per_launch": mean["SQ_INSTS_VALU"], "source": "profiles/r01_v16_pmc_sq_p{1,2}.csv"}
 
 
 def cpu_baseline(cfg, params, V, K, views: int):
@@ -317,6 +344,7 @@ def main():
     traffic = None
     if args.traffic_csv and dom_name and os.path.exists(args.traffic_csv):
         traffic = traffic_from_csv(args.traffic_csv, KERNEL_SYMBOL.get(dom_name, "k_" + dom_name))
+    valu = valu_from_csv(DEFAULT_SQ_CSVS, KERNEL_SYMBOL.get(dom_name, "k_" + dom_name)) if dom_name else None
     sb = step_bytes(Cd, cfg.N, cfg.width * cfg.height, I, I_eff, p_dim, cfg.backward) * (1 if cfg.mode == "3d" else C)
 
     out = {
@@ -339,7 +367,7 @@ def main():
                                    f"view-sharded x{world} + RCCL all-reduce of v_params" if world > 1 else "single GPU")},
         "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "algorithmic_bytes": alg, "avg_ms": dom_ms, "launches": dom_n},
+                     "algorithmic_bytes": alg, "avg_ms": dom_ms, "launches": dom_n, "valu": valu},
         "kernels_ms": {k: round(v[0], 4) for k, v in sorted(breakdown.items())},
         "allreduce_ms": allreduce_ms,
         "sets_per_s": value / C,
