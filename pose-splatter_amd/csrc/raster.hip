@@ -791,12 +791,15 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
       const float alpha = IS2D ? raw : fminf(kAlphaMax, raw);
       const bool valid = IS2D ? (b0 + k) <= last && alpha >= cut2d
                               : (b0 + k) <= last && sigma >= 0.f && alpha >= kAlphaThreshold;
-      const float ra = valid ? __builtin_amdgcn_rcpf(1.f - alpha) : 1.f;
+      // 3D: an invalid pair enters with alpha 0, so ra = rcp(1) = 1 and fac = 0 exactly
+      // without a select each
+      const float alpha_v = valid ? alpha : 0.f;
+      const float ra = IS2D ? (valid ? __builtin_amdgcn_rcpf(1.f - alpha) : 1.f) : __builtin_amdgcn_rcpf(1.f - alpha_v);
       if (IS2D)
         T = valid && (b0 + k) == last ? Tl : T * ra;
       else
         T *= ra;
-      const float fac = valid ? alpha * T : 0.f;
+      const float fac = IS2D ? (valid ? alpha * T : 0.f) : alpha_v * T;
       acc[g * kPartial + 6] = fac * vr;
       acc[g * kPartial + 7] = fac * vg;
       acc[g * kPartial + 8] = fac * vb;
