@@ -124,6 +124,10 @@ __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
         rx = r;
         ry = r;
         if (r <= radius_clip) ok = false;
+        // alpha <= opacity < 1/255 everywhere: every pair is skipped by the compositor, so the
+        // cull is exact, and it keeps opacity == 0 (sigmoid underflow) out of the backward's
+        // dL/dopacity = -v / opacity
+        if (a.op < kAlphaThreshold) ok = false;
       }
     }
     if (ok) {

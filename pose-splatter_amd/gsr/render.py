@@ -149,16 +149,17 @@ def _pinned_stats(device) -> torch.Tensor:
     return t
 
 
-# Per (device, tile count): the projection's tile histogram + emission counter, shared by
-# successive calls.  project -> offsets -> sort leaves it all zero (the emit counts each tile
-# down, the offsets kernel resets the counter), so the next projection skips its memset; a
-# call that stops in between leaves the flag False and the next one clears it.  Calls on one
-# device are stream-ordered (one library stream per device), so no two pipelines overlap.
+# Per (device, tile count, stream): the projection's tile histogram + emission counter, shared
+# by successive calls ON ONE STREAM.  project -> offsets -> sort leaves it all zero (the emit
+# counts each tile down, the offsets kernel resets the counter), so the next projection skips
+# its memset; a call that stops in between leaves the flag False and the next one clears it.
+# Keying by stream keeps renders on different streams (or threads) from sharing a buffer:
+# calls on one stream are ordered, so no two pipelines overlap on the same counts.
 _tc_cache = {}
 
 
-def _tile_counts(device, CT: int) -> list:
-    key = (str(device), CT)
+def _tile_counts(device, CT: int, stream: int) -> list:
+    key = (str(device), CT, stream)
     e = _tc_cache.get(key)
     if e is None:
         e = _tc_cache[key] = [torch.empty(CT + 1, device=device, dtype=torch.int32), False]
@@ -183,7 +184,7 @@ class _Bins:
             "chunk_base": (self.CT + 1) * 4, "tile_end": self.CT * 4, "tile_cut": self.CT * 8,
             "stats_dev": 32, "final_T": C * width * height * 8, "last": C * width * height * 4})
         self.p = dict(self.pre.ptr)
-        self.tc = _tile_counts(device, self.CT)
+        self.tc = _tile_counts(device, self.CT, _stream(device))
         self.p["tile_cnt"] = self.tc[0].data_ptr()
         self.post = self.chunks = None
         self.post_cap = self.chunk_cap = 0

@@ -67,7 +67,7 @@ def test_carve_vs_oracle(cuda, C, n, angle, seed):
     assert float(occ_diff.float().mean()) <= 1e-3, int(occ_diff.sum())
     assert float(ref[0].gt(0).float().mean()) > 0.001          # the scene carves something
     same = ~occ_diff
-    assert_close(out[1:][:, same], ref[1:][:, same], rtol=1e-5, atol=1e-6, max_frac=1e-3, what="colours")
+    assert_close(out[1:][:, same], ref[1:][:, same], rtol=1e-5, atol=1e-6, max_frac=1e-3, max_outlier=1.0, what="colours")
 
 
 @pytest.mark.gpu

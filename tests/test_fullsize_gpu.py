@@ -1,4 +1,4 @@
-"""BASELINE.json's full sizes on the GPU (configs 3, 4 and 5), where the small-case oracle
+"""BASELINE.json's full sizes on the GPU (configs 2, 3, 4 and 5), where the small-case oracle
 tests of test_parity_gpu.py cannot reach.
 
 * config 3 (3D, 200k, 576x512, 6 views): one whole view fwd+bwd against the CPU oracle
@@ -12,9 +12,14 @@ tests of test_parity_gpu.py cannot reach.
   (2.6 M and 25 M entries), and size-independent properties: bitwise determinism, batch view
   c == the single-view render of camera c, and linearity of the backward in the cotangent
   (a power-of-two scale commutes exactly with every fp32 operation of the backward).
-* config 4 (2D, 500k, 576x512): determinism and cotangent linearity (the dense reference
-  compositor is O(N x pixels) on the CPU, so its parity is covered by the small golden and
-  oracle cases).
+* config 2 (3D, 50k, 288x256, 1 view, fwd-only): the whole view against the oracle, plus the
+  gradient of a random cotangent (the backward is not part of config 2's timed step, but the
+  scene is cheap enough to check it too).
+* config 4 (2D, 500k, 576x512): determinism and cotangent linearity, and two 16x128-pixel
+  windows of the full-density scene (about 1.7 Gaussians per pixel, where the binning's
+  eps-extent cut drops many sub-1e-8 contributions) against the dense reference compositor
+  (oracle2d) over every Gaussian that can reach the window, with a window-supported
+  cotangent; Gaussians outside that set must get exactly zero gradient.
 """
 import pytest
 import torch
@@ -102,7 +107,7 @@ def test_cfg3_view_vs_oracle(cuda):
     torch.autograd.backward([rgb_o, a_o], [vr, va])
     r = assert_close(rgb_g.cpu(), rgb_o.detach(), max_frac=2e-4, max_outlier=0.02, what="rgb")
     assert_close(a_g.cpu(), a_o.detach(), max_frac=2e-4, max_outlier=0.02, what="alpha")
-    grad_close(g_g.cpu(), po.grad, max_frac=2e-3, what="grad")
+    grad_close(g_g.cpu(), po.grad, max_frac=2e-3, outlier_rel=2e-3, what="grad")
     tgt = (rgb_o.detach() + 0.05 * torch.randn(rgb_o.shape, generator=torch.Generator().manual_seed(1))).clamp(0, 1)
     psnr = lambda x: float(10 * torch.log10(1.0 / ((x - tgt) ** 2).mean()))
     assert abs(psnr(rgb_g.cpu()) - psnr(rgb_o.detach())) < 0.05, r
@@ -113,6 +118,31 @@ def test_cfg3_lists_and_properties(cuda):
     I, max_seg = _check_lists_vs_torch_sort(p, V, K, c.width, c.height, c.views, cuda)
     assert I > 2_000_000 and max_seg > 8192, (I, max_seg)   # long lists: the partitioned sort
     _properties3d(c, p, V, K, cuda)
+
+
+def test_cfg2_view_vs_oracle(cuda):
+    """BASELINE config 2 (3D, 50k Gaussians, 288x256, 1 view, seed 1002) against the oracle
+    with the config 1 tolerances (test_parity_gpu.py::test_3d_cfg1_vs_oracle)."""
+    from gsr import render as R
+    from oracle.oracle3d import render3d
+    c, p, V, K = _scene(2)
+    W, H = c.width, c.height
+    assert (c.N, W, H, c.views, c.seed) == (50_000, 288, 256, 1, 1002)
+    # forward-only, as timed: no autograd graph, no saved state
+    rgb_f, a_f, _ = _gpu3d(p, V, K, W, H, cuda)
+    assert R.last_stats()["n_isect"] > 50_000
+    vr, va = _cot(1, H, W, 8, "cpu")
+    rgb_g, a_g, g_g = _gpu3d(p, V, K, W, H, cuda, vr.to(cuda), va.to(cuda))
+    assert torch.equal(rgb_f, rgb_g) and torch.equal(a_f, a_g)
+    po = p.clone().requires_grad_(True)
+    rgb_o, a_o = render3d(po, V, K, W, H, torch.ones(3))
+    torch.autograd.backward([rgb_o, a_o], [vr, va])
+    r = assert_close(rgb_g.cpu(), rgb_o.detach(), max_frac=2e-4, max_outlier=0.02, what="cfg2 rgb")
+    assert_close(a_g.cpu(), a_o.detach(), max_frac=2e-4, max_outlier=0.02, what="cfg2 alpha")
+    grad_close(g_g.cpu(), po.grad, max_frac=2e-3, outlier_rel=2e-3, what="cfg2 grad")
+    tgt = (rgb_o.detach() + 0.05 * torch.randn(rgb_o.shape, generator=torch.Generator().manual_seed(1))).clamp(0, 1)
+    psnr = lambda x: float(10 * torch.log10(1.0 / ((x - tgt) ** 2).mean()))
+    assert abs(psnr(rgb_g.cpu()) - psnr(rgb_o.detach())) < 0.05, r
 
 
 def test_cfg5_band_vs_oracle(cuda):
@@ -132,7 +162,7 @@ def test_cfg5_band_vs_oracle(cuda):
     torch.autograd.backward([rgb_o, a_o], [vr, va])
     assert_close(rgb_g.cpu()[:, y0:y1], rgb_o.detach()[:, y0:y1], max_frac=2e-4, max_outlier=0.02, what="rgb")
     assert_close(a_g.cpu()[:, y0:y1], a_o.detach()[:, y0:y1], max_frac=2e-4, max_outlier=0.02, what="alpha")
-    grad_close(g_g.cpu(), po.grad, max_frac=2e-3, what="grad")
+    grad_close(g_g.cpu(), po.grad, max_frac=2e-3, outlier_rel=2e-3, what="grad")
     assert float(po.grad.abs().max()) > 0
 
 
@@ -165,3 +195,55 @@ def test_cfg4_2d_properties(cuda):
         assert torch.equal(a, b), "not deterministic"
     assert torch.equal(r4[2], 4.0 * r1[2])
     assert float(r1[1].max()) > 0.5 and float(r1[2].abs().max()) > 0
+
+
+@pytest.mark.parametrize("y0,x0", [(240, 192), (96, 0)])
+def test_cfg4_window_vs_oracle(cuda, y0, x0):
+    """A 16x128 window of the full 500k-Gaussian config 4 frame against the dense reference
+    compositor (src/gaussian_renderer.py:336-427 via oracle2d) restricted to the window.
+
+    Every Gaussian whose value can exceed e^-40 * opacity anywhere in the window is kept (in
+    parameter order); every other Gaussian is below 1e-17 there, i.e. below fp32 resolution of
+    the window's values, and the HIP path (eps-extent 1e-8) gives it exactly zero gradient."""
+    from gsr import render as R
+    from gsr.scenes import CONFIGS, gaussians2d
+    from oracle.oracle2d import render2d_dense
+    c = CONFIGS[4]
+    W, H = c.width, c.height
+    y1, x1 = y0 + 16, x0 + 128
+    p = gaussians2d(c.N, W, H, c.seed)
+    g = torch.Generator().manual_seed(10 + y0)
+    vr = torch.zeros(H, W, 3)
+    va = torch.zeros(H, W)
+    vr[y0:y1, x0:x1] = torch.randn(16, 128, 3, generator=g)
+    va[y0:y1, x0:x1] = torch.randn(16, 128, generator=g)
+    bg = torch.ones(3)
+    pg = p.to(cuda).requires_grad_(True)
+    rgb, alpha = R.render2d(pg, W, H, bg.to(cuda))
+    torch.autograd.backward([rgb, alpha], [vr.to(cuda), va.to(cuda)])
+    # Gaussians that can reach the window: distance from the mean to the window box, in units
+    # of the larger standard deviation (a lower bound on the rotated Mahalanobis distance)
+    s_max = torch.exp(p[:, 2:4]).amax(1)
+    dx = (x0 - p[:, 0]).clamp_min(0) + (p[:, 0] - (x1 - 1)).clamp_min(0)
+    dy = (y0 - p[:, 1]).clamp_min(0) + (p[:, 1] - (y1 - 1)).clamp_min(0)
+    keep = (dx * dx + dy * dy) / (2 * s_max * s_max + 1e-8) < 40.0
+    idx = torch.nonzero(keep)[:, 0]
+    assert 2_000 < idx.numel() < 30_000, idx.numel()
+    q = p[idx].clone()
+    q[:, 0] -= x0
+    q[:, 1] -= y0
+    qo = q.requires_grad_(True)
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)          # ~12k tiny per-Gaussian steps: op overhead, not FLOPs
+    try:
+        rgb_o, a_o = render2d_dense(qo, x1 - x0, y1 - y0, bg)
+        torch.autograd.backward([rgb_o, a_o], [vr[y0:y1, x0:x1], va[y0:y1, x0:x1]])
+    finally:
+        torch.set_num_threads(nt)
+    assert_close(rgb.detach().cpu()[y0:y1, x0:x1], rgb_o.detach(), what="cfg4 window rgb")
+    assert_close(alpha.detach().cpu()[y0:y1, x0:x1], a_o.detach(), what="cfg4 window alpha")
+    gg = pg.grad.detach().cpu()
+    grad_close(gg[idx], qo.grad, what="cfg4 window grad")
+    assert float(gg[~keep].abs().max()) == 0.0
+    # the frame is saturated here (alpha >= 0.999): the regime where A reaches 1.0f
+    assert float(a_o.max()) > 0.99 and float(qo.grad.abs().max()) > 0

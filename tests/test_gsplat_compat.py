@@ -77,7 +77,7 @@ def test_vs_oracle(cuda, N, C, W, H, seed, radius_clip, with_bg):
     assert_close(rgb.detach().cpu(), rgb_o, what="rgb")
     assert_close(alpha.detach().cpu()[..., 0], a_o, what="alpha")
     for name, t, e in zip(("means", "quats", "scales", "opacities", "colors"), leaves, g_o):
-        grad_close(t.grad.cpu(), e, what=f"v_{name}", max_frac=1e-3)
+        grad_close(t.grad.cpu(), e, what=f"v_{name}", max_frac=1e-3, outlier_rel=2e-3)
 
 
 @pytest.mark.gpu

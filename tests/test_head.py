@@ -102,7 +102,7 @@ def test_head3d_vs_oracle(cuda, pose):
     for name, a, e in zip(("net", "v0", "scale"), leaves, lo):
         if name == "scale":
             continue                                  # a sum over all rows, checked below
-        grad_close(a.grad.cpu()[keep], e.grad[keep], what=f"grad {name}", max_frac=1e-3)
+        grad_close(a.grad.cpu()[keep], e.grad[keep], what=f"grad {name}", max_frac=1e-3, outlier_rel=5e-3)
     grad_close(leaves[2].grad.cpu(), lo[2].grad, what="grad scale")
 
 
@@ -128,7 +128,17 @@ def test_pose_transform_vs_oracle(cuda):
         o, amb = _sign_fix(out.detach().cpu(), ref.detach())
         assert int(amb.sum()) < 10
         assert_close(o, ref.detach(), rtol=1e-4, atol=1e-6, what=f"pose angle={angle}")
-        grad_close(pg.grad.cpu()[~amb], pc.grad[~amb], what=f"pose grad angle={angle}", max_frac=1e-3)
+        # torch.linalg.eigh's backward divides by every eigenvalue gap, so where the
+        # Bar-Itzhack matrix has a repeated NON-top eigenvalue (the identity rotation:
+        # eigenvalues 1, -1/3, -1/3, -1/3) the reference's gradient is inf/NaN (0 * inf)
+        # although only the top eigenvector is used; the kernel differentiates the top
+        # eigenvector alone and stays finite.  Those rows are reported and excluded.
+        g_gpu = pg.grad.cpu()
+        assert bool(torch.isfinite(g_gpu).all())
+        undefined = ~torch.isfinite(pc.grad).all(1)
+        assert int(undefined.sum()) <= 4, int(undefined.sum())
+        keep = ~amb & ~undefined
+        grad_close(g_gpu[keep], pc.grad[keep], what=f"pose grad angle={angle}", max_frac=1e-3, outlier_rel=5e-3)
 
 
 @pytest.mark.gpu
@@ -160,7 +170,7 @@ def test_params_from_volume_end_to_end(cuda):
     assert out.shape == ref.shape
     o, amb = _sign_fix(out.detach().cpu(), ref.detach())
     assert_close(o, ref.detach(), rtol=1e-4, atol=1e-5, what="params")
-    grad_close(vg.grad.cpu(), vc.grad, what="grad volume", max_frac=1e-3)
+    grad_close(vg.grad.cpu(), vc.grad, what="grad volume", max_frac=1e-3, outlier_rel=5e-3)
     grad_close(sg.grad.cpu(), sc.grad, what="grad scale")
 
 

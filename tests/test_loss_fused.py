@@ -102,7 +102,7 @@ def test_fused_vs_cpu_oracle(cuda):
     assert_close(li_f, li.detach(), rtol=1e-5, what="iou_loss")
     assert_close(lm_f, lm.detach(), rtol=1e-5, what="img_loss")
     # sign(rgb - t) flips where the two renders straddle the target (|rgb - t| ~ 1e-7): rare
-    grad_close(g_f, pc.grad, what="v_params", max_frac=2e-3)
+    grad_close(g_f, pc.grad, what="v_params", max_frac=2e-3, outlier_rel=2e-3)
 
 
 @pytest.mark.gpu

@@ -213,7 +213,7 @@ def test_3d_cfg1_vs_oracle(cuda):
     rgb_o, a_o, g_o = _run_oracle3d(p, V, K, c.width, c.height, bg, vr, va)
     r = assert_close(rgb_g, rgb_o, max_frac=2e-4, max_outlier=0.02, what="rgb")
     assert_close(a_g, a_o, max_frac=2e-4, max_outlier=0.02, what="alpha")
-    grad_close(g_g, g_o, max_frac=2e-3, what="grad")
+    grad_close(g_g, g_o, max_frac=2e-3, outlier_rel=2e-3, what="grad")
     # PSNR of the rendering against the oracle render must agree to 0.05 dB vs any target
     tgt = (rgb_o + 0.05 * torch.randn(rgb_o.shape, generator=torch.Generator().manual_seed(1))).clamp(0, 1)
     psnr = lambda x: float(10 * torch.log10(1.0 / ((x - tgt) ** 2).mean()))
@@ -223,10 +223,14 @@ def test_3d_cfg1_vs_oracle(cuda):
 def test_3d_isotropic_radius_mode(cuda):
     W, H = 64, 48
     p, V, K = _scene3d(500, W, H, 1, 21, extent=0.05, scale_shift=1.0)
+    p[0:6, 13] = -200.0        # sigmoid underflows to exactly 0: no 0/0 in dL/dopacity
+    p[6:12, 13] = -7.0         # opacity < 1/255: never composited
     bg = torch.zeros(3)
     vr, va = _cot(1, H, W, 22)
     rgb_g, a_g, g_g = _run_gpu3d(p, V, K, W, H, bg, cuda, vr, va, radius_mode="isotropic_3sigma")
     rgb_o, a_o, g_o = _run_oracle3d(p, V, K, W, H, bg, vr, va, radius_mode=1)
+    assert bool(torch.isfinite(g_g).all())
+    assert float(g_g[0:12].abs().max()) == 0.0
     assert_close(rgb_g, rgb_o, what="rgb")
     grad_close(g_g, g_o, what="grad")
 
@@ -290,7 +294,7 @@ def test_3d_long_tile_lists(cuda):
     assert st["max_seg"] > 16384, st
     rgb_o, a_o, g_o = _run_oracle3d(p, V, K, W, H, bg, vr, va)
     assert_close(rgb_g, rgb_o, max_frac=1e-3, max_outlier=0.02, what="rgb")
-    grad_close(g_g, g_o, max_frac=2e-3, what="grad")
+    grad_close(g_g, g_o, max_frac=2e-3, outlier_rel=2e-3, what="grad")
 
 
 # ------------------------------------------------------------------------------------ 2D
@@ -422,3 +426,36 @@ def test_3d_band_sharding(cuda):
         torch.autograd.backward([rgb, a], [vr, va])
         total += pb.grad
     grad_close(total.cpu(), pf.grad.cpu(), what="band-summed grad")
+
+
+def test_3d_two_streams(cuda):
+    """Renders of the same shapes on two streams do not share the projection's tile-count
+    buffer: interleaved fwd+bwd on streams A and B equal the single-stream results."""
+    from gsr import render as R
+    W, H, C = 96, 80, 2
+    pa, V, K = _scene3d(3000, W, H, C, 71, extent=0.05)
+    pb, _, _ = _scene3d(3000, W, H, C, 72, extent=0.05)
+    bg = torch.ones(3, device=cuda)
+    vr, va = _cot(C, H, W, 73)
+    vr, va, Vd, Kd = vr.to(cuda), va.to(cuda), V.to(cuda), K.to(cuda)
+
+    def run(p):
+        pg = p.to(cuda).requires_grad_(True)
+        rgb, alpha = R.render3d(pg, Vd, Kd, W, H, bg)
+        torch.autograd.backward([rgb, alpha], [vr, va])
+        return rgb.detach().clone(), pg.grad.detach().clone()
+
+    ref_a, ref_b = run(pa), run(pb)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    outs = []
+    for _ in range(3):
+        with torch.cuda.stream(sa):
+            oa = run(pa)
+        with torch.cuda.stream(sb):
+            ob = run(pb)
+        outs.append((oa, ob))
+    torch.cuda.synchronize()
+    for oa, ob in outs:
+        assert torch.equal(oa[0], ref_a[0]) and torch.equal(oa[1], ref_a[1])
+        assert torch.equal(ob[0], ref_b[0]) and torch.equal(ob[1], ref_b[1])
