@@ -12,17 +12,6 @@
 
 namespace gsr {
 
-#ifdef GSR_EXP_COUNT
-__device__ unsigned long long g_cnt_bin[16];
-#define GSR_BCNT_ADD(i, v) atomicAdd(&g_cnt_bin[i], (unsigned long long)(v))
-#define GSR_BCNT_MAX(i, v) atomicMax(&g_cnt_bin[i], (unsigned long long)(v))
-#define GSR_BCLOCK() clock64()
-#else
-#define GSR_BCNT_ADD(i, v)
-#define GSR_BCNT_MAX(i, v)
-#define GSR_BCLOCK() 0ll
-#endif
-
 constexpr int kTopThreads = 1024;
 constexpr int kScanLdsTiles = 32768;   // tile scan: counts staged in LDS up to 128 KB
 constexpr int kChunkEntries = GSR_CHUNK;   // backward work unit (list entries)
@@ -213,9 +202,6 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__
     __syncthreads();
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
       const int v = hist[t];
-#ifdef GSR_EXP_DBLATOM
-      if (v) atomicAdd(&gcnt[t], v & 0x40000000);   // timing experiment: a second atomic
-#endif
       if (v) hist[t] = toff[t] + atomicSub(&gcnt[t], v) - v;
     }
     __syncthreads();
@@ -322,11 +308,8 @@ __device__ __forceinline__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, 
     }
     __syncthreads();
   }
-  [[maybe_unused]] const long long t_fix = GSR_BCLOCK();
-  [[maybe_unused]] int fix_iters = 0;
   // equal sort words: order by c*N+n — odd-even passes until nothing moves
   while (true) {
-    ++fix_iters;
     bool moved = false;
 #pragma unroll
     for (int ph = 0; ph < 2; ++ph) {
@@ -341,11 +324,6 @@ __device__ __forceinline__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, 
       __syncthreads();
     }
     if (!__syncthreads_or(moved)) break;
-  }
-  if (threadIdx.x == 0) {
-    GSR_BCNT_ADD(5, GSR_BCLOCK() - t_fix);
-    GSR_BCNT_ADD(6, fix_iters);
-    GSR_BCNT_MAX(7, fix_iters);
   }
 }
 
@@ -396,24 +374,14 @@ __global__ __launch_bounds__(NT) void k_segsort(
   const int len = tile_offset[ct + 1] - start;
   uint64_t* seg = keys + start;
   if (len <= lds_keys) {
-    [[maybe_unused]] const long long t0 = GSR_BCLOCK();
     for (int i = threadIdx.x; i < len; i += blockDim.x)
       s_keys[i] = (seg[i] & 0xffffffff00000000ull) | (uint64_t)(uint32_t)i;
     __syncthreads();
-    [[maybe_unused]] const long long t1 = GSR_BCLOCK();
     lds_radix_sort<NT>(s_keys, len, s_hist, seg);
-    [[maybe_unused]] const long long t2 = GSR_BCLOCK();
     for (int s = threadIdx.x; s < len; s += blockDim.x) {
       const uint32_t p = low_word(s_keys[s]);
       sorted_ids[start + s] = (int32_t)low_word(seg[p]);
       k_of_s[start + s] = k_of_slot[start + p];
-    }
-    if (threadIdx.x == 0) {
-      GSR_BCNT_ADD(0, t1 - t0);
-      GSR_BCNT_ADD(1, t2 - t1);
-      GSR_BCNT_ADD(2, GSR_BCLOCK() - t2);
-      GSR_BCNT_MAX(3, GSR_BCLOCK() - t0);
-      GSR_BCNT_ADD(4, 1);
     }
     return;
   }
@@ -670,16 +638,5 @@ int gsr_selftest_lds_order(int32_t* violations, void* stream) {
   return GSR_OK;
 }
 
-#ifdef GSR_EXP_COUNT
-int gsr_debug_counters_bin(unsigned long long* out, int reset) {
-  (void)hipDeviceSynchronize();
-  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(gsr::g_cnt_bin), sizeof(gsr::g_cnt_bin));
-  if (reset) {
-    unsigned long long z[16] = {0};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(gsr::g_cnt_bin), z, sizeof(z));
-  }
-  return 0;
-}
-#endif
 
 }  // extern "C"

@@ -99,10 +99,6 @@ __device__ __forceinline__ float wave_sum(float v) {
       : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]), "+v"(lo[3]), "+v"(lo[4]), "+v"(lo[5]), "+v"(lo[6]),   \
         "+v"(lo[7]), "+v"(hi[0]), "+v"(hi[1]), "+v"(hi[2]), "+v"(hi[3]), "+v"(hi[4]), "+v"(hi[5]),   \
         "+v"(hi[6]), "+v"(hi[7]))
-#ifdef GSR_EXP_NOSWAP
-__device__ __forceinline__ void swap32x8(float*, float*) {}   // timing experiment only
-__device__ __forceinline__ void swap16x8(float*, float*) {}
-#else
 __device__ __forceinline__ void swap32x8(float* lo, float* hi) {
   asm("s_nop 1");
   GSR_SWAP8("v_permlane32_swap_b32");
@@ -111,7 +107,6 @@ __device__ __forceinline__ void swap16x8(float* lo, float* hi) {
   asm("s_nop 1");
   GSR_SWAP8("v_permlane16_swap_b32");
 }
-#endif
 #undef GSR_SWAP8
 
 // Intra-row level: a lane in the upper half (of the row / half-row / quad pair) keeps the

@@ -43,9 +43,6 @@ __device__ __forceinline__ void hist_flush(int* hist, int32_t* gcount, int T) {
   for (int t = threadIdx.x; t < T; t += blockDim.x) {
     const int v = hist[t];
     if (v) atomicAdd(&gcount[t], v);
-#ifdef GSR_EXP_DBLATOM
-    if (v) atomicAdd(&gcount[t], v & 0x40000000);   // timing experiment: a second atomic
-#endif
   }
 }
 

@@ -14,21 +14,6 @@
 
 namespace gsr {
 
-#ifdef GSR_EXP_COUNT
-// work counters for timing analysis builds only (tools/count_work.py)
-__device__ unsigned long long g_cnt[16];
-#define GSR_CNT_ADD(i, v) atomicAdd(&g_cnt[i], (unsigned long long)(v))
-#define GSR_CNT_MAX(i, v) atomicMax(&g_cnt[i], (unsigned long long)(v))
-#define GSR_CLOCK() clock64()
-#else
-#define GSR_CNT_ADD(i, v)
-#define GSR_CNT_MAX(i, v)
-#define GSR_CLOCK() 0ll
-#endif
-#if defined(GSR_EXP_COUNT) || defined(GSR_EXP_TIMELINE)
-#define GSR_TIMELINE 1
-__device__ unsigned long long g_blk[32768][3];   // per forward workgroup: start, end (s_memrealtime), list length
-#endif
 
 constexpr int kRasterThreads = 256;
 constexpr int kChunk3 = GSR_CHUNK;   // backward work unit: list entries per chunk
@@ -220,9 +205,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   // XCD-aware mapping: workgroups are dealt to the 8 XCDs round-robin by id, so the four
   // quadrant workgroups of a tile get ids 32k + 8*quad + x (same id mod 8): they share one
   // XCD's L2 for the tile's records.  Busy tile u = 8k + x, in longest-first order.
-#ifdef GSR_TIMELINE
-  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
-#endif
   const int u = ((int)blockIdx.x >> 5) * 8 + ((int)blockIdx.x & 7);
   const int quad = ((int)blockIdx.x >> 3) & 3;
   if (u >= n_busy) return;
@@ -250,9 +232,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   const int cbase = chunk_base[ct];
   int kcur = 0;
   float Ts = 1.f, dr = 0.f, dg = 0.f, db = 0.f;   // dr..: this lane's share of the chunk's colour
-  [[maybe_unused]] int cnt_b = 0, cnt_s = 0;
-  [[maybe_unused]] long long clk_cull = 0, clk_comp = 0;
-  [[maybe_unused]] const long long clk_start = GSR_CLOCK();
   if constexpr (!IS2D) {
   __shared__ float4 s_q0[2][256];
   __shared__ float4 s_q1[2][256];
@@ -302,7 +281,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     for (int h = 0; h < 2; ++h) {
       const int hb = rb + 128 * h;
       if (hb >= end || __ballot(!done) == 0ull) break;
-      ++cnt_b;
       if (hb > start && ((hb - start) % kChunk3) == 0) {   // entering chunk kcur+1
         const float Dr = quad_sum(dr), Dg = quad_sum(dg), Db = quad_sum(db);
         if (q == 0) ckpt[(int64_t)(cbase + kcur) * kRasterThreads + bwd_pixel_slot(il, jl)] = make_float4(Ts, Dr, Dg, Db);
@@ -325,7 +303,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
               (unsigned char)idx;
         n += __popcll(m);
       }
-      cnt_s += n;
       __builtin_amdgcn_wave_barrier();
       for (int k0 = 0; k0 < n; k0 += 4) {
         const int k = k0 + q;
@@ -388,8 +365,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   // waits for younger record loads), composite.  false = every pixel of the wave is done.
   auto step = [&](int b0, float4& c0, float4& c1, float4& c2, int id_use, int& id_new) -> bool {
     if (__ballot(!done) == 0ull) return false;
-    [[maybe_unused]] const long long t0 = GSR_CLOCK();
-    ++cnt_b;
     if (b0 > start && ((b0 - start) % kChunk3) == 0) {   // entering chunk kcur+1
       const float Dr = quad_sum(dr), Dg = quad_sum(dg), Db = quad_sum(db);
       if (q == 0) ckpt[(int64_t)(cbase + kcur) * kRasterThreads + bwd_pixel_slot(il, jl)] = make_float4(Ts, Dr, Dg, Db);
@@ -403,7 +378,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     const bool keep = (b0 + lane < end) && cull_keep<IS2D>(c0, c1, c2, bx0, bx1, by0, by1);
     const unsigned long long m = __ballot(keep);
     const int n = __popcll(m);
-    cnt_s += n;
     if (keep) {
       const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
       s_p0[wv][slot] = c0;
@@ -414,7 +388,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     const Splat sc = rec[id_use];
     c0 = sc.p0; c1 = sc.p1; c2 = sc.p2;
     __builtin_amdgcn_wave_barrier();
-    [[maybe_unused]] const long long t1 = GSR_CLOCK();
     for (int k0 = 0; k0 < n; k0 += 4) {
       const int k = k0 + q;
       const int kk = k < n ? k : n - 1;
@@ -453,24 +426,12 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
       done = done || fs < 4;
     }
     __builtin_amdgcn_wave_barrier();
-    [[maybe_unused]] const long long t2 = GSR_CLOCK();
-    clk_cull += t1 - t0;
-    clk_comp += t2 - t1;
     return true;
   };
   for (int b0 = start; b0 < end; b0 += 128) {
     if (!step(b0, x0, x1, x2, idp, idq)) break;
     if (b0 + 64 >= end || !step(b0 + 64, y0, y1, y2, idq, idp)) break;
   }
-  }
-  if (lane == 0) {
-    GSR_CNT_ADD(0, cnt_b);
-    GSR_CNT_MAX(1, cnt_b);
-    GSR_CNT_ADD(2, cnt_s);
-    GSR_CNT_ADD(3, clk_cull);
-    GSR_CNT_ADD(4, clk_comp);
-    GSR_CNT_ADD(5, GSR_CLOCK() - clk_start);
-    GSR_CNT_MAX(6, GSR_CLOCK() - clk_start);
   }
   const float Dr = quad_sum(dr), Dg = quad_sum(dg), Db = quad_sum(db);
   cr += Dr;
@@ -557,13 +518,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   if (q == 0 && last >= 0) atomicMax(&s_max, last);
   __syncthreads();
   if (threadIdx.x == 0 && s_max >= 0) atomicMax(&tile_end[ct], s_max);   // finalised by k_raster_finalize
-#ifdef GSR_TIMELINE
-  if (threadIdx.x == 0 && blockIdx.x < 32768) {
-    g_blk[blockIdx.x][0] = rt0;
-    g_blk[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
-    g_blk[blockIdx.x][2] = (unsigned long long)(end - start);
-  }
-#endif
 }
 
 // Per busy tile: tile_end = 1 + max last over the tile's four quadrant workgroups (or the
@@ -683,7 +637,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
   // (read before the bound check: the list has a slot for every grid slot)
   const int4 cd = reinterpret_cast<const int4*>(chunk_list)[blockIdx.x];
   if ((int)blockIdx.x >= stats->n_active) return;
-  [[maybe_unused]] const long long clk_start = GSR_CLOCK();
   const int b0 = cd.x, n = cd.y, chunk = cd.z, ct = cd.w;
   const SubTile st = sub_tile<IS2D>(ct, tw, th, W, H);
   const int wv = st.wv;
@@ -760,13 +713,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
     }
     nsurv += __popcll(mk);
   }
-  [[maybe_unused]] const long long clk_loop = GSR_CLOCK();
-  if (st.lane == 0) {
-    GSR_CNT_ADD(8, nsurv);
-    GSR_CNT_ADD(9, (nsurv + 6) / 7);
-    GSR_CNT_ADD(10, clk_loop - clk_start);
-    if (wv == 0) GSR_CNT_ADD(13, 1);
-  }
   if (st.lane < kGroup) s_list[wv][nsurv + st.lane] = (short)kNull;
   __builtin_amdgcn_wave_barrier();
   // Branch-free groups of 7 survivors: an invalid (entry, pixel) pair contributes zeros and
@@ -776,11 +722,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
     acc[63] = 0.f;
 #pragma unroll
     for (int g = 0; g < kGroup; ++g) {
-#ifdef GSR_EXP_NOLIST
-      const int k = (g0 + g) & 255;   // timing experiment: no list indirection
-#else
       const int k = s_list[wv][g0 + g];
-#endif
       const float4 p0 = s_p0[k];
       const float4 p1 = s_p1[k];
       const float4 p2 = s_p2[k];
@@ -825,25 +767,13 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
       acc[g * kPartial + 5] = v_sig;   // v_opacity = vis v_al = -v_sig / o (formed per entry below)
       if (!IS2D) Sv += fac * cv;
     }
-#ifdef GSR_EXP_NORED
-    float sum = 0.f;   // timing experiment: no cross-lane reduction
-#pragma unroll
-    for (int i = 0; i < 64; ++i) sum += (i & 1) ? acc[i] : -acc[i];
-#else
     const float sum = reduce64(acc);
-#endif
     const int g = st.lane / kPartial;
     if (g < kGroup && g0 + g < nsurv)
       __hip_atomic_fetch_add(&L[st.lane - g * kPartial][wv >> 1][s_list[wv][g0 + g]], sum, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
   }
-  [[maybe_unused]] const long long clk_loop_end = GSR_CLOCK();
   __syncthreads();
-  if (st.lane == 0) {
-    GSR_CNT_ADD(11, clk_loop_end - clk_loop);
-    GSR_CNT_ADD(12, GSR_CLOCK() - clk_loop_end);
-    GSR_CNT_MAX(14, GSR_CLOCK() - clk_start);
-  }
   if (threadIdx.x < n) {
     const int k = threadIdx.x;
     float v[kPartial];
@@ -871,23 +801,6 @@ using namespace gsr;
 
 extern "C" {
 
-#ifdef GSR_TIMELINE
-int gsr_debug_blocks(unsigned long long* out) {
-  (void)hipDeviceSynchronize();
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gsr::g_blk), sizeof(gsr::g_blk)) == hipSuccess ? 0 : -2;
-}
-#endif
-#ifdef GSR_EXP_COUNT
-int gsr_debug_counters(unsigned long long* out, int reset) {
-  (void)hipDeviceSynchronize();
-  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(gsr::g_cnt), sizeof(gsr::g_cnt));
-  if (reset) {
-    unsigned long long z[16] = {0};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(gsr::g_cnt), z, sizeof(z));
-  }
-  return 0;
-}
-#endif
 
 // Self-test of the transposed wave reduction: out[l] = sum over lanes of v_lane[l] for the
 // pattern v_lane[i] = ((lane*7 + i*13) % 97) + i/4 (checked on the host by tests/).
