@@ -1,28 +1,43 @@
 #!/usr/bin/env python3
-"""Benchmark: rendered frames/s (fwd+bwd) of the MI355X rasterizer on BASELINE config 3.
+"""Benchmark: rendered frames/s (fwd+bwd) of the MI355X rasterizer on a BASELINE config.
 
-A "step" = one full pass of the hot path over one batch of synthetic input: projection →
-tile binning (incl. its one 16-byte host read) → raster fwd → raster bwd (fixed random
-cotangents) → projection bwd, for the 6 cameras of config 3 (3D, 200k Gaussians, 576x512)
-— the shape BASELINE.json's north-star target is quoted on.  Inputs are resident in HBM
-before the timed region.  value = views (frames) rendered fwd+bwd per second, summed over
-ranks.
+A "step" = one full pass of the hot path over one batch of synthetic input: projection ->
+tile binning (incl. its one 32-byte host read) -> raster fwd -> raster bwd (fixed random
+cotangents) -> projection bwd.  Default workload: BASELINE config 3 (3D, 200k Gaussians,
+576x512, 6 cameras) -- the shape BASELINE.json's north-star target is quoted on.  Inputs
+are resident in HBM before the timed region.  value = views (frames) rendered per second
+over the whole job.
 
-Multi-GPU (torchrun, one process per GPU, RCCL): every rank renders 6 cameras of its own
-(ring azimuths offset per rank) of the SAME Gaussian set and the per-rank parameter
-gradients are all-reduced (SUM) — the one real exchange of multi-view training.  Per-GPU
-work is fixed as N grows → "scaling": "weak".
+Multi-GPU (torchrun, one process per GPU, RCCL over xGMI), SURVEY.md §8(e):
+  * 3D, --shard units (default, "strong"): ONE C-view job per step; the C*th (view, tile
+    row) units are cut into `world` contiguous, work-balanced ranges (gsr.multiview.unit_shard);
+    each rank projects only the views it touches, bins only its rows, and all-reduces its
+    partial v_params in Gaussian-range buckets that overlap the projection backward.
+  * 3D, --shard views ("weak"): every rank renders C views of its own (ring offset per rank).
+  * 2D (config 4, "strong"): 8 frames x 6 views = 48 (frame, view) units, round-robin over
+    ranks; each rank renders its units batched per frame bucket and all-reduces the [8,N,9]
+    gradient per bucket (async, overlapping the next bucket).
+  * config 2 (one view, fwd-only): replicas, "weak".
+--rank-share N (one GPU, no collectives): times each of the N ranks' shares of the strong
+layout one after the other and reports the projected N-GPU time (max share + a ring
+all-reduce cost model); no multi-GPU node is needed to size the design.
 
-Also reported: the dominant kernel's roofline (algorithmic bytes per launch, SURVEY.md
-§8(d), over its HIP-event-timed average duration) and the CPU baseline (the oracle, a
-restatement of the reference semantics, timed on a bounded sample on this host).
+Also reported: the dominant kernel's roofline (algorithmic bytes per launch, SURVEY.md §8(d),
+over its HIP-event-timed average duration, events on the launch stream); roofline.traffic /
+.valu from rocprofv3 PMC passes OF THE SAME CONFIG committed under profiles/ (null when none);
+the CPU baseline (the oracle, a restatement of the reference semantics, timed on a bounded
+sample on this host); and dPSNR = |PSNR(gsr, target) - PSNR(oracle, target)| on a perturbed
+target (scripts/utils/evaluate_model.py:240-243).
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
+import math
 import os
 import platform
+import re
 import sys
 import time
 
@@ -33,36 +48,43 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# PMC counter run of the same bench command (FETCH_SIZE and WRITE_SIZE passes), committed
-DEFAULT_TRAFFIC_CSV = os.path.join(ROOT, "profiles", "r01_pmc_counters.csv")
-# SQ counter passes (tools/pmc_sq.sh) for the dominant kernel's VALU occupancy
-DEFAULT_SQ_CSVS = [os.path.join(ROOT, "profiles", f"r01_v16_pmc_sq_p{i}.csv") for i in (1, 2)]
-N_SIMDS = 256 * 4   # MI355X: 256 CUs x 4 SIMDs
+XGMI_LINK_GBS = 153.0   # one xGMI link, per direction (ring all-reduce cost model)
+N_SIMDS = 256 * 4       # MI355X: 256 CUs x 4 SIMDs
+PROFILES = os.path.join(ROOT, "profiles")
+FRAMES_2D = 8           # config 4: 8 frames x 6 views
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
+    ap.add_argument("--shard", default="units", choices=["units", "views"],
+                    help="3D, N>1: 'units' = the ranks split ONE C-view job by (view, tile row) units (strong "
+                         "scaling); 'views' = every rank renders C views of its own (weak scaling)")
+    ap.add_argument("--buckets", type=int, default=0,
+                    help="all-reduce buckets (3D: Gaussian ranges of v_params; 2D: frame ranges); 0 = default "
+                         "(3D 4, 2D 2; 1 on a single GPU)")
+    ap.add_argument("--rank-share", type=int, default=0,
+                    help="one GPU: time each of N ranks' shares of the strong layout and project N-GPU scaling")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the CPU oracle timing")
-    ap.add_argument("--cpu-views", type=int, default=1, help="views in the bounded CPU sample")
-    ap.add_argument("--shard", default="views", choices=["views", "bands"],
-                    help="N>1, 3D: 'views' = every rank renders its own 6 views (weak scaling); "
-                         "'bands' = the ranks split the tile rows of ONE 6-view job (strong scaling, "
-                         "bands balanced by the per-row list lengths of a warm-up render)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: every CPU this "
+                                                               "process may run on)")
+    ap.add_argument("--psnr", type=int, default=1, help="0 disables the dPSNR check")
     ap.add_argument("--loss", default="none", choices=["none", "fused", "torch"],
                     help="3D, 1 GPU: time render + the reference IoU/L1 training loss "
                          "(train_script.py:128-133) fused into the kernels, or as plain torch ops")
-    ap.add_argument("--traffic-csv", default=DEFAULT_TRAFFIC_CSV,
-                    help="rocprofv3 --pmc counter_collection.csv to fill roofline.traffic "
-                         "(default: the committed profiles/ counter run, if present)")
-    return ap.parse_args()
+    ap.add_argument("--pmc-dir", default=PROFILES, help="where the per-config rocprofv3 PMC passes live")
+    return ap.parse_args(argv)
 
+
+# ------------------------------------------------------------------ algorithmic bytes (§8(d))
 
 def algorithmic_bytes(kernel: str, C: int, N: int, P: int, I: int, I_eff: int, p: int) -> float:
-    """Per-launch algorithmic bytes, SURVEY.md §8(d) per-unit figures × units per launch."""
+    """Per-launch algorithmic bytes, SURVEY.md §8(d) per-unit figures x the units one launch
+    processes: C cameras (units) x N Gaussians projected, P pixels, I intersections, I_eff
+    list entries read by the raster."""
     if kernel.startswith("raster") and kernel.endswith("_fwd"):
         return 40.0 * I_eff + 20.0 * P                 # read id+xy+conic+opac+colour; write rgb+alpha+last
     if kernel.startswith("raster") and kernel.endswith("_bwd"):
@@ -76,23 +98,43 @@ def algorithmic_bytes(kernel: str, C: int, N: int, P: int, I: int, I_eff: int, p
     return 0.0
 
 
-def step_bytes(C: int, N: int, P_view: int, I: int, I_eff: int, p: int, backward: bool = True) -> float:
-    """Whole step, SURVEY.md §8(d): fwd+bwd C·N·(12p+136) + 36·I + 80·I_eff + 44·C·P;
-    fwd-only C·N·(4p+32) + 36·I + 40·I_eff + 20·C·P."""
+def step_bytes(C: int, N: int, P: int, I: int, I_eff: int, p: int, backward: bool = True) -> float:
+    """Whole launch sequence, SURVEY.md §8(d) (P = all pixels of the C units):
+    fwd+bwd C*N*(12p+136) + 36*I + 80*I_eff + 44*P; fwd-only C*N*(4p+32) + 36*I + 40*I_eff + 20*P."""
     if not backward:
-        return C * N * (4.0 * p + 32.0) + 36.0 * I + 40.0 * I_eff + 20.0 * C * P_view
-    return C * N * (12.0 * p + 136.0) + 36.0 * I + 80.0 * I_eff + 44.0 * C * P_view
+        return C * N * (4.0 * p + 32.0) + 36.0 * I + 40.0 * I_eff + 20.0 * P
+    return C * N * (12.0 * p + 136.0) + 36.0 * I + 80.0 * I_eff + 44.0 * P
 
 
 # libgsr call name (render.py timing brackets) -> substring of its dominant kernel's symbol
 KERNEL_SYMBOL = {"raster3d_bwd": "k_raster_bwd<false, false>", "raster3d_fwd": "k_raster_fwd<false>",
                  "raster2d_bwd": "k_raster_bwd<false, true>", "raster2d_fwd": "k_raster_fwd<true>",
-                 "bin_sort": "k_segsort"}
+                 "bin_sort": "k_segsort", "project3d_fwd": "k_project3d_fwd", "project3d_bwd": "k_project3d_bwd",
+                 "project2d_fwd": "k_project2d_fwd", "project2d_bwd": "k_project2d_bwd"}
+
+
+# ------------------------------------------------------------------ PMC passes of THIS config
+
+def pmc_files(config: int, kind: str, pmc_dir: str = PROFILES):
+    """Newest round's committed PMC pass(es) of `config`: kind 'traffic' ->
+    rNN_pmc_traffic_cfgC.csv; 'sq' -> [rNN_pmc_sq_cfgC_p1.csv, ..._p2.csv].  None if absent:
+    no other config's counters are ever substituted."""
+    pat = {"traffic": f"r*_pmc_traffic_cfg{config}.csv", "sq": f"r*_pmc_sq_cfg{config}_p1.csv"}[kind]
+    found = sorted(glob.glob(os.path.join(pmc_dir, pat)),
+                   key=lambda f: int(re.match(r"r(\d+)_", os.path.basename(f)).group(1)))
+    if not found:
+        return None
+    if kind == "traffic":
+        return found[-1]
+    p1 = found[-1]
+    p2 = p1.replace("_p1.csv", "_p2.csv")
+    return [p1, p2] if os.path.exists(p2) else None
 
 
 def traffic_from_csv(path: str, kernel_substr: str):
     """HBM bytes per launch from a rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE pass (KB units;
-    FETCH_SIZE doubled per the gfx950 correction in MI355X_MICROARCH.md §HBM)."""
+    FETCH_SIZE doubled per the gfx950 correction in MI355X_MICROARCH.md §HBM, calibrated there
+    for 16-B/lane streaming reads -- see tools/fetch_probe.hip for this path's access widths)."""
     import csv
     fetch, write = [], []
     with open(path) as f:
@@ -117,6 +159,8 @@ def valu_from_csv(paths, kernel_substr: str):
     the issue-slot fraction SQ_INSTS_VALU x 4 cycles (a full-rate wave64 fp32 op on a 16-lane
     SIMD) over the same SIMD-cycles.  None when the passes are missing."""
     import csv
+    if not paths:
+        return None
     acc = {}
     for path in paths:
         if not os.path.exists(path):
@@ -132,49 +176,426 @@ def valu_from_csv(paths, kernel_substr: str):
     simd_cycles = N_SIMDS * mean["GRBM_GUI_ACTIVE"] / 8.0
     return {"active_frac": 4.0 * mean["SQ_ACTIVE_INST_VALU"] / simd_cycles,
             "issue_frac": 4.0 * mean["SQ_INSTS_VALU"] / simd_cycles,
-            "insts_per_launch": mean["SQ_INSTS_VALU"], "source": "profiles/r01_v16_pmc_sq_p{1,2}.csv"}
+            "insts_per_launch": mean["SQ_INSTS_VALU"],
+            "source": [os.path.relpath(p, ROOT) for p in paths]}
 
 
-def cpu_baseline(cfg, params, V, K, views: int):
-    """The oracle (CPU restatement of the reference semantics) on `views` of the workload."""
-    from oracle.oracle3d import render3d as oracle_render3d
-    from oracle.oracle2d import render2d_dense
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
-    torch.set_num_threads(threads)
-    g = torch.Generator().manual_seed(cfg.seed + 1)
-    t0 = time.perf_counter()
-    if cfg.mode == "3d":
-        p = params.detach().cpu().clone().requires_grad_(cfg.backward)
-        rgb, alpha = oracle_render3d(p, V[:views].cpu(), K[:views].cpu(), cfg.width, cfg.height, torch.ones(3))
-        if cfg.backward:
-            vr = torch.randn(rgb.shape, generator=g)
-            va = torch.randn(alpha.shape, generator=g)
-            ((rgb * vr).sum() + (alpha * va).sum()).backward()
-        sample = (f"{views} of {cfg.views} views of {cfg.name}, "
-                  f"{'fwd+bwd' if cfg.backward else 'fwd'}, oracle/oracle3d.py")
-    else:
-        n = 2000
-        p = params[:n].detach().cpu().clone().requires_grad_(True)
-        rgb, alpha = render2d_dense(p, cfg.width, cfg.height, torch.ones(3))
-        ((rgb * torch.randn(rgb.shape, generator=g)).sum()).backward()
-        sample = f"first {n} of {cfg.N} Gaussians, 1 view, dense reference algorithm (linear in N)"
-    dt = time.perf_counter() - t0
-    value = views / dt if cfg.mode == "3d" else (n / cfg.N) / dt
+# ------------------------------------------------------------------ CPU baseline and dPSNR
+
+def cpu_quota() -> int:
+    """CPUs of this process's cgroup CPU quota (cgroup v2 cpu.max), 0 if unlimited/unknown.
+    The GPU box shows all 256 host CPUs to os.cpu_count() and sched affinity but allots each
+    GPU job a 16-CPU quota; threads beyond the quota only queue."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        return 0 if q == "max" else max(1, math.ceil(int(q) / int(period)))
+    except (OSError, ValueError):
+        return 0
+
+
+def cpu_threads(requested: int = 0) -> int:
+    """Every CPU this process may run on -- sched affinity, capped by the cgroup quota -- unless told."""
+    if requested > 0:
+        return requested
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    q = cpu_quota()
+    return min(n, q) if q else n
+
+
+def log(msg: str) -> None:
+    """Progress on stderr (the JSON line alone goes to stdout)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def cpu_model() -> str:
     cpu = platform.processor() or platform.machine()
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
                 if line.startswith("model name"):
-                    cpu = line.split(":", 1)[1].strip()
-                    break
+                    return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {"value": value, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": sample, "seconds": round(dt, 2), "cpu": cpu}
+    return cpu
 
 
-def main():
-    args = parse()
+def linear_fit(xs, ys):
+    """Least squares y = a + b x; returns (a, b, R^2)."""
+    n = len(xs)
+    mx, my = sum(xs) / n, sum(ys) / n
+    sxx = sum((x - mx) ** 2 for x in xs)
+    sxy = sum((x - mx) * (y - my) for x, y in zip(xs, ys))
+    b = sxy / sxx
+    a = my - b * mx
+    ss_res = sum((y - (a + b * x)) ** 2 for x, y in zip(xs, ys))
+    ss_tot = sum((y - my) ** 2 for y in ys)
+    return a, b, 1.0 - ss_res / ss_tot if ss_tot > 0 else 1.0
+
+
+def cpu_band_rows(cfg) -> tuple:
+    """Tile rows of view 0 in the bounded CPU sample: all of them up to config 3; a central
+    band of 8 tile rows for config 5 (a whole 1152x1024 view of 2M Gaussians is minutes)."""
+    th = (cfg.height + 15) // 16
+    if cfg.index == 5:
+        return th // 2 - 4, th // 2 + 4
+    return 0, th
+
+
+def cpu_baseline(cfg, params, V, K, threads: int):
+    """The oracle (CPU restatement of the reference semantics) on a bounded sample of the
+    workload, timed on this host.  Returns (baseline dict, oracle view-0 rgb or None)."""
+    from oracle.oracle3d import render3d as oracle_render3d
+    from oracle.oracle2d import render2d_dense
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(cfg.seed + 1)
+    out = {"unit": "frames/s", "cores": threads, "host_cpus": os.cpu_count(), "cgroup_cpu_quota": cpu_quota() or None,
+           "kind": "port", "cpu": cpu_model()}
+    if cfg.mode == "3d":
+        y0, y1 = cpu_band_rows(cfg)
+        th = (cfg.height + 15) // 16
+        band = None if (y0, y1) == (0, th) else (y0, y1)
+        t0 = time.perf_counter()
+        p = params.detach().cpu().clone().requires_grad_(cfg.backward)
+        rgb, alpha = oracle_render3d(p, V[:1].cpu(), K[:1].cpu(), cfg.width, cfg.height, torch.ones(3), band=band)
+        if cfg.backward:
+            vr = torch.randn(rgb.shape, generator=g)
+            va = torch.randn(alpha.shape, generator=g)
+            ((rgb * vr).sum() + (alpha * va).sum()).backward()
+        dt = time.perf_counter() - t0
+        frac = (y1 - y0) / th
+        out.update(value=frac / dt, seconds=round(dt, 2),
+                   sample=(f"view 0 of {cfg.views} of {cfg.name}" +
+                           (f", tile rows {y0}-{y1} of {th} (value = row fraction / time)" if band else "") +
+                           f", {'fwd+bwd' if cfg.backward else 'fwd'}, oracle/oracle3d.py"))
+        return out, rgb.detach()
+    # 2D: the dense reference algorithm is exactly linear in N with O(N*H*W) autograd memory
+    # (~18 MB per Gaussian at 576x512): time fwd+bwd at three N, fit, extrapolate to N.
+    ns = [256, 512, 1024]
+    ts = []
+    for n in ns:
+        t0 = time.perf_counter()
+        p = params[:n].detach().cpu().clone().requires_grad_(True)
+        rgb, alpha = render2d_dense(p, cfg.width, cfg.height, torch.ones(3))
+        ((rgb * torch.randn(rgb.shape, generator=g)).sum() + (alpha * torch.randn(alpha.shape, generator=g)).sum()
+         ).backward()
+        ts.append(time.perf_counter() - t0)
+        del rgb, alpha, p
+    a, b, r2 = linear_fit(ns, ts)
+    t_full = a + b * cfg.N
+    out.update(value=1.0 / t_full, seconds=round(sum(ts), 2),
+               sample=f"one frame-view of {cfg.name}: dense reference algorithm fwd+bwd timed at N={ns}, "
+                      f"fit t = a + b N, extrapolated to N={cfg.N}",
+               fit={"N": ns, "seconds": [round(t, 3) for t in ts], "a_s": a, "b_s_per_gaussian": b, "r2": r2,
+                    "t_full_s": t_full})
+    return out, None
+
+
+def psnr(pred_hw3: torch.Tensor, gt_hw3: torch.Tensor) -> float:
+    """scripts/utils/evaluate_model.py:240-243 (get_psnr, data_range 1) on [3,H,W] images."""
+    pred = pred_hw3.double().permute(2, 0, 1)[None]
+    gt = gt_hw3.double().permute(2, 0, 1)[None]
+    mse = ((pred - gt) ** 2).mean(dim=(-3, -2, -1))
+    return float(10 * torch.log10(1.0 / mse))
+
+
+def delta_psnr(cfg, params_cpu, V, K, dev, rgb_oracle_view0=None):
+    """target = the oracle render of a perturbed copy (means + N(0,0.002),
+    colours + N(0,0.05)); dPSNR = |PSNR(gsr, target) - PSNR(oracle, target)|.  3D: view 0 (the
+    CPU baseline's band for config 5); 2D: the first 2000 Gaussians of frame 0 (the dense
+    oracle is O(N) per pixel)."""
+    from gsr import render as R
+    from oracle.oracle2d import render2d_dense
+    from oracle.oracle3d import render3d as oracle_render3d
+    g = torch.Generator().manual_seed(cfg.seed + 7)
+    with torch.no_grad():
+        if cfg.mode == "3d":
+            y0, y1 = cpu_band_rows(cfg)
+            th = (cfg.height + 15) // 16
+            band = None if (y0, y1) == (0, th) else (y0, y1)
+            pt = params_cpu.clone()
+            pt[:, 0:3] += 0.002 * torch.randn(pt.shape[0], 3, generator=g)
+            pt[:, 10:13] += 0.05 * torch.randn(pt.shape[0], 3, generator=g)
+            target, _ = oracle_render3d(pt, V[:1], K[:1], cfg.width, cfg.height, torch.ones(3), band=band)
+            if rgb_oracle_view0 is None:
+                rgb_oracle_view0, _ = oracle_render3d(params_cpu, V[:1], K[:1], cfg.width, cfg.height,
+                                                      torch.ones(3), band=band)
+            opts = R.RenderOptions3D(band=band) if band else R.RenderOptions3D()
+            rgb_gpu, _ = R.render3d(params_cpu.to(dev), V[:1].to(dev), K[:1].to(dev), cfg.width, cfg.height,
+                                    torch.ones(3, device=dev), opts)
+            rows = slice(16 * y0, min(cfg.height, 16 * y1))
+            a, b, t = rgb_gpu[0].cpu()[rows], rgb_oracle_view0[0][rows], target[0][rows]
+            sample = f"view 0" + (f", pixel rows {rows.start}-{rows.stop}" if band else "")
+        else:
+            n = 2000
+            pt = params_cpu[:n].clone()
+            pt[:, 0:2] += 0.002 * torch.randn(n, 2, generator=g)
+            pt[:, 5:8] += 0.05 * torch.randn(n, 3, generator=g)
+            t, _ = render2d_dense(pt, cfg.width, cfg.height, torch.ones(3))
+            b, _ = render2d_dense(params_cpu[:n], cfg.width, cfg.height, torch.ones(3))
+            a, _ = R.render2d(params_cpu[:n].to(dev), cfg.width, cfg.height, torch.ones(3, device=dev))
+            a = a.cpu()
+            sample = f"first {n} Gaussians of frame 0"
+    pg, po = psnr(a, t), psnr(b, t)
+    return {"dpsnr_db": abs(pg - po), "psnr_gsr_db": pg, "psnr_oracle_db": po, "sample": sample,
+            "target": "oracle render of means+N(0,0.002), colours+N(0,0.05)",
+            "formula": "scripts/utils/evaluate_model.py:240-243"}
+
+
+# ------------------------------------------------------------------ workloads
+
+class Workload:
+    """One rank's share of a config's step.  step() enqueues one step; `units` is the number of
+    rendered views (frames) the WHOLE job completes per step; views_here the ones this rank
+    renders; launch_C / launch_P the cameras / pixels of the dominant launch sequence."""
+
+    def __init__(self, cfg, dev, world: int, rank: int, shard: str, buckets: int, loss: str, comm: bool):
+        from gsr import render as R
+        from gsr.scenes import gaussians2d, gaussians3d, ring_cameras
+        self.R, self.cfg, self.dev, self.world, self.rank = R, cfg, dev, world, rank
+        self.comm = comm and world > 1
+        C = cfg.views
+        g = torch.Generator().manual_seed(cfg.seed + 1)
+        self.bg = torch.ones(3, device=dev)
+        self.loss = loss
+        if cfg.mode == "2d":
+            F = FRAMES_2D
+            self.params_cpu = torch.stack([gaussians2d(cfg.N, cfg.width, cfg.height, cfg.seed + f) for f in range(F)])
+            self.V, self.K = ring_cameras(1, cfg.width, cfg.height)
+            self.p_dim = 9
+            from gsr.multiview import frame_view_units
+            self.units = frame_view_units(F, C, world, rank)
+            self.buckets = buckets or (1 if world == 1 else 2)
+            idx = [f * C + v for f, v in self.units]
+            vr = torch.randn(F * C, cfg.height, cfg.width, 3, generator=g)
+            va = torch.randn(F * C, cfg.height, cfg.width, generator=g)
+            self.v_rgb, self.v_alpha = vr[idx].to(dev), va[idx].to(dev)
+            self.units_total = F * C
+            self.views_here = len(self.units)
+            self.scaling = "strong"
+            self.layout = (f"(frame, view) units round-robin over {world} rank(s), batched per frame bucket "
+                           f"({self.buckets}), async RCCL all-reduce of the [8,N,9] gradient per bucket"
+                           if world > 1 else f"{F} frames x {C} views batched in one launch sequence")
+        else:
+            self.params_cpu = gaussians3d(cfg.N, cfg.seed)
+            self.p_dim = 14
+            self.buckets = buckets or (1 if world == 1 else 4)
+            th = (cfg.height + 15) // 16
+            self.th = th
+            if cfg.index == 2 or shard == "views" or world == 1:
+                # weak (config 2: replicas of its one fwd-only view; --shard views): every rank
+                # renders C views of its own, ring offset per rank
+                self.V, self.K = ring_cameras(C, cfg.width, cfg.height, azimuth0=2.0 * math.pi * rank / (C * world))
+                self.units_total = C * world
+                self.views_here = C
+                self.band = (0, -1)
+                self.scaling = "weak" if world > 1 else "n/a"
+                self.layout = ("single GPU" if world == 1 else
+                               f"replicas x{world}" if cfg.index == 2 else f"view-sharded x{world} (own views)")
+                self.v0, self.v1 = 0, C
+            else:
+                self.V, self.K = ring_cameras(C, cfg.width, cfg.height)
+                self.units_total = C
+                self.scaling = "strong"
+                self.weights = None
+                self.layout = None   # set by balance()
+            vr = torch.randn(C, cfg.height, cfg.width, 3, generator=g)
+            va = torch.randn(C, cfg.height, cfg.width, generator=g)
+            self.v_rgb_all, self.v_alpha_all = vr.to(dev), va.to(dev)
+        self.params = self.params_cpu.to(dev).requires_grad_(True)
+        self.Vd, self.Kd = self.V.to(dev), self.K.to(dev)
+        if cfg.mode == "3d" and self.scaling == "strong":
+            self.balance()
+
+    def balance(self, weights=None):
+        """(view, row) share of this rank, balanced by per-row list lengths of a full render."""
+        from gsr.multiview import unit_shard
+        cfg, R = self.cfg, self.R
+        if weights is None:
+            with torch.no_grad():
+                R.render3d(self.params, self.Vd, self.Kd, cfg.width, cfg.height, self.bg)
+            tw = (cfg.width + 15) // 16
+            weights = [float(x) for x in R.tile_work().reshape(cfg.views * self.th, tw).sum(1).cpu()]
+        self.weights = weights
+        self.v0, self.v1, self.band = unit_shard(cfg.views, self.th, self.world, self.rank, weights)
+        self.views_here = self.v1 - self.v0
+        self.layout = (f"(view, tile-row) units: rank {self.rank} views {self.v0}-{self.v1 - 1} rows {self.band} "
+                       f"of {cfg.views}x{self.th}, {self.buckets} RCCL all-reduce bucket(s) overlapping project_bwd")
+
+    def step(self):
+        cfg, R = self.cfg, self.R
+        self.params.grad = None
+        if cfg.mode == "2d":
+            from gsr.multiview import sharded_backward_frames
+
+            def render_units(p, sets):
+                return R.render2d_units(p, sets, cfg.width, cfg.height, self.bg)
+            if self.comm:
+                self.params.grad = sharded_backward_frames(render_units, self.params, self.units, self.v_rgb,
+                                                           self.v_alpha, self.buckets)
+            elif self.units:
+                # one rank's share without collectives (single GPU, --rank-share)
+                sets = [f for f, _ in self.units]
+                rgb, alpha = render_units(self.params, sets)
+                torch.autograd.backward([rgb, alpha], [self.v_rgb, self.v_alpha])
+            return
+        if not cfg.backward:
+            with torch.no_grad():   # config 2 is forward-only
+                R.render3d(self.params, self.Vd, self.Kd, cfg.width, cfg.height, self.bg)
+            return
+        if self.loss != "none":
+            self._loss_step()
+            return
+        if self.v1 <= self.v0:
+            if self.comm:
+                from gsr.multiview import sharded_backward_units
+                self.params.grad = sharded_backward_units(None, self.params, self.Vd, self.Kd, self.v_rgb_all,
+                                                          self.v_alpha_all, self.th, self.weights, self.buckets)
+            return
+        if self.comm and self.scaling == "strong":
+            from gsr.multiview import sharded_backward_units
+
+            def render_band(p, Vs, Ks, band, hook):
+                opts = R.RenderOptions3D(band=band, grad_buckets=self.buckets if hook else 1, grad_hook=hook)
+                return R.render3d(p, Vs, Ks, cfg.width, cfg.height, self.bg, opts)
+            self.params.grad = sharded_backward_units(render_band, self.params, self.Vd, self.Kd, self.v_rgb_all,
+                                                      self.v_alpha_all, self.th, self.weights, self.buckets)
+            return
+        opts = R.RenderOptions3D(band=self.band) if self.band != (0, -1) else R.RenderOptions3D()
+        rgb, alpha = R.render3d(self.params, self.Vd[self.v0:self.v1], self.Kd[self.v0:self.v1], cfg.width,
+                                cfg.height, self.bg, opts)
+        torch.autograd.backward([rgb, alpha], [self.v_rgb_all[self.v0:self.v1], self.v_alpha_all[self.v0:self.v1]])
+        if self.comm:   # --shard views: one all-reduce of the full gradient
+            import torch.distributed as dist
+            dist.all_reduce(self.params.grad)
+
+    def _loss_step(self):
+        cfg, R = self.cfg, self.R
+        if not hasattr(self, "timg"):
+            g3 = torch.Generator().manual_seed(cfg.seed + 3)
+            self.timg = torch.rand(cfg.views, 3, cfg.height, cfg.width, generator=g3).to(self.dev)
+            self.tmask = (torch.rand(cfg.views, cfg.height, cfg.width, generator=g3) < 0.3).float().to(self.dev)
+        if self.loss == "fused":
+            from gsr.loss import render3d_iou_l1
+            li, lm, rgb, alpha = render3d_iou_l1(self.params, self.Vd, self.Kd, cfg.width, cfg.height, self.bg,
+                                                 self.timg, self.tmask, 1.0)
+        else:
+            rgb, alpha = R.render3d(self.params, self.Vd, self.Kd, cfg.width, cfg.height, self.bg)
+            inter = (alpha * self.tmask).sum(dim=(-2, -1))
+            union = (alpha + self.tmask - alpha * self.tmask).sum(dim=(-2, -1))
+            li = 1 - ((inter + 1e-6) / (union + 1e-6)).mean()
+            lm = torch.abs(self.timg - rgb.permute(0, 3, 1, 2)).sum() / self.tmask.sum()
+        (li + lm).backward()
+
+    def launch_shape(self):
+        """(C, P) of the dominant launch sequence: cameras and pixels one launch covers."""
+        cfg = self.cfg
+        if cfg.mode == "2d":
+            per_bucket = max(1, math.ceil(self.views_here / self.buckets)) if self.comm else self.views_here
+            C = max(per_bucket, 1)
+            return C, C * cfg.width * cfg.height
+        if self.scaling == "strong" and self.world > 1 or getattr(self, "band", (0, -1)) != (0, -1):
+            rows = self.band[1] - self.band[0]
+            return self.views_here, min(rows * 16 * cfg.width, self.views_here * cfg.width * cfg.height)
+        return self.views_here, self.views_here * cfg.width * cfg.height
+
+
+def time_steps(w: Workload, steps: int, warmup: int, dist=None):
+    """Warm up, name the dominant kernel in a separately profiled pass, then time exactly
+    `steps` steps between barrier + synchronize brackets with HIP events around the dominant
+    kernel only.  Returns (elapsed_s, breakdown, dom_name, dom (avg_ms, launches))."""
+    R = w.R
+    for _ in range(warmup):
+        w.step()
+    torch.cuda.synchronize()
+    R.enable_kernel_timing(True)
+    for _ in range(max(2, min(steps, 5))):
+        w.step()
+    breakdown = R.kernel_times_ms()
+    R.enable_kernel_timing(False)
+    dom_name = max(breakdown.items(), key=lambda kv: kv[1][0] * kv[1][1])[0] if breakdown else None
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    R.enable_kernel_timing(True, only={dom_name} if dom_name else None)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        w.step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ktimes = R.kernel_times_ms()
+    R.enable_kernel_timing(False)
+    return elapsed, breakdown, dom_name, ktimes.get(dom_name, (0.0, 0)) if dom_name else (0.0, 0)
+
+
+def allreduce_ms(nbytes: int, world: int) -> float:
+    """Ring all-reduce cost model over xGMI: 2(n-1)/n * S per GPU at one link's bandwidth
+    (a conservative bound: RCCL spreads rings over the 7 links of each MI355X)."""
+    if world <= 1:
+        return 0.0
+    return 2.0 * (world - 1) / world * nbytes / (XGMI_LINK_GBS * 1e9) * 1e3
+
+
+def roofline(w: Workload, dom_name, dom, args):
+    R, cfg = w.R, w.cfg
+    st = R.last_stats()
+    I, I_eff = st.get("n_isect", 0), R.effective_isect()
+    C, P = w.launch_shape()
+    dom_ms, dom_n = dom
+    alg = algorithmic_bytes(dom_name or "", C, cfg.N, P, I, I_eff, w.p_dim)
+    achieved = alg / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    sym = KERNEL_SYMBOL.get(dom_name, "k_" + str(dom_name))
+    tfile = pmc_files(cfg.index, "traffic", args.pmc_dir) if dom_name else None
+    sq = pmc_files(cfg.index, "sq", args.pmc_dir) if dom_name else None
+    traffic = traffic_from_csv(tfile, sym) if tfile else None
+    return {"bound": "hbm", "kernel": dom_name, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "traffic_source": os.path.relpath(tfile, ROOT) if traffic is not None else None,
+            "algorithmic_bytes": alg, "avg_ms": dom_ms, "launches": dom_n,
+            "valu": valu_from_csv(sq, sym) if sq else None,
+            "units_per_launch": {"C": C, "P": P, "N": cfg.N, "I": I, "I_eff": I_eff}}, (C, P, I, I_eff)
+
+
+def rank_share_report(cfg, args, dev):
+    """--rank-share N: time each rank's share of the strong layout alone on this GPU."""
+    from gsr import render as R
+    n = args.rank_share
+    shares = []
+    weights = None
+    for r in range(n):
+        w = Workload(cfg, dev, n, r, "units", args.buckets, "none", comm=False)
+        if cfg.mode == "3d" and w.scaling == "strong":
+            if weights is None:
+                weights = w.weights
+            else:
+                w.balance(weights)
+        el, bd, dom_name, dom = time_steps(w, args.steps, args.warmup)
+        log(f"share {r}/{n}: {1000.0 * el / args.steps:.3f} ms/step ({w.layout})")
+        shares.append({"rank": r, "ms_per_step": 1000.0 * el / args.steps, "views_here": w.views_here,
+                       "layout": w.layout, "kernels_ms": {k: round(v[0], 4) for k, v in sorted(bd.items())},
+                       "I": R.last_stats().get("n_isect", 0)})
+        del w
+        torch.cuda.empty_cache()
+    grad_bytes = cfg.N * (14 if cfg.mode == "3d" else 9) * 4 * (FRAMES_2D if cfg.mode == "2d" else 1)
+    ar = allreduce_ms(grad_bytes, n)
+    worst = max(s["ms_per_step"] for s in shares)
+    units = cfg.views * (FRAMES_2D if cfg.mode == "2d" else 1)
+    return {"n": n, "shares": shares, "max_share_ms": worst, "allreduce_model_ms": ar,
+            "allreduce_model": f"ring 2(n-1)/n x {grad_bytes / 1e6:.1f} MB at {XGMI_LINK_GBS:.0f} GB/s (one link), "
+                               "not overlapped (upper bound)",
+            "projected_ms_per_step": worst + ar, "projected_value": units / ((worst + ar) * 1e-3),
+            "note": "each share timed alone on one GPU, no collectives; projected = max share + all-reduce model"}
+
+
+def main(argv=None):
+    args = parse(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -182,138 +603,40 @@ def main():
     # the driver's scaling runs use the defaults: backend "nccl" (RCCL), one GPU per rank.
     if os.environ.get("GSR_SAME_DEVICE") == "1":
         local = 0
+    dist = None
+    backend = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group(os.environ.get("GSR_DIST_BACKEND", "nccl"))
+        backend = os.environ.get("GSR_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend)
     dev = torch.device("cuda", local)
-
     from gsr import render as R
-    from gsr.scenes import CONFIGS, gaussians2d, gaussians3d, ring_cameras
+    from gsr.scenes import CONFIGS
     cfg = CONFIGS[args.config]
-    C = cfg.views
-    P = C * cfg.width * cfg.height
-    if cfg.mode == "3d":
-        params_cpu = gaussians3d(cfg.N, cfg.seed)
-        V, K = ring_cameras(C, cfg.width, cfg.height)
-        p_dim = 14
-    else:
-        params_cpu = gaussians2d(cfg.N, cfg.width, cfg.height, cfg.seed + rank)
-        V, K = ring_cameras(1, cfg.width, cfg.height)
-        p_dim = 9
-    params = params_cpu.to(dev).requires_grad_(True)
-    Vd, Kd = V.to(dev), K.to(dev)
-    bg = torch.ones(3, device=dev)
-    g = torch.Generator().manual_seed(cfg.seed + 1)
-    if cfg.mode == "3d":
-        v_rgb = torch.randn(C, cfg.height, cfg.width, 3, generator=g).to(dev)
-        v_alpha = torch.randn(C, cfg.height, cfg.width, generator=g).to(dev)
-    else:
-        v_rgb = torch.randn(cfg.height, cfg.width, 3, generator=g).to(dev)
-        v_alpha = torch.randn(cfg.height, cfg.width, generator=g).to(dev)
 
-    bands = args.shard == "bands" and cfg.mode == "3d" and world > 1
-    if bands:
-        # one 6-view job split by tile rows; bands balanced by a full warm-up render's row work
-        from gsr.multiview import band_shard, row_work, sharded_backward_bands
-        th, tw = (cfg.height + 15) // 16, (cfg.width + 15) // 16
-        with torch.no_grad():
-            R.render3d(params, Vd, Kd, cfg.width, cfg.height, bg)
-        weights = row_work(R.tile_work(), C, th, tw)
-        my_band = band_shard(th, world, rank, weights)
+    if args.rank_share > 1:
+        if world > 1:
+            raise SystemExit("--rank-share runs on ONE process")
+        rep = rank_share_report(cfg, args, dev)
+        print(json.dumps({"metric": "projected strong scaling (per-rank shares timed on one GPU)",
+                          "config": {"workload": cfg.name}, "rank_share": rep}), flush=True)
+        return
 
-        def render_band(p, Vs, Ks, band):
-            return R.render3d(p, Vs, Ks, cfg.width, cfg.height, bg, R.RenderOptions3D(band=band))
-    elif cfg.mode == "3d" and world > 1:
-        # all ranks hold the same Gaussians; this rank renders its shard of the 6*world views
-        from gsr.multiview import sharded_backward, view_shard
-        V_all, K_all = ring_cameras(C * world, cfg.width, cfg.height)
-        V_all, K_all = V_all.to(dev), K_all.to(dev)
-        assert view_shard(C * world, world, rank).stop - view_shard(C * world, world, rank).start == C
-        g2 = torch.Generator().manual_seed(cfg.seed + 2)
-        vr_all = torch.randn(C * world, cfg.height, cfg.width, 3, generator=g2).to(dev)
-        va_all = torch.randn(C * world, cfg.height, cfg.width, generator=g2).to(dev)
-
-        def render_views(p, Vs, Ks):
-            return R.render3d(p, Vs, Ks, cfg.width, cfg.height, bg)
-
-    if args.loss != "none":
-        if cfg.mode != "3d" or world > 1:
-            raise SystemExit("--loss: 3D configs on one GPU only")
-        from gsr.loss import render3d_iou_l1
-        g3 = torch.Generator().manual_seed(cfg.seed + 3)
-        timg = torch.rand(C, 3, cfg.height, cfg.width, generator=g3).to(dev)
-        tmask = (torch.rand(C, cfg.height, cfg.width, generator=g3) < 0.3).float().to(dev)
-
-    def step():
-        params.grad = None
-        if args.loss == "fused":
-            li, lm, rgb, alpha = render3d_iou_l1(params, Vd, Kd, cfg.width, cfg.height, bg, timg, tmask, 1.0)
-            (li + lm).backward()
-        elif args.loss == "torch":
-            rgb, alpha = R.render3d(params, Vd, Kd, cfg.width, cfg.height, bg)
-            inter = (alpha * tmask).sum(dim=(-2, -1))
-            union = (alpha + tmask - alpha * tmask).sum(dim=(-2, -1))
-            li = 1 - ((inter + 1e-6) / (union + 1e-6)).mean()
-            lm = torch.abs(timg - rgb.permute(0, 3, 1, 2)).sum() / tmask.sum()
-            (li + lm).backward()
-        elif bands:
-            params.grad = sharded_backward_bands(render_band, params, Vd, Kd, v_rgb, v_alpha, th, weights)
-        elif cfg.mode == "3d" and world > 1:
-            params.grad = sharded_backward(render_views, params, V_all, K_all, vr_all, va_all)
-        elif cfg.mode == "3d" and not cfg.backward:
-            with torch.no_grad():   # config 2 is forward-only
-                R.render3d(params, Vd, Kd, cfg.width, cfg.height, bg)
-        elif cfg.mode == "3d":
-            rgb, alpha = R.render3d(params, Vd, Kd, cfg.width, cfg.height, bg)
-            torch.autograd.backward([rgb, alpha], [v_rgb, v_alpha])
-        else:
-            # 2D: the reference ignores the camera, so every view of a frame is the same image
-            for _ in range(C):
-                rgb, alpha = R.render2d(params, cfg.width, cfg.height, bg)
-                torch.autograd.backward([rgb, alpha], [v_rgb, v_alpha])
-            if world > 1:
-                import torch.distributed as dist
-                dist.all_reduce(params.grad)
-
-    for _ in range(args.warmup):
-        step()
-    # per-call breakdown from a separate profiled pass (every libgsr call bracketed by
-    # events); it also names the dominant kernel
-    torch.cuda.synchronize()
-    R.enable_kernel_timing(True)
-    for _ in range(max(2, min(args.steps, 5))):
-        step()
-    breakdown = R.kernel_times_ms()
-    R.enable_kernel_timing(False)
-    dom_name = max(breakdown.items(), key=lambda kv: kv[1][0] * kv[1][1])[0] if breakdown else None
-    torch.cuda.synchronize()
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-    torch.cuda.synchronize()
-    # timed region: events only around the dominant kernel (its live average duration)
-    R.enable_kernel_timing(True, only={dom_name} if dom_name else None)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    ktimes = R.kernel_times_ms()
-    R.enable_kernel_timing(False)
+    if args.loss != "none" and (cfg.mode != "3d" or world > 1):
+        raise SystemExit("--loss: 3D configs on one GPU only")
+    w = Workload(cfg, dev, world, rank, args.shard, args.buckets, args.loss, comm=True)
+    elapsed, breakdown, dom_name, dom = time_steps(w, args.steps, args.warmup, dist)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
 
-    allreduce_ms = None
+    ar_ms = None
     if world > 1:
-        # the step's one collective, timed on its own: all_reduce(SUM) of the fp32 v_params
-        buf = torch.zeros(cfg.N, p_dim, device=dev)
+        # the step's collective volume timed on its own (10 x all_reduce of the gradient buffer)
+        buf = torch.zeros_like(w.params)
         for _ in range(3):
             dist.all_reduce(buf)
         torch.cuda.synchronize()
@@ -326,27 +649,13 @@ def main():
         torch.cuda.synchronize()
         t = torch.tensor([e0.elapsed_time(e1) / 10], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        allreduce_ms = float(t)
+        ar_ms = float(t)
 
-    st = R.last_stats()
-    I = st.get("n_isect", 0)
-    I_eff = R.effective_isect()
-    views_per_step = C if bands else C * world
-    value = views_per_step * args.steps / elapsed
+    value = w.units_total * args.steps / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
-
-    # dominant kernel (largest total time in the profiled pass), timed live in the region
-    dom_ms, dom_n = ktimes.get(dom_name, (0.0, 0)) if dom_name else (0.0, 0)
-    Pd = P if cfg.mode == "3d" else cfg.width * cfg.height
-    Cd = C if cfg.mode == "3d" else 1
-    alg = algorithmic_bytes(dom_name or "", Cd, cfg.N, Pd, I, I_eff, p_dim)
-    achieved = alg / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
-    traffic = None
-    if args.traffic_csv and dom_name and os.path.exists(args.traffic_csv):
-        traffic = traffic_from_csv(args.traffic_csv, KERNEL_SYMBOL.get(dom_name, "k_" + dom_name))
-    valu = valu_from_csv(DEFAULT_SQ_CSVS, KERNEL_SYMBOL.get(dom_name, "k_" + dom_name)) if dom_name else None
-    sb = step_bytes(Cd, cfg.N, cfg.width * cfg.height, I, I_eff, p_dim, cfg.backward) * (1 if cfg.mode == "3d" else C)
-
+    roof, (C, P, I, I_eff) = roofline(w, dom_name, dom, args)
+    sb = step_bytes(C, cfg.N, P, I, I_eff, w.p_dim, cfg.backward)
+    launches_per_step = max(1, math.ceil(w.views_here / C)) if C else 1
     out = {
         "metric": "rendered frames/sec (%s) at N_gauss x H x W" % ("fwd+bwd" if cfg.backward else "fwd"),
         "value": value,
@@ -356,35 +665,42 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "strong" if bands else "weak",
+        # N=1 carries the label of the layout the same command uses at N>1
+        "scaling": w.scaling if world > 1 else ("weak" if cfg.index == 2 or args.shard == "views" else "strong"),
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (SURVEY.md §8(d) distribution A, seed 1000+config)",
+        "data": "synthetic (SURVEY.md §8(d) distributions, seed 1000+config)",
         "config": {"workload": cfg.name, "N_gauss": cfg.N, "width": cfg.width, "height": cfg.height,
-                   "views_per_gpu": C, "background": "white", "loss": args.loss,
-                   "parallelism": (f"tile-row bands x{world} (band {my_band[0]}-{my_band[1]} on rank 0) + RCCL "
-                                   f"all-reduce of v_params" if bands else
-                                   f"view-sharded x{world} + RCCL all-reduce of v_params" if world > 1 else "single GPU")},
-        "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "algorithmic_bytes": alg, "avg_ms": dom_ms, "launches": dom_n, "valu": valu},
+                   "views": cfg.views, "frames": FRAMES_2D if cfg.mode == "2d" else 1,
+                   "units_per_step": w.units_total, "background": "white", "loss": args.loss,
+                   "parallelism": w.layout + (f"; backend {backend}" if backend else "")},
+        "roofline": roof,
         "kernels_ms": {k: round(v[0], 4) for k, v in sorted(breakdown.items())},
-        "allreduce_ms": allreduce_ms,
-        "sets_per_s": value / C,
-        "pair_evals_per_s": 2.0 * 256.0 * I_eff * (1 if cfg.mode == "3d" else C) * world / (ms_per_step * 1e-3),
-        "step_roofline": {"algorithmic_bytes": sb, "achieved": sb / (ms_per_step * 1e-3) / 1e9,
-                          "unit": "GB/s", "frac": sb / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                          "formula": ("SURVEY.md 8(d): C*N*(12p+136) + 36*I + 80*I_eff + 44*C*P per rank" if cfg.backward
-                                      else "SURVEY.md 8(d) fwd-only: C*N*(4p+32) + 36*I + 40*I_eff + 20*C*P per rank")},
-        "binning": {"I": I, "I_eff": I_eff, "max_list": st.get("max_seg"), "busy_tiles": st.get("n_busy"),
-                    "tiles": st.get("tiles")},
+        "allreduce_ms": ar_ms,
+        "sets_per_s": value / cfg.views,
+        "pair_evals_per_s": 2.0 * 256.0 * I_eff * launches_per_step * world / (ms_per_step * 1e-3),
+        "step_roofline": {"algorithmic_bytes": sb * launches_per_step,
+                          "achieved": sb * launches_per_step / (ms_per_step * 1e-3) / 1e9,
+                          "unit": "GB/s", "frac": sb * launches_per_step / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                          "formula": ("SURVEY.md 8(d): C*N*(12p+136) + 36*I + 80*I_eff + 44*P per rank" if cfg.backward
+                                      else "SURVEY.md 8(d) fwd-only: C*N*(4p+32) + 36*I + 40*I_eff + 20*P per rank")},
+        "binning": {"I": I, "I_eff": I_eff, "max_list": R.last_stats().get("max_seg"),
+                    "busy_tiles": R.last_stats().get("n_busy"), "tiles": R.last_stats().get("tiles")},
     }
+    log(f"timed {args.steps} steps: {1000.0 * elapsed / args.steps:.3f} ms/step")
     if rank == 0 and world == 1 and args.cpu_baseline:
-        cb = cpu_baseline(cfg, params_cpu, V, K, args.cpu_views)
+        log(f"CPU baseline on {cpu_threads(args.cpu_threads)} threads")
+        cb, rgb_o = cpu_baseline(cfg, w.params_cpu if cfg.mode == "3d" else w.params_cpu[0], w.V, w.K,
+                                 cpu_threads(args.cpu_threads))
         out["cpu_baseline"] = cb
         out["speedup_vs_cpu"] = value / cb["value"] if cb["value"] > 0 else None
     else:
         out["cpu_baseline"] = None
+        rgb_o = None
+    if rank == 0 and world == 1 and args.psnr:
+        log("dPSNR vs the oracle")
+        p0 = w.params_cpu if cfg.mode == "3d" else w.params_cpu[0]
+        out["dpsnr"] = delta_psnr(cfg, p0, w.V, w.K, dev, rgb_o)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

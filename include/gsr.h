@@ -114,9 +114,11 @@ int gsr_selftest_lds_order(int32_t* violations, void* stream);
  * all zero -- gsr_bin_offsets resets the counter element and gsr_bin_sort counts the tiles
  * back down, so a buffer that went through project -> offsets -> sort needs no memset.
  * Culled Gaussians get count 0.
- * [band_y0, band_y1): the tile rows this call bins (band_y1 = -1: all rows).  Multi-GPU band
- * sharding gives each rank a band; tiles outside it stay empty (background)
- * and their entries contribute nothing, so the ranks' gradients sum to the full gradient. */
+ * [band_y0, band_y1): the tile rows this call bins, counted over the C cameras' rows laid end
+ * to end (row r of camera c is global row c*th + r, th = ceil(height/16); band_y1 = -1: all
+ * C*th rows).  Multi-GPU (view, band) sharding gives each rank one
+ * contiguous range of (view, row) units; tiles outside it stay empty (background) and their
+ * entries contribute nothing, so the ranks' gradients sum to the full gradient. */
 int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride,
                       const float* viewmats, const float* Ks, int C, int width, int height,
                       float near_plane, float far_plane, float radius_clip, float eps2d,
@@ -124,13 +126,19 @@ int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride,
                       uint32_t* rect, int32_t* isect_count, int32_t* isect_offset, int32_t* tile_count,
                       int tile_count_zeroed, void* stream);
 
-/* 2D projection: params [N, >=9] (layout src/gaussian_renderer.py:314-318).  The tile rect
- * covers every pixel where opacity*exp(-q) >= eps_cut (the reference is dense; eps_cut
- * bounds the dropped mass).  Same outputs as gsr3d_project_fwd with C = 1. */
-int gsr2d_project_fwd(const float* params, int64_t N, int64_t row_stride, int width,
-                      int height, float eps_cut, float* rec, uint32_t* rect,
-                      int32_t* isect_count, int32_t* isect_offset, int32_t* tile_count,
-                      int tile_count_zeroed, void* stream);
+/* 2D projection: F parameter sets params [F][N, >=9] (layout src/gaussian_renderer.py:314-318;
+ * rows row_stride floats apart, sets set_stride floats apart) rendered as C cameras (units):
+ * cameras are grouped by set, set f owning cameras [set_begin[f], set_begin[f+1]) (set_begin:
+ * [F+1] DEVICE int32, set_begin[F] = C; NULL means F = 1 and every camera renders set 0).  The
+ * 2D renderer ignores the camera (src/gaussian_renderer.py:280-281), so a multi-frame batch
+ * (frames x views) is one call with one camera per (frame, view) unit.  The
+ * tile rect covers every pixel where opacity*exp(-q) >= eps_cut (the reference is dense;
+ * eps_cut bounds the dropped mass).  Same outputs as gsr3d_project_fwd (rec [C*N*12], rect,
+ * isect_count / isect_offset [C*N], tile_count [C*tiles + 1]); C*N < 2^31. */
+int gsr2d_project_fwd(const float* params, int64_t N, int64_t row_stride, int64_t set_stride,
+                      const int32_t* set_begin, int F, int C, int width, int height, float eps_cut,
+                      float* rec, uint32_t* rect, int32_t* isect_count, int32_t* isect_offset,
+                      int32_t* tile_count, int tile_count_zeroed, void* stream);
 
 /* ---------------------------------------------------------------- (b) binning */
 
@@ -211,40 +219,47 @@ int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t*
                      const int32_t* k_of_s, float* partial, void* stream);
 
 /* 2D index-order compositor (src/gaussian_renderer.py:416-425), integer pixel centres, on
- * the 3D kernels' structure (C = 1, index-order keys, the forward's chunk records feed a
+ * the 3D kernels' structure (C cameras of gsr2d_project_fwd, index-order keys, the forward's chunk records feed a
  * chunk-parallel backward).  rgb = canvas + (1-A)*bg, alpha = A.  Arithmetic in
  * transmittance form; a pixel stops after the entry that takes T to <= 2^-25 (the
  * reference's A == 1.0f).  Pairs with alpha < eps_cut (the binning's extent cut) are left
- * out.  final_T [H,W,2] = (T_final, T before the pixel's last composited entry). */
+ * out.  bg [C,3]; rgb [C,H,W,3], alpha [C,H,W]; final_T [C,H,W,2] = (T_final, T before the
+ * pixel's last composited entry). */
 int gsr2d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
-                     const int32_t* tile_order, const int32_t* chunk_base, int width, int height,
+                     const int32_t* tile_order, const int32_t* chunk_base, int C, int width, int height,
                      float eps_cut, const float* bg, int32_t n_busy, gsr_bin_stats* stats,
                      float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
                      uint64_t* tile_cut, float* chunk_state, int32_t* chunk_list, void* stream);
 
 /* Backward of gsr2d_raster_fwd (the reference's autograd of the recursion), same contract
- * as gsr3d_raster_bwd with C = 1. */
+ * as gsr3d_raster_bwd. */
 int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_end, const int32_t* chunk_base, const float* chunk_state,
                      const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
-                     int width, int height, float eps_cut, const float* bg,
+                     int C, int width, int height, float eps_cut, const float* bg,
                      const float* final_T, const int32_t* last, const float* v_rgb,
                      const float* v_alpha, const int32_t* k_of_s, float* partial, void* stream);
 
 /* ---------------------------------------------------------------- projection backward */
 
 /* Reduce the partial rows of each (c,n) (those below their tile's cut, in row order),
- * chain through projection and the adapter activations, sum over cameras: v_params [N,14]
- * (fully overwritten, deterministic).  depth: the projection's depth array (sort keys). */
+ * chain through projection and the adapter activations, sum over cameras: rows
+ * [n_begin, n_end) of v_params [N,14] (fully overwritten, deterministic; n_end = -1: N).
+ * Gaussian ranges let a multi-GPU caller start the all-reduce of finished rows while later
+ * ranges are still being computed.  depth: the projection's depth array (sort keys). */
 int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride,
                       const float* viewmats, const float* Ks, int C, int width, int height,
                       float eps2d, int input_mode, const float* depth, const uint32_t* rect,
                       const int32_t* isect_offset, const int32_t* isect_count,
-                      const uint64_t* tile_cut, const float* partial, float* v_params,
-                      void* stream);
+                      const uint64_t* tile_cut, const float* partial, int64_t n_begin,
+                      int64_t n_end, float* v_params, void* stream);
 
-int gsr2d_project_bwd(const float* params, int64_t N, int64_t row_stride, int width,
-                      int height, const uint32_t* rect, const int32_t* isect_offset,
+/* 2D: v_params [F,N,9] (fully overwritten): set f's gradient sums the partial rows of all its
+ * cameras (set_begin as in gsr2d_project_fwd, NULL: F = 1) in camera order, then chains
+ * through the activations once. */
+int gsr2d_project_bwd(const float* params, int64_t N, int64_t row_stride, int64_t set_stride,
+                      const int32_t* set_begin, int F, int C, int width, int height,
+                      const uint32_t* rect, const int32_t* isect_offset,
                       const int32_t* isect_count, const uint64_t* tile_cut,
                       const float* partial, float* v_params, void* stream);
 

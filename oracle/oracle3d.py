@@ -170,9 +170,10 @@ def isect_tiles(means2d, radii, depths, width, height, tile=Ref3D.TILE, depth_or
     """SURVEY.md Appendix A.2.  Returns (tile_offsets [C*T+1] int64, ids [I] int64).
 
     ids are flatten ids c*N+n; list order within a tile is (depth float bits, c*N+n) when
-    ``depth_order`` (3D), else parameter index order (2D).  ``band`` = (y0, y1) tile rows
-    restricts binning to those rows (the build's multi-GPU band sharding, not a reference
-    feature; the full-image result restricted to the band is unchanged).
+    ``depth_order`` (3D), else parameter index order (2D).  ``band`` = (y0, y1) restricts
+    binning to those tile rows, counted over the C cameras' rows laid end to end (row r of
+    camera c is global row c*th + r) -- the build's multi-GPU (view, band) sharding, not a
+    reference feature; the full-image result restricted to the band is unchanged.
     """
     C, N = depths.shape
     tw = (width + tile - 1) // tile
@@ -191,8 +192,9 @@ def isect_tiles(means2d, radii, depths, width, height, tile=Ref3D.TILE, depth_or
         y0 = torch.clamp(torch.floor(tile_y - try_), min=0, max=th).to(torch.int64)
         y1 = torch.clamp(torch.ceil(tile_y + try_), min=0, max=th).to(torch.int64)
         if band is not None:
-            y0 = y0.clamp(min=band[0])
-            y1 = y1.clamp(max=band[1])
+            cam_row = torch.arange(C, dtype=torch.int64)[:, None] * th
+            y0 = torch.maximum(y0, (band[0] - cam_row).clamp(0, th))
+            y1 = torch.minimum(y1, (band[1] - cam_row).clamp(0, th))
         live = (radii[..., 0] > 0) | (radii[..., 1] > 0)
         wcnt = torch.where(live, (x1 - x0).clamp(min=0), torch.zeros_like(x0))
         hcnt = torch.where(live, (y1 - y0).clamp(min=0), torch.zeros_like(y0))

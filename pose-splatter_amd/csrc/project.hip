@@ -96,6 +96,9 @@ __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
     __syncthreads();
   }
   const Cam cam = load_cam(viewmats + c * 16, Ks + c * 9);
+  // this camera's share of the band [band_y0, band_y1) of camera-major global tile rows
+  // (row r of camera c is global row c*th + r)
+  const int by0 = min(max(band_y0 - c * th, 0), th), by1 = min(max(band_y1 - c * th, 0), th);
   const int64_t n0 = (int64_t)blockIdx.x * kProjPerBlock;
   const int64_t n1 = min(N, n0 + kProjPerBlock);
   for (int64_t n = n0 + threadIdx.x; n < n1; n += blockDim.x) {
@@ -141,8 +144,8 @@ __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
       y0 = (int)fminf(fmaxf(floorf(tiy - try_), 0.f), (float)th);
       y1 = (int)fminf(fmaxf(ceilf(tiy + try_), 0.f), (float)th);
       // tile-row band of this rank (multi-GPU band sharding; the full image by default)
-      y0 = max(y0, band_y0);
-      y1 = min(y1, band_y1);
+      y0 = max(y0, by0);
+      y1 = min(y1, by1);
       if (x1 < x0) x1 = x0;
       if (y1 < y0) y1 = y0;
       // record: the compositing inputs plus the per-Gaussian constants of the exact sub-tile
@@ -162,14 +165,30 @@ __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
   alloc_offsets(s_cnt, (int)(n1 - n0), (int64_t)c * N + n0, counter, isect_offset);
 }
 
+// Parameter set of camera c: cameras are grouped by set, set f owning cameras
+// [set_begin[f], set_begin[f+1]) (null: one set).  Uniform per workgroup (scalar loads).
+__device__ __forceinline__ int set_of_camera(const int32_t* __restrict__ set_begin, int F, int c) {
+  if (set_begin == nullptr) return 0;
+  int f = 0;
+  while (f + 1 < F && set_begin[f + 1] <= c) ++f;
+  return f;
+}
+
+// Camera c = blockIdx.y renders parameter set set_of_camera(c) (multi-frame batches: every
+// (frame, view) unit is one camera; the 2D renderer ignores the camera itself,
+// src/gaussian_renderer.py:280-281, so the views of a frame are identical renders).
 __global__ __launch_bounds__(kProjThreads) void k_project2d_fwd(
-    const float* __restrict__ params, int64_t N, int64_t stride, int W, int H, float eps_cut,
+    const float* __restrict__ params, int64_t N, int64_t stride, int64_t set_stride,
+    const int32_t* __restrict__ set_begin, int F, int C, int W, int H, float eps_cut,
     int tw, int th, int use_lds, Splat* __restrict__ rec, uint2* __restrict__ rect,
-    int32_t* __restrict__ cnt, int32_t* __restrict__ tile_count, int32_t* __restrict__ counter,
-    int32_t* __restrict__ isect_offset) {
+    int32_t* __restrict__ cnt, int32_t* __restrict__ tile_count, int32_t* __restrict__ isect_offset) {
   extern __shared__ int hist[];
   __shared__ int s_cnt[kProjPerBlock];
+  const int c = blockIdx.y;
   const int T = tw * th;
+  int32_t* gcount = tile_count + (int64_t)c * T;
+  int32_t* counter = tile_count + (int64_t)C * T;
+  const float* pset = params + (int64_t)set_of_camera(set_begin, F, c) * set_stride;
   if (use_lds) {
     for (int t = threadIdx.x; t < T; t += blockDim.x) hist[t] = 0;
     __syncthreads();
@@ -177,7 +196,8 @@ __global__ __launch_bounds__(kProjThreads) void k_project2d_fwd(
   const int64_t n0 = (int64_t)blockIdx.x * kProjPerBlock;
   const int64_t n1 = min(N, n0 + kProjPerBlock);
   for (int64_t n = n0 + threadIdx.x; n < n1; n += blockDim.x) {
-    const Geo2D g = geo2d(params + n * stride);
+    const int64_t cn = (int64_t)c * N + n;
+    const Geo2D g = geo2d(pset + n * stride);
     int x0 = 0, x1 = 0, y0 = 0, y1 = 0;
     bool ok = g.op > eps_cut && isfinite(g.u) && isfinite(g.v);
     if (ok) {
@@ -213,14 +233,14 @@ __global__ __launch_bounds__(kProjThreads) void k_project2d_fwd(
       s.p0 = make_float4(g.u, g.v, g.op, logf(g.op / eps_cut));
       s.p1 = make_float4(g.a, g.b, g.c, -g.b / (2.f * g.c));
       s.p2 = make_float4(g.col[0], g.col[1], g.col[2], -g.b / (2.f * g.a));
-      rec[n] = s;
-      hist_add(hist, tile_count, use_lds, x0, x1, y0, y1, tw);
+      rec[cn] = s;
+      hist_add(hist, gcount, use_lds, x0, x1, y0, y1, tw);
     }
-    rect[n] = make_uint2(pack_rect_lo(x0, x1), pack_rect_lo(y0, y1));
-    cnt[n] = s_cnt[n - n0] = (x1 - x0) * (y1 - y0);
+    rect[cn] = make_uint2(pack_rect_lo(x0, x1), pack_rect_lo(y0, y1));
+    cnt[cn] = s_cnt[n - n0] = (x1 - x0) * (y1 - y0);
   }
-  if (use_lds) hist_flush(hist, tile_count, T);
-  alloc_offsets(s_cnt, (int)(n1 - n0), n0, counter, isect_offset);
+  if (use_lds) hist_flush(hist, gcount, T);
+  alloc_offsets(s_cnt, (int)(n1 - n0), (int64_t)c * N + n0, counter, isect_offset);
 }
 
 }  // namespace gsr
@@ -247,9 +267,9 @@ int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride, const 
               "gsr3d_project_fwd: bad input_mode %d", input_mode);
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   GSR_REQUIRE(tw < 65536 && th < 65536, "gsr3d_project_fwd: image too large");
-  if (band_y1 < 0) band_y1 = th;
-  GSR_REQUIRE(band_y0 >= 0 && band_y0 <= band_y1 && band_y1 <= th, "gsr3d_project_fwd: bad band [%d,%d) of %d tile rows",
-              band_y0, band_y1, th);
+  if (band_y1 < 0) band_y1 = C * th;
+  GSR_REQUIRE(band_y0 >= 0 && band_y0 <= band_y1 && (int64_t)band_y1 <= (int64_t)C * th,
+              "gsr3d_project_fwd: bad band [%d,%d) of %d x %d tile rows", band_y0, band_y1, C, th);
   // tile histogram [C*T] and the emission counter (element C*T) in one memset, unless the
   // caller's buffer is already zero (left so by the previous offsets + sort on it)
   if (!tile_count_zeroed && hipMemsetAsync(tile_count, 0, ((size_t)C * tw * th + 1) * sizeof(int32_t), (hipStream_t)stream) != hipSuccess) {
@@ -276,16 +296,23 @@ int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride, const 
   return GSR_OK;
 }
 
-int gsr2d_project_fwd(const float* params, int64_t N, int64_t row_stride, int width, int height,
+int gsr2d_project_fwd(const float* params, int64_t N, int64_t row_stride, int64_t set_stride,
+                      const int32_t* set_begin, int F, int C, int width, int height,
                       float eps_cut, float* rec, uint32_t* rect, int32_t* isect_count,
                       int32_t* isect_offset, int32_t* tile_count, int tile_count_zeroed, void* stream) {
   GSR_REQUIRE(N >= 0, "gsr2d_project_fwd: bad N=%lld", (long long)N);
+  GSR_REQUIRE(C >= 1 && C <= 65535 && F >= 1, "gsr2d_project_fwd: bad C=%d or F=%d", C, F);
+  GSR_REQUIRE(set_begin != nullptr || F == 1, "gsr2d_project_fwd: F=%d sets need set_begin", F);
+  GSR_REQUIRE((int64_t)C * N < (1ll << 31), "gsr2d_project_fwd: C*N too large for 32-bit ids");
   GSR_REQUIRE(width > 0 && height > 0, "gsr2d_project_fwd: bad image %dx%d", width, height);
   GSR_REQUIRE(row_stride >= 9, "gsr2d_project_fwd: row_stride %lld < 9", (long long)row_stride);
+  GSR_REQUIRE(F == 1 || set_stride >= N * row_stride, "gsr2d_project_fwd: set_stride %lld < N*row_stride",
+              (long long)set_stride);
   GSR_REQUIRE(eps_cut > 0.f && eps_cut < 1.f, "gsr2d_project_fwd: eps_cut must be in (0,1)");
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   GSR_REQUIRE(tw < 65536 && th < 65536, "gsr2d_project_fwd: image too large");
-  if (!tile_count_zeroed && hipMemsetAsync(tile_count, 0, ((size_t)tw * th + 1) * sizeof(int32_t), (hipStream_t)stream) != hipSuccess) {
+  if (!tile_count_zeroed &&
+      hipMemsetAsync(tile_count, 0, ((size_t)C * tw * th + 1) * sizeof(int32_t), (hipStream_t)stream) != hipSuccess) {
     set_error("gsr2d_project_fwd: tile_count memset failed");
     return GSR_ELAUNCH;
   }
@@ -293,9 +320,9 @@ int gsr2d_project_fwd(const float* params, int64_t N, int64_t row_stride, int wi
   const int T = tw * th;
   const int use_lds = T <= kHistMaxTiles;
   const size_t lds = use_lds ? (size_t)T * sizeof(int) : 0;
-  hipLaunchKernelGGL(k_project2d_fwd, dim3(ceil_div(N, kProjPerBlock)), dim3(kProjThreads), lds,
-                     (hipStream_t)stream, params, N, row_stride, width, height, eps_cut, tw, th,
-                     use_lds, (Splat*)rec, (uint2*)rect, isect_count, tile_count, tile_count + T, isect_offset);
+  hipLaunchKernelGGL(k_project2d_fwd, dim3(ceil_div(N, kProjPerBlock), C), dim3(kProjThreads), lds,
+                     (hipStream_t)stream, params, N, row_stride, set_stride, set_begin, F, C, width, height,
+                     eps_cut, tw, th, use_lds, (Splat*)rec, (uint2*)rect, isect_count, tile_count, isect_offset);
   GSR_LAUNCH_CHECK("k_project2d_fwd");
   return GSR_OK;
 }

@@ -71,13 +71,13 @@ __global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
     const uint2* __restrict__ rect,
     const int32_t* __restrict__ isect_offset, const int32_t* __restrict__ isect_count,
     const float* __restrict__ depth, const uint64_t* __restrict__ tile_cut, const float* __restrict__ partial,
-    int CPB, int G, float* __restrict__ v_params) {
+    int CPB, int G, int64_t n_begin, int64_t n_end, float* __restrict__ v_params) {
   __shared__ float s_con[kBwdThreads][kContrib + 1];
   __shared__ int s_any[kBwdThreads];
   const int g_loc = threadIdx.x % G;
   const int slot = threadIdx.x / G;
-  const int64_t n = (int64_t)blockIdx.x * G + g_loc;
-  const bool active = slot < CPB && n < N;
+  const int64_t n = n_begin + (int64_t)blockIdx.x * G + g_loc;
+  const bool active = slot < CPB && n < n_end;
   const int T = tw * th;
   float v_m[3] = {0.f, 0.f, 0.f};
   float v_M[9];
@@ -211,7 +211,7 @@ __global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
     s_any[threadIdx.x] = any;
   }
   __syncthreads();
-  if (slot != 0 || n >= N) return;
+  if (slot != 0 || n >= n_end) return;
   any = 0;
   for (int sl = 1; sl < CPB; ++sl) {
     const float* d = s_con[sl * G + g_loc];
@@ -278,25 +278,37 @@ __global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
   out[13] = v_op * a.op * (1.f - a.op);
 }
 
+// Thread per (parameter set f, Gaussian n): the partial rows of every camera of the set
+// (cameras [set_begin[f], set_begin[f+1]), in camera order) are summed first -- the 2D chain
+// below is linear in them and the same for every view of a set -- then chained once.
 __global__ __launch_bounds__(kBwdThreads) void k_project2d_bwd(
-    const float* __restrict__ params, int64_t N, int64_t stride, int tw, int th, const uint2* __restrict__ rect,
+    const float* __restrict__ params, int64_t N, int64_t stride, int64_t set_stride,
+    const int32_t* __restrict__ set_begin, int F, int n_cam, int tw, int th, const uint2* __restrict__ rect,
     const int32_t* __restrict__ isect_offset, const int32_t* __restrict__ isect_count,
     const uint64_t* __restrict__ tile_cut, const float* __restrict__ partial, float* __restrict__ v_params) {
-  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  float* out = v_params + n * 9;
-  if (isect_count[n] <= 0) {
+  const int64_t fn = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (fn >= (int64_t)F * N) return;
+  const int f = (int)(fn / N);
+  const int64_t n = fn - (int64_t)f * N;
+  const int c0 = set_begin ? set_begin[f] : 0, c1 = set_begin ? set_begin[f + 1] : n_cam;
+  float* out = v_params + fn * 9;
+  float acc[kPartial];
+#pragma unroll
+  for (int v = 0; v < kPartial; ++v) acc[v] = 0.f;
+  bool any = false;
+  for (int c = c0; c < c1; ++c) {
+    const int64_t cn = (int64_t)c * N + n;
+    if (isect_count[cn] <= 0) continue;
+    any = true;
+    const uint64_t key = ((uint64_t)(uint32_t)cn << 32) | (uint64_t)(uint32_t)cn;   // sort_key, index order
+    gather_partials(rect[cn], tw, (int64_t)c * tw * th, key, isect_offset[cn], tile_cut, partial, acc);
+  }
+  if (!any) {
 #pragma unroll
     for (int k = 0; k < 9; ++k) out[k] = 0.f;
     return;
   }
-  float acc[kPartial];
-#pragma unroll
-  for (int v = 0; v < kPartial; ++v) acc[v] = 0.f;
-  const uint64_t key = ((uint64_t)(uint32_t)n << 32) | (uint64_t)(uint32_t)n;   // sort_key, index order
-  gather_partials(rect[n], tw, 0, key, isect_offset[n], tile_cut, partial, acc);
-  (void)th;
-  const Geo2D g = geo2d(params + n * stride);
+  const Geo2D g = geo2d(params + (int64_t)f * set_stride + n * stride);
   const float va = acc[2], vb = acc[3], vc = acc[4];
   const float C = g.cs, S = g.sn;
   const float C2 = C * C, S2 = S * S, CS = C * S;
@@ -327,32 +339,38 @@ int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride, const 
                       int C, int width, int height, float eps2d, int input_mode, const float* depth,
                       const uint32_t* rect,
                       const int32_t* isect_offset, const int32_t* isect_count, const uint64_t* tile_cut,
-                      const float* partial, float* v_params, void* stream) {
+                      const float* partial, int64_t n_begin, int64_t n_end, float* v_params, void* stream) {
   GSR_REQUIRE(N >= 0 && C >= 1 && width > 0 && height > 0, "gsr3d_project_bwd: bad arguments");
   GSR_REQUIRE(row_stride >= 14, "gsr3d_project_bwd: row_stride < 14");
   GSR_REQUIRE(input_mode == GSR_INPUT_ADAPTER || input_mode == GSR_INPUT_GSPLAT,
               "gsr3d_project_bwd: bad input_mode %d", input_mode);
-  if (N == 0) return GSR_OK;
+  if (n_end < 0) n_end = N;
+  GSR_REQUIRE(n_begin >= 0 && n_begin <= n_end && n_end <= N, "gsr3d_project_bwd: bad Gaussian range [%lld,%lld) of %lld",
+              (long long)n_begin, (long long)n_end, (long long)N);
+  if (n_end == n_begin) return GSR_OK;
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   const int CPB = C < kBwdThreads ? C : kBwdThreads;   // camera slots per Gaussian
   const int G = kBwdThreads / CPB;                       // Gaussians per workgroup
-  hipLaunchKernelGGL(k_project3d_bwd, dim3(ceil_div(N, G)), dim3(kBwdThreads), 0, (hipStream_t)stream, params, N,
+  hipLaunchKernelGGL(k_project3d_bwd, dim3(ceil_div(n_end - n_begin, G)), dim3(kBwdThreads), 0, (hipStream_t)stream, params, N,
                      row_stride, viewmats, Ks, C, width, height, eps2d, input_mode, tw, th, (const uint2*)rect,
-                     isect_offset, isect_count, depth, tile_cut, partial, CPB, G, v_params);
+                     isect_offset, isect_count, depth, tile_cut, partial, CPB, G, n_begin, n_end, v_params);
   GSR_LAUNCH_CHECK("k_project3d_bwd");
   return GSR_OK;
 }
 
-int gsr2d_project_bwd(const float* params, int64_t N, int64_t row_stride, int width, int height,
+int gsr2d_project_bwd(const float* params, int64_t N, int64_t row_stride, int64_t set_stride,
+                      const int32_t* set_begin, int F, int C, int width, int height,
                       const uint32_t* rect, const int32_t* isect_offset, const int32_t* isect_count,
                       const uint64_t* tile_cut, const float* partial, float* v_params, void* stream) {
   GSR_REQUIRE(N >= 0 && width > 0 && height > 0, "gsr2d_project_bwd: bad arguments");
+  GSR_REQUIRE(C >= 1 && F >= 1 && (set_begin != nullptr || F == 1), "gsr2d_project_bwd: bad C=%d / F=%d", C, F);
   GSR_REQUIRE(row_stride >= 9, "gsr2d_project_bwd: row_stride < 9");
+  GSR_REQUIRE(F == 1 || set_stride >= N * row_stride, "gsr2d_project_bwd: set_stride < N*row_stride");
   if (N == 0) return GSR_OK;
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
-  hipLaunchKernelGGL(k_project2d_bwd, dim3(ceil_div(N, kBwdThreads)), dim3(kBwdThreads), 0, (hipStream_t)stream,
-                     params, N, row_stride, tw, th, (const uint2*)rect, isect_offset, isect_count, tile_cut, partial,
-                     v_params);
+  hipLaunchKernelGGL(k_project2d_bwd, dim3(ceil_div((int64_t)F * N, kBwdThreads)), dim3(kBwdThreads), 0,
+                     (hipStream_t)stream, params, N, row_stride, set_stride, set_begin, F, C, tw, th,
+                     (const uint2*)rect, isect_offset, isect_count, tile_cut, partial, v_params);
   GSR_LAUNCH_CHECK("k_project2d_bwd");
   return GSR_OK;
 }

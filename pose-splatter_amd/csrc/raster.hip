@@ -908,12 +908,12 @@ int gsr3d_raster_bwd_loss(const float* rec, const int32_t* sorted_ids, const int
 }
 
 int gsr2d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
-                     const int32_t* tile_order, const int32_t* chunk_base, int width, int height, float eps_cut,
+                     const int32_t* tile_order, const int32_t* chunk_base, int C, int width, int height, float eps_cut,
                      const float* bg, int32_t n_busy, gsr_bin_stats* stats, float* rgb, float* alpha,
                      float* final_T, int32_t* last, int32_t* tile_end, uint64_t* tile_cut, float* chunk_state,
                      int32_t* chunk_list, void* stream) {
   GSR_REQUIRE(eps_cut > 0.f && eps_cut < 1.f, "gsr2d_raster_fwd: eps_cut must be in (0,1)");
-  return raster_fwd<true>("gsr2d_raster_fwd", rec, nullptr, sorted_ids, tile_offset, tile_order, chunk_base, 1, width,
+  return raster_fwd<true>("gsr2d_raster_fwd", rec, nullptr, sorted_ids, tile_offset, tile_order, chunk_base, C, width,
                           height, eps_cut, bg, n_busy, stats, rgb, alpha, final_T, last, tile_end, tile_cut,
                           chunk_state, chunk_list, stream);
 }
@@ -921,13 +921,13 @@ int gsr2d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t*
 int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_end, const int32_t* chunk_base,
                      const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
-                     int width, int height, float eps_cut, const float* bg, const float* final_T,
+                     int C, int width, int height, float eps_cut, const float* bg, const float* final_T,
                      const int32_t* last, const float* v_rgb, const float* v_alpha, const int32_t* k_of_s,
                      float* partial, void* stream) {
   GSR_REQUIRE(eps_cut > 0.f && eps_cut < 1.f, "gsr2d_raster_bwd: eps_cut must be in (0,1)");
   const gsr_loss_terms none{};
   return raster_bwd<false, true>("gsr2d_raster_bwd", rec, sorted_ids, tile_offset, tile_end, chunk_base,
-                                 chunk_state, chunk_list, stats, n_chunks, 1, width, height, eps_cut, bg,
+                                 chunk_state, chunk_list, stats, n_chunks, C, width, height, eps_cut, bg,
                                  final_T, last, v_rgb, v_alpha, none, k_of_s, partial, stream);
 }
 

@@ -63,7 +63,8 @@ EXPORTS = {
     "gsr_selftest_lds_order": (ctypes.c_int, [_P, _P]),
     "gsr3d_project_fwd": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _I32, _I32, _I32, _F, _F, _F, _F,
                                          _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _I32, _P]),
-    "gsr2d_project_fwd": (ctypes.c_int, [_P, _I64, _I64, _I32, _I32, _F, _P, _P, _P, _P, _P, _I32, _P]),
+    "gsr2d_project_fwd": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I32, _I32, _I32, _I32, _F, _P, _P, _P,
+                                         _P, _P, _I32, _P]),
     "gsr_bin_offsets": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P, _P, _P]),
     "gsr_bin_sort_workspace": (_SZ, [_I64, _I64]),
     "gsr_bin_emit": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I32, _P, _P, _SZ, _P]),
@@ -73,13 +74,14 @@ EXPORTS = {
                                         _P, _P, _P, _P, _P, _P, _P]),
     "gsr3d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P,
                                         _P, _P, _P, _P, _P, _P, _P]),
-    "gsr2d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _F, _P, _I32, _P, _P, _P, _P, _P,
+    "gsr2d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _I32, _P, _P, _P, _P, _P,
                                         _P, _P, _P, _P, _P]),
-    "gsr2d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _P,
+    "gsr2d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _F, _P, _P,
                                         _P, _P, _P, _P, _P, _P]),
     "gsr3d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _I32, _I32, _I32, _F, _I32, _P, _P,
-                                         _P, _P, _P, _P, _P, _P]),
-    "gsr2d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
+                                         _P, _P, _P, _P, _I64, _I64, _P, _P]),
+    "gsr2d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P,
+                                         _P, _P]),
     "gsr_loss_workspace": (_SZ, [_I32, _I32, _I32]),
     "gsr_loss_iou_l1_fwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _SZ, _P, _P, _P, _P]),
     "gsr3d_raster_bwd_loss": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P,

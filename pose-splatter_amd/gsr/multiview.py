@@ -8,11 +8,19 @@ code at all; this is the MI355X design, not a translation.
 * ``view_shard`` — contiguous, balanced split of C views over ``world`` ranks.
 * ``sharded_backward`` — render this rank's views, backprop the caller's cotangents, and
   all-reduce the parameter gradient so every rank ends with the full multi-view gradient.
-* ``band_shard`` / ``sharded_backward_bands`` — when there are fewer views than GPUs (config
-  3/5: 6 views on 8 GPUs), every rank renders ALL views but bins only its
-  band of tile rows (``RenderOptions3D.band``); bands are balanced by per-row work (e.g. the
-  previous step's per-row list lengths).  Projection is repeated on every rank (O(N) work);
-  the raster work splits.  The same single all-reduce sums the gradients.
+* ``unit_shard`` / ``sharded_backward_units`` — STRONG scaling of one multi-view job (config
+  3/5: 6 views on 8 GPUs).  The work units are (view, tile row); laid out
+  view-major they form C*th "global rows", which are cut into ``world`` contiguous ranges of
+  balanced work (per-row list lengths of a previous render).  A rank therefore touches one
+  or two views (plus whole views in between when C > world) and projects ONLY those, binning
+  only its rows (``RenderOptions3D.band`` in global rows).  Its partial v_params is
+  all-reduced in Gaussian-range buckets, each launched as soon as the projection backward
+  has enqueued its rows, so the collective overlaps the remaining backward.
+* ``frame_view_units`` / ``sharded_backward_frames`` — config 4 (2D, 8 frames x 6 views = 48
+  units): unit u = f*V + v goes to rank u % world, so every frame's views span ranks; each
+  rank renders all its units in ONE batched launch sequence per frame bucket
+  (``gsr.render.render2d_units``) and the [F,N,9] gradient is all-reduced per frame bucket
+  (async, overlapping the next bucket's render).
 """
 from __future__ import annotations
 
@@ -21,7 +29,8 @@ from typing import Callable
 import torch
 import torch.distributed as dist
 
-__all__ = ["view_shard", "sharded_backward", "band_shard", "sharded_backward_bands", "row_work"]
+__all__ = ["view_shard", "sharded_backward", "band_shard", "row_work", "unit_shard", "sharded_backward_units",
+           "frame_view_units", "frame_buckets", "sharded_backward_frames", "bucket_bounds"]
 
 
 def view_shard(C: int, world: int, rank: int) -> slice:
@@ -91,22 +100,105 @@ def row_work(stats_tile_len, C: int, th: int, tw: int):
     return [float(x) for x in t.cpu()]
 
 
-def sharded_backward_bands(render_band: Callable, params: torch.Tensor, viewmats: torch.Tensor, Ks: torch.Tensor,
-                           v_rgb: torch.Tensor, v_alpha: torch.Tensor, rows: int, weights=None,
+def unit_shard(C: int, rows: int, world: int, rank: int, weights=None) -> tuple:
+    """This rank's contiguous share of the C*rows (view, tile row) units, view-major, balanced by
+    ``weights`` (C*rows per-unit work; uniform if None).  Returns (v0, v1, band): the views
+    [v0, v1) the rank touches and its rows as a band of global rows relative to view v0 (the
+    ``RenderOptions3D.band`` of a render of views v0..v1-1).  An empty share gives v0 == v1."""
+    g0, g1 = band_shard(C * rows, world, rank, weights)
+    if g1 <= g0:
+        return 0, 0, (0, 0)
+    v0, v1 = g0 // rows, (g1 - 1) // rows + 1
+    return v0, v1, (g0 - v0 * rows, g1 - v0 * rows)
+
+
+def bucket_bounds(n: int, buckets: int) -> list:
+    """Gaussian-range bucket boundaries used by gsr.render's bucketed projection backward."""
+    nb = max(1, min(int(buckets), n)) if n > 0 else 1
+    return [n * k // nb for k in range(nb + 1)]
+
+
+def sharded_backward_units(render_band: Callable, params: torch.Tensor, viewmats: torch.Tensor, Ks: torch.Tensor,
+                           v_rgb: torch.Tensor, v_alpha: torch.Tensor, rows: int, weights=None, buckets: int = 0,
                            group=None) -> torch.Tensor:
-    """Gradient of sum(rgb*v_rgb + alpha*v_alpha) over all views, band-sharded: this rank
-    renders every view but only its tile rows (``render_band(params, viewmats, Ks, band)``),
-    backprops, and all-reduces.  Returns the summed gradient (identical on every rank)."""
+    """Gradient of sum(rgb*v_rgb + alpha*v_alpha) over all C views, (view, row)-unit sharded.
+
+    ``render_band(p, viewmats_sub, Ks_sub, band, hook)`` renders views v0..v1-1 binned to
+    ``band``.  With ``buckets`` > 0 it must produce the gradient in ``bucket_bounds(N,
+    buckets)`` Gaussian ranges and call ``hook(rows)`` with each range as soon as it is
+    enqueued (gsr.render: ``RenderOptions3D(grad_buckets=buckets, grad_hook=hook)``); each
+    range is all-reduced asynchronously at once, overlapping the remaining backward.  With
+    ``buckets`` == 0 one all-reduce follows the backward.  Returns the summed gradient
+    (identical on every rank)."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    band = band_shard(rows, world, rank, weights)
+    v0, v1, band = unit_shard(viewmats.shape[0], rows, world, rank, weights)
     p = params.detach().requires_grad_(True)
-    if band[1] > band[0]:
-        rgb, alpha = render_band(p, viewmats, Ks, band)
-        torch.autograd.backward([rgb, alpha], [v_rgb, v_alpha])
+    pieces, works = [], []
+
+    def hook(t):
+        pieces.append(t)
+        if world > 1:
+            works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True))
+
+    use_hook = buckets > 0
+    if v1 > v0:
+        rgb, alpha = render_band(p, viewmats[v0:v1], Ks[v0:v1], band, hook if use_hook else None)
+        torch.autograd.backward([rgb, alpha], [v_rgb[v0:v1], v_alpha[v0:v1]])
         grad = p.grad
     else:
         grad = torch.zeros_like(p)
+        if use_hook:   # same collectives, same sizes, on every rank
+            b = bucket_bounds(p.shape[0], buckets)
+            for n0, n1 in zip(b[:-1], b[1:]):
+                hook(grad[n0:n1])
+    if use_hook:
+        for w in works:
+            w.wait()
+        return pieces[0] if len(pieces) == 1 and pieces[0].shape == p.shape else torch.cat(pieces)
     if world > 1:
         dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=group)
+    return grad
+
+
+def frame_view_units(F: int, V: int, world: int, rank: int) -> list:
+    """(frame, view) units of ``rank``: unit u = f*V + v goes to rank u % world (round robin), so
+    each frame's views span ranks.  Grouped by frame."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} of world {world}")
+    return [(u // V, u % V) for u in range(F * V) if u % world == rank]
+
+
+def frame_buckets(F: int, buckets: int) -> list:
+    """Frame ranges [f0, f1) of the all-reduce buckets (identical on every rank)."""
+    nb = max(1, min(int(buckets), F))
+    return [(F * k // nb, F * (k + 1) // nb) for k in range(nb)]
+
+
+def sharded_backward_frames(render_units: Callable, params: torch.Tensor, units: list, v_rgb: torch.Tensor,
+                            v_alpha: torch.Tensor, buckets: int = 2, group=None) -> torch.Tensor:
+    """Multi-frame 2D step (config 4).  params [F,N,9]: every rank holds all F frames' sets;
+    ``units``: this rank's (frame, view) units, grouped by frame (``frame_view_units``);
+    v_rgb [len(units),H,W,3] / v_alpha [len(units),H,W]: their cotangents.  The frames are cut
+    into ``buckets`` ranges; per range the rank renders its units in one batched sequence
+    (``render_units(params_range [Fr,N,9], unit_sets) -> (rgb [u,H,W,3], alpha [u,H,W])``),
+    backprops, and launches an async all-reduce of the range's [Fr,N,9] gradient, which runs
+    while the next range renders.  Returns the summed gradient [F,N,9] (identical on every rank)."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    F = params.shape[0]
+    grad = torch.zeros_like(params)
+    works = []
+    for f0, f1 in frame_buckets(F, buckets):
+        idx = [i for i, (f, _) in enumerate(units) if f0 <= f < f1]
+        if idx:
+            p = params[f0:f1].detach().requires_grad_(True)
+            sets = [units[i][0] - f0 for i in idx]
+            rgb, alpha = render_units(p, sets)
+            a, b = idx[0], idx[-1] + 1   # units are grouped by frame: a contiguous range
+            torch.autograd.backward([rgb, alpha], [v_rgb[a:b], v_alpha[a:b]])
+            grad[f0:f1].copy_(p.grad)
+        if world > 1:
+            works.append(dist.all_reduce(grad[f0:f1], op=dist.ReduceOp.SUM, group=group, async_op=True))
+    for w in works:
+        w.wait()
     return grad

@@ -10,14 +10,14 @@ way).  Intermediates live in two arenas per forward (see ``_Arena``).
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import torch
 
 from . import _lib
 from ._lib import check, lib
 
-__all__ = ["render3d", "render2d", "RenderOptions3D", "last_stats"]
+__all__ = ["render3d", "render2d", "render2d_units", "RenderOptions3D", "last_stats"]
 
 _TILE = _lib.TILE
 
@@ -55,7 +55,14 @@ class RenderOptions3D:
     eps2d: float = 0.3
     radius_mode: int = _lib.RADIUS_OPACITY_AABB
     input_mode: int = _lib.INPUT_ADAPTER   # INPUT_GSPLAT: rows hold activated gsplat inputs
-    band: tuple = (0, -1)                  # tile rows [y0, y1) binned (multi-GPU band sharding)
+    # tile rows [y0, y1) binned, counted over the C views' rows end to end (row r of view c is
+    # c*ceil(H/16) + r): a rank's contiguous share of (view, row) units (multi-GPU sharding)
+    band: tuple = (0, -1)
+    # backward: v_params is produced in `grad_buckets` contiguous Gaussian ranges, and
+    # grad_hook(rows) is called with each range's rows as soon as its kernels are enqueued
+    # (multi-GPU: an async all-reduce of finished rows overlaps the later ranges)
+    grad_buckets: int = 1
+    grad_hook: object = field(default=None, compare=False)
 
 
 _last_stats = {}
@@ -374,18 +381,58 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
     return rgb, alpha, b, (p, stride, V, Kc, bgc, width, height, opts)
 
 
-def _forward2d(params, bg, width, height, eps_cut):
+_set_cache = {}
+
+
+def _set_begin(unit_sets: tuple, F: int, dev):
+    """Device int32 [F+1] CSR of the cameras of each parameter set (cameras grouped by set),
+    cached per (sets, device); None for the single-set, single-camera case."""
+    if F == 1 and len(unit_sets) == 1:
+        return None
+    key = (unit_sets, F, str(dev))
+    t = _set_cache.get(key)
+    if t is None:
+        if any(b < a for a, b in zip(unit_sets, unit_sets[1:])) or not all(0 <= f < F for f in unit_sets):
+            raise ValueError(f"unit sets must be non-decreasing in [0, {F}), got {unit_sets}")
+        begin = [0] * (F + 1)
+        for f in unit_sets:
+            begin[f + 1] += 1
+        for f in range(F):
+            begin[f + 1] += begin[f]
+        if len(_set_cache) > 64:
+            _set_cache.clear()
+        t = _set_cache[key] = torch.tensor(begin, dtype=torch.int32).to(dev)
+    return t
+
+
+def _sets2d(params: torch.Tensor):
+    """[N,9] or [F,N,9] -> (rows, F, N, row stride, set stride) with unit row-element stride."""
+    p = params.detach()
+    if p.dtype != torch.float32:
+        p = p.float()
+    if p.dim() == 2:
+        p, stride = _rows(p, 9)
+        return p, 1, p.shape[0], stride, 0
+    F, N = p.shape[0], p.shape[1]
+    if p.stride(2) != 1 or p.stride(1) < 9 or (N > 0 and p.stride(0) < N * p.stride(1)):
+        p = p.contiguous()
+    return p, F, N, int(p.stride(1)) if N > 0 else 9, int(p.stride(0))
+
+
+def _forward2d(params, bg, width, height, eps_cut, unit_sets=(0,)):
+    """unit_sets[c] = parameter set rendered by camera (unit) c (non-decreasing)."""
     L = lib()
     dev = params.device
     stream = _stream(dev)
-    N = params.shape[0]
-    p, stride = _rows(params, 9)
-    bgc = _background(bg, 1, dev)
-    b = _Bins(dev, 1, N, width, height)
+    p, F, N, stride, set_stride = _sets2d(params)
+    C = len(unit_sets)
+    sb = _set_begin(tuple(unit_sets), F, dev)
+    bgc = _background(bg, C, dev)
+    b = _Bins(dev, C, N, width, height)
     q = b.p
     with _timed("project2d_fwd"):
-      check(L.gsr2d_project_fwd(_ptr(p), N, stride, width, height, eps_cut, q["rec"], q["rect"],
-                              q["cnt"], q["isect_off"], q["tile_cnt"], b.take_tile_counts(), stream),
+      check(L.gsr2d_project_fwd(_ptr(p), N, stride, set_stride, _ptr(sb), F, C, width, height, eps_cut, q["rec"],
+                              q["rect"], q["cnt"], q["isect_off"], q["tile_cnt"], b.take_tile_counts(), stream),
           "gsr2d_project_fwd")
     b.guess_post(with_chunks=True)
     b.offsets_launch(stream)
@@ -393,15 +440,15 @@ def _forward2d(params, bg, width, height, eps_cut):
     b.offsets_wait()
     b.ensure_post(with_chunks=True)
     b.sort(_lib.ORDER_INDEX, stream)
-    rgb = torch.empty(height, width, 3, device=dev, dtype=torch.float32)
-    alpha = torch.empty(height, width, device=dev, dtype=torch.float32)
+    rgb = torch.empty(C, height, width, 3, device=dev, dtype=torch.float32)
+    alpha = torch.empty(C, height, width, device=dev, dtype=torch.float32)
     with _timed("raster2d_fwd"):
-      check(L.gsr2d_raster_fwd(q["rec"], q["sorted_ids"], q["tile_off"], q["busy"], q["chunk_base"], width, height,
+      check(L.gsr2d_raster_fwd(q["rec"], q["sorted_ids"], q["tile_off"], q["busy"], q["chunk_base"], C, width, height,
                              eps_cut, _ptr(bgc), b.n_busy, q["stats_dev"], _ptr(rgb), _ptr(alpha), q["final_T"],
                              q["last"], q["tile_end"], q["tile_cut"], q["chunk_state"],
                              q["chunk_list"], stream), "gsr2d_raster_fwd")
     _record_stats(b)
-    return rgb, alpha, b, (p, stride, bgc, width, height, eps_cut)
+    return rgb, alpha, b, (p, F, stride, set_stride, sb, bgc, width, height, eps_cut)
 
 
 def debug_forward3d(params, viewmats, Ks, bg, width, height, opts=None):
@@ -410,7 +457,8 @@ def debug_forward3d(params, viewmats, Ks, bg, width, height, opts=None):
 
 
 def debug_forward2d(params, bg, width, height, eps_cut=1e-8):
-    return _forward2d(params, bg, width, height, eps_cut)
+    rgb, alpha, b, meta = _forward2d(params, bg, width, height, eps_cut)
+    return rgb[0], alpha[0], b, meta
 
 
 class _Render3D(torch.autograd.Function):
@@ -457,19 +505,26 @@ def backward3d(b, meta, raster) -> torch.Tensor:
         q = b.p
         with _timed("raster3d_bwd"):
             raster(L, q, partial, stream)
-        with _timed("project3d_bwd"):
-          check(L.gsr3d_project_bwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height, opts.eps2d,
-                                    opts.input_mode,
-                                    q["depth"], q["rect"], q["isect_off"], q["cnt"], q["tile_cut"],
-                                    _ptr(partial), _ptr(v_params), stream),
-                "gsr3d_project_bwd")
+        nb = max(1, min(int(opts.grad_buckets), N))
+        bounds = [N * k // nb for k in range(nb + 1)]
+        for n0, n1 in zip(bounds[:-1], bounds[1:]):
+            with _timed("project3d_bwd"):
+              check(L.gsr3d_project_bwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height, opts.eps2d,
+                                        opts.input_mode,
+                                        q["depth"], q["rect"], q["isect_off"], q["cnt"], q["tile_cut"],
+                                        _ptr(partial), n0, n1, _ptr(v_params), stream),
+                    "gsr3d_project_bwd")
+            if opts.grad_hook is not None:
+                opts.grad_hook(v_params[n0:n1])
+    elif opts.grad_hook is not None:
+        opts.grad_hook(v_params)
     return v_params
 
 
 class _Render2D(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, params, bg, width, height, eps_cut):
-        rgb, alpha, b, meta = _forward2d(params, bg, width, height, eps_cut)
+    def forward(ctx, params, bg, width, height, eps_cut, unit_sets):
+        rgb, alpha, b, meta = _forward2d(params, bg, width, height, eps_cut, unit_sets)
         ctx.b = b
         ctx.meta = meta
         ctx.params_shape = params.shape
@@ -479,31 +534,32 @@ class _Render2D(torch.autograd.Function):
     def backward(ctx, v_rgb, v_alpha):
         L = lib()
         b = ctx.b
-        p, stride, bgc, width, height, eps_cut = ctx.meta
+        p, F, stride, set_stride, sb, bgc, width, height, eps_cut = ctx.meta
         dev = p.device
         stream = _stream(dev)
-        N = b.N
+        N, C = b.N, b.C
         if v_rgb is None:
-            v_rgb = torch.zeros(height, width, 3, device=dev)
+            v_rgb = torch.zeros(C, height, width, 3, device=dev)
         if v_alpha is None:
-            v_alpha = torch.zeros(height, width, device=dev)
+            v_alpha = torch.zeros(C, height, width, device=dev)
         v_rgb = v_rgb.float().contiguous()
         v_alpha = v_alpha.float().contiguous()
-        v_params = torch.empty(N, 9, device=dev, dtype=torch.float32)
+        v_params = torch.empty(F, N, 9, device=dev, dtype=torch.float32)
         if N > 0:
             partial = torch.empty(max(b.n_isect, 1) * _lib.PARTIAL_STRIDE, device=dev, dtype=torch.float32)
             q = b.p
             with _timed("raster2d_bwd"):
               check(L.gsr2d_raster_bwd(q["rec"], q["sorted_ids"], q["tile_off"], q["tile_end"], q["chunk_base"],
                                      q["chunk_state"], q["chunk_list"], q["stats_dev"],
-                                     b.n_chunks, width, height, eps_cut, _ptr(bgc), q["final_T"], q["last"],
+                                     b.n_chunks, C, width, height, eps_cut, _ptr(bgc), q["final_T"], q["last"],
                                      _ptr(v_rgb), _ptr(v_alpha), q["k_of_s"], _ptr(partial), stream),
                   "gsr2d_raster_bwd")
             with _timed("project2d_bwd"):
-              check(L.gsr2d_project_bwd(_ptr(p), N, stride, width, height, q["rect"], q["isect_off"],
-                                      q["cnt"], q["tile_cut"], _ptr(partial), _ptr(v_params), stream),
+              check(L.gsr2d_project_bwd(_ptr(p), N, stride, set_stride, _ptr(sb), F, C, width, height, q["rect"],
+                                      q["isect_off"], q["cnt"], q["tile_cut"], _ptr(partial), _ptr(v_params),
+                                      stream),
                   "gsr2d_project_bwd")
-        return v_params.view(ctx.params_shape), None, None, None, None
+        return v_params.view(ctx.params_shape), None, None, None, None, None
 
 
 def render3d(params: torch.Tensor, viewmats: torch.Tensor, Ks: torch.Tensor, width: int, height: int,
@@ -522,4 +578,25 @@ def render2d(params: torch.Tensor, width: int, height: int, background: torch.Te
              eps_cut: float = 1e-8):
     """[N,9] raw params → rgb [H,W,3], alpha [H,W] (index-order compositing)."""
     _require_device(params, "GaussianRenderer2D")
-    return _Render2D.apply(params, background, int(width), int(height), float(eps_cut))
+    if params.dim() != 2:
+        raise ValueError(f"render2d: params must be [N,9], got {tuple(params.shape)}")
+    rgb, alpha = _Render2D.apply(params, background, int(width), int(height), float(eps_cut), (0,))
+    return rgb[0], alpha[0]
+
+
+def render2d_units(params: torch.Tensor, unit_sets, width: int, height: int, background: torch.Tensor,
+                   eps_cut: float = 1e-8):
+    """Multi-frame 2D batch in ONE launch sequence: params [F,N,9] (F frames' raw parameter
+    sets), unit_sets[c] = the frame rendered by unit (camera) c, non-decreasing (units grouped
+    by frame; a frame may have any number of units, including none).  Returns rgb [C,H,W,3],
+    alpha [C,H,W]; the gradient w.r.t. params [F,N,9] sums each frame's units.  The reference
+    ignores the camera in 2D (src/gaussian_renderer.py:280-281), so the units of a frame are
+    identical renders -- each is still rendered (units = frame x view)."""
+    _require_device(params, "GaussianRenderer2D")
+    if params.dim() != 3 or params.shape[-1] != 9:
+        raise ValueError(f"render2d_units: params must be [F,N,9], got {tuple(params.shape)}")
+    sets = tuple(int(f) for f in unit_sets)
+    if not sets:
+        raise ValueError("render2d_units: no units")
+    _set_begin(sets, params.shape[0], params.device)   # validates the grouping
+    return _Render2D.apply(params, background, int(width), int(height), float(eps_cut), sets)

@@ -52,8 +52,12 @@ def test_invalid_arguments_are_reported_not_launched():
     rc = lib.gsr3d_project_fwd(None, 10, 14, None, None, 1, 64, 64, 0.01, 1e10, 0.0, 0.3, 7, 0, 0, -1,
                                None, None, None, None, None, None, 0, None)
     assert rc == -1 and b"radius_mode" in lib.gsr_last_error()
-    rc = lib.gsr2d_project_fwd(None, 10, 9, 64, 64, 2.0, None, None, None, None, None, 0, None)
+    rc = lib.gsr2d_project_fwd(None, 10, 9, 0, None, 1, 1, 64, 64, 2.0, None, None, None, None, None, 0, None)
     assert rc == -1 and b"eps_cut" in lib.gsr_last_error()
+    rc = lib.gsr2d_project_fwd(None, 10, 9, 90, None, 2, 4, 64, 64, 1e-8, None, None, None, None, None, 0, None)
+    assert rc == -1 and b"need set_begin" in lib.gsr_last_error()
+    rc = lib.gsr2d_project_bwd(None, 10, 9, 0, None, 1, 0, 64, 64, None, None, None, None, None, None, None)
+    assert rc == -1 and b"bad C" in lib.gsr_last_error()
     rc = lib.gsr_bin_sort(None, None, None, None, None, None, 1, 10, 64, 64, 5, 0, 0, 0, 0, 0, 0, None, None, 0, None, None,
                           None)
     assert rc == -1 and b"bad order" in lib.gsr_last_error()

@@ -1,7 +1,10 @@
 """bench.py host logic that runs without a GPU: the roofline fields read from the committed
-rocprofv3 PMC passes (profiles/), and the §8(d) step-bytes formula."""
+rocprofv3 PMC passes of the SAME config (profiles/), the CPU-baseline fit, the PSNR formula
+and the §8(d) byte formulas."""
 import os
 import sys
+
+import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
@@ -11,15 +14,61 @@ import bench  # noqa: E402
 
 
 def test_traffic_from_committed_pmc():
-    t = bench.traffic_from_csv(bench.DEFAULT_TRAFFIC_CSV, bench.KERNEL_SYMBOL["raster3d_bwd"])
+    f = bench.pmc_files(3, "traffic")
+    assert f is not None and "cfg3" in os.path.basename(f)
+    t = bench.traffic_from_csv(f, bench.KERNEL_SYMBOL["raster3d_bwd"])
     assert t is not None and 1e8 < t < 1e9, t
-    assert bench.traffic_from_csv(bench.DEFAULT_TRAFFIC_CSV, "no_such_kernel") is None
+    assert bench.traffic_from_csv(f, "no_such_kernel") is None
+
+
+def test_no_cross_config_counters(tmp_path):
+    """A config without its own PMC pass reports null traffic/valu (never another config's)."""
+    assert bench.pmc_files(2, "traffic", str(tmp_path)) is None
+    assert bench.pmc_files(2, "sq", str(tmp_path)) is None
+    (tmp_path / "r01_pmc_traffic_cfg3.csv").write_text("x\n")
+    (tmp_path / "r02_pmc_traffic_cfg3.csv").write_text("x\n")
+    (tmp_path / "r10_pmc_traffic_cfg3.csv").write_text("x\n")
+    assert bench.pmc_files(2, "traffic", str(tmp_path)) is None
+    assert os.path.basename(bench.pmc_files(3, "traffic", str(tmp_path))) == "r10_pmc_traffic_cfg3.csv"
+    (tmp_path / "r02_pmc_sq_cfg5_p1.csv").write_text("x\n")
+    assert bench.pmc_files(5, "sq", str(tmp_path)) is None          # p2 missing
+    (tmp_path / "r02_pmc_sq_cfg5_p2.csv").write_text("x\n")
+    assert len(bench.pmc_files(5, "sq", str(tmp_path))) == 2
 
 
 def test_valu_from_committed_sq_passes():
-    v = bench.valu_from_csv(bench.DEFAULT_SQ_CSVS, bench.KERNEL_SYMBOL["raster3d_bwd"])
+    sq = bench.pmc_files(3, "sq")
+    v = bench.valu_from_csv(sq, bench.KERNEL_SYMBOL["raster3d_bwd"])
     assert v is not None
     assert 0.0 < v["issue_frac"] <= v["active_frac"] + 1e-9 < 1.05, v
     assert v["insts_per_launch"] > 1e7
-    assert bench.valu_from_csv(bench.DEFAULT_SQ_CSVS, "no_such_kernel") is None
+    assert bench.valu_from_csv(sq, "no_such_kernel") is None
     assert bench.valu_from_csv([os.path.join(ROOT, "profiles", "missing.csv")], "k_emit") is None
+    assert bench.valu_from_csv(None, "k_emit") is None
+
+
+def test_linear_fit_and_psnr():
+    a, b, r2 = bench.linear_fit([1, 2, 3, 4], [3.0, 5.0, 7.0, 9.0])
+    assert abs(a - 1.0) < 1e-12 and abs(b - 2.0) < 1e-12 and abs(r2 - 1.0) < 1e-12
+    _, _, r2n = bench.linear_fit([1, 2, 3], [1.0, 3.0, 2.0])
+    assert r2n < 1.0
+    x = torch.rand(8, 6, 3, dtype=torch.float64)
+    y = x + 0.1
+    # get_psnr (scripts/utils/evaluate_model.py:240-243): 10 log10(1 / mse), mse = 0.01
+    assert abs(bench.psnr(x, y) - 20.0) < 1e-9
+
+
+def test_byte_formulas_and_allreduce_model():
+    # §8(d): fwd+bwd per view N(12p+136) + 36 I + 80 I_eff + 44 P
+    assert bench.step_bytes(1, 10, 100, 7, 5, 14) == 10 * (12 * 14 + 136) + 36 * 7 + 80 * 5 + 44 * 100
+    assert bench.step_bytes(1, 10, 100, 7, 5, 14, backward=False) == 10 * (4 * 14 + 32) + 36 * 7 + 40 * 5 + 20 * 100
+    assert bench.algorithmic_bytes("raster3d_bwd", 6, 10, 100, 7, 5, 14) == 24 * 100 + 40 * 5 + 36 * 6 * 10
+    assert bench.allreduce_ms(1000, 1) == 0.0
+    # 2(n-1)/n S at 153 GB/s: 11.2 MB at n = 8 -> 0.128 ms
+    assert abs(bench.allreduce_ms(11_200_000, 8) - 2 * 7 / 8 * 11.2e6 / 153e9 * 1e3) < 1e-12
+
+
+def test_bench_args_defaults():
+    a = bench.parse([])
+    assert a.config == 3 and a.gpus == 1 and a.shard == "units" and a.cpu_threads == 0
+    assert bench.cpu_threads(3) == 3 and bench.cpu_threads(0) >= 1

@@ -42,6 +42,54 @@ def _render_band(p, V, K, band):
     return render3d(p, V, K, 40, 32, torch.ones(3), band=band)
 
 
+class _HookRender(torch.autograd.Function):
+    """The oracle band render, with the GPU path's bucketed-gradient contract: the backward
+    hands each Gaussian-range bucket of the gradient to ``hook`` (gsr.render's grad_hook)."""
+
+    @staticmethod
+    def forward(ctx, p, V, K, band, hook, buckets):
+        with torch.enable_grad():
+            pp = p.detach().requires_grad_(True)
+            rgb, a = _render_band(pp, V, K, band)
+        ctx.saved = (pp, rgb, a, hook, buckets)
+        return rgb.detach(), a.detach()
+
+    @staticmethod
+    def backward(ctx, gr, ga):
+        from gsr.multiview import bucket_bounds
+        pp, rgb, a, hook, buckets = ctx.saved
+        (g,) = torch.autograd.grad([rgb, a], [pp], [gr, ga])
+        if hook is not None:
+            b = bucket_bounds(g.shape[0], buckets)
+            for n0, n1 in zip(b[:-1], b[1:]):
+                hook(g[n0:n1])
+        return g, None, None, None, None, None
+
+
+def _frames2d():
+    g = torch.Generator().manual_seed(13)
+    P = torch.randn(4, 60, 9, generator=g)
+    P[..., 0] = torch.rand(4, 60, generator=g) * 24
+    P[..., 1] = torch.rand(4, 60, generator=g) * 20
+    vr = torch.randn(4 * 3, 20, 24, 3, generator=g)
+    va = torch.randn(4 * 3, 20, 24, generator=g)
+    return P, vr, va
+
+
+def _render_units2d(p, sets):
+    from oracle.oracle2d import render2d_dense
+    outs = [render2d_dense(p[f], 24, 20, torch.ones(3)) for f in sets]
+    return torch.stack([o[0] for o in outs]), torch.stack([o[1] for o in outs])
+
+
+def _frames_single():
+    """Single-process gradient of the 4-frame x 3-view 2D job: every unit rendered locally."""
+    from gsr.multiview import frame_view_units, sharded_backward_frames
+    P, vr, va = _frames2d()
+    units = frame_view_units(4, 3, 1, 0)
+    return sharded_backward_frames(_render_units2d, P, units, vr, va, buckets=1)
+
+
 def _worker(rank, world, port, out, mode="views"):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -50,12 +98,22 @@ def _worker(rank, world, port, out, mode="views"):
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(2)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from gsr.multiview import sharded_backward, sharded_backward_bands
+    from gsr.multiview import (frame_view_units, sharded_backward, sharded_backward_frames,
+                               sharded_backward_units)
     p, V, K, vr, va = _scene()
     if mode == "views":
         grad = sharded_backward(_render, p, V, K, vr, va)
+    elif mode == "units":
+        grad = sharded_backward_units(lambda q, v, k, band, hook: _render_band(q, v, k, band), p, V, K, vr, va,
+                                      rows=2, weights=[3.0, 1.0, 2.0, 2.0, 1.0, 1.0, 0.5, 4.0, 1.0, 1.0])
+    elif mode == "units_buckets":
+        grad = sharded_backward_units(lambda q, v, k, band, hook: _HookRender.apply(q, v, k, band, hook, 3),
+                                      p, V, K, vr, va, rows=2, buckets=3)
     else:
-        grad = sharded_backward_bands(_render_band, p, V, K, vr, va, rows=2, weights=[3.0, 1.0])
+        P, vr2, va2 = _frames2d()
+        units = frame_view_units(4, 3, world, rank)
+        idx = [f * 3 + v for f, v in units]
+        grad = sharded_backward_frames(_render_units2d, P, units, vr2[idx], va2[idx], buckets=2)
     out[rank] = grad
     dist.destroy_process_group()
 
@@ -88,32 +146,72 @@ def test_band_shard_partition():
 
 
 def test_band_render_equals_full_render_in_band():
-    """Oracle: binning only a band of tile rows leaves those rows' pixels unchanged, and the
-    band gradients sum to the full gradient."""
+    """Oracle: binning only a range of (view, tile row) units -- global rows, view-major --
+    leaves those rows' pixels unchanged, and the ranges' gradients sum to the full gradient."""
+    from gsr.multiview import unit_shard
     from oracle.oracle3d import render3d
     p, V, K, vr, va = _scene()
+    C, th = V.shape[0], 2
     full_rgb, full_a = render3d(p, V, K, 40, 32, torch.ones(3))
-    grads = []
-    for band in [(0, 1), (1, 2)]:
+    total = torch.zeros_like(p)
+    for r in range(3):
+        v0, v1, band = unit_shard(C, th, 3, r)
         pc = p.clone().requires_grad_(True)
-        rgb, a = render3d(pc, V, K, 40, 32, torch.ones(3), band=band)
-        rows = slice(16 * band[0], min(32, 16 * band[1]))
-        assert torch.equal(rgb[:, rows], full_rgb[:, rows]) and torch.equal(a[:, rows], full_a[:, rows])
+        rgb, a = render3d(pc, V[v0:v1], K[v0:v1], 40, 32, torch.ones(3), band=band)
+        for c in range(v0, v1):
+            y0 = min(max(band[0] - (c - v0) * th, 0), th)
+            y1 = min(max(band[1] - (c - v0) * th, 0), th)
+            rows = slice(16 * y0, min(32, 16 * y1))
+            assert torch.equal(rgb[c - v0, rows], full_rgb[c, rows]) and torch.equal(a[c - v0, rows], full_a[c, rows])
         # cotangents outside the band meet no Gaussians there
-        torch.autograd.backward([rgb, a], [vr, va])
-        grads.append(pc.grad)
+        torch.autograd.backward([rgb, a], [vr[v0:v1], va[v0:v1]])
+        total += pc.grad
     pf = p.clone().requires_grad_(True)
     torch.autograd.backward(list(render3d(pf, V, K, 40, 32, torch.ones(3))), [vr, va])
-    assert torch.allclose(grads[0] + grads[1], pf.grad, rtol=1e-5, atol=1e-6 * float(pf.grad.abs().max()))
+    assert torch.allclose(total, pf.grad, rtol=1e-5, atol=1e-6 * float(pf.grad.abs().max()))
 
 
-@pytest.mark.parametrize("world", [2])
-def test_band_sharded_allreduce_matches_single_process(world):
+@pytest.mark.parametrize("world,mode", [(2, "units"), (3, "units"), (2, "units_buckets"), (3, "units_buckets")])
+def test_unit_sharded_allreduce_matches_single_process(world, mode):
+    """(view, row)-unit sharding (strong scaling of one multi-view job): ranks render disjoint
+    view/row ranges; the (bucketed, async) all-reduce of their gradients is the full gradient."""
     from gsr.multiview import sharded_backward
     p, V, K, vr, va = _scene()
     ref = sharded_backward(_render, p, V, K, vr, va)
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), out, "bands"), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, mode), nprocs=world, join=True)
     for r in range(world):
         assert torch.allclose(out[r], ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max())), r
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_frame_sharded_allreduce_matches_single_process(world):
+    """Config 4's layout: (frame, view) units round-robin over ranks, batched per frame bucket,
+    async per-bucket all-reduce of the [F,N,9] gradient == the single-process gradient."""
+    ref = _frames_single()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out, "frames"), nprocs=world, join=True)
+    for r in range(world):
+        assert torch.allclose(out[r], ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max())), r
+    assert torch.equal(out[0], out[1])
+
+
+def test_unit_and_frame_partitions():
+    from gsr.multiview import frame_buckets, frame_view_units, unit_shard
+    for C, rows, world in [(6, 32, 8), (6, 64, 8), (1, 5, 8), (3, 2, 2), (6, 32, 1)]:
+        seen = []
+        for r in range(world):
+            v0, v1, (b0, b1) = unit_shard(C, rows, world, r)
+            seen += list(range(v0 * rows + b0, v0 * rows + b1))
+            if v1 > v0:   # the band starts in view v0 and ends in view v1 - 1
+                assert 0 <= b0 < rows and (v1 - 1 - v0) * rows < b1 <= (v1 - v0) * rows
+        assert seen == list(range(C * rows))
+    for F, V, world in [(8, 6, 8), (8, 6, 4), (8, 6, 3), (8, 6, 1)]:
+        units = [u for r in range(world) for u in frame_view_units(F, V, world, r)]
+        assert sorted(units) == [(f, v) for f in range(F) for v in range(V)]
+        for r in range(world):
+            fs = [f for f, _ in frame_view_units(F, V, world, r)]
+            assert fs == sorted(fs)
+    assert frame_buckets(8, 2) == [(0, 4), (4, 8)] and frame_buckets(3, 8) == [(0, 1), (1, 2), (2, 3)]

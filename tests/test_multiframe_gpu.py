@@ -1,0 +1,73 @@
+"""Multi-frame 2D batches: F frames' parameter sets rendered as
+C (frame, view) units in ONE projection -> binning -> raster sequence (gsr.render.render2d_units).
+
+Checks, on the GPU through the C ABI:
+  * every unit's image is bitwise the single-frame render of its frame (the raster of a
+    tile does not depend on the other units in the batch);
+  * each frame's gradient equals the sum over its units of single-unit gradients (to fp32
+    reordering), and is exactly zero for a frame with no unit;
+  * one unit of the batch against the CPU oracle (oracle/oracle2d.py, pinned to the
+    reference fixtures) at the reference tolerance.
+"""
+import pytest
+import torch
+
+from _util import assert_close, grad_close
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(F, N, W, H, seed):
+    from gsr.scenes import gaussians2d
+    return torch.stack([gaussians2d(N, W, H, seed + f) for f in range(F)])
+
+
+@pytest.mark.parametrize("sets", [(0, 0, 1, 2, 2, 2), (0, 2, 2), (1,)])
+def test_units_match_single_renders(cuda, sets):
+    from gsr import render as R
+    F, N, W, H = 3, 1200, 96, 80
+    P = _frames(F, N, W, H, 71)
+    bg = torch.tensor([1.0, 0.5, 0.0])
+    C = len(sets)
+    g = torch.Generator().manual_seed(72)
+    vr, va = torch.randn(C, H, W, 3, generator=g), torch.randn(C, H, W, generator=g)
+    pb = P.to(cuda).requires_grad_(True)
+    rgb, alpha = R.render2d_units(pb, sets, W, H, bg.to(cuda))
+    assert rgb.shape == (C, H, W, 3) and alpha.shape == (C, H, W)
+    torch.autograd.backward([rgb, alpha], [vr.to(cuda), va.to(cuda)])
+    ref_grad = torch.zeros(F, N, 9, dtype=torch.float64)
+    for c, f in enumerate(sets):
+        ps = P[f].to(cuda).requires_grad_(True)
+        r1, a1 = R.render2d(ps, W, H, bg.to(cuda))
+        assert torch.equal(r1, rgb[c].detach()), f"unit {c} rgb differs from its single render"
+        assert torch.equal(a1, alpha[c].detach()), f"unit {c} alpha differs from its single render"
+        torch.autograd.backward([r1, a1], [vr[c].to(cuda), va[c].to(cuda)])
+        ref_grad[f] += ps.grad.double().cpu()
+    for f in range(F):
+        if f not in sets:
+            assert torch.count_nonzero(pb.grad[f]) == 0
+        else:
+            grad_close(pb.grad[f], ref_grad[f], rtol=1e-5, rel_floor=1e-6, what=f"frame {f} grad")
+
+
+def test_unit_vs_oracle(cuda):
+    from gsr import render as R
+    from oracle.oracle2d import render2d_dense
+    F, N, W, H = 2, 800, 64, 48
+    P = _frames(F, N, W, H, 81)
+    bg = torch.ones(3)
+    sets = (0, 1, 1)
+    g = torch.Generator().manual_seed(82)
+    vr, va = torch.randn(3, H, W, 3, generator=g), torch.randn(3, H, W, generator=g)
+    vr[1:2].zero_(), va[1:2].zero_()   # frame 1's gradient comes from unit 2 only
+    vr[0].zero_(), va[0].zero_()       # frame 0 gets no cotangent
+    pb = P.to(cuda).requires_grad_(True)
+    rgb, alpha = R.render2d_units(pb, sets, W, H, bg.to(cuda))
+    torch.autograd.backward([rgb, alpha], [vr.to(cuda), va.to(cuda)])
+    po = P[1].clone().requires_grad_(True)
+    rgb_o, a_o = render2d_dense(po, W, H, bg)
+    ((rgb_o * vr[2]).sum() + (a_o * va[2]).sum()).backward()
+    assert_close(rgb[2].detach(), rgb_o.detach(), what="unit 2 rgb")
+    assert_close(alpha[1].detach(), a_o.detach(), what="unit 1 alpha")
+    grad_close(pb.grad[1], po.grad, what="frame 1 grad")
+    assert torch.count_nonzero(pb.grad[0]) == 0

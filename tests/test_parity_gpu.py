@@ -403,10 +403,12 @@ def test_2d_deterministic(cuda):
 
 @pytest.mark.gpu
 def test_3d_band_sharding(cuda):
-    """Multi-GPU band sharding on one device: each band's rows are bitwise
-    the full render's rows, and the band gradients sum to the full gradient."""
+    """Multi-GPU (view, row)-unit sharding on one device: each rank's share
+    renders only the views it touches, binned to its global rows; those rows are bitwise the
+    full render's rows, and the shares' gradients (bucketed projection backward with a
+    gradient hook, as the all-reduce path uses it) sum to the full gradient."""
     from gsr.render import RenderOptions3D, render3d
-    from gsr.multiview import band_shard
+    from gsr.multiview import unit_shard
     W, H, C = 96, 80, 3
     p, V, K = _scene3d(20000, W, H, C, 21)
     bg = torch.ones(3, device=cuda)
@@ -417,15 +419,25 @@ def test_3d_band_sharding(cuda):
     torch.autograd.backward([rgb_f, a_f], [vr, va])
     th = (H + 15) // 16
     total = torch.zeros_like(pf)
-    for r in range(3):
-        band = band_shard(th, 3, r)
-        pb = p.to(cuda).requires_grad_(True)
-        rgb, a = render3d(pb, V.to(cuda), K.to(cuda), W, H, bg, RenderOptions3D(band=band))
-        rows = slice(16 * band[0], min(H, 16 * band[1]))
-        assert torch.equal(rgb[:, rows], rgb_f[:, rows]) and torch.equal(a[:, rows], a_f[:, rows])
-        torch.autograd.backward([rgb, a], [vr, va])
-        total += pb.grad
-    grad_close(total.cpu(), pf.grad.cpu(), what="band-summed grad")
+    for world in (4, 7):
+        total.zero_()
+        for r in range(world):
+            v0, v1, band = unit_shard(C, th, world, r)
+            if v1 == v0:
+                continue
+            pieces = []
+            pb = p.to(cuda).requires_grad_(True)
+            opts = RenderOptions3D(band=band, grad_buckets=3, grad_hook=pieces.append)
+            rgb, a = render3d(pb, V[v0:v1].to(cuda), K[v0:v1].to(cuda), W, H, bg, opts)
+            for c in range(v0, v1):
+                y0 = min(max(band[0] - (c - v0) * th, 0), th)
+                y1 = min(max(band[1] - (c - v0) * th, 0), th)
+                rows = slice(16 * y0, min(H, 16 * y1))
+                assert torch.equal(rgb[c - v0, rows], rgb_f[c, rows]) and torch.equal(a[c - v0, rows], a_f[c, rows])
+            torch.autograd.backward([rgb, a], [vr[v0:v1], va[v0:v1]])
+            assert len(pieces) == 3 and torch.equal(torch.cat(pieces), pb.grad)
+            total += pb.grad
+        grad_close(total.cpu(), pf.grad.cpu(), what=f"unit-summed grad, world {world}")
 
 
 def test_3d_two_streams(cuda):
