@@ -94,6 +94,10 @@ const char* gsr_last_error(void);
  * out[l] = sum over lanes L of v_L[l] with v_L[i] = ((L*7 + i*13) % 97) + i/4.  out: 64 floats. */
 int gsr_selftest_reduce64(float* out, void* stream);
 
+/* Self-test of the per-box reduction of the raster backward (one 64-lane wave, same pattern):
+ * out[4*l + i] = sum over the 16 lanes L with L % 4 == l % 4 of v_L[4*(l/4) + i].  out: 256 floats. */
+int gsr_selftest_reduce_box16(float* out, void* stream);
+
 /* Self-test of the lane-ordered LDS atomics the tile sort's ranking relies on: writes the
  * number of violations (0 expected) to the device int *violations. */
 int gsr_selftest_lds_order(int32_t* violations, void* stream);

@@ -144,6 +144,36 @@ __device__ __forceinline__ float reduce64(float (&v)[64]) {
   return pair_level<0xB1>(e[0], e[1], b0);                                     // quad_perm [1,0,3,2]
 }
 
+// reduce_box16(v, out): the 16 lanes with equal lane bits 0-1 (a "box" of the raster
+// backward) sum each of the 64 registers; afterwards out[i] of lane l is the box sum of
+// register 4*(l>>2) + i.  The same halving butterfly as reduce64 over lane bits 5 and 4
+// (permlane32 / permlane16 swaps), then bit 3 (row_ror:8 is xor 8 inside a row) and bit 2
+// (the lower lane of a pair reads lane+4 with row_shl:4, the upper lane-4 with row_shr:4),
+// and stops there: bits 0-1 separate the boxes.  132 VALU ops for 4 x 16-lane sums of 64 values.
+__device__ __forceinline__ void reduce_box16(float (&v)[64], float (&out)[4]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) swap32x8(&v[8 * g], &v[32 + 8 * g]);
+  float a[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) a[i] = v[i] + v[i + 32];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) swap16x8(&a[8 * g], &a[16 + 8 * g]);
+  float b[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) b[i] = a[i] + a[i + 16];
+  const bool b3 = (lane & 8) != 0, b2 = (lane & 4) != 0;
+  float c[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) c[i] = pair_level<0x128>(b[i], b[i + 8], b3);   // row_ror:8
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float l = c[i] + dpp_mov<0x104>(c[i]);           // row_shl:4: lane + 4
+    const float h = c[i + 4] + dpp_mov<0x114>(c[i + 4]);   // row_shr:4: lane - 4
+    out[i] = b2 ? h : l;
+  }
+}
+
 __device__ __forceinline__ unsigned long long wave_ballot(bool p) { return __ballot(p); }
 
 // Block-wide exclusive scan of one int per thread (NT threads, multiple of 64).

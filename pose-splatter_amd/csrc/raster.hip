@@ -170,9 +170,14 @@ __device__ __forceinline__ int quad_max_i(int v) {
 // workgroups for the busy tiles: 4 per tile, rounded up to whole groups of 8 tiles (32 ids)
 __host__ __device__ __forceinline__ int busy_grid(int n_busy) { return 32 * ((n_busy + 7) / 8); }
 
-// thread index of tile pixel (il, jl) in the backward's layout (4 waves of 8x8)
+// thread index of tile pixel (il, jl) in the backward's layout: wave = the 8x8 quadrant
+// (il>>3, jl>>3); inside it lane = 4 * (pixel within its 4x4 box) + box, so the lanes of one
+// box are the lanes with equal bits 0-1 (see k_raster_bwd)
 __device__ __forceinline__ int bwd_pixel_slot(int il, int jl) {
-  return ((il >> 3) << 7) | ((jl >> 3) << 6) | ((il & 7) << 3) | (jl & 7);
+  const int wv = ((il >> 3) << 1) | (jl >> 3);
+  const int box = (((il >> 2) & 1) << 1) | ((jl >> 2) & 1);
+  const int pos = ((il & 3) << 2) | (jl & 3);
+  return (wv << 6) | (pos << 2) | box;
 }
 
 //
@@ -592,15 +597,27 @@ __device__ __forceinline__ void loss_cotangent(const gsr_loss_terms& lt, int C, 
 // ---------------------------------------------------------------- 3D backward
 // Chunk-parallel: one workgroup per (tile, GSR_CHUNK-entry chunk of its list), so no
 // pixel's back-to-front walk is longer than one chunk.  Workgroup b takes entry b of the
-// forward's chunk list (only chunks before their tile's tile_end).  The forward's chunk records give each pixel's state at the chunk's END exactly:
-// T_end (the T the forward had there) and the suffix colour sum S_end = sum of the later
-// chunks' own colour sums (positive terms, no cancellation).  Inside the chunk:
+// forward's chunk list (only chunks before their tile's tile_end).  The forward's chunk
+// records give each pixel's state at the chunk's END exactly: T_end (the T the forward had
+// there) and the suffix colour sum S_end = sum of the later chunks' own colour sums
+// (positive terms, no cancellation).  Inside the chunk:
 //   T_i recovered as T_{i+1}/(1-a_i) with v_rcp (a <= 0.999);
 //   d rgb/d c_i = a_i T_i;  d rgb/d a_i = c_i T_i - (S_i + T_f bg)/(1-a_i);  d alpha/d a_i = T_f/(1-a_i)
 //   a = o e^{-sigma} (unclamped only):  d/do = e^{-sigma},  d/dsigma = -a.
-// Each wave culls the chunk against its 8x8 sub-tile (same test as the forward), walks its
-// survivors back to front, reduces 7 entries x 9 gradients at once (reduce64), and a 4-wave
-// LDS combine stores one 9-float partial per sorted entry.
+//
+// Layout: wave w owns the 8x8 quadrant w of the tile; its lane l serves pixel l>>2 of the
+// 4x4 BOX l&3 of that quadrant.  The chunk is culled against the quadrant (exact test, as in
+// the forward), the quadrant's survivors against each of its four boxes, and every lane
+// walks its own box's survivor list back to front in straight-line groups of 7 (the wave
+// runs max over its boxes of the group count).  4x4 boxes evaluate ~0.45x the (pixel, entry)
+// pairs of 8x8 ones (tools/cull_stats.py: the wave walks 0.64x the groups at config 3).  Each
+// group's 7 entries x 9 gradient sums are reduced over the 16 lanes of each box by a
+// transposed butterfly over lane bits 5,4,3,2 (reduce_box16: two permlane-swap levels, two
+// DPP levels), after which every lane holds 4 of its box's 63 sums.  They are staged in LDS
+// and added box by box into the wave's own slot of the per-entry sums with plain
+// read-add-writes (distinct addresses inside an instruction, boxes in program order): no LDS
+// atomics (one float atomic per lane per group was ~40% of the LDS time), and the fixed-order
+// 4-slot sum at the end keeps the result bitwise deterministic.
 //
 // LOSS: the pixel cotangents are not read from v_rgb / v_alpha images but generated from the
 // training loss (loss_cotangent below, gsr3d_raster_bwd_loss).
@@ -625,25 +642,35 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
   // slot kNull: a zero-opacity record (never valid) that pads survivor groups to 7
   constexpr int kNull = kChunk3;
   constexpr int kGroup = 7;
+  constexpr int kLen = kChunk3 + kGroup;   // survivor list capacity (padded to whole groups)
   __shared__ float4 s_p0[kChunk3 + 1];
   __shared__ float4 s_p1[kChunk3 + 1];
   __shared__ float4 s_p2[kChunk3 + 1];
-  // gradient sums per entry: waves {0,1} add into pair slot 0, waves {2,3} into slot 1.  Two
-  // float adds onto 0 commute exactly, so the LDS atomics keep the result deterministic.
-  __shared__ float L[kPartial][2][kChunk3];
-  __shared__ short s_list[4][kChunk3 + kGroup];
+  // gradient sums per entry, one slot per wave (index kNull absorbs the padding's zeros)
+  __shared__ float L[kPartial][4][kChunk3 + 1];
+  __shared__ unsigned char s_list[4][kLen];     // quadrant survivors, back to front
+  __shared__ unsigned char s_box[4][4][kLen];   // per (wave, box) survivors, back to front
+  __shared__ float s_stage[4][64][4];     // per wave: the group's reduced sums, by lane
   // one workgroup per grid slot; slots past the forward's active-chunk count exit at once
   // the chunk's descriptor {first entry, entries (>= 1), chunk record row, tile} -- one load
   // (read before the bound check: the list has a slot for every grid slot)
   const int4 cd = reinterpret_cast<const int4*>(chunk_list)[blockIdx.x];
   if ((int)blockIdx.x >= stats->n_active) return;
   const int b0 = cd.x, n = cd.y, chunk = cd.z, ct = cd.w;
-  const SubTile st = sub_tile<IS2D>(ct, tw, th, W, H);
-  const int wv = st.wv;
+  int c, ty, tx;
+  tile_coords(ct, tw, th, c, ty, tx);
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int box = lane & 3, pos = lane >> 2;
+  const float off = IS2D ? 0.f : 0.5f;   // 2D: integer centres (src/gaussian_renderer.py:355-358)
+  const int qx0 = tx * kTile + (wv & 1) * 8, qy0 = ty * kTile + (wv >> 1) * 8;   // quadrant origin
+  const int bx0i = qx0 + (box & 1) * 4, by0i = qy0 + (box >> 1) * 4;             // box origin
+  const int pi = by0i + (pos >> 2), pj = bx0i + (pos & 3);
+  const bool inside = pi < H && pj < W;
+  const float px = (float)pj + off, py = (float)pi + off;
   float Tf = 1.f, Tl = 1.f, vr = 0.f, vg = 0.f, vb = 0.f, va = 0.f;
   int last = -1;
-  if (st.inside) {
-    const int64_t pix = ((int64_t)st.c * H + st.i) * W + st.j;
+  if (inside) {
+    const int64_t pix = ((int64_t)c * H + pi) * W + pj;
     last = last_in[pix];
     if (last >= b0) {
       if constexpr (IS2D) {
@@ -654,7 +681,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
         Tf = final_T[pix];
       }
       if constexpr (LOSS) {
-        loss_cotangent(lt, C, st.c, pix, (int64_t)st.i * W + st.j, (int64_t)W * H, vr, vg, vb, va);
+        loss_cotangent(lt, C, c, pix, (int64_t)pi * W + pj, (int64_t)W * H, vr, vg, vb, va);
       } else {
         vr = v_rgb[pix * 3 + 0];
         vg = v_rgb[pix * 3 + 1];
@@ -672,7 +699,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
     Sg = r.z;
     Sb = r.w;
   }
-  const float* bgc = bg + st.c * 3;
+  const float* bgc = bg + c * 3;
   const float bgdot = bgc[0] * vr + bgc[1] * vg + bgc[2] * vb;
   const float vTa = Tf * (va - bgdot);
   // the suffix colour enters only through its dot product with the pixel's colour cotangent
@@ -691,7 +718,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
     s_p1[threadIdx.x] = sp.p1;
     s_p2[threadIdx.x] = sp.p2;
   }
-  for (int i = threadIdx.x; i < kPartial * 2 * kChunk3; i += kRasterThreads) (&L[0][0][0])[i] = 0.f;
+  for (int i = threadIdx.x; i < kPartial * 4 * (kChunk3 + 1); i += kRasterThreads) (&L[0][0][0])[i] = 0.f;
   if (threadIdx.x == 0) {
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
     s_p0[kNull] = z;
@@ -699,34 +726,67 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
     s_p2[kNull] = z;
   }
   __syncthreads();
-  // cull the chunk against this wave's sub-tile; survivors are listed back to front
+  // cull the chunk against this wave's 8x8 quadrant; survivors are listed back to front
   int nsurv = 0;
+  {
+    const float x0 = (float)qx0 + off, y0 = (float)qy0 + off;
 #pragma unroll
-  for (int q = 3; q >= 0; --q) {
-    const int k = q * 64 + st.lane;
-    const bool keep = k < n && (b0 + k) <= wlast &&
-                      cull_keep<IS2D>(s_p0[k], s_p1[k], s_p2[k], st.bx0, st.bx1, st.by0, st.by1);
-    const unsigned long long mk = __ballot(keep);
-    if (keep) {
-      const unsigned long long above = st.lane == 63 ? 0ull : (mk >> (st.lane + 1));
-      s_list[wv][nsurv + __popcll(above)] = (short)k;
+    for (int q = 3; q >= 0; --q) {
+      const int k = q * 64 + lane;
+      const bool keep = k < n && (b0 + k) <= wlast &&
+                        cull_keep<IS2D>(s_p0[k], s_p1[k], s_p2[k], x0, x0 + 7.f, y0, y0 + 7.f);
+      const unsigned long long mk = __ballot(keep);
+      if (keep) {
+        const unsigned long long above = lane == 63 ? 0ull : (mk >> (lane + 1));
+        s_list[wv][nsurv + __popcll(above)] = (unsigned char)k;
+      }
+      nsurv += __popcll(mk);
     }
-    nsurv += __popcll(mk);
   }
-  if (st.lane < kGroup) s_list[wv][nsurv + st.lane] = (short)kNull;
   __builtin_amdgcn_wave_barrier();
+  // ... and the quadrant's survivors against each 4x4 box: lane l tests survivor s0 + (l>>2)
+  // against box l&3; a box's bits of the ballot keep the list order
+  int nb = 0;   // survivors of this lane's box
+  {
+    const float x0 = (float)bx0i + off, y0 = (float)by0i + off;
+    const unsigned long long boxbits = 0x1111111111111111ull << box;
+    for (int s0 = 0; s0 < nsurv; s0 += 16) {
+      const int s = s0 + pos;
+      const int k = s_list[wv][s < nsurv ? s : 0];
+      const bool keep = s < nsurv && cull_keep<IS2D>(s_p0[k], s_p1[k], s_p2[k], x0, x0 + 3.f, y0, y0 + 3.f);
+      const unsigned long long m = __ballot(keep) & boxbits;
+      if (keep) s_box[wv][box][nb + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned char)k;
+      nb += __popcll(m);
+    }
+  }
+  // groups walked by the wave: max over its boxes (lanes 4k..4k+3 hold the four counts)
+  const int ngrp = __builtin_amdgcn_readfirstlane(quad_max_i(nb));
+  const int npad = (ngrp + kGroup - 1) / kGroup * kGroup;
+  for (int s = nb + pos; s < npad; s += 16) s_box[wv][box][s] = (unsigned char)kNull;
+  __builtin_amdgcn_wave_barrier();
+  // after reduce_box16 lane l holds 4 of its box's sums, flat indices 4*(l>>2) + i = 9*g + q.
+  // They are staged in LDS (one b128 store per group), and lane f < 63 then adds flat index
+  // f = 9g + q of every box, box by box, into the wave's slot L[q][wv][entry]: inside one
+  // instruction the 63 (q, entry) addresses are distinct (a box lists an entry once), and
+  // the boxes follow in program order, so the plain read-add-write is race-free and
+  // deterministic -- no LDS atomics.
+  const int fg = lane / kPartial, fq = lane - kPartial * (lane / kPartial);
+  const bool fown = lane < kGroup * kPartial;
+  float* const Lw = &L[fq][wv][0];
+  const float* const stage_rd = &s_stage[wv][0][0] + 4 * (4 * (lane >> 2)) + (lane & 3);   // + 4*box
+  const unsigned char* my_list = s_box[wv][box];
   // Branch-free groups of 7 survivors: an invalid (entry, pixel) pair contributes zeros and
   // leaves T and S unchanged (ra = 1, fac = 0), so every group is straight-line code.
-  for (int g0 = 0; g0 < nsurv; g0 += kGroup) {
+  for (int g0 = 0; g0 < ngrp; g0 += kGroup) {
     float acc[64];
     acc[63] = 0.f;
 #pragma unroll
     for (int g = 0; g < kGroup; ++g) {
-      const int k = s_list[wv][g0 + g];
+      const int k = my_list[g0 + g];
       const float4 p0 = s_p0[k];
       const float4 p1 = s_p1[k];
       const float4 p2 = s_p2[k];
-      const float dx = p0.x - st.px, dy = p0.y - st.py;
+      const float dx = p0.x - px, dy = p0.y - py;
       const float sigma = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
       const float vis = __expf(-sigma);
       const float raw = p0.z * vis;
@@ -758,27 +818,34 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
       }
       // moments of v_sig: (dx, dy) here; the mean gradient (2a dx + b dy, b dx + 2c dy) is
       // formed from their sums per entry after the reduction
-      const float tx = v_sig * dx, ty = v_sig * dy;
-      acc[g * kPartial + 0] = tx;
-      acc[g * kPartial + 1] = ty;
-      acc[g * kPartial + 2] = tx * dx;
-      acc[g * kPartial + 3] = tx * dy;
-      acc[g * kPartial + 4] = ty * dy;
+      const float tx_ = v_sig * dx, ty_ = v_sig * dy;
+      acc[g * kPartial + 0] = tx_;
+      acc[g * kPartial + 1] = ty_;
+      acc[g * kPartial + 2] = tx_ * dx;
+      acc[g * kPartial + 3] = tx_ * dy;
+      acc[g * kPartial + 4] = ty_ * dy;
       acc[g * kPartial + 5] = v_sig;   // v_opacity = vis v_al = -v_sig / o (formed per entry below)
       if (!IS2D) Sv += fac * cv;
     }
-    const float sum = reduce64(acc);
-    const int g = st.lane / kPartial;
-    if (g < kGroup && g0 + g < nsurv)
-      __hip_atomic_fetch_add(&L[st.lane - g * kPartial][wv >> 1][s_list[wv][g0 + g]], sum, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
+    float sum[4];
+    reduce_box16(acc, sum);
+    reinterpret_cast<float4*>(&s_stage[wv][0][0])[lane] = make_float4(sum[0], sum[1], sum[2], sum[3]);
+    __builtin_amdgcn_wave_barrier();
+    if (fown) {
+#pragma unroll
+      for (int bx = 0; bx < 4; ++bx) {
+        const int k = s_box[wv][bx][g0 + fg];
+        Lw[k] += stage_rd[4 * bx];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
   if (threadIdx.x < n) {
     const int k = threadIdx.x;
     float v[kPartial];
 #pragma unroll
-    for (int q = 0; q < kPartial; ++q) v[q] = L[q][0][k] + L[q][1][k];
+    for (int q = 0; q < kPartial; ++q) v[q] = (L[q][0][k] + L[q][1][k]) + (L[q][2][k] + L[q][3][k]);
     const float4 p1 = s_p1[k];
     const float mx = v[0], my = v[1];
     v[0] = 2.f * p1.x * mx + p1.y * my;
@@ -795,6 +862,17 @@ __global__ void k_selftest_reduce64(float* out) {
   out[threadIdx.x] = reduce64(v);
 }
 
+// reduce_box16 on the same pattern: out[4*l + i] = lane l's i-th sum
+__global__ void k_selftest_reduce_box16(float* out) {
+  float v[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) v[i] = (float)((threadIdx.x * 7 + i * 13) % 97) + 0.25f * (float)i;
+  float s[4];
+  reduce_box16(v, s);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) out[4 * threadIdx.x + i] = s[i];
+}
+
 }  // namespace gsr
 
 using namespace gsr;
@@ -807,6 +885,14 @@ extern "C" {
 int gsr_selftest_reduce64(float* out, void* stream) {
   hipLaunchKernelGGL(k_selftest_reduce64, dim3(1), dim3(64), 0, (hipStream_t)stream, out);
   GSR_LAUNCH_CHECK("k_selftest_reduce64");
+  return GSR_OK;
+}
+
+// Self-test of the per-box reduction (the raster backward's): out[4*l + i] = sum over the 16
+// lanes l' with l' % 4 == l % 4 of v_l'[4*(l/4) + i], same pattern; out holds 256 floats.
+int gsr_selftest_reduce_box16(float* out, void* stream) {
+  hipLaunchKernelGGL(k_selftest_reduce_box16, dim3(1), dim3(64), 0, (hipStream_t)stream, out);
+  GSR_LAUNCH_CHECK("k_selftest_reduce_box16");
   return GSR_OK;
 }
 

@@ -31,6 +31,24 @@ def test_selftest_reduce64(cuda):
     assert torch.allclose(out.cpu().double(), v.sum(0), rtol=0, atol=1e-3), out
 
 
+def test_selftest_reduce_box16(cuda):
+    """The raster backward's per-box butterfly: lane l ends with the sums, over the 16 lanes
+    of its box (equal lane bits 0-1), of values 4*(l>>2) .. 4*(l>>2)+3."""
+    from gsr import _lib
+    out = torch.empty(256, device=cuda)
+    _lib.check(_lib.lib().gsr_selftest_reduce_box16(out.data_ptr(), torch.cuda.current_stream().cuda_stream),
+               "selftest")
+    lanes = torch.arange(64, dtype=torch.float64)[:, None]
+    i = torch.arange(64, dtype=torch.float64)[None, :]
+    v = ((lanes * 7 + i * 13) % 97) + 0.25 * i          # v[lane, value]
+    exp = torch.empty(64, 4, dtype=torch.float64)
+    for l in range(64):
+        same_box = [m for m in range(64) if m % 4 == l % 4]
+        for k in range(4):
+            exp[l, k] = v[same_box, 4 * (l // 4) + k].sum()
+    assert torch.allclose(out.cpu().double().view(64, 4), exp, rtol=0, atol=1e-3), out.view(64, 4)
+
+
 def test_selftest_lds_order(cuda):
     """The tile sort ranks keys with returning LDS atomics, relying on same-address atomics of
     one wave instruction being applied in lane order."""
