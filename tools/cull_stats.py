@@ -58,6 +58,12 @@ def main():
     ck = pos // chunk   # chunk within the tile
     t = tiles % (tw * th)
     ty, tx = t // tw, t % tw
+    walk = (ends - starts).clamp(min=0)
+    lens = toff[1:] - toff[:-1]
+    top = torch.topk(walk, 12)
+    print("longest walks (entries read before every pixel stopped):", top.values.tolist())
+    print("  their list lengths:", lens[top.indices].tolist())
+    print("walk percentiles (busy tiles):", [int(torch.quantile(walk[lens > 0].float(), q)) for q in (0.5, 0.9, 0.99)])
     print(f"{cfg.name}: I={b.n_isect} I_eff={int(n_act.sum())} chunks={int(((n_act + chunk - 1) // chunk).sum())}")
     res = {}
     G = 7
