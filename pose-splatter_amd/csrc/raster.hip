@@ -163,6 +163,11 @@ __device__ __forceinline__ int quad_min_i(int v) {
   v = min(v, dpp_i<kQuadXor1>(v));
   return min(v, dpp_i<kQuadXor2>(v));
 }
+// quad minimum of non-negative floats (transmittances): their bit patterns order like int32, so
+// the DPP-fused integer min applies (a float min needs NaN-canonicalising moves around it)
+__device__ __forceinline__ float quad_min_nonneg(float v) {
+  return __int_as_float(quad_min_i(__float_as_int(v)));
+}
 __device__ __forceinline__ int quad_max_i(int v) {
   v = max(v, dpp_i<kQuadXor1>(v));
   return max(v, dpp_i<kQuadXor2>(v));
@@ -297,7 +302,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
         ++kcur;
       }
       const int na = s_qn[buf][2 * h], nh = na + s_qn[buf][2 * h + 1];
-      int n = 0;
+      int n = 0, lastq = -1;
       for (int r0 = 0; r0 < nh; r0 += 64) {
         const int ii = r0 + lane;
         const int idx = ii < na ? 128 * h + ii : 128 * h + 64 + (ii - na);
@@ -309,9 +314,13 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
         n += __popcll(m);
       }
       __builtin_amdgcn_wave_barrier();
+      // the next group's queue slot is read one group ahead (one LDS round trip less on the
+      // serial chain of a group)
+      int idx_next = s_l[wv][q < n ? q : max(n - 1, 0)];
       for (int k0 = 0; k0 < n; k0 += 4) {
         const int k = k0 + q;
-        const int idx = s_l[wv][k < n ? k : n - 1];
+        const int idx = idx_next;
+        idx_next = s_l[wv][k + 4 < n ? k + 4 : n - 1];
         const float4 p0 = s_q0[buf][idx];
         const float4 p1 = s_q1[buf][idx];
         const float4 p2 = s_q2[buf][idx];
@@ -336,10 +345,14 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
         dr += p2.x * vis;
         dg += p2.y * vis;
         db += p2.z * vis;
-        last = con ? s_qe[buf][idx] : last;
+        lastq = con ? idx : lastq;
         if (IS2D) Tl = con ? Tq : Tl;
-        T = quad_min((IS2D ? q <= fs : q < fs) ? nT : T);
+        T = quad_min_nonneg((IS2D ? q <= fs : q < fs) ? nT : T);
         done = done || fs < 4;
+      }
+      if (lastq >= 0) {   // the entry index of this lane's latest composite, once per half
+        last = s_qe[buf][lastq];
+        lastq = -1;
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -427,7 +440,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
       db += p2.z * vis;
       last = con ? __float_as_int(p1.w) : last;
       if (IS2D) Tl = con ? Tq : Tl;
-      T = quad_min((IS2D ? q <= fs : q < fs) ? nT : T);
+      T = quad_min_nonneg((IS2D ? q <= fs : q < fs) ? nT : T);
       done = done || fs < 4;
     }
     __builtin_amdgcn_wave_barrier();
