@@ -134,7 +134,10 @@ def pmc_files(config: int, kind: str, pmc_dir: str = PROFILES):
 def traffic_from_csv(path: str, kernel_substr: str):
     """HBM bytes per launch from a rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE pass (KB units;
     FETCH_SIZE doubled per the gfx950 correction in MI355X_MICROARCH.md §HBM, calibrated there
-    for 16-B/lane streaming reads -- see tools/fetch_probe.hip for this path's access widths)."""
+    for 16-B/lane streaming reads.  tools/fetch_probe.hip calibrates this path's 48-B record
+    gathers beyond the Infinity Cache (profiles/r02_fetch_probe_*): 1.30 requests per record,
+    the 128-B lines a 16-B-aligned 48-B record touches (1.25) tallied at 64 B each, so the
+    same x2 gives the line traffic there too -- a gathered record moves >= 128 B)."""
     import csv
     fetch, write = [], []
     with open(path) as f:
