@@ -75,6 +75,8 @@ def parse(argv=None):
     ap.add_argument("--loss", default="none", choices=["none", "fused", "torch"],
                     help="3D, 1 GPU: time render + the reference IoU/L1 training loss "
                          "(train_script.py:128-133) fused into the kernels, or as plain torch ops")
+    ap.add_argument("--fwd-lanes", type=int, default=0, choices=[0, 4, 16],
+                    help="3D raster forward layout: 0 automatic, 4 or 16 lanes per pixel (gsr_set_fwd_lanes)")
     ap.add_argument("--pmc-dir", default=PROFILES, help="where the per-config rocprofv3 PMC passes live")
     return ap.parse_args(argv)
 
@@ -616,8 +618,10 @@ def main(argv=None):
         dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     from gsr import render as R
+    from gsr import _lib
     from gsr.scenes import CONFIGS
     cfg = CONFIGS[args.config]
+    _lib.check(_lib.lib().gsr_set_fwd_lanes(args.fwd_lanes), "gsr_set_fwd_lanes")
 
     if args.rank_share > 1:
         if world > 1:

@@ -26,6 +26,7 @@ constexpr int kFwdLdsPad = GSR_FWD_PAD_3D;
 #define GSR_FWD_PAD_2D 0   // 2D: every tile busy, no L2 locality to protect (6 per CU by VGPRs: measured 10% faster)
 #endif
 constexpr int kFwdLdsPad2D = GSR_FWD_PAD_2D;
+static int g_fwd_lanes = 0;   // gsr_set_fwd_lanes: 0 automatic, 4 or 16 forced
 
 
 __device__ __forceinline__ void tile_coords(int ct, int tw, int th, int& c, int& ty, int& tx) {
@@ -155,10 +156,6 @@ __device__ __forceinline__ float quad_sum(float v) {
   v += dpp_mov<kQuadXor1>(v);
   return v + dpp_mov<kQuadXor2>(v);
 }
-__device__ __forceinline__ float quad_min(float v) {
-  v = fminf(v, dpp_mov<kQuadXor1>(v));
-  return fminf(v, dpp_mov<kQuadXor2>(v));
-}
 __device__ __forceinline__ int quad_min_i(int v) {
   v = min(v, dpp_i<kQuadXor1>(v));
   return min(v, dpp_i<kQuadXor2>(v));
@@ -172,8 +169,88 @@ __device__ __forceinline__ int quad_max_i(int v) {
   v = max(v, dpp_i<kQuadXor1>(v));
   return max(v, dpp_i<kQuadXor2>(v));
 }
-// workgroups for the busy tiles: 4 per tile, rounded up to whole groups of 8 tiles (32 ids)
-__host__ __device__ __forceinline__ int busy_grid(int n_busy) { return 32 * ((n_busy + 7) / 8); }
+// Operations over the LPP lanes that serve one pixel in the forward: a DPP quad (LPP 4) or a
+// DPP row (LPP 16); q = the lane's slot in its group.  prefix: inclusive (Q) and exclusive (P)
+// products over the slots in order; suffix_excl: sum over the slots after q; next: slot q+1's
+// value.  The DPP moves run in every lane (a DPP read of a lane that is switched off returns
+// 0); only the selects depend on the slot.
+template <int LPP>
+struct PixGroup;
+template <>
+struct PixGroup<4> {
+  static __device__ __forceinline__ int min_i(int v) { return quad_min_i(v); }
+  static __device__ __forceinline__ int max_i(int v) { return quad_max_i(v); }
+  static __device__ __forceinline__ float sum(float v) { return quad_sum(v); }
+  static __device__ __forceinline__ void prefix(float x, int q, float& Q, float& P) {
+    const float d1 = dpp_mov<kQuadPrefix1>(x);
+    const float q1 = x * (q >= 1 ? d1 : 1.f);
+    const float d2 = dpp_mov<kQuadPrefix2>(q1);
+    Q = q1 * (q >= 2 ? d2 : 1.f);
+    const float d3 = dpp_mov<kQuadPrefix1>(Q);
+    P = q >= 1 ? d3 : 1.f;
+  }
+  static __device__ __forceinline__ float suffix_excl(float v, int q) {
+    const float d1 = dpp_mov<0xF9>(v);   // quad_perm [1,2,3,3]
+    const float y1 = v + (q < 3 ? d1 : 0.f);
+    const float d2 = dpp_mov<0xFE>(y1);  // quad_perm [2,3,3,3]
+    const float y2 = y1 + (q < 2 ? d2 : 0.f);
+    const float e = dpp_mov<0xF9>(y2);
+    return q < 3 ? e : 0.f;
+  }
+  static __device__ __forceinline__ float next(float v) { return dpp_mov<0xF9>(v); }
+};
+template <>
+struct PixGroup<16> {
+  static __device__ __forceinline__ int min_i(int v) {
+    v = quad_min_i(v);
+    v = min(v, dpp_i<0x141>(v));   // row_half_mirror
+    return min(v, dpp_i<0x140>(v));   // row_mirror
+  }
+  static __device__ __forceinline__ int max_i(int v) {
+    v = quad_max_i(v);
+    v = max(v, dpp_i<0x141>(v));
+    return max(v, dpp_i<0x140>(v));
+  }
+  static __device__ __forceinline__ float sum(float v) {
+    v = quad_sum(v);
+    v += dpp_mov<0x141>(v);
+    return v + dpp_mov<0x140>(v);
+  }
+  static __device__ __forceinline__ void prefix(float x, int q, float& Q, float& P) {
+    float y = x, d;
+    d = dpp_mov<0x111>(y); y *= (q >= 1 ? d : 1.f);   // row_shr:1 (lane - 1)
+    d = dpp_mov<0x112>(y); y *= (q >= 2 ? d : 1.f);
+    d = dpp_mov<0x114>(y); y *= (q >= 4 ? d : 1.f);
+    d = dpp_mov<0x118>(y); y *= (q >= 8 ? d : 1.f);
+    Q = y;
+    d = dpp_mov<0x111>(y);
+    P = q >= 1 ? d : 1.f;
+  }
+  static __device__ __forceinline__ float suffix_excl(float v, int q) {
+    float y = v, d;
+    d = dpp_mov<0x101>(y); y += (q < 15 ? d : 0.f);   // row_shl:1 (lane + 1)
+    d = dpp_mov<0x102>(y); y += (q < 14 ? d : 0.f);
+    d = dpp_mov<0x104>(y); y += (q < 12 ? d : 0.f);
+    d = dpp_mov<0x108>(y); y += (q < 8 ? d : 0.f);
+    d = dpp_mov<0x101>(y);
+    return q < 15 ? d : 0.f;
+  }
+  static __device__ __forceinline__ float next(float v) { return dpp_mov<0x101>(v); }
+};
+
+// Forward geometry per lanes-per-pixel: LPP 4 -> 4 workgroups per tile (8x8 quadrants), waves
+// of 4x4 pixels; LPP 16 -> 16 workgroups per tile (4x4 boxes), waves of 2x2 pixels (the
+// latency mode: a quarter of the serial chain, for scenes with few busy tiles).
+template <int LPP>
+struct FwdShape {
+  static constexpr int G = LPP == 4 ? 4 : 16;   // workgroups per tile
+  static constexpr int WB = LPP == 4 ? 8 : 4;   // workgroup box side
+  static constexpr int VB = WB / 2;             // wave box side
+  static_assert(VB * VB * LPP == 64, "a wave is VB x VB pixels x LPP lanes");
+};
+// workgroups for the busy tiles: G per tile, rounded up to whole groups of 8 tiles
+template <int LPP>
+__host__ __device__ __forceinline__ int busy_grid(int n_busy) { return 8 * FwdShape<LPP>::G * ((n_busy + 7) / 8); }
 
 // thread index of tile pixel (il, jl) in the backward's layout: wave = the 8x8 quadrant
 // (il>>3, jl>>3); inside it lane = 4 * (pixel within its 4x4 box) + box, so the lanes of one
@@ -197,7 +274,7 @@ __device__ __forceinline__ int bwd_pixel_slot(int il, int jl) {
 // pixel's last entry (its 1 - alpha may be exactly 0 when opacity == 1.0f).
 constexpr float kT2DMin = 2.98023224e-8f;   // 2^-25
 
-template <bool IS2D>
+template <bool IS2D, int LPP>
 __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ order, int W, int H, int tw, int th, const float* __restrict__ bg,
@@ -205,32 +282,36 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end, float4* __restrict__ ckpt,
     const int32_t* __restrict__ chunk_base, int n_busy, int64_t CT,
     uint64_t* __restrict__ tile_cut, float cut2d) {
+  static_assert(!IS2D || LPP == 4, "2D walks per wave with quads");
+  using PG = PixGroup<LPP>;
+  using FS = FwdShape<LPP>;
   __shared__ int s_max;
-  const int busy_blocks = busy_grid(n_busy);
+  const int busy_blocks = busy_grid<LPP>(n_busy);
   if ((int)blockIdx.x >= busy_blocks) {
     fill_empty<IS2D>(order, tile_offset, n_busy, busy_blocks, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
                      out_last, tile_end, tile_cut);
     return;
   }
-  // XCD-aware mapping: workgroups are dealt to the 8 XCDs round-robin by id, so the four
-  // quadrant workgroups of a tile get ids 32k + 8*quad + x (same id mod 8): they share one
-  // XCD's L2 for the tile's records.  Busy tile u = 8k + x, in longest-first order.
-  const int u = ((int)blockIdx.x >> 5) * 8 + ((int)blockIdx.x & 7);
-  const int quad = ((int)blockIdx.x >> 3) & 3;
+  // XCD-aware mapping: workgroups are dealt to the 8 XCDs round-robin by id, so the G
+  // workgroups of a tile get ids 8G*k + 8*sub + x (same id mod 8): they share one XCD's L2
+  // for the tile's records.  Busy tile u = 8k + x, in longest-first order.
+  const int u = ((int)blockIdx.x / (8 * FS::G)) * 8 + ((int)blockIdx.x & 7);
+  const int sub = ((int)blockIdx.x >> 3) & (FS::G - 1);
   if (u >= n_busy) return;
   const int ct = order[u];
   int c, ty, tx;
   tile_coords(ct, tw, th, c, ty, tx);
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int q = lane & 3, p = lane >> 2;
-  const int ox = ((quad & 1) << 3) + ((wv & 1) << 2), oy = ((quad >> 1) << 3) + ((wv >> 1) << 2);
-  const int il = oy + (p >> 2), jl = ox + (p & 3);
+  const int q = lane & (LPP - 1), p = lane / LPP;
+  const int sx = (sub % (kTile / FS::WB)) * FS::WB, sy = (sub / (kTile / FS::WB)) * FS::WB;
+  const int ox = sx + (wv & 1) * FS::VB, oy = sy + (wv >> 1) * FS::VB;
+  const int il = oy + p / FS::VB, jl = ox + p % FS::VB;
   const int i = ty * kTile + il, j = tx * kTile + jl;
   const bool inside = i < H && j < W;
   const float off = IS2D ? 0.f : 0.5f;   // 2D: integer centres (src/gaussian_renderer.py:355-358)
   const float px = (float)j + off, py = (float)i + off;
-  const float bx0 = (float)(tx * kTile + ox) + off, bx1 = bx0 + 3.f;
-  const float by0 = (float)(ty * kTile + oy) + off, by1 = by0 + 3.f;
+  const float bx0 = (float)(tx * kTile + ox) + off, bx1 = bx0 + (float)(FS::VB - 1);
+  const float by0 = (float)(ty * kTile + oy) + off, by1 = by0 + (float)(FS::VB - 1);
   const int start = tile_offset[ct], end = tile_offset[ct + 1];
   if (threadIdx.x == 0) s_max = -1;
   __syncthreads();
@@ -257,8 +338,8 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   // once per quadrant instead of once per wave.
   static_assert(kChunk3 % 128 == 0, "a round half is one 128-entry chunk");
   const int e_last = max(end - 1, start);
-  const float qx0 = (float)(tx * kTile + ((quad & 1) << 3)) + off, qx1 = qx0 + 7.f;
-  const float qy0 = (float)(ty * kTile + ((quad >> 1) << 3)) + off, qy1 = qy0 + 7.f;
+  const float qx0 = (float)(tx * kTile + sx) + off, qx1 = qx0 + (float)(FS::WB - 1);
+  const float qy0 = (float)(ty * kTile + sy) + off, qy1 = qy0 + (float)(FS::WB - 1);
   float4 c0 = make_float4(0.f, 0.f, 0.f, 0.f), c1 = c0, c2 = c0;
   int idn = 0;
   if (end > start) {
@@ -292,7 +373,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
       const int hb = rb + 128 * h;
       if (hb >= end || __ballot(!done) == 0ull) break;
       if (hb > start && ((hb - start) % kChunk3) == 0) {   // entering chunk kcur+1
-        const float Dr = quad_sum(dr), Dg = quad_sum(dg), Db = quad_sum(db);
+        const float Dr = PG::sum(dr), Dg = PG::sum(dg), Db = PG::sum(db);
         if (q == 0) ckpt[(int64_t)(cbase + kcur) * kRasterThreads + bwd_pixel_slot(il, jl)] = make_float4(Ts, Dr, Dg, Db);
         cr += Dr;
         cg += Dg;
@@ -317,10 +398,10 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
       // the next group's queue slot is read one group ahead (one LDS round trip less on the
       // serial chain of a group)
       int idx_next = s_l[wv][q < n ? q : max(n - 1, 0)];
-      for (int k0 = 0; k0 < n; k0 += 4) {
+      for (int k0 = 0; k0 < n; k0 += LPP) {
         const int k = k0 + q;
         const int idx = idx_next;
-        idx_next = s_l[wv][k + 4 < n ? k + 4 : n - 1];
+        idx_next = s_l[wv][k + LPP < n ? k + LPP : n - 1];
         const float4 p0 = s_q0[buf][idx];
         const float4 p1 = s_q1[buf][idx];
         const float4 p2 = s_q2[buf][idx];
@@ -331,14 +412,10 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
         const bool valid = IS2D ? (k < n && !done && alpha >= cut2d)
                                 : (k < n && !done && sg >= 0.f && alpha >= kAlphaThreshold);
         const float xq = valid ? 1.f - alpha : 1.f;
-        const float d1 = dpp_mov<kQuadPrefix1>(xq);
-        const float q1 = xq * (q >= 1 ? d1 : 1.f);
-        const float d2 = dpp_mov<kQuadPrefix2>(q1);
-        const float Qi = q1 * (q >= 2 ? d2 : 1.f);
-        const float d3 = dpp_mov<kQuadPrefix1>(Qi);
-        const float Pe = q >= 1 ? d3 : 1.f;
+        float Qi, Pe;
+        PG::prefix(xq, q, Qi, Pe);
         const float nT = T * Qi;
-        const int fs = quad_min_i(valid && nT <= (IS2D ? kT2DMin : kTMin) ? q : 4);
+        const int fs = PG::min_i(valid && nT <= (IS2D ? kT2DMin : kTMin) ? q : LPP);
         const bool con = valid && (IS2D ? q <= fs : q < fs);
         const float Tq = T * Pe;
         const float vis = con ? alpha * Tq : 0.f;
@@ -347,8 +424,9 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
         db += p2.z * vis;
         lastq = con ? idx : lastq;
         if (IS2D) Tl = con ? Tq : Tl;
-        T = quad_min_nonneg((IS2D ? q <= fs : q < fs) ? nT : T);
-        done = done || fs < 4;
+        // the group minimum of non-negative transmittances, on their int32 bit patterns
+        T = __int_as_float(PG::min_i(__float_as_int((IS2D ? q <= fs : q < fs) ? nT : T)));
+        done = done || fs < LPP;
       }
       if (lastq >= 0) {   // the entry index of this lane's latest composite, once per half
         last = s_qe[buf][lastq];
@@ -451,7 +529,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     if (b0 + 64 >= end || !step(b0 + 64, y0, y1, y2, idq, idp)) break;
   }
   }
-  const float Dr = quad_sum(dr), Dg = quad_sum(dg), Db = quad_sum(db);
+  const float Dr = PG::sum(dr), Dg = PG::sum(dg), Db = PG::sum(db);
   cr += Dr;
   cg += Dg;
   cb += Db;
@@ -466,18 +544,18 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     Tl = ol > last ? oT : Tl;
     last = max(last, ol);
   } else {
-    last = quad_max_i(last);
+    last = PG::max_i(last);
   }
   if (end > start) {
     // Turn this pixel's chunk records {T at chunk start, chunk colour sum} into what the
     // backward needs at each chunk's END: {T_end, suffix colour sum of the later chunks}
-    // (positive terms, summed back to front).  The pixel's four quad lanes split the chunks
-    // into four contiguous ranges: each sums its range's colour, a quad suffix of the range
+    // (positive terms, summed back to front).  The pixel's LPP lanes split the chunks into
+    // LPP contiguous ranges: each sums its range's colour, a group suffix sum of the range
     // sums gives each range's starting suffix, then each rewrites its range back to front
-    // (records re-read 8 at a time).  A quarter of the serial chain of one lane.
+    // (records re-read 8 at a time).  1/LPP of the serial chain of one lane.
     float4* ck = ckpt + (int64_t)cbase * kRasterThreads + bwd_pixel_slot(il, jl);
     if (q == 0) ck[(int64_t)kcur * kRasterThreads] = make_float4(T, 0.f, 0.f, 0.f);
-    const int per = (kcur + 3) >> 2;
+    const int per = (kcur + LPP - 1) / LPP;
     const int r0 = min(kcur, q * per), r1 = min(kcur, r0 + per);
     float Rr = 0.f, Rg = 0.f, Rb = 0.f, F = 0.f;
     for (int k0 = r0; k0 < r1; k0 += 8) {
@@ -494,15 +572,9 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
           Rb += r[u].w;
         }
     }
-    // suffix of the later ranges (lanes q+1..3) plus the current chunk's own colour
-    const float R1r = dpp_mov<0x55>(Rr), R1g = dpp_mov<0x55>(Rg), R1b = dpp_mov<0x55>(Rb);
-    const float R2r = dpp_mov<0xAA>(Rr), R2g = dpp_mov<0xAA>(Rg), R2b = dpp_mov<0xAA>(Rb);
-    const float R3r = dpp_mov<0xFF>(Rr), R3g = dpp_mov<0xFF>(Rg), R3b = dpp_mov<0xFF>(Rb);
-    const float Fn = dpp_mov<0xF9>(F);   // quad_perm [1,2,3,3]: F of the next range
-    float sr = Dr, sg = Dg, sb = Db;
-    if (q < 3) { sr += R3r; sg += R3g; sb += R3b; }
-    if (q < 2) { sr += R2r; sg += R2g; sb += R2b; }
-    if (q < 1) { sr += R1r; sg += R1g; sb += R1b; }
+    // suffix of the later ranges (slots q+1..LPP-1) plus the current chunk's own colour
+    const float Fn = PG::next(F);   // F of the next range
+    float sr = Dr + PG::suffix_excl(Rr, q), sg = Dg + PG::suffix_excl(Rg, q), sb = Db + PG::suffix_excl(Rb, q);
     float Tn = r1 < kcur ? Fn : Ts;
     for (int k0 = r1 - 1; k0 >= r0; k0 -= 8) {
       float4 r[8];
@@ -903,6 +975,13 @@ int gsr_selftest_reduce64(float* out, void* stream) {
 
 // Self-test of the per-box reduction (the raster backward's): out[4*l + i] = sum over the 16
 // lanes l' with l' % 4 == l % 4 of v_l'[4*(l/4) + i], same pattern; out holds 256 floats.
+int gsr_set_fwd_lanes(int lanes) {
+  GSR_REQUIRE(lanes == 0 || lanes == 4 || lanes == 16, "gsr_set_fwd_lanes: lanes must be 0 (auto), 4 or 16, got %d",
+              lanes);
+  gsr::g_fwd_lanes = lanes;
+  return GSR_OK;
+}
+
 int gsr_selftest_reduce_box16(float* out, void* stream) {
   hipLaunchKernelGGL(k_selftest_reduce_box16, dim3(1), dim3(64), 0, (hipStream_t)stream, out);
   GSR_LAUNCH_CHECK("k_selftest_reduce_box16");
@@ -912,6 +991,15 @@ int gsr_selftest_reduce_box16(float* out, void* stream) {
 }  // extern "C"
 
 namespace gsr {
+
+// Lanes per pixel of the 3D forward: 16 when the quad layout's 4 workgroups per busy tile
+// would fill under half of the chip's ~1 280 workgroup slots (n_busy <= kFwd16MaxBusy);
+// gsr_set_fwd_lanes forces one (tests run both layouts on the same scenes).
+constexpr int kFwd16MaxBusy = 160;
+static int fwd_lanes(int n_busy) {
+  if (g_fwd_lanes == 4 || g_fwd_lanes == 16) return g_fwd_lanes;
+  return n_busy <= kFwd16MaxBusy ? 16 : 4;
+}
 
 // Shared by the 3D and 2D entry points (2D: C = 1, index-order keys, final_T [H,W,2]).
 template <bool IS2D>
@@ -932,11 +1020,20 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
   // gsr_bin_offsets wrote)
   // Dynamic-LDS padding caps the forward at 4 workgroups per CU (measured: 4 and 5 per CU
   // beat 6, whose extra tiles in flight spill each XCD's L2; 3 starves the CU).
-  hipLaunchKernelGGL(k_raster_fwd<IS2D>, dim3((unsigned)(busy_grid(n_busy) + n_fill)), dim3(kRasterThreads),
-                     IS2D ? kFwdLdsPad2D : kFwdLdsPad, s, (const Splat*)rec, sorted_ids, tile_offset, tile_order,
-                     width, height, tw, th,
-                     bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state, chunk_base,
-                     (int)n_busy, CT, tile_cut, cut2d);
+  // 3D with few busy tiles (a single small view, a multi-GPU rank's share): 16 lanes per pixel,
+  // 16 workgroups per tile -- a quarter of the serial walk per wave, for a chip the quad layout
+  // would leave mostly idle
+  if (!IS2D && fwd_lanes(n_busy) == 16) {
+    hipLaunchKernelGGL((k_raster_fwd<false, 16>), dim3((unsigned)(busy_grid<16>(n_busy) + n_fill)),
+                       dim3(kRasterThreads), kFwdLdsPad, s, (const Splat*)rec, sorted_ids, tile_offset, tile_order,
+                       width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state,
+                       chunk_base, (int)n_busy, CT, tile_cut, cut2d);
+  } else {
+    hipLaunchKernelGGL((k_raster_fwd<IS2D, 4>), dim3((unsigned)(busy_grid<4>(n_busy) + n_fill)),
+                       dim3(kRasterThreads), IS2D ? kFwdLdsPad2D : kFwdLdsPad, s, (const Splat*)rec, sorted_ids,
+                       tile_offset, tile_order, width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end,
+                       (float4*)chunk_state, chunk_base, (int)n_busy, CT, tile_cut, cut2d);
+  }
   GSR_LAUNCH_CHECK(who);
   if (n_busy > 0) {
     hipLaunchKernelGGL(k_raster_finalize, dim3(ceil_div(n_busy, kRasterThreads)), dim3(kRasterThreads), 0, s,

@@ -61,6 +61,7 @@ EXPORTS = {
     "gsr_last_error": (ctypes.c_char_p, []),
     "gsr_selftest_reduce64": (ctypes.c_int, [_P, _P]),
     "gsr_selftest_reduce_box16": (ctypes.c_int, [_P, _P]),
+    "gsr_set_fwd_lanes": (ctypes.c_int, [_I32]),
     "gsr_selftest_lds_order": (ctypes.c_int, [_P, _P]),
     "gsr3d_project_fwd": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _I32, _I32, _I32, _F, _F, _F, _F,
                                          _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _I32, _P]),

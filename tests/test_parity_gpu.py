@@ -59,6 +59,16 @@ def test_selftest_lds_order(cuda):
     assert int(out.item()) == 0
 
 
+@pytest.fixture(params=[4, 16], ids=["lanes4", "lanes16"])
+def fwd_lanes(request, cuda):
+    """Run a test under each 3D forward layout (4 lanes per pixel / 4 workgroups per tile, and
+    16 / 16), forced through gsr_set_fwd_lanes; automatic selection afterwards."""
+    from gsr import _lib
+    _lib.check(_lib.lib().gsr_set_fwd_lanes(request.param), "gsr_set_fwd_lanes")
+    yield request.param
+    _lib.check(_lib.lib().gsr_set_fwd_lanes(0), "gsr_set_fwd_lanes")
+
+
 def _oracle3d():
     from oracle import oracle3d
     return oracle3d
@@ -107,7 +117,7 @@ def _cot(C, H, W, seed):
     (200, 48, 40, 2, 3, 1.0),
     (2000, 96, 80, 3, 4, 0.0),
 ])
-def test_3d_small_vs_oracle(cuda, N, W, H, C, seed, shift):
+def test_3d_small_vs_oracle(cuda, fwd_lanes, N, W, H, C, seed, shift):
     p, V, K = _scene3d(N, W, H, C, seed, extent=0.05, scale_shift=shift)
     bg = torch.tensor([0.1, 0.5, 0.9])
     vr, va = _cot(C, H, W, seed + 100)
@@ -128,7 +138,7 @@ def test_3d_multiview_equals_single_views(cuda):
         assert torch.equal(rgb_b[c], rgb_c[0]) and torch.equal(a_b[c], a_c[0])
 
 
-def test_3d_deterministic(cuda):
+def test_3d_deterministic(cuda, fwd_lanes):
     W, H, C = 96, 80, 2
     p, V, K = _scene3d(20000, W, H, C, 8)
     bg = torch.ones(3)
@@ -219,7 +229,7 @@ def _check_binning_exact(p, V, K, W, H, C, cuda):
     return b
 
 
-def test_3d_cfg1_vs_oracle(cuda):
+def test_3d_cfg1_vs_oracle(cuda, fwd_lanes):
     """BASELINE config 1 scene (10k Gaussians, 192x170, 1 view) fwd+bwd vs the oracle."""
     from gsr.scenes import CONFIGS, gaussians3d, ring_cameras
     c = CONFIGS[1]
@@ -253,7 +263,7 @@ def test_3d_isotropic_radius_mode(cuda):
     grad_close(g_g, g_o, what="grad")
 
 
-def test_3d_edge_cases(cuda):
+def test_3d_edge_cases(cuda, fwd_lanes):
     W, H = 48, 40
     p, V, K = _scene3d(64, W, H, 1, 31, extent=0.05, scale_shift=1.5)
     bg = torch.tensor([0.2, 0.3, 0.4])
@@ -298,7 +308,7 @@ def test_3d_speculative_arena_regrow(cuda):
     assert torch.equal(rgb1, rgb3) and torch.equal(a1, a3) and torch.equal(g1, g3)
 
 
-def test_3d_long_tile_lists(cuda):
+def test_3d_long_tile_lists(cuda, fwd_lanes):
     """> 16384 entries in one tile list: exercises the run-sort + global merge path."""
     W, H = 32, 32
     N = 40000
