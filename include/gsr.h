@@ -349,16 +349,29 @@ int gsr_pose3d_bwd(const float* params, int64_t N, int64_t row_stride, double an
                    float* g_params, void* stream);
 
 /* ---- Shape carving -----------------------------------------------
- * ShapeCarver.forward (src/shape_carver.py:330-366, adaptive=False): the [4, n_voxels]
- * volume (mask occupancy, then rgb) from C masks [C,1,H,W] and images [C,3,H,W], with the
- * scatter-min visibility of ray_cast_visibility_torch (:132-204) done as 64-bit atomicMin.
+ * ShapeCarver.forward (src/shape_carver.py:322-366): the [4, n_voxels] volume (mask
+ * occupancy, then rgb) from C masks [C,1,H,W] and images [C,3,H,W], with the scatter-min
+ * visibility of ray_cast_visibility_torch (:132-204) done as 64-bit atomicMin.
  * grid [n_voxels,3] = the model's un-posed grid points; center [3] (device) and angle pose
  * it (get_grid_points :369-374); Ks [C,3,3] and Es [C,4,4] are HOST arrays (fixed model
- * cameras).  Ties in the per-pixel minimum distance go to the lower voxel index. */
+ * cameras).  Ks_mask (host, or NULL = Ks) are the intrinsics of the mask volume: the adaptive
+ * path (:328-335) projects the masks with principal points moved to the triangulated seed and
+ * samples colours with the carver's own Ks.  Ties in the per-pixel minimum distance go to the
+ * lower voxel index. */
 size_t gsr_carve_workspace(int64_t n_voxels, int C, int height);
 int gsr_carve_volume(const float* grid, int64_t n_voxels, const float* center, double angle, const float* Ks,
-                     const float* Es, int C, const float* mask, const float* rgb, int height, int width,
-                     float fill, float nonvisible_weight, void* ws, size_t ws_bytes, float* out, void* stream);
+                     const float* Ks_mask, const float* Es, int C, const float* mask, const float* rgb, int height,
+                     int width, float fill, float nonvisible_weight, void* ws, size_t ws_bytes, float* out,
+                     void* stream);
+
+/* Adaptive cameras, step 1 of adjust_principal_points_to_seed (src/shape_carving.py:173-245):
+ * for each of C masks [C,H,W] (float, nonzero = inside; device), medoid[c] = the flat index
+ * y*W+x of the mask pixel nearest the mask centroid (float64 means and squared distances as
+ * numpy computes them; ties to the lowest index), or INT32_MAX for an empty mask (the
+ * reference raises).  medoid: device int32 [C]; ws: device, gsr_carve_medoids_workspace(C). */
+size_t gsr_carve_medoids_workspace(int C);
+int gsr_carve_medoids(const float* masks, int C, int height, int width, void* ws, size_t ws_bytes, int32_t* medoid,
+                      void* stream);
 
 #ifdef __cplusplus
 }

@@ -8,7 +8,8 @@ parity pinned by source reading):
   ('amin'), argmin ties to the lowest source index (torch_scatter's CPU order)
 * project_points_torch_single_cam :207-235, compute_voxel_colors_torch :238-301 (including
   its `_, H, W, _ = images.shape` read of a [C,3,H,W] tensor)
-* ShapeCarver.forward :330-366 (adaptive=False), get_grid_points :369-374
+* ShapeCarver.forward :322-366 (both branches), get_grid_points :369-374
+* adjust_principal_points_to_seed (src/shape_carving.py:173-245), restated below in numpy
 """
 import numpy as np
 import torch
@@ -90,11 +91,42 @@ def get_grid_points(grid, center, angle):
     return torch.einsum("abci,ji->abcj", grid, rot) + center.view(1, 1, 1, 3)
 
 
-def shape_carver_forward(grid, K, E, mask, rgb, center, angle, fill=0.45):
+def adjust_principal_points_to_seed(masks, Ks, extrinsics):
+    """src/shape_carving.py:173-245: medoid per view (np.nonzero, float64 means, argmin of the
+    squared distance), DLT triangulation of the seed, principal points moved so that the seed
+    projects through each medoid.  masks [V,H,W] numpy; Ks [V,3,3], extrinsics [V,4,4] numpy."""
+    V = masks.shape[0]
+    med = []
+    for i in range(V):
+        ys, xs = np.nonzero(masks[i])
+        if xs.size == 0:
+            raise ValueError(f"Mask {i} is empty")
+        cy, cx = ys.mean(), xs.mean()
+        j = np.argmin((ys - cy) ** 2 + (xs - cx) ** 2)
+        med.append((xs[j], ys[j]))
+    med = np.array(med, dtype=np.float64)
+    Ps = np.stack([Ks[i] @ np.concatenate([extrinsics[i][:3, :3], extrinsics[i][:3, 3:]], axis=1)
+                   for i in range(V)], axis=0)
+    A = np.vstack([r for i in range(V) for r in (med[i, 0] * Ps[i][2] - Ps[i][0], med[i, 1] * Ps[i][2] - Ps[i][1])])
+    _, _, Vt = np.linalg.svd(A)
+    Xh = Vt[-1]
+    Xh /= Xh[3]
+    X = Xh[:3]
+    new = Ks.copy()
+    for i in range(V):
+        Xc = extrinsics[i][:3, :3] @ X + extrinsics[i][:3, 3]
+        new[i, 0, 2] = med[i, 0] - Ks[i, 0, 0] * (Xc[0] / Xc[2])
+        new[i, 1, 2] = med[i, 1] - Ks[i, 1, 1] * (Xc[1] / Xc[2])
+    return new, X, med
+
+
+def shape_carver_forward(grid, K, E, mask, rgb, center, angle, fill=0.45, K_mask=None):
+    """ShapeCarver.forward; K_mask = the adapted intrinsics of the adaptive branch (the mask
+    volume uses them, the colours keep K), with center = the triangulated seed."""
     C = K.shape[0]
     g = get_grid_points(grid, center, angle)
     n1, n2, n3 = g.shape[:3]
-    mv = get_volume_torch(mask, K, E, g)
+    mv = get_volume_torch(mask, K if K_mask is None else K_mask, E, g)
     out = 0.0
     for thresh in [1, (C - 1) / C]:
         b = (mv >= thresh).flatten()

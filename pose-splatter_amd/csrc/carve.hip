@@ -1,5 +1,6 @@
 // Shape carving: the project-and-gather volume builder of
-// ShapeCarver.forward (src/shape_carver.py:330-366, non-adaptive), with the scatter-min
+// ShapeCarver.forward (src/shape_carver.py:330-366; adaptive cameras move the mask volume's
+// principal points, Ks_mask, and keep the carver's K for colours, as the reference does), with the scatter-min
 // visibility of ray_cast_visibility_torch (:132-204, torch_scatter.scatter_min at :197) as
 // a 64-bit atomicMin on (distance bits, voxel index) keys.
 //
@@ -29,7 +30,8 @@ constexpr int kCarveMaxCams = 32;
 
 struct CarveCams {
   float E[kCarveMaxCams][12];   // rows 0..2 of each extrinsic [4,4]
-  float K[kCarveMaxCams][9];
+  float K[kCarveMaxCams][9];    // colour / visibility intrinsics (the carver's own K)
+  float Km[kCarveMaxCams][9];   // mask-volume intrinsics (adaptive: principal points moved)
   float pos[kCarveMaxCams][3];  // camera centres -R^T t
 };
 
@@ -42,7 +44,8 @@ __device__ __forceinline__ void grid_point(const float* __restrict__ grid, int64
   p[2] = fmaf(g2, 1.f, fmaf(g1, 0.f, g0 * 0.f)) + center[2];
 }
 
-// K (E [p;1])[:3] -> (u, v, w) homogeneous pixel
+// K (E [p;1])[:3] -> (u, v, w) homogeneous pixel; MASK selects the mask-volume intrinsics
+template <bool MASK = false>
 __device__ __forceinline__ void project_h(const CarveCams& cm, int c, const float p[3], float& u, float& v,
                                           float& w) {
   float q[3];
@@ -51,7 +54,7 @@ __device__ __forceinline__ void project_h(const CarveCams& cm, int c, const floa
     const float* e = cm.E[c] + 4 * k;
     q[k] = fmaf(e[3], 1.f, fmaf(e[2], p[2], fmaf(e[1], p[1], e[0] * p[0])));
   }
-  const float* K = cm.K[c];
+  const float* K = MASK ? cm.Km[c] : cm.K[c];
   u = fmaf(K[2], q[2], fmaf(K[1], q[1], K[0] * q[0]));
   v = fmaf(K[5], q[2], fmaf(K[4], q[1], K[3] * q[0]));
   w = fmaf(K[8], q[2], fmaf(K[7], q[1], K[6] * q[0]));
@@ -75,7 +78,7 @@ __global__ __launch_bounds__(kCarveThreads) void k_carve_mask(
   float sum = 0.f;
   for (int cam = 0; cam < C; ++cam) {
     float u, v, w;
-    project_h(cm, cam, p, u, v, w);
+    project_h<true>(cm, cam, p, u, v, w);
     const float d = w + 1e-8f;
     const int x = round_clamp(u / d, W), y = round_clamp(v / d, H);
     sum += mask[((int64_t)cam * H + y) * W + x];
@@ -183,6 +186,68 @@ __global__ __launch_bounds__(kCarveThreads) void k_carve_volume(
   for (int k = 0; k < 4; ++k) out[(int64_t)k * N + i] = acc[k];
 }
 
+// ---------------------------------------------------------------- adaptive cameras: mask medoids
+// adjust_principal_points_to_seed (src/shape_carving.py:173-245) step 1 on the device: per view,
+// the mask pixel nearest the mask centroid (numpy: ys, xs = nonzero(mask); cy, cx = means;
+// argmin of (ys-cy)^2 + (xs-cx)^2, first in row-major order).  The coordinate sums are exact
+// int64 (so the float64 means equal numpy's), the distances are float64 with numpy's
+// rounding (no fused multiply-add), the minimum is an atomicMin on the distance's bits
+// (non-negative doubles order like uint64) and the tie goes to the lowest flat index.
+__global__ __launch_bounds__(kCarveThreads) void k_medoid_sums(const float* __restrict__ mask, int H, int W,
+                                                              unsigned long long* __restrict__ sums) {
+  const int c = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = i < (int64_t)H * W && mask[(int64_t)c * H * W + i] != 0.f;
+  unsigned long long n = in ? 1ull : 0ull, sx = in ? (unsigned long long)(i % W) : 0ull,
+                     sy = in ? (unsigned long long)(i / W) : 0ull;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    n += __shfl_xor(n, o, 64);
+    sx += __shfl_xor(sx, o, 64);
+    sy += __shfl_xor(sy, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0 && n) {
+    atomicAdd(&sums[3 * c + 0], n);
+    atomicAdd(&sums[3 * c + 1], sx);
+    atomicAdd(&sums[3 * c + 2], sy);
+  }
+}
+
+__device__ __forceinline__ double medoid_d2(int64_t i, int W, const unsigned long long* s) {
+  const double n = (double)s[0];
+  const double cx = (double)s[1] / n, cy = (double)s[2] / n;
+  const double dy = __dsub_rn((double)(i / W), cy), dx = __dsub_rn((double)(i % W), cx);
+  return __dadd_rn(__dmul_rn(dy, dy), __dmul_rn(dx, dx));
+}
+
+__global__ __launch_bounds__(kCarveThreads) void k_medoid_min(const float* __restrict__ mask, int H, int W,
+                                                             const unsigned long long* __restrict__ sums,
+                                                             unsigned long long* __restrict__ best) {
+  const int c = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)H * W || mask[(int64_t)c * H * W + i] == 0.f) return;
+  atomicMin(&best[c], (unsigned long long)__double_as_longlong(medoid_d2(i, W, sums + 3 * c)));
+}
+
+__global__ __launch_bounds__(kCarveThreads) void k_medoid_arg(const float* __restrict__ mask, int H, int W,
+                                                             const unsigned long long* __restrict__ sums,
+                                                             const unsigned long long* __restrict__ best,
+                                                             int32_t* __restrict__ arg) {
+  const int c = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)H * W || mask[(int64_t)c * H * W + i] == 0.f) return;
+  if ((unsigned long long)__double_as_longlong(medoid_d2(i, W, sums + 3 * c)) == best[c]) atomicMin(&arg[c], (int32_t)i);
+}
+
+__global__ void k_medoid_init(int C, unsigned long long* sums, unsigned long long* best, int32_t* arg) {
+  const int t = threadIdx.x;
+  for (int k = t; k < 3 * C; k += blockDim.x) sums[k] = 0ull;
+  for (int k = t; k < C; k += blockDim.x) {
+    best[k] = ~0ull;
+    arg[k] = 0x7fffffff;
+  }
+}
+
 }  // namespace gsr
 
 using namespace gsr;
@@ -194,8 +259,9 @@ size_t gsr_carve_workspace(int64_t n_voxels, int C, int height) {
 }
 
 int gsr_carve_volume(const float* grid, int64_t n_voxels, const float* center, double angle, const float* Ks,
-                     const float* Es, int C, const float* mask, const float* rgb, int height, int width,
-                     float fill, float nonvisible_weight, void* ws, size_t ws_bytes, float* out, void* stream) {
+                     const float* Ks_mask, const float* Es, int C, const float* mask, const float* rgb, int height,
+                     int width, float fill, float nonvisible_weight, void* ws, size_t ws_bytes, float* out,
+                     void* stream) {
   GSR_REQUIRE(n_voxels >= 0 && C >= 1 && C <= kCarveMaxCams && height > 0 && width > 0,
               "gsr_carve_volume: bad sizes (voxels=%lld, C=%d (max %d), image %dx%d)", (long long)n_voxels, C,
               kCarveMaxCams, width, height);
@@ -209,6 +275,7 @@ int gsr_carve_volume(const float* grid, int64_t n_voxels, const float* center, d
   for (int c = 0; c < C; ++c) {
     for (int k = 0; k < 12; ++k) cm.E[c][k] = Es[c * 16 + k];
     for (int k = 0; k < 9; ++k) cm.K[c][k] = Ks[c * 9 + k];
+    for (int k = 0; k < 9; ++k) cm.Km[c][k] = (Ks_mask ? Ks_mask : Ks)[c * 9 + k];
     // -R^T t, einsum('cij,cj->ci', R^T, t)
     for (int i = 0; i < 3; ++i) {
       float a = 0.f;
@@ -236,6 +303,31 @@ int gsr_carve_volume(const float* grid, int64_t n_voxels, const float* center, d
                      height, width, fill, nonvisible_weight, (const uint8_t*)flags, (const unsigned long long*)zbuf,
                      out);
   GSR_LAUNCH_CHECK("k_carve_volume");
+  return GSR_OK;
+}
+
+size_t gsr_carve_medoids_workspace(int C) { return (size_t)C * 4 * sizeof(unsigned long long) + 16; }
+
+int gsr_carve_medoids(const float* masks, int C, int height, int width, void* ws, size_t ws_bytes, int32_t* medoid,
+                      void* stream) {
+  GSR_REQUIRE(C >= 1 && height > 0 && width > 0 && (int64_t)height * width < (1ll << 31),
+              "gsr_carve_medoids: bad sizes (C=%d, image %dx%d)", C, width, height);
+  GSR_REQUIRE(masks && medoid && ws, "gsr_carve_medoids: null pointer");
+  GSR_REQUIRE(ws_bytes >= gsr_carve_medoids_workspace(C), "gsr_carve_medoids: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  unsigned long long* sums = (unsigned long long*)(((uintptr_t)ws + 7) & ~(uintptr_t)7);
+  unsigned long long* best = sums + 3 * C;
+  hipLaunchKernelGGL(k_medoid_init, dim3(1), dim3(256), 0, s, C, sums, best, medoid);
+  GSR_LAUNCH_CHECK("k_medoid_init");
+  const dim3 grid((unsigned)ceil_div64((int64_t)height * width, kCarveThreads), (unsigned)C);
+  hipLaunchKernelGGL(k_medoid_sums, grid, dim3(kCarveThreads), 0, s, masks, height, width, sums);
+  GSR_LAUNCH_CHECK("k_medoid_sums");
+  hipLaunchKernelGGL(k_medoid_min, grid, dim3(kCarveThreads), 0, s, masks, height, width,
+                     (const unsigned long long*)sums, best);
+  GSR_LAUNCH_CHECK("k_medoid_min");
+  hipLaunchKernelGGL(k_medoid_arg, grid, dim3(kCarveThreads), 0, s, masks, height, width,
+                     (const unsigned long long*)sums, (const unsigned long long*)best, medoid);
+  GSR_LAUNCH_CHECK("k_medoid_arg");
   return GSR_OK;
 }
 
