@@ -752,38 +752,41 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
   const int pi = by0i + (pos >> 2), pj = bx0i + (pos & 3);
   const bool inside = pi < H && pj < W;
   const float px = (float)pj + off, py = (float)pi + off;
+  // Every load is issued up front, none waiting for `last` (the per-WG latency chain is what
+  // bounds this kernel's fixed part): the pixel's state, its chunk record, the chunk's ids and
+  // sort positions; pixels that stopped before this chunk then drop them by select.
+  const float4 rck = ckpt[(int64_t)chunk * kRasterThreads + threadIdx.x];
+  const int id_mine = threadIdx.x < n ? ids[b0 + threadIdx.x] : 0;
+  const int kos_mine = threadIdx.x < n ? k_of_s[b0 + threadIdx.x] : 0;
   float Tf = 1.f, Tl = 1.f, vr = 0.f, vg = 0.f, vb = 0.f, va = 0.f;
   int last = -1;
   if (inside) {
     const int64_t pix = ((int64_t)c * H + pi) * W + pj;
     last = last_in[pix];
-    if (last >= b0) {
-      if constexpr (IS2D) {
-        const float2 t2 = reinterpret_cast<const float2*>(final_T)[pix];
-        Tf = t2.x;
-        Tl = t2.y;
-      } else {
-        Tf = final_T[pix];
-      }
-      if constexpr (LOSS) {
-        loss_cotangent(lt, C, c, pix, (int64_t)pi * W + pj, (int64_t)W * H, vr, vg, vb, va);
-      } else {
-        vr = v_rgb[pix * 3 + 0];
-        vg = v_rgb[pix * 3 + 1];
-        vb = v_rgb[pix * 3 + 2];
-        va = v_alpha[pix];
-      }
+    if constexpr (IS2D) {
+      const float2 t2 = reinterpret_cast<const float2*>(final_T)[pix];
+      Tf = t2.x;
+      Tl = t2.y;
+    } else {
+      Tf = final_T[pix];
+    }
+    if constexpr (LOSS) {
+      loss_cotangent(lt, C, c, pix, (int64_t)pi * W + pj, (int64_t)W * H, vr, vg, vb, va);
+    } else {
+      vr = v_rgb[pix * 3 + 0];
+      vg = v_rgb[pix * 3 + 1];
+      vb = v_rgb[pix * 3 + 2];
+      va = v_alpha[pix];
     }
   }
-  // state at the end of this chunk: {T_end, suffix colour sum} (forward epilogue)
-  float T = Tf, Sr = 0.f, Sg = 0.f, Sb = 0.f;
-  if (last >= b0) {
-    const float4 r = ckpt[(int64_t)chunk * kRasterThreads + threadIdx.x];
-    T = r.x;
-    Sr = r.y;
-    Sg = r.z;
-    Sb = r.w;
+  const bool live = last >= b0;
+  if (!live) {
+    Tf = Tl = 1.f;
+    vr = vg = vb = va = 0.f;
   }
+  // state at the end of this chunk: {T_end, suffix colour sum} (forward epilogue)
+  const float T0 = live ? rck.x : Tf, Sr = live ? rck.y : 0.f, Sg = live ? rck.z : 0.f, Sb = live ? rck.w : 0.f;
+  float T = T0;
   const float* bgc = bg + c * 3;
   const float bgdot = bgc[0] * vr + bgc[1] * vg + bgc[2] * vb;
   const float vTa = Tf * (va - bgdot);
@@ -798,7 +801,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wlast = max(wlast, __shfl_xor(wlast, o, 64));
   if (threadIdx.x < n) {
-    const Splat sp = rec[ids[b0 + threadIdx.x]];
+    const Splat sp = rec[id_mine];
     s_p0[threadIdx.x] = sp.p0;
     s_p1[threadIdx.x] = sp.p1;
     s_p2[threadIdx.x] = sp.p2;
@@ -816,7 +819,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
   {
     const float x0 = (float)qx0 + off, y0 = (float)qy0 + off;
 #pragma unroll
-    for (int q = 3; q >= 0; --q) {
+    for (int q = kChunk3 / 64 - 1; q >= 0; --q) {
       const int k = q * 64 + lane;
       const bool keep = k < n && (b0 + k) <= wlast &&
                         cull_keep<IS2D>(s_p0[k], s_p1[k], s_p2[k], x0, x0 + 7.f, y0, y0 + 7.f);
@@ -944,7 +947,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
     v[0] = 2.f * p1.x * mx + p1.y * my;
     v[1] = p1.y * mx + 2.f * p1.z * my;
     v[5] = -v[5] / s_p0[k].z;
-    store_partial_row(partial, k_of_s[b0 + k], v);
+    store_partial_row(partial, kos_mine, v);
   }
 }
 
