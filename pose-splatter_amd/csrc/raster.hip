@@ -324,9 +324,8 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   int kcur = 0;
   float Ts = 1.f, dr = 0.f, dg = 0.f, db = 0.f;   // dr..: this lane's share of the chunk's colour
   if constexpr (!IS2D) {
-  __shared__ float4 s_q0[2][256];
-  __shared__ float4 s_q1[2][256];
-  __shared__ float4 s_q2[2][256];
+  // one array (records of slot i at s_q[buf][0..2][i]): one address, immediate offsets
+  __shared__ float4 s_q[2][3][256];
   __shared__ int s_qe[2][256];
   __shared__ int s_qn[2][4];
   __shared__ unsigned char s_l[4][128];
@@ -357,9 +356,9 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
       if (keep) {
         const int slot = 64 * wv +
                          __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-        s_q0[buf][slot] = c0;
-        s_q1[buf][slot] = c1;
-        s_q2[buf][slot] = c2;
+        s_q[buf][0][slot] = c0;
+        s_q[buf][1][slot] = c1;
+        s_q[buf][2][slot] = c2;
         s_qe[buf][slot] = e;
       }
       if (lane == 0) s_qn[buf][wv] = __popcll(m);
@@ -387,7 +386,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
       for (int r0 = 0; r0 < nh; r0 += 64) {
         const int ii = r0 + lane;
         const int idx = ii < na ? 128 * h + ii : 128 * h + 64 + (ii - na);
-        const bool keep = ii < nh && cull_keep<IS2D>(s_q0[buf][idx], s_q1[buf][idx], s_q2[buf][idx], bx0, bx1, by0, by1);
+        const bool keep = ii < nh && cull_keep<IS2D>(s_q[buf][0][idx], s_q[buf][1][idx], s_q[buf][2][idx], bx0, bx1, by0, by1);
         const unsigned long long m = __ballot(keep);
         if (keep)
           s_l[wv][n + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] =
@@ -402,9 +401,9 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
         const int k = k0 + q;
         const int idx = idx_next;
         idx_next = s_l[wv][k + LPP < n ? k + LPP : n - 1];
-        const float4 p0 = s_q0[buf][idx];
-        const float4 p1 = s_q1[buf][idx];
-        const float4 p2 = s_q2[buf][idx];
+        const float4 p0 = s_q[buf][0][idx];
+        const float4 p1 = s_q[buf][1][idx];
+        const float4 p2 = s_q[buf][2][idx];
         const float dx = p0.x - px, dy = p0.y - py;
         const float sg = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
         const float raw = p0.z * __expf(-sg);
@@ -438,9 +437,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   } else {
   // 2D (every tile busy and long; the per-wave walk measured faster there): each wave walks
   // the list on its own in 64-entry batches.
-  __shared__ float4 s_p0[4][64];
-  __shared__ float4 s_p1[4][64];
-  __shared__ float4 s_p2[4][64];
+  __shared__ float4 s_pw[4][3][64];
   // software pipeline over 64-entry batches (records of b+1, b+2 and ids of b+3 in flight;
   // see the notes of the 2-way unrolled loop below)
   const int e_last = max(end - 1, start);
@@ -476,9 +473,9 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     const int n = __popcll(m);
     if (keep) {
       const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-      s_p0[wv][slot] = c0;
-      s_p1[wv][slot] = make_float4(c1.x, c1.y, c1.z, __int_as_float(b0 + lane));
-      s_p2[wv][slot] = c2;
+      s_pw[wv][0][slot] = c0;
+      s_pw[wv][1][slot] = make_float4(c1.x, c1.y, c1.z, __int_as_float(b0 + lane));
+      s_pw[wv][2][slot] = c2;
     }
     id_new = ids[min(b0 + 192 + lane, e_last)];
     const Splat sc = rec[id_use];
@@ -487,9 +484,9 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     for (int k0 = 0; k0 < n; k0 += 4) {
       const int k = k0 + q;
       const int kk = k < n ? k : n - 1;
-      const float4 p0 = s_p0[wv][kk];
-      const float4 p1 = s_p1[wv][kk];
-      const float4 p2 = s_p2[wv][kk];
+      const float4 p0 = s_pw[wv][0][kk];
+      const float4 p1 = s_pw[wv][1][kk];
+      const float4 p2 = s_pw[wv][2][kk];
       const float dx = p0.x - px, dy = p0.y - py;
       const float sg = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
       const float raw = p0.z * __expf(-sg);
@@ -728,9 +725,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
   constexpr int kNull = kChunk3;
   constexpr int kGroup = 7;
   constexpr int kLen = kChunk3 + kGroup;   // survivor list capacity (padded to whole groups)
-  __shared__ float4 s_p0[kChunk3 + 1];
-  __shared__ float4 s_p1[kChunk3 + 1];
-  __shared__ float4 s_p2[kChunk3 + 1];
+  __shared__ float4 s_p[3][kChunk3 + 1];   // the chunk's records, part j of entry k at s_p[j][k]
   // gradient sums per entry, one slot per wave (index kNull absorbs the padding's zeros)
   __shared__ float L[kPartial][4][kChunk3 + 1];
   __shared__ unsigned char s_list[4][kLen];     // quadrant survivors, back to front
@@ -802,16 +797,16 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
   for (int o = 32; o > 0; o >>= 1) wlast = max(wlast, __shfl_xor(wlast, o, 64));
   if (threadIdx.x < n) {
     const Splat sp = rec[id_mine];
-    s_p0[threadIdx.x] = sp.p0;
-    s_p1[threadIdx.x] = sp.p1;
-    s_p2[threadIdx.x] = sp.p2;
+    s_p[0][threadIdx.x] = sp.p0;
+    s_p[1][threadIdx.x] = sp.p1;
+    s_p[2][threadIdx.x] = sp.p2;
   }
   for (int i = threadIdx.x; i < kPartial * 4 * (kChunk3 + 1); i += kRasterThreads) (&L[0][0][0])[i] = 0.f;
   if (threadIdx.x == 0) {
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    s_p0[kNull] = z;
-    s_p1[kNull] = z;
-    s_p2[kNull] = z;
+    s_p[0][kNull] = z;
+    s_p[1][kNull] = z;
+    s_p[2][kNull] = z;
   }
   __syncthreads();
   // cull the chunk against this wave's 8x8 quadrant; survivors are listed back to front
@@ -822,7 +817,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
     for (int q = kChunk3 / 64 - 1; q >= 0; --q) {
       const int k = q * 64 + lane;
       const bool keep = k < n && (b0 + k) <= wlast &&
-                        cull_keep<IS2D>(s_p0[k], s_p1[k], s_p2[k], x0, x0 + 7.f, y0, y0 + 7.f);
+                        cull_keep<IS2D>(s_p[0][k], s_p[1][k], s_p[2][k], x0, x0 + 7.f, y0, y0 + 7.f);
       const unsigned long long mk = __ballot(keep);
       if (keep) {
         const unsigned long long above = lane == 63 ? 0ull : (mk >> (lane + 1));
@@ -841,7 +836,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
     for (int s0 = 0; s0 < nsurv; s0 += 16) {
       const int s = s0 + pos;
       const int k = s_list[wv][s < nsurv ? s : 0];
-      const bool keep = s < nsurv && cull_keep<IS2D>(s_p0[k], s_p1[k], s_p2[k], x0, x0 + 3.f, y0, y0 + 3.f);
+      const bool keep = s < nsurv && cull_keep<IS2D>(s_p[0][k], s_p[1][k], s_p[2][k], x0, x0 + 3.f, y0, y0 + 3.f);
       const unsigned long long m = __ballot(keep) & boxbits;
       if (keep) s_box[wv][box][nb + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned char)k;
       nb += __popcll(m);
@@ -875,9 +870,9 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
 #pragma unroll
     for (int g = 0; g < kGroup; ++g) {
       const int k = my_list[g0 + g];
-      const float4 p0 = s_p0[k];
-      const float4 p1 = s_p1[k];
-      const float4 p2 = s_p2[k];
+      const float4 p0 = s_p[0][k];
+      const float4 p1 = s_p[1][k];
+      const float4 p2 = s_p[2][k];
       const float dx = p0.x - px, dy = p0.y - py;
       const float sigma = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
       const float vis = __expf(-sigma);
@@ -942,11 +937,11 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
     float v[kPartial];
 #pragma unroll
     for (int q = 0; q < kPartial; ++q) v[q] = (L[q][0][k] + L[q][1][k]) + (L[q][2][k] + L[q][3][k]);
-    const float4 p1 = s_p1[k];
+    const float4 p1 = s_p[1][k];
     const float mx = v[0], my = v[1];
     v[0] = 2.f * p1.x * mx + p1.y * my;
     v[1] = p1.y * mx + 2.f * p1.z * my;
-    v[5] = -v[5] / s_p0[k].z;
+    v[5] = -v[5] / s_p[0][k].z;
     store_partial_row(partial, kos_mine, v);
   }
 }
