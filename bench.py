@@ -73,8 +73,8 @@ def parse(argv=None):
                                                                "process may run on)")
     ap.add_argument("--psnr", type=int, default=1, help="0 disables the dPSNR check")
     ap.add_argument("--loss", default="none", choices=["none", "fused", "torch"],
-                    help="3D, 1 GPU: time render + the reference IoU/L1 training loss "
-                         "(train_script.py:128-133) fused into the kernels, or as plain torch ops")
+                    help="3D, 1 GPU: time render + the reference IoU/L1/SSIM training loss "
+                         "(train_script.py:127-133) fused into libgsr kernels, or as plain torch ops")
     ap.add_argument("--fwd-lanes", type=int, default=0, choices=[0, 4, 16],
                     help="3D raster forward layout: 0 automatic, 4 or 16 lanes per pixel (gsr_set_fwd_lanes)")
     ap.add_argument("--pmc-dir", default=PROFILES, help="where the per-config rocprofv3 PMC passes live")
@@ -352,6 +352,22 @@ def delta_psnr(cfg, params_cpu, V, K, dev, rgb_oracle_view0=None):
 
 # ------------------------------------------------------------------ workloads
 
+def _torch_ssim(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """The reference's SSIM term as plain torch ops (torchmetrics' algorithm: 11-tap Gaussian,
+    sigma 1.5, reflect pad + crop, data_range 1.0) -- the `--loss torch` comparison only."""
+    import torch.nn.functional as F
+    dist = torch.arange(-5.0, 6.0, 1.0, device=x.device)
+    g = torch.exp(-torch.pow(dist / 1.5, 2) / 2)
+    g = g / g.sum()
+    C = x.shape[1]
+    kern = torch.matmul(g[:, None], g[None, :]).expand(C, 1, 11, 11)
+    p, t = F.pad(x, (5, 5, 5, 5), mode="reflect"), F.pad(y, (5, 5, 5, 5), mode="reflect")
+    mp, mt, pp, tt, pt = F.conv2d(torch.cat((p, t, p * p, t * t, p * t)), kern, groups=C).split(x.shape[0])
+    full = ((2 * mp * mt + 1e-4) * (2 * (pt - mp * mt) + 9e-4)) / ((mp * mp + mt * mt + 1e-4) *
+                                                                  (pp - mp * mp + tt - mt * mt + 9e-4))
+    return full[..., 5:-5, 5:-5].reshape(x.shape[0], -1).mean(-1).mean()
+
+
 class Workload:
     """One rank's share of a config's step.  step() enqueues one step; `units` is the number of
     rendered views (frames) the WHOLE job completes per step; views_here the ones this rank
@@ -478,22 +494,27 @@ class Workload:
             dist.all_reduce(self.params.grad)
 
     def _loss_step(self):
+        """The reference training loss on the render: IoU + L1 image + ssim_lambda * (1 - SSIM)
+        (scripts/training/train_script.py:127-133), fused (libgsr kernels) or as torch ops."""
         cfg, R = self.cfg, self.R
         if not hasattr(self, "timg"):
             g3 = torch.Generator().manual_seed(cfg.seed + 3)
             self.timg = torch.rand(cfg.views, 3, cfg.height, cfg.width, generator=g3).to(self.dev)
             self.tmask = (torch.rand(cfg.views, cfg.height, cfg.width, generator=g3) < 0.3).float().to(self.dev)
+        ssim_lambda = 1.0
         if self.loss == "fused":
-            from gsr.loss import render3d_iou_l1
+            from gsr.loss import render3d_iou_l1, ssim
             li, lm, rgb, alpha = render3d_iou_l1(self.params, self.Vd, self.Kd, cfg.width, cfg.height, self.bg,
                                                  self.timg, self.tmask, 1.0)
+            ls = ssim_lambda * (1 - ssim(self.timg, rgb))
         else:
             rgb, alpha = R.render3d(self.params, self.Vd, self.Kd, cfg.width, cfg.height, self.bg)
             inter = (alpha * self.tmask).sum(dim=(-2, -1))
             union = (alpha + self.tmask - alpha * self.tmask).sum(dim=(-2, -1))
             li = 1 - ((inter + 1e-6) / (union + 1e-6)).mean()
             lm = torch.abs(self.timg - rgb.permute(0, 3, 1, 2)).sum() / self.tmask.sum()
-        (li + lm).backward()
+            ls = ssim_lambda * (1 - _torch_ssim(self.timg, rgb.permute(0, 3, 1, 2)))
+        (li + lm + ls).backward()
 
     def launch_shape(self):
         """(C, P) of the dominant launch sequence: cameras and pixels one launch covers."""

@@ -1,17 +1,19 @@
 """Loss-fused render: the reference training step's IoU + L1 image loss
 (scripts/training/train_script.py:30-36 `get_iou_loss`, :128-130 `img_loss`) evaluated and
-differentiated on the MI355X without materialising any cotangent image.
+differentiated on the MI355X without materialising any cotangent image, and its SSIM term
+(:129, torchmetrics SSIM, data_range 1.0) as two libgsr kernels (`ssim`).
 
     iou_loss, img_loss, rgb, alpha = render3d_iou_l1(params, viewmats, Ks, W, H, bg,
                                                      target_img, target_mask, img_lambda)
-    total = iou_loss + img_loss + ssim_lambda * (1 - ssim(target_img, rgb))   # optional SSIM
+    total = iou_loss + img_loss + ssim_lambda * (1 - gsr.loss.ssim(target_img, rgb))
     total.backward()
 
 Forward: render (gsr3d_*), then one streaming pass (gsr_loss_iou_l1_fwd) reduces
 {sum a m, sum a + m - a m, sum m, sum |t - rgb|} per view in a fixed order and forms the two
 losses on the device (no host sync).  Backward: the raster backward generates every pixel's
 cotangent from those sums and the incoming loss gradients (gsr3d_raster_bwd_loss); gradients
-that reach `rgb` / `alpha` through other terms (SSIM) are added in the same kernel.
+that reach `rgb` / `alpha` through other terms (the SSIM term's rgb gradient, written by
+gsr_ssim_bwd) are added in the same kernel.
 
 Shapes follow the reference's per-view tensors stacked over C views: target_img [C,3,H,W]
 (planar, the loader's layout; [3,H,W] accepted for C=1), target_mask [C,H,W] ([H,W] for C=1).
@@ -28,7 +30,82 @@ from . import _lib
 from ._lib import check, lib
 from .render import (RenderOptions3D, _forward3d, _ptr, _require_device, _stream, _timed, backward3d)
 
-__all__ = ["render3d_iou_l1"]
+__all__ = ["render3d_iou_l1", "ssim"]
+
+
+def _taps11() -> torch.Tensor:
+    """torchmetrics' 1-D Gaussian for sigma 1.5 (11 taps), computed with the same float32 ops
+    (host tensor: libgsr copies the taps into the kernel arguments)."""
+    dist = torch.arange(-5.0, 6.0, 1.0, dtype=torch.float32)
+    g = torch.exp(-torch.pow(dist / 1.5, 2) / 2)
+    return (g / g.sum()).contiguous()
+
+
+_TAPS = None
+
+
+def _strides4(t: torch.Tensor, channels_last: bool):
+    """(view, channel, row, column) element strides of a [C,3,H,W] or [C,H,W,3] image."""
+    s = t.stride()
+    return (s[0], s[3], s[1], s[2]) if channels_last else (s[0], s[1], s[2], s[3])
+
+
+class _Ssim(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, target_img, rgb):
+        global _TAPS
+        if _TAPS is None:
+            _TAPS = _taps11()
+        L = lib()
+        dev = rgb.device
+        C, H, W = rgb.shape[0], rgb.shape[1], rgb.shape[2]
+        x = target_img.detach().to(device=dev, dtype=torch.float32)
+        y = rgb.detach().float()
+        xs = torch.tensor(_strides4(x, False), dtype=torch.int64)
+        ys = torch.tensor(_strides4(y, True), dtype=torch.int64)
+        ws = torch.empty(int(L.gsr_ssim_workspace(C, W, H)), device=dev, dtype=torch.uint8)
+        out = torch.empty((), device=dev, dtype=torch.float32)
+        with _timed("ssim_fwd"):
+            check(L.gsr_ssim_fwd(_ptr(x), xs.data_ptr(), _ptr(y), ys.data_ptr(), C, W, H, _TAPS.data_ptr(), _ptr(ws),
+                                 ws.numel(), _ptr(out), _stream(dev)), "gsr_ssim_fwd")
+        ctx.save_for_backward(x, y)
+        ctx.strides = (xs, ys)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y = ctx.saved_tensors
+        xs, ys = ctx.strides
+        L = lib()
+        dev = y.device
+        C, H, W = y.shape[0], y.shape[1], y.shape[2]
+        gy = torch.empty_strided(y.shape, y.stride(), device=dev, dtype=torch.float32)
+        g = g.detach().float().reshape(()).contiguous()
+        with _timed("ssim_bwd"):
+            check(L.gsr_ssim_bwd(_ptr(x), xs.data_ptr(), _ptr(y), ys.data_ptr(), C, W, H, _TAPS.data_ptr(), _ptr(g),
+                                 _ptr(gy), _stream(dev)), "gsr_ssim_bwd")
+        return None, gy
+
+
+def ssim(target_img: torch.Tensor, rgb: torch.Tensor) -> torch.Tensor:
+    """The reference's SSIM term on the device: torchmetrics
+    StructuralSimilarityIndexMeasure(data_range=1.0)(target_img, rgb) for C views at once (the
+    batch mean, scripts/training/train_script.py:129), differentiable w.r.t. ``rgb``.
+    target_img [C,3,H,W] (planar, the loader's layout; [3,H,W] for C=1), rgb [C,H,W,3] (the
+    renderer's layout; [H,W,3] for C=1), read in place; H, W > 10."""
+    if rgb.dim() == 3:
+        rgb = rgb[None]
+    if target_img.dim() == 3:
+        target_img = target_img[None]
+    if rgb.dim() != 4 or rgb.shape[-1] != 3:
+        raise ValueError(f"rgb must be [C,H,W,3], got {tuple(rgb.shape)}")
+    C, H, W, _ = rgb.shape
+    if target_img.shape != (C, 3, H, W):
+        raise ValueError(f"target_img must be [C,3,H,W] = {(C, 3, H, W)}, got {tuple(target_img.shape)}")
+    if H <= 10 or W <= 10:
+        raise ValueError(f"SSIM needs images larger than 10x10 (11x11 Gaussian window), got {H}x{W}")
+    _require_device(rgb, "ssim")
+    return _Ssim.apply(target_img, rgb)
 
 
 class _RenderIouL1(torch.autograd.Function):
