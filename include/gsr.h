@@ -98,9 +98,10 @@ int gsr_selftest_reduce64(float* out, void* stream);
  * out[4*l + i] = sum over the 16 lanes L with L % 4 == l % 4 of v_L[4*(l/4) + i].  out: 256 floats. */
 int gsr_selftest_reduce_box16(float* out, void* stream);
 
-/* Layout of the 3D raster forward (process-wide): 0 = automatic (16 lanes per pixel and 16
- * workgroups per tile when at most 160 tiles are busy, else 4 and 4), 4 or 16 to force one.
- * Both give the same result up to fp32 regrouping of the transmittance products. */
+/* Layout of the raster forward (process-wide): 0 = automatic (3D: 16 lanes per pixel and 16
+ * workgroups per tile with at most 160 busy tiles, else 4 lanes per pixel and 4 workgroups per
+ * tile; 2D: 1 lane per pixel, one workgroup per tile), or 1, 4 or 16 (3D only) to force one.
+ * All give the same result up to fp32 regrouping of the transmittance products. */
 int gsr_set_fwd_lanes(int lanes);
 
 /* Self-test of the lane-ordered LDS atomics the tile sort's ranking relies on: writes the

@@ -26,7 +26,7 @@ constexpr int kFwdLdsPad = GSR_FWD_PAD_3D;
 #define GSR_FWD_PAD_2D 0   // 2D: every tile busy, no L2 locality to protect (6 per CU by VGPRs: measured 10% faster)
 #endif
 constexpr int kFwdLdsPad2D = GSR_FWD_PAD_2D;
-static int g_fwd_lanes = 0;   // gsr_set_fwd_lanes: 0 automatic, 4 or 16 forced
+static int g_fwd_lanes = 0;   // gsr_set_fwd_lanes: 0 automatic, 1 / 4 / 16 forced
 
 
 __device__ __forceinline__ void tile_coords(int ct, int tw, int th, int& c, int& ty, int& tx) {
@@ -607,6 +607,213 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   if (threadIdx.x == 0 && s_max >= 0) atomicMax(&tile_end[ct], s_max);   // finalised by k_raster_finalize
 }
 
+// ---------------------------------------------------------------- forward, box layout
+// The throughput layout (2D; selectable for 3D): ONE workgroup
+// per busy tile, ONE lane per pixel, laid out as in the backward (wave = 8x8 quadrant, lane l
+// = pixel l>>2 of the 4x4 box l&3), so each pixel composites its entries with gsplat's
+// sequential recursion T <- T (1 - a) -- no quad prefix products, no DPP on the serial chain.
+// The tile's list is walked in 256-entry rounds: every thread gathers one entry's record
+// (one round ahead) into a double-buffered LDS image; per 128-entry half (one chunk) each
+// wave culls the half against its 8x8 quadrant (exact test, as everywhere), then the
+// quadrant's survivors against each 4x4 box, and every lane walks its box's survivor list in
+// order (the wave runs max over its four boxes; a lane past its own list idles).  A wave
+// leaves as soon as all its pixels are done, the workgroup as soon as all four waves are.
+// Chunk records are written per pixel at thread index = the backward's slot, coalesced.
+template <bool IS2D>
+__global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
+    const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
+    const int32_t* __restrict__ order, int W, int H, int tw, int th, const float* __restrict__ bg,
+    float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
+    int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end, float4* __restrict__ ckpt,
+    const int32_t* __restrict__ chunk_base, int n_busy, int64_t CT,
+    uint64_t* __restrict__ tile_cut, float cut2d) {
+  __shared__ float4 s_r[2][3][256];              // round records, part j of slot i at s_r[buf][j][i]
+  __shared__ unsigned char s_list[4][128];       // a half's quadrant survivors (slot in the half)
+  __shared__ unsigned char s_box[4][4][128];     // ... and each box's, in list order
+  __shared__ int s_max;
+  static_assert(kChunk3 == 128, "a round half is one chunk");
+  const int busy_blocks = (n_busy + 7) & ~7;
+  if ((int)blockIdx.x >= busy_blocks) {
+    fill_empty<IS2D>(order, tile_offset, n_busy, busy_blocks, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
+                     out_last, tile_end, tile_cut);
+    return;
+  }
+  if ((int)blockIdx.x >= n_busy) return;
+  const int ct = order[blockIdx.x];
+  int c, ty, tx;
+  tile_coords(ct, tw, th, c, ty, tx);
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int box = lane & 3, pos = lane >> 2;
+  const float off = IS2D ? 0.f : 0.5f;   // 2D: integer centres (src/gaussian_renderer.py:355-358)
+  const int qx0 = tx * kTile + (wv & 1) * 8, qy0 = ty * kTile + (wv >> 1) * 8;   // quadrant origin
+  const int bx0i = qx0 + (box & 1) * 4, by0i = qy0 + (box >> 1) * 4;             // box origin
+  const int i = by0i + (pos >> 2), j = bx0i + (pos & 3);
+  const bool inside = i < H && j < W;
+  const float px = (float)j + off, py = (float)i + off;
+  const int start = tile_offset[ct], end = tile_offset[ct + 1];
+  if (threadIdx.x == 0) s_max = -1;
+  float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f;
+  float Tl = 1.f;   // 2D: T before the latest composited entry
+  int last = -1;
+  bool done = !inside;
+  const int cbase = chunk_base[ct];
+  int kcur = 0;
+  float Ts = 1.f, dr = 0.f, dg = 0.f, db = 0.f;   // the current chunk's start T and colour
+  const int e_last = max(end - 1, start);
+  // round prefetch: this thread's entry of the next round (record in registers, id ahead)
+  float4 c0 = make_float4(0.f, 0.f, 0.f, 0.f), c1 = c0, c2 = c0;
+  int idn = 0;
+  if (end > start) {
+    const int id0 = ids[min(start + (int)threadIdx.x, e_last)];
+    idn = ids[min(start + 256 + (int)threadIdx.x, e_last)];
+    c0 = rec[id0].p0;
+    c1 = rec[id0].p1;
+    c2 = rec[id0].p2;
+  }
+  int buf = 0;
+  for (int rb = start; rb < end; rb += 256, buf ^= 1) {
+    s_r[buf][0][threadIdx.x] = c0;
+    s_r[buf][1][threadIdx.x] = c1;
+    s_r[buf][2][threadIdx.x] = c2;
+    {
+      const int id_use = idn;
+      idn = ids[min(rb + 512 + (int)threadIdx.x, e_last)];
+      c0 = rec[id_use].p0;
+      c1 = rec[id_use].p1;
+      c2 = rec[id_use].p2;
+    }
+    if (__syncthreads_count(!done) == 0) break;
+    for (int h = 0; h < 2; ++h) {
+      const int hb = rb + 128 * h;
+      if (hb >= end || __ballot(!done) == 0ull) break;
+      if (hb > start) {   // entering chunk kcur+1 (halves are chunks)
+        ckpt[(int64_t)(cbase + kcur) * kRasterThreads + threadIdx.x] = make_float4(Ts, dr, dg, db);
+        cr += dr;
+        cg += dg;
+        cb += db;
+        dr = dg = db = 0.f;
+        Ts = T;
+        ++kcur;
+      }
+      const int nh = min(128, end - hb);
+      // the half against the wave's 8x8 quadrant (two entries per lane), in list order
+      int nsurv = 0;
+      {
+        const float x0 = (float)qx0 + off, y0 = (float)qy0 + off;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int k = q * 64 + lane;
+          const int sl = 128 * h + k;
+          const bool keep = k < nh && cull_keep<IS2D>(s_r[buf][0][sl], s_r[buf][1][sl], s_r[buf][2][sl], x0,
+                                                     x0 + 7.f, y0, y0 + 7.f);
+          const unsigned long long m = __ballot(keep);
+          if (keep)
+            s_list[wv][nsurv + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] =
+                (unsigned char)k;
+          nsurv += __popcll(m);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      // ... and the quadrant's survivors against each 4x4 box
+      int nb = 0;
+      {
+        const float x0 = (float)bx0i + off, y0 = (float)by0i + off;
+        const unsigned long long boxbits = 0x1111111111111111ull << box;
+        for (int s0 = 0; s0 < nsurv; s0 += 16) {
+          const int s = s0 + pos;
+          const int k = s_list[wv][s < nsurv ? s : 0];
+          const int sl = 128 * h + k;
+          const bool keep = s < nsurv && cull_keep<IS2D>(s_r[buf][0][sl], s_r[buf][1][sl], s_r[buf][2][sl], x0,
+                                                         x0 + 3.f, y0, y0 + 3.f);
+          const unsigned long long m = __ballot(keep) & boxbits;
+          if (keep) s_box[wv][box][nb + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned char)k;
+          nb += __popcll(m);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      // steps walked by the wave: max over its boxes (lanes 4k..4k+3 hold the four counts)
+      const int nmax = __builtin_amdgcn_readfirstlane(quad_max_i(nb));
+      // the sequential walk of the box's survivors (entry index read one step ahead)
+      int k_next = s_box[wv][box][0];
+      for (int t = 0; t < nmax; ++t) {
+        const int k = k_next;
+        k_next = s_box[wv][box][t + 1 < nb ? t + 1 : 0];
+        if (t < nb && !done) {
+          const int sl = 128 * h + k;
+          const float4 p0 = s_r[buf][0][sl];
+          const float4 p1 = s_r[buf][1][sl];
+          const float4 p2 = s_r[buf][2][sl];
+          const float dx = p0.x - px, dy = p0.y - py;
+          const float sg = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
+          const float raw = p0.z * __expf(-sg);
+          const float alpha = IS2D ? raw : fminf(kAlphaMax, raw);
+          const bool valid = IS2D ? alpha >= cut2d : (sg >= 0.f && alpha >= kAlphaThreshold);
+          if (valid) {
+            const float nT = T * (1.f - alpha);
+            if (!IS2D && nT <= kTMin) {
+              done = true;   // gsplat: this entry and every later one are not composited
+            } else {
+              const float vis = alpha * T;
+              dr += p2.x * vis;
+              dg += p2.y * vis;
+              db += p2.z * vis;
+              if (IS2D) Tl = T;
+              T = nT;
+              last = hb + k;
+              if (IS2D && nT <= kT2DMin) done = true;   // the reference's A == 1.0f, after this entry
+            }
+          }
+        }
+        if ((t & 7) == 7 && __ballot(!done) == 0ull) break;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  cr += dr;
+  cg += dg;
+  cb += db;
+  if (end > start) {
+    // chunk records {T at chunk start, chunk colour} -> what the backward needs at each chunk's
+    // END: {T_end, suffix colour sum of the later chunks}, back to front (records re-read 8 at a time)
+    float4* ck = ckpt + (int64_t)cbase * kRasterThreads + threadIdx.x;
+    ck[(int64_t)kcur * kRasterThreads] = make_float4(T, 0.f, 0.f, 0.f);
+    float sr = dr, sg = dg, sb = db;
+    float Tn = Ts;
+    for (int k0 = kcur - 1; k0 >= 0; k0 -= 8) {
+      float4 r[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k0 - u >= 0) r[u] = ck[(int64_t)(k0 - u) * kRasterThreads];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k0 - u >= 0) {
+          ck[(int64_t)(k0 - u) * kRasterThreads] = make_float4(Tn, sr, sg, sb);
+          Tn = r[u].x;
+          sr += r[u].y;
+          sg += r[u].z;
+          sb += r[u].w;
+        }
+    }
+  }
+  if (inside) {
+    const int64_t pix = ((int64_t)c * H + i) * W + j;
+    const float* bgc = bg + c * 3;
+    out_rgb[pix * 3 + 0] = cr + T * bgc[0];
+    out_rgb[pix * 3 + 1] = cg + T * bgc[1];
+    out_rgb[pix * 3 + 2] = cb + T * bgc[2];
+    out_alpha[pix] = 1.f - T;
+    if (IS2D)
+      reinterpret_cast<float2*>(out_T)[pix] = make_float2(T, Tl);
+    else
+      out_T[pix] = T;
+    out_last[pix] = last;
+  }
+  if (last >= 0) atomicMax(&s_max, last);
+  __syncthreads();
+  if (threadIdx.x == 0 && s_max >= 0) tile_end[ct] = s_max;   // one workgroup per tile; finalised by k_raster_finalize
+}
+
 // Per busy tile: tile_end = 1 + max last over the tile's four quadrant workgroups (or the
 // tile's start), the cut key, and the tile's active chunks appended to the backward's list.
 // (A separate launch: finishing it inside the forward by the last-arriving quadrant
@@ -982,8 +1189,8 @@ int gsr_selftest_reduce64(float* out, void* stream) {
 // Self-test of the per-box reduction (the raster backward's): out[4*l + i] = sum over the 16
 // lanes l' with l' % 4 == l % 4 of v_l'[4*(l/4) + i], same pattern; out holds 256 floats.
 int gsr_set_fwd_lanes(int lanes) {
-  GSR_REQUIRE(lanes == 0 || lanes == 4 || lanes == 16, "gsr_set_fwd_lanes: lanes must be 0 (auto), 4 or 16, got %d",
-              lanes);
+  GSR_REQUIRE(lanes == 0 || lanes == 1 || lanes == 4 || lanes == 16,
+              "gsr_set_fwd_lanes: lanes must be 0 (auto), 1, 4 or 16, got %d", lanes);
   gsr::g_fwd_lanes = lanes;
   return GSR_OK;
 }
@@ -998,12 +1205,18 @@ int gsr_selftest_reduce_box16(float* out, void* stream) {
 
 namespace gsr {
 
-// Lanes per pixel of the 3D forward: 16 when the quad layout's 4 workgroups per busy tile
-// would fill under half of the chip's ~1 280 workgroup slots (n_busy <= kFwd16MaxBusy);
-// gsr_set_fwd_lanes forces one (tests run both layouts on the same scenes).
+// Layout of the raster forward.  3D: 16 lanes per pixel and 16 workgroups per tile with at
+// most kFwd16MaxBusy busy tiles (the quad layout would fill under half of the chip's ~1 280
+// workgroup slots, so latency rules), else 4 lanes per pixel, 4 workgroups per tile (the heavy
+// tiles' serial walks are a quarter as long as with one lane per pixel: config 3 raster fwd
+// 112 us against 287 us for the box layout).  2D (every tile busy, no early termination, so
+// throughput rules): the box layout, one lane per pixel (config 4 raster fwd 12.5 ms against
+// 15.2 ms with quads).  gsr_set_fwd_lanes forces one (tests run every layout on the same
+// scenes).
 constexpr int kFwd16MaxBusy = 160;
-static int fwd_lanes(int n_busy) {
-  if (g_fwd_lanes == 4 || g_fwd_lanes == 16) return g_fwd_lanes;
+static int fwd_lanes(bool is2d, int n_busy) {
+  if (g_fwd_lanes == 1 || g_fwd_lanes == 4 || (g_fwd_lanes == 16 && !is2d)) return g_fwd_lanes;
+  if (is2d) return 1;
   return n_busy <= kFwd16MaxBusy ? 16 : 4;
 }
 
@@ -1029,16 +1242,22 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
   // 3D with few busy tiles (a single small view, a multi-GPU rank's share): 16 lanes per pixel,
   // 16 workgroups per tile -- a quarter of the serial walk per wave, for a chip the quad layout
   // would leave mostly idle
-  if (!IS2D && fwd_lanes(n_busy) == 16) {
+  const int lanes = fwd_lanes(IS2D, n_busy);
+  if (!IS2D && lanes == 16) {
     hipLaunchKernelGGL((k_raster_fwd<false, 16>), dim3((unsigned)(busy_grid<16>(n_busy) + n_fill)),
                        dim3(kRasterThreads), kFwdLdsPad, s, (const Splat*)rec, sorted_ids, tile_offset, tile_order,
                        width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state,
                        chunk_base, (int)n_busy, CT, tile_cut, cut2d);
-  } else {
+  } else if (lanes == 4) {
     hipLaunchKernelGGL((k_raster_fwd<IS2D, 4>), dim3((unsigned)(busy_grid<4>(n_busy) + n_fill)),
                        dim3(kRasterThreads), IS2D ? kFwdLdsPad2D : kFwdLdsPad, s, (const Splat*)rec, sorted_ids,
                        tile_offset, tile_order, width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end,
                        (float4*)chunk_state, chunk_base, (int)n_busy, CT, tile_cut, cut2d);
+  } else {
+    hipLaunchKernelGGL((k_raster_fwd_box<IS2D>), dim3((unsigned)(((n_busy + 7) & ~7) + n_fill)),
+                       dim3(kRasterThreads), 0, s, (const Splat*)rec, sorted_ids, tile_offset, tile_order, width,
+                       height, tw, th, bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state, chunk_base,
+                       (int)n_busy, CT, tile_cut, cut2d);
   }
   GSR_LAUNCH_CHECK(who);
   if (n_busy > 0) {

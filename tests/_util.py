@@ -81,11 +81,11 @@ def grad_close(actual, expected, rtol=1e-4, rel_floor=1e-5, max_frac=0.0, outlie
 
 
 class forced_fwd_lanes:
-    """Force the 3D raster forward's layout (gsr_set_fwd_lanes) inside a with-block.  The
-    automatic choice (16 lanes per pixel when at most 160 tiles are busy) depends on the call's
-    busy tile count, and the two layouts group the transmittance products differently (fp32
-    rounding), so bitwise comparisons between calls of different sizes (a batch view vs a
-    single-view render, a band vs the full image) fix one layout."""
+    """Force the raster forward's layout (gsr_set_fwd_lanes) inside a with-block.  The automatic
+    choice (3D: 16 lanes per pixel when at most 160 tiles are busy, else 4)
+    depends on the call's busy tile count, and the layouts group the transmittance products
+    differently (fp32 rounding), so bitwise comparisons between calls of different sizes (a
+    batch view vs a single-view render, a band vs the full image) fix one layout."""
 
     def __init__(self, lanes: int):
         self.lanes = lanes

@@ -59,10 +59,11 @@ def test_selftest_lds_order(cuda):
     assert int(out.item()) == 0
 
 
-@pytest.fixture(params=[4, 16], ids=["lanes4", "lanes16"])
+@pytest.fixture(params=[1, 4, 16], ids=["box", "lanes4", "lanes16"])
 def fwd_lanes(request, cuda):
-    """Run a test under each 3D forward layout (4 lanes per pixel / 4 workgroups per tile, and
-    16 / 16), forced through gsr_set_fwd_lanes; automatic selection afterwards."""
+    """Run a test under each forward layout (1 lane per pixel / one workgroup per tile, 4 / 4,
+    16 / 16 -- 3D only; 2D runs the box layout for 16), forced through gsr_set_fwd_lanes;
+    automatic selection afterwards."""
     from gsr import _lib
     _lib.check(_lib.lib().gsr_set_fwd_lanes(request.param), "gsr_set_fwd_lanes")
     yield request.param
@@ -379,7 +380,7 @@ def _oracle2d(p, W, H, bg, vr, va):
 
 
 @pytest.mark.parametrize("N,W,H,seed,mu", [(3000, 128, 96, 51, 0.4), (1500, 64, 64, 52, 1.8)])
-def test_2d_vs_oracle_dense(cuda, N, W, H, seed, mu):
+def test_2d_vs_oracle_dense(cuda, fwd_lanes, N, W, H, seed, mu):
     from gsr.scenes import gaussians2d
     p = gaussians2d(N, W, H, seed)
     p[:, 2:4] += mu - 0.4
@@ -393,7 +394,7 @@ def test_2d_vs_oracle_dense(cuda, N, W, H, seed, mu):
     grad_close(grad, g_o, what="grad")
 
 
-def test_2d_saturation_and_long_lists(cuda):
+def test_2d_saturation_and_long_lists(cuda, fwd_lanes):
     """Opaque stacks drive A to exactly 1.0f (exact early stop + division-free backward);
     > 2048-entry lists exercise several checkpoint chunks, > 16384 the merge sort."""
     W, H = 32, 32
