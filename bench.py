@@ -398,7 +398,7 @@ class Workload:
             self.views_here = len(self.units)
             self.scaling = "strong"
             self.layout = (f"(frame, view) units round-robin over {world} rank(s), batched per frame bucket "
-                           f"({self.buckets}), async RCCL all-reduce of the [8,N,9] gradient per bucket"
+                           f"({self.buckets}), async all-reduce of the [8,N,9] gradient per bucket"
                            if world > 1 else f"{F} frames x {C} views batched in one launch sequence")
         else:
             self.params_cpu = gaussians3d(cfg.N, cfg.seed)
@@ -444,7 +444,7 @@ class Workload:
         self.v0, self.v1, self.band = unit_shard(cfg.views, self.th, self.world, self.rank, weights)
         self.views_here = self.v1 - self.v0
         self.layout = (f"(view, tile-row) units: rank {self.rank} views {self.v0}-{self.v1 - 1} rows {self.band} "
-                       f"of {cfg.views}x{self.th}, {self.buckets} RCCL all-reduce bucket(s) overlapping project_bwd")
+                       f"of {cfg.views}x{self.th}, {self.buckets} all-reduce bucket(s) overlapping project_bwd")
 
     def step(self):
         cfg, R = self.cfg, self.R
@@ -701,7 +701,8 @@ def main(argv=None):
         "config": {"workload": cfg.name, "N_gauss": cfg.N, "width": cfg.width, "height": cfg.height,
                    "views": cfg.views, "frames": FRAMES_2D if cfg.mode == "2d" else 1,
                    "units_per_step": w.units_total, "background": "white", "loss": args.loss,
-                   "parallelism": w.layout + (f"; backend {backend}" if backend else "")},
+                   "parallelism": w.layout + (f"; backend {backend}" + (" (RCCL)" if backend == "nccl" else "")
+                                              if backend else "")},
         "roofline": roof,
         "kernels_ms": {k: round(v[0], 4) for k, v in sorted(breakdown.items())},
         "allreduce_ms": ar_ms,
