@@ -354,14 +354,19 @@ int gsr_pose3d_bwd(const float* params, int64_t N, int64_t row_stride, double an
  * mean): x = the target [C,3,H,W] and y = the render, each given as (data, strides[4] in
  * elements for (view, channel, row, column)) so planar and channels-last images are read in
  * place.  taps11: HOST array, the normalised 1-D Gaussian (11 taps, sigma 1.5) the caller
- * computes as torchmetrics does.  Needs H, W > 10.  fwd writes the scalar *ssim (device);
- * bwd writes d(g_out * ssim)/dy into grad_y (device, y's strides), g_out a device scalar.
- * Both are deterministic (fixed-order sums). */
+ * computes as torchmetrics does.  Needs H, W > 10.  fwd writes the scalar *ssim (device) and,
+ * when factors != NULL (device, gsr_ssim_factors_size floats), each window's backward factors
+ * (dS/dmu_y, dS/dE[y^2], dS/dE[xy]); bwd blurs those onto the pixels and writes
+ * d(g_out * ssim)/dy into grad_y (device, y's strides), g_out a device scalar.  Both are
+ * deterministic (fixed-order sums). */
 size_t gsr_ssim_workspace(int C, int width, int height);
+size_t gsr_ssim_factors_size(int C, int width, int height);
 int gsr_ssim_fwd(const float* x, const int64_t* x_strides, const float* y, const int64_t* y_strides, int C, int width,
-                 int height, const float* taps11, void* ws, size_t ws_bytes, float* ssim, void* stream);
+                 int height, const float* taps11, void* ws, size_t ws_bytes, float* ssim, float* factors,
+                 void* stream);
 int gsr_ssim_bwd(const float* x, const int64_t* x_strides, const float* y, const int64_t* y_strides, int C, int width,
-                 int height, const float* taps11, const float* g_out, float* grad_y, void* stream);
+                 int height, const float* taps11, const float* factors, const float* g_out, float* grad_y,
+                 void* stream);
 
 /* ---- Shape carving -----------------------------------------------
  * ShapeCarver.forward (src/shape_carver.py:322-366): the [4, n_voxels] volume (mask

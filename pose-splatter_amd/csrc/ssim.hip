@@ -14,8 +14,8 @@
 // Backward, for the rendered image y: per window q, a = dS/dmy, b = dS/dE[y^2], c = dS/dE[xy]
 //   a = 2 mx (A2 - A1) / (B1 B2) - 2 my S (1/B1 - 1/B2),  b = -S / B2,  c = 2 A1 / (B1 B2),
 // and dL/dy_p = g / count * sum_q G(q - p) (a_q + 2 y_p b_q + x_p c_q): the same blur applied
-// to the a, b, c maps (zero outside the kept windows).  One workgroup per 16x16 tile of
-// pixels recomputes the window statistics of its 26x26 windows from a 36x36 input tile.
+// to the a, b, c maps (zero outside the kept windows).  The forward stores a, b, c per window
+// (12 B) when a backward will follow; the backward blurs them onto 16x16 pixel tiles.
 //
 // Reductions are fixed-order (per-workgroup partials, then one workgroup sums them in index
 // order), so the value is bitwise reproducible.
@@ -122,9 +122,22 @@ __device__ __forceinline__ float block_sum(float v, float* s_red) {
   return t;
 }
 
-// forward: one workgroup per (16x16 tile of window centres, channel, view); partial[block]
+// dS/dmy, dS/dE[y^2], dS/dE[xy] of one window (the backward's per-window factors)
+__device__ __forceinline__ float3 ssim_dy(const WinStats& w, float& S) {
+  const float mxy = w.mx * w.my, mxx = w.mx * w.mx, myy = w.my * w.my;
+  const float A1 = 2.f * mxy + kSsimC1, A2 = 2.f * (w.exy - mxy) + kSsimC2;
+  const float B1 = mxx + myy + kSsimC1, B2 = (w.exx - mxx) + (w.eyy - myy) + kSsimC2;
+  const float den = 1.f / (B1 * B2);
+  S = (A1 * A2) / (B1 * B2);
+  return make_float3(2.f * w.mx * (A2 - A1) * den - 2.f * w.my * S * (1.f / B1 - 1.f / B2), -S / B2,
+                     2.f * A1 * den);
+}
+
+// forward: one workgroup per (16x16 tile of window centres, channel, view); partial[block],
+// and (abc != null) the window's backward factors at abc[((view*3 + ch)*3 + k) * Hw*Ww + window]
 __global__ __launch_bounds__(kSsimThreads) void k_ssim_fwd(const Img X, const Img Y, int H, int W,
-                                                          const SsimTaps tp, float* __restrict__ partial) {
+                                                          const SsimTaps tp, float* __restrict__ partial,
+                                                          float* __restrict__ abc) {
   constexpr int R = kSsimT, P = R + 2 * kSsimR;
   __shared__ float s_x[P][P], s_y[P][P];
   __shared__ float s_h[5][P][R];
@@ -137,7 +150,20 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_fwd(const Img X, const Im
   __syncthreads();
   const int wi = threadIdx.x / R, wj = threadIdx.x % R;
   const bool kept = i0 + wi < H - kSsimR && j0 + wj < W - kSsimR;
-  const float s = kept ? ssim_of(vblur5<R>(tp, s_h, wi, wj)) : 0.f;
+  float s = 0.f;
+  if (kept) {
+    const WinStats w = vblur5<R>(tp, s_h, wi, wj);
+    if (abc) {
+      const float3 d = ssim_dy(w, s);
+      const int64_t Hw = H - 2 * kSsimR, Ww = W - 2 * kSsimR;
+      float* o = abc + (int64_t)blockIdx.z * 3 * Hw * Ww + (int64_t)(i0 - kSsimR + wi) * Ww + (j0 - kSsimR + wj);
+      o[0] = d.x;
+      o[Hw * Ww] = d.y;
+      o[2 * Hw * Ww] = d.z;
+    } else {
+      s = ssim_of(w);
+    }
+  }
   const float t = block_sum(s, s_red);
   if (threadIdx.x == 0)
     partial[((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] = t;
@@ -153,47 +179,33 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_finalize(const float* __r
   if (threadIdx.x == 0) *ssim = (float)((double)t * inv_count);
 }
 
-// backward: one workgroup per (16x16 tile of pixels, channel, view); grad of (g_out * ssim)
-// w.r.t. y, written through the Y layout's strides into gy
+// backward: one workgroup per (16x16 tile of pixels, channel, view): the per-window factors
+// a, b, c the forward stored (zero outside the kept windows) blurred back onto the pixels
+// (the taps are symmetric, so the transpose blur is the blur), grad = g/count (A + 2 y B + x C),
+// written through the Y layout's strides into gy
 __global__ __launch_bounds__(kSsimThreads) void k_ssim_bwd(const Img X, const Img Y, int H, int W, const SsimTaps tp,
-                                                          const float* __restrict__ g_out, float inv_count,
-                                                          float* __restrict__ gy) {
+                                                          const float* __restrict__ abc, const float* __restrict__ g_out,
+                                                          float inv_count, float* __restrict__ gy) {
   constexpr int T = kSsimT;                 // output pixels per side
   constexpr int R = T + 2 * kSsimR;         // windows per side (26)
-  constexpr int P = R + 2 * kSsimR;         // input patch side (36)
-  __shared__ float s_x[P][P], s_y[P][P];
-  __shared__ float s_h[5][P][R];
   __shared__ float s_abc[3][R][R];
   __shared__ float s_h2[3][R][T];
   const int c = blockIdx.z / 3, ch = blockIdx.z - 3 * c;
   const int pi0 = blockIdx.y * T, pj0 = blockIdx.x * T;   // first output pixel
-  const int i0 = pi0 - kSsimR, j0 = pj0 - kSsimR;         // first window centre
-  load_patch<R>(X, Y, c, ch, H, W, i0, j0, s_x, s_y);
-  __syncthreads();
-  hblur5<R>(tp, s_x, s_y, s_h);
-  __syncthreads();
+  const int Hw = H - 2 * kSsimR, Ww = W - 2 * kSsimR;
+  const float* m = abc + (int64_t)blockIdx.z * 3 * Hw * Ww;
+  // window (wi, wj) of the tile is centred at pixel (pi0 - 5 + wi, pj0 - 5 + wj), i.e. window
+  // index (pi0 - 10 + wi, pj0 - 10 + wj) of the map
   for (int t = threadIdx.x; t < R * R; t += kSsimThreads) {
     const int wi = t / R, wj = t - wi * R;
-    const int ci = i0 + wi, cj = j0 + wj;
-    const bool kept = ci >= kSsimR && ci < H - kSsimR && cj >= kSsimR && cj < W - kSsimR;
-    float a = 0.f, b = 0.f, cc = 0.f;
-    if (kept) {
-      const WinStats w = vblur5<R>(tp, s_h, wi, wj);
-      const float mxy = w.mx * w.my, mxx = w.mx * w.mx, myy = w.my * w.my;
-      const float A1 = 2.f * mxy + kSsimC1, A2 = 2.f * (w.exy - mxy) + kSsimC2;
-      const float B1 = mxx + myy + kSsimC1, B2 = (w.exx - mxx) + (w.eyy - myy) + kSsimC2;
-      const float den = 1.f / (B1 * B2);
-      const float S = A1 * A2 * den;
-      a = 2.f * w.mx * (A2 - A1) * den - 2.f * w.my * S * (1.f / B1 - 1.f / B2);
-      b = -S / B2;
-      cc = 2.f * A1 * den;
-    }
-    s_abc[0][wi][wj] = a;
-    s_abc[1][wi][wj] = b;
-    s_abc[2][wi][wj] = cc;
+    const int mi = pi0 - 2 * kSsimR + wi, mj = pj0 - 2 * kSsimR + wj;
+    const bool in = mi >= 0 && mi < Hw && mj >= 0 && mj < Ww;
+    const int64_t o = (int64_t)mi * Ww + mj;
+    s_abc[0][wi][wj] = in ? m[o] : 0.f;
+    s_abc[1][wi][wj] = in ? m[(int64_t)Hw * Ww + o] : 0.f;
+    s_abc[2][wi][wj] = in ? m[2 * (int64_t)Hw * Ww + o] : 0.f;
   }
   __syncthreads();
-  // transpose blur (the taps are symmetric): horizontal over the window map, then vertical
   for (int t = threadIdx.x; t < R * T; t += kSsimThreads) {
     const int r = t / T, q = t - r * T;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
@@ -220,7 +232,7 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_bwd(const Img X, const Im
       B += g * s_h2[1][pi + k][pj];
       Cc += g * s_h2[2][pi + k][pj];
     }
-    const float x = s_x[pi + 2 * kSsimR][pj + 2 * kSsimR], y = s_y[pi + 2 * kSsimR][pj + 2 * kSsimR];
+    const float x = X.at(c, ch, i, j), y = Y.at(c, ch, i, j);
     const float gs = g_out[0] * inv_count;
     gy[c * Y.sc + ch * Y.sch + (int64_t)i * Y.sr + (int64_t)j * Y.sp] = gs * (A + 2.f * y * B + x * Cc);
   }
@@ -244,8 +256,14 @@ size_t gsr_ssim_workspace(int C, int width, int height) {
   return (size_t)nb * sizeof(float) + 16;
 }
 
+size_t gsr_ssim_factors_size(int C, int width, int height) {
+  if (C < 1 || width <= 2 * kSsimR || height <= 2 * kSsimR) return 0;
+  return (size_t)C * 9 * (size_t)(width - 2 * kSsimR) * (size_t)(height - 2 * kSsimR);
+}
+
 int gsr_ssim_fwd(const float* x, const int64_t* x_strides, const float* y, const int64_t* y_strides, int C, int width,
-                 int height, const float* taps11, void* ws, size_t ws_bytes, float* ssim, void* stream) {
+                 int height, const float* taps11, void* ws, size_t ws_bytes, float* ssim, float* factors,
+                 void* stream) {
   GSR_REQUIRE(C >= 1 && width > 2 * kSsimR && height > 2 * kSsimR,
               "gsr_ssim_fwd: need C >= 1 and an image larger than %dx%d, got C=%d %dx%d", 2 * kSsimR + 1,
               2 * kSsimR + 1, C, width, height);
@@ -255,7 +273,8 @@ int gsr_ssim_fwd(const float* x, const int64_t* x_strides, const float* y, const
   const Img Y{y, y_strides[0], y_strides[1], y_strides[2], y_strides[3]};
   const dim3 grid(ceil_div(width - 2 * kSsimR, kSsimT), ceil_div(height - 2 * kSsimR, kSsimT), 3 * C);
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_ssim_fwd, grid, dim3(kSsimThreads), 0, s, X, Y, height, width, taps(taps11), (float*)ws);
+  hipLaunchKernelGGL(k_ssim_fwd, grid, dim3(kSsimThreads), 0, s, X, Y, height, width, taps(taps11), (float*)ws,
+                     factors);
   GSR_LAUNCH_CHECK("k_ssim_fwd");
   const int64_t nb = (int64_t)grid.x * grid.y * grid.z;
   const double count = 3.0 * C * (double)(width - 2 * kSsimR) * (double)(height - 2 * kSsimR);
@@ -265,16 +284,17 @@ int gsr_ssim_fwd(const float* x, const int64_t* x_strides, const float* y, const
 }
 
 int gsr_ssim_bwd(const float* x, const int64_t* x_strides, const float* y, const int64_t* y_strides, int C, int width,
-                 int height, const float* taps11, const float* g_out, float* grad_y, void* stream) {
+                 int height, const float* taps11, const float* factors, const float* g_out, float* grad_y,
+                 void* stream) {
   GSR_REQUIRE(C >= 1 && width > 2 * kSsimR && height > 2 * kSsimR, "gsr_ssim_bwd: bad C=%d or image %dx%d", C, width,
               height);
-  GSR_REQUIRE(x && y && x_strides && y_strides && taps11 && g_out && grad_y, "gsr_ssim_bwd: null pointer");
+  GSR_REQUIRE(x && y && x_strides && y_strides && taps11 && factors && g_out && grad_y, "gsr_ssim_bwd: null pointer");
   const Img X{x, x_strides[0], x_strides[1], x_strides[2], x_strides[3]};
   const Img Y{y, y_strides[0], y_strides[1], y_strides[2], y_strides[3]};
   const dim3 grid(ceil_div(width, kSsimT), ceil_div(height, kSsimT), 3 * C);
   const double count = 3.0 * C * (double)(width - 2 * kSsimR) * (double)(height - 2 * kSsimR);
   hipLaunchKernelGGL(k_ssim_bwd, grid, dim3(kSsimThreads), 0, (hipStream_t)stream, X, Y, height, width, taps(taps11),
-                     g_out, (float)(1.0 / count), grad_y);
+                     factors, g_out, (float)(1.0 / count), grad_y);
   GSR_LAUNCH_CHECK("k_ssim_bwd");
   return GSR_OK;
 }

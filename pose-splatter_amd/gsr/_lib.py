@@ -95,8 +95,9 @@ EXPORTS = {
     "gsr_pose3d_fwd": (ctypes.c_int, [_P, _I64, _I64, _D, _P, _P, _P]),
     "gsr_pose3d_bwd": (ctypes.c_int, [_P, _I64, _I64, _D, _P, _P, _P]),
     "gsr_ssim_workspace": (_SZ, [_I32, _I32, _I32]),
-    "gsr_ssim_fwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _SZ, _P, _P]),
-    "gsr_ssim_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P]),
+    "gsr_ssim_factors_size": (_SZ, [_I32, _I32, _I32]),
+    "gsr_ssim_fwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _SZ, _P, _P, _P]),
+    "gsr_ssim_bwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "gsr_carve_workspace": (_SZ, [_I64, _I32, _I32]),
     "gsr_carve_volume": (ctypes.c_int, [_P, _I64, _P, _D, _P, _P, _P, _I32, _P, _P, _I32, _I32, _F, _F, _P, _SZ,
                                         _P, _P]),

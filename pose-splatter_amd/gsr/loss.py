@@ -65,16 +65,19 @@ class _Ssim(torch.autograd.Function):
         ys = torch.tensor(_strides4(y, True), dtype=torch.int64)
         ws = torch.empty(int(L.gsr_ssim_workspace(C, W, H)), device=dev, dtype=torch.uint8)
         out = torch.empty((), device=dev, dtype=torch.float32)
+        # the backward's per-window factors, stored by the forward only when a backward can follow
+        need = bool(ctx.needs_input_grad[1])
+        fac = torch.empty(int(L.gsr_ssim_factors_size(C, W, H)) if need else 0, device=dev, dtype=torch.float32)
         with _timed("ssim_fwd"):
             check(L.gsr_ssim_fwd(_ptr(x), xs.data_ptr(), _ptr(y), ys.data_ptr(), C, W, H, _TAPS.data_ptr(), _ptr(ws),
-                                 ws.numel(), _ptr(out), _stream(dev)), "gsr_ssim_fwd")
-        ctx.save_for_backward(x, y)
+                                 ws.numel(), _ptr(out), _ptr(fac) if need else None, _stream(dev)), "gsr_ssim_fwd")
+        ctx.save_for_backward(x, y, fac)
         ctx.strides = (xs, ys)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        x, y = ctx.saved_tensors
+        x, y, fac = ctx.saved_tensors
         xs, ys = ctx.strides
         L = lib()
         dev = y.device
@@ -82,8 +85,8 @@ class _Ssim(torch.autograd.Function):
         gy = torch.empty_strided(y.shape, y.stride(), device=dev, dtype=torch.float32)
         g = g.detach().float().reshape(()).contiguous()
         with _timed("ssim_bwd"):
-            check(L.gsr_ssim_bwd(_ptr(x), xs.data_ptr(), _ptr(y), ys.data_ptr(), C, W, H, _TAPS.data_ptr(), _ptr(g),
-                                 _ptr(gy), _stream(dev)), "gsr_ssim_bwd")
+            check(L.gsr_ssim_bwd(_ptr(x), xs.data_ptr(), _ptr(y), ys.data_ptr(), C, W, H, _TAPS.data_ptr(), _ptr(fac),
+                                 _ptr(g), _ptr(gy), _stream(dev)), "gsr_ssim_bwd")
         return None, gy
 
 
