@@ -1050,11 +1050,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
     }
   }
   // groups walked by the wave: max over its boxes (lanes 4k..4k+3 hold the four counts)
-#ifdef GSR_EXP_NOLOOP
-  const int ngrp = 0;
-#else
   const int ngrp = __builtin_amdgcn_readfirstlane(quad_max_i(nb));
-#endif
   const int npad = (ngrp + kGroup - 1) / kGroup * kGroup;
   for (int s = nb + pos; s < npad; s += 16) s_box[wv][box][s] = (unsigned char)kNull;
   __builtin_amdgcn_wave_barrier();
@@ -1122,11 +1118,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
       if (!IS2D) Sv += fac * cv;
     }
     float sum[4];
-#ifdef GSR_EXP_NORED
-    sum[0] = acc[lane & 63]; sum[1] = acc[(lane + 1) & 63]; sum[2] = acc[(lane + 2) & 63]; sum[3] = acc[(lane + 3) & 63];
-#else
     reduce_box16(acc, sum);
-#endif
     reinterpret_cast<float4*>(&s_stage[wv][0][0])[lane] = make_float4(sum[0], sum[1], sum[2], sum[3]);
     __builtin_amdgcn_wave_barrier();
     if (fown) {

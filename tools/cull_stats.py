@@ -106,6 +106,23 @@ def main():
     s48 = res[(4, 8)]   # boxes: nbx=4, nby=2 -> idx = by*4+bx
     rows_layout((4, 8), [[0, 1, 2, 3], [4, 5, 6, 7]], 7, "E 4x8 per 16-lane row (2 px/lane), 7-groups")
     rows_layout((8, 4), [[0, 1, 2, 3], [4, 5, 6, 7]], 7, "E' 8x4 per 16-lane row (2 px/lane), 7-groups")
+    # F: 4x4 boxes, eight per wave (16x8 half tile, 8 lanes x 2 px per box); cost per group
+    # ~716 VALU (14 pairs per lane) vs ~422 for B's 7 pairs
+    halves = [[(2 * hy + dy) * 4 + bx for dy in (0, 1) for bx in range(4)] for hy in (0, 1)]
+    gb = rows_layout((4, 4), quads, 7, "B again")
+    gf = rows_layout((4, 4), halves, 7, "F 4x4, 8 boxes per wave (2 px/lane), 7-groups")
+    print(f"VALU model: B {float(gb) * 422:.3e}  F {float(gf) * 716:.3e}  ratio {float(gf * 716 / (gb * 422)):.3f}")
+    gf5 = rows_layout((4, 4), halves, 5, "F 5-groups")
+    # G: 4x4 boxes assigned to the four waves by survivor count (sorted, 4 consecutive per wave)
+    s44 = res[(4, 4)]
+    srt = torch.sort(s44, 1, descending=True).values
+    for G_ in (5, 6, 7, 8):
+        tot = sum(torch.ceil(srt[:, 4 * w] / G_).sum() for w in range(4))
+        print(f"G balanced 4x4, {G_}-groups: wave-groups {int(tot)} ({float(tot / g_base):.3f} x A), "
+              f"lane-pair slots {int(tot) * G_ * 64}  (B: {int(gb) * 7 * 64})")
+    for G_ in (5, 6, 8):
+        rows_layout((4, 4), quads, G_, f"B {G_}-groups")
+    print(f"VALU model F5 (~520/group): ratio {float(gf5 * 520 / (gb * 422)):.3f}")
 
 
 if __name__ == "__main__":
