@@ -196,6 +196,28 @@ int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_
                  const gsr_bin_stats* stats, void* workspace,
                  size_t workspace_bytes, int32_t* sorted_ids, int32_t* k_of_s, void* stream);
 
+/* Lazy depth order (3D).  The forward of a tile reads its depth-sorted list only until every
+ * pixel of the tile has stopped (T < 1e-4) -- at config 5 at most ~3.6k of the 16k-30k entries
+ * of its longest lists.  gsr_bin_sort_lazy sorts every list longer than min_len only up to
+ * a depth prefix of at least `prefix` entries (whole MSD digit buckets; the rest stays
+ * unsorted), and gsr3d_raster_fwd_lazy walks each tile to the end of its sorted prefix; a
+ * tile whose walk gets there (a live pixel, or a pixel whose last entry is the prefix's last)
+ * is sorted whole and rendered again from scratch inside the same call.  Every entry any
+ * kernel reads therefore comes in exact gsplat order: the outputs equal those of
+ * gsr_bin_sort + gsr3d_raster_fwd bit for bit; sorted_ids / k_of_s past a tile's tile_end
+ * are unspecified.  lazy: caller-owned int32 workspace of gsr_lazy_workspace(CT) bytes.
+ * gsr_set_lazy_sort (process-wide; default min_len 16384, prefix 4096; min_len <= 0
+ * disables); gsr_lazy_min_len returns the current min_len. */
+size_t gsr_lazy_workspace(int64_t CT);
+int gsr_set_lazy_sort(int min_len, int prefix);
+int gsr_lazy_min_len(void);
+int gsr_bin_sort_lazy(const float* depth, const uint32_t* rect, const int32_t* isect_offset,
+                      const int32_t* tile_offset, int32_t* tile_count, const int32_t* busy_tiles, int C,
+                      int64_t N, int width, int height, int64_t n_isect, int32_t max_seg, int32_t n_busy,
+                      int32_t n_sort_big, int32_t n_sort_mid, int emitted, const gsr_bin_stats* stats,
+                      void* workspace, size_t workspace_bytes, int32_t* sorted_ids, int32_t* k_of_s,
+                      int32_t* lazy, void* stream);
+
 /* ---------------------------------------------------------------- (c) rasterisation */
 
 /* Front-to-back compositing (gsplat classic).  One workgroup per non-empty 16x16 tile,
@@ -217,6 +239,17 @@ int gsr3d_raster_fwd(const float* rec, const float* depth, const int32_t* sorted
                      int height, const float* bg, int32_t n_busy, gsr_bin_stats* stats,
                      float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
                      uint64_t* tile_cut, float* chunk_state, int32_t* chunk_list, void* stream);
+
+/* gsr3d_raster_fwd over the lists of gsr_bin_sort_lazy (same outputs, see above): the tiles
+ * that read past their sorted prefix are sorted whole (sort_workspace / k_of_s / max_seg of
+ * that gsr_bin_sort_lazy call) and rendered again.  n_lazy_max: an upper bound on the tiles
+ * sorted lazily (n_sort_big when min_len >= 8191, else n_busy). */
+int gsr3d_raster_fwd_lazy(const float* rec, const float* depth, int32_t* sorted_ids, const int32_t* tile_offset,
+                          const int32_t* tile_order, const int32_t* chunk_base, int C, int width, int height,
+                          const float* bg, int32_t n_busy, gsr_bin_stats* stats, float* rgb, float* alpha,
+                          float* final_T, int32_t* last, int32_t* tile_end, uint64_t* tile_cut, float* chunk_state,
+                          int32_t* chunk_list, int32_t* lazy, int32_t n_lazy_max, int32_t max_seg,
+                          void* sort_workspace, size_t sort_workspace_bytes, int32_t* k_of_s, void* stream);
 
 /* Backward of gsr3d_raster_fwd: workgroup b takes chunk_list[b] for b < stats->n_active
  * (n_chunks bounds the grid).  v_rgb [C,H,W,3], v_alpha [C,H,W] (contiguous).  Writes the

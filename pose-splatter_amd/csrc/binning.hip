@@ -42,6 +42,26 @@ constexpr int kSortLdsKeys = GSR_SORT_LDS_KEYS;   // 128 KB of 64-bit keys at 10
 constexpr int kSortRounds = GSR_SORT_ROUNDS;      // 64-element rounds per wave (LDS keys <= rounds x threads)
 constexpr int kSortSmallKeys = 4096;
 
+// Lazy depth order (3D, long lists): the forward reads a short depth prefix of every long list
+// before all its pixels stop (config 5: at most 3 627 of the 16k-30k entries of the lists
+// longer than 16 384; tools/tile_lengths.py), so those lists are MSD-partitioned by depth as
+// before but only the digit buckets covering the first `prefix` entries are LDS-sorted.  A tile
+// whose forward reaches the end of its sorted prefix is re-sorted whole and rendered again
+// (gsr3d_raster_fwd_lazy), so every entry any kernel reads is in exact gsplat order.
+// Workspace (int32): tile_sorted[CT] (end of the sorted prefix), flag[CT], list[CT], count.
+struct LazyArgs {
+  int32_t* tile_sorted;
+  int32_t* flag;
+  int32_t* list;
+  int32_t* count;
+  int32_t* tile_end;   // mode 2: reset to -1 for the re-rendered tiles
+  int min_len;         // lists longer than this are sorted lazily
+  int prefix;          // sorted prefix target (entries)
+  int mode;            // 0 off; 1 first sort (lazy prefixes); 2 full sort of the flagged tiles
+};
+static int g_lazy_min_len = 16384;
+static int g_lazy_prefix = 4096;
+
 // ---------------------------------------------------------------- tile scan (single block)
 // tile_offset[0..CT] (list starts), chunk_base[0..CT] (starts of each tile's GSR_CHUNK-entry chunks,
 // for the chunk-parallel backward), the visit order (non-empty tiles longest-first in log2
@@ -74,8 +94,22 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(int32_t* __restrict__
   __shared__ int s_n_busy;
   extern __shared__ int s_cnt[];   // the counts, staged with coalesced loads (CT <= kScanLdsTiles)
   const bool staged = CT <= kScanLdsTiles;
-  if (staged)
-    for (int64_t i = threadIdx.x; i < CT; i += kTopThreads) s_cnt[i] = tile_count[i];
+  if (staged) {
+    // batches of 8 loads in flight per thread (one memory latency per batch, not per load)
+    for (int64_t i0 = threadIdx.x; i0 < CT; i0 += 8 * kTopThreads) {
+      int v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t i = i0 + (int64_t)j * kTopThreads;
+        v[j] = i < CT ? tile_count[i] : 0;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t i = i0 + (int64_t)j * kTopThreads;
+        if (i < CT) s_cnt[i] = v[j];
+      }
+    }
+  }
   const int32_t* cnt = staged ? s_cnt : tile_count;
   if (threadIdx.x == 0) {
     s_max = 0;
@@ -200,9 +234,21 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__
         for (int tx = x0; tx < x1; ++tx) atomicAdd(&hist[ty * tw + tx], 1);
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < T; t += blockDim.x) {
-      const int v = hist[t];
-      if (v) hist[t] = toff[t] + atomicSub(&gcnt[t], v) - v;
+    // claim this workgroup's range of every tile it hits: batches of 8 returning atomics in
+    // flight per thread (a strided loop waited one atomic round trip per tile)
+    for (int t0 = threadIdx.x; t0 < T; t0 += 8 * kEmitThreads) {
+      int v[8], base[8], got[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int t = t0 + j * kEmitThreads;
+        v[j] = t < T ? hist[t] : 0;
+        base[j] = t < T ? toff[t] : 0;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) got[j] = v[j] ? atomicSub(&gcnt[t0 + j * kEmitThreads], v[j]) : 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (v[j]) hist[t0 + j * kEmitThreads] = base[j] + got[j] - v[j];
     }
     __syncthreads();
   }
@@ -238,6 +284,76 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__
 
 __device__ __forceinline__ uint32_t sort_word(uint64_t k) { return (uint32_t)(k >> 32); }
 __device__ __forceinline__ uint32_t low_word(uint64_t k) { return (uint32_t)(k & 0xffffffffull); }
+
+// Global <-> LDS staging loops, batched so that kBatch loads per thread are in flight at once
+// (a plain strided loop waits one memory latency per iteration: ~10 iterations per list).
+constexpr int kBatch = 8;
+
+// a[i] = (sort word of src[i]) << 32 | (pbase + i), i < n
+template <int NT>
+__device__ __forceinline__ void stage_keys(uint64_t* a, const uint64_t* __restrict__ src, int n, int pbase) {
+  for (int i0 = threadIdx.x; i0 < n; i0 += kBatch * NT) {
+    uint32_t w[kBatch];
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      const int i = i0 + j * NT;
+      w[j] = sort_word(src[i < n ? i : 0]);
+    }
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      const int i = i0 + j * NT;
+      if (i < n) a[i] = ((uint64_t)w[j] << 32) | (uint64_t)(uint32_t)(pbase + i);
+    }
+  }
+}
+
+// a[i] = src[i], i < n
+template <int NT>
+__device__ __forceinline__ void copy_keys(uint64_t* a, const uint64_t* __restrict__ src, int n) {
+  for (int i0 = threadIdx.x; i0 < n; i0 += kBatch * NT) {
+    uint64_t w[kBatch];
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      const int i = i0 + j * NT;
+      w[j] = src[i < n ? i : 0];
+    }
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      const int i = i0 + j * NT;
+      if (i < n) a[i] = w[j];
+    }
+  }
+}
+
+// sorted element s (word << 32 | p, p indexing the bucket): ids[s] = c*N+n of key seg[p],
+// kos[s] = kslot[p] (its emission index)
+template <int NT>
+__device__ __forceinline__ void write_sorted(const uint64_t* a, int n, const uint64_t* __restrict__ seg,
+                                             const int32_t* __restrict__ kslot, int32_t* __restrict__ ids,
+                                             int32_t* __restrict__ kos) {
+  for (int s0 = threadIdx.x; s0 < n; s0 += kBatch * NT) {
+    uint32_t p[kBatch];
+    int32_t id[kBatch], ko[kBatch];
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      const int s = s0 + j * NT;
+      p[j] = s < n ? low_word(a[s]) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      id[j] = (int32_t)low_word(seg[p[j]]);
+      ko[j] = kslot[p[j]];
+    }
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      const int s = s0 + j * NT;
+      if (s < n) {
+        ids[s] = id[j];
+        kos[s] = ko[j];
+      }
+    }
+  }
+}
 
 // a: n <= 16*NT elements (word << 32 | p) in LDS; seg: the bucket's original keys
 // (tie-break by their low word); s_hist: (NT/64)*256 + 64 ints.
@@ -366,23 +482,34 @@ __global__ __launch_bounds__(NT) void k_segsort(
     uint64_t* __restrict__ keys, uint64_t* __restrict__ tmpk, int32_t* __restrict__ tmpp0,
     int32_t* __restrict__ tmpp1, const int32_t* __restrict__ tile_offset, const int32_t* __restrict__ busy,
     const int32_t* __restrict__ k_of_slot, int lds_keys, int32_t* __restrict__ sorted_ids,
-    int32_t* __restrict__ k_of_s) {
+    int32_t* __restrict__ k_of_s, const LazyArgs lz) {
   extern __shared__ uint64_t s_keys[];
   int* s_hist = (int*)(s_keys + lds_keys);
-  const int ct = busy[blockIdx.x];
+  int ct;
+  if (lz.mode == 2) {   // the tiles whose forward ran past their sorted prefix
+    if ((int)blockIdx.x >= *lz.count) return;
+    ct = lz.list[blockIdx.x];
+  } else {
+    ct = busy[blockIdx.x];
+  }
   const int start = tile_offset[ct];
   const int len = tile_offset[ct + 1] - start;
   uint64_t* seg = keys + start;
-  if (len <= lds_keys) {
-    for (int i = threadIdx.x; i < len; i += blockDim.x)
-      s_keys[i] = (seg[i] & 0xffffffff00000000ull) | (uint64_t)(uint32_t)i;
+  const bool lazy = lz.mode == 1 && len > lz.min_len;
+  if (lz.mode != 0 && threadIdx.x == 0) {
+    lz.tile_sorted[ct] = start + len;   // lowered below for a lazily sorted list
+    if (lz.mode == 1) {
+      lz.flag[ct] = 0;
+      if (blockIdx.x == 0) *lz.count = 0;
+    } else {
+      lz.tile_end[ct] = -1;   // the forward renders this tile again
+    }
+  }
+  if (len <= lds_keys && !lazy) {
+    stage_keys<NT>(s_keys, seg, len, 0);
     __syncthreads();
     lds_radix_sort<NT>(s_keys, len, s_hist, seg);
-    for (int s = threadIdx.x; s < len; s += blockDim.x) {
-      const uint32_t p = low_word(s_keys[s]);
-      sorted_ids[start + s] = (int32_t)low_word(seg[p]);
-      k_of_s[start + s] = k_of_slot[start + p];
-    }
+    write_sorted<NT>(s_keys, len, seg, k_of_slot + start, sorted_ids + start, k_of_s + start);
     return;
   }
   // Long list (> lds_keys): MSD partition by the top 8 varying bits of the sort word into
@@ -402,12 +529,31 @@ __global__ __launch_bounds__(NT) void k_segsort(
     __syncthreads();
     const uint32_t w0 = sort_word(seg[0]);
     uint32_t orv = 0;
-    for (int i = threadIdx.x; i < len; i += blockDim.x) orv |= sort_word(seg[i]) ^ w0;
+    for (int i0 = threadIdx.x; i0 < len; i0 += kBatch * NT) {
+      uint32_t w[kBatch];
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {
+        const int i = i0 + j * NT;
+        w[j] = sort_word(seg[i < len ? i : 0]);
+      }
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) orv |= w[j] ^ w0;
+    }
     if (orv) atomicOr(&s_or, orv);
     __syncthreads();
     const uint32_t varying = s_or;
     const int sh = varying ? max(31 - __clz(varying) - 7, 0) : 0;
-    for (int i = threadIdx.x; i < len; i += blockDim.x) atomicAdd(&s_dcur[(sort_word(seg[i]) >> sh) & 0xFFu], 1);
+    for (int i0 = threadIdx.x; i0 < len; i0 += kBatch * NT) {
+      uint32_t w[kBatch];
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) {
+        const int i = i0 + j * NT;
+        w[j] = sort_word(seg[i < len ? i : 0]);
+      }
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j)
+        if (i0 + j * NT < len) atomicAdd(&s_dcur[(w[j] >> sh) & 0xFFu], 1);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
       int acc = 0, mb = 0;
@@ -424,10 +570,21 @@ __global__ __launch_bounds__(NT) void k_segsort(
     __syncthreads();
     if (s_maxb <= lds_keys) {
       uint64_t* part = tmpk + start;
-      for (int i = threadIdx.x; i < len; i += blockDim.x) {
-        const uint64_t k = seg[i];
-        const int pos = atomicAdd(&s_dcur[(sort_word(k) >> sh) & 0xFFu], 1);
-        part[pos] = (k & 0xffffffff00000000ull) | (uint64_t)(uint32_t)i;
+      for (int i0 = threadIdx.x; i0 < len; i0 += kBatch * NT) {
+        uint32_t w[kBatch];
+#pragma unroll
+        for (int j = 0; j < kBatch; ++j) {
+          const int i = i0 + j * NT;
+          w[j] = sort_word(seg[i < len ? i : 0]);
+        }
+#pragma unroll
+        for (int j = 0; j < kBatch; ++j) {
+          const int i = i0 + j * NT;
+          if (i < len) {
+            const int pos = atomicAdd(&s_dcur[(w[j] >> sh) & 0xFFu], 1);
+            part[pos] = ((uint64_t)w[j] << 32) | (uint64_t)(uint32_t)i;
+          }
+        }
       }
       __threadfence_block();
       __syncthreads();
@@ -435,21 +592,23 @@ __global__ __launch_bounds__(NT) void k_segsort(
       while (d0 < 256) {
         const int g0 = s_dstart[d0];
         int d1 = d0 + 1;
-        while (d1 < 256 && s_dstart[d1 + 1] - g0 <= lds_keys) ++d1;
+        if (lazy) {   // a group just long enough for the prefix (fewer keys to sort)
+          while (d1 < 256 && s_dstart[d1] - g0 < lz.prefix && s_dstart[d1 + 1] - g0 <= lds_keys) ++d1;
+        } else {
+          while (d1 < 256 && s_dstart[d1 + 1] - g0 <= lds_keys) ++d1;
+        }
         const int n = s_dstart[d1] - g0;
         if (n > 0) {
-          for (int i = threadIdx.x; i < n; i += blockDim.x) s_keys[i] = part[g0 + i];
+          copy_keys<NT>(s_keys, part + g0, n);
           __syncthreads();
           lds_radix_sort<NT>(s_keys, n, s_hist, seg);
-          for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            const uint32_t pp = low_word(s_keys[i]);
-            sorted_ids[start + g0 + i] = (int32_t)low_word(seg[pp]);
-            k_of_s[start + g0 + i] = k_of_slot[start + pp];
-          }
+          write_sorted<NT>(s_keys, n, seg, k_of_slot + start, sorted_ids + start + g0, k_of_s + start + g0);
           __syncthreads();
         }
         d0 = d1;
+        if (lazy && s_dstart[d0] >= lz.prefix) break;
       }
+      if (lazy && threadIdx.x == 0) lz.tile_sorted[ct] = start + s_dstart[d0];
       return;
     }
   }
@@ -462,8 +621,7 @@ __global__ __launch_bounds__(NT) void k_segsort(
   int32_t* pB = tmpp1 + start;
   for (int r0 = 0; r0 < len; r0 += lds_keys) {
     const int rl = min(lds_keys, len - r0);
-    for (int i = threadIdx.x; i < rl; i += blockDim.x)
-      s_keys[i] = (seg[r0 + i] & 0xffffffff00000000ull) | (uint64_t)(uint32_t)(r0 + i);
+    stage_keys<NT>(s_keys, seg + r0, rl, r0);
     __syncthreads();
     lds_radix_sort<NT>(s_keys, rl, s_hist, seg);
     for (int i = threadIdx.x; i < rl; i += blockDim.x) {
@@ -583,17 +741,17 @@ int gsr_bin_emit(const float* depth, const uint32_t* rect, const int32_t* isect_
   return GSR_OK;
 }
 
-int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_offset, const int32_t* tile_offset,
+static int bin_sort_impl(const char* who, const float* depth, const uint32_t* rect, const int32_t* isect_offset, const int32_t* tile_offset,
                  int32_t* tile_count, const int32_t* busy_tiles, int C, int64_t N, int width, int height, int order, int64_t n_isect,
                  int32_t max_seg, int32_t n_busy, int32_t n_big, int32_t n_mid, int emitted, const gsr_bin_stats* stats,
-                 void* workspace, size_t workspace_bytes, int32_t* sorted_ids, int32_t* k_of_s, void* stream) {
-  GSR_REQUIRE(order == GSR_ORDER_DEPTH || order == GSR_ORDER_INDEX, "gsr_bin_sort: bad order %d", order);
-  GSR_REQUIRE(n_isect >= 0 && n_isect < (1ll << 31), "gsr_bin_sort: I=%lld out of range", (long long)n_isect);
-  GSR_REQUIRE((int64_t)C * N < (1ll << 31), "gsr_bin_sort: C*N too large for 32-bit ids");
+                 void* workspace, size_t workspace_bytes, int32_t* sorted_ids, int32_t* k_of_s, const LazyArgs& lz, void* stream) {
+  GSR_REQUIRE(order == GSR_ORDER_DEPTH || order == GSR_ORDER_INDEX, "%s: bad order %d", who, order);
+  GSR_REQUIRE(n_isect >= 0 && n_isect < (1ll << 31), "%s: I=%lld out of range", who, (long long)n_isect);
+  GSR_REQUIRE((int64_t)C * N < (1ll << 31), "%s: C*N too large for 32-bit ids", who);
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   const int64_t T = (int64_t)tw * th;
   const int64_t CT = T * C;
-  GSR_REQUIRE(workspace_bytes >= gsr_bin_sort_workspace(n_isect, CT), "gsr_bin_sort: workspace too small");
+  GSR_REQUIRE(workspace_bytes >= gsr_bin_sort_workspace(n_isect, CT), "%s: workspace too small", who);
   if (n_isect == 0 || N == 0) return GSR_OK;
   hipStream_t s = (hipStream_t)stream;
   const SortWs w = sort_ws(workspace, ws_cap(workspace_bytes));
@@ -607,7 +765,7 @@ int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_
                                 workspace, workspace_bytes, stream);
     if (rc != GSR_OK) return rc;
   }
-  GSR_REQUIRE(n_big >= 0 && n_mid >= 0 && n_big + n_mid <= n_busy, "gsr_bin_sort: bad sort classes %d/%d of %d",
+  GSR_REQUIRE(n_big >= 0 && n_mid >= 0 && n_big + n_mid <= n_busy, "%s: bad sort classes %d/%d of %d", who,
               n_big, n_mid, n_busy);
   auto hist_bytes = [](int nt) { return (size_t)((nt / 64) * 256 + 64) * sizeof(int); };
   // ONE launch: separate launches per class serialise (measured slower whenever long lists
@@ -618,14 +776,49 @@ int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_
     lds_keys = min(lds_keys, kSortLdsKeys);
     hipLaunchKernelGGL(k_segsort<kSortThreads>, dim3(n_busy), dim3(kSortThreads),
                        lds_keys * sizeof(uint64_t) + hist_bytes(kSortThreads), s, keys, tmpk, tmpp0, tmpp1,
-                       tile_offset, busy_tiles, k_of_slot, lds_keys, sorted_ids, k_of_s);
+                       tile_offset, busy_tiles, k_of_slot, lds_keys, sorted_ids, k_of_s, lz);
   } else if (n_busy > 0) {
     hipLaunchKernelGGL(k_segsort<kSortThreadsSmall>, dim3(n_busy), dim3(kSortThreadsSmall),
                        kSortSmallKeys * sizeof(uint64_t) + hist_bytes(kSortThreadsSmall), s, keys, tmpk, tmpp0,
-                       tmpp1, tile_offset, busy_tiles, k_of_slot, kSortSmallKeys, sorted_ids, k_of_s);
+                       tmpp1, tile_offset, busy_tiles, k_of_slot, kSortSmallKeys, sorted_ids, k_of_s, lz);
   }
-  GSR_LAUNCH_CHECK("k_segsort");
+  GSR_LAUNCH_CHECK(who);
   return GSR_OK;
+}
+
+int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_offset, const int32_t* tile_offset,
+                 int32_t* tile_count, const int32_t* busy_tiles, int C, int64_t N, int width, int height, int order, int64_t n_isect,
+                 int32_t max_seg, int32_t n_busy, int32_t n_big, int32_t n_mid, int emitted, const gsr_bin_stats* stats,
+                 void* workspace, size_t workspace_bytes, int32_t* sorted_ids, int32_t* k_of_s, void* stream) {
+  const LazyArgs off{};
+  return bin_sort_impl("gsr_bin_sort", depth, rect, isect_offset, tile_offset, tile_count, busy_tiles, C, N, width,
+                       height, order, n_isect, max_seg, n_busy, n_big, n_mid, emitted, stats, workspace,
+                       workspace_bytes, sorted_ids, k_of_s, off, stream);
+}
+
+size_t gsr_lazy_workspace(int64_t CT) { return (size_t)(3 * CT + 4) * sizeof(int32_t); }
+
+int gsr_set_lazy_sort(int min_len, int prefix) {
+  GSR_REQUIRE(prefix >= 1, "gsr_set_lazy_sort: prefix must be >= 1, got %d", prefix);
+  gsr::g_lazy_min_len = min_len;
+  gsr::g_lazy_prefix = prefix;
+  return GSR_OK;
+}
+
+int gsr_lazy_min_len(void) { return gsr::g_lazy_min_len; }
+
+int gsr_bin_sort_lazy(const float* depth, const uint32_t* rect, const int32_t* isect_offset,
+                      const int32_t* tile_offset, int32_t* tile_count, const int32_t* busy_tiles, int C, int64_t N,
+                      int width, int height, int64_t n_isect, int32_t max_seg, int32_t n_busy, int32_t n_big,
+                      int32_t n_mid, int emitted, const gsr_bin_stats* stats, void* workspace,
+                      size_t workspace_bytes, int32_t* sorted_ids, int32_t* k_of_s, int32_t* lazy, void* stream) {
+  GSR_REQUIRE(lazy != nullptr, "gsr_bin_sort_lazy: no lazy workspace");
+  const int64_t CT = (int64_t)C * ceil_div(width, kTile) * ceil_div(height, kTile);
+  LazyArgs lz{lazy, lazy + CT, lazy + 2 * CT, lazy + 3 * CT, nullptr, g_lazy_min_len, g_lazy_prefix, 1};
+  if (lz.min_len <= 0) lz.min_len = 1 << 30;   // disabled: every list sorted whole
+  return bin_sort_impl("gsr_bin_sort_lazy", depth, rect, isect_offset, tile_offset, tile_count, busy_tiles, C, N,
+                       width, height, GSR_ORDER_DEPTH, n_isect, max_seg, n_busy, n_big, n_mid, emitted, stats,
+                       workspace, workspace_bytes, sorted_ids, k_of_s, lz, stream);
 }
 
 // Self-test of the property the sort's ranking relies on: returning LDS atomics of one wave
@@ -640,3 +833,24 @@ int gsr_selftest_lds_order(int32_t* violations, void* stream) {
 
 
 }  // extern "C"
+
+namespace gsr {
+// The second sort of the lazy path: every tile the forward flagged (list[0..count)) sorted
+// whole (one workgroup per grid slot, slots past the device-side count leave at once).
+int bin_sort_rest(const int32_t* tile_offset, int64_t CT, int32_t max_seg, int32_t n_max, void* workspace,
+                  size_t workspace_bytes, int32_t* lazy, int32_t* tile_end, int32_t* sorted_ids, int32_t* k_of_s,
+                  hipStream_t s) {
+  if (n_max <= 0) return GSR_OK;
+  const SortWs w = sort_ws(workspace, ws_cap(workspace_bytes));
+  const LazyArgs lz{lazy, lazy + CT, lazy + 2 * CT, lazy + 3 * CT, tile_end, 1 << 30, 1, 2};
+  int lds_keys = 1024;
+  while (lds_keys < max_seg && lds_keys < kSortLdsKeys) lds_keys <<= 1;
+  lds_keys = min(lds_keys, kSortLdsKeys);
+  const size_t hist = (size_t)((kSortThreads / 64) * 256 + 64) * sizeof(int);
+  hipLaunchKernelGGL(k_segsort<kSortThreads>, dim3(n_max), dim3(kSortThreads), lds_keys * sizeof(uint64_t) + hist, s,
+                     w.keys, w.tmpk, w.tmpp0, w.tmpp1, tile_offset, (const int32_t*)nullptr, w.k_of_slot, lds_keys,
+                     sorted_ids, k_of_s, lz);
+  GSR_LAUNCH_CHECK("k_segsort (lazy rest)");
+  return GSR_OK;
+}
+}  // namespace gsr

@@ -274,6 +274,23 @@ __device__ __forceinline__ int bwd_pixel_slot(int il, int jl) {
 // pixel's last entry (its 1 - alpha may be exactly 0 when opacity == 1.0f).
 constexpr float kT2DMin = 2.98023224e-8f;   // 2^-25
 
+// Lazy depth order (3D; binning.hip LazyArgs): the forward walks each list only to the end of
+// its sorted prefix (tile_sorted) and flags the tile when the walk got there -- a pixel still
+// live, or one whose last composited entry is the prefix's last (the cut key of the next
+// entry must come from a sorted list).  rerun: the second pass over the flagged tiles
+// (list[0..count), sorted whole by then), from scratch.
+struct FwdLazy {
+  const int32_t* tile_sorted;
+  int32_t* flag;
+  int32_t* list;
+  int32_t* count;
+  int rerun;
+};
+
+__device__ __forceinline__ void lazy_flag_tile(const FwdLazy& lz, int ct) {
+  if (atomicExch(&lz.flag[ct], 1) == 0) lz.list[atomicAdd(lz.count, 1)] = ct;
+}
+
 template <bool IS2D, int LPP>
 __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
@@ -281,13 +298,16 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
     int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end, float4* __restrict__ ckpt,
     const int32_t* __restrict__ chunk_base, int n_busy, int64_t CT,
-    uint64_t* __restrict__ tile_cut, float cut2d) {
+    uint64_t* __restrict__ tile_cut, float cut2d, const FwdLazy lz) {
   static_assert(!IS2D || LPP == 4, "2D walks per wave with quads");
   using PG = PixGroup<LPP>;
   using FS = FwdShape<LPP>;
   __shared__ int s_max;
   const int busy_blocks = busy_grid<LPP>(n_busy);
-  if ((int)blockIdx.x >= busy_blocks) {
+  if (lz.rerun) {
+    order = lz.list;
+    n_busy = min(n_busy, *lz.count);
+  } else if ((int)blockIdx.x >= busy_blocks) {
     fill_empty<IS2D>(order, tile_offset, n_busy, busy_blocks, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
                      out_last, tile_end, tile_cut);
     return;
@@ -312,7 +332,8 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   const float px = (float)j + off, py = (float)i + off;
   const float bx0 = (float)(tx * kTile + ox) + off, bx1 = bx0 + (float)(FS::VB - 1);
   const float by0 = (float)(ty * kTile + oy) + off, by1 = by0 + (float)(FS::VB - 1);
-  const int start = tile_offset[ct], end = tile_offset[ct + 1];
+  const int start = tile_offset[ct], list_end = tile_offset[ct + 1];
+  const int end = lz.tile_sorted && !lz.rerun ? lz.tile_sorted[ct] : list_end;
   if (threadIdx.x == 0) s_max = -1;
   __syncthreads();
   float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f;
@@ -603,7 +624,11 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     out_last[pix] = last;
   }
   if (q == 0 && last >= 0) atomicMax(&s_max, last);
-  __syncthreads();
+  if (end < list_end) {   // lazy: did the walk reach the end of the sorted prefix?
+    if (__syncthreads_or(!done || last == end - 1) && threadIdx.x == 0) lazy_flag_tile(lz, ct);
+  } else {
+    __syncthreads();
+  }
   if (threadIdx.x == 0 && s_max >= 0) atomicMax(&tile_end[ct], s_max);   // finalised by k_raster_finalize
 }
 
@@ -626,14 +651,17 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
     float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
     int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end, float4* __restrict__ ckpt,
     const int32_t* __restrict__ chunk_base, int n_busy, int64_t CT,
-    uint64_t* __restrict__ tile_cut, float cut2d) {
+    uint64_t* __restrict__ tile_cut, float cut2d, const FwdLazy lz) {
   __shared__ float4 s_r[2][3][256];              // round records, part j of slot i at s_r[buf][j][i]
   __shared__ unsigned char s_list[4][128];       // a half's quadrant survivors (slot in the half)
   __shared__ unsigned char s_box[4][4][128];     // ... and each box's, in list order
   __shared__ int s_max;
   static_assert(kChunk3 == 128, "a round half is one chunk");
   const int busy_blocks = (n_busy + 7) & ~7;
-  if ((int)blockIdx.x >= busy_blocks) {
+  if (lz.rerun) {
+    order = lz.list;
+    n_busy = min(n_busy, *lz.count);
+  } else if ((int)blockIdx.x >= busy_blocks) {
     fill_empty<IS2D>(order, tile_offset, n_busy, busy_blocks, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
                      out_last, tile_end, tile_cut);
     return;
@@ -650,7 +678,8 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
   const int i = by0i + (pos >> 2), j = bx0i + (pos & 3);
   const bool inside = i < H && j < W;
   const float px = (float)j + off, py = (float)i + off;
-  const int start = tile_offset[ct], end = tile_offset[ct + 1];
+  const int start = tile_offset[ct], list_end = tile_offset[ct + 1];
+  const int end = lz.tile_sorted && !lz.rerun ? lz.tile_sorted[ct] : list_end;
   if (threadIdx.x == 0) s_max = -1;
   float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f;
   float Tl = 1.f;   // 2D: T before the latest composited entry
@@ -810,7 +839,11 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
     out_last[pix] = last;
   }
   if (last >= 0) atomicMax(&s_max, last);
-  __syncthreads();
+  if (end < list_end) {   // lazy: did the walk reach the end of the sorted prefix?
+    if (__syncthreads_or(!done || last == end - 1) && threadIdx.x == 0) lazy_flag_tile(lz, ct);
+  } else {
+    __syncthreads();
+  }
   if (threadIdx.x == 0 && s_max >= 0) tile_end[ct] = s_max;   // one workgroup per tile; finalised by k_raster_finalize
 }
 
@@ -1219,13 +1252,14 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
                       int width, int height, float cut2d, const float* bg, int32_t n_busy, gsr_bin_stats* stats,
                       float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
                       uint64_t* tile_cut, float* chunk_state, int32_t* chunk_list,
-                      void* stream) {
+                      void* stream, const FwdLazy& lz = FwdLazy{}, int lanes = 0, bool finalize = true) {
   GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "%s: bad C=%d or image %dx%d", who, C, width, height);
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   const int64_t CT = (int64_t)C * tw * th;
   GSR_REQUIRE(CT < (1ll << 31), "%s: too many tiles", who);
   GSR_REQUIRE(n_busy >= 0 && n_busy <= CT, "%s: n_busy=%d out of [0, %lld]", who, n_busy, (long long)CT);
-  const int64_t n_fill = std::min<int64_t>(CT - n_busy, kFillBlocks);
+  // the lazy second pass covers only its (device-counted) tiles: no empty-tile fill
+  const int64_t n_fill = lz.rerun ? 0 : std::min<int64_t>(CT - n_busy, kFillBlocks);
   hipStream_t s = (hipStream_t)stream;
   // tile_end collects max(last) of the quadrant workgroups (atomicMax from the -1 that
   // gsr_bin_offsets wrote)
@@ -1234,25 +1268,26 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
   // 3D with few busy tiles (a single small view, a multi-GPU rank's share): 16 lanes per pixel,
   // 16 workgroups per tile -- a quarter of the serial walk per wave, for a chip the quad layout
   // would leave mostly idle
-  const int lanes = fwd_lanes(IS2D, n_busy);
+  if (lanes == 0) lanes = fwd_lanes(IS2D, n_busy);
+  if (lz.rerun && n_busy == 0) return GSR_OK;
   if (!IS2D && lanes == 16) {
     hipLaunchKernelGGL((k_raster_fwd<false, 16>), dim3((unsigned)(busy_grid<16>(n_busy) + n_fill)),
                        dim3(kRasterThreads), kFwdLdsPad, s, (const Splat*)rec, sorted_ids, tile_offset, tile_order,
                        width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state,
-                       chunk_base, (int)n_busy, CT, tile_cut, cut2d);
+                       chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz);
   } else if (lanes == 4) {
     hipLaunchKernelGGL((k_raster_fwd<IS2D, 4>), dim3((unsigned)(busy_grid<4>(n_busy) + n_fill)),
                        dim3(kRasterThreads), IS2D ? kFwdLdsPad2D : kFwdLdsPad, s, (const Splat*)rec, sorted_ids,
                        tile_offset, tile_order, width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end,
-                       (float4*)chunk_state, chunk_base, (int)n_busy, CT, tile_cut, cut2d);
+                       (float4*)chunk_state, chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz);
   } else {
     hipLaunchKernelGGL((k_raster_fwd_box<IS2D>), dim3((unsigned)(((n_busy + 7) & ~7) + n_fill)),
                        dim3(kRasterThreads), 0, s, (const Splat*)rec, sorted_ids, tile_offset, tile_order, width,
                        height, tw, th, bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state, chunk_base,
-                       (int)n_busy, CT, tile_cut, cut2d);
+                       (int)n_busy, CT, tile_cut, cut2d, lz);
   }
   GSR_LAUNCH_CHECK(who);
-  if (n_busy > 0) {
+  if (finalize && n_busy > 0) {
     hipLaunchKernelGGL(k_raster_finalize, dim3(ceil_div(n_busy, kRasterThreads)), dim3(kRasterThreads), 0, s,
                        depth, sorted_ids, tile_offset, tile_order, (int)n_busy, chunk_base, tile_end,
                        tile_cut, stats, chunk_list, IS2D ? GSR_ORDER_INDEX : GSR_ORDER_DEPTH);
@@ -1293,6 +1328,40 @@ int gsr3d_raster_fwd(const float* rec, const float* depth, const int32_t* sorted
   return raster_fwd<false>("gsr3d_raster_fwd", rec, depth, sorted_ids, tile_offset, tile_order, chunk_base, C, width,
                            height, 0.f, bg, n_busy, stats, rgb, alpha, final_T, last, tile_end, tile_cut,
                            chunk_state, chunk_list, stream);
+}
+
+int gsr3d_raster_fwd_lazy(const float* rec, const float* depth, int32_t* sorted_ids, const int32_t* tile_offset,
+                          const int32_t* tile_order, const int32_t* chunk_base, int C, int width, int height,
+                          const float* bg, int32_t n_busy, gsr_bin_stats* stats, float* rgb, float* alpha,
+                          float* final_T, int32_t* last, int32_t* tile_end, uint64_t* tile_cut, float* chunk_state,
+                          int32_t* chunk_list, int32_t* lazy, int32_t n_lazy_max, int32_t max_seg,
+                          void* sort_workspace, size_t sort_workspace_bytes, int32_t* k_of_s, void* stream) {
+  GSR_REQUIRE(lazy != nullptr && sort_workspace != nullptr, "gsr3d_raster_fwd_lazy: missing workspace");
+  GSR_REQUIRE(n_lazy_max >= 0 && n_lazy_max <= n_busy, "gsr3d_raster_fwd_lazy: bad n_lazy_max %d", n_lazy_max);
+  const int64_t CT = (int64_t)C * ceil_div(width, kTile) * ceil_div(height, kTile);
+  const int lanes = fwd_lanes(false, n_busy);
+  // pass 1: every tile walks its sorted prefix; tiles that reach its end are listed
+  const FwdLazy l1{lazy, lazy + CT, lazy + 2 * CT, lazy + 3 * CT, 0};
+  int rc = raster_fwd<false>("gsr3d_raster_fwd_lazy", rec, depth, sorted_ids, tile_offset, tile_order, chunk_base, C,
+                             width, height, 0.f, bg, n_busy, stats, rgb, alpha, final_T, last, tile_end, tile_cut,
+                             chunk_state, chunk_list, stream, l1, lanes, false);
+  if (rc != GSR_OK) return rc;
+  // the listed tiles sorted whole, then rendered again from scratch (same layout)
+  rc = bin_sort_rest(tile_offset, CT, max_seg, n_lazy_max, sort_workspace, sort_workspace_bytes, lazy, tile_end,
+                     sorted_ids, k_of_s, (hipStream_t)stream);
+  if (rc != GSR_OK) return rc;
+  const FwdLazy l2{lazy, lazy + CT, lazy + 2 * CT, lazy + 3 * CT, 1};
+  rc = raster_fwd<false>("gsr3d_raster_fwd_lazy", rec, depth, sorted_ids, tile_offset, tile_order, chunk_base, C,
+                         width, height, 0.f, bg, n_lazy_max, stats, rgb, alpha, final_T, last, tile_end, tile_cut,
+                         chunk_state, chunk_list, stream, l2, lanes, false);
+  if (rc != GSR_OK) return rc;
+  if (n_busy > 0) {
+    hipLaunchKernelGGL(k_raster_finalize, dim3(ceil_div(n_busy, kRasterThreads)), dim3(kRasterThreads), 0,
+                       (hipStream_t)stream, depth, sorted_ids, tile_offset, tile_order, (int)n_busy, chunk_base,
+                       tile_end, tile_cut, stats, chunk_list, GSR_ORDER_DEPTH);
+    GSR_LAUNCH_CHECK("k_raster_finalize");
+  }
+  return GSR_OK;
 }
 
 int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,

@@ -142,7 +142,7 @@ _VIEWS = {"rec": ("pre", _F32), "depth": ("pre", _F32), "rect": ("pre", _I32), "
           "chunk_base": ("pre", _I32), "stats_dev": ("pre", _I32),
           "sorted_ids": ("post", _I32), "k_of_s": ("post", _I32), "final_T": ("pre", _F32),
           "last": ("pre", _I32), "tile_end": ("pre", _I32), "tile_cut": ("pre", _I64),
-          "chunk_state": ("chunks", _F32), "chunk_list": ("chunks", _I32)}
+          "chunk_state": ("chunks", _F32), "chunk_list": ("chunks", _I32), "lazy": ("pre", _I32)}
 
 _pinned = {}
 _size_hint = {}   # (device, C, N, W, H) -> (I, n_chunks) of the last forward of that shape
@@ -189,14 +189,15 @@ class _Bins:
             "rec": CN * 48, "depth": CN * 4, "rect": CN * 8, "cnt": CN * 4,
             "isect_off": CN * 4, "tile_off": (self.CT + 1) * 4, "busy": self.CT * 4,
             "chunk_base": (self.CT + 1) * 4, "tile_end": self.CT * 4, "tile_cut": self.CT * 8,
-            "stats_dev": 32, "final_T": C * width * height * 8, "last": C * width * height * 4})
+            "stats_dev": 32, "final_T": C * width * height * 8, "last": C * width * height * 4,
+            "lazy": (3 * self.CT + 4) * 4})
         self.p = dict(self.pre.ptr)
         self.tc = _tile_counts(device, self.CT, _stream(device))
         self.p["tile_cnt"] = self.tc[0].data_ptr()
         self.post = self.chunks = None
         self.post_cap = self.chunk_cap = 0
         self.emitted = False
-        self.n_chunks = self.n_isect = self.max_seg = self.n_busy = 0
+        self.n_chunks = self.n_isect = self.max_seg = self.n_busy = self.n_lazy = 0
         self.key = (str(device), C, N, width, height)
 
     def take_tile_counts(self) -> int:
@@ -300,6 +301,25 @@ class _Bins:
                              self.post.off["sort_ws"][1], p["sorted_ids"], p["k_of_s"], stream), "gsr_bin_sort")
         self.tc[1] = True   # offsets reset the counter, the emit counted every tile back to 0
 
+    def lazy_bound(self) -> int:
+        """0 when every list is sorted whole; else an upper bound on the lazily sorted tiles
+        (gsr_bin_sort_lazy: lists longer than gsr_lazy_min_len)."""
+        m = lib().gsr_lazy_min_len()
+        if m <= 0 or self.max_seg <= m:
+            return 0
+        return self.n_sort_big if m >= 8191 else self.n_busy
+
+    def sort_lazy(self, stream):
+        L = lib()
+        p = self.p
+        with _timed("bin_sort"):
+          check(L.gsr_bin_sort_lazy(p["depth"], p["rect"], p["isect_off"], p["tile_off"], p["tile_cnt"], p["busy"],
+                                  self.C, self.N, self.W, self.H, self.n_isect, self.max_seg, self.n_busy,
+                                  self.n_sort_big, self.n_sort_mid, int(self.emitted), p["stats_dev"], p["sort_ws"],
+                                  self.post.off["sort_ws"][1], p["sorted_ids"], p["k_of_s"], p["lazy"], stream),
+                "gsr_bin_sort_lazy")
+        self.tc[1] = True
+
 
 def _record_stats(b: _Bins):
     _last_stats.clear()
@@ -369,14 +389,26 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
     b.emit_early(_lib.ORDER_DEPTH, stream)
     b.offsets_wait()
     b.ensure_post(with_chunks=True)
-    b.sort(_lib.ORDER_DEPTH, stream)
+    n_lazy = b.n_lazy = b.lazy_bound()
+    if n_lazy:
+        b.sort_lazy(stream)
+    else:
+        b.sort(_lib.ORDER_DEPTH, stream)
     rgb = torch.empty(C, height, width, 3, device=dev, dtype=torch.float32)
     alpha = torch.empty(C, height, width, device=dev, dtype=torch.float32)
     with _timed("raster3d_fwd"):
-      check(L.gsr3d_raster_fwd(q["rec"], q["depth"], q["sorted_ids"], q["tile_off"], q["busy"], q["chunk_base"],
-                             C, width, height, _ptr(bgc), b.n_busy, q["stats_dev"], _ptr(rgb), _ptr(alpha),
-                             q["final_T"], q["last"], q["tile_end"], q["tile_cut"], q["chunk_state"],
-                             q["chunk_list"], stream), "gsr3d_raster_fwd")
+      if n_lazy:
+        check(L.gsr3d_raster_fwd_lazy(q["rec"], q["depth"], q["sorted_ids"], q["tile_off"], q["busy"],
+                                      q["chunk_base"], C, width, height, _ptr(bgc), b.n_busy, q["stats_dev"],
+                                      _ptr(rgb), _ptr(alpha), q["final_T"], q["last"], q["tile_end"], q["tile_cut"],
+                                      q["chunk_state"], q["chunk_list"], q["lazy"], n_lazy, b.max_seg,
+                                      q["sort_ws"], b.post.off["sort_ws"][1], q["k_of_s"], stream),
+              "gsr3d_raster_fwd_lazy")
+      else:
+        check(L.gsr3d_raster_fwd(q["rec"], q["depth"], q["sorted_ids"], q["tile_off"], q["busy"], q["chunk_base"],
+                                 C, width, height, _ptr(bgc), b.n_busy, q["stats_dev"], _ptr(rgb), _ptr(alpha),
+                                 q["final_T"], q["last"], q["tile_end"], q["tile_cut"], q["chunk_state"],
+                                 q["chunk_list"], stream), "gsr3d_raster_fwd")
     _record_stats(b)
     return rgb, alpha, b, (p, stride, V, Kc, bgc, width, height, opts)
 

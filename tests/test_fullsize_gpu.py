@@ -72,12 +72,26 @@ def _check_lists_vs_torch_sort(p, V, K, W, H, C, dev):
     tile = (owner // N) * T + (y0[owner] + local // w) * tw + (x0[owner] + local % w)
     dbits = b.depth[:C * N].contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
     order = torch.sort((tile << 32) | dbits[owner], stable=True).indices
-    assert torch.equal(b.sorted_ids[:I].to(torch.int64), owner[order])
     off = torch.zeros(C * T + 1, dtype=torch.int64, device=dev)
     off[1:] = torch.cumsum(torch.bincount(tile, minlength=C * T), 0)
     assert torch.equal(b.tile_off.to(torch.int64), off)
-    ks = b.k_of_s[:I].to(torch.int64)
-    assert torch.equal(torch.sort(ks).values, torch.arange(I, device=dev))
+    # emission index of every entry: the Gaussian's claimed offset + its rect's row-major index
+    kemit = b.isect_off[:C * N].to(torch.int64)[owner] + local
+    if b.n_lazy:
+        # lazy depth order (gsr_bin_sort_lazy): each list is exact up to the end of its sorted
+        # prefix, which holds every entry the forward consumed (tile_end)
+        ts = b.lazy[:C * T].to(torch.int64)
+        te = b.tile_end.to(torch.int64)
+        busy = off[1:] > off[:-1]
+        assert bool((te[busy] <= ts[busy]).all()) and bool((ts <= off[1:]).all())
+        tile_sorted = torch.sort(tile).values
+        keep = torch.arange(I, device=dev) < ts[tile_sorted]
+        print(f"[lists] lazy: {int(keep.sum())} of {I} entries in sorted prefixes, "
+              f"{int((ts[busy] < off[1:][busy]).sum())} lists partly sorted")
+    else:
+        keep = torch.ones(I, dtype=torch.bool, device=dev)
+    assert torch.equal(b.sorted_ids[:I].to(torch.int64)[keep], owner[order][keep])
+    assert torch.equal(b.k_of_s[:I].to(torch.int64)[keep], kemit[order][keep])
     return I, int(b.max_seg)
 
 
