@@ -1,7 +1,10 @@
+#!/bin/bash
+# On the GPU box: step time, sort and forward kernel times per lazy-sort setting (MIN_LEN,PREFIX)
+# at configs 5, 3 and 2.  Usage: tools/lazy_sweep.sh "0,1 8192,4096 ..."
 set -e
-cd /root/repo
-for lz in 0,1 16384,8192 16384,6144 16384,4096 8192,6144 8192,4096 12288,6144; do
-  for c in 5 3; do
+cd "$(dirname "$0")/.."
+for lz in ${1:-0,1 8192,4096}; do
+  for c in 5 3 2; do
     timeout -k 10 100 python bench.py --config $c --cpu-baseline 0 --psnr 0 --steps 20 --lazy $lz > gpurun_out/lz_${c}_${lz}.json 2>/dev/null
   done
 done
