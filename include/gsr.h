@@ -208,6 +208,11 @@ int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_
  * are unspecified.  lazy: caller-owned int32 workspace of gsr_lazy_workspace(CT) bytes.
  * gsr_set_lazy_sort (process-wide; default min_len 16384, prefix 4096; min_len <= 0
  * disables); gsr_lazy_min_len returns the current min_len. */
+/* Emission layout (process-wide, for tests and timing): 1 (default) = entries staged in LDS
+ * by tile and written out in per-tile runs when the camera has <= 8192 tiles; 0 = every entry
+ * scattered from its thread.  Same slots either way. */
+int gsr_set_emit_staged(int on);
+
 size_t gsr_lazy_workspace(int64_t CT);
 int gsr_set_lazy_sort(int min_len, int prefix);
 int gsr_lazy_min_len(void);

@@ -61,6 +61,7 @@ struct LazyArgs {
 };
 static int g_lazy_min_len = 16384;
 static int g_lazy_prefix = 4096;
+static int g_emit_staged = 1;   // gsr_set_emit_staged
 
 // ---------------------------------------------------------------- tile scan (single block)
 // tile_offset[0..CT] (list starts), chunk_base[0..CT] (starts of each tile's GSR_CHUNK-entry chunks,
@@ -266,6 +267,122 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__
         keys[slot] = key;
         k_of_slot[slot] = k++;
       }
+  }
+}
+
+// Staged emission: the same slots, but each workgroup first builds its entries in LDS grouped
+// by tile (local counting sort) and then writes them out with consecutive lanes on
+// consecutive slots.  The direct scatter above stores every 8-byte key and 4-byte emission
+// index on its own, so the runs a workgroup gives each tile (~5 entries at config 5) reach
+// HBM as partial-line writes: 906 MB written per launch for 306 MB of entries
+// (profiles/r02_pmc_traffic_cfg5.csv).  2048 Gaussians per workgroup make the runs longer.
+constexpr int kStageThreads = 1024;
+constexpr int kStagePer = 2048;          // Gaussians per workgroup
+constexpr int kStageCap = 6144;          // staged entries (16 B each)
+constexpr int kStageMaxTiles = 8192;     // cursor + offset per tile, 8 B each
+constexpr size_t kStageLds = (size_t)kStageCap * 16;
+
+__global__ __launch_bounds__(kStageThreads) void k_emit_staged(
+    const float* __restrict__ depth, const uint2* __restrict__ rect, const int32_t* __restrict__ isect_offset,
+    int64_t N, int tw, int th, int order, const int32_t* __restrict__ tile_offset, int32_t* __restrict__ tile_count,
+    uint64_t* __restrict__ keys, int32_t* __restrict__ k_of_slot, const gsr_bin_stats* __restrict__ stats,
+    int64_t cap) {
+  if (stats->n_isect > cap) return;   // see k_emit
+  constexpr int NT = kStageThreads;
+  constexpr int GPT = kStagePer / NT;   // Gaussians per thread
+  extern __shared__ uint64_t s_key[];   // [kStageCap]
+  int32_t* s_kos = (int32_t*)(s_key + kStageCap);
+  int32_t* s_slot = s_kos + kStageCap;
+  int* cur = s_slot + kStageCap;        // [T] local cursor (starts at the tile's local offset)
+  const int T = tw * th;
+  int* delta = cur + T;                 // [T] global slot - local position
+  __shared__ int s_tmp[NT / 64 + 1];
+  const int c = blockIdx.y;
+  int32_t* gcnt = tile_count + (int64_t)c * T;
+  const int32_t* toff = tile_offset + (int64_t)c * T;
+  const int64_t n0 = (int64_t)blockIdx.x * kStagePer;
+  for (int t = threadIdx.x; t < T; t += NT) cur[t] = 0;
+  uint2 rr[GPT];
+#pragma unroll
+  for (int j = 0; j < GPT; ++j) {
+    const int64_t n = n0 + threadIdx.x + j * NT;
+    rr[j] = n < N ? rect[(int64_t)c * N + n] : make_uint2(0u, 0u);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < GPT; ++j) {
+    const int x0 = rr[j].x & 0xffff, x1 = rr[j].x >> 16, y0 = rr[j].y & 0xffff, y1 = rr[j].y >> 16;
+    for (int ty = y0; ty < y1; ++ty)
+      for (int tx = x0; tx < x1; ++tx) atomicAdd(&cur[ty * tw + tx], 1);
+  }
+  __syncthreads();
+  // local offsets: thread-contiguous tile ranges, serial sums, one block scan
+  const int tpt = (T + NT - 1) / NT;
+  const int t0 = min(T, (int)threadIdx.x * tpt), t1 = min(T, t0 + tpt);
+  int mine = 0;
+  for (int t = t0; t < t1; ++t) mine += cur[t];
+  int total;
+  int run = block_exclusive_scan<NT>(mine, s_tmp, &total);
+  for (int t = t0; t < t1; ++t) {
+    const int v = cur[t];
+    delta[t] = v;   // the count, until the claim below
+    cur[t] = run;
+    run += v;
+  }
+  __syncthreads();
+  // claim the global ranges: batches of 8 returning atomics in flight per thread
+  for (int b0 = threadIdx.x; b0 < T; b0 += 8 * NT) {
+    int v[8], base[8], got[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int t = b0 + j * NT;
+      v[j] = t < T ? delta[t] : 0;
+      base[j] = t < T ? toff[t] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) got[j] = v[j] ? atomicSub(&gcnt[b0 + j * NT], v[j]) : 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int t = b0 + j * NT;
+      if (t < T) delta[t] = base[j] + got[j] - v[j] - cur[t];
+    }
+  }
+  __syncthreads();
+  const bool staged = total <= kStageCap;   // uniform: else scatter directly (huge rects)
+  uint64_t key[GPT];
+  int k0[GPT];
+#pragma unroll
+  for (int j = 0; j < GPT; ++j) {
+    const int64_t n = n0 + threadIdx.x + j * NT;
+    const int64_t cn = (int64_t)c * N + (n < N ? n : 0);
+    key[j] = sort_key(depth, cn, order);
+    k0[j] = isect_offset[cn];
+  }
+#pragma unroll
+  for (int j = 0; j < GPT; ++j) {
+    const int x0 = rr[j].x & 0xffff, x1 = rr[j].x >> 16, y0 = rr[j].y & 0xffff, y1 = rr[j].y >> 16;
+    int k = k0[j];   // emission entries of (c,n): k = offset + rect row-major index
+    for (int ty = y0; ty < y1; ++ty)
+      for (int tx = x0; tx < x1; ++tx) {
+        const int t = ty * tw + tx;
+        const int p = atomicAdd(&cur[t], 1);
+        if (staged) {
+          s_key[p] = key[j];
+          s_kos[p] = k;
+          s_slot[p] = delta[t] + p;
+        } else {
+          keys[delta[t] + p] = key[j];
+          k_of_slot[delta[t] + p] = k;
+        }
+        ++k;
+      }
+  }
+  if (!staged) return;
+  __syncthreads();
+  for (int i = threadIdx.x; i < total; i += NT) {
+    const int slot = s_slot[i];
+    keys[slot] = s_key[i];
+    k_of_slot[slot] = s_kos[i];
   }
 }
 
@@ -733,6 +850,14 @@ int gsr_bin_emit(const float* depth, const uint32_t* rect, const int32_t* isect_
   const int64_t cap = ws_cap(workspace_bytes);
   const SortWs w = sort_ws(workspace, cap);
   const int use_lds = T <= kHistMaxTiles;
+  if (T <= kStageMaxTiles && g_emit_staged) {
+    const size_t lds = kStageLds + (size_t)2 * T * sizeof(int);
+    hipLaunchKernelGGL(k_emit_staged, dim3(ceil_div(N, kStagePer), C), dim3(kStageThreads), lds, (hipStream_t)stream,
+                       depth, (const uint2*)rect, isect_offset, N, tw, th, order, tile_offset, tile_count, w.keys,
+                       w.k_of_slot, stats, cap);
+    GSR_LAUNCH_CHECK("k_emit_staged");
+    return GSR_OK;
+  }
   dim3 grid(ceil_div(N, kEmitPerBlock), C);
   hipLaunchKernelGGL(k_emit, grid, dim3(kEmitThreads), use_lds ? T * sizeof(int) : 0, (hipStream_t)stream, depth,
                      (const uint2*)rect, isect_offset, N, tw, th, order, use_lds, tile_offset, tile_count, w.keys,
@@ -806,6 +931,11 @@ int gsr_set_lazy_sort(int min_len, int prefix) {
 }
 
 int gsr_lazy_min_len(void) { return gsr::g_lazy_min_len; }
+
+int gsr_set_emit_staged(int on) {
+  gsr::g_emit_staged = on != 0;
+  return GSR_OK;
+}
 
 int gsr_bin_sort_lazy(const float* depth, const uint32_t* rect, const int32_t* isect_offset,
                       const int32_t* tile_offset, int32_t* tile_count, const int32_t* busy_tiles, int C, int64_t N,

@@ -122,3 +122,44 @@ def test_lazy_prefix_is_exact_order(cuda):
         print(f"[lazy] prefix {prefix}: {int(lazy_tiles.sum())} lists kept a partial sort, "
               f"{int(in_prefix.sum())} of {n} entries sorted")
     assert kept > 0
+
+
+class emit_staged:
+    def __init__(self, on):
+        self.on = on
+
+    def __enter__(self):
+        from gsr import _lib
+        _lib.check(_lib.lib().gsr_set_emit_staged(self.on), "gsr_set_emit_staged")
+
+    def __exit__(self, *exc):
+        from gsr import _lib
+        _lib.check(_lib.lib().gsr_set_emit_staged(1), "gsr_set_emit_staged")
+
+
+@pytest.mark.parametrize("kind", ["3d", "2d"])
+def test_staged_emit_equals_scatter(cuda, kind):
+    """LDS-staged emission (runs per tile) and the direct scatter claim the same slots up to
+    the order inside a tile's bucket, which the per-tile sort removes: sorted lists, renders
+    and gradients are bit-identical."""
+    from gsr import render as R
+    from gsr.scenes import gaussians2d
+    outs = []
+    for on in (0, 1):
+        with emit_staged(on):
+            if kind == "3d":
+                p, V, K, W, H, vr, va = _scene(cuda)
+                res, _, b = _run(p, V, K, W, H, vr, va)
+                outs.append(res + (b.sorted_ids[:b.n_isect].clone(),))
+            else:
+                W, H = 96, 80
+                q = gaussians2d(3000, W, H, 9).to(cuda).requires_grad_(True)
+                bg = torch.zeros(3, device=cuda)
+                rgb, alpha = R.render2d(q, W, H, bg)
+                g = torch.Generator().manual_seed(2)
+                torch.autograd.backward([rgb, alpha], [torch.randn(rgb.shape, generator=g).to(cuda),
+                                                       torch.randn(alpha.shape, generator=g).to(cuda)])
+                _, _, b, _ = R.debug_forward2d(q.detach(), bg, W, H)
+                outs.append((rgb.detach(), alpha.detach(), q.grad.detach(), b.sorted_ids[:b.n_isect].clone()))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
