@@ -77,6 +77,9 @@ def parse(argv=None):
                          "(train_script.py:127-133) fused into libgsr kernels, or as plain torch ops")
     ap.add_argument("--fwd-lanes", type=int, default=0, choices=[0, 4, 16],
                     help="3D raster forward layout: 0 automatic, 4 or 16 lanes per pixel (gsr_set_fwd_lanes)")
+    ap.add_argument("--emit-staged", type=int, default=-1, choices=[-1, 0, 1],
+                    help="emission layout (gsr_set_emit_staged): 1 LDS-staged per-tile runs, 0 direct "
+                         "scatter, -1 library default")
     ap.add_argument("--lazy", type=str, default="",
                     help="MIN_LEN,PREFIX: lazy depth order for 3D lists longer than MIN_LEN, sorted prefix "
                          ">= PREFIX entries (gsr_set_lazy_sort; default 16384,4096; MIN_LEN 0 disables)")
@@ -646,6 +649,8 @@ def main(argv=None):
     from gsr.scenes import CONFIGS
     cfg = CONFIGS[args.config]
     _lib.check(_lib.lib().gsr_set_fwd_lanes(args.fwd_lanes), "gsr_set_fwd_lanes")
+    if args.emit_staged >= 0:
+        _lib.check(_lib.lib().gsr_set_emit_staged(args.emit_staged), "gsr_set_emit_staged")
     if args.lazy:
         mn, pf = (int(x) for x in args.lazy.split(","))
         _lib.check(_lib.lib().gsr_set_lazy_sort(mn, pf), "gsr_set_lazy_sort")

@@ -209,7 +209,8 @@ int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_
  * gsr_set_lazy_sort (process-wide; default min_len 16384, prefix 4096; min_len <= 0
  * disables); gsr_lazy_min_len returns the current min_len. */
 /* Emission layout (process-wide, for tests and timing): 1 (default) = entries staged in LDS
- * by tile and written out in per-tile runs when the camera has <= 8192 tiles; 0 = every entry
+ * by tile and written out in per-tile runs when the camera has <= 8192 tiles and the call
+ * has >= 256 workgroups of 2048 Gaussians (per camera); 0 = every entry
  * scattered from its thread.  Same slots either way. */
 int gsr_set_emit_staged(int on);
 
