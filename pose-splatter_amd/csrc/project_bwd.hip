@@ -62,8 +62,12 @@ __device__ __forceinline__ void gather_partials(const uint2 r, int tw, int64_t c
 // chain (rotation / scale / quaternion normalisation / adapter activations).
 constexpr int kContrib = 16;   // v_m[3], V_M[9], v_col[3], v_op
 
+// 5 workgroups of 256 threads per CU (96 VGPRs, 16 B/lane spilled): the kernel waits on its
+// gathers (tile cut keys, then the partial rows) most of the time, so occupancy pays --
+// config 5 486 -> 449 us, config 3 56.5 -> 54.7 us; 6 per CU (80 VGPRs, 88 B spilled) is
+// slower (636 / 77 us)
 #ifndef GSR_PBWD_MINB
-#define GSR_PBWD_MINB 1
+#define GSR_PBWD_MINB 5
 #endif
 __global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
     const float* __restrict__ params, int64_t N, int64_t stride, const float* __restrict__ viewmats,
