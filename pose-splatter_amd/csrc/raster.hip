@@ -858,16 +858,32 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_finalize(
     int32_t* __restrict__ tile_end, uint64_t* __restrict__ tile_cut, gsr_bin_stats* __restrict__ stats,
     int32_t* __restrict__ chunk_list, int key_order) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= n_busy) return;
-  const int ct = order[b];
-  const int start = tile_offset[ct], end = tile_offset[ct + 1];
-  const int m = tile_end[ct];
-  const int te = m >= 0 ? m + 1 : start;
-  tile_end[ct] = te;
-  tile_cut[ct] = te < end ? sort_key(depth, ids[te], key_order) : ~0ull;
+  const int lane = threadIdx.x & 63;
+  const bool in = b < n_busy;
+  const int ct = in ? order[b] : 0;
+  int start = 0, end = 0, te = 0;
+  if (in) {
+    start = tile_offset[ct];
+    end = tile_offset[ct + 1];
+    const int m = tile_end[ct];
+    te = m >= 0 ? m + 1 : start;
+    tile_end[ct] = te;
+    tile_cut[ct] = te < end ? sort_key(depth, ids[te], key_order) : ~0ull;
+  }
   const int nact = (te - start + kChunk3 - 1) / kChunk3;
-  if (nact > 0) {
-    const int pos = atomicAdd(&stats->n_active, nact);
+  // one atomic per wave on the active-chunk counter (one per tile serialised ~700 atomics on
+  // one address at config 3)
+  int incl = nact;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  int base = 0;
+  if (lane == 63 && incl > 0) base = atomicAdd(&stats->n_active, incl);
+  base = __shfl(base, 63, 64);
+  if (in && nact > 0) {
+    const int pos = base + incl - nact;
     const int cbase = chunk_base[ct];
     int4* desc = reinterpret_cast<int4*>(chunk_list);
     for (int k = 0; k < nact; ++k) {
