@@ -214,6 +214,11 @@ int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_
  * scattered from its thread.  Same slots either way. */
 int gsr_set_emit_staged(int on);
 
+/* Sort layout (process-wide, default 1): with at most 128 busy tiles and a list longer than
+ * 1024 (but <= 16384) entries, lists are sorted in 1024-key blocks by separate workgroups and
+ * merged by rank (same order); 0 = one workgroup per list always. */
+int gsr_set_split_sort(int on);
+
 size_t gsr_lazy_workspace(int64_t CT);
 int gsr_set_lazy_sort(int min_len, int prefix);
 int gsr_lazy_min_len(void);

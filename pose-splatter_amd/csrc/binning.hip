@@ -62,6 +62,7 @@ struct LazyArgs {
 static int g_lazy_min_len = 16384;
 static int g_lazy_prefix = 4096;
 static int g_emit_staged = 1;   // gsr_set_emit_staged
+static int g_split_sort = 1;    // gsr_set_split_sort
 
 // ---------------------------------------------------------------- tile scan (single block)
 // tile_offset[0..CT] (list starts), chunk_base[0..CT] (starts of each tile's GSR_CHUNK-entry chunks,
@@ -767,6 +768,84 @@ __global__ __launch_bounds__(NT) void k_segsort(
   }
 }
 
+// ---------------------------------------------------------------- split sort (few busy tiles)
+// With few busy tiles (a single small view, a multi-GPU rank's share) one workgroup per list
+// leaves the chip idle and the longest list's LDS sort is the whole binning's latency (config
+// 2: 35 us for 8 649 keys).  The lists are then cut into blocks of kSplitBlock keys, each
+// sorted by its own workgroup (same LDS radix sort and tie rule), and a second launch places
+// every key at its final position: its rank in its own block plus, for every other block of
+// the list, the number of keys below it there (binary searches over the list's sorted blocks
+// staged in LDS).  The keys (depth word << 32 | c*N+n) of one list are unique, so the ranks
+// are exactly the stable order of the one-workgroup sort.
+#ifndef GSR_SPLIT_BLOCK
+#define GSR_SPLIT_BLOCK 1024
+#endif
+constexpr int kSplitBlock = GSR_SPLIT_BLOCK;
+constexpr int kSplitThreads = 256;
+constexpr int kSplitMaxBusy = 128;
+constexpr int kSplitRankThreads = 1024;   // two keys per thread: the binary searches are serial LDS round trips
+
+__global__ __launch_bounds__(kSplitThreads) void k_split_blocksort(
+    const uint64_t* __restrict__ keys, uint64_t* __restrict__ tmpk, int32_t* __restrict__ tmpp,
+    const int32_t* __restrict__ tile_offset, const int32_t* __restrict__ busy, const int32_t* __restrict__ k_of_slot,
+    int nb_max, int32_t* __restrict__ sorted_ids, int32_t* __restrict__ k_of_s) {
+  __shared__ uint64_t s_keys[kSplitBlock];
+  __shared__ int s_hist[(kSplitThreads / 64) * 256 + 64];
+  const int u = blockIdx.x / nb_max, j = blockIdx.x - u * nb_max;
+  const int ct = busy[u];
+  const int start = tile_offset[ct];
+  const int len = tile_offset[ct + 1] - start;
+  const int b0 = j * kSplitBlock;
+  if (b0 >= len) return;
+  const int n = min(kSplitBlock, len - b0);
+  const uint64_t* seg = keys + start;
+  stage_keys<kSplitThreads>(s_keys, seg + b0, n, b0);
+  __syncthreads();
+  lds_radix_sort<kSplitThreads>(s_keys, n, s_hist, seg);
+  if (len <= kSplitBlock) {   // one block: final order
+    write_sorted<kSplitThreads>(s_keys, n, seg, k_of_slot + start, sorted_ids + start, k_of_s + start);
+    return;
+  }
+  for (int i = threadIdx.x; i < n; i += kSplitThreads) {
+    const uint32_t p = low_word(s_keys[i]);
+    tmpk[start + b0 + i] = seg[p];   // the full key: (depth word << 32 | c*N+n)
+    tmpp[start + b0 + i] = (int32_t)p;
+  }
+}
+
+__global__ __launch_bounds__(kSplitRankThreads) void k_split_rank(
+    const uint64_t* __restrict__ tmpk, const int32_t* __restrict__ tmpp, const int32_t* __restrict__ tile_offset,
+    const int32_t* __restrict__ busy, const int32_t* __restrict__ k_of_slot, int nb_max,
+    int32_t* __restrict__ sorted_ids, int32_t* __restrict__ k_of_s) {
+  extern __shared__ uint64_t s_all[];   // the list's sorted blocks
+  const int u = blockIdx.x / nb_max, j = blockIdx.x - u * nb_max;
+  const int ct = busy[u];
+  const int start = tile_offset[ct];
+  const int len = tile_offset[ct + 1] - start;
+  const int nb = (len + kSplitBlock - 1) / kSplitBlock;
+  if (nb <= 1 || j >= nb) return;
+  copy_keys<kSplitRankThreads>(s_all, tmpk + start, len);
+  __syncthreads();
+  const int b0 = j * kSplitBlock;
+  const int n = min(kSplitBlock, len - b0);
+  for (int i = threadIdx.x; i < n; i += kSplitRankThreads) {
+    const uint64_t k = s_all[b0 + i];
+    int pos = i;
+    for (int jj = 0; jj < nb; ++jj) {
+      if (jj == j) continue;
+      int lo = jj * kSplitBlock, hi = min(lo + kSplitBlock, len);   // keys of block jj below k
+      const int base = lo;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s_all[mid] < k) lo = mid + 1; else hi = mid;
+      }
+      pos += lo - base;
+    }
+    sorted_ids[start + pos] = (int32_t)low_word(k);
+    k_of_s[start + pos] = k_of_slot[start + tmpp[start + b0 + i]];
+  }
+}
+
 __global__ void k_selftest_lds_order(int32_t* violations) {
   __shared__ int hist[4][256];
   __shared__ int got[256];
@@ -895,6 +974,17 @@ static int bin_sort_impl(const char* who, const float* depth, const uint32_t* re
   GSR_REQUIRE(n_big >= 0 && n_mid >= 0 && n_big + n_mid <= n_busy, "%s: bad sort classes %d/%d of %d", who,
               n_big, n_mid, n_busy);
   auto hist_bytes = [](int nt) { return (size_t)((nt / 64) * 256 + 64) * sizeof(int); };
+  if (lz.mode == 0 && g_split_sort && n_busy > 0 && n_busy <= kSplitMaxBusy && max_seg > kSplitBlock &&
+      max_seg <= kSortLdsKeys) {
+    const int nb_max = (max_seg + kSplitBlock - 1) / kSplitBlock;
+    hipLaunchKernelGGL(k_split_blocksort, dim3(n_busy * nb_max), dim3(kSplitThreads), 0, s, keys, tmpk, tmpp0,
+                       tile_offset, busy_tiles, k_of_slot, nb_max, sorted_ids, k_of_s);
+    GSR_LAUNCH_CHECK("k_split_blocksort");
+    hipLaunchKernelGGL(k_split_rank, dim3(n_busy * nb_max), dim3(kSplitRankThreads), (size_t)max_seg * sizeof(uint64_t), s,
+                       tmpk, tmpp0, tile_offset, busy_tiles, k_of_slot, nb_max, sorted_ids, k_of_s);
+    GSR_LAUNCH_CHECK("k_split_rank");
+    return GSR_OK;
+  }
   // ONE launch: separate launches per class serialise (measured slower whenever long lists
   // exist); the small shape only when every list is short (e.g. the 2D configs)
   if (n_big + n_mid > 0) {
@@ -933,6 +1023,11 @@ int gsr_set_lazy_sort(int min_len, int prefix) {
 }
 
 int gsr_lazy_min_len(void) { return gsr::g_lazy_min_len; }
+
+int gsr_set_split_sort(int on) {
+  gsr::g_split_sort = on != 0;
+  return GSR_OK;
+}
 
 int gsr_set_emit_staged(int on) {
   gsr::g_emit_staged = on != 0;

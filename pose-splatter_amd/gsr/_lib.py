@@ -75,6 +75,7 @@ EXPORTS = {
     "gsr3d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _I32, _P, _P, _P,
                                         _P, _P, _P, _P, _P, _P, _P]),
     "gsr_set_emit_staged": (ctypes.c_int, [_I32]),
+    "gsr_set_split_sort": (ctypes.c_int, [_I32]),
     "gsr_lazy_workspace": (_SZ, [_I64]),
     "gsr_set_lazy_sort": (ctypes.c_int, [_I32, _I32]),
     "gsr_lazy_min_len": (ctypes.c_int, []),

@@ -163,6 +163,9 @@ def test_cfg2_view_vs_oracle(cuda):
     tgt = (rgb_o.detach() + 0.05 * torch.randn(rgb_o.shape, generator=torch.Generator().manual_seed(1))).clamp(0, 1)
     psnr = lambda x: float(10 * torch.log10(1.0 / ((x - tgt) ** 2).mean()))
     assert abs(psnr(rgb_g.cpu()) - psnr(rgb_o.detach())) < 0.05, r
+    # the tile lists (36 busy tiles: the split block sort + rank merge) against a stable sort
+    I, max_seg = _check_lists_vs_torch_sort(p, V, K, W, H, c.views, cuda)
+    assert max_seg > 2048
 
 
 def test_cfg5_band_vs_oracle(cuda):

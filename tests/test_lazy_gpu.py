@@ -163,3 +163,39 @@ def test_staged_emit_equals_scatter(cuda, kind):
                 outs.append((rgb.detach(), alpha.detach(), q.grad.detach(), b.sorted_ids[:b.n_isect].clone()))
     for x, y in zip(*outs):
         assert torch.equal(x, y)
+
+
+class split_sort:
+    def __init__(self, on):
+        self.on = on
+
+    def __enter__(self):
+        from gsr import _lib
+        _lib.check(_lib.lib().gsr_set_split_sort(self.on), "gsr_set_split_sort")
+
+    def __exit__(self, *exc):
+        from gsr import _lib
+        _lib.check(_lib.lib().gsr_set_split_sort(1), "gsr_set_split_sort")
+
+
+def test_split_sort_equals_one_workgroup_sort(cuda):
+    """Few busy tiles with long lists (BASELINE config 2's scene: 36 busy tiles, lists up to
+    8 649): the block sorts + rank merge give exactly the one-workgroup-per-list order, and
+    the same renders and gradients."""
+    from gsr import render as R
+    from gsr.scenes import CONFIGS, gaussians3d, ring_cameras
+    c = CONFIGS[2]
+    p = gaussians3d(c.N, c.seed).to(cuda)
+    V, K = ring_cameras(c.views, c.width, c.height)
+    V, K = V.to(cuda), K.to(cuda)
+    g = torch.Generator().manual_seed(8)
+    vr = torch.randn(c.views, c.height, c.width, 3, generator=g).to(cuda)
+    va = torch.randn(c.views, c.height, c.width, generator=g).to(cuda)
+    outs = []
+    for on in (0, 1):
+        with split_sort(on):
+            res, _, b = _run(p, V, K, c.width, c.height, vr, va)
+            assert b.n_busy <= 128 and b.max_seg > 1024, (b.n_busy, b.max_seg)
+            outs.append(res + (b.sorted_ids[:b.n_isect].clone(),))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
