@@ -782,7 +782,10 @@ __global__ __launch_bounds__(NT) void k_segsort(
 #endif
 constexpr int kSplitBlock = GSR_SPLIT_BLOCK;
 constexpr int kSplitThreads = 256;
-constexpr int kSplitMaxBusy = 128;
+#ifndef GSR_SPLIT_MAX_BUSY
+#define GSR_SPLIT_MAX_BUSY 128
+#endif
+constexpr int kSplitMaxBusy = GSR_SPLIT_MAX_BUSY;
 constexpr int kSplitRankThreads = 1024;   // two keys per thread: the binary searches are serial LDS round trips
 
 __global__ __launch_bounds__(kSplitThreads) void k_split_blocksort(
