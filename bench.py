@@ -57,8 +57,8 @@ FRAMES_2D = 8           # config 4: 8 frames x 6 views
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
     ap.add_argument("--shard", default="units", choices=["units", "views"],
                     help="3D, N>1: 'units' = the ranks split ONE C-view job by (view, tile row) units (strong "
