@@ -50,6 +50,12 @@ __device__ __forceinline__ void tile_coords(int ct, int tw, int th, int& c, int&
 // relative margin absorbs rounding, so culling changes the work, never the result.  The
 // per-Gaussian constants (L and the two edge slopes) come precomputed in the record's .w
 // slots (gsr3d_project_fwd), so the test has no transcendental.
+// sigma = a dx^2 + b dx dy + c dy^2 of a record's conic (a, b, c) = p1.xyz, one definition
+// for every kernel (the backward's alpha must be the forward's, bit for bit)
+__device__ __forceinline__ float conic_sigma(const float4 p1, float dx, float dy) {
+  return p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
+}
+
 template <bool IS2D>
 __device__ __forceinline__ bool cull_keep(const float4 p0, const float4 p1, const float4 p2, float bx0, float bx1,
                                           float by0, float by1) {
@@ -426,7 +432,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
         const float4 p1 = s_q[buf][1][idx];
         const float4 p2 = s_q[buf][2][idx];
         const float dx = p0.x - px, dy = p0.y - py;
-        const float sg = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
+        const float sg = conic_sigma(p1, dx, dy);
         const float raw = p0.z * __expf(-sg);
         const float alpha = IS2D ? raw : fminf(kAlphaMax, raw);
         const bool valid = IS2D ? (k < n && !done && alpha >= cut2d)
@@ -509,7 +515,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
       const float4 p1 = s_pw[wv][1][kk];
       const float4 p2 = s_pw[wv][2][kk];
       const float dx = p0.x - px, dy = p0.y - py;
-      const float sg = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
+      const float sg = conic_sigma(p1, dx, dy);
       const float raw = p0.z * __expf(-sg);
       const float alpha = IS2D ? raw : fminf(kAlphaMax, raw);
       const bool valid = IS2D ? (k < n && !done && alpha >= cut2d)
@@ -654,7 +660,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
     uint64_t* __restrict__ tile_cut, float cut2d, const FwdLazy lz) {
   __shared__ float4 s_r[2][3][256];              // round records, part j of slot i at s_r[buf][j][i]
   __shared__ unsigned char s_list[4][128];       // a half's quadrant survivors (slot in the half)
-  __shared__ unsigned char s_box[4][4][128];     // ... and each box's, in list order
+  __shared__ unsigned char s_box[4][4][129];     // ... and each box's, in list order (+1: read-ahead)
   __shared__ int s_max;
   static_assert(kChunk3 == 128, "a round half is one chunk");
   const int busy_blocks = (n_busy + 7) & ~7;
@@ -767,14 +773,14 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
       int k_next = s_box[wv][box][0];
       for (int t = 0; t < nmax; ++t) {
         const int k = k_next;
-        k_next = s_box[wv][box][t + 1 < nb ? t + 1 : 0];
+        k_next = s_box[wv][box][t + 1];   // past the list: read, never used
         if (t < nb && !done) {
           const int sl = 128 * h + k;
           const float4 p0 = s_r[buf][0][sl];
           const float4 p1 = s_r[buf][1][sl];
           const float4 p2 = s_r[buf][2][sl];
           const float dx = p0.x - px, dy = p0.y - py;
-          const float sg = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
+          const float sg = conic_sigma(p1, dx, dy);
           const float raw = p0.z * __expf(-sg);
           const float alpha = IS2D ? raw : fminf(kAlphaMax, raw);
           const bool valid = IS2D ? alpha >= cut2d : (sg >= 0.f && alpha >= kAlphaThreshold);
@@ -794,7 +800,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
             }
           }
         }
-        if ((t & 7) == 7 && __ballot(!done) == 0ull) break;
+        if ((t & (IS2D ? 31 : 7)) == (IS2D ? 31 : 7) && __ballot(!done) == 0ull) break;
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -1049,6 +1055,10 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
     mu = last < b0 + kChunk3 ? mu_last : (Sv + Tf * mu_last) / T;
   }
   int wlast = last;
+  // the pixel's last entry as a slot of this chunk: lastk for the range test (the pad slot
+  // kNull is past it), lastq for the 2D equality (-1 when the last entry is in a later chunk)
+  const int lastk = min(last - b0, kChunk3 - 1);   // < 0: the pixel stopped before this chunk
+  const int lastq = last - b0 < kChunk3 ? last - b0 : -1;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wlast = max(wlast, __shfl_xor(wlast, o, 64));
   if (threadIdx.x < n) {
@@ -1126,21 +1136,21 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
       const float4 p1 = s_p[1][k];
       const float4 p2 = s_p[2][k];
       const float dx = p0.x - px, dy = p0.y - py;
-      const float sigma = p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
+      const float sigma = conic_sigma(p1, dx, dy);
       const float vis = __expf(-sigma);
       const float raw = p0.z * vis;
       const float alpha = IS2D ? raw : fminf(kAlphaMax, raw);
-      const bool valid = IS2D ? (b0 + k) <= last && alpha >= cut2d
-                              : (b0 + k) <= last && sigma >= 0.f && alpha >= kAlphaThreshold;
-      // 3D: an invalid pair enters with alpha 0, so ra = rcp(1) = 1 and fac = 0 exactly
-      // without a select each
+      // an invalid pair enters with alpha 0: ra = rcp(1) = 1, fac = 0 and (2D) v_sig = -0,
+      // mu unchanged, exactly, without a select each.  2D: the pixel's last entry (valid by
+      // construction) takes its T from the forward -- its 1 - alpha may be exactly 0.
+      const bool valid = IS2D ? k <= lastk && alpha >= cut2d : k <= lastk && sigma >= 0.f && alpha >= kAlphaThreshold;
       const float alpha_v = valid ? alpha : 0.f;
-      const float ra = IS2D ? (valid ? __builtin_amdgcn_rcpf(1.f - alpha) : 1.f) : __builtin_amdgcn_rcpf(1.f - alpha_v);
+      const float ra = __builtin_amdgcn_rcpf(1.f - alpha_v);
       if (IS2D)
-        T = valid && (b0 + k) == last ? Tl : T * ra;
+        T = k == lastq ? Tl : T * ra;
       else
         T *= ra;
-      const float fac = IS2D ? (valid ? alpha * T : 0.f) : alpha_v * T;
+      const float fac = alpha_v * T;
       acc[g * kPartial + 6] = fac * vr;
       acc[g * kPartial + 7] = fac * vg;
       acc[g * kPartial + 8] = fac * vb;
@@ -1148,8 +1158,8 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
       float v_sig;
       if constexpr (IS2D) {
         const float dmu = cv - mu;
-        v_sig = valid ? -raw * (T * dmu) : 0.f;
-        mu = valid ? mu + alpha * dmu : mu;
+        v_sig = -alpha_v * (T * dmu);
+        mu = mu + alpha_v * dmu;
       } else {
         const float v_al = T * cv + ra * (vTa - Sv);
         const bool unclamped = valid && raw <= kAlphaMax;
