@@ -165,10 +165,16 @@ def traffic_from_csv(path: str, kernel_substr: str):
 
 
 def valu_from_csv(paths, kernel_substr: str):
-    """VALU occupancy of one kernel from rocprofv3 SQ passes: SQ_ACTIVE_INST_VALU (quad-cycles,
-    summed over SIMDs) x 4 over N_SIMDS x the kernel's cycles (GRBM_GUI_ACTIVE / 8 XCDs), and
-    the issue-slot fraction SQ_INSTS_VALU x 4 cycles (a full-rate wave64 fp32 op on a 16-lane
-    SIMD) over the same SIMD-cycles.  None when the passes are missing."""
+    """VALU use of one kernel from rocprofv3 SQ passes, in the cycle model of
+    MI355X_MICROARCH.md: a wave64 VALU instruction occupies its SIMD (32 lanes) for 2 cycles,
+    and the SQ_ACTIVE_INST_* counters count quad-cycles per wave.  SIMD-cycles = N_SIMDS x
+    the kernel's cycles (GRBM_GUI_ACTIVE / 8 XCDs).
+      issue_frac  = SQ_INSTS_VALU x 2 / SIMD-cycles: the share of the SIMDs' VALU issue
+                    capacity used (1.0 = VALU-issue-bound; transcendentals cost somewhat more);
+      wave_active = SQ_ACTIVE_INST_VALU x 4 / SIMD-cycles: wave-cycles spent in VALU
+                    instructions per SIMD-cycle (summed over the waves of a SIMD, so it
+                    exceeds 1 when waves overlap -- not a utilisation).
+    None when the passes are missing."""
     import csv
     if not paths:
         return None
@@ -185,8 +191,8 @@ def valu_from_csv(paths, kernel_substr: str):
         return None
     mean = {k: sum(v) / len(v) for k, v in acc.items()}
     simd_cycles = N_SIMDS * mean["GRBM_GUI_ACTIVE"] / 8.0
-    return {"active_frac": 4.0 * mean["SQ_ACTIVE_INST_VALU"] / simd_cycles,
-            "issue_frac": 4.0 * mean["SQ_INSTS_VALU"] / simd_cycles,
+    return {"issue_frac": 2.0 * mean["SQ_INSTS_VALU"] / simd_cycles,
+            "wave_active": 4.0 * mean["SQ_ACTIVE_INST_VALU"] / simd_cycles,
             "insts_per_launch": mean["SQ_INSTS_VALU"],
             "source": [os.path.relpath(p, ROOT) for p in paths]}
 

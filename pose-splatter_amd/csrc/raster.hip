@@ -771,32 +771,43 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
       const int nmax = __builtin_amdgcn_readfirstlane(quad_max_i(nb));
       // the sequential walk of the box's survivors (entry index read one step ahead)
       int k_next = s_box[wv][box][0];
+      const float4* const rh = &s_r[buf][0][128 * h];
       for (int t = 0; t < nmax; ++t) {
         const int k = k_next;
         k_next = s_box[wv][box][t + 1];   // past the list: read, never used
         if (t < nb && !done) {
-          const int sl = 128 * h + k;
-          const float4 p0 = s_r[buf][0][sl];
-          const float4 p1 = s_r[buf][1][sl];
-          const float4 p2 = s_r[buf][2][sl];
+          __builtin_assume((unsigned)k < 256u);   // a byte: the address is one shift-add
+          const float4* rk = rh + k;   // the half's records: part j at rk[256 j]
+          const float4 p0 = rk[0];
+          const float4 p1 = rk[256];
+          const float4 p2 = rk[512];
           const float dx = p0.x - px, dy = p0.y - py;
           const float sg = conic_sigma(p1, dx, dy);
           const float raw = p0.z * __expf(-sg);
           const float alpha = IS2D ? raw : fminf(kAlphaMax, raw);
           const bool valid = IS2D ? alpha >= cut2d : (sg >= 0.f && alpha >= kAlphaThreshold);
           if (valid) {
-            const float nT = T * (1.f - alpha);
-            if (!IS2D && nT <= kTMin) {
-              done = true;   // gsplat: this entry and every later one are not composited
-            } else {
+            if constexpr (IS2D) {
               const float vis = alpha * T;
               dr += p2.x * vis;
               dg += p2.y * vis;
               db += p2.z * vis;
-              if (IS2D) Tl = T;
-              T = nT;
+              Tl = T;
+              T *= 1.f - alpha;
               last = hb + k;
-              if (IS2D && nT <= kT2DMin) done = true;   // the reference's A == 1.0f, after this entry
+              if (T <= kT2DMin) done = true;   // the reference's A == 1.0f, after this entry
+            } else {
+              const float nT = T * (1.f - alpha);
+              if (nT <= kTMin) {
+                done = true;   // gsplat: this entry and every later one are not composited
+              } else {
+                const float vis = alpha * T;
+                dr += p2.x * vis;
+                dg += p2.y * vis;
+                db += p2.z * vis;
+                T = nT;
+                last = hb + k;
+              }
             }
           }
         }

@@ -40,7 +40,7 @@ def test_valu_from_committed_sq_passes():
     sq = bench.pmc_files(3, "sq")
     v = bench.valu_from_csv(sq, bench.KERNEL_SYMBOL["raster3d_bwd"])
     assert v is not None
-    assert 0.0 < v["issue_frac"] <= v["active_frac"] + 1e-9 < 1.05, v
+    assert 0.0 < v["issue_frac"] < 1.0 and v["wave_active"] > v["issue_frac"], v
     assert v["insts_per_launch"] > 1e7
     assert bench.valu_from_csv(sq, "no_such_kernel") is None
     assert bench.valu_from_csv([os.path.join(ROOT, "profiles", "missing.csv")], "k_emit") is None
