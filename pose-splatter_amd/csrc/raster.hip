@@ -770,8 +770,41 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
       // steps walked by the wave: max over its boxes (lanes 4k..4k+3 hold the four counts)
       const int nmax = __builtin_amdgcn_readfirstlane(quad_max_i(nb));
       // the sequential walk of the box's survivors (entry index read one step ahead)
-      int k_next = s_box[wv][box][0];
       const float4* const rh = &s_r[buf][0][128 * h];
+      if constexpr (IS2D) {
+        // 2D walks branch-free (lists are long and rarely saturate; the branchy walk spent as
+        // many scalar as vector instructions on exec masks): a box's list is padded to the
+        // wave's step count with a real quadrant survivor (finite record), which a step past
+        // nb reads and leaves out by select -- the same sums, bit for bit.
+        for (int s = nb + pos; s < nmax; s += 16) s_box[wv][box][s] = s_list[wv][0];
+        __builtin_amdgcn_wave_barrier();
+        int k_next = s_box[wv][box][0];
+        for (int t = 0; t < nmax; ++t) {
+          const int k = k_next;
+          k_next = s_box[wv][box][t + 1];   // past the padded list: read, never used
+          __builtin_assume((unsigned)k < 128u);
+          const float4* rk = rh + k;   // the half's records: part j at rk[256 j]
+          const float4 p0 = rk[0];
+          const float4 p1 = rk[256];
+          const float4 p2 = rk[512];
+          const float dx = p0.x - px, dy = p0.y - py;
+          const float sg = conic_sigma(p1, dx, dy);
+          const float alpha = p0.z * __expf(-sg);
+          const bool valid = t < nb && !done && alpha >= cut2d;
+          const float vis = valid ? alpha * T : 0.f;
+          dr += p2.x * vis;
+          dg += p2.y * vis;
+          db += p2.z * vis;
+          Tl = valid ? T : Tl;
+          T = valid ? T * (1.f - alpha) : T;
+          last = valid ? hb + k : last;
+          done = done || (valid && T <= kT2DMin);   // the reference's A == 1.0f, after this entry
+          if ((t & 31) == 31 && __ballot(!done) == 0ull) break;
+        }
+        __builtin_amdgcn_wave_barrier();
+        continue;
+      }
+      int k_next = s_box[wv][box][0];
       for (int t = 0; t < nmax; ++t) {
         const int k = k_next;
         k_next = s_box[wv][box][t + 1];   // past the list: read, never used
