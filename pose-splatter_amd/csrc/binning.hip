@@ -276,13 +276,16 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__
 // consecutive slots.  The direct scatter above stores every 8-byte key and 4-byte emission
 // index on its own, so the runs a workgroup gives each tile (~5 entries at config 5) reach
 // HBM as partial-line writes: 906 MB written per launch for 306 MB of entries
-// (profiles/r02_pmc_traffic_cfg5.csv).  2048 Gaussians per workgroup make the runs longer.
+// (profiles/r02_pmc_traffic_cfg5.csv).  2048 Gaussians per workgroup make the runs longer
+// (GPT = 2 per thread, 3D: ~2 entries per Gaussian).  2D Gaussians cover ~5 tiles each (config
+// 4), so 2048 of them overflow the stage and fell back to the scattered writes (2.1 ms at
+// config 4): index-order (2D) emission takes 1024 per workgroup (GPT = 1).
 constexpr int kStageThreads = 1024;
-constexpr int kStagePer = 2048;          // Gaussians per workgroup
 constexpr int kStageCap = 6144;          // staged entries (16 B each)
 constexpr int kStageMaxTiles = 8192;     // cursor + offset per tile, 8 B each
 constexpr size_t kStageLds = (size_t)kStageCap * 16;
 
+template <int GPT>
 __global__ __launch_bounds__(kStageThreads) void k_emit_staged(
     const float* __restrict__ depth, const uint2* __restrict__ rect, const int32_t* __restrict__ isect_offset,
     int64_t N, int tw, int th, int order, const int32_t* __restrict__ tile_offset, int32_t* __restrict__ tile_count,
@@ -290,7 +293,7 @@ __global__ __launch_bounds__(kStageThreads) void k_emit_staged(
     int64_t cap) {
   if (stats->n_isect > cap) return;   // see k_emit
   constexpr int NT = kStageThreads;
-  constexpr int GPT = kStagePer / NT;   // Gaussians per thread
+  constexpr int kStagePer = GPT * NT;   // Gaussians per workgroup
   extern __shared__ uint64_t s_key[];   // [kStageCap]
   int32_t* s_kos = (int32_t*)(s_key + kStageCap);
   int32_t* s_slot = s_kos + kStageCap;
@@ -934,11 +937,18 @@ int gsr_bin_emit(const float* depth, const uint32_t* rect, const int32_t* isect_
   const int use_lds = T <= kHistMaxTiles;
   // staged when it fills the chip with its 1024-thread workgroups (config 2's 25 would leave
   // most CUs idle: 7.3 us scattered vs 9.8 us staged; config 3 30 -> 27 us, config 5 450 -> 230 us)
-  if (T <= kStageMaxTiles && g_emit_staged && ceil_div(N, kStagePer) * C >= 256) {
+  const int gpt = order == GSR_ORDER_INDEX ? 1 : 2;   // Gaussians per thread (see k_emit_staged)
+  const int64_t per = (int64_t)gpt * kStageThreads;
+  if (T <= kStageMaxTiles && g_emit_staged && ceil_div(N, per) * C >= 256) {
     const size_t lds = kStageLds + (size_t)2 * T * sizeof(int);
-    hipLaunchKernelGGL(k_emit_staged, dim3(ceil_div(N, kStagePer), C), dim3(kStageThreads), lds, (hipStream_t)stream,
-                       depth, (const uint2*)rect, isect_offset, N, tw, th, order, tile_offset, tile_count, w.keys,
-                       w.k_of_slot, stats, cap);
+    if (gpt == 1)
+      hipLaunchKernelGGL(k_emit_staged<1>, dim3(ceil_div(N, per), C), dim3(kStageThreads), lds, (hipStream_t)stream,
+                         depth, (const uint2*)rect, isect_offset, N, tw, th, order, tile_offset, tile_count, w.keys,
+                         w.k_of_slot, stats, cap);
+    else
+      hipLaunchKernelGGL(k_emit_staged<2>, dim3(ceil_div(N, per), C), dim3(kStageThreads), lds, (hipStream_t)stream,
+                         depth, (const uint2*)rect, isect_offset, N, tw, th, order, tile_offset, tile_count, w.keys,
+                         w.k_of_slot, stats, cap);
     GSR_LAUNCH_CHECK("k_emit_staged");
     return GSR_OK;
   }

@@ -248,9 +248,10 @@ class _Bins:
             return
         L = lib()
         p = self.p
-        check(L.gsr_bin_emit(p["depth"] if order == _lib.ORDER_DEPTH else None, p["rect"], p["isect_off"],
-                             p["tile_off"], p["tile_cnt"], self.C, self.N, self.W, self.H, order, p["stats_dev"],
-                             p["sort_ws"], self.post.off["sort_ws"][1], stream), "gsr_bin_emit")
+        with _timed("bin_emit"):
+          check(L.gsr_bin_emit(p["depth"] if order == _lib.ORDER_DEPTH else None, p["rect"], p["isect_off"],
+                               p["tile_off"], p["tile_cnt"], self.C, self.N, self.W, self.H, order, p["stats_dev"],
+                               p["sort_ws"], self.post.off["sort_ws"][1], stream), "gsr_bin_emit")
         self.emitted = True
 
     def offsets_wait(self):
