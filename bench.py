@@ -22,6 +22,13 @@ Multi-GPU (torchrun, one process per GPU, RCCL over xGMI), SURVEY.md §8(e):
 layout one after the other and reports the projected N-GPU time (max share + a ring
 all-reduce cost model); no multi-GPU node is needed to size the design.
 
+Launch: the steps run capacity-bounded (gsr.render "bounded": no host synchronisation, every
+buffer and grid from the previous step's bounds, overflow checked on the device and by
+check_overflow() after the timed region).  On one GPU the K timed steps are captured as ONE
+HIP graph (torch.cuda.CUDAGraph) before the timed region and replayed once inside it, with
+external HIP timing events around the dominant kernel of every step (--graph 0: eager
+launches).  `--gpus N` without a launcher starts N ranks itself (torch.distributed.run).
+
 Also reported: the dominant kernel's roofline (algorithmic bytes per launch, SURVEY.md §8(d),
 over its HIP-event-timed average duration, events on the launch stream); roofline.traffic /
 .valu from rocprofv3 PMC passes OF THE SAME CONFIG committed under profiles/ (null when none);
@@ -66,8 +73,13 @@ def parse(argv=None):
     ap.add_argument("--buckets", type=int, default=0,
                     help="all-reduce buckets (3D: Gaussian ranges of v_params; 2D: frame ranges); 0 = default "
                          "(3D 4, 2D 2; 1 on a single GPU)")
-    ap.add_argument("--rank-share", type=int, default=0,
-                    help="one GPU: time each of N ranks' shares of the strong layout and project N-GPU scaling")
+    ap.add_argument("--rank-share", type=str, default="",
+                    help="one GPU: time each rank's share of the strong layout alone and project N-GPU scaling; "
+                         "N or a list N1,N2,... (e.g. 2,4,8)")
+    ap.add_argument("--view-cost", type=float, default=0.3,
+                    help="3D strong layout: cost of each view a rank touches (its projection fwd+bwd of all N "
+                         "Gaussians), in list entries per Gaussian (x N) -- the unit partition balances "
+                         "entries read + view_cost x views touched")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the CPU oracle timing")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: every CPU this "
                                                                "process may run on)")
@@ -84,6 +96,12 @@ def parse(argv=None):
                     help="MIN_LEN,PREFIX: lazy depth order for 3D lists longer than MIN_LEN, sorted prefix "
                          ">= PREFIX entries (gsr_set_lazy_sort; default 16384,4096; MIN_LEN 0 disables)")
     ap.add_argument("--pmc-dir", default=PROFILES, help="where the per-config rocprofv3 PMC passes live")
+    ap.add_argument("--capacity", default="bounded", choices=["bounded", "exact"],
+                    help="bounded: no host sync per step (bounds from the previous step, checked on device); "
+                         "exact: one 32-byte stats read-back per forward")
+    ap.add_argument("--graph", type=int, default=-1, choices=[-1, 0, 1],
+                    help="1: capture the timed steps as one HIP graph (needs --capacity bounded); 0: eager "
+                         "launches; -1: 1 on a single GPU with bounded capacity, else 0")
     return ap.parse_args(argv)
 
 
@@ -385,10 +403,12 @@ class Workload:
     rendered views (frames) the WHOLE job completes per step; views_here the ones this rank
     renders; launch_C / launch_P the cameras / pixels of the dominant launch sequence."""
 
-    def __init__(self, cfg, dev, world: int, rank: int, shard: str, buckets: int, loss: str, comm: bool):
+    def __init__(self, cfg, dev, world: int, rank: int, shard: str, buckets: int, loss: str, comm: bool,
+                 view_cost: float = 0.3):
         from gsr import render as R
         from gsr.scenes import gaussians2d, gaussians3d, ring_cameras
         self.R, self.cfg, self.dev, self.world, self.rank = R, cfg, dev, world, rank
+        self.view_cost = view_cost * cfg.N   # in list entries (the row weights' unit)
         self.comm = comm and world > 1
         C = cfg.views
         g = torch.Generator().manual_seed(cfg.seed + 1)
@@ -453,7 +473,7 @@ class Workload:
             tw = (cfg.width + 15) // 16
             weights = [float(x) for x in R.tile_work().reshape(cfg.views * self.th, tw).sum(1).cpu()]
         self.weights = weights
-        self.v0, self.v1, self.band = unit_shard(cfg.views, self.th, self.world, self.rank, weights)
+        self.v0, self.v1, self.band = unit_shard(cfg.views, self.th, self.world, self.rank, weights, self.view_cost)
         self.views_here = self.v1 - self.v0
         self.layout = (f"(view, tile-row) units: rank {self.rank} views {self.v0}-{self.v1 - 1} rows {self.band} "
                        f"of {cfg.views}x{self.th}, {self.buckets} all-reduce bucket(s) overlapping project_bwd")
@@ -486,7 +506,8 @@ class Workload:
             if self.comm:
                 from gsr.multiview import sharded_backward_units
                 self.params.grad = sharded_backward_units(None, self.params, self.Vd, self.Kd, self.v_rgb_all,
-                                                          self.v_alpha_all, self.th, self.weights, self.buckets)
+                                                          self.v_alpha_all, self.th, self.weights, self.buckets,
+                                                          view_cost=self.view_cost)
             return
         if self.comm and self.scaling == "strong":
             from gsr.multiview import sharded_backward_units
@@ -495,7 +516,8 @@ class Workload:
                 opts = R.RenderOptions3D(band=band, grad_buckets=self.buckets if hook else 1, grad_hook=hook)
                 return R.render3d(p, Vs, Ks, cfg.width, cfg.height, self.bg, opts)
             self.params.grad = sharded_backward_units(render_band, self.params, self.Vd, self.Kd, self.v_rgb_all,
-                                                      self.v_alpha_all, self.th, self.weights, self.buckets)
+                                                      self.v_alpha_all, self.th, self.weights, self.buckets,
+                                                      view_cost=self.view_cost)
             return
         opts = R.RenderOptions3D(band=self.band) if self.band != (0, -1) else R.RenderOptions3D()
         rgb, alpha = R.render3d(self.params, self.Vd[self.v0:self.v1], self.Kd[self.v0:self.v1], cfg.width,
@@ -541,10 +563,13 @@ class Workload:
         return self.views_here, self.views_here * cfg.width * cfg.height
 
 
-def time_steps(w: Workload, steps: int, warmup: int, dist=None):
+def time_steps(w: Workload, steps: int, warmup: int, dist=None, graph: bool = False):
     """Warm up, name the dominant kernel in a separately profiled pass, then time exactly
     `steps` steps between barrier + synchronize brackets with HIP events around the dominant
-    kernel only.  Returns (elapsed_s, breakdown, dom_name, dom (avg_ms, launches))."""
+    kernel only.  graph: the `steps` steps are captured as ONE HIP graph beforehand (external
+    timing events around the dominant kernel of each step become nodes of the graph) and the
+    timed region replays it once.  Returns (elapsed_s, breakdown, dom_name, dom (avg_ms,
+    launches))."""
     R = w.R
     for _ in range(warmup):
         w.step()
@@ -556,13 +581,33 @@ def time_steps(w: Workload, steps: int, warmup: int, dist=None):
     R.enable_kernel_timing(False)
     dom_name = max(breakdown.items(), key=lambda kv: kv[1][0] * kv[1][1])[0] if breakdown else None
     torch.cuda.synchronize()
+    g = None
+    if graph:
+        # torch's capture rules: warm up on a side stream, then capture on the graph's stream
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                w.step()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        R.enable_kernel_timing(True, only={dom_name} if dom_name else None)
+        with torch.cuda.graph(g):
+            for _ in range(steps):
+                w.step()
+        torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    R.enable_kernel_timing(True, only={dom_name} if dom_name else None)
+    if g is None:
+        R.enable_kernel_timing(True, only={dom_name} if dom_name else None)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        w.step()
+    if g is not None:
+        g.replay()
+    else:
+        for _ in range(steps):
+            w.step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -570,6 +615,8 @@ def time_steps(w: Workload, steps: int, warmup: int, dist=None):
     elapsed = time.perf_counter() - t0
     ktimes = R.kernel_times_ms()
     R.enable_kernel_timing(False)
+    R.check_overflow(w.dev)   # a bounded step over its bounds would have rendered NaN: fail loudly
+    del g
     return elapsed, breakdown, dom_name, ktimes.get(dom_name, (0.0, 0)) if dom_name else (0.0, 0)
 
 
@@ -601,40 +648,67 @@ def roofline(w: Workload, dom_name, dom, args):
             "units_per_launch": {"C": C, "P": P, "N": cfg.N, "I": I, "I_eff": I_eff}}, (C, P, I, I_eff)
 
 
-def rank_share_report(cfg, args, dev):
+def rank_share_report(cfg, args, dev, n: int, weights=None):
     """--rank-share N: time each rank's share of the strong layout alone on this GPU."""
     from gsr import render as R
-    n = args.rank_share
     shares = []
-    weights = None
     for r in range(n):
-        w = Workload(cfg, dev, n, r, "units", args.buckets, "none", comm=False)
+        w = Workload(cfg, dev, n, r, "units", args.buckets, "none", comm=False, view_cost=args.view_cost)
         if cfg.mode == "3d" and w.scaling == "strong":
             if weights is None:
                 weights = w.weights
             else:
                 w.balance(weights)
-        el, bd, dom_name, dom = time_steps(w, args.steps, args.warmup)
+        el, bd, dom_name, dom = time_steps(w, args.steps, args.warmup, graph=args.graph == 1)
         log(f"share {r}/{n}: {1000.0 * el / args.steps:.3f} ms/step ({w.layout})")
+        kern = {k: round(v[0], 4) for k, v in sorted(bd.items())}
+        kern_sum = sum(v[0] * v[1] for v in bd.values()) / max(2, min(args.steps, 5))   # per step (breakdown pass)
         shares.append({"rank": r, "ms_per_step": 1000.0 * el / args.steps, "views_here": w.views_here,
-                       "layout": w.layout, "kernels_ms": {k: round(v[0], 4) for k, v in sorted(bd.items())},
+                       "layout": w.layout, "kernels_ms": kern, "kernel_sum_ms": kern_sum,
                        "I": R.last_stats().get("n_isect", 0)})
         del w
         torch.cuda.empty_cache()
     grad_bytes = cfg.N * (14 if cfg.mode == "3d" else 9) * 4 * (FRAMES_2D if cfg.mode == "2d" else 1)
     ar = allreduce_ms(grad_bytes, n)
+    ar7 = ar / 7.0
     worst = max(s["ms_per_step"] for s in shares)
     units = cfg.views * (FRAMES_2D if cfg.mode == "2d" else 1)
     return {"n": n, "shares": shares, "max_share_ms": worst, "allreduce_model_ms": ar,
             "allreduce_model": f"ring 2(n-1)/n x {grad_bytes / 1e6:.1f} MB at {XGMI_LINK_GBS:.0f} GB/s (one link), "
                                "not overlapped (upper bound)",
+            "allreduce_7link_ms": ar7,
             "projected_ms_per_step": worst + ar, "projected_value": units / ((worst + ar) * 1e-3),
-            "note": "each share timed alone on one GPU, no collectives; projected = max share + all-reduce model"}
+            "projected_ms_per_step_7link": worst + ar7, "projected_value_7link": units / ((worst + ar7) * 1e-3),
+            "view_cost": args.view_cost if cfg.mode == "3d" else None,
+            "note": "each share timed alone on one GPU, no collectives; projected = max share + all-reduce model "
+                    "(one link: upper bound; 7 links: the ring spread over all of a GPU's xGMI links)"}
+
+
+def _spawn_ranks(args, argv) -> int:
+    """`--gpus N` without a launcher: start N ranks (one process per GPU) with
+    torch.distributed.run on 127.0.0.1 and return its exit code.  Runs before this process
+    touches the GPU, and starts a child instead of exec-ing."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)]
+    cmd += list(sys.argv[1:] if argv is None else argv)
+    log(f"--gpus {args.gpus} without a launcher: starting {args.gpus} ranks ({' '.join(cmd[1:6])} ...)")
+    return subprocess.call(cmd)
 
 
 def main(argv=None):
     args = parse(argv)
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and not args.rank_share:
+        raise SystemExit(_spawn_ranks(args, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus and not args.rank_share:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # GSR_DIST_BACKEND=gloo + GSR_SAME_DEVICE=1 rehearse N ranks on a single GPU (box tests);
@@ -654,6 +728,11 @@ def main(argv=None):
     from gsr import _lib
     from gsr.scenes import CONFIGS
     cfg = CONFIGS[args.config]
+    R.set_capacity_mode(args.capacity)
+    if args.graph == -1:
+        args.graph = int(world == 1 and args.capacity == "bounded" and args.loss == "none")
+    if args.graph and args.capacity != "bounded":
+        raise SystemExit("--graph 1 needs --capacity bounded (an exact step waits on the host)")
     _lib.check(_lib.lib().gsr_set_fwd_lanes(args.fwd_lanes), "gsr_set_fwd_lanes")
     if args.emit_staged >= 0:
         _lib.check(_lib.lib().gsr_set_emit_staged(args.emit_staged), "gsr_set_emit_staged")
@@ -661,18 +740,26 @@ def main(argv=None):
         mn, pf = (int(x) for x in args.lazy.split(","))
         _lib.check(_lib.lib().gsr_set_lazy_sort(mn, pf), "gsr_set_lazy_sort")
 
-    if args.rank_share > 1:
+    if args.rank_share:
         if world > 1:
             raise SystemExit("--rank-share runs on ONE process")
-        rep = rank_share_report(cfg, args, dev)
+        ns = [int(x) for x in args.rank_share.split(",")]
+        reps = []
+        one = None
+        for n in ns:
+            reps.append(rank_share_report(cfg, args, dev, n))
+            log(f"N={n}: max share {reps[-1]['max_share_ms']:.3f} ms, projected {reps[-1]['projected_ms_per_step']:.3f} ms")
         print(json.dumps({"metric": "projected strong scaling (per-rank shares timed on one GPU)",
-                          "config": {"workload": cfg.name}, "rank_share": rep}), flush=True)
+                          "config": {"workload": cfg.name, "capacity": args.capacity,
+                                     "launch": "HIP graph per share" if args.graph else "eager"},
+                          "rank_share": reps[0] if len(reps) == 1 else None,
+                          "rank_shares": reps}), flush=True)
         return
 
     if args.loss != "none" and (cfg.mode != "3d" or world > 1):
         raise SystemExit("--loss: 3D configs on one GPU only")
-    w = Workload(cfg, dev, world, rank, args.shard, args.buckets, args.loss, comm=True)
-    elapsed, breakdown, dom_name, dom = time_steps(w, args.steps, args.warmup, dist)
+    w = Workload(cfg, dev, world, rank, args.shard, args.buckets, args.loss, comm=True, view_cost=args.view_cost)
+    elapsed, breakdown, dom_name, dom = time_steps(w, args.steps, args.warmup, dist, graph=bool(args.graph))
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -718,6 +805,9 @@ def main(argv=None):
         "config": {"workload": cfg.name, "N_gauss": cfg.N, "width": cfg.width, "height": cfg.height,
                    "views": cfg.views, "frames": FRAMES_2D if cfg.mode == "2d" else 1,
                    "units_per_step": w.units_total, "background": "white", "loss": args.loss,
+                   "capacity": args.capacity,
+                   "launch": (f"one HIP graph of the {args.steps} timed steps, replayed once" if args.graph
+                              else "eager launches"),
                    "parallelism": w.layout + (f"; backend {backend}" + (" (RCCL)" if backend == "nccl" else "")
                                               if backend else "")},
         "roofline": roof,

@@ -24,8 +24,14 @@
  *   - Plain pointers to DEVICE memory; the caller (PyTorch's caching allocator) owns all
  *     memory.  The library allocates nothing and frees nothing.  Inputs are read-only.
  *   - Every call enqueues on the caller's stream (a hipStream_t passed as void*); no call
- *     synchronises the device.  The only host read the caller needs is gsr_bin_stats
- *     (filled on the device by gsr_bin_offsets; the first 24 bytes) to size the intersection buffers.
+ *     synchronises the device.  The caller either reads gsr_bin_stats back (filled on the
+ *     device by gsr_bin_offsets; the first 32 bytes) to size the intersection buffers
+ *     exactly, or -- with NO host read at all -- passes upper bounds (gsr_bin_caps) to
+ *     gsr_bin_offsets and sizes every buffer and grid from them.  A bound that does not hold
+ *     is detected on the device: stats->overflow gets a GSR_OVF_* bit, every later kernel of
+ *     the call writes NaN to its float outputs (rgb, alpha, v_params) instead of computing,
+ *     and the bits are OR-ed into the caller's sticky status word.  A bounded call therefore
+ *     never returns a silently wrong render ("Threading / streams").
  *   - Return 0 on success; negative on failure (GSR_E*).  gsr_last_error() returns a
  *     thread-local message for the last failure of the calling thread.  No C++ exception
  *     crosses the ABI.
@@ -73,21 +79,64 @@ extern "C" {
 #define GSR_INPUT_GSPLAT 1             /* 3D rows: activated gsplat rasterization() inputs */
 
 #ifndef GSR_CHUNK
-#define GSR_CHUNK 128                  /* list entries per backward work unit (chunk; 128: measured best of 64/128/192/256) */
+#define GSR_CHUNK 128                  /* list entries per LDS-staged backward sub-chunk; the work unit
+                                          ("chunk", gsr_bin_caps.chunk_entries) is a power-of-two
+                                          multiple of it (default GSR_CHUNK) */
 #endif
 #define GSR_PARTIAL_STRIDE 12          /* floats per partial row (9 used, 16 B aligned) */
+
+/* stats->overflow bits (capacity-bounded calls; 0 = every bound held) */
+#define GSR_OVF_ISECT 1      /* I > caps->isect: intersection buffers too small              */
+#define GSR_OVF_CHUNKS 2     /* chunks > caps->chunks: chunk records / descriptors too small */
+#define GSR_OVF_BUSY 4       /* more busy tiles than the sort / raster grids cover (n_busy)  */
+#define GSR_OVF_SEG 8        /* a list longer than the split sort's geometry (max_seg)       */
+#define GSR_OVF_LAZY 16      /* more lazily sorted tiles than the re-render covers            */
+#define GSR_OVF_UNIT 32      /* a raster backward given another chunk_entries than gsr_bin_offsets */
 
 typedef struct gsr_bin_stats {
   int64_t n_isect;     /* total (Gaussian, tile) intersections I                     */
   int32_t max_seg;     /* longest per-tile list                                       */
   int32_t n_busy;      /* tiles with a non-empty list                                 */
-  int32_t n_chunks;    /* sum over tiles of ceil(list length / GSR_CHUNK)              */
+  int32_t n_chunks;    /* sum over tiles of ceil(list length / chunk_entries)          */
   int32_t n_active;    /* chunks the 3D backward visits (appended by gsr3d_raster_fwd)   */
   int32_t n_sort_big;  /* tiles with lists >= 8192 entries (the first of the busy order)   */
   int32_t n_sort_mid;  /* tiles with 4096..8191 entries (the next ones)                    */
-} gsr_bin_stats;       /* 32 bytes; counters zeroed by gsr_bin_offsets                  */
+  /* ---- capacity-bounded calls (gsr_bin_caps); zero for exact (read-back) calls ---- */
+  int64_t isect_cap;   /* copy of caps->isect (0: unbounded)                          */
+  int64_t chunk_cap;   /* copy of caps->chunks (0: unbounded)                         */
+  int32_t overflow;    /* GSR_OVF_* bits; nonzero: this call's outputs are NaN        */
+  int32_t chunk_entries; /* list entries per backward work unit (copy of caps->chunk_entries) */
+  int32_t* status;     /* copy of caps->status (device; may be NULL)                  */
+  int64_t reserved[2];
+} gsr_bin_stats;       /* 80 bytes; written by gsr_bin_offsets                         */
+
+/* Upper bounds for a call that does not read stats back (gsr_bin_offsets).  The caller sizes
+ * the intersection buffers (sort workspace, sorted_ids, k_of_s, partial rows) for `isect`
+ * entries and the chunk buffers for `chunks`, and passes grid bounds (n_busy, max_seg,
+ * n_lazy_max, n_chunks) to the later calls instead of read-back values.  status: an optional
+ * caller-owned DEVICE int32 that accumulates (OR) the overflow bits of every bounded call that
+ * reaches its raster forward (a sticky flag the caller inspects when convenient). */
+typedef struct gsr_bin_caps {
+  int64_t isect;
+  int64_t chunks;
+  int32_t* status;
+  /* list entries per backward work unit (a "chunk": one chunk record per pixel in the forward,
+   * one workgroup in the backward, which walks it back to front in GSR_CHUNK-entry sub-chunks
+   * carrying each pixel's state): 0 = GSR_CHUNK, else a power of two >= GSR_CHUNK.  Longer
+   * units write fewer chunk records and re-read the pixel state less often; shorter ones give
+   * the backward more parallelism (long, early-terminating 3D lists). */
+  int32_t chunk_entries;
+  int32_t reserved;
+} gsr_bin_caps;
 
 int gsr_version(void);
+/* ABI revision of this header (bumped whenever a prototype or struct above changes; the
+ * Python binding refuses a library whose revision differs).  Revision 3: gsr_bin_stats grew
+ * to 80 bytes and gained the bounded-call fields; gsr_bin_offsets takes gsr_bin_caps;
+ * gsr3d_project_bwd / gsr2d_project_bwd take the stats (NaN rows on overflow); gsr_bin_sort /
+ * gsr_bin_sort_lazy take mutable stats. */
+#define GSR_ABI_VERSION 3
+int gsr_abi_version(void);
 const char* gsr_last_error(void);
 
 /* Self-test of the cross-lane reduction used by the backward kernels (one 64-lane wave):
@@ -157,10 +206,14 @@ int gsr2d_project_fwd(const float* params, int64_t N, int64_t row_stride, int64_
  * order: the stats.n_busy non-empty tiles first, longest lists first, then the empty tiles),
  * tile_end [CT] (set to -1: the raster forward's atomicMax target), tile_cut [CT] (zeroed;
  * the raster forward writes the cut keys) and stats (device).  Resets the emission counter
- * tile_count[CT] to 0 (the per-tile counts are consumed by gsr_bin_sort). */
+ * tile_count[CT] to 0 (the per-tile counts are consumed by gsr_bin_sort).
+ * caps (HOST struct, may be NULL): the bounds of a call that will not read stats back; the
+ * scan records them in stats and sets GSR_OVF_ISECT / GSR_OVF_CHUNKS when I or the chunk count
+ * exceeds them (isect = chunks = 0: an exact call, the caller reads stats back and sizes from
+ * it), and the backward work-unit length (chunk_entries).  NULL: exact, GSR_CHUNK. */
 int gsr_bin_offsets(int32_t* tile_count, int64_t CT, int32_t* tile_offset,
                     int32_t* chunk_base, int32_t* busy_tiles, int32_t* tile_end,
-                    uint64_t* tile_cut, gsr_bin_stats* stats, void* stream);
+                    uint64_t* tile_cut, const gsr_bin_caps* caps, gsr_bin_stats* stats, void* stream);
 
 /* Workspace for gsr_bin_sort, bytes (depends on the I read back from stats). */
 size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT);
@@ -185,7 +238,11 @@ int gsr_bin_emit(const float* depth, const uint32_t* rect, const int32_t* isect_
  *                   backward stores that entry's partial row.
  * Sort key per entry: (sort word << 32) | c*N+n, sort word = depth float bits (3D, order
  * GSR_ORDER_DEPTH) or c*N+n (2D, GSR_ORDER_INDEX).  max_seg, n_busy and the sort classes
- * n_sort_big / n_sort_mid (workgroup shapes by list length) come from stats (host copy).
+ * n_sort_big / n_sort_mid only choose workgroup shapes and grids: the read-back values, or
+ * bounds (a bounded call: n_isect = caps->isect, n_busy >= the true busy-tile count, max_seg and
+ * the classes from an earlier call).  Every list is sorted correctly for any max_seg / class
+ * values; a busy count above n_busy (GSR_OVF_BUSY) or, in the split sort, a list longer than
+ * max_seg (GSR_OVF_SEG) is flagged in stats->overflow.
  * emitted != 0: gsr_bin_emit already ran on this workspace (same workspace_bytes) and I fit;
  * otherwise the emit runs here.  stats: the device gsr_bin_stats. */
 int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_offset,
@@ -193,7 +250,7 @@ int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_
                  const int32_t* busy_tiles, int C, int64_t N,
                  int width, int height, int order, int64_t n_isect, int32_t max_seg,
                  int32_t n_busy, int32_t n_sort_big, int32_t n_sort_mid, int emitted,
-                 const gsr_bin_stats* stats, void* workspace,
+                 gsr_bin_stats* stats, void* workspace,
                  size_t workspace_bytes, int32_t* sorted_ids, int32_t* k_of_s, void* stream);
 
 /* Lazy depth order (3D).  The forward of a tile reads its depth-sorted list only until every
@@ -225,7 +282,7 @@ int gsr_lazy_min_len(void);
 int gsr_bin_sort_lazy(const float* depth, const uint32_t* rect, const int32_t* isect_offset,
                       const int32_t* tile_offset, int32_t* tile_count, const int32_t* busy_tiles, int C,
                       int64_t N, int width, int height, int64_t n_isect, int32_t max_seg, int32_t n_busy,
-                      int32_t n_sort_big, int32_t n_sort_mid, int emitted, const gsr_bin_stats* stats,
+                      int32_t n_sort_big, int32_t n_sort_mid, int emitted, gsr_bin_stats* stats,
                       void* workspace, size_t workspace_bytes, int32_t* sorted_ids, int32_t* k_of_s,
                       int32_t* lazy, void* stream);
 
@@ -233,7 +290,10 @@ int gsr_bin_sort_lazy(const float* depth, const uint32_t* rect, const int32_t* i
 
 /* Front-to-back compositing (gsplat classic).  One workgroup per non-empty 16x16 tile,
  * visited in tile_order (the busy_tiles array of gsr_bin_offsets: non-empty tiles
- * longest-first, then the empty ones); n_busy = stats.n_busy as read back by the host.
+ * longest-first, then the empty ones).  The kernels take the busy-tile count from the device
+ * stats; n_busy sizes the grid (and picks the layout): stats.n_busy as read back, or a bound
+ * (a bounded call; the sort has flagged GSR_OVF_BUSY if it does not hold).  With
+ * stats->overflow set the call writes NaN to rgb / alpha and nothing else.
  * Empty tiles get the background (written by extra fill workgroups).  bg [C,3].
  * Outputs rgb [C,H,W,3], alpha [C,H,W], final_T [C,H,W] (exact transmittance, kept for the
  * backward), last [C,H,W] (index of the last contributing sorted entry, -1 if none),
@@ -263,12 +323,15 @@ int gsr3d_raster_fwd_lazy(const float* rec, const float* depth, int32_t* sorted_
                           void* sort_workspace, size_t sort_workspace_bytes, int32_t* k_of_s, void* stream);
 
 /* Backward of gsr3d_raster_fwd: workgroup b takes chunk_list[b] for b < stats->n_active
- * (n_chunks bounds the grid).  v_rgb [C,H,W,3], v_alpha [C,H,W] (contiguous).  Writes the
- * partial row k_of_s[s] of every sorted entry s in [tile start, tile_end). */
+ * (n_chunks bounds the grid).  chunk_entries: the caps->chunk_entries given to gsr_bin_offsets
+ * (0 = GSR_CHUNK); it selects the one- or the multi-sub-chunk kernel, and a mismatch with the
+ * forward is flagged GSR_OVF_UNIT (NaN gradients).  v_rgb [C,H,W,3], v_alpha [C,H,W]
+ * (contiguous).  Writes the partial row k_of_s[s] of every sorted entry s in [tile start,
+ * tile_end). */
 int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_end, const int32_t* chunk_base, const float* chunk_state,
                      const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
-                     int C, int width, int height, const float* bg, const float* final_T,
+                     int32_t chunk_entries, int C, int width, int height, const float* bg, const float* final_T,
                      const int32_t* last, const float* v_rgb, const float* v_alpha,
                      const int32_t* k_of_s, float* partial, void* stream);
 
@@ -290,7 +353,7 @@ int gsr2d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t*
 int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_end, const int32_t* chunk_base, const float* chunk_state,
                      const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
-                     int C, int width, int height, float eps_cut, const float* bg,
+                     int32_t chunk_entries, int C, int width, int height, float eps_cut, const float* bg,
                      const float* final_T, const int32_t* last, const float* v_rgb,
                      const float* v_alpha, const int32_t* k_of_s, float* partial, void* stream);
 
@@ -300,22 +363,24 @@ int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t*
  * chain through projection and the adapter activations, sum over cameras: rows
  * [n_begin, n_end) of v_params [N,14] (fully overwritten, deterministic; n_end = -1: N).
  * Gaussian ranges let a multi-GPU caller start the all-reduce of finished rows while later
- * ranges are still being computed.  depth: the projection's depth array (sort keys). */
+ * ranges are still being computed.  depth: the projection's depth array (sort keys).
+ * stats: the forward's device gsr_bin_stats (may be NULL): with stats->overflow set the rows
+ * are written as NaN. */
 int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride,
                       const float* viewmats, const float* Ks, int C, int width, int height,
                       float eps2d, int input_mode, const float* depth, const uint32_t* rect,
                       const int32_t* isect_offset, const int32_t* isect_count,
                       const uint64_t* tile_cut, const float* partial, int64_t n_begin,
-                      int64_t n_end, float* v_params, void* stream);
+                      int64_t n_end, const gsr_bin_stats* stats, float* v_params, void* stream);
 
 /* 2D: v_params [F,N,9] (fully overwritten): set f's gradient sums the partial rows of all its
  * cameras (set_begin as in gsr2d_project_fwd, NULL: F = 1) in camera order, then chains
- * through the activations once. */
+ * through the activations once.  stats as in gsr3d_project_bwd. */
 int gsr2d_project_bwd(const float* params, int64_t N, int64_t row_stride, int64_t set_stride,
                       const int32_t* set_begin, int F, int C, int width, int height,
                       const uint32_t* rect, const int32_t* isect_offset,
                       const int32_t* isect_count, const uint64_t* tile_cut,
-                      const float* partial, float* v_params, void* stream);
+                      const float* partial, const gsr_bin_stats* stats, float* v_params, void* stream);
 
 /* ---- Loss-fused backward ------------------------------------------
  * The reference training step (scripts/training/train_script.py:30-36, 128-133) takes
@@ -351,7 +416,7 @@ typedef struct gsr_loss_terms {
 int gsr3d_raster_bwd_loss(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                           const int32_t* tile_end, const int32_t* chunk_base,
                           const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats,
-                          int32_t n_chunks, int C, int width, int height, const float* bg,
+                          int32_t n_chunks, int32_t chunk_entries, int C, int width, int height, const float* bg,
                           const float* final_T, const int32_t* last, const gsr_loss_terms* loss,
                           const int32_t* k_of_s, float* partial, void* stream);
 
@@ -397,7 +462,9 @@ int gsr_pose3d_bwd(const float* params, int64_t N, int64_t row_stride, double an
  * torchmetrics StructuralSimilarityIndexMeasure(data_range=1.0) of C image pairs (the batch
  * mean): x = the target [C,3,H,W] and y = the render, each given as (data, strides[4] in
  * elements for (view, channel, row, column)) so planar and channels-last images are read in
- * place.  taps11: HOST array, the normalised 1-D Gaussian (11 taps, sigma 1.5) the caller
+ * place.  x_strides / y_strides: HOST int64 arrays (read on the host when the call is made;
+ * the exception to the device-pointer convention, like taps11).
+ * taps11: HOST array, the normalised 1-D Gaussian (11 taps, sigma 1.5) the caller
  * computes as torchmetrics does.  Needs H, W > 10.  fwd writes the scalar *ssim (device) and,
  * when factors != NULL (device, gsr_ssim_factors_size floats), each window's backward factors
  * (dS/dmu_y, dS/dE[y^2], dS/dE[xy]); bwd blurs those onto the pixels and writes

@@ -88,6 +88,7 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(int32_t* __restrict__
                                                           int32_t* __restrict__ order,
                                                           int32_t* __restrict__ tile_end,
                                                           uint64_t* __restrict__ tile_cut,
+                                                          const gsr_bin_caps caps,
                                                           gsr_bin_stats* __restrict__ stats) {
   constexpr int NW = kTopThreads / 64;
   __shared__ int s_w[3][NW];
@@ -122,13 +123,16 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(int32_t* __restrict__
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t R = ((CT + NW - 1) / NW + 63) & ~int64_t(63);
   const int64_t i0 = min<int64_t>(CT, R * wv), i1 = min<int64_t>(CT, i0 + R);
+  // backward work units ("chunks") of 2^ushift list entries (caps.chunk_entries, checked on the host)
+  const int ushift = 31 - __clz(caps.chunk_entries > 0 ? caps.chunk_entries : kChunkEntries);
+  const int umask = (1 << ushift) - 1;
   // pass 1: per-wave totals, log2-length buckets, longest list
   int sc = 0, sk = 0, se = 0, mx = 0;
   for (int64_t i = i0 + lane; i < i1; i += 64) {
     const int v = cnt[i];
     sc += v;
-    sk += (v + kChunkEntries - 1) / kChunkEntries;
-    se += v == 0;
+    sk += (v + umask) >> ushift;
+    se += v <= 0;   // (never negative: a corrupted count must not index past the visit order)
     mx = max(mx, v);
     if (v > 0) atomicAdd(&s_bucket[31 - __clz(v)], 1);
   }
@@ -176,6 +180,15 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(int32_t* __restrict__
     stats->n_busy = n_busy;
     stats->n_chunks = tk;
     stats->n_active = 0;
+    // bounded call: the caller sized the intersection / chunk buffers without reading I back
+    int ovf = 0;
+    if (caps.isect > 0 && (int64_t)tc > caps.isect) ovf |= GSR_OVF_ISECT;
+    if (caps.chunks > 0 && (int64_t)tk > caps.chunks) ovf |= GSR_OVF_CHUNKS;
+    stats->isect_cap = caps.isect;
+    stats->chunk_cap = caps.chunks;
+    stats->overflow = ovf;
+    stats->status = caps.status;
+    stats->chunk_entries = 1 << ushift;
   }
   __syncthreads();
   // pass 2: 64-tile rounds per wave
@@ -185,9 +198,9 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(int32_t* __restrict__
     const int64_t i = base + lane;
     const bool in = i < i1;
     const int v = in ? cnt[i] : 0;
-    const int kc = (v + kChunkEntries - 1) / kChunkEntries;
+    const int kc = (v + umask) >> ushift;
     const int iv = wave_incl_scan(v), ik = wave_incl_scan(kc);
-    const unsigned long long empty = __ballot(in && v == 0);
+    const unsigned long long empty = __ballot(in && v <= 0);
     if (in) {
       tile_offset[i] = cc + iv - v;
       chunk_base[i] = ck + ik - kc;
@@ -207,6 +220,20 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(int32_t* __restrict__
 }
 
 // ---------------------------------------------------------------- emission
+// Overflow bits set by the tile scan (stable while any later kernel of the call runs, so a
+// workgroup's threads all read the same value); the sort kernels add GSR_OVF_BUSY / SEG / LAZY,
+// which only the raster and projection backward (later launches) act on.
+constexpr int kOvfCapacity = GSR_OVF_ISECT | GSR_OVF_CHUNKS;
+
+// A bounded call over its caps emits nothing; the projection left its per-tile counts in
+// tile_count, which the NEXT call's projection relies on finding zero: workgroup x = 0 of each
+// camera clears that camera's counts.
+__device__ __forceinline__ void emit_skip_counts(int32_t* __restrict__ tile_count, int T) {
+  if (blockIdx.x != 0) return;
+  int32_t* g = tile_count + (int64_t)blockIdx.y * T;
+  for (int t = threadIdx.x; t < T; t += blockDim.x) g[t] = 0;
+}
+
 __global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__ depth, const uint2* __restrict__ rect,
                                                       const int32_t* __restrict__ isect_offset, int64_t N, int tw,
                                                       int th, int order, int use_lds,
@@ -214,6 +241,10 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__
                                                       int32_t* __restrict__ tile_count, uint64_t* __restrict__ keys,
                                                       int32_t* __restrict__ k_of_slot, int per_block,
                                                       const gsr_bin_stats* __restrict__ stats, int64_t cap) {
+  if (stats->overflow & kOvfCapacity) {   // bounded call over its caps: nothing is emitted
+    emit_skip_counts(tile_count, tw * th);
+    return;
+  }
   // launched before the host has read I back (gsr_bin_emit): a workspace too small for this
   // call's I makes every workgroup leave at once, and the host emits again with a larger one
   if (stats->n_isect > cap) return;
@@ -282,8 +313,14 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__
 // config 4): index-order (2D) emission takes 1024 per workgroup (GPT = 1).
 constexpr int kStageThreads = 1024;
 constexpr int kStageCap = 6144;          // staged entries (16 B each)
-constexpr int kStageMaxTiles = 8192;     // cursor + offset per tile, 8 B each
 constexpr size_t kStageLds = (size_t)kStageCap * 16;
+// cursor + offset per tile (8 B each) in what is left of the 160 KB of LDS after the stage and
+// the kernel's static LDS (s_tmp: 17 ints; 256 B reserved) -- 8 160 tiles, so e.g. a 2048x1024
+// view (8 192 tiles) takes the direct scatter instead of failing to launch
+constexpr int kLdsBytes = 160 * 1024;
+constexpr int kStageStaticLds = 256;
+constexpr int kStageMaxTiles = (int)((kLdsBytes - kStageLds - kStageStaticLds) / 8);
+static_assert(kStageMaxTiles >= 4096, "staged emission needs room for a 4096-tile camera");
 
 template <int GPT>
 __global__ __launch_bounds__(kStageThreads) void k_emit_staged(
@@ -291,6 +328,10 @@ __global__ __launch_bounds__(kStageThreads) void k_emit_staged(
     int64_t N, int tw, int th, int order, const int32_t* __restrict__ tile_offset, int32_t* __restrict__ tile_count,
     uint64_t* __restrict__ keys, int32_t* __restrict__ k_of_slot, const gsr_bin_stats* __restrict__ stats,
     int64_t cap) {
+  if (stats->overflow & kOvfCapacity) {   // see k_emit
+    emit_skip_counts(tile_count, tw * th);
+    return;
+  }
   if (stats->n_isect > cap) return;   // see k_emit
   constexpr int NT = kStageThreads;
   constexpr int kStagePer = GPT * NT;   // Gaussians per workgroup
@@ -603,14 +644,22 @@ __global__ __launch_bounds__(NT) void k_segsort(
     uint64_t* __restrict__ keys, uint64_t* __restrict__ tmpk, int32_t* __restrict__ tmpp0,
     int32_t* __restrict__ tmpp1, const int32_t* __restrict__ tile_offset, const int32_t* __restrict__ busy,
     const int32_t* __restrict__ k_of_slot, int lds_keys, int32_t* __restrict__ sorted_ids,
-    int32_t* __restrict__ k_of_s, const LazyArgs lz) {
+    int32_t* __restrict__ k_of_s, const LazyArgs lz, gsr_bin_stats* __restrict__ stats) {
   extern __shared__ uint64_t s_keys[];
   int* s_hist = (int*)(s_keys + lds_keys);
+  if (stats->overflow & kOvfCapacity) return;   // bounded call over its caps: nothing to sort
   int ct;
+  // the grid covers gridDim.x lists (the busy count read back, or a bound): more lists than
+  // that is flagged for the raster (which then writes NaN) instead of leaving lists unsorted
   if (lz.mode == 2) {   // the tiles whose forward ran past their sorted prefix
-    if ((int)blockIdx.x >= *lz.count) return;
+    const int cnt = *lz.count;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && cnt > (int)gridDim.x) atomicOr(&stats->overflow, GSR_OVF_LAZY);
+    if ((int)blockIdx.x >= cnt) return;
     ct = lz.list[blockIdx.x];
   } else {
+    const int nb = stats->n_busy;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && nb > (int)gridDim.x) atomicOr(&stats->overflow, GSR_OVF_BUSY);
+    if ((int)blockIdx.x >= nb) return;
     ct = busy[blockIdx.x];
   }
   const int start = tile_offset[ct];
@@ -785,22 +834,30 @@ __global__ __launch_bounds__(NT) void k_segsort(
 #endif
 constexpr int kSplitBlock = GSR_SPLIT_BLOCK;
 constexpr int kSplitThreads = 256;
+static_assert(kSplitBlock <= 16 * kSplitThreads, "lds_radix_sort<256> sorts at most 4096 keys");
 #ifndef GSR_SPLIT_MAX_BUSY
 #define GSR_SPLIT_MAX_BUSY 128
 #endif
 constexpr int kSplitMaxBusy = GSR_SPLIT_MAX_BUSY;
-constexpr int kSplitRankThreads = 1024;   // two keys per thread: the binary searches are serial LDS round trips
+constexpr int kSplitRankThreads = 1024;   // one key per thread (1024-key blocks): the binary searches are serial LDS round trips
 
 __global__ __launch_bounds__(kSplitThreads) void k_split_blocksort(
     const uint64_t* __restrict__ keys, uint64_t* __restrict__ tmpk, int32_t* __restrict__ tmpp,
     const int32_t* __restrict__ tile_offset, const int32_t* __restrict__ busy, const int32_t* __restrict__ k_of_slot,
-    int nb_max, int32_t* __restrict__ sorted_ids, int32_t* __restrict__ k_of_s) {
+    int nb_max, int32_t* __restrict__ sorted_ids, int32_t* __restrict__ k_of_s, gsr_bin_stats* __restrict__ stats) {
   __shared__ uint64_t s_keys[kSplitBlock];
   __shared__ int s_hist[(kSplitThreads / 64) * 256 + 64];
+  if (stats->overflow & kOvfCapacity) return;
   const int u = blockIdx.x / nb_max, j = blockIdx.x - u * nb_max;
+  const int nb = stats->n_busy;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (int64_t)nb * nb_max > (int64_t)gridDim.x)
+    atomicOr(&stats->overflow, GSR_OVF_BUSY);
+  if (u >= nb) return;
   const int ct = busy[u];
   const int start = tile_offset[ct];
   const int len = tile_offset[ct + 1] - start;
+  // the grid gives each list nb_max blocks: a longer list is flagged, not half sorted
+  if (j == 0 && threadIdx.x == 0 && len > nb_max * kSplitBlock) atomicOr(&stats->overflow, GSR_OVF_SEG);
   const int b0 = j * kSplitBlock;
   if (b0 >= len) return;
   const int n = min(kSplitBlock, len - b0);
@@ -822,14 +879,17 @@ __global__ __launch_bounds__(kSplitThreads) void k_split_blocksort(
 __global__ __launch_bounds__(kSplitRankThreads) void k_split_rank(
     const uint64_t* __restrict__ tmpk, const int32_t* __restrict__ tmpp, const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ busy, const int32_t* __restrict__ k_of_slot, int nb_max,
-    int32_t* __restrict__ sorted_ids, int32_t* __restrict__ k_of_s) {
-  extern __shared__ uint64_t s_all[];   // the list's sorted blocks
+    int32_t* __restrict__ sorted_ids, int32_t* __restrict__ k_of_s, const gsr_bin_stats* __restrict__ stats) {
+  extern __shared__ uint64_t s_all[];   // the list's sorted blocks (nb_max * kSplitBlock keys)
+  if (stats->overflow & kOvfCapacity) return;
   const int u = blockIdx.x / nb_max, j = blockIdx.x - u * nb_max;
+  if (u >= stats->n_busy) return;
   const int ct = busy[u];
   const int start = tile_offset[ct];
   const int len = tile_offset[ct + 1] - start;
   const int nb = (len + kSplitBlock - 1) / kSplitBlock;
-  if (nb <= 1 || j >= nb) return;
+  // (a list longer than the LDS image was flagged GSR_OVF_SEG by k_split_blocksort)
+  if (nb <= 1 || j >= nb || nb > nb_max) return;
   copy_keys<kSplitRankThreads>(s_all, tmpk + start, len);
   __syncthreads();
   const int b0 = j * kSplitBlock;
@@ -880,13 +940,22 @@ using namespace gsr;
 
 extern "C" {
 
+int gsr_abi_version(void) { return GSR_ABI_VERSION; }
+
 int gsr_bin_offsets(int32_t* tile_count, int64_t CT, int32_t* tile_offset, int32_t* chunk_base,
-                    int32_t* busy_tiles, int32_t* tile_end, uint64_t* tile_cut, gsr_bin_stats* stats,
-                    void* stream) {
+                    int32_t* busy_tiles, int32_t* tile_end, uint64_t* tile_cut, const gsr_bin_caps* caps,
+                    gsr_bin_stats* stats, void* stream) {
   GSR_REQUIRE(CT >= 1 && CT < (1ll << 31), "gsr_bin_offsets: bad CT=%lld", (long long)CT);
+  gsr_bin_caps cp{0, 0, nullptr, 0, 0};
+  if (caps != nullptr) cp = *caps;
+  GSR_REQUIRE(cp.isect >= 0 && cp.isect < (1ll << 31) && cp.chunks >= 0 && cp.chunks < (1ll << 31),
+              "gsr_bin_offsets: bad caps (I %lld, chunks %lld)", (long long)cp.isect, (long long)cp.chunks);
+  const int ce = cp.chunk_entries;
+  GSR_REQUIRE(ce == 0 || (ce >= kChunkEntries && ce <= (1 << 20) && (ce & (ce - 1)) == 0),
+              "gsr_bin_offsets: chunk_entries %d is not 0 or a power of two in [%d, 2^20]", ce, kChunkEntries);
   const size_t lds = CT <= kScanLdsTiles ? (size_t)CT * sizeof(int) : 0;
   hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kTopThreads), lds, (hipStream_t)stream, tile_count, CT, tile_offset,
-                     chunk_base, busy_tiles, tile_end, tile_cut, stats);
+                     chunk_base, busy_tiles, tile_end, tile_cut, cp, stats);
   GSR_LAUNCH_CHECK("k_tile_scan");
   return GSR_OK;
 }
@@ -962,7 +1031,7 @@ int gsr_bin_emit(const float* depth, const uint32_t* rect, const int32_t* isect_
 
 static int bin_sort_impl(const char* who, const float* depth, const uint32_t* rect, const int32_t* isect_offset, const int32_t* tile_offset,
                  int32_t* tile_count, const int32_t* busy_tiles, int C, int64_t N, int width, int height, int order, int64_t n_isect,
-                 int32_t max_seg, int32_t n_busy, int32_t n_big, int32_t n_mid, int emitted, const gsr_bin_stats* stats,
+                 int32_t max_seg, int32_t n_busy, int32_t n_big, int32_t n_mid, int emitted, gsr_bin_stats* stats,
                  void* workspace, size_t workspace_bytes, int32_t* sorted_ids, int32_t* k_of_s, const LazyArgs& lz, void* stream) {
   GSR_REQUIRE(order == GSR_ORDER_DEPTH || order == GSR_ORDER_INDEX, "%s: bad order %d", who, order);
   GSR_REQUIRE(n_isect >= 0 && n_isect < (1ll << 31), "%s: I=%lld out of range", who, (long long)n_isect);
@@ -991,10 +1060,11 @@ static int bin_sort_impl(const char* who, const float* depth, const uint32_t* re
       max_seg <= kSortLdsKeys) {
     const int nb_max = (max_seg + kSplitBlock - 1) / kSplitBlock;
     hipLaunchKernelGGL(k_split_blocksort, dim3(n_busy * nb_max), dim3(kSplitThreads), 0, s, keys, tmpk, tmpp0,
-                       tile_offset, busy_tiles, k_of_slot, nb_max, sorted_ids, k_of_s);
+                       tile_offset, busy_tiles, k_of_slot, nb_max, sorted_ids, k_of_s, stats);
     GSR_LAUNCH_CHECK("k_split_blocksort");
-    hipLaunchKernelGGL(k_split_rank, dim3(n_busy * nb_max), dim3(kSplitRankThreads), (size_t)max_seg * sizeof(uint64_t), s,
-                       tmpk, tmpp0, tile_offset, busy_tiles, k_of_slot, nb_max, sorted_ids, k_of_s);
+    hipLaunchKernelGGL(k_split_rank, dim3(n_busy * nb_max), dim3(kSplitRankThreads),
+                       (size_t)nb_max * kSplitBlock * sizeof(uint64_t), s, tmpk, tmpp0, tile_offset, busy_tiles,
+                       k_of_slot, nb_max, sorted_ids, k_of_s, stats);
     GSR_LAUNCH_CHECK("k_split_rank");
     return GSR_OK;
   }
@@ -1006,11 +1076,11 @@ static int bin_sort_impl(const char* who, const float* depth, const uint32_t* re
     lds_keys = min(lds_keys, kSortLdsKeys);
     hipLaunchKernelGGL(k_segsort<kSortThreads>, dim3(n_busy), dim3(kSortThreads),
                        lds_keys * sizeof(uint64_t) + hist_bytes(kSortThreads), s, keys, tmpk, tmpp0, tmpp1,
-                       tile_offset, busy_tiles, k_of_slot, lds_keys, sorted_ids, k_of_s, lz);
+                       tile_offset, busy_tiles, k_of_slot, lds_keys, sorted_ids, k_of_s, lz, stats);
   } else if (n_busy > 0) {
     hipLaunchKernelGGL(k_segsort<kSortThreadsSmall>, dim3(n_busy), dim3(kSortThreadsSmall),
                        kSortSmallKeys * sizeof(uint64_t) + hist_bytes(kSortThreadsSmall), s, keys, tmpk, tmpp0,
-                       tmpp1, tile_offset, busy_tiles, k_of_slot, kSortSmallKeys, sorted_ids, k_of_s, lz);
+                       tmpp1, tile_offset, busy_tiles, k_of_slot, kSortSmallKeys, sorted_ids, k_of_s, lz, stats);
   }
   GSR_LAUNCH_CHECK(who);
   return GSR_OK;
@@ -1018,7 +1088,7 @@ static int bin_sort_impl(const char* who, const float* depth, const uint32_t* re
 
 int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_offset, const int32_t* tile_offset,
                  int32_t* tile_count, const int32_t* busy_tiles, int C, int64_t N, int width, int height, int order, int64_t n_isect,
-                 int32_t max_seg, int32_t n_busy, int32_t n_big, int32_t n_mid, int emitted, const gsr_bin_stats* stats,
+                 int32_t max_seg, int32_t n_busy, int32_t n_big, int32_t n_mid, int emitted, gsr_bin_stats* stats,
                  void* workspace, size_t workspace_bytes, int32_t* sorted_ids, int32_t* k_of_s, void* stream) {
   const LazyArgs off{};
   return bin_sort_impl("gsr_bin_sort", depth, rect, isect_offset, tile_offset, tile_count, busy_tiles, C, N, width,
@@ -1050,7 +1120,7 @@ int gsr_set_emit_staged(int on) {
 int gsr_bin_sort_lazy(const float* depth, const uint32_t* rect, const int32_t* isect_offset,
                       const int32_t* tile_offset, int32_t* tile_count, const int32_t* busy_tiles, int C, int64_t N,
                       int width, int height, int64_t n_isect, int32_t max_seg, int32_t n_busy, int32_t n_big,
-                      int32_t n_mid, int emitted, const gsr_bin_stats* stats, void* workspace,
+                      int32_t n_mid, int emitted, gsr_bin_stats* stats, void* workspace,
                       size_t workspace_bytes, int32_t* sorted_ids, int32_t* k_of_s, int32_t* lazy, void* stream) {
   GSR_REQUIRE(lazy != nullptr, "gsr_bin_sort_lazy: no lazy workspace");
   const int64_t CT = (int64_t)C * ceil_div(width, kTile) * ceil_div(height, kTile);
@@ -1079,7 +1149,7 @@ namespace gsr {
 // whole (one workgroup per grid slot, slots past the device-side count leave at once).
 int bin_sort_rest(const int32_t* tile_offset, int64_t CT, int32_t max_seg, int32_t n_max, void* workspace,
                   size_t workspace_bytes, int32_t* lazy, int32_t* tile_end, int32_t* sorted_ids, int32_t* k_of_s,
-                  hipStream_t s) {
+                  gsr_bin_stats* stats, hipStream_t s) {
   if (n_max <= 0) return GSR_OK;
   const SortWs w = sort_ws(workspace, ws_cap(workspace_bytes));
   const LazyArgs lz{lazy, lazy + CT, lazy + 2 * CT, lazy + 3 * CT, tile_end, 1 << 30, 1, 2};
@@ -1089,7 +1159,7 @@ int bin_sort_rest(const int32_t* tile_offset, int64_t CT, int32_t max_seg, int32
   const size_t hist = (size_t)((kSortThreads / 64) * 256 + 64) * sizeof(int);
   hipLaunchKernelGGL(k_segsort<kSortThreads>, dim3(n_max), dim3(kSortThreads), lds_keys * sizeof(uint64_t) + hist, s,
                      w.keys, w.tmpk, w.tmpp0, w.tmpp1, tile_offset, (const int32_t*)nullptr, w.k_of_slot, lds_keys,
-                     sorted_ids, k_of_s, lz);
+                     sorted_ids, k_of_s, lz, stats);
   GSR_LAUNCH_CHECK("k_segsort (lazy rest)");
   return GSR_OK;
 }

@@ -213,6 +213,6 @@ __device__ __forceinline__ uint32_t pack_rect_lo(int a, int b) {
 // binning.hip: the lazy path's second sort (every tile flagged by the forward, sorted whole)
 int bin_sort_rest(const int32_t* tile_offset, int64_t CT, int32_t max_seg, int32_t n_max, void* workspace,
                   size_t workspace_bytes, int32_t* lazy, int32_t* tile_end, int32_t* sorted_ids, int32_t* k_of_s,
-                  hipStream_t s);
+                  gsr_bin_stats* stats, hipStream_t s);
 
 }  // namespace gsr

@@ -4,6 +4,7 @@
 // that its tile histogram fits in LDS (tiles of one camera).  The histogram is flushed with
 // one coalesced no-return atomic per non-empty tile per workgroup (MI355X float/int atomics
 // execute at the memory side — scattered per-entry atomics would be ~17x slower).
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 
@@ -44,6 +45,22 @@ __device__ __forceinline__ void hist_flush(int* hist, int32_t* gcount, int T) {
     const int v = hist[t];
     if (v) atomicAdd(&gcount[t], v);
   }
+}
+
+// Zero the tile histogram + emission counter.  (A kernel rather than hipMemsetAsync: a memset
+// node captured into a HIP graph left garbage in this buffer on every replay after the first
+// on ROCm 7.2 -- tools/diag_graph3.py -- while a kernel node replays correctly.)
+__global__ void k_zero_i32(int32_t* __restrict__ p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = 0;
+}
+
+static int zero_counts(int32_t* p, int64_t n, hipStream_t s) {
+  const int threads = 256;
+  const int blocks = (int)std::min<int64_t>((n + threads - 1) / threads, 1024);
+  hipLaunchKernelGGL(k_zero_i32, dim3(blocks), dim3(threads), 0, s, p, n);
+  GSR_LAUNCH_CHECK("k_zero_i32");
+  return GSR_OK;
 }
 
 // Emission offsets without a separate scan pass: the workgroup's (c,n) items [cn0, cn0+m)
@@ -272,9 +289,9 @@ int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride, const 
               "gsr3d_project_fwd: bad band [%d,%d) of %d x %d tile rows", band_y0, band_y1, C, th);
   // tile histogram [C*T] and the emission counter (element C*T) in one memset, unless the
   // caller's buffer is already zero (left so by the previous offsets + sort on it)
-  if (!tile_count_zeroed && hipMemsetAsync(tile_count, 0, ((size_t)C * tw * th + 1) * sizeof(int32_t), (hipStream_t)stream) != hipSuccess) {
-    set_error("gsr3d_project_fwd: tile_count memset failed");
-    return GSR_ELAUNCH;
+  if (!tile_count_zeroed) {
+    const int rc = zero_counts(tile_count, (int64_t)C * tw * th + 1, (hipStream_t)stream);
+    if (rc != GSR_OK) return rc;
   }
   if (N == 0) return GSR_OK;
   const int T = tw * th;
@@ -311,10 +328,9 @@ int gsr2d_project_fwd(const float* params, int64_t N, int64_t row_stride, int64_
   GSR_REQUIRE(eps_cut > 0.f && eps_cut < 1.f, "gsr2d_project_fwd: eps_cut must be in (0,1)");
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   GSR_REQUIRE(tw < 65536 && th < 65536, "gsr2d_project_fwd: image too large");
-  if (!tile_count_zeroed &&
-      hipMemsetAsync(tile_count, 0, ((size_t)C * tw * th + 1) * sizeof(int32_t), (hipStream_t)stream) != hipSuccess) {
-    set_error("gsr2d_project_fwd: tile_count memset failed");
-    return GSR_ELAUNCH;
+  if (!tile_count_zeroed) {
+    const int rc = zero_counts(tile_count, (int64_t)C * tw * th + 1, (hipStream_t)stream);
+    if (rc != GSR_OK) return rc;
   }
   if (N == 0) return GSR_OK;
   const int T = tw * th;

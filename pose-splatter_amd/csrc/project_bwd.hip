@@ -75,12 +75,18 @@ __global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
     const uint2* __restrict__ rect,
     const int32_t* __restrict__ isect_offset, const int32_t* __restrict__ isect_count,
     const float* __restrict__ depth, const uint64_t* __restrict__ tile_cut, const float* __restrict__ partial,
-    int CPB, int G, int64_t n_begin, int64_t n_end, float* __restrict__ v_params) {
+    int CPB, int G, int64_t n_begin, int64_t n_end, const gsr_bin_stats* __restrict__ stats,
+    float* __restrict__ v_params) {
   __shared__ float s_con[kBwdThreads][kContrib + 1];
   __shared__ int s_any[kBwdThreads];
   const int g_loc = threadIdx.x % G;
   const int slot = threadIdx.x / G;
   const int64_t n = n_begin + (int64_t)blockIdx.x * G + g_loc;
+  if (stats != nullptr && stats->overflow) {   // the forward's bounds did not hold: NaN rows
+    if (slot == 0 && n < n_end)
+      for (int k = 0; k < 14; ++k) v_params[n * 14 + k] = __builtin_nanf("");
+    return;
+  }
   const bool active = slot < CPB && n < n_end;
   const int T = tw * th;
   float v_m[3] = {0.f, 0.f, 0.f};
@@ -320,12 +326,18 @@ __global__ __launch_bounds__(kBwdThreads) void k_project2d_bwd_staged(
     const float* __restrict__ params, int64_t N, int64_t stride, int64_t set_stride,
     const int32_t* __restrict__ set_begin, int F, int n_cam, int tw, int th, const uint2* __restrict__ rect,
     const int32_t* __restrict__ isect_offset, const int32_t* __restrict__ isect_count,
-    const uint64_t* __restrict__ tile_cut, const float* __restrict__ partial, float* __restrict__ v_params) {
+    const uint64_t* __restrict__ tile_cut, const float* __restrict__ partial, const gsr_bin_stats* __restrict__ stats,
+    float* __restrict__ v_params) {
   __shared__ float4 s_rows[3 * kStageRows];
   __shared__ int s_lo, s_hi;
   const int f = blockIdx.y;
   const int64_t n = (int64_t)blockIdx.x * kBwdThreads + threadIdx.x;
   const bool own = n < N;
+  if (stats != nullptr && stats->overflow) {   // the forward's bounds did not hold: NaN rows
+    if (own)
+      for (int k = 0; k < 9; ++k) v_params[((int64_t)f * N + n) * 9 + k] = __builtin_nanf("");
+    return;
+  }
   const int c0 = set_begin ? set_begin[f] : 0, c1 = set_begin ? set_begin[f + 1] : n_cam;
   const float4* rows4 = reinterpret_cast<const float4*>(partial);
   static_assert(kPartialStride == 12, "a partial row is 3 float4");
@@ -415,7 +427,8 @@ int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride, const 
                       int C, int width, int height, float eps2d, int input_mode, const float* depth,
                       const uint32_t* rect,
                       const int32_t* isect_offset, const int32_t* isect_count, const uint64_t* tile_cut,
-                      const float* partial, int64_t n_begin, int64_t n_end, float* v_params, void* stream) {
+                      const float* partial, int64_t n_begin, int64_t n_end, const gsr_bin_stats* stats,
+                      float* v_params, void* stream) {
   GSR_REQUIRE(N >= 0 && C >= 1 && width > 0 && height > 0, "gsr3d_project_bwd: bad arguments");
   GSR_REQUIRE(row_stride >= 14, "gsr3d_project_bwd: row_stride < 14");
   GSR_REQUIRE(input_mode == GSR_INPUT_ADAPTER || input_mode == GSR_INPUT_GSPLAT,
@@ -429,7 +442,7 @@ int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride, const 
   const int G = kBwdThreads / CPB;                       // Gaussians per workgroup
   hipLaunchKernelGGL(k_project3d_bwd, dim3(ceil_div(n_end - n_begin, G)), dim3(kBwdThreads), 0, (hipStream_t)stream, params, N,
                      row_stride, viewmats, Ks, C, width, height, eps2d, input_mode, tw, th, (const uint2*)rect,
-                     isect_offset, isect_count, depth, tile_cut, partial, CPB, G, n_begin, n_end, v_params);
+                     isect_offset, isect_count, depth, tile_cut, partial, CPB, G, n_begin, n_end, stats, v_params);
   GSR_LAUNCH_CHECK("k_project3d_bwd");
   return GSR_OK;
 }
@@ -437,7 +450,8 @@ int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride, const 
 int gsr2d_project_bwd(const float* params, int64_t N, int64_t row_stride, int64_t set_stride,
                       const int32_t* set_begin, int F, int C, int width, int height,
                       const uint32_t* rect, const int32_t* isect_offset, const int32_t* isect_count,
-                      const uint64_t* tile_cut, const float* partial, float* v_params, void* stream) {
+                      const uint64_t* tile_cut, const float* partial, const gsr_bin_stats* stats, float* v_params,
+                      void* stream) {
   GSR_REQUIRE(N >= 0 && width > 0 && height > 0, "gsr2d_project_bwd: bad arguments");
   GSR_REQUIRE(C >= 1 && F >= 1 && (set_begin != nullptr || F == 1), "gsr2d_project_bwd: bad C=%d / F=%d", C, F);
   GSR_REQUIRE(row_stride >= 9, "gsr2d_project_bwd: row_stride < 9");
@@ -447,7 +461,7 @@ int gsr2d_project_bwd(const float* params, int64_t N, int64_t row_stride, int64_
   GSR_REQUIRE(F <= 65535, "gsr2d_project_bwd: F=%d > 65535 parameter sets", F);
   hipLaunchKernelGGL(k_project2d_bwd_staged, dim3(ceil_div(N, kBwdThreads), F), dim3(kBwdThreads), 0,
                      (hipStream_t)stream, params, N, row_stride, set_stride, set_begin, F, C, tw, th,
-                     (const uint2*)rect, isect_offset, isect_count, tile_cut, partial, v_params);
+                     (const uint2*)rect, isect_offset, isect_count, tile_cut, partial, stats, v_params);
   GSR_LAUNCH_CHECK("k_project2d_bwd_staged");
   return GSR_OK;
 }

@@ -134,6 +134,25 @@ __device__ void fill_empty(const int32_t* __restrict__ order, const int32_t* __r
   }
 }
 
+// A bounded call whose bounds did not hold (stats->overflow): every pixel of the call gets NaN
+// rgb / alpha (tile-strided over the whole grid), so the failure cannot pass as a render.
+__device__ void nan_fill(int64_t CT, int W, int H, int tw, int th, float* __restrict__ out_rgb,
+                         float* __restrict__ out_alpha) {
+  const float nan = __builtin_nanf("");
+  for (int64_t t = blockIdx.x; t < CT; t += gridDim.x) {
+    int c, ty, tx;
+    tile_coords((int)t, tw, th, c, ty, tx);
+    const int i = ty * kTile + (threadIdx.x >> 4), j = tx * kTile + (threadIdx.x & 15);
+    if (i < H && j < W) {
+      const int64_t pix = ((int64_t)c * H + i) * W + j;
+      out_rgb[pix * 3 + 0] = nan;
+      out_rgb[pix * 3 + 1] = nan;
+      out_rgb[pix * 3 + 2] = nan;
+      out_alpha[pix] = nan;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- 3D forward
 // Work unit: a 4x4-pixel sub-tile per wave, FOUR lanes per pixel, 4 workgroups of 4 waves per
 // tile (one per 8x8 quadrant).  3D: the quadrant's waves share 256-entry rounds -- each entry
@@ -304,19 +323,28 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
     int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end, float4* __restrict__ ckpt,
     const int32_t* __restrict__ chunk_base, int n_busy, int64_t CT,
-    uint64_t* __restrict__ tile_cut, float cut2d, const FwdLazy lz) {
+    uint64_t* __restrict__ tile_cut, float cut2d, const FwdLazy lz, const gsr_bin_stats* __restrict__ stats) {
   static_assert(!IS2D || LPP == 4, "2D walks per wave with quads");
   using PG = PixGroup<LPP>;
   using FS = FwdShape<LPP>;
   __shared__ int s_max;
+  // n_busy sizes the grid (the read-back busy count or a bound); the tiles come from the device
+  // count, which the sort has checked against that bound (GSR_OVF_BUSY)
   const int busy_blocks = busy_grid<LPP>(n_busy);
+  if (stats->overflow) {
+    nan_fill(CT, W, H, tw, th, out_rgb, out_alpha);
+    return;
+  }
   if (lz.rerun) {
     order = lz.list;
     n_busy = min(n_busy, *lz.count);
-  } else if ((int)blockIdx.x >= busy_blocks) {
-    fill_empty<IS2D>(order, tile_offset, n_busy, busy_blocks, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
-                     out_last, tile_end, tile_cut);
-    return;
+  } else {
+    n_busy = stats->n_busy;
+    if ((int)blockIdx.x >= busy_blocks) {
+      fill_empty<IS2D>(order, tile_offset, n_busy, busy_blocks, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
+                       out_last, tile_end, tile_cut);
+      return;
+    }
   }
   // XCD-aware mapping: workgroups are dealt to the 8 XCDs round-robin by id, so the G
   // workgroups of a tile get ids 8G*k + 8*sub + x (same id mod 8): they share one XCD's L2
@@ -346,8 +374,10 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   float Tl = 1.f;   // 2D: T before this lane's latest composited entry
   int last = -1;
   bool done = !inside;
-  // chunk records for the chunk-parallel backward (per pixel, per GSR_CHUNK-entry chunk)
+  // chunk records for the chunk-parallel backward (per pixel, per chunk of stats->chunk_entries
+  // list entries, a power-of-two multiple of the 128-entry round half)
   const int cbase = chunk_base[ct];
+  const int umask = stats->chunk_entries - 1;
   int kcur = 0;
   float Ts = 1.f, dr = 0.f, dg = 0.f, db = 0.f;   // dr..: this lane's share of the chunk's colour
   if constexpr (!IS2D) {
@@ -398,7 +428,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     for (int h = 0; h < 2; ++h) {
       const int hb = rb + 128 * h;
       if (hb >= end || __ballot(!done) == 0ull) break;
-      if (hb > start && ((hb - start) % kChunk3) == 0) {   // entering chunk kcur+1
+      if (hb > start && ((hb - start) & umask) == 0) {   // entering chunk kcur+1
         const float Dr = PG::sum(dr), Dg = PG::sum(dg), Db = PG::sum(db);
         if (q == 0) ckpt[(int64_t)(cbase + kcur) * kRasterThreads + bwd_pixel_slot(il, jl)] = make_float4(Ts, Dr, Dg, Db);
         cr += Dr;
@@ -485,7 +515,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   // waits for younger record loads), composite.  false = every pixel of the wave is done.
   auto step = [&](int b0, float4& c0, float4& c1, float4& c2, int id_use, int& id_new) -> bool {
     if (__ballot(!done) == 0ull) return false;
-    if (b0 > start && ((b0 - start) % kChunk3) == 0) {   // entering chunk kcur+1
+    if (b0 > start && ((b0 - start) & umask) == 0) {   // entering chunk kcur+1
       const float Dr = quad_sum(dr), Dg = quad_sum(dg), Db = quad_sum(db);
       if (q == 0) ckpt[(int64_t)(cbase + kcur) * kRasterThreads + bwd_pixel_slot(il, jl)] = make_float4(Ts, Dr, Dg, Db);
       cr += Dr;
@@ -657,20 +687,27 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
     float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
     int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end, float4* __restrict__ ckpt,
     const int32_t* __restrict__ chunk_base, int n_busy, int64_t CT,
-    uint64_t* __restrict__ tile_cut, float cut2d, const FwdLazy lz) {
+    uint64_t* __restrict__ tile_cut, float cut2d, const FwdLazy lz, const gsr_bin_stats* __restrict__ stats) {
   __shared__ float4 s_r[2][3][256];              // round records, part j of slot i at s_r[buf][j][i]
   __shared__ unsigned char s_list[4][128];       // a half's quadrant survivors (slot in the half)
   __shared__ unsigned char s_box[4][4][129];     // ... and each box's, in list order (+1: read-ahead)
   __shared__ int s_max;
   static_assert(kChunk3 == 128, "a round half is one chunk");
-  const int busy_blocks = (n_busy + 7) & ~7;
+  const int busy_blocks = (n_busy + 7) & ~7;   // n_busy: the grid's bound (see k_raster_fwd)
+  if (stats->overflow) {
+    nan_fill(CT, W, H, tw, th, out_rgb, out_alpha);
+    return;
+  }
   if (lz.rerun) {
     order = lz.list;
     n_busy = min(n_busy, *lz.count);
-  } else if ((int)blockIdx.x >= busy_blocks) {
-    fill_empty<IS2D>(order, tile_offset, n_busy, busy_blocks, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
-                     out_last, tile_end, tile_cut);
-    return;
+  } else {
+    n_busy = stats->n_busy;
+    if ((int)blockIdx.x >= busy_blocks) {
+      fill_empty<IS2D>(order, tile_offset, n_busy, busy_blocks, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
+                       out_last, tile_end, tile_cut);
+      return;
+    }
   }
   if ((int)blockIdx.x >= n_busy) return;
   const int ct = order[blockIdx.x];
@@ -692,6 +729,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
   int last = -1;
   bool done = !inside;
   const int cbase = chunk_base[ct];
+  const int umask = stats->chunk_entries - 1;   // chunk = a power-of-two multiple of 128 entries
   int kcur = 0;
   float Ts = 1.f, dr = 0.f, dg = 0.f, db = 0.f;   // the current chunk's start T and colour
   const int e_last = max(end - 1, start);
@@ -721,7 +759,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
     for (int h = 0; h < 2; ++h) {
       const int hb = rb + 128 * h;
       if (hb >= end || __ballot(!done) == 0ull) break;
-      if (hb > start) {   // entering chunk kcur+1 (halves are chunks)
+      if (hb > start && ((hb - start) & umask) == 0) {   // entering chunk kcur+1 (every few halves)
         ckpt[(int64_t)(cbase + kcur) * kRasterThreads + threadIdx.x] = make_float4(Ts, dr, dg, db);
         cr += dr;
         cg += dg;
@@ -907,9 +945,15 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_finalize(
     const int32_t* __restrict__ order, int n_busy, const int32_t* __restrict__ chunk_base,
     int32_t* __restrict__ tile_end, uint64_t* __restrict__ tile_cut, gsr_bin_stats* __restrict__ stats,
     int32_t* __restrict__ chunk_list, int key_order) {
+  const int ovf = stats->overflow;
+  if (ovf) {   // bounded call over its bounds: report to the caller's sticky status, nothing else
+    if (blockIdx.x == 0 && threadIdx.x == 0 && stats->status != nullptr) atomicOr(stats->status, ovf);
+    return;
+  }
+  (void)n_busy;   // the grid's bound; the tiles are the device count's
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
-  const bool in = b < n_busy;
+  const bool in = b < stats->n_busy;
   const int ct = in ? order[b] : 0;
   int start = 0, end = 0, te = 0;
   if (in) {
@@ -920,7 +964,8 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_finalize(
     tile_end[ct] = te;
     tile_cut[ct] = te < end ? sort_key(depth, ids[te], key_order) : ~0ull;
   }
-  const int nact = (te - start + kChunk3 - 1) / kChunk3;
+  const int U = stats->chunk_entries;
+  const int nact = (te - start + U - 1) / U;
   // one atomic per wave on the active-chunk counter (one per tile serialised ~700 atomics on
   // one address at config 3)
   int incl = nact;
@@ -937,8 +982,8 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_finalize(
     const int cbase = chunk_base[ct];
     int4* desc = reinterpret_cast<int4*>(chunk_list);
     for (int k = 0; k < nact; ++k) {
-      const int b0 = start + k * kChunk3;
-      desc[pos + k] = make_int4(b0, min(kChunk3, te - b0), cbase + k, ct);
+      const int b0 = start + k * U;
+      desc[pos + k] = make_int4(b0, min(U, te - b0), cbase + k, ct);
     }
   }
 }
@@ -1017,7 +1062,7 @@ __device__ __forceinline__ void loss_cotangent(const gsr_loss_terms& lt, int C, 
 // T_i = T_{i+1} / (1 - a_i) as in 3D, except at the pixel's last entry, whose T comes from
 // the forward (final_T .y) -- the one entry whose 1 - a may be exactly 0.  No clamp: every
 // valid pair feeds the sigma / opacity gradients.
-template <bool LOSS, bool IS2D>
+template <bool LOSS, bool IS2D, bool MULTI>
 __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ tile_end, const int32_t* __restrict__ chunk_base,
@@ -1041,7 +1086,13 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
   // the chunk's descriptor {first entry, entries (>= 1), chunk record row, tile} -- one load
   // (read before the bound check: the list has a slot for every grid slot)
   const int4 cd = reinterpret_cast<const int4*>(chunk_list)[blockIdx.x];
-  if ((int)blockIdx.x >= stats->n_active) return;
+  if (stats->overflow || (int)blockIdx.x >= stats->n_active) return;
+  // MULTI = false: units of exactly one sub-chunk (no loop: the loop's back-edge keeps ~40 more
+  // VGPRs live and costs a wave per SIMD); a forward with longer units is flagged, not half done
+  if (!MULTI && stats->chunk_entries != kChunk3) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&stats->overflow, GSR_OVF_UNIT);
+    return;
+  }
   const int b0 = cd.x, n = cd.y, chunk = cd.z, ct = cd.w;
   int c, ty, tx;
   tile_coords(ct, tw, th, c, ty, tx);
@@ -1053,12 +1104,19 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
   const int pi = by0i + (pos >> 2), pj = bx0i + (pos & 3);
   const bool inside = pi < H && pj < W;
   const float px = (float)pj + off, py = (float)pi + off;
+  // A work unit ("chunk", stats->chunk_entries list entries) is walked back to front in
+  // sub-chunks of kChunk3 entries staged in LDS; the pixel's state (T, and the suffix term: Sv
+  // in 3D, mu in 2D) carries from one sub-chunk into the previous one, so the pixel state and
+  // the chunk record are read once per unit.
+  const int nsub = MULTI ? (n + kChunk3 - 1) / kChunk3 : 1;
+  int sb0 = b0 + (nsub - 1) * kChunk3;   // the current sub-chunk [sb0, sb0 + sn)
+  int sn = b0 + n - sb0;
   // Every load is issued up front, none waiting for `last` (the per-WG latency chain is what
-  // bounds this kernel's fixed part): the pixel's state, its chunk record, the chunk's ids and
-  // sort positions; pixels that stopped before this chunk then drop them by select.
+  // bounds this kernel's fixed part): the pixel's state, its chunk record, the last sub-chunk's
+  // ids and sort positions; pixels that stopped before this unit then drop them by select.
   const float4 rck = ckpt[(int64_t)chunk * kRasterThreads + threadIdx.x];
-  const int id_mine = threadIdx.x < n ? ids[b0 + threadIdx.x] : 0;
-  const int kos_mine = threadIdx.x < n ? k_of_s[b0 + threadIdx.x] : 0;
+  int id_mine = threadIdx.x < sn ? ids[sb0 + threadIdx.x] : 0;
+  int kos_mine = threadIdx.x < sn ? k_of_s[sb0 + threadIdx.x] : 0;
   float Tf = 1.f, Tl = 1.f, vr = 0.f, vg = 0.f, vb = 0.f, va = 0.f;
   int last = -1;
   if (inside) {
@@ -1085,7 +1143,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
     Tf = Tl = 1.f;
     vr = vg = vb = va = 0.f;
   }
-  // state at the end of this chunk: {T_end, suffix colour sum} (forward epilogue)
+  // state at the end of this unit: {T_end, suffix colour sum} (forward epilogue)
   const float T0 = live ? rck.x : Tf, Sr = live ? rck.y : 0.f, Sg = live ? rck.z : 0.f, Sb = live ? rck.w : 0.f;
   float T = T0;
   const float* bgc = bg + c * 3;
@@ -1096,155 +1154,172 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
   float mu = 0.f;   // 2D
   if constexpr (IS2D) {
     const float mu_last = bgdot - va;
-    mu = last < b0 + kChunk3 ? mu_last : (Sv + Tf * mu_last) / T;
+    mu = last < b0 + n ? mu_last : (Sv + Tf * mu_last) / T;
   }
   int wlast = last;
-  // the pixel's last entry as a slot of this chunk: lastk for the range test (the pad slot
-  // kNull is past it), lastq for the 2D equality (-1 when the last entry is in a later chunk)
-  const int lastk = min(last - b0, kChunk3 - 1);   // < 0: the pixel stopped before this chunk
-  const int lastq = last - b0 < kChunk3 ? last - b0 : -1;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wlast = max(wlast, __shfl_xor(wlast, o, 64));
-  if (threadIdx.x < n) {
-    const Splat sp = rec[id_mine];
-    s_p[0][threadIdx.x] = sp.p0;
-    s_p[1][threadIdx.x] = sp.p1;
-    s_p[2][threadIdx.x] = sp.p2;
-  }
-  for (int i = threadIdx.x; i < kPartial * 4 * (kChunk3 + 1); i += kRasterThreads) (&L[0][0][0])[i] = 0.f;
-  if (threadIdx.x == 0) {
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    s_p[0][kNull] = z;
-    s_p[1][kNull] = z;
-    s_p[2][kNull] = z;
-  }
-  __syncthreads();
-  // cull the chunk against this wave's 8x8 quadrant; survivors are listed back to front
-  int nsurv = 0;
-  {
-    const float x0 = (float)qx0 + off, y0 = (float)qy0 + off;
-#pragma unroll
-    for (int q = kChunk3 / 64 - 1; q >= 0; --q) {
-      const int k = q * 64 + lane;
-      const bool keep = k < n && (b0 + k) <= wlast &&
-                        cull_keep<IS2D>(s_p[0][k], s_p[1][k], s_p[2][k], x0, x0 + 7.f, y0, y0 + 7.f);
-      const unsigned long long mk = __ballot(keep);
-      if (keep) {
-        const unsigned long long above = lane == 63 ? 0ull : (mk >> (lane + 1));
-        s_list[wv][nsurv + __popcll(above)] = (unsigned char)k;
-      }
-      nsurv += __popcll(mk);
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  // ... and the quadrant's survivors against each 4x4 box: lane l tests survivor s0 + (l>>2)
-  // against box l&3; a box's bits of the ballot keep the list order
-  int nb = 0;   // survivors of this lane's box
-  {
-    const float x0 = (float)bx0i + off, y0 = (float)by0i + off;
-    const unsigned long long boxbits = 0x1111111111111111ull << box;
-    for (int s0 = 0; s0 < nsurv; s0 += 16) {
-      const int s = s0 + pos;
-      const int k = s_list[wv][s < nsurv ? s : 0];
-      const bool keep = s < nsurv && cull_keep<IS2D>(s_p[0][k], s_p[1][k], s_p[2][k], x0, x0 + 3.f, y0, y0 + 3.f);
-      const unsigned long long m = __ballot(keep) & boxbits;
-      if (keep) s_box[wv][box][nb + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned char)k;
-      nb += __popcll(m);
-    }
-  }
-  // groups walked by the wave: max over its boxes (lanes 4k..4k+3 hold the four counts)
-  const int ngrp = __builtin_amdgcn_readfirstlane(quad_max_i(nb));
-  const int npad = (ngrp + kGroup - 1) / kGroup * kGroup;
-  for (int s = nb + pos; s < npad; s += 16) s_box[wv][box][s] = (unsigned char)kNull;
-  __builtin_amdgcn_wave_barrier();
-  // after reduce_box16 lane l holds 4 of its box's sums, flat indices 4*(l>>2) + i = 9*g + q.
-  // They are staged in LDS (one b128 store per group), and lane f < 63 then adds flat index
-  // f = 9g + q of every box, box by box, into the wave's slot L[q][wv][entry]: inside one
-  // instruction the 63 (q, entry) addresses are distinct (a box lists an entry once), and
-  // the boxes follow in program order, so the plain read-add-write is race-free and
-  // deterministic -- no LDS atomics.
+  Splat sp = {};
+  if (threadIdx.x < sn) sp = rec[id_mine];
   const int fg = lane / kPartial, fq = lane - kPartial * (lane / kPartial);
   const bool fown = lane < kGroup * kPartial;
   float* const Lw = &L[fq][wv][0];
   const float* const stage_rd = &s_stage[wv][0][0] + 4 * (4 * (lane >> 2)) + (lane & 3);   // + 4*box
   const unsigned char* my_list = s_box[wv][box];
-  // Branch-free groups of 7 survivors: an invalid (entry, pixel) pair contributes zeros and
-  // leaves T and S unchanged (ra = 1, fac = 0), so every group is straight-line code.
-  for (int g0 = 0; g0 < ngrp; g0 += kGroup) {
-    float acc[64];
-    acc[63] = 0.f;
+  for (int sub = nsub - 1; sub >= 0; --sub) {
+    if (sub != nsub - 1) __syncthreads();   // the previous sub-chunk's LDS is consumed
+    if (threadIdx.x < sn) {
+      s_p[0][threadIdx.x] = sp.p0;
+      s_p[1][threadIdx.x] = sp.p1;
+      s_p[2][threadIdx.x] = sp.p2;
+    }
+    // the next (earlier) sub-chunk's ids and sort positions, in flight during this one's walk
+    int id_next = 0, kos_next = 0;
+    if (sub > 0 && threadIdx.x < kChunk3) {
+      id_next = ids[sb0 - kChunk3 + threadIdx.x];
+      kos_next = k_of_s[sb0 - kChunk3 + threadIdx.x];
+    }
+    for (int i = threadIdx.x; i < kPartial * 4 * (kChunk3 + 1); i += kRasterThreads) (&L[0][0][0])[i] = 0.f;
+    if (threadIdx.x == 0) {
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      s_p[0][kNull] = z;
+      s_p[1][kNull] = z;
+      s_p[2][kNull] = z;
+    }
+    __syncthreads();
+    // the pixel's last entry as a slot of this sub-chunk: lastk for the range test (the pad
+    // slot kNull is past it), lastq for the 2D equality (never a slot when the last entry is
+    // in a later sub-chunk or before this one)
+    const int lastk = min(last - sb0, kChunk3 - 1);   // < 0: the pixel stopped before this sub-chunk
+    const int lastq = last - sb0 < kChunk3 ? last - sb0 : -1;
+    // cull the sub-chunk against this wave's 8x8 quadrant; survivors are listed back to front
+    int nsurv = 0;
+    {
+      const float x0 = (float)qx0 + off, y0 = (float)qy0 + off;
 #pragma unroll
-    for (int g = 0; g < kGroup; ++g) {
-      const int k = my_list[g0 + g];
-      const float4 p0 = s_p[0][k];
+      for (int q = kChunk3 / 64 - 1; q >= 0; --q) {
+        const int k = q * 64 + lane;
+        const bool keep = k < sn && (sb0 + k) <= wlast &&
+                          cull_keep<IS2D>(s_p[0][k], s_p[1][k], s_p[2][k], x0, x0 + 7.f, y0, y0 + 7.f);
+        const unsigned long long mk = __ballot(keep);
+        if (keep) {
+          const unsigned long long above = lane == 63 ? 0ull : (mk >> (lane + 1));
+          s_list[wv][nsurv + __popcll(above)] = (unsigned char)k;
+        }
+        nsurv += __popcll(mk);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ... and the quadrant's survivors against each 4x4 box: lane l tests survivor s0 + (l>>2)
+    // against box l&3; a box's bits of the ballot keep the list order
+    int nb = 0;   // survivors of this lane's box
+    {
+      const float x0 = (float)bx0i + off, y0 = (float)by0i + off;
+      const unsigned long long boxbits = 0x1111111111111111ull << box;
+      for (int s0 = 0; s0 < nsurv; s0 += 16) {
+        const int s = s0 + pos;
+        const int k = s_list[wv][s < nsurv ? s : 0];
+        const bool keep = s < nsurv && cull_keep<IS2D>(s_p[0][k], s_p[1][k], s_p[2][k], x0, x0 + 3.f, y0, y0 + 3.f);
+        const unsigned long long m = __ballot(keep) & boxbits;
+        if (keep) s_box[wv][box][nb + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned char)k;
+        nb += __popcll(m);
+      }
+    }
+    // groups walked by the wave: max over its boxes (lanes 4k..4k+3 hold the four counts)
+    const int ngrp = __builtin_amdgcn_readfirstlane(quad_max_i(nb));
+    const int npad = (ngrp + kGroup - 1) / kGroup * kGroup;
+    for (int s = nb + pos; s < npad; s += 16) s_box[wv][box][s] = (unsigned char)kNull;
+    __builtin_amdgcn_wave_barrier();
+    // after reduce_box16 lane l holds 4 of its box's sums, flat indices 4*(l>>2) + i = 9*g + q.
+    // They are staged in LDS (one b128 store per group), and lane f < 63 then adds flat index
+    // f = 9g + q of every box, box by box, into the wave's slot L[q][wv][entry]: inside one
+    // instruction the 63 (q, entry) addresses are distinct (a box lists an entry once), and
+    // the boxes follow in program order, so the plain read-add-write is race-free and
+    // deterministic -- no LDS atomics.
+    // Branch-free groups of 7 survivors: an invalid (entry, pixel) pair contributes zeros and
+    // leaves T and S unchanged (ra = 1, fac = 0), so every group is straight-line code.
+    for (int g0 = 0; g0 < ngrp; g0 += kGroup) {
+      float acc[64];
+      acc[63] = 0.f;
+#pragma unroll
+      for (int g = 0; g < kGroup; ++g) {
+        const int k = my_list[g0 + g];
+        const float4 p0 = s_p[0][k];
+        const float4 p1 = s_p[1][k];
+        const float4 p2 = s_p[2][k];
+        const float dx = p0.x - px, dy = p0.y - py;
+        const float sigma = conic_sigma(p1, dx, dy);
+        const float vis = __expf(-sigma);
+        const float raw = p0.z * vis;
+        const float alpha = IS2D ? raw : fminf(kAlphaMax, raw);
+        // an invalid pair enters with alpha 0: ra = rcp(1) = 1, fac = 0 and (2D) v_sig = -0,
+        // mu unchanged, exactly, without a select each.  2D: the pixel's last entry (valid by
+        // construction) takes its T from the forward -- its 1 - alpha may be exactly 0.
+        const bool valid = IS2D ? k <= lastk && alpha >= cut2d : k <= lastk && sigma >= 0.f && alpha >= kAlphaThreshold;
+        const float alpha_v = valid ? alpha : 0.f;
+        const float ra = __builtin_amdgcn_rcpf(1.f - alpha_v);
+        if (IS2D)
+          T = k == lastq ? Tl : T * ra;
+        else
+          T *= ra;
+        const float fac = alpha_v * T;
+        acc[g * kPartial + 6] = fac * vr;
+        acc[g * kPartial + 7] = fac * vg;
+        acc[g * kPartial + 8] = fac * vb;
+        const float cv = p2.x * vr + p2.y * vg + p2.z * vb;
+        float v_sig;
+        if constexpr (IS2D) {
+          const float dmu = cv - mu;
+          v_sig = -alpha_v * (T * dmu);
+          mu = mu + alpha_v * dmu;
+        } else {
+          const float v_al = T * cv + ra * (vTa - Sv);
+          const bool unclamped = valid && raw <= kAlphaMax;
+          v_sig = unclamped ? -raw * v_al : 0.f;
+        }
+        // moments of v_sig: (dx, dy) here; the mean gradient (2a dx + b dy, b dx + 2c dy) is
+        // formed from their sums per entry after the reduction
+        const float tx_ = v_sig * dx, ty_ = v_sig * dy;
+        acc[g * kPartial + 0] = tx_;
+        acc[g * kPartial + 1] = ty_;
+        acc[g * kPartial + 2] = tx_ * dx;
+        acc[g * kPartial + 3] = tx_ * dy;
+        acc[g * kPartial + 4] = ty_ * dy;
+        acc[g * kPartial + 5] = v_sig;   // v_opacity = vis v_al = -v_sig / o (formed per entry below)
+        if (!IS2D) Sv += fac * cv;
+      }
+      float sum[4];
+      reduce_box16(acc, sum);
+      reinterpret_cast<float4*>(&s_stage[wv][0][0])[lane] = make_float4(sum[0], sum[1], sum[2], sum[3]);
+      __builtin_amdgcn_wave_barrier();
+      if (fown) {
+#pragma unroll
+        for (int bx = 0; bx < 4; ++bx) {
+          const int k = s_box[wv][bx][g0 + fg];
+          Lw[k] += stage_rd[4 * bx];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    // the next sub-chunk's records, gathered while this one's rows are summed and stored
+    if (sub > 0 && threadIdx.x < kChunk3) sp = rec[id_next];
+    __syncthreads();
+    if (threadIdx.x < sn) {
+      const int k = threadIdx.x;
+      float v[kPartial];
+#pragma unroll
+      for (int q = 0; q < kPartial; ++q) v[q] = (L[q][0][k] + L[q][1][k]) + (L[q][2][k] + L[q][3][k]);
       const float4 p1 = s_p[1][k];
-      const float4 p2 = s_p[2][k];
-      const float dx = p0.x - px, dy = p0.y - py;
-      const float sigma = conic_sigma(p1, dx, dy);
-      const float vis = __expf(-sigma);
-      const float raw = p0.z * vis;
-      const float alpha = IS2D ? raw : fminf(kAlphaMax, raw);
-      // an invalid pair enters with alpha 0: ra = rcp(1) = 1, fac = 0 and (2D) v_sig = -0,
-      // mu unchanged, exactly, without a select each.  2D: the pixel's last entry (valid by
-      // construction) takes its T from the forward -- its 1 - alpha may be exactly 0.
-      const bool valid = IS2D ? k <= lastk && alpha >= cut2d : k <= lastk && sigma >= 0.f && alpha >= kAlphaThreshold;
-      const float alpha_v = valid ? alpha : 0.f;
-      const float ra = __builtin_amdgcn_rcpf(1.f - alpha_v);
-      if (IS2D)
-        T = k == lastq ? Tl : T * ra;
-      else
-        T *= ra;
-      const float fac = alpha_v * T;
-      acc[g * kPartial + 6] = fac * vr;
-      acc[g * kPartial + 7] = fac * vg;
-      acc[g * kPartial + 8] = fac * vb;
-      const float cv = p2.x * vr + p2.y * vg + p2.z * vb;
-      float v_sig;
-      if constexpr (IS2D) {
-        const float dmu = cv - mu;
-        v_sig = -alpha_v * (T * dmu);
-        mu = mu + alpha_v * dmu;
-      } else {
-        const float v_al = T * cv + ra * (vTa - Sv);
-        const bool unclamped = valid && raw <= kAlphaMax;
-        v_sig = unclamped ? -raw * v_al : 0.f;
-      }
-      // moments of v_sig: (dx, dy) here; the mean gradient (2a dx + b dy, b dx + 2c dy) is
-      // formed from their sums per entry after the reduction
-      const float tx_ = v_sig * dx, ty_ = v_sig * dy;
-      acc[g * kPartial + 0] = tx_;
-      acc[g * kPartial + 1] = ty_;
-      acc[g * kPartial + 2] = tx_ * dx;
-      acc[g * kPartial + 3] = tx_ * dy;
-      acc[g * kPartial + 4] = ty_ * dy;
-      acc[g * kPartial + 5] = v_sig;   // v_opacity = vis v_al = -v_sig / o (formed per entry below)
-      if (!IS2D) Sv += fac * cv;
+      const float mx = v[0], my = v[1];
+      v[0] = 2.f * p1.x * mx + p1.y * my;
+      v[1] = p1.y * mx + 2.f * p1.z * my;
+      v[5] = -v[5] / s_p[0][k].z;
+      store_partial_row(partial, kos_mine, v);
     }
-    float sum[4];
-    reduce_box16(acc, sum);
-    reinterpret_cast<float4*>(&s_stage[wv][0][0])[lane] = make_float4(sum[0], sum[1], sum[2], sum[3]);
-    __builtin_amdgcn_wave_barrier();
-    if (fown) {
-#pragma unroll
-      for (int bx = 0; bx < 4; ++bx) {
-        const int k = s_box[wv][bx][g0 + fg];
-        Lw[k] += stage_rd[4 * bx];
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  __syncthreads();
-  if (threadIdx.x < n) {
-    const int k = threadIdx.x;
-    float v[kPartial];
-#pragma unroll
-    for (int q = 0; q < kPartial; ++q) v[q] = (L[q][0][k] + L[q][1][k]) + (L[q][2][k] + L[q][3][k]);
-    const float4 p1 = s_p[1][k];
-    const float mx = v[0], my = v[1];
-    v[0] = 2.f * p1.x * mx + p1.y * my;
-    v[1] = p1.y * mx + 2.f * p1.z * my;
-    v[5] = -v[5] / s_p[0][k].z;
-    store_partial_row(partial, kos_mine, v);
+    sb0 -= kChunk3;
+    sn = kChunk3;
+    id_mine = id_next;
+    kos_mine = kos_next;
   }
 }
 
@@ -1329,7 +1404,8 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
   GSR_REQUIRE(CT < (1ll << 31), "%s: too many tiles", who);
   GSR_REQUIRE(n_busy >= 0 && n_busy <= CT, "%s: n_busy=%d out of [0, %lld]", who, n_busy, (long long)CT);
   // the lazy second pass covers only its (device-counted) tiles: no empty-tile fill
-  const int64_t n_fill = lz.rerun ? 0 : std::min<int64_t>(CT - n_busy, kFillBlocks);
+  // (at least one fill workgroup: with a bounded n_busy the true count may be lower)
+  const int64_t n_fill = lz.rerun ? 0 : std::max<int64_t>(1, std::min<int64_t>(CT - n_busy, kFillBlocks));
   hipStream_t s = (hipStream_t)stream;
   // tile_end collects max(last) of the quadrant workgroups (atomicMax from the -1 that
   // gsr_bin_offsets wrote)
@@ -1344,17 +1420,17 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
     hipLaunchKernelGGL((k_raster_fwd<false, 16>), dim3((unsigned)(busy_grid<16>(n_busy) + n_fill)),
                        dim3(kRasterThreads), kFwdLdsPad, s, (const Splat*)rec, sorted_ids, tile_offset, tile_order,
                        width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state,
-                       chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz);
+                       chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz, stats);
   } else if (lanes == 4) {
     hipLaunchKernelGGL((k_raster_fwd<IS2D, 4>), dim3((unsigned)(busy_grid<4>(n_busy) + n_fill)),
                        dim3(kRasterThreads), IS2D ? kFwdLdsPad2D : kFwdLdsPad, s, (const Splat*)rec, sorted_ids,
                        tile_offset, tile_order, width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end,
-                       (float4*)chunk_state, chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz);
+                       (float4*)chunk_state, chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz, stats);
   } else {
     hipLaunchKernelGGL((k_raster_fwd_box<IS2D>), dim3((unsigned)(((n_busy + 7) & ~7) + n_fill)),
                        dim3(kRasterThreads), 0, s, (const Splat*)rec, sorted_ids, tile_offset, tile_order, width,
                        height, tw, th, bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state, chunk_base,
-                       (int)n_busy, CT, tile_cut, cut2d, lz);
+                       (int)n_busy, CT, tile_cut, cut2d, lz, stats);
   }
   GSR_LAUNCH_CHECK(who);
   if (finalize && n_busy > 0) {
@@ -1370,18 +1446,26 @@ template <bool LOSS, bool IS2D>
 static int raster_bwd(const char* who, const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                       const int32_t* tile_end, const int32_t* chunk_base,
                       const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
-                      int C, int width, int height, float cut2d, const float* bg, const float* final_T,
-                      const int32_t* last, const float* v_rgb, const float* v_alpha, const gsr_loss_terms& lt,
-                      const int32_t* k_of_s, float* partial, void* stream) {
+                      int32_t chunk_entries, int C, int width, int height, float cut2d, const float* bg,
+                      const float* final_T, const int32_t* last, const float* v_rgb, const float* v_alpha,
+                      const gsr_loss_terms& lt, const int32_t* k_of_s, float* partial, void* stream) {
   GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "%s: bad C=%d or image %dx%d", who, C, width, height);
   GSR_REQUIRE(n_chunks >= 0, "%s: bad n_chunks", who);
+  GSR_REQUIRE(chunk_entries == 0 || (chunk_entries >= kChunk3 && (chunk_entries & (chunk_entries - 1)) == 0),
+              "%s: chunk_entries %d is not 0 or a power of two >= %d", who, chunk_entries, kChunk3);
   if (n_chunks == 0) return GSR_OK;
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   // n_chunks bounds the forward's active-chunk count (stats->n_active, device-side)
-  hipLaunchKernelGGL((k_raster_bwd<LOSS, IS2D>), dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
-                     (const Splat*)rec, sorted_ids, tile_offset, tile_end, chunk_base,
-                     (const float4*)chunk_state, width, height, tw, th, bg, final_T, last, v_rgb, v_alpha, partial,
-                     chunk_list, stats, k_of_s, lt, C, cut2d);
+  if (chunk_entries > kChunk3)
+    hipLaunchKernelGGL((k_raster_bwd<LOSS, IS2D, true>), dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
+                       (const Splat*)rec, sorted_ids, tile_offset, tile_end, chunk_base,
+                       (const float4*)chunk_state, width, height, tw, th, bg, final_T, last, v_rgb, v_alpha, partial,
+                       chunk_list, stats, k_of_s, lt, C, cut2d);
+  else
+    hipLaunchKernelGGL((k_raster_bwd<LOSS, IS2D, false>), dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
+                       (const Splat*)rec, sorted_ids, tile_offset, tile_end, chunk_base,
+                       (const float4*)chunk_state, width, height, tw, th, bg, final_T, last, v_rgb, v_alpha, partial,
+                       chunk_list, stats, k_of_s, lt, C, cut2d);
   GSR_LAUNCH_CHECK(who);
   return GSR_OK;
 }
@@ -1418,7 +1502,7 @@ int gsr3d_raster_fwd_lazy(const float* rec, const float* depth, int32_t* sorted_
   if (rc != GSR_OK) return rc;
   // the listed tiles sorted whole, then rendered again from scratch (same layout)
   rc = bin_sort_rest(tile_offset, CT, max_seg, n_lazy_max, sort_workspace, sort_workspace_bytes, lazy, tile_end,
-                     sorted_ids, k_of_s, (hipStream_t)stream);
+                     sorted_ids, k_of_s, stats, (hipStream_t)stream);
   if (rc != GSR_OK) return rc;
   const FwdLazy l2{lazy, lazy + CT, lazy + 2 * CT, lazy + 3 * CT, 1};
   rc = raster_fwd<false>("gsr3d_raster_fwd_lazy", rec, depth, sorted_ids, tile_offset, tile_order, chunk_base, C,
@@ -1437,25 +1521,25 @@ int gsr3d_raster_fwd_lazy(const float* rec, const float* depth, int32_t* sorted_
 int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_end, const int32_t* chunk_base,
                      const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
-                     int C, int width, int height, const float* bg, const float* final_T, const int32_t* last,
-                     const float* v_rgb, const float* v_alpha, const int32_t* k_of_s, float* partial,
-                     void* stream) {
+                     int32_t chunk_entries, int C, int width, int height, const float* bg, const float* final_T,
+                     const int32_t* last, const float* v_rgb, const float* v_alpha, const int32_t* k_of_s,
+                     float* partial, void* stream) {
   const gsr_loss_terms none{};
   return raster_bwd<false, false>("gsr3d_raster_bwd", rec, sorted_ids, tile_offset, tile_end, chunk_base,
-                                  chunk_state, chunk_list, stats, n_chunks, C, width, height, 0.f, bg,
+                                  chunk_state, chunk_list, stats, n_chunks, chunk_entries, C, width, height, 0.f, bg,
                                   final_T, last, v_rgb, v_alpha, none, k_of_s, partial, stream);
 }
 
 int gsr3d_raster_bwd_loss(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                           const int32_t* tile_end, const int32_t* chunk_base,
                           const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats,
-                          int32_t n_chunks, int C, int width, int height, const float* bg, const float* final_T,
-                          const int32_t* last, const gsr_loss_terms* loss, const int32_t* k_of_s, float* partial,
-                          void* stream) {
+                          int32_t n_chunks, int32_t chunk_entries, int C, int width, int height, const float* bg,
+                          const float* final_T, const int32_t* last, const gsr_loss_terms* loss,
+                          const int32_t* k_of_s, float* partial, void* stream) {
   GSR_REQUIRE(loss != nullptr && loss->rgb && loss->target_img && loss->target_mask && loss->sums && loss->grad_out,
               "gsr3d_raster_bwd_loss: incomplete loss terms");
   return raster_bwd<true, false>("gsr3d_raster_bwd_loss", rec, sorted_ids, tile_offset, tile_end, chunk_base,
-                                 chunk_state, chunk_list, stats, n_chunks, C, width, height, 0.f, bg,
+                                 chunk_state, chunk_list, stats, n_chunks, chunk_entries, C, width, height, 0.f, bg,
                                  final_T, last, nullptr, nullptr, *loss, k_of_s, partial, stream);
 }
 
@@ -1473,13 +1557,13 @@ int gsr2d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t*
 int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_end, const int32_t* chunk_base,
                      const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
-                     int C, int width, int height, float eps_cut, const float* bg, const float* final_T,
-                     const int32_t* last, const float* v_rgb, const float* v_alpha, const int32_t* k_of_s,
-                     float* partial, void* stream) {
+                     int32_t chunk_entries, int C, int width, int height, float eps_cut, const float* bg,
+                     const float* final_T, const int32_t* last, const float* v_rgb, const float* v_alpha,
+                     const int32_t* k_of_s, float* partial, void* stream) {
   GSR_REQUIRE(eps_cut > 0.f && eps_cut < 1.f, "gsr2d_raster_bwd: eps_cut must be in (0,1)");
   const gsr_loss_terms none{};
   return raster_bwd<false, true>("gsr2d_raster_bwd", rec, sorted_ids, tile_offset, tile_end, chunk_base,
-                                 chunk_state, chunk_list, stats, n_chunks, C, width, height, eps_cut, bg,
+                                 chunk_state, chunk_list, stats, n_chunks, chunk_entries, C, width, height, eps_cut, bg,
                                  final_T, last, v_rgb, v_alpha, none, k_of_s, partial, stream);
 }
 

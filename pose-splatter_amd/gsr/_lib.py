@@ -10,7 +10,7 @@ import ctypes
 import os
 import threading
 
-__all__ = ["LIB_PATH", "GsrLibraryError", "lib", "check", "BinStats", "LossTerms", "EXPORTS",
+__all__ = ["LIB_PATH", "GsrLibraryError", "lib", "check", "BinStats", "BinCaps", "LossTerms", "EXPORTS", "ABI_VERSION",
            "RADIUS_OPACITY_AABB", "RADIUS_ISOTROPIC_3SIGMA", "ORDER_DEPTH", "ORDER_INDEX", "TILE"]
 
 LIB_PATH = os.environ.get(
@@ -26,6 +26,13 @@ ORDER_INDEX = 1
 INPUT_ADAPTER = 0
 INPUT_GSPLAT = 1
 
+ABI_VERSION = 3   # include/gsr.h GSR_ABI_VERSION this binding is written for
+
+# stats->overflow bits of a capacity-bounded call (include/gsr.h GSR_OVF_*)
+OVF_BITS = {1: "intersections > isect cap", 2: "chunks > chunk cap", 4: "busy tiles > n_busy bound",
+            8: "list longer than the split sort's max_seg", 16: "lazily sorted tiles > n_lazy_max bound",
+            32: "raster backward chunk_entries differs from the forward's"}
+
 GSR_EINVAL = -1
 GSR_ELAUNCH = -2
 GSR_ECAPACITY = -3
@@ -38,7 +45,19 @@ class GsrLibraryError(RuntimeError):
 class BinStats(ctypes.Structure):
     _fields_ = [("n_isect", ctypes.c_int64), ("max_seg", ctypes.c_int32), ("n_busy", ctypes.c_int32),
                 ("n_chunks", ctypes.c_int32), ("n_active", ctypes.c_int32),
-                ("n_sort_big", ctypes.c_int32), ("n_sort_mid", ctypes.c_int32)]
+                ("n_sort_big", ctypes.c_int32), ("n_sort_mid", ctypes.c_int32),
+                ("isect_cap", ctypes.c_int64), ("chunk_cap", ctypes.c_int64), ("overflow", ctypes.c_int32),
+                ("chunk_entries", ctypes.c_int32), ("status", ctypes.c_void_p), ("reserved", ctypes.c_int64 * 2)]
+
+
+class BinCaps(ctypes.Structure):
+    """gsr_bin_caps: bounds of a call that does not read the stats back (0 = unbounded)."""
+    _fields_ = [("isect", ctypes.c_int64), ("chunks", ctypes.c_int64), ("status", ctypes.c_void_p),
+                ("chunk_entries", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+def describe_overflow(bits: int) -> str:
+    return ", ".join(v for k, v in OVF_BITS.items() if bits & k) or "none"
 
 
 class LossTerms(ctypes.Structure):
@@ -58,6 +77,7 @@ _SZ = ctypes.c_size_t
 # name -> (restype, argtypes); must list every function declared in include/gsr.h
 EXPORTS = {
     "gsr_version": (ctypes.c_int, []),
+    "gsr_abi_version": (ctypes.c_int, []),
     "gsr_last_error": (ctypes.c_char_p, []),
     "gsr_selftest_reduce64": (ctypes.c_int, [_P, _P]),
     "gsr_selftest_reduce_box16": (ctypes.c_int, [_P, _P]),
@@ -67,7 +87,7 @@ EXPORTS = {
                                          _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _I32, _P]),
     "gsr2d_project_fwd": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I32, _I32, _I32, _I32, _F, _P, _P, _P,
                                          _P, _P, _I32, _P]),
-    "gsr_bin_offsets": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P, _P, _P]),
+    "gsr_bin_offsets": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P, ctypes.POINTER(BinCaps), _P, _P]),
     "gsr_bin_sort_workspace": (_SZ, [_I64, _I64]),
     "gsr_bin_emit": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I32, _P, _P, _SZ, _P]),
     "gsr_bin_sort": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I32, _I64, _I32,
@@ -83,19 +103,19 @@ EXPORTS = {
                                          _I32, _I32, _I32, _P, _P, _SZ, _P, _P, _P, _P]),
     "gsr3d_raster_fwd_lazy": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _I32, _P, _P, _P,
                                              _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _P, _SZ, _P, _P]),
-    "gsr3d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P,
+    "gsr3d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _P,
                                         _P, _P, _P, _P, _P, _P, _P]),
     "gsr2d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _I32, _P, _P, _P, _P, _P,
                                         _P, _P, _P, _P, _P]),
-    "gsr2d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _F, _P, _P,
+    "gsr2d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _F, _P, _P,
                                         _P, _P, _P, _P, _P, _P]),
     "gsr3d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _I32, _I32, _I32, _F, _I32, _P, _P,
-                                         _P, _P, _P, _P, _I64, _I64, _P, _P]),
+                                         _P, _P, _P, _P, _I64, _I64, _P, _P, _P]),
     "gsr2d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P,
-                                         _P, _P]),
+                                         _P, _P, _P]),
     "gsr_loss_workspace": (_SZ, [_I32, _I32, _I32]),
     "gsr_loss_iou_l1_fwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _SZ, _P, _P, _P, _P]),
-    "gsr3d_raster_bwd_loss": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P,
+    "gsr3d_raster_bwd_loss": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _P,
                                              _P, _P, ctypes.POINTER(LossTerms), _P, _P, _P]),
     "gsr_head_select_workspace": (_SZ, [_I64]),
     "gsr_head_select": (ctypes.c_int, [_P, _I64, _D, _F, _D, _I32, _I32, _I32, _P, _SZ, _P, _P, _P, _P]),
@@ -134,6 +154,15 @@ def lib():
             handle = ctypes.CDLL(LIB_PATH)
         except OSError as e:
             raise GsrLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+        try:
+            abi = handle.gsr_abi_version
+        except AttributeError:
+            raise GsrLibraryError(f"{LIB_PATH} predates gsr_abi_version (ABI < 3): rebuild it "
+                                  "(`make -C pose-splatter_amd/csrc`)") from None
+        abi.restype = ctypes.c_int
+        if abi() != ABI_VERSION:
+            raise GsrLibraryError(f"{LIB_PATH} has ABI revision {abi()}, this binding expects {ABI_VERSION}: "
+                                  "rebuild the library or update gsr/_lib.py")
         for name, (res, args) in EXPORTS.items():
             fn = getattr(handle, name)
             fn.restype = res

@@ -150,7 +150,7 @@ class _RenderIouL1(torch.autograd.Function):
         def raster(L, q, partial, stream):
             check(L.gsr3d_raster_bwd_loss(q["rec"], q["sorted_ids"], q["tile_off"], q["tile_end"],
                                           q["chunk_base"], q["chunk_state"], q["chunk_list"],
-                                          q["stats_dev"], b.n_chunks, b.C, width, height, _ptr(bgc),
+                                          q["stats_dev"], b.n_chunks, b.chunk_entries, b.C, width, height, _ptr(bgc),
                                           q["final_T"], q["last"], ctypes.byref(terms), q["k_of_s"],
                                           _ptr(partial), stream), "gsr3d_raster_bwd_loss")
         v_params = backward3d(b, ctx.meta, raster)

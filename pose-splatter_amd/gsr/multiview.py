@@ -29,7 +29,8 @@ from typing import Callable
 import torch
 import torch.distributed as dist
 
-__all__ = ["view_shard", "sharded_backward", "band_shard", "row_work", "unit_shard", "sharded_backward_units",
+__all__ = ["view_shard", "sharded_backward", "band_shard", "row_work", "unit_bounds", "unit_shard",
+           "sharded_backward_units",
            "frame_view_units", "frame_buckets", "sharded_backward_frames", "bucket_bounds"]
 
 
@@ -100,12 +101,62 @@ def row_work(stats_tile_len, C: int, th: int, tw: int):
     return [float(x) for x in t.cpu()]
 
 
-def unit_shard(C: int, rows: int, world: int, rank: int, weights=None) -> tuple:
+def unit_bounds(C: int, rows: int, world: int, weights=None, view_cost: float = 0.0) -> list:
+    """Boundaries g_0 = 0 <= g_1 <= ... <= g_world = C*rows of a contiguous partition of the
+    view-major (view, tile row) units that minimises the largest rank cost
+        cost(range) = sum of its unit weights + view_cost * (number of views it touches)
+    -- every touched view costs a rank a projection forward and backward of all N Gaussians,
+    whatever share of its rows the rank renders.  view_cost 0: plain weight balancing
+    (``band_shard``).  Bisection on the bottleneck with a greedy fill (optimal for contiguous
+    ranges, since a range's cost only grows when it is extended)."""
+    U = C * rows
+    if world < 1:
+        raise ValueError(f"bad world {world}")
+    w = [1.0] * U if weights is None else [max(float(x), 0.0) for x in weights]
+    if len(w) != U:
+        raise ValueError(f"weights must have {U} entries")
+    if view_cost <= 0.0:
+        return [band_shard(U, world, r, w)[0] for r in range(world)] + [U]
+
+    def fill(B):
+        """Greedy ranges under bottleneck B: their starts (None if more than world needed)."""
+        starts, cost, view = [0], 0.0, -1
+        for u in range(U):
+            v = u // rows
+            add = w[u] + (view_cost if v != view else 0.0)
+            if cost > 0.0 and cost + add > B:
+                starts.append(u)
+                if len(starts) > world:
+                    return None
+                cost, view = w[u] + view_cost, v
+            else:
+                cost += add
+                view = v
+        return starts
+
+    lo = max(max(w) + view_cost, (sum(w) + C * view_cost) / world)
+    hi = sum(w) + C * view_cost
+    for _ in range(60):
+        mid = 0.5 * (lo + hi)
+        if fill(mid) is None:
+            lo = mid
+        else:
+            hi = mid
+    starts = fill(hi)
+    # fewer ranges than ranks: the last ones stay empty (the bottleneck is already optimal)
+    return starts + [U] * (world + 1 - len(starts))
+
+
+def unit_shard(C: int, rows: int, world: int, rank: int, weights=None, view_cost: float = 0.0) -> tuple:
     """This rank's contiguous share of the C*rows (view, tile row) units, view-major, balanced by
-    ``weights`` (C*rows per-unit work; uniform if None).  Returns (v0, v1, band): the views
-    [v0, v1) the rank touches and its rows as a band of global rows relative to view v0 (the
-    ``RenderOptions3D.band`` of a render of views v0..v1-1).  An empty share gives v0 == v1."""
-    g0, g1 = band_shard(C * rows, world, rank, weights)
+    ``weights`` (C*rows per-unit work; uniform if None) plus ``view_cost`` per touched view
+    (``unit_bounds``).  Returns (v0, v1, band): the views [v0, v1) the rank touches and its
+    rows as a band of global rows relative to view v0 (the ``RenderOptions3D.band`` of a
+    render of views v0..v1-1).  An empty share gives v0 == v1."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} of world {world}")
+    b = unit_bounds(C, rows, world, weights, view_cost)
+    g0, g1 = b[rank], b[rank + 1]
     if g1 <= g0:
         return 0, 0, (0, 0)
     v0, v1 = g0 // rows, (g1 - 1) // rows + 1
@@ -120,7 +171,7 @@ def bucket_bounds(n: int, buckets: int) -> list:
 
 def sharded_backward_units(render_band: Callable, params: torch.Tensor, viewmats: torch.Tensor, Ks: torch.Tensor,
                            v_rgb: torch.Tensor, v_alpha: torch.Tensor, rows: int, weights=None, buckets: int = 0,
-                           group=None) -> torch.Tensor:
+                           group=None, view_cost: float = 0.0) -> torch.Tensor:
     """Gradient of sum(rgb*v_rgb + alpha*v_alpha) over all C views, (view, row)-unit sharded.
 
     ``render_band(p, viewmats_sub, Ks_sub, band, hook)`` renders views v0..v1-1 binned to
@@ -132,7 +183,7 @@ def sharded_backward_units(render_band: Callable, params: torch.Tensor, viewmats
     (identical on every rank)."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    v0, v1, band = unit_shard(viewmats.shape[0], rows, world, rank, weights)
+    v0, v1, band = unit_shard(viewmats.shape[0], rows, world, rank, weights, view_cost)
     p = params.detach().requires_grad_(True)
     pieces, works = [], []
 

@@ -4,20 +4,37 @@
 parameters (the same tensor ``GaussianRenderer.render`` receives,
 src/gaussian_renderer.py:157-211 and :269-334).  All device memory comes from PyTorch's
 caching allocator; every libgsr call is enqueued on ``torch.cuda.current_stream()``.
-The one host synchronisation per forward is the ``gsr_bin_stats`` read (into pinned host
-memory) that sizes the intersection buffers (gsplat reads its intersection count the same
-way).  Intermediates live in two arenas per forward (see ``_Arena``).
+
+Two capacity modes ("Threading / streams"):
+
+* ``"exact"`` (default): one host synchronisation per forward, the ``gsr_bin_stats`` read
+  (into pinned host memory) that sizes the intersection buffers exactly (gsplat reads its
+  intersection count the same way, src/gaussian_renderer.py:196-208).
+* ``"bounded"``: NO host synchronisation.  Buffers and grids are sized from upper bounds
+  derived from an earlier call of the same shape (+25 % intersections / chunks, +12.5 %
+  busy tiles); the device checks every bound and, if one fails, the call writes NaN to
+  rgb / alpha / v_params and ORs ``GSR_OVF_*`` bits into a sticky per-device status word.
+  The previous bounded call's stats are read back asynchronously and checked at the next
+  call (raising ``CapacityOverflowError`` if it overflowed); ``check_overflow()`` checks the
+  sticky word explicitly (e.g. after a captured HIP graph replays).  A bounded step has no
+  host wait, so it can be captured in a HIP graph (``torch.cuda.CUDAGraph``).
+
+Intermediates live in two arenas per forward (see ``_Arena``).
 """
 from __future__ import annotations
 
+import contextlib
 from dataclasses import dataclass, field
 
 import torch
 
+import ctypes
+
 from . import _lib
 from ._lib import check, lib
 
-__all__ = ["render3d", "render2d", "render2d_units", "RenderOptions3D", "last_stats"]
+__all__ = ["render3d", "render2d", "render2d_units", "RenderOptions3D", "last_stats", "set_capacity_mode",
+           "capacity_mode", "check_overflow", "overflow_status", "CapacityOverflowError", "set_chunk_entries"]
 
 _TILE = _lib.TILE
 
@@ -63,6 +80,77 @@ class RenderOptions3D:
     # (multi-GPU: an async all-reduce of finished rows overlaps the later ranges)
     grad_buckets: int = 1
     grad_hook: object = field(default=None, compare=False)
+    # "exact" | "bounded" | None (the module default, set_capacity_mode)
+    capacity: str | None = None
+
+
+class CapacityOverflowError(RuntimeError):
+    """A capacity-bounded render exceeded its bounds: its outputs were written as NaN."""
+
+
+_capacity_default = "exact"
+# list entries per backward work unit (gsr_bin_caps.chunk_entries): 3D lists stop early and
+# the heavy tiles need the chunk-parallel backward's spread; 2D lists are walked whole, so
+# longer units re-read the pixel state and write chunk records 4x less often
+_chunk_entries = {"3d": 128, "2d": 512}
+
+
+def set_chunk_entries(mode: str, entries: int) -> None:
+    """Backward work-unit length for "3d" or "2d" renders (a power of two >= 128)."""
+    if mode not in _chunk_entries or entries < 128 or entries & (entries - 1):
+        raise ValueError(f"chunk entries for {mode!r} must be a power of two >= 128, got {entries}")
+    _chunk_entries[mode] = int(entries)
+
+
+def set_capacity_mode(mode: str) -> None:
+    """Module default for calls that do not choose: "exact" (one stats read-back per forward)
+    or "bounded" (no host synchronisation; bounds from the previous call of the same shape)."""
+    global _capacity_default
+    if mode not in ("exact", "bounded"):
+        raise ValueError(f"capacity mode must be 'exact' or 'bounded', got {mode!r}")
+    _capacity_default = mode
+
+
+@contextlib.contextmanager
+def capacity_mode(mode: str):
+    """``with capacity_mode("bounded"): ...`` -- the module default inside the block."""
+    old = _capacity_default
+    set_capacity_mode(mode)
+    try:
+        yield
+    finally:
+        set_capacity_mode(old)
+
+
+_status = {}   # device -> int32 [1] sticky overflow bits (device memory, OR-ed by the kernels)
+
+
+def _status_buf(device) -> torch.Tensor:
+    key = str(device)
+    t = _status.get(key)
+    if t is None:
+        t = _status[key] = torch.zeros(1, device=device, dtype=torch.int32)
+    return t
+
+
+def overflow_status(device=None, reset: bool = False) -> int:
+    """The sticky GSR_OVF_* bits of every call on ``device`` since the last reset (synchronises)."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    t = _status_buf(dev)
+    bits = int(t.item())
+    if reset:
+        t.zero_()
+    return bits
+
+
+def check_overflow(device=None) -> None:
+    """Raise CapacityOverflowError if any call on ``device`` overflowed its bounds since the
+    last check (synchronises; resets the status)."""
+    bits = overflow_status(device, reset=True)
+    if bits:
+        _size_hint.clear()
+        raise CapacityOverflowError(f"gsr: a capacity-bounded render exceeded its bounds ({_lib.describe_overflow(bits)}); "
+                                    "its outputs were NaN -- the bounds are reset, re-run the step")
 
 
 _last_stats = {}
@@ -96,21 +184,17 @@ class _timed:
 
     def __enter__(self):
         if _timers is not None and (_timed_only is None or self.name in _timed_only):
-            self.s = torch.cuda.Event(enable_timing=True)
+            # inside a HIP graph capture the events become record nodes of the graph (external)
+            self.s = torch.cuda.Event(enable_timing=True, external=_capturing())
             self.s.record()
         return self
 
     def __exit__(self, *exc):
         if self.s is not None:
-            e = torch.cuda.Event(enable_timing=True)
+            e = torch.cuda.Event(enable_timing=True, external=_capturing())
             e.record()
             _timers.setdefault(self.name, []).append((self.s, e))
         return False
-
-
-def last_stats() -> dict:
-    """Binning statistics of the most recent forward (I, I_eff, max list, busy tiles)."""
-    return dict(_last_stats)
 
 
 class _Arena:
@@ -145,8 +229,14 @@ _VIEWS = {"rec": ("pre", _F32), "depth": ("pre", _F32), "rect": ("pre", _I32), "
           "chunk_state": ("chunks", _F32), "chunk_list": ("chunks", _I32), "lazy": ("pre", _I32)}
 
 _pinned = {}
-_size_hint = {}   # (device, C, N, W, H) -> (I, n_chunks) of the last forward of that shape
+# (device, C, N, W, H) -> stats of the last exactly sized (or observed bounded) forward of that
+# shape: I, chunks, max_seg, busy, big, mid -- the bounds of bounded calls and the speculative
+# arena sizes of exact ones
+_size_hint = {}
+_monitors = {}    # shape key -> [pinned stats copy, event] of the last bounded eager forward
 _bg_cache = {}
+_STATS_BYTES = 128   # >= sizeof(gsr_bin_stats) (80)
+_STATS_I32 = _STATS_BYTES // 4
 
 
 def _pinned_stats(device) -> torch.Tensor:
@@ -154,6 +244,50 @@ def _pinned_stats(device) -> torch.Tensor:
     if t is None:
         t = _pinned[device] = torch.empty(8, dtype=torch.int32, pin_memory=True)
     return t
+
+
+def _hint_from(st) -> dict:
+    """Hint dict from the int32 words of a gsr_bin_stats (first 8 words)."""
+    return {"I": (st[0] & 0xFFFFFFFF) | (st[1] << 32), "max_seg": st[2], "busy": st[3], "chunks": st[4],
+            "big": st[6], "mid": st[7]}
+
+
+def _capturing() -> bool:
+    return torch.cuda.is_current_stream_capturing()
+
+
+def _monitor_check(key) -> None:
+    """The previous bounded forward of this shape: if its stats have arrived (non-blocking),
+    raise on overflow, else refresh the shape's bounds from what it observed."""
+    m = _monitors.get(key)
+    if m is None or m[1] is None or not m[1].query():
+        return
+    st = m[0].tolist()
+    m[1] = None
+    ovf = st[12]   # gsr_bin_stats.overflow (byte 48)
+    if ovf:
+        _size_hint.pop(key, None)
+        raise CapacityOverflowError(f"gsr: the previous capacity-bounded render of this shape exceeded its bounds "
+                                    f"({_lib.describe_overflow(ovf)}); its outputs were NaN -- the bounds are "
+                                    "reset, re-run the step")
+    h = _hint_from(st)
+    old = _size_hint.get(key)
+    if old is not None:   # keep bounds monotone over a window: shrink slowly, grow at once
+        h = {k: max(v, int(0.9 * old[k])) for k, v in h.items()}
+    _size_hint[key] = h
+
+
+def _monitor_enqueue(b) -> None:
+    """Copy this bounded forward's stats to pinned memory behind its kernels (no wait)."""
+    if _capturing():
+        return
+    m = _monitors.get(b.key)
+    if m is None:
+        m = [torch.empty(_STATS_I32, dtype=torch.int32, pin_memory=True), None]
+        _monitors[b.key] = m
+    m[0].copy_(b.pre.view("stats_dev", _I32), non_blocking=True)
+    m[1] = torch.cuda.Event()
+    m[1].record()
 
 
 # Per (device, tile count, stream): the projection's tile histogram + emission counter, shared
@@ -176,9 +310,9 @@ def _tile_counts(device, CT: int, stream: int) -> list:
 class _Bins:
     """Per-call intermediates shared by forward and backward: two arenas, one sized before
     the stats readback (per-Gaussian and per-tile buffers) and one after it (per-intersection
-    buffers)."""
+    buffers).  A bounded call sizes both before any kernel runs and never reads back."""
 
-    def __init__(self, device, C, N, width, height):
+    def __init__(self, device, C, N, width, height, capacity=None, key_extra=None, chunk_entries=128):
         self.device = device
         self.C, self.N, self.W, self.H = C, N, width, height
         self.tw = (width + _TILE - 1) // _TILE
@@ -189,7 +323,7 @@ class _Bins:
             "rec": CN * 48, "depth": CN * 4, "rect": CN * 8, "cnt": CN * 4,
             "isect_off": CN * 4, "tile_off": (self.CT + 1) * 4, "busy": self.CT * 4,
             "chunk_base": (self.CT + 1) * 4, "tile_end": self.CT * 4, "tile_cut": self.CT * 8,
-            "stats_dev": 32, "final_T": C * width * height * 8, "last": C * width * height * 4,
+            "stats_dev": _STATS_BYTES, "final_T": C * width * height * 8, "last": C * width * height * 4,
             "lazy": (3 * self.CT + 4) * 4})
         self.p = dict(self.pre.ptr)
         self.tc = _tile_counts(device, self.CT, _stream(device))
@@ -198,7 +332,42 @@ class _Bins:
         self.post_cap = self.chunk_cap = 0
         self.emitted = False
         self.n_chunks = self.n_isect = self.max_seg = self.n_busy = self.n_lazy = 0
-        self.key = (str(device), C, N, width, height)
+        self.n_sort_big = self.n_sort_mid = self.n_lazy_max = 0
+        # the shape whose previous call bounds this one (band / unit grouping included: they
+        # change the lists as much as the shape does)
+        self.key = (str(device), C, N, width, height, key_extra)
+        mode = capacity or _capacity_default
+        if mode not in ("exact", "bounded"):
+            raise ValueError(f"capacity mode must be 'exact' or 'bounded', got {mode!r}")
+        self.bounded = False
+        if mode == "bounded":
+            if not _capturing():
+                _monitor_check(self.key)
+            hint = _size_hint.get(self.key)
+            if hint is not None:
+                self._set_bounds(hint)
+            elif _capturing():
+                raise RuntimeError("gsr: a bounded render captured in a graph needs bounds from an earlier call "
+                                   "of the same shape (run one step before capturing)")
+        self.chunk_entries = int(chunk_entries)
+        self.caps = _lib.BinCaps(self.post_cap if self.bounded else 0, self.chunk_cap if self.bounded else 0,
+                                 _status_buf(device).data_ptr(), self.chunk_entries, 0)
+
+    def _set_bounds(self, h: dict) -> None:
+        """Bounded call: every buffer and grid from the shape's hint plus margins (the device
+        checks each bound; gsr_bin_stats.overflow)."""
+        self.bounded = True
+        self.alloc_post(int(h["I"] * 1.25) + 4096)
+        self.alloc_chunks(int(h["chunks"] * 1.25) + 64)
+        self.n_isect = self.post_cap
+        self.n_chunks = self.chunk_cap
+        self.n_busy = min(self.CT, int(h["busy"] * 1.125) + 8)
+        self.max_seg = int(h["max_seg"] * 1.25) + 64
+        self.n_sort_big = min(h["big"], self.n_busy)
+        self.n_sort_mid = min(h["mid"], self.n_busy - self.n_sort_big)
+        if self.max_seg >= 4096 and self.n_sort_big + self.n_sort_mid == 0:
+            self.n_sort_mid = 1   # the 1024-thread sort shape (any shape sorts every list correctly)
+        self.n_lazy_max = min(self.n_busy, int(h["big"] * 1.25) + 4)
 
     def take_tile_counts(self) -> int:
         """For the projection call: 1 if the shared tile_count buffer is known to be zero."""
@@ -209,11 +378,13 @@ class _Bins:
         """Before the stats readback: size the per-intersection and per-chunk arenas from the
         last call with the same shapes (plus 25 %), so their allocation overlaps the GPU's
         projection/scan and the emit can be enqueued before the readback (emit_early)."""
+        if self.bounded:
+            return
         hint = _size_hint.get(self.key)
         if hint is not None:
-            self.alloc_post(int(hint[0] * 1.25) + 1024)
+            self.alloc_post(int(hint["I"] * 1.25) + 1024)
             if with_chunks:
-                self.alloc_chunks(int(hint[1] * 1.25) + 16)
+                self.alloc_chunks(int(hint["chunks"] * 1.25) + 16)
 
     def __getattr__(self, name):
         # typed views of arena buffers (not used on the hot path)
@@ -234,9 +405,11 @@ class _Bins:
         p = self.p
         with _timed("bin_offsets"):
           check(L.gsr_bin_offsets(p["tile_cnt"], self.CT, p["tile_off"], p["chunk_base"], p["busy"], p["tile_end"],
-                                p["tile_cut"], p["stats_dev"], stream), "gsr_bin_offsets")
+                                p["tile_cut"], ctypes.byref(self.caps), p["stats_dev"], stream), "gsr_bin_offsets")
+        if self.bounded:
+            return
         self._host = _pinned_stats(self.device)
-        self._host.copy_(self.pre.view("stats_dev", _I32), non_blocking=True)
+        self._host.copy_(self.pre.view("stats_dev", _I32)[:8], non_blocking=True)
         self._ev = torch.cuda.Event()
         self._ev.record()
 
@@ -255,6 +428,8 @@ class _Bins:
         self.emitted = True
 
     def offsets_wait(self):
+        if self.bounded:   # nothing to wait for: the bounds are set
+            return
         ev = self._ev
         while not ev.query():   # the one host sync of the forward (spin: lowest wake-up latency)
             pass
@@ -282,6 +457,8 @@ class _Bins:
     def ensure_post(self, with_chunks: bool):
         """After the stats readback: keep the speculatively sized arenas if they are big enough
         (an emit_early into a too-small arena did nothing; sort() then emits)."""
+        if self.bounded:
+            return
         if self.post is None or self.n_isect > self.post_cap:
             self.alloc_post(int(self.n_isect * 1.25))
             self.emitted = False
@@ -289,7 +466,8 @@ class _Bins:
             self.alloc_chunks(int(self.n_chunks * 1.25))
         elif self.chunks is None:
             self.alloc_chunks(1)
-        _size_hint[self.key] = (self.n_isect, self.n_chunks)
+        _size_hint[self.key] = {"I": self.n_isect, "chunks": self.n_chunks, "max_seg": self.max_seg,
+                                "busy": self.n_busy, "big": self.n_sort_big, "mid": self.n_sort_mid}
 
     def sort(self, order, stream):
         L = lib()
@@ -303,11 +481,14 @@ class _Bins:
         self.tc[1] = True   # offsets reset the counter, the emit counted every tile back to 0
 
     def lazy_bound(self) -> int:
-        """0 when every list is sorted whole; else an upper bound on the lazily sorted tiles
-        (gsr_bin_sort_lazy: lists longer than gsr_lazy_min_len)."""
+        """0 when every list is sorted whole; else the grid of the lazy re-sort / re-render
+        (gsr_bin_sort_lazy: lists longer than gsr_lazy_min_len): the lists of >= 8192 entries
+        when min_len >= 8191 (the device flags GSR_OVF_LAZY if more tiles need it)."""
         m = lib().gsr_lazy_min_len()
         if m <= 0 or self.max_seg <= m:
             return 0
+        if self.bounded:
+            return max(1, self.n_lazy_max if m >= 8191 else self.n_busy)
         return self.n_sort_big if m >= 8191 else self.n_busy
 
     def sort_lazy(self, stream):
@@ -324,8 +505,23 @@ class _Bins:
 
 def _record_stats(b: _Bins):
     _last_stats.clear()
-    _last_stats.update(n_isect=b.n_isect, max_seg=b.max_seg, n_busy=b.n_busy, tiles=b.CT)
+    _last_stats["tiles"] = b.CT
     _last_stats["_bins"] = b
+    if b.bounded:   # read lazily (last_stats synchronises) -- the forward itself never waits
+        _last_stats["_lazy"] = True
+        _monitor_enqueue(b)
+    else:
+        _last_stats.update(n_isect=b.n_isect, max_seg=b.max_seg, n_busy=b.n_busy)
+
+
+def last_stats() -> dict:
+    """Binning statistics of the most recent forward (I, max list, busy tiles; a bounded
+    call's are read from the device here, which synchronises)."""
+    if _last_stats.pop("_lazy", False):
+        b = _last_stats["_bins"]
+        h = _hint_from(b.pre.view("stats_dev", _I32)[:8].tolist())
+        _last_stats.update(n_isect=h["I"], max_seg=h["max_seg"], n_busy=h["busy"])
+    return dict(_last_stats)
 
 
 def effective_isect(stats: dict | None = None) -> int:
@@ -377,7 +573,8 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
     V = viewmats.detach().to(device=dev, dtype=torch.float32).contiguous()
     Kc = Ks.detach().to(device=dev, dtype=torch.float32).contiguous()
     bgc = _background(bg, C, dev)
-    b = _Bins(dev, C, N, width, height)
+    b = _Bins(dev, C, N, width, height, opts.capacity, ("3d", opts.band, opts.input_mode, opts.radius_mode),
+              _chunk_entries["3d"])
     q = b.p
     with _timed("project3d_fwd"):
       check(L.gsr3d_project_fwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height,
@@ -452,7 +649,7 @@ def _sets2d(params: torch.Tensor):
     return p, F, N, int(p.stride(1)) if N > 0 else 9, int(p.stride(0))
 
 
-def _forward2d(params, bg, width, height, eps_cut, unit_sets=(0,)):
+def _forward2d(params, bg, width, height, eps_cut, unit_sets=(0,), capacity=None):
     """unit_sets[c] = parameter set rendered by camera (unit) c (non-decreasing)."""
     L = lib()
     dev = params.device
@@ -461,7 +658,7 @@ def _forward2d(params, bg, width, height, eps_cut, unit_sets=(0,)):
     C = len(unit_sets)
     sb = _set_begin(tuple(unit_sets), F, dev)
     bgc = _background(bg, C, dev)
-    b = _Bins(dev, C, N, width, height)
+    b = _Bins(dev, C, N, width, height, capacity, ("2d", tuple(unit_sets), F), _chunk_entries["2d"])
     q = b.p
     with _timed("project2d_fwd"):
       check(L.gsr2d_project_fwd(_ptr(p), N, stride, set_stride, _ptr(sb), F, C, width, height, eps_cut, q["rec"],
@@ -518,7 +715,7 @@ class _Render3D(torch.autograd.Function):
         def raster(L, q, partial, stream):
             check(L.gsr3d_raster_bwd(q["rec"], q["sorted_ids"], q["tile_off"], q["tile_end"], q["chunk_base"],
                                      q["chunk_state"], q["chunk_list"], q["stats_dev"],
-                                     b.n_chunks, C, width, height, _ptr(bgc), q["final_T"], q["last"],
+                                     b.n_chunks, b.chunk_entries, C, width, height, _ptr(bgc), q["final_T"], q["last"],
                                      _ptr(v_rgb), _ptr(v_alpha), q["k_of_s"], _ptr(partial), stream),
                   "gsr3d_raster_bwd")
         v_params = backward3d(b, ctx.meta, raster)
@@ -545,7 +742,7 @@ def backward3d(b, meta, raster) -> torch.Tensor:
               check(L.gsr3d_project_bwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height, opts.eps2d,
                                         opts.input_mode,
                                         q["depth"], q["rect"], q["isect_off"], q["cnt"], q["tile_cut"],
-                                        _ptr(partial), n0, n1, _ptr(v_params), stream),
+                                        _ptr(partial), n0, n1, q["stats_dev"], _ptr(v_params), stream),
                     "gsr3d_project_bwd")
             if opts.grad_hook is not None:
                 opts.grad_hook(v_params[n0:n1])
@@ -556,8 +753,8 @@ def backward3d(b, meta, raster) -> torch.Tensor:
 
 class _Render2D(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, params, bg, width, height, eps_cut, unit_sets):
-        rgb, alpha, b, meta = _forward2d(params, bg, width, height, eps_cut, unit_sets)
+    def forward(ctx, params, bg, width, height, eps_cut, unit_sets, capacity=None):
+        rgb, alpha, b, meta = _forward2d(params, bg, width, height, eps_cut, unit_sets, capacity)
         ctx.b = b
         ctx.meta = meta
         ctx.params_shape = params.shape
@@ -584,15 +781,16 @@ class _Render2D(torch.autograd.Function):
             with _timed("raster2d_bwd"):
               check(L.gsr2d_raster_bwd(q["rec"], q["sorted_ids"], q["tile_off"], q["tile_end"], q["chunk_base"],
                                      q["chunk_state"], q["chunk_list"], q["stats_dev"],
-                                     b.n_chunks, C, width, height, eps_cut, _ptr(bgc), q["final_T"], q["last"],
+                                     b.n_chunks, b.chunk_entries, C, width, height, eps_cut, _ptr(bgc), q["final_T"],
+                                     q["last"],
                                      _ptr(v_rgb), _ptr(v_alpha), q["k_of_s"], _ptr(partial), stream),
                   "gsr2d_raster_bwd")
             with _timed("project2d_bwd"):
               check(L.gsr2d_project_bwd(_ptr(p), N, stride, set_stride, _ptr(sb), F, C, width, height, q["rect"],
-                                      q["isect_off"], q["cnt"], q["tile_cut"], _ptr(partial), _ptr(v_params),
-                                      stream),
+                                      q["isect_off"], q["cnt"], q["tile_cut"], _ptr(partial), q["stats_dev"],
+                                      _ptr(v_params), stream),
                   "gsr2d_project_bwd")
-        return v_params.view(ctx.params_shape), None, None, None, None, None
+        return v_params.view(ctx.params_shape), None, None, None, None, None, None
 
 
 def render3d(params: torch.Tensor, viewmats: torch.Tensor, Ks: torch.Tensor, width: int, height: int,
@@ -608,17 +806,17 @@ def render3d(params: torch.Tensor, viewmats: torch.Tensor, Ks: torch.Tensor, wid
 
 
 def render2d(params: torch.Tensor, width: int, height: int, background: torch.Tensor,
-             eps_cut: float = 1e-8):
+             eps_cut: float = 1e-8, capacity: str | None = None):
     """[N,9] raw params → rgb [H,W,3], alpha [H,W] (index-order compositing)."""
     _require_device(params, "GaussianRenderer2D")
     if params.dim() != 2:
         raise ValueError(f"render2d: params must be [N,9], got {tuple(params.shape)}")
-    rgb, alpha = _Render2D.apply(params, background, int(width), int(height), float(eps_cut), (0,))
+    rgb, alpha = _Render2D.apply(params, background, int(width), int(height), float(eps_cut), (0,), capacity)
     return rgb[0], alpha[0]
 
 
 def render2d_units(params: torch.Tensor, unit_sets, width: int, height: int, background: torch.Tensor,
-                   eps_cut: float = 1e-8):
+                   eps_cut: float = 1e-8, capacity: str | None = None):
     """Multi-frame 2D batch in ONE launch sequence: params [F,N,9] (F frames' raw parameter
     sets), unit_sets[c] = the frame rendered by unit (camera) c, non-decreasing (units grouped
     by frame; a frame may have any number of units, including none).  Returns rgb [C,H,W,3],
@@ -632,4 +830,4 @@ def render2d_units(params: torch.Tensor, unit_sets, width: int, height: int, bac
     if not sets:
         raise ValueError("render2d_units: no units")
     _set_begin(sets, params.shape[0], params.device)   # validates the grouping
-    return _Render2D.apply(params, background, int(width), int(height), float(eps_cut), sets)
+    return _Render2D.apply(params, background, int(width), int(height), float(eps_cut), sets, capacity)

@@ -35,6 +35,28 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, name), f"{name} missing from {_lib.LIB_PATH}"
     assert set(_declared()) == set(_lib.EXPORTS), "ctypes prototypes out of sync with gsr.h"
     assert lib.gsr_version() >= 1
+    assert lib.gsr_abi_version() == _lib.ABI_VERSION
+
+
+def test_abi_version_matches_header():
+    from gsr import _lib
+    src = open(HEADER).read()
+    assert re.search(r"#define GSR_ABI_VERSION (\d+)", src).group(1) == str(_lib.ABI_VERSION)
+
+
+def test_overflow_bits_match_header():
+    from gsr import _lib
+    src = open(HEADER).read()
+    bits = {int(v): k for k, v in re.findall(r"#define (GSR_OVF_\w+) (\d+)", src)}
+    assert set(bits) == set(_lib.OVF_BITS), (bits, _lib.OVF_BITS)
+
+
+def test_bin_offsets_rejects_bad_caps():
+    from gsr import _lib
+    lib = _lib.lib()
+    caps = _lib.BinCaps(-5, 0, None)
+    rc = lib.gsr_bin_offsets(None, 100, None, None, None, None, None, ctypes.byref(caps), None, None)
+    assert rc == -1 and b"bad caps" in lib.gsr_last_error()
 
 
 def test_invalid_arguments_are_reported_not_launched():
@@ -56,7 +78,7 @@ def test_invalid_arguments_are_reported_not_launched():
     assert rc == -1 and b"eps_cut" in lib.gsr_last_error()
     rc = lib.gsr2d_project_fwd(None, 10, 9, 90, None, 2, 4, 64, 64, 1e-8, None, None, None, None, None, 0, None)
     assert rc == -1 and b"need set_begin" in lib.gsr_last_error()
-    rc = lib.gsr2d_project_bwd(None, 10, 9, 0, None, 1, 0, 64, 64, None, None, None, None, None, None, None)
+    rc = lib.gsr2d_project_bwd(None, 10, 9, 0, None, 1, 0, 64, 64, None, None, None, None, None, None, None, None)
     assert rc == -1 and b"bad C" in lib.gsr_last_error()
     rc = lib.gsr_bin_sort(None, None, None, None, None, None, 1, 10, 64, 64, 5, 0, 0, 0, 0, 0, 0, None, None, 0, None, None,
                           None)
@@ -102,7 +124,7 @@ def test_struct_layouts_match_header(tmp_path):
     if cc is None:
         pytest.skip("no C compiler")
     src = tmp_path / "layout.c"
-    structs = {"gsr_bin_stats": _lib.BinStats, "gsr_loss_terms": _lib.LossTerms}
+    structs = {"gsr_bin_stats": _lib.BinStats, "gsr_bin_caps": _lib.BinCaps, "gsr_loss_terms": _lib.LossTerms}
     lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "gsr.h"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
@@ -126,5 +148,5 @@ def test_loss_entry_points_validate():
     assert lib.gsr_loss_workspace(6, 576, 512) >= 6 * 16
     rc = lib.gsr_loss_iou_l1_fwd(None, None, None, None, 0, 64, 64, 1.0, None, 0, None, None, None, None)
     assert rc == -1 and b"bad C" in lib.gsr_last_error()
-    rc = lib.gsr3d_raster_bwd_loss(*([None] * 8), 1, 1, 64, 64, None, None, None, None, None, None, None)
+    rc = lib.gsr3d_raster_bwd_loss(*([None] * 8), 1, 0, 1, 64, 64, None, None, None, None, None, None, None)
     assert rc == -1 and b"loss terms" in lib.gsr_last_error()

@@ -72,3 +72,19 @@ def test_bench_args_defaults():
     a = bench.parse([])
     assert a.config == 3 and a.gpus == 1 and a.shard == "units" and a.cpu_threads == 0
     assert bench.cpu_threads(3) == 3 and bench.cpu_threads(0) >= 1
+
+
+def test_gpus_without_launcher_spawns_ranks(monkeypatch):
+    """`bench.py --gpus 2` with no launcher environment starts 2 ranks itself (never silently
+    reports n_gpus 1); a launcher whose WORLD_SIZE disagrees with --gpus is an error."""
+    import pytest
+    calls = []
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench, "_spawn_ranks", lambda args, argv: calls.append((args.gpus, argv)) or 7)
+    with pytest.raises(SystemExit) as e:
+        bench.main(["--gpus", "2", "--steps", "3"])
+    assert e.value.code == 7 and calls == [(2, ["--gpus", "2", "--steps", "3"])]
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    with pytest.raises(SystemExit) as e:
+        bench.main(["--gpus", "2"])
+    assert "WORLD_SIZE=4" in str(e.value.code)

@@ -215,3 +215,36 @@ def test_unit_and_frame_partitions():
             fs = [f for f, _ in frame_view_units(F, V, world, r)]
             assert fs == sorted(fs)
     assert frame_buckets(8, 2) == [(0, 4), (4, 8)] and frame_buckets(3, 8) == [(0, 1), (1, 2), (2, 3)]
+
+
+def test_unit_bounds_charge_touched_views():
+    """With a per-view cost the partition keeps ranks on few views: the bottleneck (max over
+    ranks of weights + view_cost x views touched) is never worse than plain weight balancing's
+    and is optimal against brute force on small cases."""
+    import itertools
+    from gsr.multiview import unit_bounds, unit_shard
+
+    def cost(b, w, rows, vc):
+        out = []
+        for g0, g1 in zip(b[:-1], b[1:]):
+            views = len({u // rows for u in range(g0, g1)})
+            out.append(sum(w[g0:g1]) + vc * views)
+        return max(out)
+
+    g = torch.Generator().manual_seed(3)
+    for C, rows, world, vc in [(6, 8, 8, 5.0), (6, 8, 4, 20.0), (3, 4, 2, 3.0), (2, 5, 3, 0.5), (6, 32, 8, 40.0)]:
+        w = [float(x) for x in torch.rand(C * rows, generator=g) * 10]
+        b = unit_bounds(C, rows, world, w, vc)
+        assert b[0] == 0 and b[-1] == C * rows and all(x <= y for x, y in zip(b, b[1:])) and len(b) == world + 1
+        plain = unit_bounds(C, rows, world, w, 0.0)
+        assert cost(b, w, rows, vc) <= cost(plain, w, rows, vc) + 1e-9
+        if C * rows <= 12:   # brute force over all contiguous partitions
+            U = C * rows
+            best = min(cost([0, *cuts, U], w, rows, vc)
+                       for cuts in itertools.combinations_with_replacement(range(U + 1), world - 1))
+            assert cost(b, w, rows, vc) <= best + 1e-6
+        seen = []
+        for r in range(world):
+            v0, v1, (b0, b1) = unit_shard(C, rows, world, r, w, vc)
+            seen += list(range(v0 * rows + b0, v0 * rows + b1))
+        assert seen == list(range(C * rows))

@@ -335,7 +335,8 @@ def _golden(name):
 
 
 GOLDEN_2D = ["n1_64x48_black", "n2_64x48_white", "n40_64x48_white", "n40_96x80_grey",
-             "n256_96x80_white", "n256_96x80_dense", "n64_offscreen_64x48"]
+             "n256_96x80_white", "n256_96x80_dense", "n64_offscreen_64x48",
+             "n2500_128x96_cfg4", "n5200_64x48_cfg4density"]
 
 
 def _run_gpu2d(p, W, H, bg, cuda, v_rgb=None, v_alpha=None):
