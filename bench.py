@@ -9,11 +9,14 @@ are resident in HBM before the timed region.  value = views (frames) rendered pe
 over the whole job.
 
 Multi-GPU (torchrun, one process per GPU, RCCL over xGMI), SURVEY.md §8(e):
-  * 3D, --shard units (default, "strong"): ONE C-view job per step; the C*th (view, tile
-    row) units are cut into `world` contiguous, work-balanced ranges (gsr.multiview.unit_shard);
-    each rank projects only the views it touches, bins only its rows, and all-reduces its
-    partial v_params in Gaussian-range buckets that overlap the projection backward.
-  * 3D, --shard views ("weak"): every rank renders C views of its own (ring offset per rank).
+  * 3D, --shard views (default, "weak"): a multi-camera batch -- every rank renders C views of
+    its own (ring offset per rank) of the same Gaussians, and the [N,14] gradient is
+    all-reduced in Gaussian-range buckets that overlap the projection backward.
+  * 3D, --shard units ("strong"): ONE C-view job per step; the C*th (view, tile row) units are
+    cut into `world` contiguous ranges balanced by list entries read plus a per-view cost
+    (gsr.multiview.unit_shard); each rank projects only the views it touches, bins only its
+    rows, and all-reduces its partial v_params in buckets (latency- and exchange-bound at
+    configs 3 and 5: DESIGN.md §5, --rank-share).
   * 2D (config 4, "strong"): 8 frames x 6 views = 48 (frame, view) units, round-robin over
     ranks; each rank renders its units batched per frame bucket and all-reduces the [8,N,9]
     gradient per bucket (async, overlapping the next bucket).
@@ -67,9 +70,11 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
-    ap.add_argument("--shard", default="units", choices=["units", "views"],
-                    help="3D, N>1: 'units' = the ranks split ONE C-view job by (view, tile row) units (strong "
-                         "scaling); 'views' = every rank renders C views of its own (weak scaling)")
+    ap.add_argument("--shard", default="views", choices=["units", "views"],
+                    help="3D, N>1: 'views' (default) = a multi-camera batch, every rank renders C views of its own "
+                         "and the Gaussian gradient is all-reduced (weak scaling); 'units' = the ranks split ONE "
+                         "C-view job by (view, tile row) units (strong scaling; latency- and exchange-bound, "
+                         "see DESIGN.md §5 and --rank-share)")
     ap.add_argument("--buckets", type=int, default=0,
                     help="all-reduce buckets (3D: Gaussian ranges of v_params; 2D: frame ranges); 0 = default "
                          "(3D 4, 2D 2; 1 on a single GPU)")
@@ -96,6 +101,8 @@ def parse(argv=None):
                     help="MIN_LEN,PREFIX: lazy depth order for 3D lists longer than MIN_LEN, sorted prefix "
                          ">= PREFIX entries (gsr_set_lazy_sort; default 16384,4096; MIN_LEN 0 disables)")
     ap.add_argument("--pmc-dir", default=PROFILES, help="where the per-config rocprofv3 PMC passes live")
+    ap.add_argument("--chunk-entries", type=str, default="",
+                    help="3D,2D backward work-unit lengths (gsr.render.set_chunk_entries; default 128,512)")
     ap.add_argument("--capacity", default="bounded", choices=["bounded", "exact"],
                     help="bounded: no host sync per step (bounds from the previous step, checked on device); "
                          "exact: one 32-byte stats read-back per forward")
@@ -447,7 +454,10 @@ class Workload:
                 self.band = (0, -1)
                 self.scaling = "weak" if world > 1 else "n/a"
                 self.layout = ("single GPU" if world == 1 else
-                               f"replicas x{world}" if cfg.index == 2 else f"view-sharded x{world} (own views)")
+                               f"replicas x{world}" if cfg.index == 2 else
+                               f"multi-camera batch: each of {world} ranks renders {C} views of its own, "
+                               f"{self.buckets} async all-reduce bucket(s) of the [N,14] gradient overlapping "
+                               "project_bwd")
                 self.v0, self.v1 = 0, C
             else:
                 self.V, self.K = ring_cameras(C, cfg.width, cfg.height)
@@ -519,13 +529,30 @@ class Workload:
                                                       self.v_alpha_all, self.th, self.weights, self.buckets,
                                                       view_cost=self.view_cost)
             return
+        if self.comm:
+            # --shard views: every rank renders its own C views; the gradient is all-reduced in
+            # Gaussian-range buckets, each launched as soon as the projection backward has
+            # enqueued it (async RCCL), overlapping the rest of the backward
+            import torch.distributed as dist
+            works, pieces = [], []
+
+            def hook(t):
+                pieces.append(t)
+                works.append(dist.all_reduce(t, async_op=True))
+            opts = R.RenderOptions3D(grad_buckets=self.buckets, grad_hook=hook)
+            p = self.params.detach().requires_grad_(True)
+            rgb, alpha = R.render3d(p, self.Vd, self.Kd, cfg.width, cfg.height, self.bg, opts)
+            torch.autograd.backward([rgb, alpha], [self.v_rgb_all, self.v_alpha_all])
+            for wk in works:
+                wk.wait()
+            # the buckets are slices of the one v_params tensor the backward returned
+            full = pieces[0]._base if pieces[0]._base is not None else pieces[0]
+            self.params.grad = full.view_as(self.params)
+            return
         opts = R.RenderOptions3D(band=self.band) if self.band != (0, -1) else R.RenderOptions3D()
         rgb, alpha = R.render3d(self.params, self.Vd[self.v0:self.v1], self.Kd[self.v0:self.v1], cfg.width,
                                 cfg.height, self.bg, opts)
         torch.autograd.backward([rgb, alpha], [self.v_rgb_all[self.v0:self.v1], self.v_alpha_all[self.v0:self.v1]])
-        if self.comm:   # --shard views: one all-reduce of the full gradient
-            import torch.distributed as dist
-            dist.all_reduce(self.params.grad)
 
     def _loss_step(self):
         """The reference training loss on the render: IoU + L1 image + ssim_lambda * (1 - SSIM)
@@ -592,7 +619,6 @@ def time_steps(w: Workload, steps: int, warmup: int, dist=None, graph: bool = Fa
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        R.enable_kernel_timing(True, only={dom_name} if dom_name else None)
         with torch.cuda.graph(g):
             for _ in range(steps):
                 w.step()
@@ -613,6 +639,15 @@ def time_steps(w: Workload, steps: int, warmup: int, dist=None, graph: bool = Fa
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if g is not None:
+        # ROCm rejects timing events inside a captured graph ("External events are disallowed
+        # in rocm"): the dominant kernel is timed with HIP events around each of its launches
+        # on its stream over the same number of eager bounded steps (no host sync between
+        # them), right after the graph-timed region -- the same kernel on the same inputs
+        R.enable_kernel_timing(True, only={dom_name} if dom_name else None)
+        for _ in range(steps):
+            w.step()
+        torch.cuda.synchronize()
     ktimes = R.kernel_times_ms()
     R.enable_kernel_timing(False)
     R.check_overflow(w.dev)   # a bounded step over its bounds would have rendered NaN: fail loudly
@@ -644,6 +679,9 @@ def roofline(w: Workload, dom_name, dom, args):
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "traffic_source": os.path.relpath(tfile, ROOT) if traffic is not None else None,
             "algorithmic_bytes": alg, "avg_ms": dom_ms, "launches": dom_n,
+            "timing": ("HIP events around each launch on its stream, over the timed steps" if not args.graph else
+                       "HIP events around each launch on its stream, over as many eager bounded steps run right "
+                       "after the graph-timed region (ROCm rejects timing events inside a captured graph)"),
             "valu": valu_from_csv(sq, sym) if sq else None,
             "units_per_launch": {"C": C, "P": P, "N": cfg.N, "I": I, "I_eff": I_eff}}, (C, P, I, I_eff)
 
@@ -729,6 +767,10 @@ def main(argv=None):
     from gsr.scenes import CONFIGS
     cfg = CONFIGS[args.config]
     R.set_capacity_mode(args.capacity)
+    if args.chunk_entries:
+        c3, c2 = (int(x) for x in args.chunk_entries.split(","))
+        R.set_chunk_entries("3d", c3)
+        R.set_chunk_entries("2d", c2)
     if args.graph == -1:
         args.graph = int(world == 1 and args.capacity == "bounded" and args.loss == "none")
     if args.graph and args.capacity != "bounded":
@@ -805,7 +847,7 @@ def main(argv=None):
         "config": {"workload": cfg.name, "N_gauss": cfg.N, "width": cfg.width, "height": cfg.height,
                    "views": cfg.views, "frames": FRAMES_2D if cfg.mode == "2d" else 1,
                    "units_per_step": w.units_total, "background": "white", "loss": args.loss,
-                   "capacity": args.capacity,
+                   "capacity": args.capacity, "chunk_entries": dict(R._chunk_entries),
                    "launch": (f"one HIP graph of the {args.steps} timed steps, replayed once" if args.graph
                               else "eager launches"),
                    "parallelism": w.layout + (f"; backend {backend}" + (" (RCCL)" if backend == "nccl" else "")

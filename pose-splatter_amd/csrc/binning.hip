@@ -241,13 +241,15 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__
                                                       int32_t* __restrict__ tile_count, uint64_t* __restrict__ keys,
                                                       int32_t* __restrict__ k_of_slot, int per_block,
                                                       const gsr_bin_stats* __restrict__ stats, int64_t cap) {
-  if (stats->overflow & kOvfCapacity) {   // bounded call over its caps: nothing is emitted
-    emit_skip_counts(tile_count, tw * th);
+  // launched before the host has read I back (gsr_bin_emit): a workspace too small for this
+  // call's I makes every workgroup leave at once, and the host emits again with a larger one.
+  // A bounded call over its caps emits nothing.  (Both words load together, one branch.)
+  const int ovf = stats->overflow & kOvfCapacity;
+  const int64_t n_isect = stats->n_isect;
+  if (ovf | (n_isect > cap)) {
+    if (ovf) emit_skip_counts(tile_count, tw * th);
     return;
   }
-  // launched before the host has read I back (gsr_bin_emit): a workspace too small for this
-  // call's I makes every workgroup leave at once, and the host emits again with a larger one
-  if (stats->n_isect > cap) return;
   // Slots are claimed by counting each tile's count down to zero (slot = tile start +
   // remaining count - 1): no separate cursor array, and tile_count is left zeroed.
   extern __shared__ int hist[];
@@ -328,11 +330,12 @@ __global__ __launch_bounds__(kStageThreads) void k_emit_staged(
     int64_t N, int tw, int th, int order, const int32_t* __restrict__ tile_offset, int32_t* __restrict__ tile_count,
     uint64_t* __restrict__ keys, int32_t* __restrict__ k_of_slot, const gsr_bin_stats* __restrict__ stats,
     int64_t cap) {
-  if (stats->overflow & kOvfCapacity) {   // see k_emit
-    emit_skip_counts(tile_count, tw * th);
+  const int ovf = stats->overflow & kOvfCapacity;   // see k_emit
+  const int64_t n_isect = stats->n_isect;
+  if (ovf | (n_isect > cap)) {
+    if (ovf) emit_skip_counts(tile_count, tw * th);
     return;
   }
-  if (stats->n_isect > cap) return;   // see k_emit
   constexpr int NT = kStageThreads;
   constexpr int kStagePer = GPT * NT;   // Gaussians per workgroup
   extern __shared__ uint64_t s_key[];   // [kStageCap]
@@ -647,21 +650,15 @@ __global__ __launch_bounds__(NT) void k_segsort(
     int32_t* __restrict__ k_of_s, const LazyArgs lz, gsr_bin_stats* __restrict__ stats) {
   extern __shared__ uint64_t s_keys[];
   int* s_hist = (int*)(s_keys + lds_keys);
-  if (stats->overflow & kOvfCapacity) return;   // bounded call over its caps: nothing to sort
-  int ct;
   // the grid covers gridDim.x lists (the busy count read back, or a bound): more lists than
-  // that is flagged for the raster (which then writes NaN) instead of leaving lists unsorted
-  if (lz.mode == 2) {   // the tiles whose forward ran past their sorted prefix
-    const int cnt = *lz.count;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && cnt > (int)gridDim.x) atomicOr(&stats->overflow, GSR_OVF_LAZY);
-    if ((int)blockIdx.x >= cnt) return;
-    ct = lz.list[blockIdx.x];
-  } else {
-    const int nb = stats->n_busy;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && nb > (int)gridDim.x) atomicOr(&stats->overflow, GSR_OVF_BUSY);
-    if ((int)blockIdx.x >= nb) return;
-    ct = busy[blockIdx.x];
-  }
+  // that is flagged for the raster (which then writes NaN) instead of leaving lists unsorted.
+  // The counts and this workgroup's tile load together (both lists hold a slot per grid slot).
+  const int ct = lz.mode == 2 ? lz.list[blockIdx.x] : busy[blockIdx.x];
+  const int nb = lz.mode == 2 ? *lz.count : stats->n_busy;
+  if ((stats->overflow & kOvfCapacity) | (ct < 0)) return;   // bounded call over its caps: nothing to sort
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nb > (int)gridDim.x)
+    atomicOr(&stats->overflow, lz.mode == 2 ? GSR_OVF_LAZY : GSR_OVF_BUSY);
+  if ((int)blockIdx.x >= nb) return;
   const int start = tile_offset[ct];
   const int len = tile_offset[ct + 1] - start;
   uint64_t* seg = keys + start;

@@ -82,11 +82,10 @@ __global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
   const int g_loc = threadIdx.x % G;
   const int slot = threadIdx.x / G;
   const int64_t n = n_begin + (int64_t)blockIdx.x * G + g_loc;
-  if (stats != nullptr && stats->overflow) {   // the forward's bounds did not hold: NaN rows
-    if (slot == 0 && n < n_end)
-      for (int k = 0; k < 14; ++k) v_params[n * 14 + k] = __builtin_nanf("");
-    return;
-  }
+  // the forward's bounds did not hold: NaN rows, and no partial row is read (their offsets may
+  // lie past the buffers).  The flag loads with the first gathers and is tested inside the
+  // camera loop, so it adds no round trip of its own.
+  const bool ovf = stats != nullptr && stats->overflow != 0;
   const bool active = slot < CPB && n < n_end;
   const int T = tw * th;
   float v_m[3] = {0.f, 0.f, 0.f};
@@ -106,7 +105,7 @@ __global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
       const uint2 rc = rect[cn];
       const int off = isect_offset[cn];
       const uint64_t key = sort_key(depth, cn, GSR_ORDER_DEPTH);
-      if (cnt <= 0) continue;
+      if (cnt <= 0 || ovf) continue;
       float acc[kPartial];
 #pragma unroll
       for (int v = 0; v < kPartial; ++v) acc[v] = 0.f;
@@ -234,6 +233,11 @@ __global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
   }
   any |= s_any[threadIdx.x];
   float* out = v_params + n * 14;
+  if (ovf) {
+#pragma unroll
+    for (int k = 0; k < 14; ++k) out[k] = __builtin_nanf("");
+    return;
+  }
   if (!any) {
 #pragma unroll
     for (int k = 0; k < 14; ++k) out[k] = 0.f;
@@ -333,11 +337,9 @@ __global__ __launch_bounds__(kBwdThreads) void k_project2d_bwd_staged(
   const int f = blockIdx.y;
   const int64_t n = (int64_t)blockIdx.x * kBwdThreads + threadIdx.x;
   const bool own = n < N;
-  if (stats != nullptr && stats->overflow) {   // the forward's bounds did not hold: NaN rows
-    if (own)
-      for (int k = 0; k < 9; ++k) v_params[((int64_t)f * N + n) * 9 + k] = __builtin_nanf("");
-    return;
-  }
+  // the forward's bounds did not hold: NaN rows, no partial row read (loaded with the first
+  // gathers, tested in the camera loop: no round trip of its own)
+  const bool ovf = stats != nullptr && stats->overflow != 0;
   const int c0 = set_begin ? set_begin[f] : 0, c1 = set_begin ? set_begin[f + 1] : n_cam;
   const float4* rows4 = reinterpret_cast<const float4*>(partial);
   static_assert(kPartialStride == 12, "a partial row is 3 float4");
@@ -347,7 +349,7 @@ __global__ __launch_bounds__(kBwdThreads) void k_project2d_bwd_staged(
   bool any = false;
   for (int c = c0; c < c1; ++c) {
     const int64_t cn = (int64_t)c * N + n;
-    const int cnt = own ? isect_count[cn] : 0;
+    const int cnt = own && !ovf ? isect_count[cn] : 0;
     uint2 r = make_uint2(0u, 0u);
     int off = 0;
     if (cnt > 0) {
@@ -409,6 +411,11 @@ __global__ __launch_bounds__(kBwdThreads) void k_project2d_bwd_staged(
   if (!own) return;
   const int64_t fn = (int64_t)f * N + n;
   float* out = v_params + fn * 9;
+  if (ovf) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) out[k] = __builtin_nanf("");
+    return;
+  }
   if (!any) {
 #pragma unroll
     for (int k = 0; k < 9; ++k) out[k] = 0.f;

@@ -331,28 +331,32 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   // n_busy sizes the grid (the read-back busy count or a bound); the tiles come from the device
   // count, which the sort has checked against that bound (GSR_OVF_BUSY)
   const int busy_blocks = busy_grid<LPP>(n_busy);
-  if (stats->overflow) {
+  // XCD-aware mapping: workgroups are dealt to the 8 XCDs round-robin by id, so the G
+  // workgroups of a tile get ids 8G*k + 8*sub + x (same id mod 8): they share one XCD's L2
+  // for the tile's records.  Busy tile u = 8k + x, in longest-first order.
+  const int u = ((int)blockIdx.x / (8 * FS::G)) * 8 + ((int)blockIdx.x & 7);
+  const int sub = ((int)blockIdx.x >> 3) & (FS::G - 1);
+  // the device counts and this workgroup's tile are loaded together (one round trip before
+  // any work, as with a host count); the tile index is clamped in range and used only if real
+  if (lz.rerun) order = lz.list;
+  const int ct = order[min(u, (int)CT - 1)];
+  const int ovf = stats->overflow;
+  const int nb_dev = lz.rerun ? *lz.count : stats->n_busy;
+  if (ovf | (ct < 0)) {
     nan_fill(CT, W, H, tw, th, out_rgb, out_alpha);
     return;
   }
   if (lz.rerun) {
-    order = lz.list;
-    n_busy = min(n_busy, *lz.count);
+    n_busy = min(n_busy, nb_dev);
   } else {
-    n_busy = stats->n_busy;
+    n_busy = nb_dev;
     if ((int)blockIdx.x >= busy_blocks) {
       fill_empty<IS2D>(order, tile_offset, n_busy, busy_blocks, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
                        out_last, tile_end, tile_cut);
       return;
     }
   }
-  // XCD-aware mapping: workgroups are dealt to the 8 XCDs round-robin by id, so the G
-  // workgroups of a tile get ids 8G*k + 8*sub + x (same id mod 8): they share one XCD's L2
-  // for the tile's records.  Busy tile u = 8k + x, in longest-first order.
-  const int u = ((int)blockIdx.x / (8 * FS::G)) * 8 + ((int)blockIdx.x & 7);
-  const int sub = ((int)blockIdx.x >> 3) & (FS::G - 1);
   if (u >= n_busy) return;
-  const int ct = order[u];
   int c, ty, tx;
   tile_coords(ct, tw, th, c, ty, tx);
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -694,15 +698,19 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
   __shared__ int s_max;
   static_assert(kChunk3 == 128, "a round half is one chunk");
   const int busy_blocks = (n_busy + 7) & ~7;   // n_busy: the grid's bound (see k_raster_fwd)
-  if (stats->overflow) {
+  // device counts and this workgroup's tile in one round trip (see k_raster_fwd)
+  if (lz.rerun) order = lz.list;
+  const int ct = order[min((int)blockIdx.x, (int)CT - 1)];
+  const int ovf = stats->overflow;
+  const int nb_dev = lz.rerun ? *lz.count : stats->n_busy;
+  if (ovf | (ct < 0)) {
     nan_fill(CT, W, H, tw, th, out_rgb, out_alpha);
     return;
   }
   if (lz.rerun) {
-    order = lz.list;
-    n_busy = min(n_busy, *lz.count);
+    n_busy = min(n_busy, nb_dev);
   } else {
-    n_busy = stats->n_busy;
+    n_busy = nb_dev;
     if ((int)blockIdx.x >= busy_blocks) {
       fill_empty<IS2D>(order, tile_offset, n_busy, busy_blocks, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
                        out_last, tile_end, tile_cut);
@@ -710,7 +718,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
     }
   }
   if ((int)blockIdx.x >= n_busy) return;
-  const int ct = order[blockIdx.x];
   int c, ty, tx;
   tile_coords(ct, tw, th, c, ty, tx);
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1062,8 +1069,13 @@ __device__ __forceinline__ void loss_cotangent(const gsr_loss_terms& lt, int C, 
 // T_i = T_{i+1} / (1 - a_i) as in 3D, except at the pixel's last entry, whose T comes from
 // the forward (final_T .y) -- the one entry whose 1 - a may be exactly 0.  No clamp: every
 // valid pair feeds the sigma / opacity gradients.
+// minimum workgroups per CU of the MULTI variant (build knob for measurements; the one-sub-chunk
+// variant fits 5 per CU in 84 VGPRs on its own)
+#ifndef GSR_BWD_MULTI_MINB
+#define GSR_BWD_MULTI_MINB 1
+#endif
 template <bool LOSS, bool IS2D, bool MULTI>
-__global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
+__global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : 1) void k_raster_bwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ tile_end, const int32_t* __restrict__ chunk_base,
     const float4* __restrict__ ckpt, int W, int H, int tw, int th,
@@ -1085,12 +1097,15 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
   // one workgroup per grid slot; slots past the forward's active-chunk count exit at once
   // the chunk's descriptor {first entry, entries (>= 1), chunk record row, tile} -- one load
   // (read before the bound check: the list has a slot for every grid slot)
-  const int4 cd = reinterpret_cast<const int4*>(chunk_list)[blockIdx.x];
-  if (stats->overflow || (int)blockIdx.x >= stats->n_active) return;
+  // The descriptor and the three stats words load together and ONE branch tests them (separate
+  // tests made the compiler wait for each load in turn: three extra round trips per workgroup).
   // MULTI = false: units of exactly one sub-chunk (no loop: the loop's back-edge keeps ~40 more
-  // VGPRs live and costs a wave per SIMD); a forward with longer units is flagged, not half done
-  if (!MULTI && stats->chunk_entries != kChunk3) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&stats->overflow, GSR_OVF_UNIT);
+  // VGPRs live and costs a wave per SIMD); a forward with longer units is flagged, not half done.
+  const int4 cd = reinterpret_cast<const int4*>(chunk_list)[blockIdx.x];
+  const int n_act = stats->n_active, ovf = stats->overflow, ce = stats->chunk_entries;
+  const bool unit_bad = !MULTI && ce != kChunk3;
+  if ((ovf != 0) | ((int)blockIdx.x >= n_act) | unit_bad | (cd.y <= 0)) {
+    if (unit_bad && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&stats->overflow, GSR_OVF_UNIT);
     return;
   }
   const int b0 = cd.x, n = cd.y, chunk = cd.z, ct = cd.w;
@@ -1159,6 +1174,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
   int wlast = last;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wlast = max(wlast, __shfl_xor(wlast, o, 64));
+  wlast = __builtin_amdgcn_readfirstlane(wlast);   // wave-uniform: an SGPR across the sub-chunk loop
   Splat sp = {};
   if (threadIdx.x < sn) sp = rec[id_mine];
   const int fg = lane / kPartial, fq = lane - kPartial * (lane / kPartial);
@@ -1172,12 +1188,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
       s_p[0][threadIdx.x] = sp.p0;
       s_p[1][threadIdx.x] = sp.p1;
       s_p[2][threadIdx.x] = sp.p2;
-    }
-    // the next (earlier) sub-chunk's ids and sort positions, in flight during this one's walk
-    int id_next = 0, kos_next = 0;
-    if (sub > 0 && threadIdx.x < kChunk3) {
-      id_next = ids[sb0 - kChunk3 + threadIdx.x];
-      kos_next = k_of_s[sb0 - kChunk3 + threadIdx.x];
     }
     for (int i = threadIdx.x; i < kPartial * 4 * (kChunk3 + 1); i += kRasterThreads) (&L[0][0][0])[i] = 0.f;
     if (threadIdx.x == 0) {
@@ -1301,8 +1311,14 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
       }
       __builtin_amdgcn_wave_barrier();
     }
-    // the next sub-chunk's records, gathered while this one's rows are summed and stored
-    if (sub > 0 && threadIdx.x < kChunk3) sp = rec[id_next];
+    // the next (earlier) sub-chunk's ids, sort positions and records, gathered while this
+    // one's rows are summed and stored (not during the walk: registers)
+    int kos_next = 0;
+    if (sub > 0 && threadIdx.x < kChunk3) {
+      const int id_next = ids[sb0 - kChunk3 + threadIdx.x];
+      kos_next = k_of_s[sb0 - kChunk3 + threadIdx.x];
+      sp = rec[id_next];
+    }
     __syncthreads();
     if (threadIdx.x < sn) {
       const int k = threadIdx.x;
@@ -1318,7 +1334,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_bwd(
     }
     sb0 -= kChunk3;
     sn = kChunk3;
-    id_mine = id_next;
     kos_mine = kos_next;
   }
 }

@@ -89,10 +89,13 @@ class CapacityOverflowError(RuntimeError):
 
 
 _capacity_default = "exact"
-# list entries per backward work unit (gsr_bin_caps.chunk_entries): 3D lists stop early and
-# the heavy tiles need the chunk-parallel backward's spread; 2D lists are walked whole, so
-# longer units re-read the pixel state and write chunk records 4x less often
-_chunk_entries = {"3d": 128, "2d": 512}
+# list entries per backward work unit (gsr_bin_caps.chunk_entries).  Units of several 128-entry
+# sub-chunks re-read the pixel state and write chunk records less often, but the sub-chunk
+# loop's back-edge costs the backward a wave per SIMD (127 VGPRs, 84 without the loop), which
+# the saved traffic does not repay: config 4 raster bwd 19.0 ms at 128 against 20.1 / 20.2 ms
+# at 256 / 512 (21.5-22.8 ms when forced to 5 waves, with spills); config 3 148 vs 167 us at
+# 256 (tools/gpu_units.sh, profiles/r03_units_*.json).  128 for both.
+_chunk_entries = {"3d": 128, "2d": 128}
 
 
 def set_chunk_entries(mode: str, entries: int) -> None:

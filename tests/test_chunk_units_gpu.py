@@ -60,7 +60,7 @@ def test_3d_units_match_single_chunks(cuda, units):
     grad_close(got[2], ref[2], what=f"3d grad, {units}-entry units")
 
 
-@pytest.mark.parametrize("units", [128, 256, 1024, 4096])
+@pytest.mark.parametrize("units", [256, 512, 1024, 4096])
 def test_2d_units_match_default(cuda, units):
     from gsr import render as R
     from gsr.scenes import gaussians2d
@@ -78,8 +78,8 @@ def test_2d_units_match_default(cuda, units):
         torch.autograd.backward([rgb, alpha], [vr, va])
         return rgb.detach().cpu(), alpha.detach().cpu(), pg.grad.cpu()
 
-    ref = run()   # default: 512-entry units
-    assert R.last_stats()["_bins"].chunk_entries == 512
+    ref = run()   # default: 128-entry units (no sub-chunk loop)
+    assert R.last_stats()["_bins"].chunk_entries == 128
     with chunk_entries("2d", units):
         got = run()
     assert torch.equal(ref[1], got[1])
