@@ -70,7 +70,8 @@ def test_byte_formulas_and_allreduce_model():
 
 def test_bench_args_defaults():
     a = bench.parse([])
-    assert a.config == 3 and a.gpus == 1 and a.shard == "units" and a.cpu_threads == 0
+    assert a.config == 3 and a.gpus == 1 and a.shard == "views" and a.cpu_threads == 0
+    assert a.capacity == "bounded" and a.graph == -1
     assert bench.cpu_threads(3) == 3 and bench.cpu_threads(0) >= 1
 
 
