@@ -300,7 +300,9 @@ int gsr_bin_sort_lazy(const float* depth, const uint32_t* rect, const int32_t* i
  * tile_end [CT] (1 + max last over the tile, or the tile's start), tile_cut [CT] (sort key
  * of the tile's entry at tile_end, ~0 if none: an entry has a partial row iff its key is
  * below its tile's cut), and for the
- * chunk-parallel backward: chunk_state [n_chunks*256*4] ({T at the chunk's end, the rgb
+ * chunk-parallel backward (both NULL: a forward with no backward to follow -- no records are
+ * written and tile_end keeps the raw maximum of last, -1 for none; tile_cut is not set):
+ * chunk_state [n_chunks*256*4] ({T at the chunk's end, the rgb
  * sum of all later chunks} per pixel of the tile, for every GSR_CHUNK-entry chunk the tile's
  * walk reached) and chunk_list [n_chunks][4] (a descriptor {first sorted entry, entry count, chunk_state row, tile} for
  * each chunk before its tile's tile_end, in no particular order; their count is added to

@@ -70,16 +70,17 @@ static int zero_counts(int32_t* p, int64_t n, hipStream_t s) {
 // through isect_offset, the tile sort orders entries by key, and each Gaussian's rows are
 // summed in rect order -- so results stay bitwise deterministic.  s_cnt: the items' counts.
 constexpr int kProjItems = kProjPerBlock / kProjThreads;
+template <int ITEMS = kProjItems>
 __device__ __forceinline__ void alloc_offsets(const int* s_cnt, int m, int64_t cn0, int32_t* __restrict__ counter,
                                               int32_t* __restrict__ isect_offset) {
   __shared__ int s_tmp[kProjThreads / 64 + 1];
   __shared__ int s_base;
   __syncthreads();
-  int v[kProjItems];
+  int v[ITEMS];
   int acc = 0;
 #pragma unroll
-  for (int j = 0; j < kProjItems; ++j) {
-    const int i = threadIdx.x * kProjItems + j;
+  for (int j = 0; j < ITEMS; ++j) {
+    const int i = threadIdx.x * ITEMS + j;
     v[j] = i < m ? s_cnt[i] : 0;
     acc += v[j];
   }
@@ -89,14 +90,17 @@ __device__ __forceinline__ void alloc_offsets(const int* s_cnt, int m, int64_t c
   __syncthreads();
   run += s_base;
 #pragma unroll
-  for (int j = 0; j < kProjItems; ++j) {
-    const int i = threadIdx.x * kProjItems + j;
+  for (int j = 0; j < ITEMS; ++j) {
+    const int i = threadIdx.x * ITEMS + j;
     if (i < m) isect_offset[cn0 + i] = run;
     run += v[j];
   }
 }
 
-template <int RMODE>
+// ITEMS Gaussians per thread: 4 (1024 per workgroup) when the call has enough workgroups to
+// fill the chip, else 1 (a single small view, a multi-GPU rank's share: 4 serial items per
+// thread were the kernel's latency -- config 2 12.4 us)
+template <int RMODE, int ITEMS>
 __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
     const float* __restrict__ params, int64_t N, int64_t stride, const float* __restrict__ viewmats,
     const float* __restrict__ Ks, int W, int H, float near_plane, float far_plane,
@@ -104,7 +108,8 @@ __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
     Splat* __restrict__ rec, float* __restrict__ depth, uint2* __restrict__ rect, int32_t* __restrict__ cnt,
     int32_t* __restrict__ tile_count, int32_t* __restrict__ counter, int32_t* __restrict__ isect_offset) {
   extern __shared__ int hist[];
-  __shared__ int s_cnt[kProjPerBlock];
+  constexpr int kPer = ITEMS * kProjThreads;
+  __shared__ int s_cnt[kPer];
   const int c = blockIdx.y;
   const int T = tw * th;
   int32_t* gcount = tile_count + (int64_t)c * T;
@@ -116,8 +121,8 @@ __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
   // this camera's share of the band [band_y0, band_y1) of camera-major global tile rows
   // (row r of camera c is global row c*th + r)
   const int by0 = min(max(band_y0 - c * th, 0), th), by1 = min(max(band_y1 - c * th, 0), th);
-  const int64_t n0 = (int64_t)blockIdx.x * kProjPerBlock;
-  const int64_t n1 = min(N, n0 + kProjPerBlock);
+  const int64_t n0 = (int64_t)blockIdx.x * kPer;
+  const int64_t n1 = min(N, n0 + kPer);
   for (int64_t n = n0 + threadIdx.x; n < n1; n += blockDim.x) {
     const int64_t cn = (int64_t)c * N + n;
     const Act3D a = activate3d(params + n * stride, input_mode);
@@ -179,7 +184,7 @@ __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
     cnt[cn] = s_cnt[n - n0] = (x1 - x0) * (y1 - y0);
   }
   if (use_lds) hist_flush(hist, gcount, T);
-  alloc_offsets(s_cnt, (int)(n1 - n0), (int64_t)c * N + n0, counter, isect_offset);
+  alloc_offsets<ITEMS>(s_cnt, (int)(n1 - n0), (int64_t)c * N + n0, counter, isect_offset);
 }
 
 // Parameter set of camera c: cameras are grouped by set, set f owning cameras
@@ -297,18 +302,23 @@ int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride, const 
   const int T = tw * th;
   const int use_lds = T <= kHistMaxTiles;
   const size_t lds = use_lds ? (size_t)T * sizeof(int) : 0;
-  dim3 grid(ceil_div(N, kProjPerBlock), C);
   hipStream_t s = (hipStream_t)stream;
-  if (radius_mode == GSR_RADIUS_OPACITY_AABB)
-    hipLaunchKernelGGL(k_project3d_fwd<GSR_RADIUS_OPACITY_AABB>, grid, dim3(kProjThreads), lds, s,
-                       params, N, row_stride, viewmats, Ks, width, height, near_plane, far_plane,
-                       radius_clip, eps2d, input_mode, tw, th, band_y0, band_y1, use_lds, (Splat*)rec, depth,
-                       (uint2*)rect, isect_count, tile_count, tile_count + (int64_t)C * T, isect_offset);
-  else
-    hipLaunchKernelGGL(k_project3d_fwd<GSR_RADIUS_ISOTROPIC_3SIGMA>, grid, dim3(kProjThreads), lds, s,
-                       params, N, row_stride, viewmats, Ks, width, height, near_plane, far_plane,
-                       radius_clip, eps2d, input_mode, tw, th, band_y0, band_y1, use_lds, (Splat*)rec, depth,
-                       (uint2*)rect, isect_count, tile_count, tile_count + (int64_t)C * T, isect_offset);
+  // one item per thread unless 4 per thread still gives >= 2 workgroups per CU
+  const bool wide = (int64_t)ceil_div(N, kProjPerBlock) * C >= 512;
+  const dim3 grid(ceil_div(N, wide ? kProjPerBlock : kProjThreads), C);
+#define GSR_PROJ3D_LAUNCH(RM, IT)                                                                              \
+  hipLaunchKernelGGL((k_project3d_fwd<RM, IT>), grid, dim3(kProjThreads), lds, s, params, N, row_stride, viewmats, \
+                     Ks, width, height, near_plane, far_plane, radius_clip, eps2d, input_mode, tw, th, band_y0,      \
+                     band_y1, use_lds, (Splat*)rec, depth, (uint2*)rect, isect_count, tile_count,                   \
+                     tile_count + (int64_t)C * T, isect_offset)
+  if (radius_mode == GSR_RADIUS_OPACITY_AABB) {
+    if (wide) GSR_PROJ3D_LAUNCH(GSR_RADIUS_OPACITY_AABB, kProjItems);
+    else GSR_PROJ3D_LAUNCH(GSR_RADIUS_OPACITY_AABB, 1);
+  } else {
+    if (wide) GSR_PROJ3D_LAUNCH(GSR_RADIUS_ISOTROPIC_3SIGMA, kProjItems);
+    else GSR_PROJ3D_LAUNCH(GSR_RADIUS_ISOTROPIC_3SIGMA, 1);
+  }
+#undef GSR_PROJ3D_LAUNCH
   GSR_LAUNCH_CHECK("k_project3d_fwd");
   return GSR_OK;
 }

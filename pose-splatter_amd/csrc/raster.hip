@@ -342,7 +342,10 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   const int ct = order[min(u, (int)CT - 1)];
   const int ovf = stats->overflow;
   const int nb_dev = lz.rerun ? *lz.count : stats->n_busy;
-  if (ovf | (ct < 0)) {
+  // (a lazy re-render's list holds only *lz.count tiles: slots past it are stale, never a fault)
+  if (ovf | ((ct < 0) & (u < nb_dev))) {
+    // (the sticky status is also set here: a forward with no backward skips the finalize)
+    if (blockIdx.x == 0 && threadIdx.x == 0 && stats->status != nullptr) atomicOr(stats->status, ovf);
     nan_fill(CT, W, H, tw, th, out_rgb, out_alpha);
     return;
   }
@@ -434,7 +437,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
       if (hb >= end || __ballot(!done) == 0ull) break;
       if (hb > start && ((hb - start) & umask) == 0) {   // entering chunk kcur+1
         const float Dr = PG::sum(dr), Dg = PG::sum(dg), Db = PG::sum(db);
-        if (q == 0) ckpt[(int64_t)(cbase + kcur) * kRasterThreads + bwd_pixel_slot(il, jl)] = make_float4(Ts, Dr, Dg, Db);
+        if (q == 0 && ckpt) ckpt[(int64_t)(cbase + kcur) * kRasterThreads + bwd_pixel_slot(il, jl)] = make_float4(Ts, Dr, Dg, Db);
         cr += Dr;
         cg += Dg;
         cb += Db;
@@ -521,7 +524,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     if (__ballot(!done) == 0ull) return false;
     if (b0 > start && ((b0 - start) & umask) == 0) {   // entering chunk kcur+1
       const float Dr = quad_sum(dr), Dg = quad_sum(dg), Db = quad_sum(db);
-      if (q == 0) ckpt[(int64_t)(cbase + kcur) * kRasterThreads + bwd_pixel_slot(il, jl)] = make_float4(Ts, Dr, Dg, Db);
+      if (q == 0 && ckpt) ckpt[(int64_t)(cbase + kcur) * kRasterThreads + bwd_pixel_slot(il, jl)] = make_float4(Ts, Dr, Dg, Db);
       cr += Dr;
       cg += Dg;
       cb += Db;
@@ -604,7 +607,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   } else {
     last = PG::max_i(last);
   }
-  if (end > start) {
+  if (end > start && ckpt) {   // (no chunk records: a forward with no backward to follow)
     // Turn this pixel's chunk records {T at chunk start, chunk colour sum} into what the
     // backward needs at each chunk's END: {T_end, suffix colour sum of the later chunks}
     // (positive terms, summed back to front).  The pixel's LPP lanes split the chunks into
@@ -703,7 +706,10 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
   const int ct = order[min((int)blockIdx.x, (int)CT - 1)];
   const int ovf = stats->overflow;
   const int nb_dev = lz.rerun ? *lz.count : stats->n_busy;
-  if (ovf | (ct < 0)) {
+  // (a lazy re-render's list holds only *lz.count tiles: slots past it are stale, never a fault)
+  if (ovf | ((ct < 0) & ((int)blockIdx.x < nb_dev))) {
+    // (the sticky status is also set here: a forward with no backward skips the finalize)
+    if (blockIdx.x == 0 && threadIdx.x == 0 && stats->status != nullptr) atomicOr(stats->status, ovf);
     nan_fill(CT, W, H, tw, th, out_rgb, out_alpha);
     return;
   }
@@ -767,7 +773,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
       const int hb = rb + 128 * h;
       if (hb >= end || __ballot(!done) == 0ull) break;
       if (hb > start && ((hb - start) & umask) == 0) {   // entering chunk kcur+1 (every few halves)
-        ckpt[(int64_t)(cbase + kcur) * kRasterThreads + threadIdx.x] = make_float4(Ts, dr, dg, db);
+        if (ckpt) ckpt[(int64_t)(cbase + kcur) * kRasterThreads + threadIdx.x] = make_float4(Ts, dr, dg, db);
         cr += dr;
         cg += dg;
         cb += db;
@@ -897,7 +903,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
   cr += dr;
   cg += dg;
   cb += db;
-  if (end > start) {
+  if (end > start && ckpt) {
     // chunk records {T at chunk start, chunk colour} -> what the backward needs at each chunk's
     // END: {T_end, suffix colour sum of the later chunks}, back to front (records re-read 8 at a time)
     float4* ck = ckpt + (int64_t)cbase * kRasterThreads + threadIdx.x;
@@ -1448,7 +1454,8 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
                        (int)n_busy, CT, tile_cut, cut2d, lz, stats);
   }
   GSR_LAUNCH_CHECK(who);
-  if (finalize && n_busy > 0) {
+  // no chunk list: a forward with no backward to follow (no records, no finalize)
+  if (finalize && n_busy > 0 && chunk_list != nullptr) {
     hipLaunchKernelGGL(k_raster_finalize, dim3(ceil_div(n_busy, kRasterThreads)), dim3(kRasterThreads), 0, s,
                        depth, sorted_ids, tile_offset, tile_order, (int)n_busy, chunk_base, tile_end,
                        tile_cut, stats, chunk_list, IS2D ? GSR_ORDER_INDEX : GSR_ORDER_DEPTH);
@@ -1524,7 +1531,7 @@ int gsr3d_raster_fwd_lazy(const float* rec, const float* depth, int32_t* sorted_
                          width, height, 0.f, bg, n_lazy_max, stats, rgb, alpha, final_T, last, tile_end, tile_cut,
                          chunk_state, chunk_list, stream, l2, lanes, false);
   if (rc != GSR_OK) return rc;
-  if (n_busy > 0) {
+  if (n_busy > 0 && chunk_list != nullptr) {
     hipLaunchKernelGGL(k_raster_finalize, dim3(ceil_div(n_busy, kRasterThreads)), dim3(kRasterThreads), 0,
                        (hipStream_t)stream, depth, sorted_ids, tile_offset, tile_order, (int)n_busy, chunk_base,
                        tile_end, tile_cut, stats, chunk_list, GSR_ORDER_DEPTH);

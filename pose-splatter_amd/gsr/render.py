@@ -315,7 +315,8 @@ class _Bins:
     the stats readback (per-Gaussian and per-tile buffers) and one after it (per-intersection
     buffers).  A bounded call sizes both before any kernel runs and never reads back."""
 
-    def __init__(self, device, C, N, width, height, capacity=None, key_extra=None, chunk_entries=128):
+    def __init__(self, device, C, N, width, height, capacity=None, key_extra=None, chunk_entries=128,
+                 need_bwd=True):
         self.device = device
         self.C, self.N, self.W, self.H = C, N, width, height
         self.tw = (width + _TILE - 1) // _TILE
@@ -339,6 +340,7 @@ class _Bins:
         # the shape whose previous call bounds this one (band / unit grouping included: they
         # change the lists as much as the shape does)
         self.key = (str(device), C, N, width, height, key_extra)
+        self.need_bwd = need_bwd   # False: no chunk records, no finalize (tile_end left raw)
         mode = capacity or _capacity_default
         if mode not in ("exact", "bounded"):
             raise ValueError(f"capacity mode must be 'exact' or 'bounded', got {mode!r}")
@@ -353,7 +355,9 @@ class _Bins:
                 raise RuntimeError("gsr: a bounded render captured in a graph needs bounds from an earlier call "
                                    "of the same shape (run one step before capturing)")
         self.chunk_entries = int(chunk_entries)
-        self.caps = _lib.BinCaps(self.post_cap if self.bounded else 0, self.chunk_cap if self.bounded else 0,
+        # (a forward with no backward writes no chunk records: no chunk bound to check)
+        self.caps = _lib.BinCaps(self.post_cap if self.bounded else 0,
+                                 self.chunk_cap if self.bounded and need_bwd else 0,
                                  _status_buf(device).data_ptr(), self.chunk_entries, 0)
 
     def _set_bounds(self, h: dict) -> None:
@@ -361,7 +365,7 @@ class _Bins:
         checks each bound; gsr_bin_stats.overflow)."""
         self.bounded = True
         self.alloc_post(int(h["I"] * 1.25) + 4096)
-        self.alloc_chunks(int(h["chunks"] * 1.25) + 64)
+        self.alloc_chunks(int(h["chunks"] * 1.25) + 64 if self.need_bwd else 1)
         self.n_isect = self.post_cap
         self.n_chunks = self.chunk_cap
         self.n_busy = min(self.CT, int(h["busy"] * 1.125) + 8)
@@ -532,9 +536,18 @@ def effective_isect(stats: dict | None = None) -> int:
     s = _last_stats if stats is None else stats
     if "_bins" not in s:
         return 0
-    te = s["_bins"].tile_end.to(torch.int64)
-    st = s["_bins"].tile_off[:-1].to(torch.int64)
-    return int((te - st).clamp(min=0).sum())
+    return int(_tile_entries(s["_bins"]).sum())
+
+
+def _tile_entries(b) -> torch.Tensor:
+    """Per-tile list entries the raster read, [C*T] int64 (tile_end - start; a forward with
+    no backward leaves tile_end raw: the maximum last, -1 for none, the start for empty tiles)."""
+    te = b.tile_end.to(torch.int64)
+    st = b.tile_off[:-1].to(torch.int64)
+    if not b.need_bwd:
+        ln = b.tile_off[1:].to(torch.int64) - st
+        te = torch.where((ln > 0) & (te >= st), te + 1, st)
+    return (te - st).clamp(min=0)
 
 
 def tile_work(stats: dict | None = None) -> torch.Tensor:
@@ -543,9 +556,7 @@ def tile_work(stats: dict | None = None) -> torch.Tensor:
     s = _last_stats if stats is None else stats
     if "_bins" not in s:
         raise RuntimeError("tile_work: no forward has run")
-    te = s["_bins"].tile_end.to(torch.int64)
-    st = s["_bins"].tile_off[:-1].to(torch.int64)
-    return (te - st).clamp(min=0)
+    return _tile_entries(s["_bins"])
 
 
 def _background(bg: torch.Tensor, C: int, dev) -> torch.Tensor:
@@ -565,8 +576,9 @@ def _background(bg: torch.Tensor, C: int, dev) -> torch.Tensor:
     return hit[1]
 
 
-def _forward3d(params, viewmats, Ks, bg, width, height, opts):
-    """Projection → binning → raster fwd.  Returns (rgb, alpha, bins, meta)."""
+def _forward3d(params, viewmats, Ks, bg, width, height, opts, need_bwd=True):
+    """Projection → binning → raster fwd.  Returns (rgb, alpha, bins, meta).  need_bwd False: no
+    backward will follow (no grad needed), so no chunk records and no finalize."""
     L = lib()
     dev = params.device
     stream = _stream(dev)
@@ -577,7 +589,7 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
     Kc = Ks.detach().to(device=dev, dtype=torch.float32).contiguous()
     bgc = _background(bg, C, dev)
     b = _Bins(dev, C, N, width, height, opts.capacity, ("3d", opts.band, opts.input_mode, opts.radius_mode),
-              _chunk_entries["3d"])
+              _chunk_entries["3d"], need_bwd)
     q = b.p
     with _timed("project3d_fwd"):
       check(L.gsr3d_project_fwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height,
@@ -585,11 +597,12 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
                               opts.radius_mode, opts.input_mode, opts.band[0], opts.band[1], q["rec"], q["depth"],
                               q["rect"], q["cnt"], q["isect_off"], q["tile_cnt"], b.take_tile_counts(), stream),
           "gsr3d_project_fwd")
-    b.guess_post(with_chunks=True)
+    b.guess_post(with_chunks=need_bwd)
     b.offsets_launch(stream)
     b.emit_early(_lib.ORDER_DEPTH, stream)
     b.offsets_wait()
-    b.ensure_post(with_chunks=True)
+    b.ensure_post(with_chunks=need_bwd)
+    cs, cl = (q["chunk_state"], q["chunk_list"]) if need_bwd else (None, None)
     n_lazy = b.n_lazy = b.lazy_bound()
     if n_lazy:
         b.sort_lazy(stream)
@@ -602,14 +615,14 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts):
         check(L.gsr3d_raster_fwd_lazy(q["rec"], q["depth"], q["sorted_ids"], q["tile_off"], q["busy"],
                                       q["chunk_base"], C, width, height, _ptr(bgc), b.n_busy, q["stats_dev"],
                                       _ptr(rgb), _ptr(alpha), q["final_T"], q["last"], q["tile_end"], q["tile_cut"],
-                                      q["chunk_state"], q["chunk_list"], q["lazy"], n_lazy, b.max_seg,
+                                      cs, cl, q["lazy"], n_lazy, b.max_seg,
                                       q["sort_ws"], b.post.off["sort_ws"][1], q["k_of_s"], stream),
               "gsr3d_raster_fwd_lazy")
       else:
         check(L.gsr3d_raster_fwd(q["rec"], q["depth"], q["sorted_ids"], q["tile_off"], q["busy"], q["chunk_base"],
                                  C, width, height, _ptr(bgc), b.n_busy, q["stats_dev"], _ptr(rgb), _ptr(alpha),
-                                 q["final_T"], q["last"], q["tile_end"], q["tile_cut"], q["chunk_state"],
-                                 q["chunk_list"], stream), "gsr3d_raster_fwd")
+                                 q["final_T"], q["last"], q["tile_end"], q["tile_cut"], cs, cl, stream),
+              "gsr3d_raster_fwd")
     _record_stats(b)
     return rgb, alpha, b, (p, stride, V, Kc, bgc, width, height, opts)
 
@@ -652,7 +665,7 @@ def _sets2d(params: torch.Tensor):
     return p, F, N, int(p.stride(1)) if N > 0 else 9, int(p.stride(0))
 
 
-def _forward2d(params, bg, width, height, eps_cut, unit_sets=(0,), capacity=None):
+def _forward2d(params, bg, width, height, eps_cut, unit_sets=(0,), capacity=None, need_bwd=True):
     """unit_sets[c] = parameter set rendered by camera (unit) c (non-decreasing)."""
     L = lib()
     dev = params.device
@@ -661,25 +674,25 @@ def _forward2d(params, bg, width, height, eps_cut, unit_sets=(0,), capacity=None
     C = len(unit_sets)
     sb = _set_begin(tuple(unit_sets), F, dev)
     bgc = _background(bg, C, dev)
-    b = _Bins(dev, C, N, width, height, capacity, ("2d", tuple(unit_sets), F), _chunk_entries["2d"])
+    b = _Bins(dev, C, N, width, height, capacity, ("2d", tuple(unit_sets), F), _chunk_entries["2d"], need_bwd)
     q = b.p
     with _timed("project2d_fwd"):
       check(L.gsr2d_project_fwd(_ptr(p), N, stride, set_stride, _ptr(sb), F, C, width, height, eps_cut, q["rec"],
                               q["rect"], q["cnt"], q["isect_off"], q["tile_cnt"], b.take_tile_counts(), stream),
           "gsr2d_project_fwd")
-    b.guess_post(with_chunks=True)
+    b.guess_post(with_chunks=need_bwd)
     b.offsets_launch(stream)
     b.emit_early(_lib.ORDER_INDEX, stream)
     b.offsets_wait()
-    b.ensure_post(with_chunks=True)
+    b.ensure_post(with_chunks=need_bwd)
     b.sort(_lib.ORDER_INDEX, stream)
+    cs, cl = (q["chunk_state"], q["chunk_list"]) if need_bwd else (None, None)
     rgb = torch.empty(C, height, width, 3, device=dev, dtype=torch.float32)
     alpha = torch.empty(C, height, width, device=dev, dtype=torch.float32)
     with _timed("raster2d_fwd"):
       check(L.gsr2d_raster_fwd(q["rec"], q["sorted_ids"], q["tile_off"], q["busy"], q["chunk_base"], C, width, height,
                              eps_cut, _ptr(bgc), b.n_busy, q["stats_dev"], _ptr(rgb), _ptr(alpha), q["final_T"],
-                             q["last"], q["tile_end"], q["tile_cut"], q["chunk_state"],
-                             q["chunk_list"], stream), "gsr2d_raster_fwd")
+                             q["last"], q["tile_end"], q["tile_cut"], cs, cl, stream), "gsr2d_raster_fwd")
     _record_stats(b)
     return rgb, alpha, b, (p, F, stride, set_stride, sb, bgc, width, height, eps_cut)
 
@@ -696,8 +709,8 @@ def debug_forward2d(params, bg, width, height, eps_cut=1e-8):
 
 class _Render3D(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, params, viewmats, Ks, bg, width, height, opts: RenderOptions3D):
-        rgb, alpha, b, meta = _forward3d(params, viewmats, Ks, bg, width, height, opts)
+    def forward(ctx, params, viewmats, Ks, bg, width, height, opts: RenderOptions3D, need_bwd=True):
+        rgb, alpha, b, meta = _forward3d(params, viewmats, Ks, bg, width, height, opts, need_bwd)
         ctx.b = b
         ctx.meta = meta
         ctx.params_shape = params.shape
@@ -722,7 +735,7 @@ class _Render3D(torch.autograd.Function):
                                      _ptr(v_rgb), _ptr(v_alpha), q["k_of_s"], _ptr(partial), stream),
                   "gsr3d_raster_bwd")
         v_params = backward3d(b, ctx.meta, raster)
-        return v_params.view(ctx.params_shape), None, None, None, None, None, None
+        return v_params.view(ctx.params_shape), None, None, None, None, None, None, None
 
 
 def backward3d(b, meta, raster) -> torch.Tensor:
@@ -756,8 +769,8 @@ def backward3d(b, meta, raster) -> torch.Tensor:
 
 class _Render2D(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, params, bg, width, height, eps_cut, unit_sets, capacity=None):
-        rgb, alpha, b, meta = _forward2d(params, bg, width, height, eps_cut, unit_sets, capacity)
+    def forward(ctx, params, bg, width, height, eps_cut, unit_sets, capacity=None, need_bwd=True):
+        rgb, alpha, b, meta = _forward2d(params, bg, width, height, eps_cut, unit_sets, capacity, need_bwd)
         ctx.b = b
         ctx.meta = meta
         ctx.params_shape = params.shape
@@ -793,7 +806,12 @@ class _Render2D(torch.autograd.Function):
                                       q["isect_off"], q["cnt"], q["tile_cut"], _ptr(partial), q["stats_dev"],
                                       _ptr(v_params), stream),
                   "gsr2d_project_bwd")
-        return v_params.view(ctx.params_shape), None, None, None, None, None, None
+        return v_params.view(ctx.params_shape), None, None, None, None, None, None, None
+
+
+def _needs_grad(params: torch.Tensor) -> bool:
+    """Whether a backward can follow this render (else no chunk records / finalize)."""
+    return torch.is_grad_enabled() and params.requires_grad
 
 
 def render3d(params: torch.Tensor, viewmats: torch.Tensor, Ks: torch.Tensor, width: int, height: int,
@@ -805,7 +823,7 @@ def render3d(params: torch.Tensor, viewmats: torch.Tensor, Ks: torch.Tensor, wid
         raise ValueError(f"viewmats must be [C,4,4], got {tuple(viewmats.shape)}")
     if Ks.dim() != 3 or Ks.shape[1:] != (3, 3) or Ks.shape[0] != viewmats.shape[0]:
         raise ValueError(f"Ks must be [C,3,3] matching viewmats, got {tuple(Ks.shape)}")
-    return _Render3D.apply(params, viewmats, Ks, background, int(width), int(height), opts)
+    return _Render3D.apply(params, viewmats, Ks, background, int(width), int(height), opts, _needs_grad(params))
 
 
 def render2d(params: torch.Tensor, width: int, height: int, background: torch.Tensor,
@@ -814,7 +832,8 @@ def render2d(params: torch.Tensor, width: int, height: int, background: torch.Te
     _require_device(params, "GaussianRenderer2D")
     if params.dim() != 2:
         raise ValueError(f"render2d: params must be [N,9], got {tuple(params.shape)}")
-    rgb, alpha = _Render2D.apply(params, background, int(width), int(height), float(eps_cut), (0,), capacity)
+    rgb, alpha = _Render2D.apply(params, background, int(width), int(height), float(eps_cut), (0,), capacity,
+                                 _needs_grad(params))
     return rgb[0], alpha[0]
 
 
@@ -833,4 +852,5 @@ def render2d_units(params: torch.Tensor, unit_sets, width: int, height: int, bac
     if not sets:
         raise ValueError("render2d_units: no units")
     _set_begin(sets, params.shape[0], params.device)   # validates the grouping
-    return _Render2D.apply(params, background, int(width), int(height), float(eps_cut), sets, capacity)
+    return _Render2D.apply(params, background, int(width), int(height), float(eps_cut), sets, capacity,
+                           _needs_grad(params))

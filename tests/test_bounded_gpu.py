@@ -41,6 +41,13 @@ def _step3d(p, V, K, W, H, vr, va, capacity):
     return rgb.detach(), alpha.detach(), pg.grad
 
 
+def _poison(dev, byte=0xFF):
+    """Hand 0xFF-filled blocks (-1 words, NaN floats) to the caching allocator: the next
+    arenas reuse them, so a kernel reading a slot no kernel of this call wrote shows up."""
+    ts = [torch.full((1 << k,), byte, dtype=torch.uint8, device=dev) for k in range(10, 27) for _ in range(3)]
+    del ts
+
+
 def _same(a, b):
     return all(torch.equal(x, y) for x, y in zip(a, b))
 
@@ -62,9 +69,28 @@ def test_bounded_equals_exact_3d(cuda, lanes):
     with forced_fwd_lanes(lanes):
         ex = _step3d(*sc, capacity="exact")
         for _ in range(2):   # the first bounded call uses the exact call's bounds, the second its own
+            _poison(cuda)
             bd = _step3d(*sc, capacity="bounded")
             torch.cuda.synchronize()
             assert _same(ex, bd)
+    R.check_overflow(cuda)
+
+
+def test_bounded_forward_only(cuda):
+    """A bounded render with no gradient (no chunk records, so no chunk bound) equals the exact
+    one, also when its bounds come from a training step of the same shape."""
+    from gsr import render as R
+    p, V, K, W, H, vr, va = _scene3d(cuda)
+    bg = torch.ones(3, device=cuda)
+    with torch.no_grad():
+        ex = R.render3d(p, V, K, W, H, bg, R.RenderOptions3D(capacity="exact"))
+        for _ in range(3):
+            _poison(cuda)
+            assert _same(ex, R.render3d(p, V, K, W, H, bg, R.RenderOptions3D(capacity="bounded")))
+    _step3d(p, V, K, W, H, vr, va, "bounded")
+    with torch.no_grad():
+        assert _same(ex, R.render3d(p, V, K, W, H, bg, R.RenderOptions3D(capacity="bounded")))
+    torch.cuda.synchronize()
     R.check_overflow(cuda)
 
 
@@ -77,6 +103,7 @@ def test_bounded_split_sort_and_lazy(cuda):
     ex = _step3d(*sc, capacity="exact")
     b = R.last_stats()["_bins"]
     assert b.n_busy <= 128 and b.max_seg > 1024, (b.n_busy, b.max_seg)
+    _poison(cuda)   # the lazy re-render's list past its device count is stale (was: NaN tiles)
     assert _same(ex, _step3d(*sc, capacity="bounded"))
     # lazy: lists longer than 512 sorted to a 256-entry prefix, most tiles re-rendered
     _lib.check(L.gsr_set_lazy_sort(512, 256), "gsr_set_lazy_sort")
@@ -85,6 +112,7 @@ def test_bounded_split_sort_and_lazy(cuda):
         R._size_hint.clear()
         ex = _step3d(*sc, capacity="exact")
         assert R.last_stats()["_bins"].n_lazy > 0
+        _poison(cuda)
         assert _same(ex, _step3d(*sc, capacity="bounded"))
     finally:
         _lib.check(L.gsr_set_lazy_sort(16384, 4096), "gsr_set_lazy_sort")

@@ -109,3 +109,37 @@ def test_unit_mismatch_is_flagged(cuda):
     assert torch.isnan(v).all()
     st = b.pre.view("stats_dev", torch.int32).tolist()
     assert st[12] & 32, st
+
+
+@pytest.mark.parametrize("lanes", [0, 1, 4, 16])
+def test_forward_only_matches(cuda, lanes):
+    """A render with no gradient needed writes no chunk records and skips the finalize; its
+    rgb / alpha equal the training forward's bitwise, and the tile work (list entries read,
+    the multi-GPU balancing weights) is the same."""
+    from gsr import render as R
+    from _util import forced_fwd_lanes
+    p, V, K, W, H, vr, va = _scene3d(cuda)
+    bg = torch.ones(3, device=cuda)
+    with forced_fwd_lanes(lanes):
+        pg = p.clone().requires_grad_(True)
+        rgb, alpha = R.render3d(pg, V, K, W, H, bg)
+        work = R.tile_work().clone()
+        with torch.no_grad():
+            rgb2, alpha2 = R.render3d(p, V, K, W, H, bg)
+        assert not R.last_stats()["_bins"].need_bwd
+        work2 = R.tile_work()
+    assert torch.equal(rgb.detach(), rgb2) and torch.equal(alpha.detach(), alpha2)
+    assert torch.equal(work, work2)
+
+
+def test_forward_only_2d(cuda):
+    from gsr import render as R
+    from gsr.scenes import gaussians2d
+    W, H = 96, 80
+    p = gaussians2d(3000, W, H, 71).to(cuda)
+    bg = torch.ones(3, device=cuda)
+    pg = p.clone().requires_grad_(True)
+    rgb, alpha = R.render2d(pg, W, H, bg)
+    with torch.no_grad():
+        rgb2, alpha2 = R.render2d(p, W, H, bg)
+    assert torch.equal(rgb.detach(), rgb2) and torch.equal(alpha.detach(), alpha2)

@@ -1,2 +1,2 @@
 cd $GRAFT_REPO_ROOT
-timeout -k 10 120 python -u tools/diag_graph3.py
+timeout -k 10 120 python -u tools/diag_bounded.py
