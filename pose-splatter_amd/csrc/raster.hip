@@ -1080,6 +1080,13 @@ __device__ __forceinline__ void loss_cotangent(const gsr_loss_terms& lt, int C, 
 #ifndef GSR_BWD_MULTI_MINB
 #define GSR_BWD_MULTI_MINB 1
 #endif
+#ifdef GSR_BWD_TRACE
+// timing build only (tools/bwd_trace.py): per workgroup {wall clock at 7 points, hw id, groups}
+__device__ unsigned long long* g_bwd_trace = nullptr;
+#define BWD_T(i) if (threadIdx.x == 0) tr[i] = wall_clock64()   // (LDS: registers would cost occupancy)
+#else
+#define BWD_T(i)
+#endif
 template <bool LOSS, bool IS2D, bool MULTI>
 __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : 1) void k_raster_bwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
@@ -1107,6 +1114,11 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : 1) voi
   // tests made the compiler wait for each load in turn: three extra round trips per workgroup).
   // MULTI = false: units of exactly one sub-chunk (no loop: the loop's back-edge keeps ~40 more
   // VGPRs live and costs a wave per SIMD); a forward with longer units is flagged, not half done.
+#ifdef GSR_BWD_TRACE
+  __shared__ unsigned long long tr[8];
+  __shared__ int tr_nb[16];
+  BWD_T(0);
+#endif
   const int4 cd = reinterpret_cast<const int4*>(chunk_list)[blockIdx.x];
   const int n_act = stats->n_active, ovf = stats->overflow, ce = stats->chunk_entries;
   const bool unit_bad = !MULTI && ce != kChunk3;
@@ -1114,6 +1126,7 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : 1) voi
     if (unit_bad && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&stats->overflow, GSR_OVF_UNIT);
     return;
   }
+  BWD_T(1);
   const int b0 = cd.x, n = cd.y, chunk = cd.z, ct = cd.w;
   int c, ty, tx;
   tile_coords(ct, tw, th, c, ty, tx);
@@ -1181,8 +1194,15 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : 1) voi
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wlast = max(wlast, __shfl_xor(wlast, o, 64));
   wlast = __builtin_amdgcn_readfirstlane(wlast);   // wave-uniform: an SGPR across the sub-chunk loop
-  Splat sp = {};
-  if (threadIdx.x < sn) sp = rec[id_mine];
+  // the records as three float4 registers (a Splat variable assigned under a branch and in the
+  // sub-chunk loop went through 48 B of scratch per lane: a store + reload on the load chain)
+  const float4* const rec4 = reinterpret_cast<const float4*>(rec);
+  float4 sp0 = make_float4(0.f, 0.f, 0.f, 0.f), sp1 = sp0, sp2 = sp0;
+  if (threadIdx.x < sn) {
+    sp0 = rec4[3 * (int64_t)id_mine + 0];
+    sp1 = rec4[3 * (int64_t)id_mine + 1];
+    sp2 = rec4[3 * (int64_t)id_mine + 2];
+  }
   const int fg = lane / kPartial, fq = lane - kPartial * (lane / kPartial);
   const bool fown = lane < kGroup * kPartial;
   float* const Lw = &L[fq][wv][0];
@@ -1191,9 +1211,9 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : 1) voi
   for (int sub = nsub - 1; sub >= 0; --sub) {
     if (sub != nsub - 1) __syncthreads();   // the previous sub-chunk's LDS is consumed
     if (threadIdx.x < sn) {
-      s_p[0][threadIdx.x] = sp.p0;
-      s_p[1][threadIdx.x] = sp.p1;
-      s_p[2][threadIdx.x] = sp.p2;
+      s_p[0][threadIdx.x] = sp0;
+      s_p[1][threadIdx.x] = sp1;
+      s_p[2][threadIdx.x] = sp2;
     }
     for (int i = threadIdx.x; i < kPartial * 4 * (kChunk3 + 1); i += kRasterThreads) (&L[0][0][0])[i] = 0.f;
     if (threadIdx.x == 0) {
@@ -1203,6 +1223,7 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : 1) voi
       s_p[2][kNull] = z;
     }
     __syncthreads();
+    BWD_T(2);
     // the pixel's last entry as a slot of this sub-chunk: lastk for the range test (the pad
     // slot kNull is past it), lastq for the 2D equality (never a slot when the last entry is
     // in a later sub-chunk or before this one)
@@ -1246,6 +1267,10 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : 1) voi
     const int npad = (ngrp + kGroup - 1) / kGroup * kGroup;
     for (int s = nb + pos; s < npad; s += 16) s_box[wv][box][s] = (unsigned char)kNull;
     __builtin_amdgcn_wave_barrier();
+#ifdef GSR_BWD_TRACE
+    if (pos == 0) tr_nb[wv * 4 + box] = nb;
+#endif
+    BWD_T(3);
     // after reduce_box16 lane l holds 4 of its box's sums, flat indices 4*(l>>2) + i = 9*g + q.
     // They are staged in LDS (one b128 store per group), and lane f < 63 then adds flat index
     // f = 9g + q of every box, box by box, into the wave's slot L[q][wv][entry]: inside one
@@ -1323,9 +1348,13 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : 1) voi
     if (sub > 0 && threadIdx.x < kChunk3) {
       const int id_next = ids[sb0 - kChunk3 + threadIdx.x];
       kos_next = k_of_s[sb0 - kChunk3 + threadIdx.x];
-      sp = rec[id_next];
+      sp0 = rec4[3 * (int64_t)id_next + 0];
+      sp1 = rec4[3 * (int64_t)id_next + 1];
+      sp2 = rec4[3 * (int64_t)id_next + 2];
     }
+    BWD_T(4);
     __syncthreads();
+    BWD_T(5);
     if (threadIdx.x < sn) {
       const int k = threadIdx.x;
       float v[kPartial];
@@ -1341,8 +1370,26 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : 1) voi
     sb0 -= kChunk3;
     sn = kChunk3;
     kos_mine = kos_next;
+#ifdef GSR_BWD_TRACE
+    if (threadIdx.x == 0) tr[7] = ((unsigned long long)__smid() << 32) | (unsigned)ngrp;
+#endif
   }
+#ifdef GSR_BWD_TRACE
+  __syncthreads();
+  BWD_T(6);
+  if (threadIdx.x == 0 && g_bwd_trace != nullptr) {
+    ulonglong2* dst = reinterpret_cast<ulonglong2*>(g_bwd_trace + (int64_t)blockIdx.x * 16);
+    for (int i = 0; i < 4; ++i) dst[i] = make_ulonglong2(tr[2 * i], tr[2 * i + 1]);
+    int4* dn = reinterpret_cast<int4*>(dst + 4);
+    for (int i = 0; i < 4; ++i) dn[i] = make_int4(tr_nb[4 * i], tr_nb[4 * i + 1], tr_nb[4 * i + 2], tr_nb[4 * i + 3]);
+  }
+#endif
 }
+#ifdef GSR_BWD_TRACE
+extern "C" int gsr_debug_bwd_trace(void* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_bwd_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 __global__ void k_selftest_reduce64(float* out) {
   float v[64];
