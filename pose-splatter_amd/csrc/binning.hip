@@ -447,6 +447,12 @@ __global__ __launch_bounds__(kStageThreads) void k_emit_staged(
 // bounded odd-even fix-up — the order a stable radix sort of gsplat's keys over emission
 // order gives.
 
+#ifdef GSR_SORT_TRACE
+__shared__ unsigned long long s_sort_ts[8];   // per-phase wall clock of the sort (thread 0)
+#define SORT_T(i) if (threadIdx.x == 0) s_sort_ts[i] = wall_clock64()
+#else
+#define SORT_T(i)
+#endif
 __device__ __forceinline__ uint32_t sort_word(uint64_t k) { return (uint32_t)(k >> 32); }
 __device__ __forceinline__ uint32_t low_word(uint64_t k) { return (uint32_t)(k & 0xffffffffull); }
 
@@ -454,22 +460,51 @@ __device__ __forceinline__ uint32_t low_word(uint64_t k) { return (uint32_t)(k &
 // (a plain strided loop waits one memory latency per iteration: ~10 iterations per list).
 constexpr int kBatch = 8;
 
-// a[i] = (sort word of src[i]) << 32 | (pbase + i), i < n
+// a[i] = (sort word of src[i]) << 32 | (pbase + i), i < n.  Returns this thread's OR of
+// (word ^ src[0]'s word): the bits that vary inside the list, once OR-ed over the block.
+// (16 loads in flight per thread: a list of up to 16 NT keys arrives in one round trip)
+constexpr int kStageBatch = 16;
 template <int NT>
-__device__ __forceinline__ void stage_keys(uint64_t* a, const uint64_t* __restrict__ src, int n, int pbase) {
-  for (int i0 = threadIdx.x; i0 < n; i0 += kBatch * NT) {
-    uint32_t w[kBatch];
+__device__ __forceinline__ uint32_t stage_keys(uint64_t* a, const uint64_t* __restrict__ src, int n, int pbase) {
+  const uint32_t w0 = sort_word(src[0]);
+  uint32_t orv = 0;
+  for (int i0 = threadIdx.x; i0 < n; i0 += kStageBatch * NT) {
+    uint32_t w[kStageBatch];
 #pragma unroll
-    for (int j = 0; j < kBatch; ++j) {
+    for (int j = 0; j < kStageBatch; ++j) {
       const int i = i0 + j * NT;
       w[j] = sort_word(src[i < n ? i : 0]);
     }
 #pragma unroll
-    for (int j = 0; j < kBatch; ++j) {
+    for (int j = 0; j < kStageBatch; ++j) {
       const int i = i0 + j * NT;
+      orv |= w[j] ^ w0;   // (a clamped duplicate of src[0] adds nothing)
       if (i < n) a[i] = ((uint64_t)w[j] << 32) | (uint64_t)(uint32_t)(pbase + i);
     }
   }
+  return orv;
+}
+
+// The varying bits of the sort words: the block OR of every thread's `orv` (s_misc[0] must be
+// zero on entry; it is left holding the result).  One atomic per wave.
+template <int NT>
+__device__ __forceinline__ uint32_t block_varying(uint32_t orv, int* s_misc) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) orv |= (uint32_t)__shfl_xor((int)orv, o, 64);
+  if ((threadIdx.x & 63) == 0 && orv) atomicOr((unsigned*)&s_misc[0], orv);
+  __syncthreads();
+  return (uint32_t)s_misc[0];
+}
+
+// The same from keys already in LDS
+template <int NT>
+__device__ __forceinline__ uint32_t lds_varying(const uint64_t* a, int n, int* s_misc) {
+  if (threadIdx.x == 0) s_misc[0] = 0;
+  __syncthreads();
+  const uint32_t w0 = sort_word(a[0]);
+  uint32_t orv = 0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) orv |= sort_word(a[i]) ^ w0;
+  return block_varying<NT>(orv, s_misc);
 }
 
 // a[i] = src[i], i < n
@@ -520,23 +555,73 @@ __device__ __forceinline__ void write_sorted(const uint64_t* a, int n, const uin
   }
 }
 
+// write_sorted for a list held whole in LDS (p indexes a, capacity >= n 64-bit slots): the
+// sorted p's move to registers, the list's ids (low words of seg) and emission indices are then
+// loaded COALESCED into the same LDS (as two n-word arrays), and each sorted entry reads its
+// pair there.  A long list's write was two random global gathers per key, all issued by the
+// one workgroup that owns the list (~17 us of a 42 us sort at 11 880 keys).
+template <int NT>
+__device__ __forceinline__ void write_sorted_lds(uint64_t* a, int n, const uint64_t* __restrict__ seg,
+                                                 const int32_t* __restrict__ kslot, int32_t* __restrict__ ids,
+                                                 int32_t* __restrict__ kos) {
+  // the direct path's longest list: lds_keys <= kSortLdsKeys (kSortThreads) or kSortSmallKeys
+  constexpr int kMaxKeys = NT == kSortThreadsSmall ? kSortSmallKeys : kSortLdsKeys;
+  constexpr int kMaxPer = (kMaxKeys + NT - 1) / NT;
+  static_assert(kMaxPer <= 16, "sorted positions held in registers");
+  uint16_t pv[kMaxPer];
+#pragma unroll
+  for (int j = 0; j < kMaxPer; ++j) {
+    const int s = (int)threadIdx.x + j * NT;
+    pv[j] = s < n ? (uint16_t)low_word(a[s]) : (uint16_t)0;
+  }
+  __syncthreads();
+  uint32_t* xid = reinterpret_cast<uint32_t*>(a);
+  int32_t* xk = reinterpret_cast<int32_t*>(a) + n;
+  for (int i0 = threadIdx.x; i0 < n; i0 += kMaxPer * NT) {   // one round trip
+    uint32_t id[kMaxPer];
+    int32_t ko[kMaxPer];
+#pragma unroll
+    for (int j = 0; j < kMaxPer; ++j) {
+      const int i = i0 + j * NT;
+      id[j] = low_word(seg[i < n ? i : 0]);
+      ko[j] = kslot[i < n ? i : 0];
+    }
+#pragma unroll
+    for (int j = 0; j < kMaxPer; ++j) {
+      const int i = i0 + j * NT;
+      if (i < n) {
+        xid[i] = id[j];
+        xk[i] = ko[j];
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kMaxPer; ++j) {
+    const int s = (int)threadIdx.x + j * NT;
+    if (s < n) {
+      ids[s] = (int32_t)xid[pv[j]];
+      kos[s] = xk[pv[j]];
+    }
+  }
+}
+
 // a: n <= 16*NT elements (word << 32 | p) in LDS; seg: the bucket's original keys
 // (tie-break by their low word); s_hist: (NT/64)*256 + 64 ints.
+// varying: the bits in which the sort words differ (block_varying / lds_varying).
 template <int NT>
-__device__ __forceinline__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, const uint64_t* __restrict__ seg) {
+__device__ __forceinline__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, const uint64_t* __restrict__ seg,
+                                               uint32_t varying) {
   constexpr int kSortWaves = NT / 64;
   constexpr int kWaveBits = kSortWaves == 16 ? 4 : (kSortWaves == 8 ? 3 : 2);
   static_assert(kSortWaves == 16 || kSortWaves == 8 || kSortWaves == 4, "16, 8 or 4 waves");
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int* s_misc = s_hist + kSortWaves * 256;
-  if (threadIdx.x == 0) s_misc[0] = 0;
-  __syncthreads();
-  const uint32_t w0 = sort_word(a[0]);
-  uint32_t orv = 0;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) orv |= sort_word(a[i]) ^ w0;
-  if (orv) atomicOr((unsigned*)&s_misc[0], orv);
-  __syncthreads();
-  const uint32_t varying = (uint32_t)s_misc[0];
+  if (threadIdx.x == 0) {   // tie-run count and long-run flag (the passes' barriers order these)
+    s_misc[1] = 0;
+    s_misc[2] = 0;
+  }
+  SORT_T(1);
   const int per_wave = (((n + kSortWaves - 1) / kSortWaves) + 63) & ~63;
   const int rounds = per_wave >> 6;
   for (int shift = 0; shift < 32; shift += 8) {
@@ -588,8 +673,53 @@ __device__ __forceinline__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, 
       }
     }
     __syncthreads();
+    SORT_T(2 + shift / 8);
   }
-  // equal sort words: order by c*N+n — odd-even passes until nothing moves
+  SORT_T(6);
+  // equal sort words: order by c*N+n.  One pass lists the runs of equal words (rare: a few per
+  // long list), then one thread per run insertion-sorts it by the keys' low words -- one
+  // round of gathers for all runs (odd-even transposition until nothing moved needed ~4
+  // barrier-separated passes, each waiting on a gather whenever the list had a tie).
+  int* s_runs = s_hist;   // the counters are free now
+  constexpr int kMaxRuns = kSortWaves * 256;
+  constexpr int kMaxRunLen = 32;
+  for (int i = threadIdx.x; i < n; i += NT) {
+    const uint32_t w = sort_word(a[i]);
+    const bool starts = i + 1 < n && sort_word(a[i + 1]) == w && (i == 0 || sort_word(a[i - 1]) != w);
+    if (starts) {
+      const int r = atomicAdd(&s_misc[1], 1);
+      if (r < kMaxRuns) s_runs[r] = i;
+    }
+  }
+  __syncthreads();
+  const int n_runs = s_misc[1];
+  if (n_runs <= kMaxRuns) {
+    for (int r = threadIdx.x; r < n_runs; r += NT) {
+      const int i0 = s_runs[r];
+      const uint32_t w = sort_word(a[i0]);
+      int i1 = i0 + 1;
+      while (i1 < n && i1 - i0 <= kMaxRunLen && sort_word(a[i1]) == w) ++i1;
+      if (i1 - i0 > kMaxRunLen) {   // a long run (degenerate depths): the odd-even passes below
+        s_misc[2] = 1;
+        continue;
+      }
+      for (int i = i0 + 1; i < i1; ++i) {   // insertion sort of a[i0..i1) by low_word(seg[p])
+        const uint64_t x = a[i];
+        const uint32_t kx = low_word(seg[low_word(x)]);
+        int j = i - 1;
+        while (j >= i0 && low_word(seg[low_word(a[j])]) > kx) {
+          a[j + 1] = a[j];
+          --j;
+        }
+        a[j + 1] = x;
+      }
+    }
+    __syncthreads();
+    SORT_T(7);
+    if (s_misc[2] == 0) return;
+  }
+  // (more runs than the list can hold, or a run too long for one thread: odd-even passes
+  // until nothing moves)
   while (true) {
     bool moved = false;
 #pragma unroll
@@ -606,6 +736,7 @@ __device__ __forceinline__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, 
     }
     if (!__syncthreads_or(moved)) break;
   }
+  SORT_T(7);
 }
 
 __device__ __forceinline__ int next_pow2(int v) {
@@ -642,6 +773,26 @@ __device__ __forceinline__ void merge_runs(const uint64_t* __restrict__ a, const
 }
 
 // Outputs: sorted_ids[s] = c*N+n of sorted entry s; k_of_s[s] = its emission entry index.
+#ifdef GSR_SORT_TRACE
+// timing build only (tools/sort_trace.py): per workgroup {start, end, list length, hw id}
+__device__ unsigned long long* g_sort_trace = nullptr;
+extern "C" int gsr_debug_sort_trace(void* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_sort_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
+}
+struct SortTrace {
+  unsigned long long t0;
+  int len;
+  __device__ ~SortTrace() {
+    __syncthreads();
+    if (threadIdx.x == 0 && g_sort_trace != nullptr && len >= 0) {
+      ulonglong2* d = reinterpret_cast<ulonglong2*>(g_sort_trace + 12 * (int64_t)blockIdx.x);
+      d[0] = make_ulonglong2(t0, wall_clock64());
+      d[1] = make_ulonglong2((unsigned long long)len, (unsigned long long)__smid());
+      for (int i = 0; i < 4; ++i) d[2 + i] = make_ulonglong2(s_sort_ts[2 * i], s_sort_ts[2 * i + 1]);
+    }
+  }
+};
+#endif
 template <int NT>
 __global__ __launch_bounds__(NT) void k_segsort(
     uint64_t* __restrict__ keys, uint64_t* __restrict__ tmpk, int32_t* __restrict__ tmpp0,
@@ -661,6 +812,16 @@ __global__ __launch_bounds__(NT) void k_segsort(
   if ((int)blockIdx.x >= nb) return;
   const int start = tile_offset[ct];
   const int len = tile_offset[ct + 1] - start;
+#ifdef GSR_SORT_TRACE
+  __shared__ unsigned long long s_t0;
+  if (threadIdx.x == 0) {
+    s_t0 = wall_clock64();
+    for (int i = 0; i < 8; ++i) s_sort_ts[i] = 0;
+  }
+  SortTrace st_{0, -1};
+  st_.t0 = s_t0;   // (read by thread 0 only)
+  st_.len = len;
+#endif
   uint64_t* seg = keys + start;
   const bool lazy = lz.mode == 1 && len > lz.min_len;
   if (lz.mode != 0 && threadIdx.x == 0) {
@@ -673,10 +834,13 @@ __global__ __launch_bounds__(NT) void k_segsort(
     }
   }
   if (len <= lds_keys && !lazy) {
-    stage_keys<NT>(s_keys, seg, len, 0);
+    int* s_misc = s_hist + (NT / 64) * 256;
+    if (threadIdx.x == 0) s_misc[0] = 0;
     __syncthreads();
-    lds_radix_sort<NT>(s_keys, len, s_hist, seg);
-    write_sorted<NT>(s_keys, len, seg, k_of_slot + start, sorted_ids + start, k_of_s + start);
+    // the varying bits are OR-ed while staging (the barrier after the staging is block_varying's)
+    const uint32_t varying = block_varying<NT>(stage_keys<NT>(s_keys, seg, len, 0), s_misc);
+    lds_radix_sort<NT>(s_keys, len, s_hist, seg, varying);
+    write_sorted_lds<NT>(s_keys, len, seg, k_of_slot + start, sorted_ids + start, k_of_s + start);
     return;
   }
   // Long list (> lds_keys): MSD partition by the top 8 varying bits of the sort word into
@@ -768,7 +932,7 @@ __global__ __launch_bounds__(NT) void k_segsort(
         if (n > 0) {
           copy_keys<NT>(s_keys, part + g0, n);
           __syncthreads();
-          lds_radix_sort<NT>(s_keys, n, s_hist, seg);
+          lds_radix_sort<NT>(s_keys, n, s_hist, seg, lds_varying<NT>(s_keys, n, s_hist + (NT / 64) * 256));
           write_sorted<NT>(s_keys, n, seg, k_of_slot + start, sorted_ids + start + g0, k_of_s + start + g0);
           __syncthreads();
         }
@@ -790,7 +954,7 @@ __global__ __launch_bounds__(NT) void k_segsort(
     const int rl = min(lds_keys, len - r0);
     stage_keys<NT>(s_keys, seg + r0, rl, r0);
     __syncthreads();
-    lds_radix_sort<NT>(s_keys, rl, s_hist, seg);
+    lds_radix_sort<NT>(s_keys, rl, s_hist, seg, lds_varying<NT>(s_keys, rl, s_hist + (NT / 64) * 256));
     for (int i = threadIdx.x; i < rl; i += blockDim.x) {
       const uint32_t p = low_word(s_keys[i]);
       kA[r0 + i] = (s_keys[i] & 0xffffffff00000000ull) | (uint64_t)low_word(seg[p]);
@@ -861,7 +1025,8 @@ __global__ __launch_bounds__(kSplitThreads) void k_split_blocksort(
   const uint64_t* seg = keys + start;
   stage_keys<kSplitThreads>(s_keys, seg + b0, n, b0);
   __syncthreads();
-  lds_radix_sort<kSplitThreads>(s_keys, n, s_hist, seg);
+  lds_radix_sort<kSplitThreads>(s_keys, n, s_hist, seg,
+                                lds_varying<kSplitThreads>(s_keys, n, s_hist + (kSplitThreads / 64) * 256));
   if (len <= kSplitBlock) {   // one block: final order
     write_sorted<kSplitThreads>(s_keys, n, seg, k_of_slot + start, sorted_ids + start, k_of_s + start);
     return;
