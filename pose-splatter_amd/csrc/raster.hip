@@ -316,6 +316,17 @@ __device__ __forceinline__ void lazy_flag_tile(const FwdLazy& lz, int ct) {
   if (atomicExch(&lz.flag[ct], 1) == 0) lz.list[atomicAdd(lz.count, 1)] = ct;
 }
 
+#ifdef GSR_FWD_TRACE
+// timing build only (tools/fwd_trace.py): per workgroup {start, first round in, walk done, end,
+// rounds, list entries, hw id}
+__device__ unsigned long long* g_fwd_trace = nullptr;
+extern "C" int gsr_debug_fwd_trace(void* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_fwd_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
+}
+#define FWD_T(i) if (threadIdx.x == 0) s_ftr[i] = wall_clock64()
+#else
+#define FWD_T(i)
+#endif
 template <bool IS2D, int LPP>
 __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
@@ -328,6 +339,11 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   using PG = PixGroup<LPP>;
   using FS = FwdShape<LPP>;
   __shared__ int s_max;
+#ifdef GSR_FWD_TRACE
+  __shared__ unsigned long long s_ftr[4];
+  int n_rounds = 0;
+  FWD_T(0);
+#endif
   // n_busy sizes the grid (the read-back busy count or a bound); the tiles come from the device
   // count, which the sort has checked against that bound (GSR_OVF_BUSY)
   const int busy_blocks = busy_grid<LPP>(n_busy);
@@ -432,6 +448,9 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
       c0 = sn.p0; c1 = sn.p1; c2 = sn.p2;
     }
     if (__syncthreads_count(!done) == 0) break;
+#ifdef GSR_FWD_TRACE
+    if (n_rounds++ == 0) FWD_T(1);
+#endif
     for (int h = 0; h < 2; ++h) {
       const int hb = rb + 128 * h;
       if (hb >= end || __ballot(!done) == 0ull) break;
@@ -590,6 +609,10 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     if (b0 + 64 >= end || !step(b0 + 64, y0, y1, y2, idq, idp)) break;
   }
   }
+#ifdef GSR_FWD_TRACE
+  __syncthreads();
+  FWD_T(2);
+#endif
   const float Dr = PG::sum(dr), Dg = PG::sum(dg), Db = PG::sum(db);
   cr += Dr;
   cg += Dg;
@@ -673,6 +696,16 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
     __syncthreads();
   }
   if (threadIdx.x == 0 && s_max >= 0) atomicMax(&tile_end[ct], s_max);   // finalised by k_raster_finalize
+#ifdef GSR_FWD_TRACE
+  FWD_T(3);
+  if (threadIdx.x == 0 && g_fwd_trace != nullptr) {
+    ulonglong2* d = reinterpret_cast<ulonglong2*>(g_fwd_trace + 8 * (int64_t)blockIdx.x);
+    d[0] = make_ulonglong2(s_ftr[0], s_ftr[1]);
+    d[1] = make_ulonglong2(s_ftr[2], s_ftr[3]);
+    d[2] = make_ulonglong2((unsigned long long)n_rounds, (unsigned long long)(list_end - start));
+    d[3] = make_ulonglong2((unsigned long long)__smid(), (unsigned long long)ct);
+  }
+#endif
 }
 
 // ---------------------------------------------------------------- forward, box layout
