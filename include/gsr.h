@@ -107,7 +107,9 @@ typedef struct gsr_bin_stats {
   int32_t overflow;    /* GSR_OVF_* bits; nonzero: this call's outputs are NaN        */
   int32_t chunk_entries; /* list entries per backward work unit (copy of caps->chunk_entries) */
   int32_t* status;     /* copy of caps->status (device; may be NULL)                  */
-  int64_t reserved[2];
+  int32_t n_sort_long; /* tiles with lists >= 1024 entries (the sort's one-workgroup lists) */
+  int32_t reserved32;
+  int64_t reserved;
 } gsr_bin_stats;       /* 80 bytes; written by gsr_bin_offsets                         */
 
 /* Upper bounds for a call that does not read stats back (gsr_bin_offsets).  The caller sizes
@@ -135,7 +137,8 @@ int gsr_version(void);
  * to 80 bytes and gained the bounded-call fields; gsr_bin_offsets takes gsr_bin_caps;
  * gsr3d_project_bwd / gsr2d_project_bwd take the stats (NaN rows on overflow); gsr_bin_sort /
  * gsr_bin_sort_lazy take mutable stats. */
-#define GSR_ABI_VERSION 3
+/* Revision 4: gsr_bin_stats.n_sort_long (in the former reserved words; size unchanged). */
+#define GSR_ABI_VERSION 4
 int gsr_abi_version(void);
 const char* gsr_last_error(void);
 

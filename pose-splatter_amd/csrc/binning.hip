@@ -170,6 +170,7 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(int32_t* __restrict__
         stats->n_sort_big = acc;
         stats->n_sort_mid = c;
       }
+      if (b == 9) stats->n_sort_long = acc;   // lists >= 1024 (kWaveSortKeys): one workgroup each
       s_bucket[b] = acc;
       acc += c;
     }
@@ -772,6 +773,173 @@ __device__ __forceinline__ void merge_runs(const uint64_t* __restrict__ a, const
   }
 }
 
+// Short lists (< kWaveSortKeys entries) are sorted by ONE wave each, kSortWaves of them per
+// workgroup side by side (the tile scan counts the longer lists: stats->n_sort_long; the busy
+// order puts them first): the same stable LSD radix sort on the sort word as lds_radix_sort,
+// with wave-ordered LDS atomics for the in-round rank, a wave scan of the wave's 256 counters
+// and no workgroup barrier -- a 1 024-thread workgroup spent ~10 us of barriers and round trips
+// on a list of a few hundred entries (config 3: 233 such lists, 9.4 us of each CU's sort).
+constexpr int kWaveSortKeys = 1024;
+constexpr int kWaveRounds = kWaveSortKeys / 64;
+
+__device__ __forceinline__ int wave_excl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  return x - v;
+}
+
+// a: this wave's LDS region (>= kWaveSortKeys slots); hist: its 256 counters.  n < kWaveSortKeys.
+__device__ __forceinline__ void wave_sort_list(uint64_t* a, int* hist, int n, const uint64_t* __restrict__ seg,
+                                               const int32_t* __restrict__ kslot, int32_t* __restrict__ ids,
+                                               int32_t* __restrict__ kos) {
+  const int lane = threadIdx.x & 63;
+  const int rounds = (n + 63) >> 6;
+  // stage (all loads in flight at once) and OR the varying bits of the sort words
+  const uint32_t w0 = sort_word(seg[0]);
+  uint32_t orv = 0;
+  {
+    uint32_t w[kWaveRounds];
+#pragma unroll
+    for (int r = 0; r < kWaveRounds; ++r) {
+      const int i = r * 64 + lane;
+      w[r] = r < rounds ? sort_word(seg[i < n ? i : 0]) : w0;
+    }
+#pragma unroll
+    for (int r = 0; r < kWaveRounds; ++r) {
+      const int i = r * 64 + lane;
+      orv |= w[r] ^ w0;
+      if (r < rounds && i < n) a[i] = ((uint64_t)w[r] << 32) | (uint64_t)(uint32_t)i;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) orv |= (uint32_t)__shfl_xor((int)orv, o, 64);
+  __builtin_amdgcn_wave_barrier();
+  for (int shift = 0; shift < 32; shift += 8) {
+    if (((orv >> shift) & 0xFFu) == 0u) continue;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) hist[lane * 4 + k] = 0;
+    __builtin_amdgcn_wave_barrier();
+    uint64_t el[kWaveRounds];
+    int rk[kWaveRounds];
+#pragma unroll
+    for (int r = 0; r < kWaveRounds; ++r) {
+      if (r < rounds) {
+        const int i = r * 64 + lane;
+        const bool valid = i < n;
+        el[r] = valid ? a[i] : 0ull;
+        const uint32_t d = (sort_word(el[r]) >> shift) & 0xFFu;
+        // lane-ordered returning atomics (as lds_radix_sort): the rank among equal digits
+        rk[r] = valid ? (int)((d << 23) | (uint32_t)atomicAdd(&hist[d], 1)) : -1;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    {
+      int c[4], sum = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        c[k] = hist[lane * 4 + k];
+        sum += c[k];
+      }
+      int run = wave_excl_scan(sum);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        hist[lane * 4 + k] = run;
+        run += c[k];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < kWaveRounds; ++r)
+      if (r < rounds && rk[r] >= 0) a[hist[rk[r] >> 23] + (rk[r] & 0x7FFFFF)] = el[r];
+    __builtin_amdgcn_wave_barrier();
+  }
+  // equal sort words: each run insertion-sorted by its keys' low words (c*N+n) by the lane
+  // that finds its start; a run longer than 32 (degenerate depths): odd-even passes
+  bool long_run = false;
+  for (int i = lane; i < n; i += 64) {
+    const uint32_t w = sort_word(a[i]);
+    if (i + 1 < n && sort_word(a[i + 1]) == w && (i == 0 || sort_word(a[i - 1]) != w)) {
+      int i1 = i + 1;
+      while (i1 < n && i1 - i <= 32 && sort_word(a[i1]) == w) ++i1;
+      if (i1 - i > 32) {
+        long_run = true;
+        continue;
+      }
+      for (int k = i + 1; k < i1; ++k) {
+        const uint64_t x = a[k];
+        const uint32_t kx = low_word(seg[low_word(x)]);
+        int j = k - 1;
+        while (j >= i && low_word(seg[low_word(a[j])]) > kx) {
+          a[j + 1] = a[j];
+          --j;
+        }
+        a[j + 1] = x;
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (__ballot(long_run) != 0ull) {
+    while (true) {
+      bool moved = false;
+      for (int ph = 0; ph < 2; ++ph) {
+        for (int i = 2 * lane + ph; i + 1 < n; i += 128) {
+          const uint64_t x = a[i], y = a[i + 1];
+          if (sort_word(x) == sort_word(y) && low_word(seg[low_word(x)]) > low_word(seg[low_word(y)])) {
+            a[i] = y;
+            a[i + 1] = x;
+            moved = true;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (__ballot(moved) == 0ull) break;
+    }
+  }
+  // write out through the region (as write_sorted_lds): sorted p's to registers, the list's
+  // ids / emission indices coalesced into LDS, then each sorted entry reads its pair
+  uint16_t pv[kWaveRounds];
+#pragma unroll
+  for (int r = 0; r < kWaveRounds; ++r) {
+    const int s = r * 64 + lane;
+    pv[r] = s < n ? (uint16_t)low_word(a[s]) : (uint16_t)0;
+  }
+  __builtin_amdgcn_wave_barrier();
+  uint32_t* xid = reinterpret_cast<uint32_t*>(a);
+  int32_t* xk = reinterpret_cast<int32_t*>(a) + n;
+  {
+    uint32_t id[kWaveRounds];
+    int32_t ko[kWaveRounds];
+#pragma unroll
+    for (int r = 0; r < kWaveRounds; ++r) {
+      const int i = r * 64 + lane;
+      id[r] = r < rounds ? low_word(seg[i < n ? i : 0]) : 0u;
+      ko[r] = r < rounds ? kslot[i < n ? i : 0] : 0;
+    }
+#pragma unroll
+    for (int r = 0; r < kWaveRounds; ++r) {
+      const int i = r * 64 + lane;
+      if (r < rounds && i < n) {
+        xid[i] = id[r];
+        xk[i] = ko[r];
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int r = 0; r < kWaveRounds; ++r) {
+    const int s = r * 64 + lane;
+    if (r < rounds && s < n) {
+      ids[s] = (int32_t)xid[pv[r]];
+      kos[s] = xk[pv[r]];
+    }
+  }
+}
+
 // Outputs: sorted_ids[s] = c*N+n of sorted entry s; k_of_s[s] = its emission entry index.
 #ifdef GSR_SORT_TRACE
 // timing build only (tools/sort_trace.py): per workgroup {start, end, list length, hw id}
@@ -806,10 +974,29 @@ __global__ __launch_bounds__(NT) void k_segsort(
   // The counts and this workgroup's tile load together (both lists hold a slot per grid slot).
   const int ct = lz.mode == 2 ? lz.list[blockIdx.x] : busy[blockIdx.x];
   const int nb = lz.mode == 2 ? *lz.count : stats->n_busy;
+  // lists from busy slot n_long on are short: kSortWaves of them per workgroup, a wave each
+  // (the lazy re-sort's list is not in length order: one list per workgroup)
+  constexpr int kSortWaves = NT / 64;
+  const int n_long = lz.mode == 2 || lds_keys < kSortWaves * kWaveSortKeys ? nb : stats->n_sort_long;
   if ((stats->overflow & kOvfCapacity) | (ct < 0)) return;   // bounded call over its caps: nothing to sort
   if (blockIdx.x == 0 && threadIdx.x == 0 && nb > (int)gridDim.x)
     atomicOr(&stats->overflow, lz.mode == 2 ? GSR_OVF_LAZY : GSR_OVF_BUSY);
-  if ((int)blockIdx.x >= nb) return;
+  if ((int)blockIdx.x >= n_long) {
+    const int wv = threadIdx.x >> 6;
+    const int u = n_long + ((int)blockIdx.x - n_long) * kSortWaves + wv;
+    if (lz.mode == 1 && blockIdx.x == (unsigned)n_long && threadIdx.x == 0 && n_long == 0) *lz.count = 0;
+    if (u >= nb) return;
+    const int ctw = busy[u];
+    const int st = tile_offset[ctw];
+    const int ln = tile_offset[ctw + 1] - st;
+    if (lz.mode == 1 && (threadIdx.x & 63) == 0) {   // never lazy (short)
+      lz.tile_sorted[ctw] = st + ln;
+      lz.flag[ctw] = 0;
+    }
+    wave_sort_list(s_keys + wv * kWaveSortKeys, s_hist + wv * 256, ln, keys + st, k_of_slot + st, sorted_ids + st,
+                   k_of_s + st);
+    return;
+  }
   const int start = tile_offset[ct];
   const int len = tile_offset[ct + 1] - start;
 #ifdef GSR_SORT_TRACE
@@ -1233,9 +1420,9 @@ static int bin_sort_impl(const char* who, const float* depth, const uint32_t* re
   // ONE launch: separate launches per class serialise (measured slower whenever long lists
   // exist); the small shape only when every list is short (e.g. the 2D configs)
   if (n_big + n_mid > 0) {
-    int lds_keys = 1024;
-    while (lds_keys < max_seg && lds_keys < kSortLdsKeys) lds_keys <<= 1;
-    lds_keys = min(lds_keys, kSortLdsKeys);
+    // the full LDS image: the short lists are sorted a wave each in kWaveSortKeys-key slices of
+    // it (the kernel's registers allow one workgroup per CU whatever its LDS)
+    const int lds_keys = kSortLdsKeys;
     hipLaunchKernelGGL(k_segsort<kSortThreads>, dim3(n_busy), dim3(kSortThreads),
                        lds_keys * sizeof(uint64_t) + hist_bytes(kSortThreads), s, keys, tmpk, tmpp0, tmpp1,
                        tile_offset, busy_tiles, k_of_slot, lds_keys, sorted_ids, k_of_s, lz, stats);

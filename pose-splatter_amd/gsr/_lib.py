@@ -26,7 +26,7 @@ ORDER_INDEX = 1
 INPUT_ADAPTER = 0
 INPUT_GSPLAT = 1
 
-ABI_VERSION = 3   # include/gsr.h GSR_ABI_VERSION this binding is written for
+ABI_VERSION = 4   # include/gsr.h GSR_ABI_VERSION this binding is written for
 
 # stats->overflow bits of a capacity-bounded call (include/gsr.h GSR_OVF_*)
 OVF_BITS = {1: "intersections > isect cap", 2: "chunks > chunk cap", 4: "busy tiles > n_busy bound",
@@ -47,7 +47,8 @@ class BinStats(ctypes.Structure):
                 ("n_chunks", ctypes.c_int32), ("n_active", ctypes.c_int32),
                 ("n_sort_big", ctypes.c_int32), ("n_sort_mid", ctypes.c_int32),
                 ("isect_cap", ctypes.c_int64), ("chunk_cap", ctypes.c_int64), ("overflow", ctypes.c_int32),
-                ("chunk_entries", ctypes.c_int32), ("status", ctypes.c_void_p), ("reserved", ctypes.c_int64 * 2)]
+                ("chunk_entries", ctypes.c_int32), ("status", ctypes.c_void_p), ("n_sort_long", ctypes.c_int32),
+                ("reserved32", ctypes.c_int32), ("reserved", ctypes.c_int64)]
 
 
 class BinCaps(ctypes.Structure):
