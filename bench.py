@@ -70,6 +70,9 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
+    ap.add_argument("--exchange", default="dense", choices=["dense", "sparse"],
+                    help="--shard units (3D): all-reduce the dense gradient in async buckets, or exchange only "
+                         "the rows each rank touched (gsr.multiview.sparse_sum)")
     ap.add_argument("--shard", default="views", choices=["units", "views"],
                     help="3D, N>1: 'views' (default) = a multi-camera batch, every rank renders C views of its own "
                          "and the Gaussian gradient is all-reduced (weak scaling); 'units' = the ranks split ONE "
@@ -423,11 +426,12 @@ class Workload:
     renders; launch_C / launch_P the cameras / pixels of the dominant launch sequence."""
 
     def __init__(self, cfg, dev, world: int, rank: int, shard: str, buckets: int, loss: str, comm: bool,
-                 view_cost: float = 0.3):
+                 view_cost: float = 0.3, exchange: str = "dense"):
         from gsr import render as R
         from gsr.scenes import gaussians2d, gaussians3d, ring_cameras
         self.R, self.cfg, self.dev, self.world, self.rank = R, cfg, dev, world, rank
         self.view_cost = view_cost * cfg.N   # in list entries (the row weights' unit)
+        self.exchange = exchange
         self.comm = comm and world > 1
         C = cfg.views
         g = torch.Generator().manual_seed(cfg.seed + 1)
@@ -498,7 +502,9 @@ class Workload:
         self.v0, self.v1, self.band = unit_shard(cfg.views, self.th, self.world, self.rank, weights, self.view_cost)
         self.views_here = self.v1 - self.v0
         self.layout = (f"(view, tile-row) units: rank {self.rank} views {self.v0}-{self.v1 - 1} rows {self.band} "
-                       f"of {cfg.views}x{self.th}, {self.buckets} all-reduce bucket(s) overlapping project_bwd")
+                       f"of {cfg.views}x{self.th}, " +
+                       (f"{self.buckets} all-reduce bucket(s) overlapping project_bwd" if self.exchange == "dense" else
+                        "sparse exchange of the touched gradient rows (all-gather)"))
 
     def step(self):
         cfg, R = self.cfg, self.R
@@ -529,7 +535,7 @@ class Workload:
                 from gsr.multiview import sharded_backward_units
                 self.params.grad = sharded_backward_units(None, self.params, self.Vd, self.Kd, self.v_rgb_all,
                                                           self.v_alpha_all, self.th, self.weights, self.buckets,
-                                                          view_cost=self.view_cost)
+                                                          view_cost=self.view_cost, exchange=self.exchange)
             return
         if self.comm and self.scaling == "strong":
             from gsr.multiview import sharded_backward_units
@@ -539,7 +545,7 @@ class Workload:
                 return R.render3d(p, Vs, Ks, cfg.width, cfg.height, self.bg, opts)
             self.params.grad = sharded_backward_units(render_band, self.params, self.Vd, self.Kd, self.v_rgb_all,
                                                       self.v_alpha_all, self.th, self.weights, self.buckets,
-                                                      view_cost=self.view_cost)
+                                                      view_cost=self.view_cost, exchange=self.exchange)
             return
         if self.comm:
             # --shard views: every rank renders its own C views; the gradient is all-reduced in
@@ -713,9 +719,12 @@ def rank_share_report(cfg, args, dev, n: int, weights=None):
         log(f"share {r}/{n}: {1000.0 * el / args.steps:.3f} ms/step ({w.layout})")
         kern = {k: round(v[0], 4) for k, v in sorted(bd.items())}
         kern_sum = sum(v[0] * v[1] for v in bd.values()) / max(2, min(args.steps, 5))   # per step (breakdown pass)
+        touched = None   # Gaussians with a nonzero gradient row in this share (the sparse exchange's rows)
+        if cfg.mode == "3d" and w.params.grad is not None:
+            touched = int(w.params.grad.ne(0).any(1).sum())
         shares.append({"rank": r, "ms_per_step": 1000.0 * el / args.steps, "views_here": w.views_here,
                        "layout": w.layout, "kernels_ms": kern, "kernel_sum_ms": kern_sum,
-                       "I": R.last_stats().get("n_isect", 0)})
+                       "I": R.last_stats().get("n_isect", 0), "touched_rows": touched})
         del w
         torch.cuda.empty_cache()
     grad_bytes = cfg.N * (14 if cfg.mode == "3d" else 9) * 4 * (FRAMES_2D if cfg.mode == "2d" else 1)
@@ -723,7 +732,20 @@ def rank_share_report(cfg, args, dev, n: int, weights=None):
     ar7 = ar / 7.0
     worst = max(s["ms_per_step"] for s in shares)
     units = cfg.views * (FRAMES_2D if cfg.mode == "2d" else 1)
-    return {"n": n, "shares": shares, "max_share_ms": worst, "allreduce_model_ms": ar,
+    sparse = {}
+    if cfg.mode == "3d" and all(s["touched_rows"] is not None for s in shares):
+        # gsr.multiview.sparse_sum: all-gather of every rank's touched rows (index + 14 floats),
+        # padded to the longest list: a ring moves (n-1) lists through each rank's link
+        kmax = max(s["touched_rows"] for s in shares)
+        sp_bytes = (n - 1) * kmax * (14 * 4 + 8)
+        sp = sp_bytes / (XGMI_LINK_GBS * 1e9) * 1e3
+        sparse = {"sparse_exchange": f"all-gather of the touched rows (max {kmax} of {cfg.N}, 64 B each), "
+                                     f"{sp_bytes / 1e6:.1f} MB through one {XGMI_LINK_GBS:.0f} GB/s link",
+                  "sparse_exchange_model_ms": sp, "sparse_exchange_7link_ms": sp / 7.0,
+                  "projected_ms_per_step_sparse": worst + sp, "projected_value_sparse": units / ((worst + sp) * 1e-3),
+                  "projected_ms_per_step_sparse_7link": worst + sp / 7.0,
+                  "projected_value_sparse_7link": units / ((worst + sp / 7.0) * 1e-3)}
+    return {"n": n, "shares": shares, "max_share_ms": worst, **sparse, "allreduce_model_ms": ar,
             "allreduce_model": f"ring 2(n-1)/n x {grad_bytes / 1e6:.1f} MB at {XGMI_LINK_GBS:.0f} GB/s (one link), "
                                "not overlapped (upper bound)",
             "allreduce_7link_ms": ar7,
@@ -812,7 +834,8 @@ def main(argv=None):
 
     if args.loss != "none" and (cfg.mode != "3d" or world > 1):
         raise SystemExit("--loss: 3D configs on one GPU only")
-    w = Workload(cfg, dev, world, rank, args.shard, args.buckets, args.loss, comm=True, view_cost=args.view_cost)
+    w = Workload(cfg, dev, world, rank, args.shard, args.buckets, args.loss, comm=True, view_cost=args.view_cost,
+                 exchange=args.exchange)
     elapsed, breakdown, dom_name, dom = time_steps(w, args.steps, args.warmup, dist, graph=bool(args.graph))
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)

@@ -169,9 +169,43 @@ def bucket_bounds(n: int, buckets: int) -> list:
     return [n * k // nb for k in range(nb + 1)]
 
 
+def sparse_sum(grad: torch.Tensor, group=None) -> torch.Tensor:
+    """The sum over ranks of a partial gradient of which each rank holds only the rows it touched
+    (a (view, tile-row) share: config 5 at 8 ranks touches 2-12 % of the Gaussians per rank,
+    tools/touched.py), exchanging only those rows instead of all-reducing the dense [N, D]:
+    every rank lists its nonzero rows (index + values), the lists are all-gathered (padded to the
+    longest: index 0 with a zero row, which adds nothing) and every rank adds them into a dense
+    result in rank order -- the same sum, bitwise, on every rank (a list holds an index once, so
+    each add is one value per row).  One small all-gather of the counts precedes it (a host
+    read: the padded size)."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world == 1:
+        return grad
+    flat = grad.reshape(grad.shape[0], -1)
+    idx = torch.nonzero(flat.ne(0).any(1)).flatten()
+    k = torch.tensor([idx.numel()], device=grad.device, dtype=torch.int64)
+    ks = [torch.zeros_like(k) for _ in range(world)]
+    dist.all_gather(ks, k, group=group)
+    kmax = max(int(x) for x in ks)
+    if kmax == 0:
+        return torch.zeros_like(grad)
+    idx_pad = torch.zeros(kmax, device=grad.device, dtype=torch.int64)
+    val_pad = torch.zeros(kmax, flat.shape[1], device=grad.device, dtype=grad.dtype)
+    idx_pad[:idx.numel()] = idx
+    val_pad[:idx.numel()] = flat[idx]
+    idxs = [torch.empty_like(idx_pad) for _ in range(world)]
+    vals = [torch.empty_like(val_pad) for _ in range(world)]
+    dist.all_gather(idxs, idx_pad, group=group)
+    dist.all_gather(vals, val_pad, group=group)
+    out = torch.zeros_like(flat)
+    for i, v in zip(idxs, vals):
+        out.index_add_(0, i, v)
+    return out.view_as(grad)
+
+
 def sharded_backward_units(render_band: Callable, params: torch.Tensor, viewmats: torch.Tensor, Ks: torch.Tensor,
                            v_rgb: torch.Tensor, v_alpha: torch.Tensor, rows: int, weights=None, buckets: int = 0,
-                           group=None, view_cost: float = 0.0) -> torch.Tensor:
+                           group=None, view_cost: float = 0.0, exchange: str = "dense") -> torch.Tensor:
     """Gradient of sum(rgb*v_rgb + alpha*v_alpha) over all C views, (view, row)-unit sharded.
 
     ``render_band(p, viewmats_sub, Ks_sub, band, hook)`` renders views v0..v1-1 binned to
@@ -179,12 +213,23 @@ def sharded_backward_units(render_band: Callable, params: torch.Tensor, viewmats
     buckets)`` Gaussian ranges and call ``hook(rows)`` with each range as soon as it is
     enqueued (gsr.render: ``RenderOptions3D(grad_buckets=buckets, grad_hook=hook)``); each
     range is all-reduced asynchronously at once, overlapping the remaining backward.  With
-    ``buckets`` == 0 one all-reduce follows the backward.  Returns the summed gradient
-    (identical on every rank)."""
+    ``buckets`` == 0 one all-reduce follows the backward.  ``exchange="sparse"``: the rows a
+    rank touched are exchanged instead (``sparse_sum``, after the backward; buckets ignored).
+    Returns the summed gradient (identical on every rank)."""
+    if exchange not in ("dense", "sparse"):
+        raise ValueError(f"exchange must be 'dense' or 'sparse', got {exchange!r}")
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     v0, v1, band = unit_shard(viewmats.shape[0], rows, world, rank, weights, view_cost)
     p = params.detach().requires_grad_(True)
+    if exchange == "sparse":
+        if v1 > v0:
+            rgb, alpha = render_band(p, viewmats[v0:v1], Ks[v0:v1], band, None)
+            torch.autograd.backward([rgb, alpha], [v_rgb[v0:v1], v_alpha[v0:v1]])
+            grad = p.grad
+        else:
+            grad = torch.zeros_like(p)
+        return sparse_sum(grad, group)
     pieces, works = [], []
 
     def hook(t):

@@ -106,6 +106,10 @@ def _worker(rank, world, port, out, mode="views"):
     elif mode == "units":
         grad = sharded_backward_units(lambda q, v, k, band, hook: _render_band(q, v, k, band), p, V, K, vr, va,
                                       rows=2, weights=[3.0, 1.0, 2.0, 2.0, 1.0, 1.0, 0.5, 4.0, 1.0, 1.0])
+    elif mode == "units_sparse":
+        grad = sharded_backward_units(lambda q, v, k, band, hook: _render_band(q, v, k, band), p, V, K, vr, va,
+                                      rows=2, weights=[3.0, 1.0, 2.0, 2.0, 1.0, 1.0, 0.5, 4.0, 1.0, 1.0],
+                                      exchange="sparse")
     elif mode == "units_buckets":
         grad = sharded_backward_units(lambda q, v, k, band, hook: _HookRender.apply(q, v, k, band, hook, 3),
                                       p, V, K, vr, va, rows=2, buckets=3)
@@ -171,10 +175,12 @@ def test_band_render_equals_full_render_in_band():
     assert torch.allclose(total, pf.grad, rtol=1e-5, atol=1e-6 * float(pf.grad.abs().max()))
 
 
-@pytest.mark.parametrize("world,mode", [(2, "units"), (3, "units"), (2, "units_buckets"), (3, "units_buckets")])
+@pytest.mark.parametrize("world,mode", [(2, "units"), (3, "units"), (2, "units_buckets"), (3, "units_buckets"),
+                                        (2, "units_sparse"), (4, "units_sparse")])
 def test_unit_sharded_allreduce_matches_single_process(world, mode):
     """(view, row)-unit sharding (strong scaling of one multi-view job): ranks render disjoint
-    view/row ranges; the (bucketed, async) all-reduce of their gradients is the full gradient."""
+    view/row ranges; the (bucketed, async) all-reduce of their gradients -- or the exchange of
+    only the rows each rank touched (units_sparse) -- is the full gradient."""
     from gsr.multiview import sharded_backward
     p, V, K, vr, va = _scene()
     ref = sharded_backward(_render, p, V, K, vr, va)
@@ -183,6 +189,38 @@ def test_unit_sharded_allreduce_matches_single_process(world, mode):
     mp.spawn(_worker, args=(world, _free_port(), out, mode), nprocs=world, join=True)
     for r in range(world):
         assert torch.allclose(out[r], ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max())), r
+    if mode == "units_sparse":   # the same sum, in the same order, on every rank
+        assert all(torch.equal(out[0], out[r]) for r in range(world))
+
+
+def _sparse_worker(rank, world, port, out):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "pose-splatter_amd")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gsr.multiview import sparse_sum
+    g = torch.Generator().manual_seed(100 + rank)
+    part = torch.zeros(50, 14)
+    rows = torch.randperm(50, generator=g)[: 5 + 7 * rank]   # ragged, overlapping, rank 0 small
+    part[rows] = torch.randn(len(rows), 14, generator=g)
+    if rank == world - 1:
+        part.zero_()          # a rank that touched nothing
+    out[rank] = (part, sparse_sum(part))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sparse_sum_equals_dense_sum(world):
+    """sparse_sum: ragged and overlapping touched-row sets, a rank with none -- the dense sum."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_sparse_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    dense = sum(out[r][0] for r in range(world))
+    for r in range(world):
+        assert torch.allclose(out[r][1], dense, rtol=1e-6, atol=1e-6)
+        assert torch.equal(out[r][1], out[0][1])
 
 
 @pytest.mark.parametrize("world", [2, 4])
