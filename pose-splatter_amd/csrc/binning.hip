@@ -461,24 +461,52 @@ __device__ __forceinline__ uint32_t low_word(uint64_t k) { return (uint32_t)(k &
 // (a plain strided loop waits one memory latency per iteration: ~10 iterations per list).
 constexpr int kBatch = 8;
 
+// A sort group: GT consecutive threads of the workgroup (whole waves) that sort one list in
+// their own slice of the LDS image.  sync(): __syncthreads() when the group is the whole
+// workgroup (ctr == nullptr, uniform over the workgroup), else an arrival counter in LDS -- the
+// group's waves are resident together, so spinning on it cannot deadlock, and the release /
+// acquire fences order every LDS access of the group around it.
+template <int GT>
+struct SortGroup {
+  int tid;      // thread index in the group
+  int* ctr;     // LDS arrival counter (zeroed before the group's first sync), or nullptr
+  int phase;    // arrivals of this group's waves so far (uniform)
+  __device__ __forceinline__ void sync() {
+    if (ctr == nullptr) {
+      __syncthreads();
+      return;
+    }
+    phase += GT / 64;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < phase) __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+};
+// the group's counters in LDS: W waves' digit counters (W x 256 ints), then 64 misc ints
+// (varying bits, tie-run count and flags, the scan's wave sums, the barrier counter last)
+constexpr int kGroupMisc = 64;
+__host__ __device__ constexpr int group_ints(int waves) { return waves * 256 + kGroupMisc; }
+
 // a[i] = (sort word of src[i]) << 32 | (pbase + i), i < n.  Returns this thread's OR of
-// (word ^ src[0]'s word): the bits that vary inside the list, once OR-ed over the block.
-// (16 loads in flight per thread: a list of up to 16 NT keys arrives in one round trip)
+// (word ^ src[0]'s word): the bits that vary inside the list, once OR-ed over the group.
+// (16 loads in flight per thread: a list of up to 16 GT keys arrives in one round trip)
 constexpr int kStageBatch = 16;
-template <int NT>
-__device__ __forceinline__ uint32_t stage_keys(uint64_t* a, const uint64_t* __restrict__ src, int n, int pbase) {
+template <int GT>
+__device__ __forceinline__ uint32_t stage_keys(const SortGroup<GT>& g, uint64_t* a, const uint64_t* __restrict__ src,
+                                               int n, int pbase) {
   const uint32_t w0 = sort_word(src[0]);
   uint32_t orv = 0;
-  for (int i0 = threadIdx.x; i0 < n; i0 += kStageBatch * NT) {
+  for (int i0 = g.tid; i0 < n; i0 += kStageBatch * GT) {
     uint32_t w[kStageBatch];
 #pragma unroll
     for (int j = 0; j < kStageBatch; ++j) {
-      const int i = i0 + j * NT;
+      const int i = i0 + j * GT;
       w[j] = sort_word(src[i < n ? i : 0]);
     }
 #pragma unroll
     for (int j = 0; j < kStageBatch; ++j) {
-      const int i = i0 + j * NT;
+      const int i = i0 + j * GT;
       orv |= w[j] ^ w0;   // (a clamped duplicate of src[0] adds nothing)
       if (i < n) a[i] = ((uint64_t)w[j] << 32) | (uint64_t)(uint32_t)(pbase + i);
     }
@@ -486,32 +514,61 @@ __device__ __forceinline__ uint32_t stage_keys(uint64_t* a, const uint64_t* __re
   return orv;
 }
 
-// The varying bits of the sort words: the block OR of every thread's `orv` (s_misc[0] must be
+// The varying bits of the sort words: the group OR of every thread's `orv` (s_misc[0] must be
 // zero on entry; it is left holding the result).  One atomic per wave.
-template <int NT>
-__device__ __forceinline__ uint32_t block_varying(uint32_t orv, int* s_misc) {
+template <int GT>
+__device__ __forceinline__ uint32_t block_varying(SortGroup<GT>& g, uint32_t orv, int* s_misc) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) orv |= (uint32_t)__shfl_xor((int)orv, o, 64);
   if ((threadIdx.x & 63) == 0 && orv) atomicOr((unsigned*)&s_misc[0], orv);
-  __syncthreads();
+  g.sync();
   return (uint32_t)s_misc[0];
 }
 
 // The same from keys already in LDS
-template <int NT>
-__device__ __forceinline__ uint32_t lds_varying(const uint64_t* a, int n, int* s_misc) {
-  if (threadIdx.x == 0) s_misc[0] = 0;
-  __syncthreads();
+template <int GT>
+__device__ __forceinline__ uint32_t lds_varying(SortGroup<GT>& g, const uint64_t* a, int n, int* s_misc) {
+  if (g.tid == 0) s_misc[0] = 0;
+  g.sync();
   const uint32_t w0 = sort_word(a[0]);
   uint32_t orv = 0;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) orv |= sort_word(a[i]) ^ w0;
-  return block_varying<NT>(orv, s_misc);
+  for (int i = g.tid; i < n; i += GT) orv |= sort_word(a[i]) ^ w0;
+  return block_varying<GT>(g, orv, s_misc);
+}
+
+// Group-wide exclusive scan of one int per thread; s_tmp holds GT/64 + 1 ints.
+template <int GT>
+__device__ __forceinline__ int group_exclusive_scan(SortGroup<GT>& g, int v, int* s_tmp, int* total) {
+  const int lane = threadIdx.x & 63;
+  const int w = g.tid >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_tmp[w] = x;
+  g.sync();
+  if (g.tid == 0) {
+    int acc = 0;
+    for (int k = 0; k < GT / 64; ++k) {
+      const int t = s_tmp[k];
+      s_tmp[k] = acc;
+      acc += t;
+    }
+    s_tmp[GT / 64] = acc;
+  }
+  g.sync();
+  const int res = x - v + s_tmp[w];
+  *total = s_tmp[GT / 64];
+  g.sync();
+  return res;
 }
 
 // a[i] = src[i], i < n
 template <int NT>
-__device__ __forceinline__ void copy_keys(uint64_t* a, const uint64_t* __restrict__ src, int n) {
-  for (int i0 = threadIdx.x; i0 < n; i0 += kBatch * NT) {
+__device__ __forceinline__ void copy_keys(uint64_t* a, const uint64_t* __restrict__ src, int n, int tid = -1) {
+  for (int i0 = tid >= 0 ? tid : (int)threadIdx.x; i0 < n; i0 += kBatch * NT) {
     uint64_t w[kBatch];
 #pragma unroll
     for (int j = 0; j < kBatch; ++j) {
@@ -556,50 +613,47 @@ __device__ __forceinline__ void write_sorted(const uint64_t* a, int n, const uin
   }
 }
 
-// write_sorted for a list held whole in LDS (p indexes a, capacity >= n 64-bit slots): the
-// sorted p's move to registers, the list's ids (low words of seg) and emission indices are then
-// loaded COALESCED into the same LDS (as two n-word arrays), and each sorted entry reads its
-// pair there.  A long list's write was two random global gathers per key, all issued by the
-// one workgroup that owns the list (~17 us of a 42 us sort at 11 880 keys).
-template <int NT>
-__device__ __forceinline__ void write_sorted_lds(uint64_t* a, int n, const uint64_t* __restrict__ seg,
-                                                 const int32_t* __restrict__ kslot, int32_t* __restrict__ ids,
-                                                 int32_t* __restrict__ kos) {
-  // the direct path's longest list: lds_keys <= kSortLdsKeys (kSortThreads) or kSortSmallKeys
-  constexpr int kMaxKeys = NT == kSortThreadsSmall ? kSortSmallKeys : kSortLdsKeys;
-  constexpr int kMaxPer = (kMaxKeys + NT - 1) / NT;
-  static_assert(kMaxPer <= 16, "sorted positions held in registers");
+// write_sorted for a list held whole in LDS (p indexes a, capacity >= n 64-bit slots, n <= 16
+// GT): the sorted p's move to registers, the list's ids (low words of seg) and emission indices
+// are then loaded COALESCED into the same LDS (as two n-word arrays), and each sorted entry
+// reads its pair there.  A long list's write was two random global gathers per key, all issued
+// by the one workgroup that owns the list (~17 us of a 42 us sort at 11 880 keys).
+template <int GT>
+__device__ __forceinline__ void write_sorted_lds(SortGroup<GT>& g, uint64_t* a, int n,
+                                                 const uint64_t* __restrict__ seg, const int32_t* __restrict__ kslot,
+                                                 int32_t* __restrict__ ids, int32_t* __restrict__ kos) {
+  constexpr int kMaxPer = 16;   // every caller's slice holds at most 16 GT keys
   uint16_t pv[kMaxPer];
 #pragma unroll
   for (int j = 0; j < kMaxPer; ++j) {
-    const int s = (int)threadIdx.x + j * NT;
+    const int s = g.tid + j * GT;
     pv[j] = s < n ? (uint16_t)low_word(a[s]) : (uint16_t)0;
   }
-  __syncthreads();
+  g.sync();
   uint32_t* xid = reinterpret_cast<uint32_t*>(a);
   int32_t* xk = reinterpret_cast<int32_t*>(a) + n;
-  for (int i0 = threadIdx.x; i0 < n; i0 += kMaxPer * NT) {   // one round trip
+  for (int i0 = g.tid; i0 < n; i0 += kMaxPer * GT) {   // one round trip
     uint32_t id[kMaxPer];
     int32_t ko[kMaxPer];
 #pragma unroll
     for (int j = 0; j < kMaxPer; ++j) {
-      const int i = i0 + j * NT;
+      const int i = i0 + j * GT;
       id[j] = low_word(seg[i < n ? i : 0]);
       ko[j] = kslot[i < n ? i : 0];
     }
 #pragma unroll
     for (int j = 0; j < kMaxPer; ++j) {
-      const int i = i0 + j * NT;
+      const int i = i0 + j * GT;
       if (i < n) {
         xid[i] = id[j];
         xk[i] = ko[j];
       }
     }
   }
-  __syncthreads();
+  g.sync();
 #pragma unroll
   for (int j = 0; j < kMaxPer; ++j) {
-    const int s = (int)threadIdx.x + j * NT;
+    const int s = g.tid + j * GT;
     if (s < n) {
       ids[s] = (int32_t)xid[pv[j]];
       kos[s] = xk[pv[j]];
@@ -607,18 +661,19 @@ __device__ __forceinline__ void write_sorted_lds(uint64_t* a, int n, const uint6
   }
 }
 
-// a: n <= 16*NT elements (word << 32 | p) in LDS; seg: the bucket's original keys
-// (tie-break by their low word); s_hist: (NT/64)*256 + 64 ints.
-// varying: the bits in which the sort words differ (block_varying / lds_varying).
-template <int NT>
-__device__ __forceinline__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, const uint64_t* __restrict__ seg,
-                                               uint32_t varying) {
-  constexpr int kSortWaves = NT / 64;
+// a: n <= 16*GT elements (word << 32 | p) in LDS; seg: the bucket's original keys (tie-break
+// by their low word); s_hist: the group's group_ints(GT/64) counters (the misc ints follow the
+// digit counters).  varying: the bits in which the sort words differ (block_varying /
+// lds_varying).
+template <int GT>
+__device__ __forceinline__ void lds_radix_sort(SortGroup<GT>& g, uint64_t* a, int n, int* s_hist,
+                                               const uint64_t* __restrict__ seg, uint32_t varying) {
+  constexpr int kSortWaves = GT / 64;
   constexpr int kWaveBits = kSortWaves == 16 ? 4 : (kSortWaves == 8 ? 3 : 2);
   static_assert(kSortWaves == 16 || kSortWaves == 8 || kSortWaves == 4, "16, 8 or 4 waves");
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wv = g.tid >> 6, lane = threadIdx.x & 63;
   int* s_misc = s_hist + kSortWaves * 256;
-  if (threadIdx.x == 0) {   // tie-run count and long-run flag (the passes' barriers order these)
+  if (g.tid == 0) {   // tie-run count and long-run flag (the passes' barriers order these)
     s_misc[1] = 0;
     s_misc[2] = 0;
   }
@@ -645,27 +700,27 @@ __device__ __forceinline__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, 
         rk[r] = valid ? (int)((d << 23) | (uint32_t)atomicAdd(&s_hist[wv * 256 + d], 1)) : -1;   // pos < 2^23
       }
     }
-    __syncthreads();
-    // digit-major, wave-minor exclusive scan of the 16 x 256 counters: 4 per thread
+    g.sync();
+    // digit-major, wave-minor exclusive scan of the W x 256 counters: 4 per thread
     {
       int v[4];
       int sum = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int c = threadIdx.x * 4 + j;
+        const int c = g.tid * 4 + j;
         v[j] = s_hist[(c & (kSortWaves - 1)) * 256 + (c >> kWaveBits)];
         sum += v[j];
       }
       int total;
-      int run = block_exclusive_scan<NT>(sum, s_misc + 8, &total);
+      int run = group_exclusive_scan<GT>(g, sum, s_misc + 8, &total);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int c = threadIdx.x * 4 + j;
+        const int c = g.tid * 4 + j;
         s_hist[(c & (kSortWaves - 1)) * 256 + (c >> kWaveBits)] = run;
         run += v[j];
       }
     }
-    __syncthreads();
+    g.sync();
 #pragma unroll
     for (int r = 0; r < kSortRounds; ++r) {
       if (r < rounds && rk[r] >= 0) {
@@ -673,7 +728,7 @@ __device__ __forceinline__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, 
         a[s_hist[wv * 256 + d] + (rk[r] & 0x7FFFFF)] = el[r];
       }
     }
-    __syncthreads();
+    g.sync();
     SORT_T(2 + shift / 8);
   }
   SORT_T(6);
@@ -684,7 +739,7 @@ __device__ __forceinline__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, 
   int* s_runs = s_hist;   // the counters are free now
   constexpr int kMaxRuns = kSortWaves * 256;
   constexpr int kMaxRunLen = 32;
-  for (int i = threadIdx.x; i < n; i += NT) {
+  for (int i = g.tid; i < n; i += GT) {
     const uint32_t w = sort_word(a[i]);
     const bool starts = i + 1 < n && sort_word(a[i + 1]) == w && (i == 0 || sort_word(a[i - 1]) != w);
     if (starts) {
@@ -692,10 +747,10 @@ __device__ __forceinline__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, 
       if (r < kMaxRuns) s_runs[r] = i;
     }
   }
-  __syncthreads();
+  g.sync();
   const int n_runs = s_misc[1];
   if (n_runs <= kMaxRuns) {
-    for (int r = threadIdx.x; r < n_runs; r += NT) {
+    for (int r = g.tid; r < n_runs; r += GT) {
       const int i0 = s_runs[r];
       const uint32_t w = sort_word(a[i0]);
       int i1 = i0 + 1;
@@ -715,17 +770,18 @@ __device__ __forceinline__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, 
         a[j + 1] = x;
       }
     }
-    __syncthreads();
+    g.sync();
     SORT_T(7);
     if (s_misc[2] == 0) return;
   }
   // (more runs than the list can hold, or a run too long for one thread: odd-even passes
-  // until nothing moves)
+  // until nothing moves; s_misc[3] collects "moved" over the group)
   while (true) {
     bool moved = false;
+    if (g.tid == 0) s_misc[3] = 0;
 #pragma unroll
     for (int ph = 0; ph < 2; ++ph) {
-      for (int i = 2 * threadIdx.x + ph; i + 1 < n; i += 2 * blockDim.x) {
+      for (int i = 2 * g.tid + ph; i + 1 < n; i += 2 * GT) {
         const uint64_t x = a[i], y = a[i + 1];
         if (sort_word(x) == sort_word(y) && low_word(seg[low_word(x)]) > low_word(seg[low_word(y)])) {
           a[i] = y;
@@ -733,9 +789,13 @@ __device__ __forceinline__ void lds_radix_sort(uint64_t* a, int n, int* s_hist, 
           moved = true;
         }
       }
-      __syncthreads();
+      g.sync();
     }
-    if (!__syncthreads_or(moved)) break;
+    if (__ballot(moved) != 0ull && lane == 0) atomicOr(&s_misc[3], 1);
+    g.sync();
+    const bool any = s_misc[3] != 0;
+    g.sync();
+    if (!any) break;
   }
   SORT_T(7);
 }
@@ -974,28 +1034,78 @@ __global__ __launch_bounds__(NT) void k_segsort(
   // The counts and this workgroup's tile load together (both lists hold a slot per grid slot).
   const int ct = lz.mode == 2 ? lz.list[blockIdx.x] : busy[blockIdx.x];
   const int nb = lz.mode == 2 ? *lz.count : stats->n_busy;
-  // lists from busy slot n_long on are short: kSortWaves of them per workgroup, a wave each
-  // (the lazy re-sort's list is not in length order: one list per workgroup)
+  // List classes (the busy order is by log2 length, longest first; tile scan counts): A
+  // (>= 8192 entries, or every list of the 256-thread shape that is >= 1024) one workgroup
+  // each; B (4096..8191) two per workgroup, 8 waves and an 8 192-key slice each; C
+  // (1024..4095) four per workgroup, 4 waves and 4 096 keys each; D (< 1024) a wave each.
+  // The groups of B / C synchronise through LDS counters (SortGroup), not workgroup barriers,
+  // so a long list no longer holds 16 waves through every barrier of a short one.  The lazy
+  // re-sort's list is not in length order: one list per workgroup.
   constexpr int kSortWaves = NT / 64;
-  const int n_long = lz.mode == 2 || lds_keys < kSortWaves * kWaveSortKeys ? nb : stats->n_sort_long;
+  const bool pack = lz.mode != 2 && lds_keys >= kSortWaves * kWaveSortKeys;
+  int n_long = pack ? stats->n_sort_long : nb;
+  int nA = !pack ? nb : (NT == 1024 ? stats->n_sort_big : n_long);
+  int nAB = !pack ? nb : (NT == 1024 ? nA + stats->n_sort_mid : nA);
+  if (lz.mode == 1) {   // a list that may be sorted lazily (longer than min_len) takes class A
+    if (lz.min_len < kWaveSortKeys - 1) nA = nAB = n_long = nb;
+    else if (lz.min_len < 4095) nA = nAB = n_long;
+    else if (lz.min_len < 8191) nA = nAB;
+  }
+  const int wA = nA, wB = wA + (nAB - nA + 1) / 2, wC = wB + (n_long - nAB + 3) / 4;
   if ((stats->overflow & kOvfCapacity) | (ct < 0)) return;   // bounded call over its caps: nothing to sort
   if (blockIdx.x == 0 && threadIdx.x == 0 && nb > (int)gridDim.x)
     atomicOr(&stats->overflow, lz.mode == 2 ? GSR_OVF_LAZY : GSR_OVF_BUSY);
-  if ((int)blockIdx.x >= n_long) {
+  if (lz.mode == 1 && blockIdx.x == 0 && threadIdx.x == 0 && nA == 0) *lz.count = 0;
+  if ((int)blockIdx.x >= wC) {   // D: a wave per list
     const int wv = threadIdx.x >> 6;
-    const int u = n_long + ((int)blockIdx.x - n_long) * kSortWaves + wv;
-    if (lz.mode == 1 && blockIdx.x == (unsigned)n_long && threadIdx.x == 0 && n_long == 0) *lz.count = 0;
+    const int u = n_long + ((int)blockIdx.x - wC) * kSortWaves + wv;
     if (u >= nb) return;
     const int ctw = busy[u];
     const int st = tile_offset[ctw];
     const int ln = tile_offset[ctw + 1] - st;
-    if (lz.mode == 1 && (threadIdx.x & 63) == 0) {   // never lazy (short)
+    if (lz.mode == 1 && (threadIdx.x & 63) == 0) {   // sorted whole (at most a wave's slice)
       lz.tile_sorted[ctw] = st + ln;
       lz.flag[ctw] = 0;
     }
     wave_sort_list(s_keys + wv * kWaveSortKeys, s_hist + wv * 256, ln, keys + st, k_of_slot + st, sorted_ids + st,
                    k_of_s + st);
     return;
+  }
+  if constexpr (NT == 1024) {
+    if ((int)blockIdx.x >= wA) {   // B or C: 2 or 4 lists per workgroup
+      const bool is_b = (int)blockIdx.x < wB;
+      const int W = is_b ? 8 : 4;   // waves per group
+      const int gi = (threadIdx.x >> 6) / W;
+      const int u = is_b ? nA + ((int)blockIdx.x - wA) * 2 + gi : nAB + ((int)blockIdx.x - wB) * 4 + gi;
+      int* ghist = s_hist + gi * group_ints(W);
+      int* gmisc = ghist + W * 256;
+      uint64_t* slice = s_keys + gi * (lds_keys / (is_b ? 2 : 4));
+      if ((threadIdx.x & (64 * W - 1)) == 0) {
+        gmisc[0] = 0;                 // varying bits
+        gmisc[kGroupMisc - 1] = 0;    // barrier counter
+      }
+      __syncthreads();   // the last workgroup-wide barrier of this path
+      if (u >= (is_b ? nAB : n_long)) return;
+      const int ctg = busy[u];
+      const int st = tile_offset[ctg];
+      const int ln = tile_offset[ctg + 1] - st;
+      if (lz.mode == 1 && (threadIdx.x & (64 * W - 1)) == 0) {   // sorted whole (fits the slice)
+        lz.tile_sorted[ctg] = st + ln;
+        lz.flag[ctg] = 0;
+      }
+      if (is_b) {
+        SortGroup<512> g{(int)threadIdx.x & 511, gmisc + kGroupMisc - 1, 0};
+        const uint32_t varying = block_varying<512>(g, stage_keys<512>(g, slice, keys + st, ln, 0), gmisc);
+        lds_radix_sort<512>(g, slice, ln, ghist, keys + st, varying);
+        write_sorted_lds<512>(g, slice, ln, keys + st, k_of_slot + st, sorted_ids + st, k_of_s + st);
+      } else {
+        SortGroup<256> g{(int)threadIdx.x & 255, gmisc + kGroupMisc - 1, 0};
+        const uint32_t varying = block_varying<256>(g, stage_keys<256>(g, slice, keys + st, ln, 0), gmisc);
+        lds_radix_sort<256>(g, slice, ln, ghist, keys + st, varying);
+        write_sorted_lds<256>(g, slice, ln, keys + st, k_of_slot + st, sorted_ids + st, k_of_s + st);
+      }
+      return;
+    }
   }
   const int start = tile_offset[ct];
   const int len = tile_offset[ct + 1] - start;
@@ -1020,14 +1130,15 @@ __global__ __launch_bounds__(NT) void k_segsort(
       lz.tile_end[ct] = -1;   // the forward renders this tile again
     }
   }
+  SortGroup<NT> g{(int)threadIdx.x, nullptr, 0};   // the whole workgroup
   if (len <= lds_keys && !lazy) {
     int* s_misc = s_hist + (NT / 64) * 256;
     if (threadIdx.x == 0) s_misc[0] = 0;
     __syncthreads();
     // the varying bits are OR-ed while staging (the barrier after the staging is block_varying's)
-    const uint32_t varying = block_varying<NT>(stage_keys<NT>(s_keys, seg, len, 0), s_misc);
-    lds_radix_sort<NT>(s_keys, len, s_hist, seg, varying);
-    write_sorted_lds<NT>(s_keys, len, seg, k_of_slot + start, sorted_ids + start, k_of_s + start);
+    const uint32_t varying = block_varying<NT>(g, stage_keys<NT>(g, s_keys, seg, len, 0), s_misc);
+    lds_radix_sort<NT>(g, s_keys, len, s_hist, seg, varying);
+    write_sorted_lds<NT>(g, s_keys, len, seg, k_of_slot + start, sorted_ids + start, k_of_s + start);
     return;
   }
   // Long list (> lds_keys): MSD partition by the top 8 varying bits of the sort word into
@@ -1119,7 +1230,7 @@ __global__ __launch_bounds__(NT) void k_segsort(
         if (n > 0) {
           copy_keys<NT>(s_keys, part + g0, n);
           __syncthreads();
-          lds_radix_sort<NT>(s_keys, n, s_hist, seg, lds_varying<NT>(s_keys, n, s_hist + (NT / 64) * 256));
+          lds_radix_sort<NT>(g, s_keys, n, s_hist, seg, lds_varying<NT>(g, s_keys, n, s_hist + (NT / 64) * 256));
           write_sorted<NT>(s_keys, n, seg, k_of_slot + start, sorted_ids + start + g0, k_of_s + start + g0);
           __syncthreads();
         }
@@ -1139,9 +1250,9 @@ __global__ __launch_bounds__(NT) void k_segsort(
   int32_t* pB = tmpp1 + start;
   for (int r0 = 0; r0 < len; r0 += lds_keys) {
     const int rl = min(lds_keys, len - r0);
-    stage_keys<NT>(s_keys, seg + r0, rl, r0);
+    stage_keys<NT>(g, s_keys, seg + r0, rl, r0);
     __syncthreads();
-    lds_radix_sort<NT>(s_keys, rl, s_hist, seg, lds_varying<NT>(s_keys, rl, s_hist + (NT / 64) * 256));
+    lds_radix_sort<NT>(g, s_keys, rl, s_hist, seg, lds_varying<NT>(g, s_keys, rl, s_hist + (NT / 64) * 256));
     for (int i = threadIdx.x; i < rl; i += blockDim.x) {
       const uint32_t p = low_word(s_keys[i]);
       kA[r0 + i] = (s_keys[i] & 0xffffffff00000000ull) | (uint64_t)low_word(seg[p]);
@@ -1210,10 +1321,11 @@ __global__ __launch_bounds__(kSplitThreads) void k_split_blocksort(
   if (b0 >= len) return;
   const int n = min(kSplitBlock, len - b0);
   const uint64_t* seg = keys + start;
-  stage_keys<kSplitThreads>(s_keys, seg + b0, n, b0);
+  SortGroup<kSplitThreads> g{(int)threadIdx.x, nullptr, 0};
+  stage_keys<kSplitThreads>(g, s_keys, seg + b0, n, b0);
   __syncthreads();
-  lds_radix_sort<kSplitThreads>(s_keys, n, s_hist, seg,
-                                lds_varying<kSplitThreads>(s_keys, n, s_hist + (kSplitThreads / 64) * 256));
+  lds_radix_sort<kSplitThreads>(g, s_keys, n, s_hist, seg,
+                                lds_varying<kSplitThreads>(g, s_keys, n, s_hist + (kSplitThreads / 64) * 256));
   if (len <= kSplitBlock) {   // one block: final order
     write_sorted<kSplitThreads>(s_keys, n, seg, k_of_slot + start, sorted_ids + start, k_of_s + start);
     return;
@@ -1404,7 +1516,8 @@ static int bin_sort_impl(const char* who, const float* depth, const uint32_t* re
   }
   GSR_REQUIRE(n_big >= 0 && n_mid >= 0 && n_big + n_mid <= n_busy, "%s: bad sort classes %d/%d of %d", who,
               n_big, n_mid, n_busy);
-  auto hist_bytes = [](int nt) { return (size_t)((nt / 64) * 256 + 64) * sizeof(int); };
+  // counters: the 1024-thread shape's largest layout is class C (four 4-wave groups)
+  auto hist_bytes = [](int nt) { return (size_t)(nt == 1024 ? 4 * group_ints(4) : group_ints(nt / 64)) * sizeof(int); };
   if (lz.mode == 0 && g_split_sort && n_busy > 0 && n_busy <= kSplitMaxBusy && max_seg > kSplitBlock &&
       max_seg <= kSortLdsKeys) {
     const int nb_max = (max_seg + kSplitBlock - 1) / kSplitBlock;
