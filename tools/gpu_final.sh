@@ -4,11 +4,13 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-V=${V:-r03_v4}
+V=${V:-r03_v5}
 R=${R:-03}
 if [ -z "$SKIP_PMC" ]; then
   bash tools/pmc_config.sh $R 3 > gpurun_out/${V}_pmc.log 2>&1 || { tail -20 gpurun_out/${V}_pmc.log; exit 1; }
   cp gpurun_out/pmc_cfg3/r${R}_pmc_*cfg3*.csv profiles/
+fi
+if [ -z "$SKIP_TRACE" ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${V}_trace_cfg3 -o run -- python -u bench.py --config 3 --steps 20 --warmup 3 --cpu-baseline 0 --psnr 0 > gpurun_out/${V}_trace_cfg3.json 2> gpurun_out/${V}_trace_cfg3.err || { tail -20 gpurun_out/${V}_trace_cfg3.err; exit 1; }
 fi
 for c in ${CONFIGS:-3 2 5 4}; do
