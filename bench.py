@@ -73,11 +73,13 @@ def parse(argv=None):
     ap.add_argument("--exchange", default="dense", choices=["dense", "sparse"],
                     help="--shard units (3D): all-reduce the dense gradient in async buckets, or exchange only "
                          "the rows each rank touched (gsr.multiview.sparse_sum)")
-    ap.add_argument("--shard", default="views", choices=["units", "views"],
+    ap.add_argument("--shard", default=None, choices=["units", "views", "frames"],
                     help="3D, N>1: 'views' (default) = a multi-camera batch, every rank renders C views of its own "
                          "and the Gaussian gradient is all-reduced (weak scaling); 'units' = the ranks split ONE "
                          "C-view job by (view, tile row) units (strong scaling; latency- and exchange-bound, "
-                         "see DESIGN.md §5 and --rank-share)")
+                         "see DESIGN.md §5 and --rank-share).  2D (config 4), N>1: 'frames' (default) = frame f "
+                         "with all its views on rank f %% N, no Gaussian-gradient exchange (the frames' sets are "
+                         "disjoint); 'units' = (frame, view) units round-robin with a per-frame-bucket all-reduce")
     ap.add_argument("--buckets", type=int, default=0,
                     help="all-reduce buckets (3D: Gaussian ranges of v_params; 2D: frame ranges); 0 = default "
                          "(3D 4, 2D 2; 1 on a single GPU)")
@@ -109,10 +111,19 @@ def parse(argv=None):
     ap.add_argument("--capacity", default="bounded", choices=["bounded", "exact"],
                     help="bounded: no host sync per step (bounds from the previous step, checked on device); "
                          "exact: one 32-byte stats read-back per forward")
+    ap.add_argument("--split", type=int, default=1,
+                    help="3D, one GPU: render the views in SPLIT groups, each group's whole fwd+bwd on its own HIP "
+                         "stream (forked and joined inside the step, so a captured graph holds SPLIT independent "
+                         "branches), gradients summed at the join")
     ap.add_argument("--graph", type=int, default=-1, choices=[-1, 0, 1],
                     help="1: capture the timed steps as one HIP graph (needs --capacity bounded); 0: eager "
                          "launches; -1: 1 on a single GPU with bounded capacity, else 0")
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    if a.shard is None:
+        a.shard = "frames" if a.config == 4 else "views"
+    if a.shard == "frames" and a.config != 4:
+        raise SystemExit("--shard frames is the 2D multi-frame layout (config 4)")
+    return a
 
 
 # ------------------------------------------------------------------ algorithmic bytes (§8(d))
@@ -437,14 +448,16 @@ class Workload:
         g = torch.Generator().manual_seed(cfg.seed + 1)
         self.bg = torch.ones(3, device=dev)
         self.loss = loss
+        self.split = 1
         if cfg.mode == "2d":
             F = FRAMES_2D
             self.params_cpu = torch.stack([gaussians2d(cfg.N, cfg.width, cfg.height, cfg.seed + f) for f in range(F)])
             self.V, self.K = ring_cameras(1, cfg.width, cfg.height)
             self.p_dim = 9
-            from gsr.multiview import frame_view_units
-            self.units = frame_view_units(F, C, world, rank)
-            self.buckets = buckets or (1 if world == 1 else 2)
+            from gsr.multiview import frame_owner_units, frame_view_units
+            self.owned = shard == "frames"
+            self.units = (frame_owner_units if self.owned else frame_view_units)(F, C, world, rank)
+            self.buckets = buckets or (1 if world == 1 or self.owned else 2)
             idx = [f * C + v for f, v in self.units]
             vr = torch.randn(F * C, cfg.height, cfg.width, 3, generator=g)
             va = torch.randn(F * C, cfg.height, cfg.width, generator=g)
@@ -452,9 +465,14 @@ class Workload:
             self.units_total = F * C
             self.views_here = len(self.units)
             self.scaling = "strong"
-            self.layout = (f"(frame, view) units round-robin over {world} rank(s), batched per frame bucket "
-                           f"({self.buckets}), async all-reduce of the [8,N,9] gradient per bucket"
-                           if world > 1 else f"{F} frames x {C} views batched in one launch sequence")
+            if world == 1:
+                self.layout = f"{F} frames x {C} views batched in one launch sequence"
+            elif self.owned:
+                self.layout = (f"frame owners: frame f with its {C} views on rank f % {world}, batched in one launch "
+                               "sequence; no Gaussian-gradient exchange (disjoint frame sets)")
+            else:
+                self.layout = (f"(frame, view) units round-robin over {world} rank(s), batched per frame bucket "
+                               f"({self.buckets}), async all-reduce of the [8,N,9] gradient per bucket")
         else:
             self.params_cpu = gaussians3d(cfg.N, cfg.seed)
             self.p_dim = 14
@@ -510,11 +528,14 @@ class Workload:
         cfg, R = self.cfg, self.R
         self.params.grad = None
         if cfg.mode == "2d":
-            from gsr.multiview import sharded_backward_frames
+            from gsr.multiview import owned_backward_frames, sharded_backward_frames
 
             def render_units(p, sets):
                 return R.render2d_units(p, sets, cfg.width, cfg.height, self.bg)
-            if self.comm:
+            if self.comm and self.owned:
+                self.params.grad = owned_backward_frames(render_units, self.params, self.units, self.v_rgb,
+                                                         self.v_alpha)
+            elif self.comm:
                 self.params.grad = sharded_backward_frames(render_units, self.params, self.units, self.v_rgb,
                                                            self.v_alpha, self.buckets)
             elif self.units:
@@ -567,10 +588,43 @@ class Workload:
             full = pieces[0]._base if pieces[0]._base is not None else pieces[0]
             self.params.grad = full.view_as(self.params)
             return
+        if self.split > 1 and self.band == (0, -1):
+            self._split_step()
+            return
         opts = R.RenderOptions3D(band=self.band) if self.band != (0, -1) else R.RenderOptions3D()
         rgb, alpha = R.render3d(self.params, self.Vd[self.v0:self.v1], self.Kd[self.v0:self.v1], cfg.width,
                                 cfg.height, self.bg, opts)
         torch.autograd.backward([rgb, alpha], [self.v_rgb_all[self.v0:self.v1], self.v_alpha_all[self.v0:self.v1]])
+
+    def _split_step(self):
+        """--split G: the views in G groups, each group's fwd+bwd on its own stream; the groups'
+        gradients are summed on the step's stream after the join."""
+        cfg, R = self.cfg, self.R
+        n = self.v1 - self.v0
+        G = min(self.split, n)
+        if not hasattr(self, "_streams"):
+            self._streams = [torch.cuda.Stream(self.dev) for _ in range(G)]
+        cur = torch.cuda.current_stream(self.dev)
+        grads = []
+        for gi in range(G):
+            a = self.v0 + n * gi // G
+            b = self.v0 + n * (gi + 1) // G
+            st = self._streams[gi]
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                p = self.params.detach().requires_grad_(True)
+                rgb, alpha = R.render3d(p, self.Vd[a:b], self.Kd[a:b], cfg.width, cfg.height, self.bg,
+                                        R.RenderOptions3D(tag=gi))
+                torch.autograd.backward([rgb, alpha], [self.v_rgb_all[a:b], self.v_alpha_all[a:b]])
+                grads.append(p.grad)
+        for st in self._streams[:G]:
+            cur.wait_stream(st)
+        for g in grads:
+            g.record_stream(cur)
+        tot = grads[0]
+        for g in grads[1:]:
+            tot = tot + g
+        self.params.grad = tot
 
     def _loss_step(self):
         """The reference training loss on the render: IoU + L1 image + ssim_lambda * (1 - SSIM)
@@ -605,6 +659,9 @@ class Workload:
         if self.scaling == "strong" and self.world > 1 or getattr(self, "band", (0, -1)) != (0, -1):
             rows = self.band[1] - self.band[0]
             return self.views_here, min(rows * 16 * cfg.width, self.views_here * cfg.width * cfg.height)
+        if self.split > 1:   # one launch covers one view group (the last group's stats)
+            c = self.views_here - self.views_here * (self.split - 1) // self.split
+            return c, c * cfg.width * cfg.height
         return self.views_here, self.views_here * cfg.width * cfg.height
 
 
@@ -709,7 +766,8 @@ def rank_share_report(cfg, args, dev, n: int, weights=None):
     from gsr import render as R
     shares = []
     for r in range(n):
-        w = Workload(cfg, dev, n, r, "units", args.buckets, "none", comm=False, view_cost=args.view_cost)
+        w = Workload(cfg, dev, n, r, args.shard if cfg.mode == "2d" else "units", args.buckets, "none", comm=False,
+                     view_cost=args.view_cost)
         if cfg.mode == "3d" and w.scaling == "strong":
             if weights is None:
                 weights = w.weights
@@ -728,6 +786,8 @@ def rank_share_report(cfg, args, dev, n: int, weights=None):
         del w
         torch.cuda.empty_cache()
     grad_bytes = cfg.N * (14 if cfg.mode == "3d" else 9) * 4 * (FRAMES_2D if cfg.mode == "2d" else 1)
+    if cfg.mode == "2d" and args.shard == "frames":
+        grad_bytes = 0   # frame owners: every frame's gradient is complete on its rank
     ar = allreduce_ms(grad_bytes, n)
     ar7 = ar / 7.0
     worst = max(s["ms_per_step"] for s in shares)
@@ -836,6 +896,10 @@ def main(argv=None):
         raise SystemExit("--loss: 3D configs on one GPU only")
     w = Workload(cfg, dev, world, rank, args.shard, args.buckets, args.loss, comm=True, view_cost=args.view_cost,
                  exchange=args.exchange)
+    if args.split > 1:
+        if world > 1 or cfg.mode != "3d" or not cfg.backward or args.loss != "none":
+            raise SystemExit("--split: 3D fwd+bwd configs on one GPU, loss none")
+        w.split = args.split
     elapsed, breakdown, dom_name, dom = time_steps(w, args.steps, args.warmup, dist, graph=bool(args.graph))
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -843,7 +907,7 @@ def main(argv=None):
         elapsed = float(t)
 
     ar_ms = None
-    if world > 1:
+    if world > 1 and not getattr(w, "owned", False):   # the frame-owner layout has no collective
         # the step's collective volume timed on its own (10 x all_reduce of the gradient buffer)
         buf = torch.zeros_like(w.params)
         for _ in range(3):
@@ -885,6 +949,7 @@ def main(argv=None):
                    "capacity": args.capacity, "chunk_entries": dict(R._chunk_entries),
                    "launch": (f"one HIP graph of the {args.steps} timed steps, replayed once" if args.graph
                               else "eager launches"),
+                   "split": w.split,
                    "parallelism": w.layout + (f"; backend {backend}" + (" (RCCL)" if backend == "nccl" else "")
                                               if backend else "")},
         "roofline": roof,

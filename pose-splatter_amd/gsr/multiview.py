@@ -21,6 +21,10 @@ code at all; this is the MI355X design, not a translation.
   rank renders all its units in ONE batched launch sequence per frame bucket
   (``gsr.render.render2d_units``) and the [F,N,9] gradient is all-reduced per frame bucket
   (async, overlapping the next bucket's render).
+* ``frame_owner_units`` / ``owned_backward_frames`` — config 4 in the frame-owner layout: frame
+  f with all its views goes to rank f % world.  Frames have disjoint Gaussian sets, so every
+  frame's gradient is complete on its owner: no Gaussian-gradient exchange at all (optionally an
+  all-gather of the frames, for callers that want the whole [F,N,9] on every rank).
 """
 from __future__ import annotations
 
@@ -31,7 +35,8 @@ import torch.distributed as dist
 
 __all__ = ["view_shard", "sharded_backward", "band_shard", "row_work", "unit_bounds", "unit_shard",
            "sharded_backward_units",
-           "frame_view_units", "frame_buckets", "sharded_backward_frames", "bucket_bounds"]
+           "frame_view_units", "frame_buckets", "sharded_backward_frames", "bucket_bounds",
+           "frame_owner_units", "owned_backward_frames", "sparse_sum"]
 
 
 def view_shard(C: int, world: int, rank: int) -> slice:
@@ -263,6 +268,49 @@ def frame_view_units(F: int, V: int, world: int, rank: int) -> list:
     if world < 1 or not 0 <= rank < world:
         raise ValueError(f"bad rank {rank} of world {world}")
     return [(u // V, u % V) for u in range(F * V) if u % world == rank]
+
+
+def frame_owner_units(F: int, V: int, world: int, rank: int) -> list:
+    """(frame, view) units of ``rank`` in the frame-owner layout: frame f and ALL its views go
+    to rank f % world (config 4 at 8 ranks: one frame, 6 units per rank).  The frames' Gaussian
+    sets are disjoint, so each frame's gradient is complete on its owner and no Gaussian-gradient
+    exchange is needed (data-parallel training over frames: the owner back-propagates its
+    frames into the network, whose weight gradients DP all-reduces anyway).  Grouped by frame."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} of world {world}")
+    return [(f, v) for f in range(F) if f % world == rank for v in range(V)]
+
+
+def owned_backward_frames(render_units: Callable, params: torch.Tensor, units: list, v_rgb: torch.Tensor,
+                          v_alpha: torch.Tensor, gather: bool = False, group=None) -> torch.Tensor:
+    """Multi-frame 2D step in the frame-owner layout (``frame_owner_units``).  params [F,N,9];
+    this rank renders all its units in ONE batched launch sequence and backprops them.  Returns
+    the [F,N,9] gradient with this rank's frames filled (other frames zero) -- complete for every
+    owned frame, with no collective.  ``gather=True`` also all-gathers every frame's gradient
+    from its owner (an all-gather, half an all-reduce's traffic), so every rank ends with the
+    full [F,N,9] gradient, identical to the single-process one."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    F = params.shape[0]
+    grad = torch.zeros_like(params)
+    owned = sorted({f for f, _ in units})
+    if units:
+        f0, f1 = owned[0], owned[-1] + 1
+        p = params[f0:f1].detach().requires_grad_(True)
+        rgb, alpha = render_units(p, [f - f0 for f, _ in units])
+        torch.autograd.backward([rgb, alpha], [v_rgb, v_alpha])
+        for f in owned:   # frames between owned ones (world 1 excepted) are not this rank's
+            grad[f].copy_(p.grad[f - f0])
+    if gather and world > 1:
+        # frames f, f + world, ... belong to rank f % world: gather one frame slot per round
+        for f0 in range(0, F, world):
+            n = min(world, F - f0)
+            mine = grad[f0 + rank] if rank < n else torch.zeros_like(grad[0])
+            slots = [torch.empty_like(grad[0]) for _ in range(world)]
+            dist.all_gather(slots, mine.contiguous(), group=group)
+            for r in range(n):
+                grad[f0 + r].copy_(slots[r])
+    return grad
 
 
 def frame_buckets(F: int, buckets: int) -> list:

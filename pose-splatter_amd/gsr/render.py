@@ -82,6 +82,9 @@ class RenderOptions3D:
     grad_hook: object = field(default=None, compare=False)
     # "exact" | "bounded" | None (the module default, set_capacity_mode)
     capacity: str | None = None
+    # distinguishes calls of one shape whose lists differ (e.g. different view groups rendered
+    # concurrently): a bounded call takes its bounds from the previous call with the same tag
+    tag: int = 0
 
 
 class CapacityOverflowError(RuntimeError):
@@ -588,7 +591,7 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts, need_bwd=True):
     V = viewmats.detach().to(device=dev, dtype=torch.float32).contiguous()
     Kc = Ks.detach().to(device=dev, dtype=torch.float32).contiguous()
     bgc = _background(bg, C, dev)
-    b = _Bins(dev, C, N, width, height, opts.capacity, ("3d", opts.band, opts.input_mode, opts.radius_mode),
+    b = _Bins(dev, C, N, width, height, opts.capacity, ("3d", opts.band, opts.input_mode, opts.radius_mode, opts.tag),
               _chunk_entries["3d"], need_bwd)
     q = b.p
     with _timed("project3d_fwd"):

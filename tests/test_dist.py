@@ -113,6 +113,15 @@ def _worker(rank, world, port, out, mode="views"):
     elif mode == "units_buckets":
         grad = sharded_backward_units(lambda q, v, k, band, hook: _HookRender.apply(q, v, k, band, hook, 3),
                                       p, V, K, vr, va, rows=2, buckets=3)
+    elif mode in ("owned", "owned_gather"):
+        from gsr.multiview import frame_owner_units, owned_backward_frames
+        P, vr2, va2 = _frames2d()
+        units = frame_owner_units(4, 3, world, rank)
+        idx = [f * 3 + v for f, v in units]
+        grad = owned_backward_frames(_render_units2d, P, units, vr2[idx], va2[idx], gather=mode == "owned_gather")
+        out[rank] = (grad, sorted({f for f, _ in units}))
+        dist.destroy_process_group()
+        return
     else:
         P, vr2, va2 = _frames2d()
         units = frame_view_units(4, 3, world, rank)
@@ -236,6 +245,31 @@ def test_frame_sharded_allreduce_matches_single_process(world):
     assert torch.equal(out[0], out[1])
 
 
+@pytest.mark.parametrize("world,mode", [(2, "owned"), (3, "owned"), (2, "owned_gather"), (3, "owned_gather")])
+def test_frame_owner_layout_matches_single_process(world, mode):
+    """Config 4's frame-owner layout: each rank renders all views of its frames (f % world) and
+    holds those frames' complete gradient with no collective; with gather=True every rank ends
+    with the full [F,N,9] gradient (an all-gather of the owners' frames)."""
+    ref = _frames_single()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out, mode), nprocs=world, join=True)
+    owners = {}
+    for r in range(world):
+        grad, frames = out[r]
+        assert frames == [f for f in range(4) if f % world == r]
+        for f in range(4):
+            if f in frames or mode == "owned_gather":
+                assert torch.allclose(grad[f], ref[f], rtol=1e-5, atol=1e-6 * float(ref.abs().max())), (r, f)
+            else:
+                assert float(grad[f].abs().max()) == 0.0
+        for f in frames:
+            owners[f] = r
+    assert sorted(owners) == [0, 1, 2, 3]
+    if mode == "owned_gather":
+        assert all(torch.equal(out[0][0], out[r][0]) for r in range(world))
+
+
 def test_unit_and_frame_partitions():
     from gsr.multiview import frame_buckets, frame_view_units, unit_shard
     for C, rows, world in [(6, 32, 8), (6, 64, 8), (1, 5, 8), (3, 2, 2), (6, 32, 1)]:
@@ -253,6 +287,13 @@ def test_unit_and_frame_partitions():
             fs = [f for f, _ in frame_view_units(F, V, world, r)]
             assert fs == sorted(fs)
     assert frame_buckets(8, 2) == [(0, 4), (4, 8)] and frame_buckets(3, 8) == [(0, 1), (1, 2), (2, 3)]
+    from gsr.multiview import frame_owner_units
+    for F, V, world in [(8, 6, 8), (8, 6, 4), (8, 6, 3), (8, 6, 1), (3, 6, 8)]:
+        units = [u for r in range(world) for u in frame_owner_units(F, V, world, r)]
+        assert sorted(units) == [(f, v) for f in range(F) for v in range(V)]
+        for r in range(world):
+            own = frame_owner_units(F, V, world, r)
+            assert own == sorted(own) and all(f % world == r for f, _ in own)
 
 
 def test_unit_bounds_charge_touched_views():
