@@ -619,8 +619,9 @@ class Workload:
                 grads.append(p.grad)
         for st in self._streams[:G]:
             cur.wait_stream(st)
-        for g in grads:
-            g.record_stream(cur)
+        if not torch.cuda.is_current_stream_capturing():   # (a capture's pool is private to the graph)
+            for g in grads:
+                g.record_stream(cur)
         tot = grads[0]
         for g in grads[1:]:
             tot = tot + g

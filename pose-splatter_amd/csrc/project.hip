@@ -106,11 +106,19 @@ __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
     const float* __restrict__ Ks, int W, int H, float near_plane, float far_plane,
     float radius_clip, float eps2d, int input_mode, int tw, int th, int band_y0, int band_y1, int use_lds,
     Splat* __restrict__ rec, float* __restrict__ depth, uint2* __restrict__ rect, int32_t* __restrict__ cnt,
-    int32_t* __restrict__ tile_count, int32_t* __restrict__ counter, int32_t* __restrict__ isect_offset) {
+    int32_t* __restrict__ tile_count, int32_t* __restrict__ counter, int32_t* __restrict__ isect_offset,
+    int C, int n_blocks) {
   extern __shared__ int hist[];
   constexpr int kPer = ITEMS * kProjThreads;
   __shared__ int s_cnt[kPer];
-  const int c = blockIdx.y;
+  // XCD-grouped mapping: workgroups are dealt to the 8 XCDs round-robin by id, so ids 8k + x
+  // (k = 0, 1, ...) run on XCD x.  The C cameras of one Gaussian block get consecutive k on the
+  // same x: they read the block's parameter rows from that XCD's L2 instead of C times from HBM
+  // (config 5: 6 x 112 MB of rows fetched per launch with camera-major ids).
+  const int x = (int)blockIdx.x & 7, k = (int)blockIdx.x >> 3;
+  const int c = k % C;
+  const int blk = (k / C) * 8 + x;
+  if (blk >= n_blocks) return;
   const int T = tw * th;
   int32_t* gcount = tile_count + (int64_t)c * T;
   if (use_lds) {
@@ -121,7 +129,7 @@ __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
   // this camera's share of the band [band_y0, band_y1) of camera-major global tile rows
   // (row r of camera c is global row c*th + r)
   const int by0 = min(max(band_y0 - c * th, 0), th), by1 = min(max(band_y1 - c * th, 0), th);
-  const int64_t n0 = (int64_t)blockIdx.x * kPer;
+  const int64_t n0 = (int64_t)blk * kPer;
   const int64_t n1 = min(N, n0 + kPer);
   for (int64_t n = n0 + threadIdx.x; n < n1; n += blockDim.x) {
     const int64_t cn = (int64_t)c * N + n;
@@ -305,12 +313,15 @@ int gsr3d_project_fwd(const float* params, int64_t N, int64_t row_stride, const 
   hipStream_t s = (hipStream_t)stream;
   // one item per thread unless 4 per thread still gives >= 2 workgroups per CU
   const bool wide = (int64_t)ceil_div(N, kProjPerBlock) * C >= 512;
-  const dim3 grid(ceil_div(N, wide ? kProjPerBlock : kProjThreads), C);
+  const int n_blocks = (int)ceil_div(N, wide ? kProjPerBlock : kProjThreads);
+  const int64_t n_ids = (int64_t)ceil_div(n_blocks, 8) * 8 * C;   // XCD-grouped ids (see the kernel)
+  GSR_REQUIRE(n_ids < (1ll << 31), "gsr3d_project_fwd: too many workgroups (%lld)", (long long)n_ids);
+  const dim3 grid((unsigned)n_ids);
 #define GSR_PROJ3D_LAUNCH(RM, IT)                                                                              \
   hipLaunchKernelGGL((k_project3d_fwd<RM, IT>), grid, dim3(kProjThreads), lds, s, params, N, row_stride, viewmats, \
                      Ks, width, height, near_plane, far_plane, radius_clip, eps2d, input_mode, tw, th, band_y0,      \
                      band_y1, use_lds, (Splat*)rec, depth, (uint2*)rect, isect_count, tile_count,                   \
-                     tile_count + (int64_t)C * T, isect_offset)
+                     tile_count + (int64_t)C * T, isect_offset, C, n_blocks)
   if (radius_mode == GSR_RADIUS_OPACITY_AABB) {
     if (wide) GSR_PROJ3D_LAUNCH(GSR_RADIUS_OPACITY_AABB, kProjItems);
     else GSR_PROJ3D_LAUNCH(GSR_RADIUS_OPACITY_AABB, 1);
