@@ -327,8 +327,15 @@ extern "C" int gsr_debug_fwd_trace(void* buf) {
 #else
 #define FWD_T(i)
 #endif
+// minimum workgroups per CU of the 3D quad-layout raster forward (build knob for measurements):
+// 6 fit 25.9 KB of LDS (queue entry offsets as bytes) and 79 VGPRs without spills -- config 3
+// raster fwd 116.2 -> 111.0 us, config 5 416 -> 408 us (r03s2 A/B on one box); the 16-lane
+// layout (few busy tiles: latency, not occupancy) keeps the compiler's choice
+#ifndef GSR_FWD_MINB
+#define GSR_FWD_MINB 6
+#endif
 template <bool IS2D, int LPP>
-__global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
+__global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MINB) void k_raster_fwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ order, int W, int H, int tw, int th, const float* __restrict__ bg,
     float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
@@ -406,7 +413,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
   if constexpr (!IS2D) {
   // one array (records of slot i at s_q[buf][0..2][i]): one address, immediate offsets
   __shared__ float4 s_q[2][3][256];
-  __shared__ int s_qe[2][256];
+  __shared__ unsigned char s_qe[2][256];   // entry - round base (LDS: 6 workgroups per CU)
   __shared__ int s_qn[2][4];
   __shared__ unsigned char s_l[4][128];
   // 3D -- shared rounds: the quadrant workgroup walks the list in 256-entry rounds; wave w gathers
@@ -439,7 +446,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
         s_q[buf][0][slot] = c0;
         s_q[buf][1][slot] = c1;
         s_q[buf][2][slot] = c2;
-        s_qe[buf][slot] = e;
+        s_qe[buf][slot] = (unsigned char)(64 * wv + lane);   // e - rb
       }
       if (lane == 0) s_qn[buf][wv] = __popcll(m);
       const int id_use = idn;
@@ -511,7 +518,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd(
         done = done || fs < LPP;
       }
       if (lastq >= 0) {   // the entry index of this lane's latest composite, once per half
-        last = s_qe[buf][lastq];
+        last = rb + s_qe[buf][lastq];
         lastq = -1;
       }
       __builtin_amdgcn_wave_barrier();
