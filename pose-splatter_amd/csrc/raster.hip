@@ -277,14 +277,17 @@ struct FwdShape {
 template <int LPP>
 __host__ __device__ __forceinline__ int busy_grid(int n_busy) { return 8 * FwdShape<LPP>::G * ((n_busy + 7) / 8); }
 
-// thread index of tile pixel (il, jl) in the backward's layout: wave = the 8x8 quadrant
-// (il>>3, jl>>3); inside it lane = 4 * (pixel within its 4x4 box) + box, so the lanes of one
-// box are the lanes with equal bits 0-1 (see k_raster_bwd)
+// slot of tile pixel (il, jl) in a chunk record: box-major inside the 8x8 quadrant wv,
+// 64 * wv + 16 * box + pos (pos = pixel within its 4x4 box).  The quad forward writes one 4x4
+// box per wave, so its 16 records are 256 contiguous bytes (full lines; the backward's
+// lane-interleaved order, 64 * wv + 4 * pos + box, put them 64 B apart); a backward or box-
+// forward wave (lane = 4 * pos + box) covers its quadrant's 1 KB, permuted, in one access.
+__device__ __forceinline__ int ckpt_slot_of(int wv, int box, int pos) { return (wv << 6) | (box << 4) | pos; }
 __device__ __forceinline__ int bwd_pixel_slot(int il, int jl) {
   const int wv = ((il >> 3) << 1) | (jl >> 3);
   const int box = (((il >> 2) & 1) << 1) | ((jl >> 2) & 1);
   const int pos = ((il & 3) << 2) | (jl & 3);
-  return (wv << 6) | (pos << 2) | box;
+  return ckpt_slot_of(wv, box, pos);
 }
 
 //
@@ -736,7 +739,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
     const int32_t* __restrict__ chunk_base, int n_busy, int64_t CT,
     uint64_t* __restrict__ tile_cut, float cut2d, const FwdLazy lz, const gsr_bin_stats* __restrict__ stats) {
   __shared__ float4 s_r[2][3][256];              // round records, part j of slot i at s_r[buf][j][i]
-  __shared__ unsigned char s_list[4][128];       // a half's quadrant survivors (slot in the half)
   __shared__ unsigned char s_box[4][4][129];     // ... and each box's, in list order (+1: read-ahead)
   __shared__ int s_max;
   static_assert(kChunk3 == 128, "a round half is one chunk");
@@ -809,11 +811,15 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
       c2 = rec[id_use].p2;
     }
     if (__syncthreads_count(!done) == 0) break;
+    // a half's quadrant survivors (slot in the half), kept in this wave's own slots of the other
+    // round buffer: dead since the round barrier, and rewritten only by this wave at the next
+    // round's start (LDS 27.2 -> 26.6 KB: 6 workgroups per CU)
+    unsigned char* const s_list_w = reinterpret_cast<unsigned char*>(&s_r[buf ^ 1][0][64 * wv]);
     for (int h = 0; h < 2; ++h) {
       const int hb = rb + 128 * h;
       if (hb >= end || __ballot(!done) == 0ull) break;
       if (hb > start && ((hb - start) & umask) == 0) {   // entering chunk kcur+1 (every few halves)
-        if (ckpt) ckpt[(int64_t)(cbase + kcur) * kRasterThreads + threadIdx.x] = make_float4(Ts, dr, dg, db);
+        if (ckpt) ckpt[(int64_t)(cbase + kcur) * kRasterThreads + ckpt_slot_of(wv, box, pos)] = make_float4(Ts, dr, dg, db);
         cr += dr;
         cg += dg;
         cb += db;
@@ -834,7 +840,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
                                                      x0 + 7.f, y0, y0 + 7.f);
           const unsigned long long m = __ballot(keep);
           if (keep)
-            s_list[wv][nsurv + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+            s_list_w[nsurv + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] =
                 (unsigned char)k;
           nsurv += __popcll(m);
@@ -848,7 +854,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
         const unsigned long long boxbits = 0x1111111111111111ull << box;
         for (int s0 = 0; s0 < nsurv; s0 += 16) {
           const int s = s0 + pos;
-          const int k = s_list[wv][s < nsurv ? s : 0];
+          const int k = s_list_w[s < nsurv ? s : 0];
           const int sl = 128 * h + k;
           const bool keep = s < nsurv && cull_keep<IS2D>(s_r[buf][0][sl], s_r[buf][1][sl], s_r[buf][2][sl], x0,
                                                          x0 + 3.f, y0, y0 + 3.f);
@@ -867,7 +873,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
         // many scalar as vector instructions on exec masks): a box's list is padded to the
         // wave's step count with a real quadrant survivor (finite record), which a step past
         // nb reads and leaves out by select -- the same sums, bit for bit.
-        for (int s = nb + pos; s < nmax; s += 16) s_box[wv][box][s] = s_list[wv][0];
+        for (int s = nb + pos; s < nmax; s += 16) s_box[wv][box][s] = s_list_w[0];
         __builtin_amdgcn_wave_barrier();
         int k_next = s_box[wv][box][0];
         for (int t = 0; t < nmax; ++t) {
@@ -946,7 +952,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
   if (end > start && ckpt) {
     // chunk records {T at chunk start, chunk colour} -> what the backward needs at each chunk's
     // END: {T_end, suffix colour sum of the later chunks}, back to front (records re-read 8 at a time)
-    float4* ck = ckpt + (int64_t)cbase * kRasterThreads + threadIdx.x;
+    float4* ck = ckpt + (int64_t)cbase * kRasterThreads + ckpt_slot_of(wv, box, pos);
     ck[(int64_t)kcur * kRasterThreads] = make_float4(T, 0.f, 0.f, 0.f);
     float sr = dr, sg = dg, sb = db;
     float Tn = Ts;
@@ -1188,7 +1194,7 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : 1) voi
   // Every load is issued up front, none waiting for `last` (the per-WG latency chain is what
   // bounds this kernel's fixed part): the pixel's state, its chunk record, the last sub-chunk's
   // ids and sort positions; pixels that stopped before this unit then drop them by select.
-  const float4 rck = ckpt[(int64_t)chunk * kRasterThreads + threadIdx.x];
+  const float4 rck = ckpt[(int64_t)chunk * kRasterThreads + ckpt_slot_of(wv, box, pos)];
   int id_mine = threadIdx.x < sn ? ids[sb0 + threadIdx.x] : 0;
   int kos_mine = threadIdx.x < sn ? k_of_s[sb0 + threadIdx.x] : 0;
   float Tf = 1.f, Tl = 1.f, vr = 0.f, vg = 0.f, vb = 0.f, va = 0.f;
