@@ -72,15 +72,7 @@ static int g_split_sort = 1;    // gsr_set_split_sort
 // target) and zeroes tile_cut.  Each wave owns a contiguous range of tiles and walks it in
 // 64-tile rounds (coalesced loads and stores, in-wave scans); the counts are staged in LDS
 // when they fit.
-__device__ __forceinline__ int wave_incl_scan(int v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(v, o, 64);
-    if (lane >= o) v += y;
-  }
-  return v;
-}
+__device__ __forceinline__ int wave_incl_scan(int v) { return wave_incl_scan_dpp(v); }
 
 __global__ __launch_bounds__(kTopThreads) void k_tile_scan(int32_t* __restrict__ tile_count, int64_t CT,
                                                           int32_t* __restrict__ tile_offset,
@@ -150,46 +142,48 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(int32_t* __restrict__
     atomicMax(&s_max, mx);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int tc = 0, tk = 0, te = 0;
-    for (int w = 0; w < NW; ++w) {
-      const int a = s_w[0][w], b = s_w[1][w], c = s_w[2][w];
-      s_w[0][w] = tc;
-      s_w[1][w] = tk;
-      s_w[2][w] = te;
-      tc += a;
-      tk += b;
-      te += c;
+  if (threadIdx.x < 64) {
+    // wave 0: the per-wave totals and the log2 buckets scanned across lanes (one thread walking
+    // them serially was ~100 dependent LDS round trips -- the scan's latency at few tiles)
+    const int l = threadIdx.x;
+    const int a = l < NW ? s_w[0][l] : 0, b = l < NW ? s_w[1][l] : 0, c = l < NW ? s_w[2][l] : 0;
+    const int ia = wave_incl_scan(a), ib = wave_incl_scan(b), ic = wave_incl_scan(c);
+    if (l < NW) {
+      s_w[0][l] = ia - a;
+      s_w[1][l] = ib - b;
+      s_w[2][l] = ic - c;
     }
-    const int n_busy = (int)CT - te;
-    s_n_busy = n_busy;
-    int acc = 0;
-    for (int b = 31; b >= 0; --b) {
-      const int c = s_bucket[b];
-      if (b == 12) {   // sort classes: lists >= 8192 (buckets >= 13) and 4096..8191 (bucket 12)
-        stats->n_sort_big = acc;
-        stats->n_sort_mid = c;
-      }
-      if (b == 9) stats->n_sort_long = acc;   // lists >= 1024 (kWaveSortKeys): one workgroup each
-      s_bucket[b] = acc;
-      acc += c;
+    const int tc = __shfl(ia, 63, 64), tk = __shfl(ib, 63, 64), te = __shfl(ic, 63, 64);
+    // buckets longest first: lane l holds bucket 31 - l; its start = the lists in longer buckets
+    const int bk = l < 32 ? s_bucket[31 - l] : 0;
+    const int ex = wave_incl_scan(bk) - bk;
+    if (l < 32) s_bucket[31 - l] = ex;
+    // sort classes: lists >= 8192 (buckets >= 13: lanes < 19) and 4096..8191 (bucket 12: lane 19);
+    // lists >= 1024 (kWaveSortKeys, buckets >= 10: lanes < 22) take one workgroup each
+    const int n_big = __shfl(ex, 19, 64), n_mid = __shfl(bk, 19, 64), n_long = __shfl(ex, 22, 64);
+    if (l == 0) {
+      const int n_busy = (int)CT - te;
+      s_n_busy = n_busy;
+      stats->n_sort_big = n_big;
+      stats->n_sort_mid = n_mid;
+      stats->n_sort_long = n_long;
+      tile_offset[CT] = tc;
+      chunk_base[CT] = tk;
+      stats->n_isect = tc;
+      stats->max_seg = s_max;
+      stats->n_busy = n_busy;
+      stats->n_chunks = tk;
+      stats->n_active = 0;
+      // bounded call: the caller sized the intersection / chunk buffers without reading I back
+      int ovf = 0;
+      if (caps.isect > 0 && (int64_t)tc > caps.isect) ovf |= GSR_OVF_ISECT;
+      if (caps.chunks > 0 && (int64_t)tk > caps.chunks) ovf |= GSR_OVF_CHUNKS;
+      stats->isect_cap = caps.isect;
+      stats->chunk_cap = caps.chunks;
+      stats->overflow = ovf;
+      stats->status = caps.status;
+      stats->chunk_entries = 1 << ushift;
     }
-    tile_offset[CT] = tc;
-    chunk_base[CT] = tk;
-    stats->n_isect = tc;
-    stats->max_seg = s_max;
-    stats->n_busy = n_busy;
-    stats->n_chunks = tk;
-    stats->n_active = 0;
-    // bounded call: the caller sized the intersection / chunk buffers without reading I back
-    int ovf = 0;
-    if (caps.isect > 0 && (int64_t)tc > caps.isect) ovf |= GSR_OVF_ISECT;
-    if (caps.chunks > 0 && (int64_t)tk > caps.chunks) ovf |= GSR_OVF_CHUNKS;
-    stats->isect_cap = caps.isect;
-    stats->chunk_cap = caps.chunks;
-    stats->overflow = ovf;
-    stats->status = caps.status;
-    stats->chunk_entries = 1 << ushift;
   }
   __syncthreads();
   // pass 2: 64-tile rounds per wave
@@ -541,22 +535,14 @@ template <int GT>
 __device__ __forceinline__ int group_exclusive_scan(SortGroup<GT>& g, int v, int* s_tmp, int* total) {
   const int lane = threadIdx.x & 63;
   const int w = g.tid >> 6;
-  int x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
+  const int x = wave_incl_scan_dpp(v);
   if (lane == 63) s_tmp[w] = x;
   g.sync();
-  if (g.tid == 0) {
-    int acc = 0;
-    for (int k = 0; k < GT / 64; ++k) {
-      const int t = s_tmp[k];
-      s_tmp[k] = acc;
-      acc += t;
-    }
-    s_tmp[GT / 64] = acc;
+  if (g.tid < 64) {   // the group's first wave scans the wave totals (lane k: wave k)
+    const int t = lane < GT / 64 ? s_tmp[lane] : 0;
+    const int it = wave_incl_scan_dpp(t);
+    if (lane < GT / 64) s_tmp[lane] = it - t;
+    if (lane == GT / 64 - 1) s_tmp[GT / 64] = it;
   }
   g.sync();
   const int res = x - v + s_tmp[w];
@@ -842,16 +828,7 @@ __device__ __forceinline__ void merge_runs(const uint64_t* __restrict__ a, const
 constexpr int kWaveSortKeys = 1024;
 constexpr int kWaveRounds = kWaveSortKeys / 64;
 
-__device__ __forceinline__ int wave_excl_scan(int v) {
-  const int lane = threadIdx.x & 63;
-  int x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  return x - v;
-}
+__device__ __forceinline__ int wave_excl_scan(int v) { return wave_incl_scan_dpp(v) - v; }
 
 // a: this wave's LDS region (>= kWaveSortKeys slots); hist: its 256 counters.  n < kWaveSortKeys.
 __device__ __forceinline__ void wave_sort_list(uint64_t* a, int* hist, int n, const uint64_t* __restrict__ seg,

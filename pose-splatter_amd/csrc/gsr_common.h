@@ -64,6 +64,21 @@ __device__ __forceinline__ float dpp_mov(float v) {
       float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
 }
 
+// Inclusive prefix sum over the 64 lanes of a wave in six DPP adds (Hillis-Steele inside each
+// 16-lane row with row_shr 1/2/4/8 -- lanes shifted in from outside the row read 0 -- then
+// row_bcast:15 adds row r's last lane into row r+1 for rows 1 and 3, and row_bcast:31 adds
+// lane 31 into rows 2 and 3).  Register-to-register: a __shfl_up ladder is six dependent
+// ds_bpermute round trips through the LDS crossbar.  Every lane must be active.
+__device__ __forceinline__ int wave_incl_scan_dpp(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);   // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
 __device__ __forceinline__ float readlane_f(float v, int lane) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
 }
@@ -182,22 +197,14 @@ template <int NT>
 __device__ __forceinline__ int block_exclusive_scan(int v, int* s_tmp, int* total) {
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  int x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
+  const int x = wave_incl_scan_dpp(v);
   if (lane == 63) s_tmp[w] = x;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int k = 0; k < NT / 64; ++k) {
-      int t = s_tmp[k];
-      s_tmp[k] = acc;
-      acc += t;
-    }
-    s_tmp[NT / 64] = acc;
+  if (threadIdx.x < 64) {   // wave 0 scans the wave totals (lane k: wave k)
+    const int t = lane < NT / 64 ? s_tmp[lane] : 0;
+    const int it = wave_incl_scan_dpp(t);
+    if (lane < NT / 64) s_tmp[lane] = it - t;
+    if (lane == NT / 64 - 1) s_tmp[NT / 64] = it;
   }
   __syncthreads();
   int res = x - v + s_tmp[w];

@@ -1027,12 +1027,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_finalize(
   const int nact = (te - start + U - 1) / U;
   // one atomic per wave on the active-chunk counter (one per tile serialised ~700 atomics on
   // one address at config 3)
-  int incl = nact;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += y;
-  }
+  const int incl = wave_incl_scan_dpp(nact);
   int base = 0;
   if (lane == 63 && incl > 0) base = atomicAdd(&stats->n_active, incl);
   base = __shfl(base, 63, 64);
