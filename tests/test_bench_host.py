@@ -73,6 +73,13 @@ def test_bench_args_defaults():
     assert a.config == 3 and a.gpus == 1 and a.shard == "views" and a.cpu_threads == 0
     assert a.capacity == "bounded" and a.graph == -1
     assert bench.cpu_threads(3) == 3 and bench.cpu_threads(0) >= 1
+    assert a.split == 1
+    # config 4 (2D) defaults to the frame-owner layout; frames is a 2D-only layout
+    assert bench.parse(["--config", "4"]).shard == "frames"
+    assert bench.parse(["--config", "4", "--shard", "units"]).shard == "units"
+    import pytest
+    with pytest.raises(SystemExit):
+        bench.parse(["--config", "3", "--shard", "frames"])
 
 
 def test_gpus_without_launcher_spawns_ranks(monkeypatch):
