@@ -128,13 +128,10 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(int32_t* __restrict__
     mx = max(mx, v);
     if (v > 0) atomicAdd(&s_bucket[31 - __clz(v)], 1);
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    sc += __shfl_xor(sc, o, 64);
-    sk += __shfl_xor(sk, o, 64);
-    se += __shfl_xor(se, o, 64);
-    mx = max(mx, __shfl_xor(mx, o, 64));
-  }
+  sc = wave_sum_i(sc);
+  sk = wave_sum_i(sk);
+  se = wave_sum_i(se);
+  mx = wave_max_i(mx);
   if (lane == 0) {
     s_w[0][wv] = sc;
     s_w[1][wv] = sk;
@@ -153,14 +150,16 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(int32_t* __restrict__
       s_w[1][l] = ib - b;
       s_w[2][l] = ic - c;
     }
-    const int tc = __shfl(ia, 63, 64), tk = __shfl(ib, 63, 64), te = __shfl(ic, 63, 64);
+    const int tc = __builtin_amdgcn_readlane(ia, 63), tk = __builtin_amdgcn_readlane(ib, 63),
+              te = __builtin_amdgcn_readlane(ic, 63);
     // buckets longest first: lane l holds bucket 31 - l; its start = the lists in longer buckets
     const int bk = l < 32 ? s_bucket[31 - l] : 0;
     const int ex = wave_incl_scan(bk) - bk;
     if (l < 32) s_bucket[31 - l] = ex;
     // sort classes: lists >= 8192 (buckets >= 13: lanes < 19) and 4096..8191 (bucket 12: lane 19);
     // lists >= 1024 (kWaveSortKeys, buckets >= 10: lanes < 22) take one workgroup each
-    const int n_big = __shfl(ex, 19, 64), n_mid = __shfl(bk, 19, 64), n_long = __shfl(ex, 22, 64);
+    const int n_big = __builtin_amdgcn_readlane(ex, 19), n_mid = __builtin_amdgcn_readlane(bk, 19),
+              n_long = __builtin_amdgcn_readlane(ex, 22);
     if (l == 0) {
       const int n_busy = (int)CT - te;
       s_n_busy = n_busy;
@@ -208,8 +207,8 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(int32_t* __restrict__
         order[n_busy + ce + r] = (int32_t)i;
       }
     }
-    cc += __shfl(iv, 63, 64);
-    ck += __shfl(ik, 63, 64);
+    cc += __builtin_amdgcn_readlane(iv, 63);
+    ck += __builtin_amdgcn_readlane(ik, 63);
     ce += __popcll(empty);
   }
 }
@@ -512,8 +511,7 @@ __device__ __forceinline__ uint32_t stage_keys(const SortGroup<GT>& g, uint64_t*
 // zero on entry; it is left holding the result).  One atomic per wave.
 template <int GT>
 __device__ __forceinline__ uint32_t block_varying(SortGroup<GT>& g, uint32_t orv, int* s_misc) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) orv |= (uint32_t)__shfl_xor((int)orv, o, 64);
+  orv = (uint32_t)wave_or_i((int)orv);
   if ((threadIdx.x & 63) == 0 && orv) atomicOr((unsigned*)&s_misc[0], orv);
   g.sync();
   return (uint32_t)s_misc[0];
@@ -853,8 +851,7 @@ __device__ __forceinline__ void wave_sort_list(uint64_t* a, int* hist, int n, co
       if (r < rounds && i < n) a[i] = ((uint64_t)w[r] << 32) | (uint64_t)(uint32_t)i;
     }
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) orv |= (uint32_t)__shfl_xor((int)orv, o, 64);
+  orv = (uint32_t)wave_or_i((int)orv);
   __builtin_amdgcn_wave_barrier();
   for (int shift = 0; shift < 32; shift += 8) {
     if (((orv >> shift) & 0xFFu) == 0u) continue;

@@ -79,6 +79,30 @@ __device__ __forceinline__ int wave_incl_scan_dpp(int v) {
   return v;
 }
 
+// Wave-wide reductions with a wave-uniform result: xor-1 / xor-2 quad swaps and the two row
+// mirrors reduce each 16-lane row in registers (DPP), then the four row results are combined
+// from v_readlane (scalar).  Every lane must be active.
+template <int CTRL>
+__device__ __forceinline__ int dpp_row_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
+}
+#define GSR_WAVE_REDUCE(NAME, OP)                                                              \
+  __device__ __forceinline__ int NAME(int v) {                                                 \
+    v = OP(v, dpp_row_i<0xB1>(v));  /* quad_perm [1,0,3,2] */                                  \
+    v = OP(v, dpp_row_i<0x4E>(v));  /* quad_perm [2,3,0,1] */                                  \
+    v = OP(v, dpp_row_i<0x141>(v)); /* row_half_mirror */                                      \
+    v = OP(v, dpp_row_i<0x140>(v)); /* row_mirror */                                           \
+    return OP(OP(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),            \
+              OP(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));          \
+  }
+__device__ __forceinline__ int gsr_add_i(int a, int b) { return a + b; }
+__device__ __forceinline__ int gsr_max_i(int a, int b) { return a > b ? a : b; }
+__device__ __forceinline__ int gsr_or_i(int a, int b) { return a | b; }
+GSR_WAVE_REDUCE(wave_sum_i, gsr_add_i)
+GSR_WAVE_REDUCE(wave_max_i, gsr_max_i)
+GSR_WAVE_REDUCE(wave_or_i, gsr_or_i)
+#undef GSR_WAVE_REDUCE
+
 __device__ __forceinline__ float readlane_f(float v, int lane) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
 }

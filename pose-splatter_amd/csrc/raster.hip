@@ -1030,7 +1030,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_finalize(
   const int incl = wave_incl_scan_dpp(nact);
   int base = 0;
   if (lane == 63 && incl > 0) base = atomicAdd(&stats->n_active, incl);
-  base = __shfl(base, 63, 64);
+  base = __builtin_amdgcn_readlane(base, 63);
   if (in && nact > 0) {
     const int pos = base + incl - nact;
     const int cbase = chunk_base[ct];
@@ -1231,10 +1231,7 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : 1) voi
     const float mu_last = bgdot - va;
     mu = last < b0 + n ? mu_last : (Sv + Tf * mu_last) / T;
   }
-  int wlast = last;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) wlast = max(wlast, __shfl_xor(wlast, o, 64));
-  wlast = __builtin_amdgcn_readfirstlane(wlast);   // wave-uniform: an SGPR across the sub-chunk loop
+  const int wlast = wave_max_i(last);   // wave-uniform (an SGPR across the sub-chunk loop)
   // the records as three float4 registers (a Splat variable assigned under a branch and in the
   // sub-chunk loop went through 48 B of scratch per lane: a store + reload on the load chain)
   const float4* const rec4 = reinterpret_cast<const float4*>(rec);
