@@ -1144,7 +1144,8 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : 1) voi
   constexpr int kLen = kChunk3 + kGroup;   // survivor list capacity (padded to whole groups)
   __shared__ float4 s_p[3][kChunk3 + 1];   // the chunk's records, part j of entry k at s_p[j][k]
   // gradient sums per entry, one slot per wave (index kNull absorbs the padding's zeros)
-  __shared__ float L[kPartial][4][kChunk3 + 1];
+  __shared__ __attribute__((aligned(16))) float L[kPartial][4][kChunk3 + 1];
+  static_assert((kPartial * 4 * (kChunk3 + 1)) % 4 == 0, "L is zeroed in float4 stores");
   __shared__ unsigned char s_list[4][kLen];     // quadrant survivors, back to front
   __shared__ unsigned char s_box[4][4][kLen];   // per (wave, box) survivors, back to front
   __shared__ float s_stage[4][64][4];     // per wave: the group's reduced sums, by lane
@@ -1253,7 +1254,8 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : 1) voi
       s_p[1][threadIdx.x] = sp1;
       s_p[2][threadIdx.x] = sp2;
     }
-    for (int i = threadIdx.x; i < kPartial * 4 * (kChunk3 + 1); i += kRasterThreads) (&L[0][0][0])[i] = 0.f;
+    for (int i = threadIdx.x; i < kPartial * (kChunk3 + 1); i += kRasterThreads)   // b128 stores
+      reinterpret_cast<float4*>(&L[0][0][0])[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (threadIdx.x == 0) {
       const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
       s_p[0][kNull] = z;
