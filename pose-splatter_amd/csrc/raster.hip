@@ -73,6 +73,34 @@ __device__ __forceinline__ bool cull_keep(const float4 p0, const float4 p1, cons
   return fminf(s1, s2) <= L * 1.001f + 1e-3f;
 }
 
+// The survivors list[0, nsurv) of an 8x8 quadrant (origin (qx, qy), pixel centres) against its
+// four 4x4 boxes, ONE survivor per lane: its record is read from LDS once and tested against all
+// four boxes (box b at (qx + 4 (b & 1), qy + 4 (b >> 1))); box b's survivors are appended in
+// list order to boxl[b * stride + ..].  n[b]: the four counts (wave-uniform).  (A lane per
+// (survivor, box) pair read every record four times and walked 16 survivors per round trip.)
+template <bool IS2D>
+__device__ __forceinline__ void box4_cull(const unsigned char* __restrict__ list, int nsurv, const float4* r0,
+                                          const float4* r1, const float4* r2, float qx, float qy,
+                                          unsigned char* boxl, int stride, int (&n)[4]) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  n[0] = n[1] = n[2] = n[3] = 0;
+  for (int s0 = 0; s0 < nsurv; s0 += 64) {
+    const int s = s0 + lane;
+    const bool in = s < nsurv;
+    const int k = list[in ? s : 0];
+    const float4 a = r0[k], b = r1[k], c = r2[k];
+#pragma unroll
+    for (int bx = 0; bx < 4; ++bx) {
+      const float x0 = qx + (float)((bx & 1) * 4), y0 = qy + (float)((bx >> 1) * 4);
+      const bool keep = in && cull_keep<IS2D>(a, b, c, x0, x0 + 3.f, y0, y0 + 3.f);
+      const unsigned long long m = __ballot(keep);
+      if (keep) boxl[bx * stride + n[bx] + __popcll(m & below)] = (unsigned char)k;
+      n[bx] += __popcll(m);
+    }
+  }
+}
+
 struct SubTile {
   int c, ty, tx, wv, lane, i, j;
   float px, py, bx0, bx1, by0, by1;
@@ -731,7 +759,7 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
 // leaves as soon as all its pixels are done, the workgroup as soon as all four waves are.
 // Chunk records are written per pixel at thread index = the backward's slot, coalesced.
 template <bool IS2D>
-__global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
+__global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ order, int W, int H, int tw, int th, const float* __restrict__ bg,
     float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
@@ -848,24 +876,13 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_fwd_box(
       }
       __builtin_amdgcn_wave_barrier();
       // ... and the quadrant's survivors against each 4x4 box
-      int nb = 0;
-      {
-        const float x0 = (float)bx0i + off, y0 = (float)by0i + off;
-        const unsigned long long boxbits = 0x1111111111111111ull << box;
-        for (int s0 = 0; s0 < nsurv; s0 += 16) {
-          const int s = s0 + pos;
-          const int k = s_list_w[s < nsurv ? s : 0];
-          const int sl = 128 * h + k;
-          const bool keep = s < nsurv && cull_keep<IS2D>(s_r[buf][0][sl], s_r[buf][1][sl], s_r[buf][2][sl], x0,
-                                                         x0 + 3.f, y0, y0 + 3.f);
-          const unsigned long long m = __ballot(keep) & boxbits;
-          if (keep) s_box[wv][box][nb + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned char)k;
-          nb += __popcll(m);
-        }
-      }
+      int nbx[4];
+      box4_cull<IS2D>(s_list_w, nsurv, &s_r[buf][0][128 * h], &s_r[buf][1][128 * h], &s_r[buf][2][128 * h],
+                      (float)qx0 + off, (float)qy0 + off, &s_box[wv][0][0], 129, nbx);
+      const int nb = box == 0 ? nbx[0] : box == 1 ? nbx[1] : box == 2 ? nbx[2] : nbx[3];
       __builtin_amdgcn_wave_barrier();
-      // steps walked by the wave: max over its boxes (lanes 4k..4k+3 hold the four counts)
-      const int nmax = __builtin_amdgcn_readfirstlane(quad_max_i(nb));
+      // steps walked by the wave: max over its boxes
+      const int nmax = max(max(nbx[0], nbx[1]), max(nbx[2], nbx[3]));
       // the sequential walk of the box's survivors (entry index read one step ahead)
       const float4* const rh = &s_r[buf][0][128 * h];
       if constexpr (IS2D) {
@@ -1287,23 +1304,14 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : 1) voi
       }
     }
     __builtin_amdgcn_wave_barrier();
-    // ... and the quadrant's survivors against each 4x4 box: lane l tests survivor s0 + (l>>2)
-    // against box l&3; a box's bits of the ballot keep the list order
-    int nb = 0;   // survivors of this lane's box
-    {
-      const float x0 = (float)bx0i + off, y0 = (float)by0i + off;
-      const unsigned long long boxbits = 0x1111111111111111ull << box;
-      for (int s0 = 0; s0 < nsurv; s0 += 16) {
-        const int s = s0 + pos;
-        const int k = s_list[wv][s < nsurv ? s : 0];
-        const bool keep = s < nsurv && cull_keep<IS2D>(s_p[0][k], s_p[1][k], s_p[2][k], x0, x0 + 3.f, y0, y0 + 3.f);
-        const unsigned long long m = __ballot(keep) & boxbits;
-        if (keep) s_box[wv][box][nb + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned char)k;
-        nb += __popcll(m);
-      }
-    }
-    // groups walked by the wave: max over its boxes (lanes 4k..4k+3 hold the four counts)
-    const int ngrp = __builtin_amdgcn_readfirstlane(quad_max_i(nb));
+    // ... and the quadrant's survivors against each 4x4 box (one survivor per lane, all four
+    // boxes; box4_cull keeps the list order)
+    int nbx[4];
+    box4_cull<IS2D>(s_list[wv], nsurv, s_p[0], s_p[1], s_p[2], (float)qx0 + off, (float)qy0 + off,
+                    &s_box[wv][0][0], kLen, nbx);
+    const int nb = box == 0 ? nbx[0] : box == 1 ? nbx[1] : box == 2 ? nbx[2] : nbx[3];   // this lane's box
+    // groups walked by the wave: max over its boxes
+    const int ngrp = max(max(nbx[0], nbx[1]), max(nbx[2], nbx[3]));
     const int npad = (ngrp + kGroup - 1) / kGroup * kGroup;
     for (int s = nb + pos; s < npad; s += 16) s_box[wv][box][s] = (unsigned char)kNull;
     __builtin_amdgcn_wave_barrier();
