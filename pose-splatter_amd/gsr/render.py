@@ -14,15 +14,25 @@ Two capacity modes ("Threading / streams"):
   derived from an earlier call of the same shape (+25 % intersections / chunks, +12.5 %
   busy tiles); the device checks every bound and, if one fails, the call writes NaN to
   rgb / alpha / v_params and ORs ``GSR_OVF_*`` bits into a sticky per-device status word.
-  The previous bounded call's stats are read back asynchronously and checked at the next
-  call (raising ``CapacityOverflowError`` if it overflowed); ``check_overflow()`` checks the
-  sticky word explicitly (e.g. after a captured HIP graph replays).  A bounded step has no
-  host wait, so it can be captured in a HIP graph (``torch.cuda.CUDAGraph``).
+  Every bounded eager call's stats are copied to pinned memory behind its kernels and queued
+  (per shape, oldest first); completed copies are checked at the next call of the shape
+  (raising ``CapacityOverflowError`` for the first one that overflowed, refreshing the
+  shape's bounds from the others), and the autograd backward of a bounded call waits for its
+  own forward's copy -- after enqueuing its kernels -- and raises before returning, so a NaN
+  gradient never reaches ``.grad`` / the optimizer.  ``check_overflow()`` checks the sticky
+  word explicitly (e.g. after a captured HIP graph replays).  A bounded step has no host
+  wait, so it can be captured in a HIP graph (``torch.cuda.CUDAGraph``).
+* ``"auto"`` (the drop-in renderers' default, src/gaussian_renderer.py): bounded when a
+  backward will follow (it checks the forward as above) and an earlier call of the shape
+  left bounds; exact otherwise (the first call of a shape, forward-only calls).  An eager
+  ``model``-style training step then has no mid-forward host wait; the backward's check
+  waits only for a forward that finished long before (the loss kernels run meanwhile).
 
 Intermediates live in two arenas per forward (see ``_Arena``).
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 from dataclasses import dataclass, field
 
@@ -80,7 +90,7 @@ class RenderOptions3D:
     # (multi-GPU: an async all-reduce of finished rows overlaps the later ranges)
     grad_buckets: int = 1
     grad_hook: object = field(default=None, compare=False)
-    # "exact" | "bounded" | None (the module default, set_capacity_mode)
+    # "exact" | "bounded" | "auto" | None (the module default, set_capacity_mode)
     capacity: str | None = None
     # distinguishes calls of one shape whose lists differ (e.g. different view groups rendered
     # concurrently): a bounded call takes its bounds from the previous call with the same tag
@@ -108,12 +118,16 @@ def set_chunk_entries(mode: str, entries: int) -> None:
     _chunk_entries[mode] = int(entries)
 
 
+_MODES = ("exact", "bounded", "auto")
+
+
 def set_capacity_mode(mode: str) -> None:
-    """Module default for calls that do not choose: "exact" (one stats read-back per forward)
-    or "bounded" (no host synchronisation; bounds from the previous call of the same shape)."""
+    """Module default for calls that do not choose: "exact" (one stats read-back per forward),
+    "bounded" (no host synchronisation; bounds from the previous call of the same shape) or
+    "auto" (bounded when a backward will follow and bounds exist, else exact)."""
     global _capacity_default
-    if mode not in ("exact", "bounded"):
-        raise ValueError(f"capacity mode must be 'exact' or 'bounded', got {mode!r}")
+    if mode not in _MODES:
+        raise ValueError(f"capacity mode must be one of {_MODES}, got {mode!r}")
     _capacity_default = mode
 
 
@@ -189,15 +203,17 @@ class _timed:
         self.s = None
 
     def __enter__(self):
-        if _timers is not None and (_timed_only is None or self.name in _timed_only):
-            # inside a HIP graph capture the events become record nodes of the graph (external)
-            self.s = torch.cuda.Event(enable_timing=True, external=_capturing())
+        # (nothing while a HIP graph is being captured: ROCm rejects timing events inside a
+        # captured graph, "External events are disallowed in rocm" -- ADVICE r3)
+        if (_timers is not None and (_timed_only is None or self.name in _timed_only)
+                and not _capturing()):
+            self.s = torch.cuda.Event(enable_timing=True)
             self.s.record()
         return self
 
     def __exit__(self, *exc):
         if self.s is not None:
-            e = torch.cuda.Event(enable_timing=True, external=_capturing())
+            e = torch.cuda.Event(enable_timing=True)
             e.record()
             _timers.setdefault(self.name, []).append((self.s, e))
         return False
@@ -239,7 +255,9 @@ _pinned = {}
 # shape: I, chunks, max_seg, busy, big, mid -- the bounds of bounded calls and the speculative
 # arena sizes of exact ones
 _size_hint = {}
-_monitors = {}    # shape key -> [pinned stats copy, event] of the last bounded eager forward
+_monitors = {}    # shape key -> deque of _Monitor: bounded eager forwards, oldest first
+_monitor_pool = []   # free pinned stats buffers
+_MAX_PENDING = 16    # per shape: past this many unchecked forwards the oldest is waited for
 _bg_cache = {}
 _STATS_BYTES = 128   # >= sizeof(gsr_bin_stats) (80)
 _STATS_I32 = _STATS_BYTES // 4
@@ -262,38 +280,77 @@ def _capturing() -> bool:
     return torch.cuda.is_current_stream_capturing()
 
 
-def _monitor_check(key) -> None:
-    """The previous bounded forward of this shape: if its stats have arrived (non-blocking),
-    raise on overflow, else refresh the shape's bounds from what it observed."""
-    m = _monitors.get(key)
-    if m is None or m[1] is None or not m[1].query():
+class _Monitor:
+    """One bounded eager forward's stats, copied to pinned memory behind its kernels."""
+    __slots__ = ("key", "host", "event", "done")
+
+    def __init__(self, key, host, event):
+        self.key, self.host, self.event, self.done = key, host, event, False
+
+
+def _monitor_process(m: _Monitor) -> None:
+    """A monitor whose copy has arrived: raise if its forward overflowed, else refresh the
+    shape's bounds from what it observed.  Runs once per monitor."""
+    if m.done:
         return
-    st = m[0].tolist()
-    m[1] = None
+    m.done = True
+    st = m.host.tolist()
+    _monitor_pool.append(m.host)
     ovf = st[12]   # gsr_bin_stats.overflow (byte 48)
     if ovf:
-        _size_hint.pop(key, None)
-        raise CapacityOverflowError(f"gsr: the previous capacity-bounded render of this shape exceeded its bounds "
-                                    f"({_lib.describe_overflow(ovf)}); its outputs were NaN -- the bounds are "
-                                    "reset, re-run the step")
+        _size_hint.pop(m.key, None)
+        raise CapacityOverflowError(f"gsr: a capacity-bounded render of this shape exceeded its bounds "
+                                    f"({_lib.describe_overflow(ovf)}); its outputs and gradients were NaN -- the "
+                                    "bounds are reset (the next call sizes exactly), re-run the step")
     h = _hint_from(st)
-    old = _size_hint.get(key)
+    old = _size_hint.get(m.key)
     if old is not None:   # keep bounds monotone over a window: shrink slowly, grow at once
         h = {k: max(v, int(0.9 * old[k])) for k, v in h.items()}
-    _size_hint[key] = h
+    _size_hint[m.key] = h
+
+
+def _monitor_check(key) -> None:
+    """Every bounded forward of this shape whose stats have arrived, oldest first (no wait):
+    raise on the first overflow, refresh the bounds from the others (one slot
+    per shape dropped the earlier calls of a host running several steps ahead)."""
+    dq = _monitors.get(key)
+    while dq:
+        m = dq[0]
+        if not m.done and not m.event.query():
+            return
+        dq.popleft()
+        _monitor_process(m)
 
 
 def _monitor_enqueue(b) -> None:
-    """Copy this bounded forward's stats to pinned memory behind its kernels (no wait)."""
+    """Copy this bounded forward's stats to pinned memory behind its kernels (no wait) and
+    queue them for the checks (b.monitor: the backward's own check)."""
+    b.monitor = None
     if _capturing():
         return
-    m = _monitors.get(b.key)
-    if m is None:
-        m = [torch.empty(_STATS_I32, dtype=torch.int32, pin_memory=True), None]
-        _monitors[b.key] = m
-    m[0].copy_(b.pre.view("stats_dev", _I32), non_blocking=True)
-    m[1] = torch.cuda.Event()
-    m[1].record()
+    dq = _monitors.setdefault(b.key, collections.deque())
+    if len(dq) >= _MAX_PENDING:   # a host far ahead of the GPU: wait for the oldest
+        m = dq.popleft()
+        m.event.synchronize()
+        _monitor_process(m)
+    host = _monitor_pool.pop() if _monitor_pool else torch.empty(_STATS_I32, dtype=torch.int32, pin_memory=True)
+    host.copy_(b.pre.view("stats_dev", _I32), non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    b.monitor = _Monitor(b.key, host, ev)
+    dq.append(b.monitor)
+
+
+def _backward_check(b) -> None:
+    """After a bounded call's backward kernels are enqueued: wait for ITS forward's stats copy
+    (finished long before, in a training step) and raise if the forward overflowed -- the
+    NaN v_params is never returned to autograd.  (The backward's own GSR_OVF_UNIT goes to the
+    sticky word, check_overflow.)"""
+    m = getattr(b, "monitor", None)
+    if m is None or m.done:
+        return
+    m.event.synchronize()
+    _monitor_process(m)
 
 
 # Per (device, tile count, stream): the projection's tile histogram + emission counter, shared
@@ -345,9 +402,15 @@ class _Bins:
         self.key = (str(device), C, N, width, height, key_extra)
         self.need_bwd = need_bwd   # False: no chunk records, no finalize (tile_end left raw)
         mode = capacity or _capacity_default
-        if mode not in ("exact", "bounded"):
-            raise ValueError(f"capacity mode must be 'exact' or 'bounded', got {mode!r}")
+        if mode not in _MODES:
+            raise ValueError(f"capacity mode must be one of {_MODES}, got {mode!r}")
         self.bounded = False
+        self.monitor = None
+        if mode == "auto":
+            # bounded only where a backward follows to check it, and where bounds exist
+            if need_bwd and not _capturing():
+                _monitor_check(self.key)
+            mode = "bounded" if need_bwd and (self.key in _size_hint or _capturing()) else "exact"
         if mode == "bounded":
             if not _capturing():
                 _monitor_check(self.key)
@@ -738,6 +801,7 @@ class _Render3D(torch.autograd.Function):
                                      _ptr(v_rgb), _ptr(v_alpha), q["k_of_s"], _ptr(partial), stream),
                   "gsr3d_raster_bwd")
         v_params = backward3d(b, ctx.meta, raster)
+        _backward_check(b)   # a bounded forward that overflowed raises here, before .grad
         return v_params.view(ctx.params_shape), None, None, None, None, None, None, None
 
 
@@ -809,6 +873,7 @@ class _Render2D(torch.autograd.Function):
                                       q["isect_off"], q["cnt"], q["tile_cut"], _ptr(partial), q["stats_dev"],
                                       _ptr(v_params), stream),
                   "gsr2d_project_bwd")
+        _backward_check(b)   # a bounded forward that overflowed raises here, before .grad
         return v_params.view(ctx.params_shape), None, None, None, None, None, None, None
 
 

@@ -33,6 +33,11 @@ except ImportError:  # pragma: no cover
     _gsr_render = importlib.import_module("gsr.render")
 
 
+def _check_capacity(capacity: str) -> None:
+    if capacity not in _gsr_render._MODES:
+        raise ValueError(f"Unknown capacity '{capacity}'. Expected one of {list(_gsr_render._MODES)}.")
+
+
 class GaussianRenderer(ABC, nn.Module):
     """Abstract base class for Gaussian renderers (src/gaussian_renderer.py:23-107)."""
 
@@ -73,15 +78,23 @@ class GaussianRenderer3D(GaussianRenderer):
 
     ``radius_mode`` selects gsplat's per-Gaussian extent rule: ``"opacity_aabb"`` (gsplat
     >= 1.5, default) or ``"isotropic_3sigma"`` (gsplat <= 1.4).
+
+    ``capacity`` (gsr.render): ``"auto"`` (default) sizes a training call's intersection
+    buffers from the previous call of the same shape with no host wait and checks them in
+    the backward (which raises ``CapacityOverflowError`` before any NaN gradient is
+    returned); ``"exact"`` reads the intersection count back every forward, as gsplat does.
     """
 
-    def __init__(self, width: int, height: int, device: str = "cuda", radius_mode: str = "opacity_aabb"):
+    def __init__(self, width: int, height: int, device: str = "cuda", radius_mode: str = "opacity_aabb",
+                 capacity: str = "auto"):
         super().__init__(width, height, device)
         modes = {"opacity_aabb": 0, "isotropic_3sigma": 1}
         if radius_mode not in modes:
             raise ValueError(f"Unknown radius_mode '{radius_mode}'. Expected one of {sorted(modes)}.")
         self.radius_mode = radius_mode
-        self._opts = _gsr_render.RenderOptions3D(radius_mode=modes[radius_mode])
+        _check_capacity(capacity)
+        self.capacity = capacity
+        self._opts = _gsr_render.RenderOptions3D(radius_mode=modes[radius_mode], capacity=capacity)
 
     def get_num_params(self) -> int:
         return 14
@@ -125,7 +138,8 @@ class GaussianRenderer2D(GaussianRenderer):
     [2:4], rotation [4] (radians), colors [5:8], logit opacity [8].  Compositing follows
     parameter index order with integer pixel centres, exactly like the reference.
     ``viewmat`` and ``K`` are ignored.  ``kernel_size``, ``sigma_cutoff`` and ``batch_size``
-    are accepted and stored but, as in the reference's live path, unused.
+    are accepted and stored but, as in the reference's live path, unused.  ``capacity``: as
+    for GaussianRenderer3D.
     """
 
     def __init__(
@@ -137,12 +151,15 @@ class GaussianRenderer2D(GaussianRenderer):
         sigma_cutoff: float = 3.0,
         batch_size: int = 1,
         eps_cut: float = 1e-8,
+        capacity: str = "auto",
     ):
         super().__init__(width, height, device)
         self.kernel_size = kernel_size
         self.sigma_cutoff = sigma_cutoff
         self.batch_size = batch_size
         self.eps_cut = eps_cut
+        _check_capacity(capacity)
+        self.capacity = capacity
 
     def get_num_params(self) -> int:
         return 9
@@ -166,7 +183,7 @@ class GaussianRenderer2D(GaussianRenderer):
             final_rgb = canvas + self.background_color.to(dev).view(1, 1, 3)
             return final_rgb, alpha_canvas
         return _gsr_render.render2d(gaussian_params, self.width, self.height, self.background_color,
-                                    self.eps_cut)
+                                    self.eps_cut, capacity=self.capacity)
 
 
 def create_renderer(
@@ -178,15 +195,16 @@ def create_renderer(
 ) -> GaussianRenderer:
     """Factory (src/gaussian_renderer.py:522-563): "2d" or "3d", case-insensitive.
 
-    2D forwards ``**kwargs`` (kernel_size, sigma_cutoff, batch_size, eps_cut); 3D drops them
-    like the reference, except ``radius_mode`` which only this implementation knows.
+    2D forwards ``**kwargs`` (kernel_size, sigma_cutoff, batch_size, eps_cut, capacity); 3D
+    drops them like the reference, except ``radius_mode`` and ``capacity``, which only this
+    implementation knows.
     """
     mode = mode.lower()
 
     if mode == "2d":
         return GaussianRenderer2D(width, height, device, **kwargs)
     elif mode == "3d":
-        extra = {k: kwargs[k] for k in ("radius_mode",) if k in kwargs}
+        extra = {k: kwargs[k] for k in ("radius_mode", "capacity") if k in kwargs}
         return GaussianRenderer3D(width, height, device, **extra)
     else:
         raise ValueError(

@@ -150,26 +150,64 @@ def _shrunk(key_fn, **scale):
     return key
 
 
+def _overflowing_step3d(p, V, K, W, H, vr, va):
+    """A bounded training step whose forward overflows: NaN rgb / alpha, and the backward
+    raises CapacityOverflowError before any gradient reaches .grad (ADVICE r3 / VERDICT r3)."""
+    from gsr import render as R
+    pg = p.detach().clone().requires_grad_(True)
+    rgb, alpha = R.render3d(pg, V, K, W, H, torch.ones(3, device=p.device), R.RenderOptions3D(capacity="bounded"))
+    torch.cuda.synchronize()
+    assert torch.isnan(rgb).all() and torch.isnan(alpha).all()
+    with pytest.raises(R.CapacityOverflowError):
+        torch.autograd.backward([rgb, alpha], [vr, va])
+    assert pg.grad is None
+    return rgb
+
+
 @pytest.mark.parametrize("bound,bit", [("I", 1), ("chunks", 2), ("busy", 4)])
 def test_forced_overflow_3d(cuda, bound, bit):
     from gsr import _lib, render as R
     sc = _scene3d(cuda)
     ex = _step3d(*sc, capacity="exact")
     _shrunk(lambda k: True, **{bound: 0.25})
-    rgb, alpha, grad = _step3d(*sc, capacity="bounded")
-    torch.cuda.synchronize()
-    assert torch.isnan(rgb).all() and torch.isnan(alpha).all() and torch.isnan(grad).all()
+    _overflowing_step3d(*sc)
     bits = R.overflow_status(cuda)
     assert bits & bit, _lib.describe_overflow(bits)
-    # the next bounded call of the shape reports the previous one's overflow ...
-    with pytest.raises(R.CapacityOverflowError):
-        _step3d(*sc, capacity="bounded")
     with pytest.raises(R.CapacityOverflowError):
         R.check_overflow(cuda)
-    # ... and an exact call afterwards is correct (the emission counters were left zero)
-    assert _same(ex, _step3d(*sc, capacity="exact"))
+    # the backward dropped the shape's bounds: the next call sizes exactly, and it is correct
+    # (the emission counters were left zero); the one after is bounded again
     assert _same(ex, _step3d(*sc, capacity="bounded"))
+    assert not R.last_stats()["_bins"].bounded
+    assert _same(ex, _step3d(*sc, capacity="bounded"))
+    assert R.last_stats()["_bins"].bounded
     R.check_overflow(cuda)
+
+
+def test_forced_overflow_forward_only_next_call_raises(cuda):
+    """No backward to check it: a forward-only bounded call that overflowed is reported by the
+    next call of the shape, also when several calls were queued behind it unchecked (the
+    monitors are a FIFO per shape)."""
+    from gsr import render as R
+    p, V, K, W, H, vr, va = _scene3d(cuda)
+    bg = torch.ones(3, device=cuda)
+    opts = R.RenderOptions3D(capacity="bounded")
+    with torch.no_grad():
+        ex = R.render3d(p, V, K, W, H, bg, R.RenderOptions3D(capacity="exact"))
+        key = _shrunk(lambda k: True)
+        good = dict(R._size_hint[key])
+        R._size_hint[key] = dict(good, I=good["I"] // 8)
+        torch.cuda.synchronize()
+        torch.cuda._sleep(400_000_000)   # keep the GPU busy while the host queues the calls
+        bad = R.render3d(p, V, K, W, H, bg, opts)   # overflows; nothing waits for it
+        R._size_hint[key] = good
+        later = [R.render3d(p, V, K, W, H, bg, opts) for _ in range(3)]   # queued behind it
+        with pytest.raises(R.CapacityOverflowError):
+            torch.cuda.synchronize()
+            R.render3d(p, V, K, W, H, bg, opts)
+    assert torch.isnan(bad[0]).all()
+    assert all(_same(ex, o) for o in later)
+    R.overflow_status(cuda, reset=True)
 
 
 def test_forced_overflow_split_sort_segment(cuda):
@@ -179,9 +217,7 @@ def test_forced_overflow_split_sort_segment(cuda):
     b = R.last_stats()["_bins"]
     assert b.n_busy <= 128 and b.max_seg > 2200, (b.n_busy, b.max_seg)
     _shrunk(lambda k: True, max_seg=0.3)
-    rgb, alpha, grad = _step3d(*sc, capacity="bounded")
-    torch.cuda.synchronize()
-    assert torch.isnan(rgb).all() and torch.isnan(grad).all()
+    _overflowing_step3d(*sc)
     assert R.overflow_status(cuda, reset=True) & 8
 
 
@@ -199,11 +235,9 @@ def test_forced_overflow_lazy(cuda):
         assert b.n_lazy > 0 and b.n_sort_big > 4, (b.n_lazy, b.n_sort_big)
         key = _shrunk(lambda k: True)
         R._size_hint[key]["big"] = 0   # the re-render covers 4 tiles (the margin)
-        rgb, alpha, grad = _step3d(*sc, capacity="bounded")
-        torch.cuda.synchronize()
+        _overflowing_step3d(*sc)
         bits = R.overflow_status(cuda, reset=True)
         assert bits & 16, _lib.describe_overflow(bits)
-        assert torch.isnan(rgb).all() and torch.isnan(grad).all()
     finally:
         _lib.check(L.gsr_set_lazy_sort(16384, 4096), "gsr_set_lazy_sort")
 
@@ -214,13 +248,16 @@ def test_forced_overflow_2d(cuda):
     W, H = 96, 80
     p = gaussians2d(3000, W, H, 7).to(cuda)
     bg = torch.ones(3, device=cuda)
-    R.render2d(p, W, H, bg, capacity="exact")
+    pg = p.clone().requires_grad_(True)
+    R.render2d(pg, W, H, bg, capacity="exact")   # (a training call: the bounds of the key)
     _shrunk(lambda k: True, I=0.2)
     pg = p.clone().requires_grad_(True)
     rgb, alpha = R.render2d(pg, W, H, bg, capacity="bounded")
-    (rgb.sum() + alpha.sum()).backward()
     torch.cuda.synchronize()
-    assert torch.isnan(rgb).all() and torch.isnan(pg.grad).all()
+    assert torch.isnan(rgb).all()
+    with pytest.raises(R.CapacityOverflowError):
+        (rgb.sum() + alpha.sum()).backward()
+    assert pg.grad is None
     assert R.overflow_status(cuda, reset=True) & 1
 
 

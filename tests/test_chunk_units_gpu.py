@@ -109,6 +109,9 @@ def test_unit_mismatch_is_flagged(cuda):
     assert torch.isnan(v).all()
     st = b.pre.view("stats_dev", torch.int32).tolist()
     assert st[12] & 32, st
+    # ... and reported to the sticky status word: check_overflow() raises
+    with pytest.raises(R.CapacityOverflowError, match="chunk_entries differs"):
+        R.check_overflow(cuda)
 
 
 @pytest.mark.parametrize("lanes", [0, 1, 4, 16])

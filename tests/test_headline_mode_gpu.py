@@ -1,0 +1,203 @@
+"""The mode bench.py times, at BASELINE.json's full sizes, and the drop-in's capacity mode.
+
+* bench.py times capacity-bounded steps captured in ONE HIP graph (gsr.render "bounded",
+  torch.cuda.CUDAGraph).  Here that exact mode -- bounds from the previous step, a captured
+  fwd+bwd step replayed -- is checked bitwise against the default exact eager step (rgb,
+  alpha and v_params) on config 3's and config 5's whole 6-view workloads (2.6 M and 25 M
+  list entries, lazy depth order at config 5), also after the parameters move in place
+  between replays (VERDICT r3 "the timed mode has no full-size parity test").  The exact
+  eager step itself is what test_fullsize_gpu.py checks against the oracle.
+* The drop-in renderers (src/gaussian_renderer.py) default to capacity "auto": a training
+  call is bounded once an earlier call of the shape left bounds, and its backward checks the
+  forward's overflow word and raises CapacityOverflowError BEFORE any gradient is returned,
+  so no NaN reaches .grad / the optimizer.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _clean(cuda):
+    from gsr import render as R
+    R.overflow_status(cuda, reset=True)
+    yield
+    R.overflow_status(cuda, reset=True)
+    R._size_hint.clear()
+    R._monitors.clear()
+
+
+def _scene(idx, dev):
+    from gsr.scenes import CONFIGS, gaussians3d, ring_cameras
+    c = CONFIGS[idx]
+    V, K = ring_cameras(c.views, c.width, c.height)
+    g = torch.Generator().manual_seed(c.seed + 1)
+    vr = torch.randn(c.views, c.height, c.width, 3, generator=g).to(dev)
+    va = torch.randn(c.views, c.height, c.width, generator=g).to(dev)
+    return c, gaussians3d(c.N, c.seed).to(dev), V.to(dev), K.to(dev), vr, va
+
+
+@pytest.mark.parametrize("idx", [3, 5])
+def test_graph_bounded_equals_exact_fullsize(cuda, idx):
+    from gsr import render as R
+    c, p0, V, K, vr, va = _scene(idx, cuda)
+    W, H = c.width, c.height
+    bg = torch.ones(3, device=cuda)
+
+    def eager(p, capacity):
+        pg = p.detach().clone().requires_grad_(True)
+        rgb, alpha = R.render3d(pg, V, K, W, H, bg, R.RenderOptions3D(capacity=capacity))
+        torch.autograd.backward([rgb, alpha], [vr, va])
+        return rgb.detach(), alpha.detach(), pg.grad
+
+    ref = eager(p0, "exact")
+    params = p0.clone().requires_grad_(True)
+    opts = R.RenderOptions3D(capacity="bounded")
+
+    def step():
+        params.grad = None
+        rgb, alpha = R.render3d(params, V, K, W, H, bg, opts)
+        torch.autograd.backward([rgb, alpha], [vr, va])
+        return rgb, alpha
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        g_rgb, g_alpha = step()
+    g_grad = params.grad
+    for k in range(2):
+        if k:
+            with torch.no_grad():
+                params.copy_(p0)
+                params[:, 0:3] += 0.002
+            ref = eager(params, "exact")
+        graph.replay()
+        torch.cuda.synchronize()
+        R.check_overflow(cuda)
+        assert torch.equal(ref[0], g_rgb), ("rgb", k)
+        assert torch.equal(ref[1], g_alpha), ("alpha", k)
+        assert torch.equal(ref[2], g_grad), ("v_params", k)
+        print(f"[cfg{idx}] replay {k}: rgb/alpha/v_params bitwise equal to the exact eager step "
+              f"({R.last_stats()['n_isect']} intersections)")
+    del graph
+
+
+def _dropin_step(r, p, V, K, vr, va):
+    pg = p.detach().clone().requires_grad_(True)
+    rgb, alpha = r.render(pg, V, K)
+    torch.autograd.backward([rgb, alpha], [vr, va])
+    return rgb.detach(), alpha.detach(), pg
+
+
+def test_dropin_auto_mode(cuda):
+    """create_renderer("3d") defaults to "auto": the first training call of a shape is exact,
+    later ones bounded with no host wait in the forward; results bitwise equal."""
+    from gsr import render as R
+    from src.gaussian_renderer import create_renderer
+    from gsr.scenes import gaussians3d, ring_cameras
+    W, H, C = 192, 170, 3
+    r = create_renderer("3d", W, H, device="cuda")
+    assert r.capacity == "auto"
+    r.set_background_color(torch.ones(3, device=cuda))
+    p = gaussians3d(20000, 31).to(cuda)
+    V, K = ring_cameras(C, W, H)
+    V, K = V.to(cuda), K.to(cuda)
+    g = torch.Generator().manual_seed(32)
+    vr = torch.randn(C, H, W, 3, generator=g).to(cuda)
+    va = torch.randn(C, H, W, generator=g).to(cuda)
+    outs = []
+    for k in range(3):
+        outs.append(_dropin_step(r, p, V, K, vr, va))
+        assert R.last_stats()["_bins"].bounded == (k > 0), k
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1])
+        assert torch.equal(o[2].grad, outs[0][2].grad)
+    # forward-only calls stay exact (no backward would check them)
+    with torch.no_grad():
+        r.render(p, V, K)
+    assert not R.last_stats()["_bins"].bounded
+    R.check_overflow(cuda)
+
+
+def test_dropin_auto_overflow_raises_in_backward(cuda):
+    """A much denser scene of the same shape after a sparse one: the bounded forward overflows,
+    and loss.backward() raises CapacityOverflowError -- no gradient (NaN or otherwise) reaches
+    .grad.  The call after it sizes exactly and is correct."""
+    from gsr import render as R
+    from src.gaussian_renderer import create_renderer
+    from gsr.scenes import gaussians3d, ring_cameras
+    W, H, C = 192, 170, 2
+    r = create_renderer("3d", W, H, device="cuda")
+    V, K = ring_cameras(C, W, H)
+    V, K = V.to(cuda), K.to(cuda)
+    g = torch.Generator().manual_seed(5)
+    vr = torch.randn(C, H, W, 3, generator=g).to(cuda)
+    va = torch.randn(C, H, W, generator=g).to(cuda)
+    dense = gaussians3d(20000, 41).to(cuda)
+    sparse = dense.clone()
+    sparse[2000:, 13] = -10.0      # opacity < 1/255: culled, no tiles (90 % of the scene)
+    _dropin_step(r, sparse, V, K, vr, va)   # exact: leaves the (small) bounds
+    _dropin_step(r, sparse, V, K, vr, va)   # bounded, fits
+    assert R.last_stats()["_bins"].bounded
+    pg = dense.clone().requires_grad_(True)
+    rgb, alpha = r.render(pg, V, K)
+    assert R.last_stats()["_bins"].bounded
+    loss = (rgb * vr).sum() + (alpha * va).sum()
+    with pytest.raises(R.CapacityOverflowError):
+        loss.backward()
+    assert pg.grad is None
+    R.overflow_status(cuda, reset=True)
+    # bounds dropped: the retry is exact and equals an exact-mode renderer's result
+    got = _dropin_step(r, dense, V, K, vr, va)
+    assert not R.last_stats()["_bins"].bounded
+    ref = _dropin_step(create_renderer("3d", W, H, device="cuda", capacity="exact"), dense, V, K, vr, va)
+    torch.cuda.synchronize()
+    assert torch.equal(got[0], ref[0]) and torch.equal(got[2].grad, ref[2].grad)
+    assert torch.isfinite(got[2].grad).all()
+
+
+def test_kernel_timing_during_capture(cuda):
+    """Kernel timing left on while a bounded step is captured: no timing events are recorded
+    inside the capture (ROCm rejects them), the capture succeeds."""
+    from gsr import render as R
+    c, p0, V, K, vr, va = _scene(3, cuda)
+    p = p0[:20000].contiguous()
+    W, H = 192, 170
+    V, K = V[:2], K[:2]
+    vr, va = vr[:2, :H, :W].contiguous(), va[:2, :H, :W].contiguous()
+    bg = torch.ones(3, device=cuda)
+    params = p.clone().requires_grad_(True)
+    opts = R.RenderOptions3D(capacity="bounded")
+
+    def step():
+        params.grad = None
+        rgb, alpha = R.render3d(params, V, K, W, H, bg, opts)
+        torch.autograd.backward([rgb, alpha], [vr, va])
+
+    step()
+    torch.cuda.synchronize()
+    R.enable_kernel_timing(True)
+    try:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            step()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        n_before = sum(len(v) for v in R._timers.values())
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+        assert sum(len(v) for v in R._timers.values()) == n_before
+        graph.replay()
+        torch.cuda.synchronize()
+    finally:
+        R.enable_kernel_timing(False)
+    R.check_overflow(cuda)
