@@ -2,24 +2,30 @@
 """Benchmark: rendered frames/s (fwd+bwd) of the MI355X rasterizer on a BASELINE config.
 
 A "step" = one full pass of the hot path over one batch of synthetic input: projection ->
-tile binning (incl. its one 32-byte host read) -> raster fwd -> raster bwd (fixed random
-cotangents) -> projection bwd.  Default workload: BASELINE config 3 (3D, 200k Gaussians,
+tile binning -> raster fwd -> raster bwd (fixed random cotangents) -> projection bwd.  The
+timed steps run capacity-bounded (no host read; `--capacity exact` adds the 32-byte stats
+read-back per forward that gsplat's count read-back corresponds to).  Default workload: BASELINE config 3 (3D, 200k Gaussians,
 576x512, 6 cameras) -- the shape BASELINE.json's north-star target is quoted on.  Inputs
 are resident in HBM before the timed region.  value = views (frames) rendered per second
 over the whole job.
 
-Multi-GPU (torchrun, one process per GPU, RCCL over xGMI), SURVEY.md §8(e):
+Multi-GPU (torchrun, one process per GPU, RCCL over xGMI), SURVEY.md §8(e).  At N > 1 the
+line reports the default layout as `value` AND the config's other layout next to it (keys
+"weak" / "strong" / "frame_owners", each with its own value, ms_per_step and allreduce_ms):
   * 3D, --shard views (default, "weak"): a multi-camera batch -- every rank renders C views of
     its own (ring offset per rank) of the same Gaussians, and the [N,14] gradient is
     all-reduced in Gaussian-range buckets that overlap the projection backward.
-  * 3D, --shard units ("strong"): ONE C-view job per step; the C*th (view, tile row) units are
-    cut into `world` contiguous ranges balanced by list entries read plus a per-view cost
-    (gsr.multiview.unit_shard); each rank projects only the views it touches, bins only its
-    rows, and all-reduces its partial v_params in buckets (latency- and exchange-bound at
-    configs 3 and 5: DESIGN.md §5, --rank-share).
-  * 2D (config 4, "strong"): 8 frames x 6 views = 48 (frame, view) units, round-robin over
-    ranks; each rank renders its units batched per frame bucket and all-reduces the [8,N,9]
-    gradient per bucket (async, overlapping the next bucket).
+  * 3D, --shard units ("strong", reported under "strong"): ONE C-view job per step; the C*th
+    (view, tile row) units are cut into `world` contiguous ranges balanced by list entries
+    read plus a per-view cost (gsr.multiview.unit_shard); each rank projects only the views
+    it touches, bins only its rows, and all-reduces its partial v_params in buckets
+    (latency- and exchange-bound at configs 3 and 5: DESIGN.md §5, --rank-share).
+  * 2D (config 4), --shard units (default, "strong"): 8 frames x 6 views = 48 (frame, view)
+    units, round-robin over ranks; each rank renders its units batched per frame bucket and
+    all-reduces the [8,N,9] gradient per bucket (async, overlapping the next bucket) -- the
+    RCCL Gaussian-gradient all-reduce SURVEY.md §8(e) asks the benchmark to exercise.
+  * 2D, --shard frames (reported under "frame_owners"): frame f with all its views on rank
+    f % N, no Gaussian-gradient exchange (the frames' sets are disjoint).
   * config 2 (one view, fwd-only): replicas, "weak".
 --rank-share N (one GPU, no collectives): times each of the N ranks' shares of the strong
 layout one after the other and reports the projected N-GPU time (max share + a ring
@@ -77,9 +83,10 @@ def parse(argv=None):
                     help="3D, N>1: 'views' (default) = a multi-camera batch, every rank renders C views of its own "
                          "and the Gaussian gradient is all-reduced (weak scaling); 'units' = the ranks split ONE "
                          "C-view job by (view, tile row) units (strong scaling; latency- and exchange-bound, "
-                         "see DESIGN.md §5 and --rank-share).  2D (config 4), N>1: 'frames' (default) = frame f "
-                         "with all its views on rank f %% N, no Gaussian-gradient exchange (the frames' sets are "
-                         "disjoint); 'units' = (frame, view) units round-robin with a per-frame-bucket all-reduce")
+                         "see DESIGN.md §5 and --rank-share).  2D (config 4), N>1: 'units' (default) = (frame, "
+                         "view) units round-robin with a per-frame-bucket all-reduce; 'frames' = frame f with all "
+                         "its views on rank f %% N, no Gaussian-gradient exchange (the frames' sets are disjoint). "
+                         "At N>1 the other layout of the config is timed too and reported in the same line")
     ap.add_argument("--buckets", type=int, default=0,
                     help="all-reduce buckets (3D: Gaussian ranges of v_params; 2D: frame ranges); 0 = default "
                          "(3D 4, 2D 2; 1 on a single GPU)")
@@ -120,7 +127,7 @@ def parse(argv=None):
                          "launches; -1: 1 on a single GPU with bounded capacity, else 0")
     a = ap.parse_args(argv)
     if a.shard is None:
-        a.shard = "frames" if a.config == 4 else "views"
+        a.shard = "units" if a.config == 4 else "views"
     if a.shard == "frames" and a.config != 4:
         raise SystemExit("--shard frames is the 2D multi-frame layout (config 4)")
     return a
@@ -373,8 +380,8 @@ def psnr(pred_hw3: torch.Tensor, gt_hw3: torch.Tensor) -> float:
 def delta_psnr(cfg, params_cpu, V, K, dev, rgb_oracle_view0=None):
     """target = the oracle render of a perturbed copy (means + N(0,0.002),
     colours + N(0,0.05)); dPSNR = |PSNR(gsr, target) - PSNR(oracle, target)|.  3D: view 0 (the
-    CPU baseline's band for config 5); 2D: the first 2000 Gaussians of frame 0 (the dense
-    oracle is O(N) per pixel)."""
+    CPU baseline's band for config 5); 2D: a 16x128 window of frame 0 at full density (the
+    dense oracle is O(N) per pixel, so it runs over the Gaussians that can reach the window)."""
     from gsr import render as R
     from oracle.oracle2d import render2d_dense
     from oracle.oracle3d import render3d as oracle_render3d
@@ -398,15 +405,34 @@ def delta_psnr(cfg, params_cpu, V, K, dev, rgb_oracle_view0=None):
             a, b, t = rgb_gpu[0].cpu()[rows], rgb_oracle_view0[0][rows], target[0][rows]
             sample = f"view 0" + (f", pixel rows {rows.start}-{rows.stop}" if band else "")
         else:
-            n = 2000
-            pt = params_cpu[:n].clone()
-            pt[:, 0:2] += 0.002 * torch.randn(n, 2, generator=g)
-            pt[:, 5:8] += 0.05 * torch.randn(n, 3, generator=g)
-            t, _ = render2d_dense(pt, cfg.width, cfg.height, torch.ones(3))
-            b, _ = render2d_dense(params_cpu[:n], cfg.width, cfg.height, torch.ones(3))
-            a, _ = R.render2d(params_cpu[:n].to(dev), cfg.width, cfg.height, torch.ones(3, device=dev))
-            a = a.cpu()
-            sample = f"first {n} Gaussians of frame 0"
+            # the full-density frame (all N Gaussians) in the 16x128 window that
+            # tests/test_cfg4_window_vs_oracle checks: the dense reference compositor over every
+            # Gaussian that can reach the window (e^-40 * opacity bound), the GPU's full render cropped
+            y0, x0 = 240, 192
+            y1, x1 = y0 + 16, x0 + 128
+            p = params_cpu
+            s_max = torch.exp(p[:, 2:4]).amax(1)
+            dx = (x0 - p[:, 0]).clamp_min(0) + (p[:, 0] - (x1 - 1)).clamp_min(0)
+            dy = (y0 - p[:, 1]).clamp_min(0) + (p[:, 1] - (y1 - 1)).clamp_min(0)
+            idx = torch.nonzero((dx * dx + dy * dy) / (2 * s_max * s_max + 1e-8) < 40.0)[:, 0]
+            q = p[idx].clone()
+            q[:, 0] -= x0
+            q[:, 1] -= y0
+            qt = q.clone()
+            qt[:, 0:2] += 0.002 * torch.randn(q.shape[0], 2, generator=g)
+            qt[:, 5:8] += 0.05 * torch.randn(q.shape[0], 3, generator=g)
+            nt = torch.get_num_threads()
+            torch.set_num_threads(1)   # ~10k tiny per-Gaussian steps: op overhead, not FLOPs
+            try:
+                t, _ = render2d_dense(qt, x1 - x0, y1 - y0, torch.ones(3))
+                b, _ = render2d_dense(q, x1 - x0, y1 - y0, torch.ones(3))
+            finally:
+                torch.set_num_threads(nt)
+            a, _ = R.render2d(params_cpu.to(dev), cfg.width, cfg.height, torch.ones(3, device=dev))
+            a = a.cpu()[y0:y1, x0:x1]
+            sample = (f"frame 0 at full density ({params_cpu.shape[0]} Gaussians), window rows {y0}-{y1} "
+                      f"cols {x0}-{x1} (tests/test_fullsize_gpu.py::test_cfg4_window_vs_oracle); oracle over the "
+                      f"{idx.numel()} Gaussians that can reach it")
     pg, po = psnr(a, t), psnr(b, t)
     return {"dpsnr_db": abs(pg - po), "psnr_gsr_db": pg, "psnr_oracle_db": po, "sample": sample,
             "target": "oracle render of means+N(0,0.002), colours+N(0,0.05)",
@@ -469,7 +495,8 @@ class Workload:
                 self.layout = f"{F} frames x {C} views batched in one launch sequence"
             elif self.owned:
                 self.layout = (f"frame owners: frame f with its {C} views on rank f % {world}, batched in one launch "
-                               "sequence; no Gaussian-gradient exchange (disjoint frame sets)")
+                               "sequence; no Gaussian-gradient exchange (disjoint frame sets); the network weight all-reduce "
+                               "that frame-parallel training adds is outside the rasterizer and not counted")
             else:
                 self.layout = (f"(frame, view) units round-robin over {world} rank(s), batched per frame bucket "
                                f"({self.buckets}), async all-reduce of the [8,N,9] gradient per bucket")
@@ -762,6 +789,77 @@ def roofline(w: Workload, dom_name, dom, args):
             "units_per_launch": {"C": C, "P": P, "N": cfg.N, "I": I, "I_eff": I_eff}}, (C, P, I, I_eff)
 
 
+def _sync(dev) -> None:
+    if torch.device(dev).type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def measure_allreduce_ms(w, dist, dev, reps: int = 10):
+    """The step's Gaussian-gradient collective on its own: `reps` x all_reduce of a buffer the
+    size of the gradient the layout exchanges (max over ranks); None for a layout with no
+    collective (2D frame owners).  HIP events on the stream on a GPU, wall clock otherwise."""
+    if getattr(w, "owned", False):
+        return None
+    buf = torch.zeros_like(w.params)
+    for _ in range(3):
+        dist.all_reduce(buf)
+    _sync(dev)
+    dist.barrier()
+    if torch.device(dev).type == "cuda":
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            dist.all_reduce(buf)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+    else:
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dist.all_reduce(buf)
+        ms = 1000.0 * (time.perf_counter() - t0) / reps
+    t = torch.tensor([ms], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t)
+
+
+def other_layouts(cfg, shard: str) -> list:
+    """Multi-GPU layouts reported NEXT TO the default one in the same JSON line:
+    3D fwd+bwd -- the weak multi-camera batch ('views') and the strong one-job split ('units')
+    both; config 4 -- the round-robin (frame, view) units with their all-reduce and the frame
+    owners with none.  Config 2 (one fwd-only view) has replicas only."""
+    if cfg.mode == "3d" and cfg.backward and cfg.index != 2:
+        return [x for x in ("views", "units") if x != shard]
+    if cfg.mode == "2d":
+        return [x for x in ("units", "frames") if x != shard]
+    return []
+
+
+LAYOUT_KEY = {"views": "weak", "units": "strong", "frames": "frame_owners"}
+
+
+def measure_layout(cfg, args, dev, world, rank, shard, dist, make_workload=None, timer=None) -> dict:
+    """One more layout of the same config on the same ranks, timed like the headline one
+    (warmup, barrier-bracketed K steps, max over ranks): value = the units the whole job
+    completes per second, plus its own collective timing."""
+    make_workload = make_workload or Workload
+    timer = timer or time_steps
+    w = make_workload(cfg, dev, world, rank, shard, args.buckets, "none", comm=True, view_cost=args.view_cost,
+                      exchange=args.exchange)
+    elapsed = timer(w, args.steps, args.warmup, dist, graph=False)[0]
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t)
+    out = {"value": w.units_total * args.steps / elapsed, "unit": "frames/s",
+           "ms_per_step": 1000.0 * elapsed / args.steps, "scaling": w.scaling, "shard": shard,
+           "units_per_step": w.units_total, "parallelism": w.layout,
+           "launch": "eager launches", "allreduce_ms": measure_allreduce_ms(w, dist, dev)}
+    del w
+    if torch.device(dev).type == "cuda":
+        torch.cuda.empty_cache()
+    return out
+
+
 def rank_share_report(cfg, args, dev, n: int, weights=None):
     """--rank-share N: time each rank's share of the strong layout alone on this GPU."""
     from gsr import render as R
@@ -907,24 +1005,7 @@ def main(argv=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
 
-    ar_ms = None
-    if world > 1 and not getattr(w, "owned", False):   # the frame-owner layout has no collective
-        # the step's collective volume timed on its own (10 x all_reduce of the gradient buffer)
-        buf = torch.zeros_like(w.params)
-        for _ in range(3):
-            dist.all_reduce(buf)
-        torch.cuda.synchronize()
-        dist.barrier()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(10):
-            dist.all_reduce(buf)
-        e1.record()
-        torch.cuda.synchronize()
-        t = torch.tensor([e0.elapsed_time(e1) / 10], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ar_ms = float(t)
-
+    ar_ms = measure_allreduce_ms(w, dist, dev) if world > 1 else None
     value = w.units_total * args.steps / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
     roof, (C, P, I, I_eff) = roofline(w, dom_name, dom, args)
@@ -967,6 +1048,14 @@ def main(argv=None):
                     "busy_tiles": R.last_stats().get("n_busy"), "tiles": R.last_stats().get("tiles")},
     }
     log(f"timed {args.steps} steps: {1000.0 * elapsed / args.steps:.3f} ms/step")
+    out["layout"] = LAYOUT_KEY.get(args.shard, args.shard) if cfg.index != 2 else "replicas"
+    if world > 1:
+        del w
+        torch.cuda.empty_cache()
+        w = None
+        for sh in other_layouts(cfg, args.shard):
+            log(f"also timing the '{sh}' layout")
+            out[LAYOUT_KEY[sh]] = measure_layout(cfg, args, dev, world, rank, sh, dist)
     if rank == 0 and world == 1 and args.cpu_baseline:
         log(f"CPU baseline on {cpu_threads(args.cpu_threads)} threads")
         cb, rgb_o = cpu_baseline(cfg, w.params_cpu if cfg.mode == "3d" else w.params_cpu[0], w.V, w.K,

@@ -74,9 +74,10 @@ def test_bench_args_defaults():
     assert a.capacity == "bounded" and a.graph == -1
     assert bench.cpu_threads(3) == 3 and bench.cpu_threads(0) >= 1
     assert a.split == 1
-    # config 4 (2D) defaults to the frame-owner layout; frames is a 2D-only layout
-    assert bench.parse(["--config", "4"]).shard == "frames"
-    assert bench.parse(["--config", "4", "--shard", "units"]).shard == "units"
+    # config 4 (2D) defaults to the round-robin layout with its all-reduce;
+    # frames is a 2D-only layout
+    assert bench.parse(["--config", "4"]).shard == "units"
+    assert bench.parse(["--config", "4", "--shard", "frames"]).shard == "frames"
     import pytest
     with pytest.raises(SystemExit):
         bench.parse(["--config", "3", "--shard", "frames"])
@@ -96,3 +97,82 @@ def test_gpus_without_launcher_spawns_ranks(monkeypatch):
     with pytest.raises(SystemExit) as e:
         bench.main(["--gpus", "2"])
     assert "WORLD_SIZE=4" in str(e.value.code)
+
+
+def _layout_worker(rank, world, port, q):
+    """One rank of a gloo rehearsal of bench.measure_layout with a CPU stand-in workload whose
+    step all-reduces its gradient (the host logic only: timing brackets, max over ranks, the
+    per-layout collective timing, the JSON keys)."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gsr.scenes import CONFIGS
+
+        class FakeWorkload:
+            def __init__(self, cfg, dev, world, rank, shard, buckets, loss, comm, view_cost, exchange):
+                self.params = torch.zeros(64, 14)
+                self.owned = shard == "frames"
+                self.units_total = cfg.views * (world if shard == "views" else 1) * (8 if cfg.mode == "2d" else 1)
+                self.scaling = "weak" if shard == "views" else "strong"
+                self.layout = f"fake {shard}"
+
+            def step(self):
+                if not self.owned:
+                    g = torch.ones_like(self.params)
+                    dist.all_reduce(g)
+
+        def timer(w, steps, warmup, dist_, graph=False):
+            for _ in range(warmup):
+                w.step()
+            dist_.barrier()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                w.step()
+            dist_.barrier()
+            return time.perf_counter() - t0, {}, None, (0.0, 0)
+
+        import time
+        args = bench.parse(["--steps", "3", "--warmup", "1"])
+        res = {}
+        for idx in (3, 4):
+            cfg = CONFIGS[idx]
+            shard = bench.parse(["--config", str(idx)]).shard
+            for sh in bench.other_layouts(cfg, shard):
+                res[(idx, bench.LAYOUT_KEY[sh])] = bench.measure_layout(cfg, args, "cpu", world, rank, sh, dist,
+                                                                        make_workload=FakeWorkload, timer=timer)
+        if rank == 0:
+            q.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_other_layouts_reported_gloo_world2():
+    """at N > 1 one bench.py run reports config 3's weak (default) AND strong
+    layouts, and config 4's round-robin all-reduce layout (default) AND the frame owners, each
+    with its own value and collective timing -- rehearsed with two gloo ranks on the CPU."""
+    import multiprocessing as mp
+    import socket
+    from gsr.scenes import CONFIGS
+    assert bench.parse(["--config", "4"]).shard == "units"   # the all-reduce layout is the default
+    assert bench.other_layouts(CONFIGS[3], "views") == ["units"]
+    assert bench.other_layouts(CONFIGS[4], "units") == ["frames"]
+    assert bench.other_layouts(CONFIGS[2], "views") == []
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_layout_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    strong = res[(3, "strong")]
+    assert strong["scaling"] == "strong" and strong["value"] > 0 and strong["allreduce_ms"] is not None
+    assert strong["units_per_step"] == CONFIGS[3].views
+    owners = res[(4, "frame_owners")]
+    assert owners["value"] > 0 and owners["allreduce_ms"] is None   # no Gaussian-gradient collective
+    assert set(strong) >= {"value", "ms_per_step", "allreduce_ms", "parallelism", "scaling"}
