@@ -76,8 +76,12 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
-    ap.add_argument("--exchange", default="dense", choices=["dense", "sparse"],
-                    help="--shard units (3D): all-reduce the dense gradient in async buckets, or exchange only "
+    ap.add_argument("--exchange", default="rows", choices=["rows", "dense", "sparse"],
+                    help="--shard units (3D): 'rows' (default) = the device sparse exchange -- each share's "
+                         "backward writes only its touched gradient rows into a fixed-capacity block, the "
+                         "blocks are all-gathered and summed in rank order on the device (no host read, "
+                         "graph-capturable; gsr.multiview.rows_backward_units); 'dense' = all-reduce the dense "
+                         "gradient in async buckets; 'sparse' = the host-synchronising torch variant (exchange only "
                          "the rows each rank touched (gsr.multiview.sparse_sum)")
     ap.add_argument("--shard", default=None, choices=["units", "views", "frames"],
                     help="3D, N>1: 'views' (default) = a multi-camera batch, every rank renders C views of its own "
@@ -549,7 +553,32 @@ class Workload:
         self.layout = (f"(view, tile-row) units: rank {self.rank} views {self.v0}-{self.v1 - 1} rows {self.band} "
                        f"of {cfg.views}x{self.th}, " +
                        (f"{self.buckets} all-reduce bucket(s) overlapping project_bwd" if self.exchange == "dense" else
+                        "device sparse exchange: touched gradient rows in a fixed-capacity block, all-gathered, "
+                        "summed in rank order" if self.exchange == "rows" else
                         "sparse exchange of the touched gradient rows (all-gather)"))
+        if self.exchange == "rows":
+            self._setup_rows()
+
+    def _render_band_rows(self, p, Vs, Ks, band, gr):
+        cfg, R = self.cfg, self.R
+        return R.render3d(p, Vs, Ks, cfg.width, cfg.height, self.bg, R.RenderOptions3D(band=band, grad_rows=gr))
+
+    def _setup_rows(self):
+        """Row-block capacity of the device sparse exchange: this share's touched rows, measured
+        once with a block that holds every Gaussian, maximised over the ranks (+25 %)."""
+        from gsr.multiview import GradRows, rows_capacity
+        touched = 0
+        if self.v1 > self.v0:
+            probe = GradRows(self.cfg.N, self.dev)
+            p = self.params.detach().requires_grad_(True)
+            rgb, alpha = self._render_band_rows(p, self.Vd[self.v0:self.v1], self.Kd[self.v0:self.v1], self.band, probe)
+            torch.autograd.backward([rgb, alpha], [self.v_rgb_all[self.v0:self.v1], self.v_alpha_all[self.v0:self.v1]])
+            touched = probe.count()
+            del probe
+        self.touched = touched
+        self.grad_rows = GradRows(rows_capacity(touched), self.dev)
+        # --rank-share (no collectives): the scatter-add runs over `world` copies of this block
+        self._gathered = None
 
     def step(self):
         cfg, R = self.cfg, self.R
@@ -577,6 +606,9 @@ class Workload:
             return
         if self.loss != "none":
             self._loss_step()
+            return
+        if self.scaling == "strong" and self.exchange == "rows":
+            self._rows_step()
             return
         if self.v1 <= self.v0:
             if self.comm:
@@ -622,6 +654,34 @@ class Workload:
         rgb, alpha = R.render3d(self.params, self.Vd[self.v0:self.v1], self.Kd[self.v0:self.v1], cfg.width,
                                 cfg.height, self.bg, opts)
         torch.autograd.backward([rgb, alpha], [self.v_rgb_all[self.v0:self.v1], self.v_alpha_all[self.v0:self.v1]])
+
+    def _rows_step(self):
+        """Strong layout with the device sparse exchange (gsr.multiview.rows_backward_units).
+        Without collectives (--rank-share) the share's own work is timed: its render + backward
+        into the row block, then the zero-fill + rank-ordered scatter-add over `world` blocks of
+        this block's size (the gathered blocks stand in for the all-gather's output)."""
+        from gsr import _lib
+        from gsr.multiview import rows_backward_units
+        if self.comm:
+            self.params.grad = rows_backward_units(self._render_band_rows, self.params, self.Vd, self.Kd,
+                                                   self.v_rgb_all, self.v_alpha_all, self.th, self.grad_rows,
+                                                   self.weights, view_cost=self.view_cost,
+                                                   status=self.R._status_buf(self.dev))
+            return
+        if self.v1 > self.v0:
+            p = self.params.detach().requires_grad_(True)
+            rgb, alpha = self._render_band_rows(p, self.Vd[self.v0:self.v1], self.Kd[self.v0:self.v1], self.band,
+                                                self.grad_rows)
+            torch.autograd.backward([rgb, alpha], [self.v_rgb_all[self.v0:self.v1], self.v_alpha_all[self.v0:self.v1]])
+        if self._gathered is None:
+            self._gathered = self.grad_rows.block[None].repeat(self.world, 1, 1)
+        self._gathered[0].copy_(self.grad_rows.block)
+        out = torch.zeros(self.cfg.N, 14, device=self.dev)
+        L = _lib.lib()
+        _lib.check(L.gsr_rows_scatter_add(self._gathered.data_ptr(), self.world, self.grad_rows.cap, out.data_ptr(),
+                                          self.cfg.N, None, torch.cuda.current_stream(self.dev).cuda_stream),
+                   "gsr_rows_scatter_add")
+        self.params.grad = out
 
     def _split_step(self):
         """--split G: the views in G groups, each group's fwd+bwd on its own stream; the groups'
@@ -866,7 +926,7 @@ def rank_share_report(cfg, args, dev, n: int, weights=None):
     shares = []
     for r in range(n):
         w = Workload(cfg, dev, n, r, args.shard if cfg.mode == "2d" else "units", args.buckets, "none", comm=False,
-                     view_cost=args.view_cost)
+                     view_cost=args.view_cost, exchange=args.exchange)
         if cfg.mode == "3d" and w.scaling == "strong":
             if weights is None:
                 weights = w.weights
@@ -877,11 +937,14 @@ def rank_share_report(cfg, args, dev, n: int, weights=None):
         kern = {k: round(v[0], 4) for k, v in sorted(bd.items())}
         kern_sum = sum(v[0] * v[1] for v in bd.values()) / max(2, min(args.steps, 5))   # per step (breakdown pass)
         touched = None   # Gaussians with a nonzero gradient row in this share (the sparse exchange's rows)
-        if cfg.mode == "3d" and w.params.grad is not None:
+        if cfg.mode == "3d" and getattr(w, "grad_rows", None) is not None:
+            touched = w.grad_rows.count() if w.v1 > w.v0 else 0
+        elif cfg.mode == "3d" and w.params.grad is not None:
             touched = int(w.params.grad.ne(0).any(1).sum())
         shares.append({"rank": r, "ms_per_step": 1000.0 * el / args.steps, "views_here": w.views_here,
                        "layout": w.layout, "kernels_ms": kern, "kernel_sum_ms": kern_sum,
-                       "I": R.last_stats().get("n_isect", 0), "touched_rows": touched})
+                       "I": R.last_stats().get("n_isect", 0), "touched_rows": touched,
+                       "row_cap": w.grad_rows.cap if getattr(w, "grad_rows", None) is not None else None})
         del w
         torch.cuda.empty_cache()
     grad_bytes = cfg.N * (14 if cfg.mode == "3d" else 9) * 4 * (FRAMES_2D if cfg.mode == "2d" else 1)
@@ -893,13 +956,17 @@ def rank_share_report(cfg, args, dev, n: int, weights=None):
     units = cfg.views * (FRAMES_2D if cfg.mode == "2d" else 1)
     sparse = {}
     if cfg.mode == "3d" and all(s["touched_rows"] is not None for s in shares):
-        # gsr.multiview.sparse_sum: all-gather of every rank's touched rows (index + 14 floats),
-        # padded to the longest list: a ring moves (n-1) lists through each rank's link
+        # the sparse exchange: an all-gather of every rank's touched rows (index + 14 floats, 64 B),
+        # padded to one size -- the longest list (sparse_sum) or the common row-block capacity
+        # (the device "rows" exchange: the max over ranks of touched + 25 %) -- a ring moves
+        # (n-1) of them through each rank's link
         kmax = max(s["touched_rows"] for s in shares)
-        sp_bytes = (n - 1) * kmax * (14 * 4 + 8)
+        caps = [s["row_cap"] for s in shares if s.get("row_cap")]
+        kpad = max(caps) + 1 if caps else kmax
+        sp_bytes = (n - 1) * kpad * 64
         sp = sp_bytes / (XGMI_LINK_GBS * 1e9) * 1e3
-        sparse = {"sparse_exchange": f"all-gather of the touched rows (max {kmax} of {cfg.N}, 64 B each), "
-                                     f"{sp_bytes / 1e6:.1f} MB through one {XGMI_LINK_GBS:.0f} GB/s link",
+        sparse = {"sparse_exchange": f"all-gather of the touched rows (max {kmax} of {cfg.N}, padded to {kpad}, "
+                                     f"64 B each), {sp_bytes / 1e6:.1f} MB through one {XGMI_LINK_GBS:.0f} GB/s link",
                   "sparse_exchange_model_ms": sp, "sparse_exchange_7link_ms": sp / 7.0,
                   "projected_ms_per_step_sparse": worst + sp, "projected_value_sparse": units / ((worst + sp) * 1e-3),
                   "projected_ms_per_step_sparse_7link": worst + sp / 7.0,

@@ -92,6 +92,7 @@ extern "C" {
 #define GSR_OVF_SEG 8        /* a list longer than the split sort's geometry (max_seg)       */
 #define GSR_OVF_LAZY 16      /* more lazily sorted tiles than the re-render covers            */
 #define GSR_OVF_UNIT 32      /* a raster backward given another chunk_entries than gsr_bin_offsets */
+#define GSR_OVF_EXCHANGE 64  /* a rank touched more Gaussians than its gradient row block holds */
 
 typedef struct gsr_bin_stats {
   int64_t n_isect;     /* total (Gaussian, tile) intersections I                     */
@@ -138,7 +139,9 @@ int gsr_version(void);
  * gsr3d_project_bwd / gsr2d_project_bwd take the stats (NaN rows on overflow); gsr_bin_sort /
  * gsr_bin_sort_lazy take mutable stats. */
 /* Revision 4: gsr_bin_stats.n_sort_long (in the former reserved words; size unchanged). */
-#define GSR_ABI_VERSION 4
+/* Revision 5: the sparse gradient row blocks (gsr3d_touched_rows, gsr3d_project_bwd_rows,
+ * gsr_rows_scatter_add, GSR_OVF_EXCHANGE). */
+#define GSR_ABI_VERSION 5
 int gsr_abi_version(void);
 const char* gsr_last_error(void);
 
@@ -377,6 +380,40 @@ int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride,
                       const int32_t* isect_offset, const int32_t* isect_count,
                       const uint64_t* tile_cut, const float* partial, int64_t n_begin,
                       int64_t n_end, const gsr_bin_stats* stats, float* v_params, void* stream);
+
+/* ---- Sparse gradient rows of a band share (multi-GPU strong layout) ----
+ * A (view, tile-row) share of one multi-view job touches few Gaussians (config 5 at 8 ranks:
+ * 2-12 %; the projection clamps every rect to the band, so the Gaussians with a nonzero
+ * isect_count are exactly the touched ones).  Instead of the dense [N,14] v_params the share's
+ * projection backward writes only their rows, compacted into a caller-owned ROW BLOCK of
+ * cap + 1 rows of GSR_ROW_FLOATS floats:
+ *   row 0      = header {int32 count (may exceed cap: overflow), int32 cap, 0, ...};
+ *   row 1 + i  = {int32 n, 0, v_params[n][0..13]}   for i < min(count, cap), any order.
+ * The blocks of all ranks are all-gathered (one equal-size collective, no host read) and
+ * summed into the dense result in rank order by gsr_rows_scatter_add, so every rank ends
+ * with the same bits.  Each call is stream-ordered and sized by cap: a whole step, exchange
+ * included, can be captured in a HIP graph. */
+#define GSR_ROW_FLOATS 16
+
+/* Zero the header, then list the Gaussians n with isect_count[c*N + n] > 0 for some camera c:
+ * header count := their number, rows 1 + i := {n, 0, 0...} for the first cap of them. */
+int gsr3d_touched_rows(const int32_t* isect_count, int64_t N, int C, int64_t cap, float* block, void* stream);
+
+/* gsr3d_project_bwd for the Gaussians listed in `block` (gsr3d_touched_rows): their 14
+ * gradients go to words 2..15 of their rows (deterministic per row; stats->overflow set: NaN). */
+int gsr3d_project_bwd_rows(const float* params, int64_t N, int64_t row_stride,
+                           const float* viewmats, const float* Ks, int C, int width, int height,
+                           float eps2d, int input_mode, const float* depth, const uint32_t* rect,
+                           const int32_t* isect_offset, const int32_t* isect_count,
+                           const uint64_t* tile_cut, const float* partial, const gsr_bin_stats* stats,
+                           int64_t cap, float* block, void* stream);
+
+/* v_params [N,14] += the rows of `world` gathered blocks (blocks[r] at r * (cap + 1) rows),
+ * rank 0 first (one stream-ordered launch per rank; a block lists an n at most once).  A header
+ * whose count exceeds cap: v_params is written all NaN and *status (device, may be NULL) gets
+ * GSR_OVF_EXCHANGE. */
+int gsr_rows_scatter_add(const float* blocks, int world, int64_t cap, float* v_params, int64_t N,
+                         int32_t* status, void* stream);
 
 /* 2D: v_params [F,N,9] (fully overwritten): set f's gradient sums the partial rows of all its
  * cameras (set_begin as in gsr2d_project_fwd, NULL: F = 1) in camera order, then chains

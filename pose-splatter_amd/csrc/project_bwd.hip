@@ -12,6 +12,9 @@
 //   R(q) with q re-normalised (gsplat) after the adapter's q/(|q|+1e-8)
 //   scales = exp, colours clamp(0,1) (pass-through on [0,1] inclusive), opacity sigmoid.
 // 2D chain: (a,b,c)(theta, ia, ib), ia = 1/(2 sx^2 + 1e-8), sx = exp(ls).
+#include <algorithm>
+#include <cstdint>
+
 #include "project_math.h"
 
 namespace gsr {
@@ -69,6 +72,9 @@ constexpr int kContrib = 16;   // v_m[3], V_M[9], v_col[3], v_op
 #ifndef GSR_PBWD_MINB
 #define GSR_PBWD_MINB 5
 #endif
+// ROWS: the Gaussians are those listed in a row block (gsr3d_touched_rows; row 1 + i holds n)
+// and the gradients go to their rows instead of v_params (the sparse exchange of a band share).
+template <bool ROWS>
 __global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
     const float* __restrict__ params, int64_t N, int64_t stride, const float* __restrict__ viewmats,
     const float* __restrict__ Ks, int C, int W, int H, float eps2d, int input_mode, int tw, int th,
@@ -76,17 +82,27 @@ __global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
     const int32_t* __restrict__ isect_offset, const int32_t* __restrict__ isect_count,
     const float* __restrict__ depth, const uint64_t* __restrict__ tile_cut, const float* __restrict__ partial,
     int CPB, int G, int64_t n_begin, int64_t n_end, const gsr_bin_stats* __restrict__ stats,
-    float* __restrict__ v_params) {
+    float* __restrict__ v_params, float* __restrict__ block, int64_t cap) {
   __shared__ float s_con[kBwdThreads][kContrib + 1];
   __shared__ int s_any[kBwdThreads];
   const int g_loc = threadIdx.x % G;
   const int slot = threadIdx.x / G;
-  const int64_t n = n_begin + (int64_t)blockIdx.x * G + g_loc;
+  const int64_t i_row = (int64_t)blockIdx.x * G + g_loc;   // ROWS: the row of this Gaussian
+  int64_t n;
+  bool listed = true;
+  if constexpr (ROWS) {
+    const int64_t count = min((int64_t)reinterpret_cast<const int32_t*>(block)[0], cap);
+    listed = i_row < count;
+    n = listed ? reinterpret_cast<const int32_t*>(block)[(1 + i_row) * GSR_ROW_FLOATS] : 0;
+  } else {
+    n = n_begin + i_row;
+    listed = n < n_end;
+  }
   // the forward's bounds did not hold: NaN rows, and no partial row is read (their offsets may
   // lie past the buffers).  The flag loads with the first gathers and is tested inside the
   // camera loop, so it adds no round trip of its own.
   const bool ovf = stats != nullptr && stats->overflow != 0;
-  const bool active = slot < CPB && n < n_end;
+  const bool active = slot < CPB && listed;
   const int T = tw * th;
   float v_m[3] = {0.f, 0.f, 0.f};
   float v_M[9];
@@ -220,7 +236,7 @@ __global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
     s_any[threadIdx.x] = any;
   }
   __syncthreads();
-  if (slot != 0 || n >= n_end) return;
+  if (slot != 0 || !listed) return;
   any = 0;
   for (int sl = 1; sl < CPB; ++sl) {
     const float* d = s_con[sl * G + g_loc];
@@ -232,7 +248,7 @@ __global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
     any |= s_any[sl * G + g_loc];
   }
   any |= s_any[threadIdx.x];
-  float* out = v_params + n * 14;
+  float* out = ROWS ? block + (1 + i_row) * GSR_ROW_FLOATS + 2 : v_params + n * 14;
   if (ovf) {
 #pragma unroll
     for (int k = 0; k < 14; ++k) out[k] = __builtin_nanf("");
@@ -290,6 +306,64 @@ __global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
 #pragma unroll
   for (int k = 0; k < 3; ++k) out[10 + k] = (a.craw[k] >= 0.f && a.craw[k] <= 1.f) ? v_col[k] : 0.f;
   out[13] = v_op * a.op * (1.f - a.op);
+}
+
+// The Gaussians of a band share: n with a nonzero rect in any camera.  One returning atomic
+// per wave claims the wave's rows (positions follow arrival order; the exchange's sum is
+// per row, so the order does not change a bit of the result).
+__global__ __launch_bounds__(kBwdThreads) void k_touched_rows(const int32_t* __restrict__ isect_count, int64_t N,
+                                                              int C, int64_t cap, float* __restrict__ block) {
+  const int64_t n = (int64_t)blockIdx.x * kBwdThreads + threadIdx.x;
+  bool any = false;
+  if (n < N)
+    for (int c = 0; c < C; ++c) any |= isect_count[(int64_t)c * N + n] > 0;
+  const unsigned long long m = __ballot(any);
+  const int lane = threadIdx.x & 63;
+  int base = 0;
+  if (lane == 0 && m) base = atomicAdd(reinterpret_cast<int32_t*>(block), __popcll(m));
+  base = __builtin_amdgcn_readfirstlane(base);
+  if (any) {
+    const int64_t i = base + __popcll(m & ((1ull << lane) - 1ull));
+    if (i < cap) {
+      int32_t* row = reinterpret_cast<int32_t*>(block + (1 + i) * GSR_ROW_FLOATS);
+      row[0] = (int32_t)n;
+      row[1] = 0;
+    }
+  }
+}
+
+__global__ void k_rows_header(float* __restrict__ block, int64_t cap) {
+  int32_t* h = reinterpret_cast<int32_t*>(block);
+  if (threadIdx.x < GSR_ROW_FLOATS) h[threadIdx.x] = threadIdx.x == 1 ? (int32_t)min<int64_t>(cap, INT32_MAX) : 0;
+}
+
+// v_params += rank r's rows (a rank lists an n once: plain read-add-writes, no atomics; the
+// ranks follow in launch order, so every rank sums in the same order).  Any header over its
+// cap: the exchange lost rows, so the result is NaN and the sticky status says why.
+__global__ __launch_bounds__(kBwdThreads) void k_rows_scatter_add(const float* __restrict__ blocks, int world,
+                                                                  int64_t cap, int r, float* __restrict__ v_params,
+                                                                  int64_t N, int32_t* __restrict__ status) {
+  bool bad = false;
+  for (int q = 0; q < world; ++q) bad |= reinterpret_cast<const int32_t*>(blocks + (int64_t)q * (cap + 1) * GSR_ROW_FLOATS)[0] > cap;
+  const int64_t i = (int64_t)blockIdx.x * kBwdThreads + threadIdx.x;
+  if (bad) {
+    if (r == 0) {
+      for (int64_t k = i; k < N * 14; k += (int64_t)gridDim.x * kBwdThreads) v_params[k] = __builtin_nanf("");
+      if (i == 0 && status != nullptr) atomicOr(status, GSR_OVF_EXCHANGE);
+    }
+    return;
+  }
+  const float* blk = blocks + (int64_t)r * (cap + 1) * GSR_ROW_FLOATS;
+  const int64_t count = reinterpret_cast<const int32_t*>(blk)[0];
+  if (i >= count) return;
+  const float4* row = reinterpret_cast<const float4*>(blk + (1 + i) * GSR_ROW_FLOATS);
+  const float4 a = row[0], b = row[1], c = row[2], d = row[3];
+  const int64_t n = __float_as_int(a.x);
+  if (n < 0 || n >= N) return;
+  float* o = v_params + n * 14;
+  const float g[14] = {a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+#pragma unroll
+  for (int k = 0; k < 14; ++k) o[k] += g[k];
 }
 
 // The 2D chain of one (set f, Gaussian n) from its camera-summed partials.
@@ -447,10 +521,61 @@ int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride, const 
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   const int CPB = C < kBwdThreads ? C : kBwdThreads;   // camera slots per Gaussian
   const int G = kBwdThreads / CPB;                       // Gaussians per workgroup
-  hipLaunchKernelGGL(k_project3d_bwd, dim3(ceil_div(n_end - n_begin, G)), dim3(kBwdThreads), 0, (hipStream_t)stream, params, N,
-                     row_stride, viewmats, Ks, C, width, height, eps2d, input_mode, tw, th, (const uint2*)rect,
-                     isect_offset, isect_count, depth, tile_cut, partial, CPB, G, n_begin, n_end, stats, v_params);
+  hipLaunchKernelGGL(k_project3d_bwd<false>, dim3(ceil_div(n_end - n_begin, G)), dim3(kBwdThreads), 0,
+                     (hipStream_t)stream, params, N, row_stride, viewmats, Ks, C, width, height, eps2d, input_mode, tw,
+                     th, (const uint2*)rect, isect_offset, isect_count, depth, tile_cut, partial, CPB, G, n_begin,
+                     n_end, stats, v_params, nullptr, (int64_t)0);
   GSR_LAUNCH_CHECK("k_project3d_bwd");
+  return GSR_OK;
+}
+
+int gsr3d_touched_rows(const int32_t* isect_count, int64_t N, int C, int64_t cap, float* block, void* stream) {
+  GSR_REQUIRE(N >= 0 && C >= 1 && cap >= 0 && block != nullptr, "gsr3d_touched_rows: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_rows_header, dim3(1), dim3(64), 0, s, block, cap);
+  GSR_LAUNCH_CHECK("k_rows_header");
+  if (N == 0) return GSR_OK;
+  hipLaunchKernelGGL(k_touched_rows, dim3(ceil_div(N, kBwdThreads)), dim3(kBwdThreads), 0, s, isect_count, N, C, cap,
+                     block);
+  GSR_LAUNCH_CHECK("k_touched_rows");
+  return GSR_OK;
+}
+
+int gsr3d_project_bwd_rows(const float* params, int64_t N, int64_t row_stride, const float* viewmats, const float* Ks,
+                           int C, int width, int height, float eps2d, int input_mode, const float* depth,
+                           const uint32_t* rect, const int32_t* isect_offset, const int32_t* isect_count,
+                           const uint64_t* tile_cut, const float* partial, const gsr_bin_stats* stats, int64_t cap,
+                           float* block, void* stream) {
+  GSR_REQUIRE(N >= 0 && C >= 1 && width > 0 && height > 0 && cap >= 0 && block != nullptr,
+              "gsr3d_project_bwd_rows: bad arguments");
+  GSR_REQUIRE(row_stride >= 14, "gsr3d_project_bwd_rows: row_stride < 14");
+  GSR_REQUIRE(input_mode == GSR_INPUT_ADAPTER || input_mode == GSR_INPUT_GSPLAT,
+              "gsr3d_project_bwd_rows: bad input_mode %d", input_mode);
+  if (N == 0 || cap == 0) return GSR_OK;
+  const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
+  const int CPB = C < kBwdThreads ? C : kBwdThreads;
+  const int G = kBwdThreads / CPB;
+  // the grid covers cap rows; workgroups past the header's count exit at once
+  hipLaunchKernelGGL(k_project3d_bwd<true>, dim3(ceil_div(cap, G)), dim3(kBwdThreads), 0, (hipStream_t)stream, params,
+                     N, row_stride, viewmats, Ks, C, width, height, eps2d, input_mode, tw, th, (const uint2*)rect,
+                     isect_offset, isect_count, depth, tile_cut, partial, CPB, G, (int64_t)0, N, stats,
+                     (float*)nullptr, block, cap);
+  GSR_LAUNCH_CHECK("k_project3d_bwd<rows>");
+  return GSR_OK;
+}
+
+int gsr_rows_scatter_add(const float* blocks, int world, int64_t cap, float* v_params, int64_t N, int32_t* status,
+                         void* stream) {
+  GSR_REQUIRE(blocks != nullptr && v_params != nullptr && world >= 1 && cap >= 0 && N >= 0,
+              "gsr_rows_scatter_add: bad arguments");
+  if (N == 0) return GSR_OK;
+  // the grid covers cap rows and (for the NaN fill) is grid-strided over v_params
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(std::max<int64_t>(cap, 1), kBwdThreads), 1 << 20));
+  for (int r = 0; r < world; ++r) {
+    hipLaunchKernelGGL(k_rows_scatter_add, dim3(grid), dim3(kBwdThreads), 0, (hipStream_t)stream, blocks, world, cap, r,
+                       v_params, N, status);
+    GSR_LAUNCH_CHECK("k_rows_scatter_add");
+  }
   return GSR_OK;
 }
 

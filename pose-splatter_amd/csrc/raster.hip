@@ -365,9 +365,6 @@ extern "C" int gsr_debug_fwd_trace(void* buf) {
 #ifndef GSR_FWD_MINB
 #define GSR_FWD_MINB 6
 #endif
-#ifndef GSR_FWD_PF
-#define GSR_FWD_PF 0
-#endif
 template <bool IS2D, int LPP>
 __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MINB) void k_raster_fwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
@@ -518,68 +515,6 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
         n += __popcll(m);
       }
       __builtin_amdgcn_wave_barrier();
-#if GSR_FWD_PF == 2
-      // Software-pipelined composite: the T-independent head of group g+1 (records, alpha, the
-      // quad prefix products of 1 - alpha) is computed in the same block as the T-dependent
-      // tail of group g, so the in-order wave issues one group's transmittance chain while the
-      // next group's LDS reads and exponential are in flight.  A pixel already done takes no
-      // part (T, colour, last unchanged), as the unpipelined `!done` in `valid` made it.
-      struct Head {
-        float alpha, Q, P, r, g, b;
-        int idx;
-        bool v;
-      };
-      auto head = [&](int k, int idx) {
-        Head hd;
-        const float4 p0 = s_q[buf][0][idx];
-        const float4 p1 = s_q[buf][1][idx];
-        const float4 p2 = s_q[buf][2][idx];
-        const float dx = p0.x - px, dy = p0.y - py;
-        const float sg = conic_sigma(p1, dx, dy);
-        hd.alpha = fminf(kAlphaMax, p0.z * __expf(-sg));
-        hd.v = k < n && sg >= 0.f && hd.alpha >= kAlphaThreshold;
-        PG::prefix(hd.v ? 1.f - hd.alpha : 1.f, q, hd.Q, hd.P);
-        hd.r = p2.x;
-        hd.g = p2.y;
-        hd.b = p2.z;
-        hd.idx = idx;
-        return hd;
-      };
-      int idx_next = s_l[wv][q + LPP < n ? q + LPP : max(n - 1, 0)];
-      Head cur = head(q, s_l[wv][q < n ? q : max(n - 1, 0)]);
-      for (int k0 = 0; k0 < n; k0 += LPP) {
-        const Head hd = cur;
-        cur = head(k0 + LPP + q, idx_next);   // past the list: read, never used
-        idx_next = s_l[wv][k0 + 2 * LPP + q < n ? k0 + 2 * LPP + q : n - 1];
-        const float nT = T * hd.Q;
-        const int fs = PG::min_i(hd.v && nT <= kTMin ? q : LPP);
-        const bool con = !done && hd.v && q < fs;
-        const float vis = con ? hd.alpha * (T * hd.P) : 0.f;
-        dr += hd.r * vis;
-        dg += hd.g * vis;
-        db += hd.b * vis;
-        lastq = con ? hd.idx : lastq;
-        const float Tn = __int_as_float(PG::min_i(__float_as_int(q < fs ? nT : T)));
-        T = done ? T : Tn;
-        done = done || fs < LPP;
-      }
-#else
-#if GSR_FWD_PF == 1
-      // the next group's records are read one group ahead, its queue slot two ahead: no LDS
-      // round trip on the serial chain of a group (the heavy tiles' walks are that chain)
-      int idx_pf = s_l[wv][q < n ? q : max(n - 1, 0)];
-      float4 f0 = s_q[buf][0][idx_pf], f1 = s_q[buf][1][idx_pf];
-      int idx_next = s_l[wv][q + LPP < n ? q + LPP : max(n - 1, 0)];
-      for (int k0 = 0; k0 < n; k0 += LPP) {
-        const int k = k0 + q;
-        const int idx = idx_pf;
-        const float4 p0 = f0, p1 = f1;
-        const float4 p2 = s_q[buf][2][idx];
-        idx_pf = idx_next;
-        f0 = s_q[buf][0][idx_pf];
-        f1 = s_q[buf][1][idx_pf];
-        idx_next = s_l[wv][k + 2 * LPP < n ? k + 2 * LPP : n - 1];
-#else
       // the next group's queue slot is read one group ahead (one LDS round trip less on the
       // serial chain of a group)
       int idx_next = s_l[wv][q < n ? q : max(n - 1, 0)];
@@ -590,7 +525,6 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
         const float4 p0 = s_q[buf][0][idx];
         const float4 p1 = s_q[buf][1][idx];
         const float4 p2 = s_q[buf][2][idx];
-#endif
         const float dx = p0.x - px, dy = p0.y - py;
         const float sg = conic_sigma(p1, dx, dy);
         const float raw = p0.z * __expf(-sg);
@@ -614,7 +548,6 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
         T = __int_as_float(PG::min_i(__float_as_int((IS2D ? q <= fs : q < fs) ? nT : T)));
         done = done || fs < LPP;
       }
-#endif  // GSR_FWD_PF == 2
       if (lastq >= 0) {   // the entry index of this lane's latest composite, once per half
         last = rb + s_qe[buf][lastq];
         lastq = -1;

@@ -26,12 +26,14 @@ ORDER_INDEX = 1
 INPUT_ADAPTER = 0
 INPUT_GSPLAT = 1
 
-ABI_VERSION = 4   # include/gsr.h GSR_ABI_VERSION this binding is written for
+ABI_VERSION = 5   # include/gsr.h GSR_ABI_VERSION this binding is written for
 
 # stats->overflow bits of a capacity-bounded call (include/gsr.h GSR_OVF_*)
 OVF_BITS = {1: "intersections > isect cap", 2: "chunks > chunk cap", 4: "busy tiles > n_busy bound",
             8: "list longer than the split sort's max_seg", 16: "lazily sorted tiles > n_lazy_max bound",
-            32: "raster backward chunk_entries differs from the forward's"}
+            32: "raster backward chunk_entries differs from the forward's",
+            64: "a rank touched more Gaussians than its gradient row block holds"}
+ROW_FLOATS = 16   # GSR_ROW_FLOATS: floats per row of a sparse gradient row block
 
 GSR_EINVAL = -1
 GSR_ELAUNCH = -2
@@ -112,6 +114,10 @@ EXPORTS = {
                                         _P, _P, _P, _P, _P, _P]),
     "gsr3d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _I32, _I32, _I32, _F, _I32, _P, _P,
                                          _P, _P, _P, _P, _I64, _I64, _P, _P, _P]),
+    "gsr3d_touched_rows": (ctypes.c_int, [_P, _I64, _I32, _I64, _P, _P]),
+    "gsr3d_project_bwd_rows": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _I32, _I32, _I32, _F, _I32, _P, _P,
+                                              _P, _P, _P, _P, _P, _I64, _P, _P]),
+    "gsr_rows_scatter_add": (ctypes.c_int, [_P, _I32, _I64, _P, _I64, _P, _P]),
     "gsr2d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P,
                                          _P, _P, _P]),
     "gsr_loss_workspace": (_SZ, [_I32, _I32, _I32]),

@@ -21,6 +21,13 @@ code at all; this is the MI355X design, not a translation.
   rank renders all its units in ONE batched launch sequence per frame bucket
   (``gsr.render.render2d_units``) and the [F,N,9] gradient is all-reduced per frame bucket
   (async, overlapping the next bucket's render).
+* ``GradRows`` / ``rows_backward_units`` — the strong layout's SPARSE exchange on the device:
+  the share's backward writes only the gradient rows of the Gaussians it touched into a
+  fixed-capacity row block (no dense [N,14] write), the blocks are all-gathered (one
+  equal-size collective, no host read of counts) and ``gsr_rows_scatter_add`` sums them into
+  the dense gradient in rank order -- the same bits on every rank.  Capacity overflow is
+  caught on the device (NaN gradient + GSR_OVF_EXCHANGE in the sticky status).  Nothing in
+  the step waits on the host, so it can be captured in a HIP graph with RCCL.
 * ``frame_owner_units`` / ``owned_backward_frames`` — config 4 in the frame-owner layout: frame
   f with all its views goes to rank f % world.  Frames have disjoint Gaussian sets, so every
   frame's gradient is complete on its owner: no Gaussian-gradient exchange at all (optionally an
@@ -34,7 +41,7 @@ import torch
 import torch.distributed as dist
 
 __all__ = ["view_shard", "sharded_backward", "band_shard", "row_work", "unit_bounds", "unit_shard",
-           "sharded_backward_units",
+           "sharded_backward_units", "GradRows", "rows_backward_units", "rows_capacity",
            "frame_view_units", "frame_buckets", "sharded_backward_frames", "bucket_bounds",
            "frame_owner_units", "owned_backward_frames", "sparse_sum"]
 
@@ -260,6 +267,72 @@ def sharded_backward_units(render_band: Callable, params: torch.Tensor, viewmats
     if world > 1:
         dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=group)
     return grad
+
+
+class GradRows:
+    """A device row block of ``cap`` sparse gradient rows (include/gsr.h GSR_ROW_FLOATS layout:
+    row 0 = header {count, cap}, row 1 + i = {n, 0, v_params[n][0..13]}), written by a band
+    render's backward when passed as ``RenderOptions3D(grad_rows=...)``."""
+
+    def __init__(self, cap: int, device):
+        from . import _lib
+        self.cap = int(cap)
+        self.block = torch.zeros(self.cap + 1, _lib.ROW_FLOATS, device=device, dtype=torch.float32)
+
+    def count(self) -> int:
+        """Rows the last backward listed (a host read: diagnostics and capacity sizing only)."""
+        return int(self.block[0].view(torch.int32)[0])
+
+
+def rows_capacity(touched: int, group=None, margin: float = 1.25, slack: int = 1024) -> int:
+    """One capacity for every rank's row block (the all-gather needs equal sizes): the largest
+    touched-row count over the ranks (one host read, at setup) plus a margin."""
+    t = torch.tensor([int(touched)], dtype=torch.int64)
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        if dist.get_backend(group) == "nccl":
+            t = t.cuda()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(int(t) * margin) + slack
+
+
+def rows_backward_units(render_band_rows: Callable, params: torch.Tensor, viewmats: torch.Tensor,
+                        Ks: torch.Tensor, v_rgb: torch.Tensor, v_alpha: torch.Tensor, rows: int,
+                        grad_rows: GradRows, weights=None, group=None, view_cost: float = 0.0,
+                        status: torch.Tensor | None = None) -> torch.Tensor:
+    """Gradient of sum(rgb*v_rgb + alpha*v_alpha) over all C views, (view, row)-unit sharded,
+    with the device sparse exchange.  ``render_band_rows(p, viewmats_sub, Ks_sub, band, grad_rows)``
+    renders views v0..v1-1 binned to ``band`` with ``RenderOptions3D(grad_rows=grad_rows)``;
+    its backward leaves the touched rows in ``grad_rows.block``.  The blocks of all ranks are
+    all-gathered and summed in rank order (``gsr_rows_scatter_add``): identical bits on every
+    rank, no host synchronisation (a rank with more touched rows than the capacity makes the
+    result NaN and sets GSR_OVF_EXCHANGE in ``status``)."""
+    from . import _lib
+    L = _lib.lib()
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    v0, v1, band = unit_shard(viewmats.shape[0], rows, world, rank, weights, view_cost)
+    dev = params.device
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    p = params.detach().requires_grad_(True)
+    if v1 > v0:
+        rgb, alpha = render_band_rows(p, viewmats[v0:v1], Ks[v0:v1], band, grad_rows)
+        torch.autograd.backward([rgb, alpha], [v_rgb[v0:v1], v_alpha[v0:v1]])
+    else:   # an empty share: a header with no rows
+        _lib.check(L.gsr3d_touched_rows(None, 0, 1, grad_rows.cap, grad_rows.block.data_ptr(), stream),
+                   "gsr3d_touched_rows")
+    blk = grad_rows.block
+    if world > 1:
+        gathered = torch.empty((world,) + tuple(blk.shape), device=dev, dtype=blk.dtype)
+        if dist.get_backend(group) == "nccl":
+            dist.all_gather_into_tensor(gathered, blk, group=group)
+        else:
+            dist.all_gather(list(gathered.unbind(0)), blk, group=group)
+    else:
+        gathered = blk[None]
+    out = torch.zeros(params.shape[0], 14, device=dev, dtype=torch.float32)
+    _lib.check(L.gsr_rows_scatter_add(gathered.data_ptr(), world, grad_rows.cap, out.data_ptr(), params.shape[0],
+                                      None if status is None else status.data_ptr(), stream), "gsr_rows_scatter_add")
+    return out
 
 
 def frame_view_units(F: int, V: int, world: int, rank: int) -> list:

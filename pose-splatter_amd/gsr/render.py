@@ -92,6 +92,10 @@ class RenderOptions3D:
     grad_hook: object = field(default=None, compare=False)
     # "exact" | "bounded" | "auto" | None (the module default, set_capacity_mode)
     capacity: str | None = None
+    # sparse gradient rows (gsr.multiview.GradRows): the backward writes only the rows of the
+    # Gaussians this (band) render touched into grad_rows.block (gsr3d_touched_rows +
+    # gsr3d_project_bwd_rows) and returns no dense gradient (params.grad stays None)
+    grad_rows: object = field(default=None, compare=False)
     # distinguishes calls of one shape whose lists differ (e.g. different view groups rendered
     # concurrently): a bounded call takes its bounds from the previous call with the same tag
     tag: int = 0
@@ -802,6 +806,8 @@ class _Render3D(torch.autograd.Function):
                   "gsr3d_raster_bwd")
         v_params = backward3d(b, ctx.meta, raster)
         _backward_check(b)   # a bounded forward that overflowed raises here, before .grad
+        if v_params is None:   # sparse gradient rows (opts.grad_rows): no dense gradient
+            return None, None, None, None, None, None, None, None
         return v_params.view(ctx.params_shape), None, None, None, None, None, None, None
 
 
@@ -812,6 +818,8 @@ def backward3d(b, meta, raster) -> torch.Tensor:
     p, stride, V, Kc, bgc, width, height, opts = meta
     stream = _stream(p.device)
     C, N = b.C, b.N
+    if opts.grad_rows is not None:
+        return _backward3d_rows(L, b, meta, raster, stream)
     v_params = torch.empty(N, 14, device=p.device, dtype=torch.float32)
     if N > 0:
         partial = torch.empty(max(b.n_isect, 1) * _lib.PARTIAL_STRIDE, device=p.device, dtype=torch.float32)
@@ -832,6 +840,28 @@ def backward3d(b, meta, raster) -> torch.Tensor:
     elif opts.grad_hook is not None:
         opts.grad_hook(v_params)
     return v_params
+
+
+def _backward3d_rows(L, b, meta, raster, stream) -> None:
+    """The backward of a band share whose gradient leaves as sparse rows (opts.grad_rows, a
+    gsr.multiview.GradRows): list the Gaussians the share touched, run the raster backward, and
+    chain only their partial rows into the row block -- no dense [N,14] write."""
+    p, stride, V, Kc, bgc, width, height, opts = meta
+    rows = opts.grad_rows
+    C, N = b.C, b.N
+    q = b.p
+    check(L.gsr3d_touched_rows(q["cnt"], N, C, rows.cap, rows.block.data_ptr(), stream), "gsr3d_touched_rows")
+    if N == 0:
+        return None
+    partial = torch.empty(max(b.n_isect, 1) * _lib.PARTIAL_STRIDE, device=p.device, dtype=torch.float32)
+    with _timed("raster3d_bwd"):
+        raster(L, q, partial, stream)
+    with _timed("project3d_bwd"):
+        check(L.gsr3d_project_bwd_rows(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height, opts.eps2d,
+                                       opts.input_mode, q["depth"], q["rect"], q["isect_off"], q["cnt"],
+                                       q["tile_cut"], _ptr(partial), q["stats_dev"], rows.cap,
+                                       rows.block.data_ptr(), stream), "gsr3d_project_bwd_rows")
+    return None
 
 
 class _Render2D(torch.autograd.Function):

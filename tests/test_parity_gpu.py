@@ -85,7 +85,9 @@ def _scene3d(N, W, H, C, seed, extent=0.11, scale_shift=0.0):
 
 def _run_gpu3d(p, V, K, W, H, bg, cuda, v_rgb=None, v_alpha=None, radius_mode="opacity_aabb"):
     from src.gaussian_renderer import GaussianRenderer3D
-    r = GaussianRenderer3D(W, H, device="cuda", radius_mode=radius_mode)
+    # exact capacity: these tests change scenes within one shape (the drop-in's "auto" default
+    # would size a later call from an earlier, smaller one and raise; tests/test_headline_mode_gpu.py)
+    r = GaussianRenderer3D(W, H, device="cuda", radius_mode=radius_mode, capacity="exact")
     r.set_background_color(bg.to(cuda))
     pg = p.to(cuda).requires_grad_(True)
     rgb, alpha = r.render(pg, V.to(cuda), K.to(cuda))
@@ -341,7 +343,7 @@ GOLDEN_2D = ["n1_64x48_black", "n2_64x48_white", "n40_64x48_white", "n40_96x80_g
 
 def _run_gpu2d(p, W, H, bg, cuda, v_rgb=None, v_alpha=None):
     from src.gaussian_renderer import GaussianRenderer2D
-    r = GaussianRenderer2D(W, H, device="cuda")
+    r = GaussianRenderer2D(W, H, device="cuda", capacity="exact")
     r.set_background_color(bg.to(cuda))
     pg = p.to(cuda).requires_grad_(True)
     rgb, alpha = r.render(pg, None, None)
