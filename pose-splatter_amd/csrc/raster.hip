@@ -355,8 +355,17 @@ extern "C" int gsr_debug_fwd_trace(void* buf) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_fwd_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
 }
 #define FWD_T(i) if (threadIdx.x == 0) s_ftr[i] = wall_clock64()
+// per-round phase accumulators of wave 0 (3D quad layout): 0 gather wait + quadrant cull,
+// 1 round barrier, 2 box culls, 3 composites
+#define FWD_P(k)                                          \
+  if (threadIdx.x == 0) {                                 \
+    const unsigned long long now_ = wall_clock64();       \
+    f_acc[k] += now_ - f_t;                               \
+    f_t = now_;                                           \
+  }
 #else
 #define FWD_T(i)
+#define FWD_P(k)
 #endif
 // minimum workgroups per CU of the 3D quad-layout raster forward (build knob for measurements):
 // 6 fit 25.9 KB of LDS (queue entry offsets as bytes) and 79 VGPRs without spills -- config 3
@@ -380,6 +389,8 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
 #ifdef GSR_FWD_TRACE
   __shared__ unsigned long long s_ftr[4];
   int n_rounds = 0;
+  unsigned long long f_acc[4] = {0ull, 0ull, 0ull, 0ull}, f_t = wall_clock64();
+  unsigned long long f_groups = 0, f_surv = 0;
   FWD_T(0);
 #endif
   // n_busy sizes the grid (the read-back busy count or a bound); the tiles come from the device
@@ -467,6 +478,9 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
   }
   int buf = 0;
   for (int rb = start; rb < end; rb += 256, buf ^= 1) {
+#ifdef GSR_FWD_TRACE
+    if (threadIdx.x == 0) f_t = wall_clock64();
+#endif
     {
       const int e = rb + 64 * wv + lane;
       const bool keep = e < end && cull_keep<IS2D>(c0, c1, c2, qx0, qx1, qy0, qy1);
@@ -485,7 +499,9 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
       const Splat sn = rec[id_use];
       c0 = sn.p0; c1 = sn.p1; c2 = sn.p2;
     }
+    FWD_P(0);
     if (__syncthreads_count(!done) == 0) break;
+    FWD_P(1);
 #ifdef GSR_FWD_TRACE
     if (n_rounds++ == 0) FWD_T(1);
 #endif
@@ -515,6 +531,11 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
         n += __popcll(m);
       }
       __builtin_amdgcn_wave_barrier();
+      FWD_P(2);
+#ifdef GSR_FWD_TRACE
+      f_groups += (n + LPP - 1) / LPP;
+      f_surv += n;
+#endif
       // the next group's queue slot is read one group ahead (one LDS round trip less on the
       // serial chain of a group)
       int idx_next = s_l[wv][q < n ? q : max(n - 1, 0)];
@@ -553,6 +574,7 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
         lastq = -1;
       }
       __builtin_amdgcn_wave_barrier();
+      FWD_P(3);
     }
   }
   } else {
@@ -737,11 +759,15 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
 #ifdef GSR_FWD_TRACE
   FWD_T(3);
   if (threadIdx.x == 0 && g_fwd_trace != nullptr) {
-    ulonglong2* d = reinterpret_cast<ulonglong2*>(g_fwd_trace + 8 * (int64_t)blockIdx.x);
+    ulonglong2* d = reinterpret_cast<ulonglong2*>(g_fwd_trace + 16 * (int64_t)blockIdx.x);
     d[0] = make_ulonglong2(s_ftr[0], s_ftr[1]);
     d[1] = make_ulonglong2(s_ftr[2], s_ftr[3]);
     d[2] = make_ulonglong2((unsigned long long)n_rounds, (unsigned long long)(list_end - start));
     d[3] = make_ulonglong2((unsigned long long)__smid(), (unsigned long long)ct);
+    d[4] = make_ulonglong2(f_acc[0], f_acc[1]);
+    d[5] = make_ulonglong2(f_acc[2], f_acc[3]);
+    d[6] = make_ulonglong2(f_groups, f_surv);
+    d[7] = make_ulonglong2(0ull, 0ull);
   }
 #endif
 }

@@ -20,14 +20,14 @@ for _ in range(4):
     w.step()
 torch.cuda.synchronize()
 L = _lib.lib()
-buf = torch.zeros(8 << 17, dtype=torch.int64, device=dev)
+buf = torch.zeros(16 << 17, dtype=torch.int64, device=dev)
 L.gsr_debug_fwd_trace.argtypes = [ctypes.c_void_p]
 assert L.gsr_debug_fwd_trace(buf.data_ptr()) == 0
 for rep in range(2):
     buf.zero_()
     w.step()
     torch.cuda.synchronize()
-    t = buf.view(-1, 8).cpu()
+    t = buf.view(-1, 16).cpu()
     t = t[t[:, 0] != 0].double()
     t0 = t[:, 0].min()
     a, f, wd, e = [(t[:, k] - t0) * 0.01 for k in range(4)]
@@ -46,9 +46,20 @@ for rep in range(2):
           f"epilogue {float(epi.mean()):.2f} (p90 {float(torch.quantile(epi, 0.9)):.2f}) us")
     print(f"   rounds mean {float(rounds.mean()):.1f} max {int(rounds.max())}; us per round {float((walk / rounds.clamp(min=1)).mean()):.2f}")
     order = torch.argsort(d, descending=True)
-    for i in order[:6].tolist():
+    ph = t[:, 8:12] * 0.01   # wave 0's per-phase totals (us): gather+cull, barrier, box culls, composites
+    groups, surv = t[:, 12], t[:, 13]
+    for i in order[:12].tolist():
+        r = max(int(rounds[i]), 1)
         print(f"   WG len {int(ln[i])} rounds {int(rounds[i])} start {float(a[i]):.1f} first {float(first[i]):.1f} "
-              f"walk {float(walk[i]):.1f} epi {float(epi[i]):.1f} end {float(e[i]):.1f}")
+              f"walk {float(walk[i]):.1f} epi {float(epi[i]):.1f} end {float(e[i]):.1f} | per round (us): "
+              f"gather+cull {float(ph[i, 0]) / r:.2f} barrier {float(ph[i, 1]) / r:.2f} "
+              f"boxcull {float(ph[i, 2]) / r:.2f} composite {float(ph[i, 3]) / r:.2f} | wave0 groups/round "
+              f"{float(groups[i]) / r:.1f} survivors/round {float(surv[i]) / r:.1f} "
+              f"ns/group {1000.0 * float(ph[i, 3]) / max(float(groups[i]), 1.0):.0f}")
+    tot = ph.sum(0)
+    print(f"   all WGs, wave 0 phase totals (us): gather+cull {float(tot[0]):.0f} barrier {float(tot[1]):.0f} "
+          f"boxcull {float(tot[2]):.0f} composite {float(tot[3]):.0f}; ns per composite group "
+          f"{1000.0 * float(tot[3]) / max(float(groups.sum()), 1.0):.0f}")
     hist = torch.bincount(rounds.long())
     print("   WGs by rounds:", {i: int(c) for i, c in enumerate(hist.tolist()) if c})
     for thr in (8, 10, 12, 16):
