@@ -76,12 +76,14 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
-    ap.add_argument("--exchange", default="rows", choices=["rows", "dense", "sparse"],
-                    help="--shard units (3D): 'rows' (default) = the device sparse exchange -- each share's "
-                         "backward writes only its touched gradient rows into a fixed-capacity block, the "
-                         "blocks are all-gathered and summed in rank order on the device (no host read, "
-                         "graph-capturable; gsr.multiview.rows_backward_units); 'dense' = all-reduce the dense "
-                         "gradient in async buckets; 'sparse' = the host-synchronising torch variant (exchange only "
+    ap.add_argument("--exchange", default="dense", choices=["dense", "rows", "sparse"],
+                    help="--shard units (3D): 'dense' (default) = all-reduce the dense gradient in async buckets "
+                         "overlapping project_bwd; 'rows' = the device sparse exchange -- each share's backward "
+                         "writes only the gradient rows of the Gaussians it composited into a fixed-capacity "
+                         "block, the blocks are all-gathered and summed in rank order on the device (no host "
+                         "read, graph-capturable; gsr.multiview.rows_backward_units; at config 5, 8 ranks a share "
+                         "composites 17-21 %% of the Gaussians, where it breaks even with the dense all-reduce: "
+                         "DESIGN.md §5); 'sparse' = the host-synchronising torch variant (exchange only "
                          "the rows each rank touched (gsr.multiview.sparse_sum)")
     ap.add_argument("--shard", default=None, choices=["units", "views", "frames"],
                     help="3D, N>1: 'views' (default) = a multi-camera batch, every rank renders C views of its own "

@@ -382,9 +382,9 @@ int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride,
                       int64_t n_end, const gsr_bin_stats* stats, float* v_params, void* stream);
 
 /* ---- Sparse gradient rows of a band share (multi-GPU strong layout) ----
- * A (view, tile-row) share of one multi-view job touches few Gaussians (config 5 at 8 ranks:
- * 2-12 %; the projection clamps every rect to the band, so the Gaussians with a nonzero
- * isect_count are exactly the touched ones).  Instead of the dense [N,14] v_params the share's
+ * A (view, tile-row) share of one multi-view job gives a gradient to few Gaussians (config 5
+ * at 8 ranks: 2-12 %: the band's walks stop early, so most Gaussians that reach its tiles are
+ * never composited).  Instead of the dense [N,14] v_params the share's
  * projection backward writes only their rows, compacted into a caller-owned ROW BLOCK of
  * cap + 1 rows of GSR_ROW_FLOATS floats:
  *   row 0      = header {int32 count (may exceed cap: overflow), int32 cap, 0, ...};
@@ -395,9 +395,14 @@ int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride,
  * included, can be captured in a HIP graph. */
 #define GSR_ROW_FLOATS 16
 
-/* Zero the header, then list the Gaussians n with isect_count[c*N + n] > 0 for some camera c:
- * header count := their number, rows 1 + i := {n, 0, 0...} for the first cap of them. */
-int gsr3d_touched_rows(const int32_t* isect_count, int64_t N, int C, int64_t cap, float* block, void* stream);
+/* After the forward (its finalize set tile_end): zero the header, then list the Gaussians n that
+ * own a list entry before their tile's cut in any of the call's busy tiles (tile_order, the
+ * device busy count in stats; n_busy bounds it) -- exactly those the raster backward gives a
+ * partial row.  header count := their number, rows 1 + i := {n, 0, 0...} for the first cap.
+ * flags: caller workspace of N bytes (rounded up to 4).  N == 0 or n_busy == 0: the header only. */
+int gsr3d_touched_rows(const int32_t* sorted_ids, const int32_t* tile_offset, const int32_t* tile_end,
+                       const int32_t* tile_order, const gsr_bin_stats* stats, int32_t n_busy, int64_t N,
+                       int64_t cap, uint8_t* flags, float* block, void* stream);
 
 /* gsr3d_project_bwd for the Gaussians listed in `block` (gsr3d_touched_rows): their 14
  * gradients go to words 2..15 of their rows (deterministic per row; stats->overflow set: NaN). */

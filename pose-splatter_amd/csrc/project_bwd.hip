@@ -308,15 +308,29 @@ __global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
   out[13] = v_op * a.op * (1.f - a.op);
 }
 
-// The Gaussians of a band share: n with a nonzero rect in any camera.  One returning atomic
-// per wave claims the wave's rows (positions follow arrival order; the exchange's sum is
-// per row, so the order does not change a bit of the result).
-__global__ __launch_bounds__(kBwdThreads) void k_touched_rows(const int32_t* __restrict__ isect_count, int64_t N,
-                                                              int C, int64_t cap, float* __restrict__ block) {
+// The Gaussians a band share's backward gives a gradient: those with at least one list entry
+// before its tile's cut (tile_end), i.e. a partial row the raster backward wrote.  (A nonzero
+// rect is not enough: in config 5's dense centre nearly every Gaussian reaches a band's tiles,
+// but the walks stop early and ~11 % of them get a gradient.)  One workgroup per busy tile
+// flags its consumed entries' Gaussians; the flags are then compacted into the row block.
+__global__ __launch_bounds__(kBwdThreads) void k_mark_touched(const int32_t* __restrict__ sorted_ids,
+                                                              const int32_t* __restrict__ tile_offset,
+                                                              const int32_t* __restrict__ tile_end,
+                                                              const int32_t* __restrict__ order,
+                                                              const gsr_bin_stats* __restrict__ stats, int64_t N,
+                                                              uint8_t* __restrict__ flag) {
+  if ((int)blockIdx.x >= stats->n_busy || stats->overflow) return;
+  const int ct = order[blockIdx.x];
+  const int b = tile_offset[ct], e = tile_end[ct];
+  for (int k = b + (int)threadIdx.x; k < e; k += kBwdThreads) flag[sorted_ids[k] % N] = 1;
+}
+
+// One returning atomic per wave claims the wave's rows (positions follow arrival order; the
+// exchange's sum is per row, so the order does not change a bit of the result).
+__global__ __launch_bounds__(kBwdThreads) void k_touched_rows(const uint8_t* __restrict__ flag, int64_t N, int64_t cap,
+                                                              float* __restrict__ block) {
   const int64_t n = (int64_t)blockIdx.x * kBwdThreads + threadIdx.x;
-  bool any = false;
-  if (n < N)
-    for (int c = 0; c < C; ++c) any |= isect_count[(int64_t)c * N + n] > 0;
+  const bool any = n < N && flag[n] != 0;
   const unsigned long long m = __ballot(any);
   const int lane = threadIdx.x & 63;
   int base = 0;
@@ -330,6 +344,10 @@ __global__ __launch_bounds__(kBwdThreads) void k_touched_rows(const int32_t* __r
       row[1] = 0;
     }
   }
+}
+
+__global__ void k_zero_u32(uint32_t* __restrict__ p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0u;
 }
 
 __global__ void k_rows_header(float* __restrict__ block, int64_t cap) {
@@ -529,14 +547,23 @@ int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride, const 
   return GSR_OK;
 }
 
-int gsr3d_touched_rows(const int32_t* isect_count, int64_t N, int C, int64_t cap, float* block, void* stream) {
-  GSR_REQUIRE(N >= 0 && C >= 1 && cap >= 0 && block != nullptr, "gsr3d_touched_rows: bad arguments");
+int gsr3d_touched_rows(const int32_t* sorted_ids, const int32_t* tile_offset, const int32_t* tile_end,
+                       const int32_t* tile_order, const gsr_bin_stats* stats, int32_t n_busy, int64_t N, int64_t cap,
+                       uint8_t* flags, float* block, void* stream) {
+  GSR_REQUIRE(N >= 0 && n_busy >= 0 && cap >= 0 && block != nullptr, "gsr3d_touched_rows: bad arguments");
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_rows_header, dim3(1), dim3(64), 0, s, block, cap);
   GSR_LAUNCH_CHECK("k_rows_header");
-  if (N == 0) return GSR_OK;
-  hipLaunchKernelGGL(k_touched_rows, dim3(ceil_div(N, kBwdThreads)), dim3(kBwdThreads), 0, s, isect_count, N, C, cap,
-                     block);
+  if (N == 0 || n_busy == 0) return GSR_OK;
+  GSR_REQUIRE(sorted_ids && tile_offset && tile_end && tile_order && stats && flags, "gsr3d_touched_rows: null buffer");
+  const int64_t words = ceil_div(N, (int64_t)4);
+  hipLaunchKernelGGL(k_zero_u32, dim3((unsigned)std::min<int64_t>(ceil_div(words, (int64_t)kBwdThreads), 1024)),
+                     dim3(kBwdThreads), 0, s, (uint32_t*)flags, words);
+  GSR_LAUNCH_CHECK("k_zero_u32");
+  hipLaunchKernelGGL(k_mark_touched, dim3(n_busy), dim3(kBwdThreads), 0, s, sorted_ids, tile_offset, tile_end,
+                     tile_order, stats, N, flags);
+  GSR_LAUNCH_CHECK("k_mark_touched");
+  hipLaunchKernelGGL(k_touched_rows, dim3(ceil_div(N, kBwdThreads)), dim3(kBwdThreads), 0, s, flags, N, cap, block);
   GSR_LAUNCH_CHECK("k_touched_rows");
   return GSR_OK;
 }

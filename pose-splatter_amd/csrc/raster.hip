@@ -1161,6 +1161,9 @@ __device__ __forceinline__ void loss_cotangent(const gsr_loss_terms& lt, int C, 
 // valid pair feeds the sigma / opacity gradients.
 // minimum workgroups per CU of the MULTI variant (build knob for measurements; the one-sub-chunk
 // variant fits 5 per CU in 84 VGPRs on its own)
+#ifndef GSR_BWD_MINB
+#define GSR_BWD_MINB 1
+#endif
 #ifndef GSR_BWD_MULTI_MINB
 #define GSR_BWD_MULTI_MINB 1
 #endif
@@ -1172,7 +1175,7 @@ __device__ unsigned long long* g_bwd_trace = nullptr;
 #define BWD_T(i)
 #endif
 template <bool LOSS, bool IS2D, bool MULTI>
-__global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : 1) void k_raster_bwd(
+__global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BWD_MINB) void k_raster_bwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ tile_end, const int32_t* __restrict__ chunk_base,
     const float4* __restrict__ ckpt, int W, int H, int tw, int th,
@@ -1183,7 +1186,10 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : 1) voi
   static_assert(!(LOSS && IS2D), "the fused loss is the 3D training loss");
   // slot kNull: a zero-opacity record (never valid) that pads survivor groups to 7
   constexpr int kNull = kChunk3;
-  constexpr int kGroup = 7;
+#ifndef GSR_BWD_GROUP
+#define GSR_BWD_GROUP 7
+#endif
+  constexpr int kGroup = GSR_BWD_GROUP;
   constexpr int kLen = kChunk3 + kGroup;   // survivor list capacity (padded to whole groups)
   __shared__ float4 s_p[3][kChunk3 + 1];   // the chunk's records, part j of entry k at s_p[j][k]
   // gradient sums per entry, one slot per wave (index kNull absorbs the padding's zeros)

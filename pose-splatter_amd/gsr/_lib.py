@@ -114,7 +114,7 @@ EXPORTS = {
                                         _P, _P, _P, _P, _P, _P]),
     "gsr3d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _I32, _I32, _I32, _F, _I32, _P, _P,
                                          _P, _P, _P, _P, _I64, _I64, _P, _P, _P]),
-    "gsr3d_touched_rows": (ctypes.c_int, [_P, _I64, _I32, _I64, _P, _P]),
+    "gsr3d_touched_rows": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I64, _I64, _P, _P, _P]),
     "gsr3d_project_bwd_rows": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _I32, _I32, _I32, _F, _I32, _P, _P,
                                               _P, _P, _P, _P, _P, _I64, _P, _P]),
     "gsr_rows_scatter_add": (ctypes.c_int, [_P, _I32, _I64, _P, _I64, _P, _P]),

@@ -318,8 +318,8 @@ def rows_backward_units(render_band_rows: Callable, params: torch.Tensor, viewma
         rgb, alpha = render_band_rows(p, viewmats[v0:v1], Ks[v0:v1], band, grad_rows)
         torch.autograd.backward([rgb, alpha], [v_rgb[v0:v1], v_alpha[v0:v1]])
     else:   # an empty share: a header with no rows
-        _lib.check(L.gsr3d_touched_rows(None, 0, 1, grad_rows.cap, grad_rows.block.data_ptr(), stream),
-                   "gsr3d_touched_rows")
+        _lib.check(L.gsr3d_touched_rows(None, None, None, None, None, 0, 0, grad_rows.cap, None,
+                                        grad_rows.block.data_ptr(), stream), "gsr3d_touched_rows")
     blk = grad_rows.block
     if world > 1:
         gathered = torch.empty((world,) + tuple(blk.shape), device=dev, dtype=blk.dtype)

@@ -850,7 +850,9 @@ def _backward3d_rows(L, b, meta, raster, stream) -> None:
     rows = opts.grad_rows
     C, N = b.C, b.N
     q = b.p
-    check(L.gsr3d_touched_rows(q["cnt"], N, C, rows.cap, rows.block.data_ptr(), stream), "gsr3d_touched_rows")
+    flags = torch.empty((N + 3) // 4 * 4, device=p.device, dtype=torch.uint8)
+    check(L.gsr3d_touched_rows(q["sorted_ids"], q["tile_off"], q["tile_end"], q["busy"], q["stats_dev"], b.n_busy, N,
+                               rows.cap, flags.data_ptr(), rows.block.data_ptr(), stream), "gsr3d_touched_rows")
     if N == 0:
         return None
     partial = torch.empty(max(b.n_isect, 1) * _lib.PARTIAL_STRIDE, device=p.device, dtype=torch.float32)

@@ -4,9 +4,9 @@ gsr_rows_scatter_add; gsr.multiview.rows_backward_units), on one GPU.
 The ranks of a (view, tile-row) unit partition are played one after the other in this
 process (the collective is then the stacking of their blocks; the gloo / RCCL all-gather
 itself is exercised by tools/gpu_dist.sh and the driver's multi-GPU runs):
-* each share's row block lists exactly the Gaussians with a nonzero rect in its band, and each
-  listed row is bitwise the dense backward's row of the same share (unlisted rows are zero
-  there);
+* each share's row block lists exactly the Gaussians owning a list entry before their tile's cut
+  (the partial rows the raster backward writes), and each listed row is bitwise the dense
+  backward's row of the same share (unlisted rows are zero there);
 * the rank-ordered scatter-add of the blocks equals ((0 + g_0) + g_1) + ... of the dense
   partial gradients, bitwise -- the sum a rank-ordered dense reduction gives, on every rank;
 * with one share covering everything, rows_backward_units equals the dense gradient bitwise;
@@ -62,7 +62,15 @@ def test_rows_equal_dense_partials_and_rank_ordered_sum(cuda):
         g_none, b2 = _share(p, V, K, W, H, vr, va, v0, v1, band, gr)
         assert g_none is None                       # no dense gradient in rows mode
         cnt = gr.count()
-        touched = (b2.cnt[:(v1 - v0) * N].view(v1 - v0, N) > 0).any(0)
+        # the Gaussians owning an entry before their tile's cut (tile_end): exactly the partial
+        # rows the raster backward wrote
+        off, te = b2.tile_off.long(), b2.tile_end.long()
+        CT = off.numel() - 1
+        I = int(off[-1])
+        tile_of = torch.repeat_interleave(torch.arange(CT, device=cuda), off[1:] - off[:-1])
+        used = torch.arange(I, device=cuda) < te[tile_of]
+        touched = torch.zeros(N, dtype=torch.bool, device=cuda)
+        touched[b2.sorted_ids[:I].long()[used] % N] = True
         assert cnt == int(touched.sum()) and cnt > 0, (cnt, int(touched.sum()))
         rows = gr.block[1:1 + cnt]
         n = rows[:, 0].contiguous().view(torch.int32).long()
