@@ -109,7 +109,7 @@ typedef struct gsr_bin_stats {
   int32_t chunk_entries; /* list entries per backward work unit (copy of caps->chunk_entries) */
   int32_t* status;     /* copy of caps->status (device; may be NULL)                  */
   int32_t n_sort_long; /* tiles with lists >= 1024 entries (the sort's one-workgroup lists) */
-  int32_t reserved32;
+  int32_t masks;       /* 1: the emission stored 3D quadrant masks in k_of_s (gsr_bin_emit rec) */
   int64_t reserved;
 } gsr_bin_stats;       /* 80 bytes; written by gsr_bin_offsets                         */
 
@@ -140,7 +140,9 @@ int gsr_version(void);
  * gsr_bin_sort_lazy take mutable stats. */
 /* Revision 4: gsr_bin_stats.n_sort_long (in the former reserved words; size unchanged). */
 /* Revision 5: the sparse gradient row blocks (gsr3d_touched_rows, gsr3d_project_bwd_rows,
- * gsr_rows_scatter_add, GSR_OVF_EXCHANGE). */
+ * gsr_rows_scatter_add, GSR_OVF_EXCHANGE); quadrant masks: gsr_bin_emit / gsr_bin_sort /
+ * gsr_bin_sort_lazy take `rec` after `depth`, gsr3d_raster_fwd takes `k_of_s` after
+ * `sorted_ids`, gsr_bin_stats.masks (the former reserved32) says whether they were stored. */
 #define GSR_ABI_VERSION 5
 int gsr_abi_version(void);
 const char* gsr_last_error(void);
@@ -229,10 +231,17 @@ size_t gsr_bin_sort_workspace(int64_t n_isect, int64_t CT);
  * workspace_bytes, and if this call's I (stats->n_isect, device) exceeds what the
  * workspace holds, the kernel does nothing -- the caller then sizes a workspace from the
  * read-back I and calls gsr_bin_sort with emitted = 0.  tile_count is consumed (counted
- * down to zero) by an emit that ran. */
-int gsr_bin_emit(const float* depth, const uint32_t* rect, const int32_t* isect_offset,
+ * down to zero) by an emit that ran.
+ * rec (3D, depth order; may be NULL): gsr3d_project_fwd's records.  When given, each entry's
+ * emission index carries the entry's QUADRANT MASK in bits 28..31 (k_of_s after the sort):
+ * bit q set iff the raster's exact cull keeps the record for 8x8 quadrant q of the tile
+ * (q = 2 * row + column), so the raster forward can skip -- not even gather -- entries that
+ * cannot reach its quadrant (at config 3 an entry reaches 1.27 of its tile's 4 quadrants).
+ * Needs a workspace of at most 2^28 entries; mask the bits (& 0x0FFFFFFF) to use an index.
+ * An emission that stores masks sets stats->masks = 1 (gsr_bin_offsets resets it). */
+int gsr_bin_emit(const float* depth, const float* rec, const uint32_t* rect, const int32_t* isect_offset,
                  const int32_t* tile_offset, int32_t* tile_count, int C, int64_t N, int width,
-                 int height, int order, const gsr_bin_stats* stats, void* workspace,
+                 int height, int order, gsr_bin_stats* stats, void* workspace,
                  size_t workspace_bytes, void* stream);
 
 /* Emit (tile, key) pairs and sort each tile's list in LDS.  depth: gsr3d_project_fwd's
@@ -251,7 +260,7 @@ int gsr_bin_emit(const float* depth, const uint32_t* rect, const int32_t* isect_
  * max_seg (GSR_OVF_SEG) is flagged in stats->overflow.
  * emitted != 0: gsr_bin_emit already ran on this workspace (same workspace_bytes) and I fit;
  * otherwise the emit runs here.  stats: the device gsr_bin_stats. */
-int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_offset,
+int gsr_bin_sort(const float* depth, const float* rec, const uint32_t* rect, const int32_t* isect_offset,
                  const int32_t* tile_offset, int32_t* tile_count,
                  const int32_t* busy_tiles, int C, int64_t N,
                  int width, int height, int order, int64_t n_isect, int32_t max_seg,
@@ -285,7 +294,7 @@ int gsr_set_split_sort(int on);
 size_t gsr_lazy_workspace(int64_t CT);
 int gsr_set_lazy_sort(int min_len, int prefix);
 int gsr_lazy_min_len(void);
-int gsr_bin_sort_lazy(const float* depth, const uint32_t* rect, const int32_t* isect_offset,
+int gsr_bin_sort_lazy(const float* depth, const float* rec, const uint32_t* rect, const int32_t* isect_offset,
                       const int32_t* tile_offset, int32_t* tile_count, const int32_t* busy_tiles, int C,
                       int64_t N, int width, int height, int64_t n_isect, int32_t max_seg, int32_t n_busy,
                       int32_t n_sort_big, int32_t n_sort_mid, int emitted, gsr_bin_stats* stats,
@@ -312,8 +321,12 @@ int gsr_bin_sort_lazy(const float* depth, const uint32_t* rect, const int32_t* i
  * sum of all later chunks} per pixel of the tile, for every GSR_CHUNK-entry chunk the tile's
  * walk reached) and chunk_list [n_chunks][4] (a descriptor {first sorted entry, entry count, chunk_state row, tile} for
  * each chunk before its tile's tile_end, in no particular order; their count is added to
- * stats->n_active).  stats: the device gsr_bin_stats of gsr_bin_offsets. */
-int gsr3d_raster_fwd(const float* rec, const float* depth, const int32_t* sorted_ids, const int32_t* tile_offset,
+ * stats->n_active).  stats: the device gsr_bin_stats of gsr_bin_offsets.
+ * k_of_s (may be NULL): the sort's emission indices; when the emission stored quadrant masks
+ * in them (stats->masks, gsr_bin_emit given rec) a quadrant workgroup gathers only the entries
+ * whose bit is set.  The outputs are the same bit for bit either way. */
+int gsr3d_raster_fwd(const float* rec, const float* depth, const int32_t* sorted_ids, const int32_t* k_of_s,
+                     const int32_t* tile_offset,
                      const int32_t* tile_order, const int32_t* chunk_base, int C, int width,
                      int height, const float* bg, int32_t n_busy, gsr_bin_stats* stats,
                      float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
@@ -322,7 +335,8 @@ int gsr3d_raster_fwd(const float* rec, const float* depth, const int32_t* sorted
 /* gsr3d_raster_fwd over the lists of gsr_bin_sort_lazy (same outputs, see above): the tiles
  * that read past their sorted prefix are sorted whole (sort_workspace / k_of_s / max_seg of
  * that gsr_bin_sort_lazy call) and rendered again.  n_lazy_max: an upper bound on the tiles
- * sorted lazily (n_sort_big when min_len >= 8191, else n_busy). */
+ * sorted lazily (n_sort_big when min_len >= 8191, else n_busy).  Quadrant masks in k_of_s
+ * (stats->masks) are used as in gsr3d_raster_fwd. */
 int gsr3d_raster_fwd_lazy(const float* rec, const float* depth, int32_t* sorted_ids, const int32_t* tile_offset,
                           const int32_t* tile_order, const int32_t* chunk_base, int C, int width, int height,
                           const float* bg, int32_t n_busy, gsr_bin_stats* stats, float* rgb, float* alpha,

@@ -173,6 +173,7 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(int32_t* __restrict__
       stats->n_busy = n_busy;
       stats->n_chunks = tk;
       stats->n_active = 0;
+      stats->masks = 0;   // set by an emission that stores quadrant masks
       // bounded call: the caller sized the intersection / chunk buffers without reading I back
       int ovf = 0;
       if (caps.isect > 0 && (int64_t)tc > caps.isect) ovf |= GSR_OVF_ISECT;
@@ -228,13 +229,14 @@ __device__ __forceinline__ void emit_skip_counts(int32_t* __restrict__ tile_coun
   for (int t = threadIdx.x; t < T; t += blockDim.x) g[t] = 0;
 }
 
-__global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__ depth, const uint2* __restrict__ rect,
+__global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__ depth, const Splat* __restrict__ rec,
+                                                      const uint2* __restrict__ rect,
                                                       const int32_t* __restrict__ isect_offset, int64_t N, int tw,
                                                       int th, int order, int use_lds,
                                                       const int32_t* __restrict__ tile_offset,
                                                       int32_t* __restrict__ tile_count, uint64_t* __restrict__ keys,
                                                       int32_t* __restrict__ k_of_slot, int per_block,
-                                                      const gsr_bin_stats* __restrict__ stats, int64_t cap) {
+                                                      gsr_bin_stats* __restrict__ stats, int64_t cap) {
   // launched before the host has read I back (gsr_bin_emit): a workspace too small for this
   // call's I makes every workgroup leave at once, and the host emits again with a larger one.
   // A bounded call over its caps emits nothing.  (Both words load together, one branch.)
@@ -244,6 +246,7 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__
     if (ovf) emit_skip_counts(tile_count, tw * th);
     return;
   }
+  if (rec != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) stats->masks = 1;
   // Slots are claimed by counting each tile's count down to zero (slot = tile start +
   // remaining count - 1): no separate cursor array, and tile_count is left zeroed.
   extern __shared__ int hist[];
@@ -288,12 +291,16 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__
     if (x1 <= x0 || y1 <= y0) continue;
     const uint64_t key = sort_key(depth, cn, order);
     int k = isect_offset[cn];   // emission entries of (c,n): k = offset + rect row-major index
+    Splat sp{};
+    if (rec != nullptr) sp = rec[cn];
     for (int ty = y0; ty < y1; ++ty)
       for (int tx = x0; tx < x1; ++tx) {
         const int t = ty * tw + tx;
         const int slot = use_lds ? atomicAdd(&hist[t], 1) : toff[t] + atomicSub(&gcnt[t], 1) - 1;
+        // 3D: the entry's quadrant mask in the top bits (gsr_common.h quad_mask)
+        const int mk = rec != nullptr ? quad_mask<false>(sp.p0, sp.p1, sp.p2, tx, ty) << kMaskShift : 0;
         keys[slot] = key;
-        k_of_slot[slot] = k++;
+        k_of_slot[slot] = k++ | mk;
       }
   }
 }
@@ -320,9 +327,10 @@ static_assert(kStageMaxTiles >= 4096, "staged emission needs room for a 4096-til
 
 template <int GPT>
 __global__ __launch_bounds__(kStageThreads) void k_emit_staged(
-    const float* __restrict__ depth, const uint2* __restrict__ rect, const int32_t* __restrict__ isect_offset,
+    const float* __restrict__ depth, const Splat* __restrict__ rec, const uint2* __restrict__ rect,
+    const int32_t* __restrict__ isect_offset,
     int64_t N, int tw, int th, int order, const int32_t* __restrict__ tile_offset, int32_t* __restrict__ tile_count,
-    uint64_t* __restrict__ keys, int32_t* __restrict__ k_of_slot, const gsr_bin_stats* __restrict__ stats,
+    uint64_t* __restrict__ keys, int32_t* __restrict__ k_of_slot, gsr_bin_stats* __restrict__ stats,
     int64_t cap) {
   const int ovf = stats->overflow & kOvfCapacity;   // see k_emit
   const int64_t n_isect = stats->n_isect;
@@ -330,6 +338,7 @@ __global__ __launch_bounds__(kStageThreads) void k_emit_staged(
     if (ovf) emit_skip_counts(tile_count, tw * th);
     return;
   }
+  if (rec != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) stats->masks = 1;
   constexpr int NT = kStageThreads;
   constexpr int kStagePer = GPT * NT;   // Gaussians per workgroup
   extern __shared__ uint64_t s_key[];   // [kStageCap]
@@ -404,17 +413,21 @@ __global__ __launch_bounds__(kStageThreads) void k_emit_staged(
   for (int j = 0; j < GPT; ++j) {
     const int x0 = rr[j].x & 0xffff, x1 = rr[j].x >> 16, y0 = rr[j].y & 0xffff, y1 = rr[j].y >> 16;
     int k = k0[j];   // emission entries of (c,n): k = offset + rect row-major index
+    // 3D: each entry's quadrant mask goes to the top bits of its emission index (quad_mask)
+    Splat sp{};
+    if (rec != nullptr && x1 > x0 && y1 > y0) sp = rec[(int64_t)c * N + n0 + threadIdx.x + j * NT];
     for (int ty = y0; ty < y1; ++ty)
       for (int tx = x0; tx < x1; ++tx) {
         const int t = ty * tw + tx;
         const int p = atomicAdd(&cur[t], 1);
+        const int kk = k | (rec != nullptr ? quad_mask<false>(sp.p0, sp.p1, sp.p2, tx, ty) << kMaskShift : 0);
         if (staged) {
           s_key[p] = key[j];
-          s_kos[p] = k;
+          s_kos[p] = kk;
           s_slot[p] = delta[t] + p;
         } else {
           keys[delta[t] + p] = key[j];
-          k_of_slot[delta[t] + p] = k;
+          k_of_slot[delta[t] + p] = kk;
         }
         ++k;
       }
@@ -1425,9 +1438,9 @@ static SortWs sort_ws(void* workspace, int64_t cap) {
   return w;
 }
 
-int gsr_bin_emit(const float* depth, const uint32_t* rect, const int32_t* isect_offset, const int32_t* tile_offset,
-                 int32_t* tile_count, int C, int64_t N, int width, int height, int order,
-                 const gsr_bin_stats* stats, void* workspace, size_t workspace_bytes, void* stream) {
+int gsr_bin_emit(const float* depth, const float* rec, const uint32_t* rect, const int32_t* isect_offset,
+                 const int32_t* tile_offset, int32_t* tile_count, int C, int64_t N, int width, int height, int order,
+                 gsr_bin_stats* stats, void* workspace, size_t workspace_bytes, void* stream) {
   GSR_REQUIRE(order == GSR_ORDER_DEPTH || order == GSR_ORDER_INDEX, "gsr_bin_emit: bad order %d", order);
   GSR_REQUIRE(order == GSR_ORDER_INDEX || depth != nullptr, "gsr_bin_emit: depth order needs the depth array");
   GSR_REQUIRE(C >= 1 && N >= 0 && (int64_t)C * N < (1ll << 31), "gsr_bin_emit: bad C=%d or N=%lld", C,
@@ -1437,6 +1450,9 @@ int gsr_bin_emit(const float* depth, const uint32_t* rect, const int32_t* isect_
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   const int64_t T = (int64_t)tw * th;
   const int64_t cap = ws_cap(workspace_bytes);
+  GSR_REQUIRE(rec == nullptr || (order == GSR_ORDER_DEPTH && cap <= kEmitIndexMask + 1ll),
+              "gsr_bin_emit: quadrant masks (rec != NULL) need depth order and a workspace of at most 2^28 entries "
+              "(%lld); pass rec = NULL", (long long)cap);
   const SortWs w = sort_ws(workspace, cap);
   const int use_lds = T <= kHistMaxTiles;
   // staged when it fills the chip with its 1024-thread workgroups (config 2's 25 would leave
@@ -1447,24 +1463,24 @@ int gsr_bin_emit(const float* depth, const uint32_t* rect, const int32_t* isect_
     const size_t lds = kStageLds + (size_t)2 * T * sizeof(int);
     if (gpt == 1)
       hipLaunchKernelGGL(k_emit_staged<1>, dim3(ceil_div(N, per), C), dim3(kStageThreads), lds, (hipStream_t)stream,
-                         depth, (const uint2*)rect, isect_offset, N, tw, th, order, tile_offset, tile_count, w.keys,
+                         depth, (const Splat*)rec, (const uint2*)rect, isect_offset, N, tw, th, order, tile_offset, tile_count, w.keys,
                          w.k_of_slot, stats, cap);
     else
       hipLaunchKernelGGL(k_emit_staged<2>, dim3(ceil_div(N, per), C), dim3(kStageThreads), lds, (hipStream_t)stream,
-                         depth, (const uint2*)rect, isect_offset, N, tw, th, order, tile_offset, tile_count, w.keys,
+                         depth, (const Splat*)rec, (const uint2*)rect, isect_offset, N, tw, th, order, tile_offset, tile_count, w.keys,
                          w.k_of_slot, stats, cap);
     GSR_LAUNCH_CHECK("k_emit_staged");
     return GSR_OK;
   }
   dim3 grid(ceil_div(N, kEmitPerBlock), C);
   hipLaunchKernelGGL(k_emit, grid, dim3(kEmitThreads), use_lds ? T * sizeof(int) : 0, (hipStream_t)stream, depth,
-                     (const uint2*)rect, isect_offset, N, tw, th, order, use_lds, tile_offset, tile_count, w.keys,
+                     (const Splat*)rec, (const uint2*)rect, isect_offset, N, tw, th, order, use_lds, tile_offset, tile_count, w.keys,
                      w.k_of_slot, kEmitPerBlock, stats, cap);
   GSR_LAUNCH_CHECK("k_emit");
   return GSR_OK;
 }
 
-static int bin_sort_impl(const char* who, const float* depth, const uint32_t* rect, const int32_t* isect_offset, const int32_t* tile_offset,
+static int bin_sort_impl(const char* who, const float* depth, const float* rec, const uint32_t* rect, const int32_t* isect_offset, const int32_t* tile_offset,
                  int32_t* tile_count, const int32_t* busy_tiles, int C, int64_t N, int width, int height, int order, int64_t n_isect,
                  int32_t max_seg, int32_t n_busy, int32_t n_big, int32_t n_mid, int emitted, gsr_bin_stats* stats,
                  void* workspace, size_t workspace_bytes, int32_t* sorted_ids, int32_t* k_of_s, const LazyArgs& lz, void* stream) {
@@ -1484,8 +1500,8 @@ static int bin_sort_impl(const char* who, const float* depth, const uint32_t* re
   int32_t* tmpp1 = w.tmpp1;
   int32_t* k_of_slot = w.k_of_slot;
   if (!emitted) {
-    const int rc = gsr_bin_emit(depth, rect, isect_offset, tile_offset, tile_count, C, N, width, height, order, stats,
-                                workspace, workspace_bytes, stream);
+    const int rc = gsr_bin_emit(depth, rec, rect, isect_offset, tile_offset, tile_count, C, N, width, height, order,
+                                stats, workspace, workspace_bytes, stream);
     if (rc != GSR_OK) return rc;
   }
   GSR_REQUIRE(n_big >= 0 && n_mid >= 0 && n_big + n_mid <= n_busy, "%s: bad sort classes %d/%d of %d", who,
@@ -1522,12 +1538,12 @@ static int bin_sort_impl(const char* who, const float* depth, const uint32_t* re
   return GSR_OK;
 }
 
-int gsr_bin_sort(const float* depth, const uint32_t* rect, const int32_t* isect_offset, const int32_t* tile_offset,
+int gsr_bin_sort(const float* depth, const float* rec, const uint32_t* rect, const int32_t* isect_offset, const int32_t* tile_offset,
                  int32_t* tile_count, const int32_t* busy_tiles, int C, int64_t N, int width, int height, int order, int64_t n_isect,
                  int32_t max_seg, int32_t n_busy, int32_t n_big, int32_t n_mid, int emitted, gsr_bin_stats* stats,
                  void* workspace, size_t workspace_bytes, int32_t* sorted_ids, int32_t* k_of_s, void* stream) {
   const LazyArgs off{};
-  return bin_sort_impl("gsr_bin_sort", depth, rect, isect_offset, tile_offset, tile_count, busy_tiles, C, N, width,
+  return bin_sort_impl("gsr_bin_sort", depth, rec, rect, isect_offset, tile_offset, tile_count, busy_tiles, C, N, width,
                        height, order, n_isect, max_seg, n_busy, n_big, n_mid, emitted, stats, workspace,
                        workspace_bytes, sorted_ids, k_of_s, off, stream);
 }
@@ -1553,7 +1569,7 @@ int gsr_set_emit_staged(int on) {
   return GSR_OK;
 }
 
-int gsr_bin_sort_lazy(const float* depth, const uint32_t* rect, const int32_t* isect_offset,
+int gsr_bin_sort_lazy(const float* depth, const float* rec, const uint32_t* rect, const int32_t* isect_offset,
                       const int32_t* tile_offset, int32_t* tile_count, const int32_t* busy_tiles, int C, int64_t N,
                       int width, int height, int64_t n_isect, int32_t max_seg, int32_t n_busy, int32_t n_big,
                       int32_t n_mid, int emitted, gsr_bin_stats* stats, void* workspace,
@@ -1562,7 +1578,7 @@ int gsr_bin_sort_lazy(const float* depth, const uint32_t* rect, const int32_t* i
   const int64_t CT = (int64_t)C * ceil_div(width, kTile) * ceil_div(height, kTile);
   LazyArgs lz{lazy, lazy + CT, lazy + 2 * CT, lazy + 3 * CT, nullptr, g_lazy_min_len, g_lazy_prefix, 1};
   if (lz.min_len <= 0) lz.min_len = 1 << 30;   // disabled: every list sorted whole
-  return bin_sort_impl("gsr_bin_sort_lazy", depth, rect, isect_offset, tile_offset, tile_count, busy_tiles, C, N,
+  return bin_sort_impl("gsr_bin_sort_lazy", depth, rec, rect, isect_offset, tile_offset, tile_count, busy_tiles, C, N,
                        width, height, GSR_ORDER_DEPTH, n_isect, max_seg, n_busy, n_big, n_mid, emitted, stats,
                        workspace, workspace_bytes, sorted_ids, k_of_s, lz, stream);
 }

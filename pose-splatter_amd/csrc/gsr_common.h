@@ -246,4 +246,59 @@ int bin_sort_rest(const int32_t* tile_offset, int64_t CT, int32_t max_seg, int32
                   size_t workspace_bytes, int32_t* lazy, int32_t* tile_end, int32_t* sorted_ids, int32_t* k_of_s,
                   gsr_bin_stats* stats, hipStream_t s);
 
+// ---------------------------------------------------------------- per-wave culling
+// A wave owns an 8x8 sub-tile of its 16x16 tile.  An entry can only change a pixel of the
+// sub-tile if its level set {opacity*exp(-sigma) >= cut} (3D: cut = 1/255, gsplat's skip
+// threshold; 2D: eps_cut) meets the sub-tile's pixel-centre box B, i.e. iff
+// min over B of sigma <= L = ln(opacity/cut).  That minimum is computed exactly: sigma is a
+// convex quadratic with its minimum at the mean, so when the mean lies outside B the
+// minimiser lies on an edge of B facing the mean, and along an edge the best point is the
+// clamped 1-D optimum.  With dx fixed to the mean's nearest x in B, the best dy is
+// clamp(-b dx / 2c); likewise for y; the smaller of the two values is the box minimum (the
+// non-facing "edge" evaluates a segment inside B, never below the true minimum).  A small
+// relative margin absorbs rounding, so culling changes the work, never the result.  The
+// per-Gaussian constants (L and the two edge slopes) come precomputed in the record's .w
+// slots (gsr3d_project_fwd), so the test has no transcendental.
+// sigma = a dx^2 + b dx dy + c dy^2 of a record's conic (a, b, c) = p1.xyz, one definition
+// for every kernel (the backward's alpha must be the forward's, bit for bit)
+__device__ __forceinline__ float conic_sigma(const float4 p1, float dx, float dy) {
+  return p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
+}
+
+template <bool IS2D>
+__device__ __forceinline__ bool cull_keep(const float4 p0, const float4 p1, const float4 p2, float bx0, float bx1,
+                                          float by0, float by1) {
+  (void)IS2D;   // 3D: L = ln(opacity * 255); 2D: L = ln(opacity / eps_cut)
+  const float L = p0.w;   // < 0: the Gaussian never reaches the cut anywhere
+  if (!(L >= 0.f)) return false;
+  const float a = p1.x, b = p1.y, c = p1.z;
+  if (!(a > 0.f && c > 0.f && 4.f * a * c > b * b)) return true;   // not positive definite: keep
+  const float dxe = p0.x - fminf(fmaxf(p0.x, bx0), bx1);
+  const float dye = p0.y - fminf(fmaxf(p0.y, by0), by1);
+  const float dy1 = fminf(fmaxf(p1.w * dxe, p0.y - by1), p0.y - by0);   // p1.w = -b / 2c
+  const float dx2 = fminf(fmaxf(p2.w * dye, p0.x - bx1), p0.x - bx0);   // p2.w = -b / 2a
+  const float s1 = a * dxe * dxe + b * dxe * dy1 + c * dy1 * dy1;
+  const float s2 = a * dx2 * dx2 + b * dx2 * dye + c * dye * dye;
+  return fminf(s1, s2) <= L * 1.001f + 1e-3f;
+}
+
+// Quadrant mask of a (record, tile) list entry: bit q (q = 2 * (quadrant row) + quadrant
+// column of the 16x16 tile) is set iff cull_keep keeps the record for that 8x8 quadrant's
+// pixel-centre box -- the same test on the same fp32 box bounds as the raster forward's
+// quadrant workgroups, so a workgroup may skip (not even gather) an entry whose bit is clear.
+// Stored by the emission in the top bits of the entry's emission index (k_of_s).
+constexpr int kMaskShift = 28;                         // k_of_s bits 28..31
+constexpr int32_t kEmitIndexMask = (1 << kMaskShift) - 1;
+template <bool IS2D>
+__device__ __forceinline__ int quad_mask(const float4 p0, const float4 p1, const float4 p2, int tx, int ty) {
+  const float off = IS2D ? 0.f : 0.5f;
+  int m = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float x0 = (float)(tx * kTile + (q & 1) * 8) + off, y0 = (float)(ty * kTile + (q >> 1) * 8) + off;
+    if (cull_keep<IS2D>(p0, p1, p2, x0, x0 + 7.f, y0, y0 + 7.f)) m |= 1 << q;
+  }
+  return m;
+}
+
 }  // namespace gsr

@@ -37,41 +37,8 @@ __device__ __forceinline__ void tile_coords(int ct, int tw, int th, int& c, int&
   tx = t - ty * tw;
 }
 
-// ---------------------------------------------------------------- per-wave culling
-// A wave owns an 8x8 sub-tile of its 16x16 tile.  An entry can only change a pixel of the
-// sub-tile if its level set {opacity*exp(-sigma) >= cut} (3D: cut = 1/255, gsplat's skip
-// threshold; 2D: eps_cut) meets the sub-tile's pixel-centre box B, i.e. iff
-// min over B of sigma <= L = ln(opacity/cut).  That minimum is computed exactly: sigma is a
-// convex quadratic with its minimum at the mean, so when the mean lies outside B the
-// minimiser lies on an edge of B facing the mean, and along an edge the best point is the
-// clamped 1-D optimum.  With dx fixed to the mean's nearest x in B, the best dy is
-// clamp(-b dx / 2c); likewise for y; the smaller of the two values is the box minimum (the
-// non-facing "edge" evaluates a segment inside B, never below the true minimum).  A small
-// relative margin absorbs rounding, so culling changes the work, never the result.  The
-// per-Gaussian constants (L and the two edge slopes) come precomputed in the record's .w
-// slots (gsr3d_project_fwd), so the test has no transcendental.
-// sigma = a dx^2 + b dx dy + c dy^2 of a record's conic (a, b, c) = p1.xyz, one definition
-// for every kernel (the backward's alpha must be the forward's, bit for bit)
-__device__ __forceinline__ float conic_sigma(const float4 p1, float dx, float dy) {
-  return p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
-}
-
-template <bool IS2D>
-__device__ __forceinline__ bool cull_keep(const float4 p0, const float4 p1, const float4 p2, float bx0, float bx1,
-                                          float by0, float by1) {
-  (void)IS2D;   // 3D: L = ln(opacity * 255); 2D: L = ln(opacity / eps_cut)
-  const float L = p0.w;   // < 0: the Gaussian never reaches the cut anywhere
-  if (!(L >= 0.f)) return false;
-  const float a = p1.x, b = p1.y, c = p1.z;
-  if (!(a > 0.f && c > 0.f && 4.f * a * c > b * b)) return true;   // not positive definite: keep
-  const float dxe = p0.x - fminf(fmaxf(p0.x, bx0), bx1);
-  const float dye = p0.y - fminf(fmaxf(p0.y, by0), by1);
-  const float dy1 = fminf(fmaxf(p1.w * dxe, p0.y - by1), p0.y - by0);   // p1.w = -b / 2c
-  const float dx2 = fminf(fmaxf(p2.w * dye, p0.x - bx1), p0.x - bx0);   // p2.w = -b / 2a
-  const float s1 = a * dxe * dxe + b * dxe * dy1 + c * dy1 * dy1;
-  const float s2 = a * dx2 * dx2 + b * dx2 * dye + c * dye * dye;
-  return fminf(s1, s2) <= L * 1.001f + 1e-3f;
-}
+// (per-wave culling: conic_sigma / cull_keep / quad_mask live in gsr_common.h -- the binning
+// computes each entry's quadrant mask with the same test)
 
 // The survivors list[0, nsurv) of an 8x8 quadrant (origin (qx, qy), pixel centres) against its
 // four 4x4 boxes, ONE survivor per lane: its record is read from LDS once and tested against all
@@ -376,7 +343,8 @@ extern "C" int gsr_debug_fwd_trace(void* buf) {
 #endif
 template <bool IS2D, int LPP>
 __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MINB) void k_raster_fwd(
-    const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
+    const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ kos,
+    const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ order, int W, int H, int tw, int th, const float* __restrict__ bg,
     float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
     int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end, float4* __restrict__ ckpt,
@@ -469,12 +437,23 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
   const float qx0 = (float)(tx * kTile + sx) + off, qx1 = qx0 + (float)(FS::WB - 1);
   const float qy0 = (float)(ty * kTile + sy) + off, qy1 = qy0 + (float)(FS::WB - 1);
   float4 c0 = make_float4(0.f, 0.f, 0.f, 0.f), c1 = c0, c2 = c0;
+  // quadrant masks (kos: gsr_bin_emit's bits 28..31): an entry whose bit for this workgroup's
+  // 8x8 quadrant is clear cannot reach it -- its record is not even gathered (an entry reaches
+  // 1.27 of its tile's 4 quadrants at config 3).  Kept entries still take the exact cull.
+  const int qbit = kMaskShift + ((sy >> 3) << 1) + (sx >> 3);
+  if (!stats->masks) kos = nullptr;   // this call's emission stored no masks
   int idn = 0;
+  bool ucur = false, un = false;
   if (end > start) {
-    const int id0 = ids[min(start + 64 * wv + lane, e_last)];
-    idn = ids[min(start + 256 + 64 * wv + lane, e_last)];
-    const Splat s0 = rec[id0];
-    c0 = s0.p0; c1 = s0.p1; c2 = s0.p2;
+    const int e0 = min(start + 64 * wv + lane, e_last), e1 = min(start + 256 + 64 * wv + lane, e_last);
+    const int id0 = ids[e0];
+    idn = ids[e1];
+    ucur = kos == nullptr || ((kos[e0] >> qbit) & 1);
+    un = kos == nullptr || ((kos[e1] >> qbit) & 1);
+    if (ucur) {
+      const Splat s0 = rec[id0];
+      c0 = s0.p0; c1 = s0.p1; c2 = s0.p2;
+    }
   }
   int buf = 0;
   for (int rb = start; rb < end; rb += 256, buf ^= 1) {
@@ -483,7 +462,7 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
 #endif
     {
       const int e = rb + 64 * wv + lane;
-      const bool keep = e < end && cull_keep<IS2D>(c0, c1, c2, qx0, qx1, qy0, qy1);
+      const bool keep = e < end && ucur && cull_keep<IS2D>(c0, c1, c2, qx0, qx1, qy0, qy1);
       const unsigned long long m = __ballot(keep);
       if (keep) {
         const int slot = 64 * wv +
@@ -495,9 +474,14 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
       }
       if (lane == 0) s_qn[buf][wv] = __popcll(m);
       const int id_use = idn;
-      idn = ids[min(rb + 512 + 64 * wv + lane, e_last)];
-      const Splat sn = rec[id_use];
-      c0 = sn.p0; c1 = sn.p1; c2 = sn.p2;
+      ucur = un;
+      const int e2 = min(rb + 512 + 64 * wv + lane, e_last);
+      idn = ids[e2];
+      un = kos == nullptr || ((kos[e2] >> qbit) & 1);
+      if (ucur) {
+        const Splat sn = rec[id_use];
+        c0 = sn.p0; c1 = sn.p1; c2 = sn.p2;
+      }
     }
     FWD_P(0);
     if (__syncthreads_count(!done) == 0) break;
@@ -786,12 +770,14 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
 // Chunk records are written per pixel at thread index = the backward's slot, coalesced.
 template <bool IS2D>
 __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
-    const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
+    const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ kos,
+    const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ order, int W, int H, int tw, int th, const float* __restrict__ bg,
     float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
     int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end, float4* __restrict__ ckpt,
     const int32_t* __restrict__ chunk_base, int n_busy, int64_t CT,
     uint64_t* __restrict__ tile_cut, float cut2d, const FwdLazy lz, const gsr_bin_stats* __restrict__ stats) {
+  (void)kos;   // one workgroup per tile: the waves' own quadrant culls decide
   __shared__ float4 s_r[2][3][256];              // round records, part j of slot i at s_r[buf][j][i]
   __shared__ unsigned char s_box[4][4][129];     // ... and each box's, in list order (+1: read-ahead)
   __shared__ int s_max;
@@ -1198,6 +1184,7 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
   __shared__ unsigned char s_list[4][kLen];     // quadrant survivors, back to front
   __shared__ unsigned char s_box[4][4][kLen];   // per (wave, box) survivors, back to front
   __shared__ float s_stage[4][64][4];     // per wave: the group's reduced sums, by lane
+  __shared__ unsigned char s_mask[kChunk3];   // 3D: each entry's quadrant mask (k_of_s bits 28..31)
   // one workgroup per grid slot; slots past the forward's active-chunk count exit at once
   // the chunk's descriptor {first entry, entries (>= 1), chunk record row, tile} -- one load
   // (read before the bound check: the list has a slot for every grid slot)
@@ -1212,6 +1199,7 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
 #endif
   const int4 cd = reinterpret_cast<const int4*>(chunk_list)[blockIdx.x];
   const int n_act = stats->n_active, ovf = stats->overflow, ce = stats->chunk_entries;
+  const bool use_masks = !IS2D && stats->masks != 0;
   const bool unit_bad = !MULTI && ce != kChunk3;
   if ((ovf != 0) | ((int)blockIdx.x >= n_act) | unit_bad | (cd.y <= 0)) {
     if (unit_bad && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1306,6 +1294,7 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
       s_p[0][threadIdx.x] = sp0;
       s_p[1][threadIdx.x] = sp1;
       s_p[2][threadIdx.x] = sp2;
+      s_mask[threadIdx.x] = (unsigned char)((unsigned)kos_mine >> kMaskShift);
     }
     for (int i = threadIdx.x; i < kPartial * (kChunk3 + 1); i += kRasterThreads)   // b128 stores
       reinterpret_cast<float4*>(&L[0][0][0])[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1329,8 +1318,11 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
 #pragma unroll
       for (int q = kChunk3 / 64 - 1; q >= 0; --q) {
         const int k = q * 64 + lane;
+        // the quadrant test: the emission's mask bit where it stored masks (the same cull_keep on
+        // the same bounds, no record reads), else the test itself
         const bool keep = k < sn && (sb0 + k) <= wlast &&
-                          cull_keep<IS2D>(s_p[0][k], s_p[1][k], s_p[2][k], x0, x0 + 7.f, y0, y0 + 7.f);
+                          (use_masks ? ((s_mask[k] >> wv) & 1) != 0
+                                     : cull_keep<IS2D>(s_p[0][k], s_p[1][k], s_p[2][k], x0, x0 + 7.f, y0, y0 + 7.f));
         const unsigned long long mk = __ballot(keep);
         if (keep) {
           const unsigned long long above = lane == 63 ? 0ull : (mk >> (lane + 1));
@@ -1449,7 +1441,7 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
       v[0] = 2.f * p1.x * mx + p1.y * my;
       v[1] = p1.y * mx + 2.f * p1.z * my;
       v[5] = -v[5] / s_p[0][k].z;
-      store_partial_row(partial, kos_mine, v);
+      store_partial_row(partial, kos_mine & kEmitIndexMask, v);   // (bits 28..31: the 3D quadrant mask)
     }
     sb0 -= kChunk3;
     sn = kChunk3;
@@ -1545,7 +1537,7 @@ static int fwd_lanes(bool is2d, int n_busy) {
 // Shared by the 3D and 2D entry points (2D: C = 1, index-order keys, final_T [H,W,2]).
 template <bool IS2D>
 static int raster_fwd(const char* who, const float* rec, const float* depth, const int32_t* sorted_ids,
-                      const int32_t* tile_offset, const int32_t* tile_order, const int32_t* chunk_base, int C,
+                      const int32_t* kos, const int32_t* tile_offset, const int32_t* tile_order, const int32_t* chunk_base, int C,
                       int width, int height, float cut2d, const float* bg, int32_t n_busy, gsr_bin_stats* stats,
                       float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
                       uint64_t* tile_cut, float* chunk_state, int32_t* chunk_list,
@@ -1570,17 +1562,17 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
   if (lz.rerun && n_busy == 0) return GSR_OK;
   if (!IS2D && lanes == 16) {
     hipLaunchKernelGGL((k_raster_fwd<false, 16>), dim3((unsigned)(busy_grid<16>(n_busy) + n_fill)),
-                       dim3(kRasterThreads), kFwdLdsPad, s, (const Splat*)rec, sorted_ids, tile_offset, tile_order,
+                       dim3(kRasterThreads), kFwdLdsPad, s, (const Splat*)rec, sorted_ids, kos, tile_offset, tile_order,
                        width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state,
                        chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz, stats);
   } else if (lanes == 4) {
     hipLaunchKernelGGL((k_raster_fwd<IS2D, 4>), dim3((unsigned)(busy_grid<4>(n_busy) + n_fill)),
-                       dim3(kRasterThreads), IS2D ? kFwdLdsPad2D : kFwdLdsPad, s, (const Splat*)rec, sorted_ids,
+                       dim3(kRasterThreads), IS2D ? kFwdLdsPad2D : kFwdLdsPad, s, (const Splat*)rec, sorted_ids, kos,
                        tile_offset, tile_order, width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end,
                        (float4*)chunk_state, chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz, stats);
   } else {
     hipLaunchKernelGGL((k_raster_fwd_box<IS2D>), dim3((unsigned)(((n_busy + 7) & ~7) + n_fill)),
-                       dim3(kRasterThreads), 0, s, (const Splat*)rec, sorted_ids, tile_offset, tile_order, width,
+                       dim3(kRasterThreads), 0, s, (const Splat*)rec, sorted_ids, kos, tile_offset, tile_order, width,
                        height, tw, th, bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state, chunk_base,
                        (int)n_busy, CT, tile_cut, cut2d, lz, stats);
   }
@@ -1627,12 +1619,13 @@ static int raster_bwd(const char* who, const float* rec, const int32_t* sorted_i
 
 extern "C" {
 
-int gsr3d_raster_fwd(const float* rec, const float* depth, const int32_t* sorted_ids, const int32_t* tile_offset,
+int gsr3d_raster_fwd(const float* rec, const float* depth, const int32_t* sorted_ids, const int32_t* k_of_s,
+                     const int32_t* tile_offset,
                      const int32_t* tile_order, const int32_t* chunk_base, int C, int width, int height,
                      const float* bg, int32_t n_busy, gsr_bin_stats* stats, float* rgb, float* alpha,
                      float* final_T, int32_t* last, int32_t* tile_end, uint64_t* tile_cut, float* chunk_state,
                      int32_t* chunk_list, void* stream) {
-  return raster_fwd<false>("gsr3d_raster_fwd", rec, depth, sorted_ids, tile_offset, tile_order, chunk_base, C, width,
+  return raster_fwd<false>("gsr3d_raster_fwd", rec, depth, sorted_ids, k_of_s, tile_offset, tile_order, chunk_base, C, width,
                            height, 0.f, bg, n_busy, stats, rgb, alpha, final_T, last, tile_end, tile_cut,
                            chunk_state, chunk_list, stream);
 }
@@ -1649,7 +1642,8 @@ int gsr3d_raster_fwd_lazy(const float* rec, const float* depth, int32_t* sorted_
   const int lanes = fwd_lanes(false, n_busy);
   // pass 1: every tile walks its sorted prefix; tiles that reach its end are listed
   const FwdLazy l1{lazy, lazy + CT, lazy + 2 * CT, lazy + 3 * CT, 0};
-  int rc = raster_fwd<false>("gsr3d_raster_fwd_lazy", rec, depth, sorted_ids, tile_offset, tile_order, chunk_base, C,
+  int rc = raster_fwd<false>("gsr3d_raster_fwd_lazy", rec, depth, sorted_ids, k_of_s,
+                             tile_offset, tile_order, chunk_base, C,
                              width, height, 0.f, bg, n_busy, stats, rgb, alpha, final_T, last, tile_end, tile_cut,
                              chunk_state, chunk_list, stream, l1, lanes, false);
   if (rc != GSR_OK) return rc;
@@ -1658,7 +1652,8 @@ int gsr3d_raster_fwd_lazy(const float* rec, const float* depth, int32_t* sorted_
                      sorted_ids, k_of_s, stats, (hipStream_t)stream);
   if (rc != GSR_OK) return rc;
   const FwdLazy l2{lazy, lazy + CT, lazy + 2 * CT, lazy + 3 * CT, 1};
-  rc = raster_fwd<false>("gsr3d_raster_fwd_lazy", rec, depth, sorted_ids, tile_offset, tile_order, chunk_base, C,
+  rc = raster_fwd<false>("gsr3d_raster_fwd_lazy", rec, depth, sorted_ids, k_of_s,
+                         tile_offset, tile_order, chunk_base, C,
                          width, height, 0.f, bg, n_lazy_max, stats, rgb, alpha, final_T, last, tile_end, tile_cut,
                          chunk_state, chunk_list, stream, l2, lanes, false);
   if (rc != GSR_OK) return rc;
@@ -1702,7 +1697,7 @@ int gsr2d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t*
                      float* final_T, int32_t* last, int32_t* tile_end, uint64_t* tile_cut, float* chunk_state,
                      int32_t* chunk_list, void* stream) {
   GSR_REQUIRE(eps_cut > 0.f && eps_cut < 1.f, "gsr2d_raster_fwd: eps_cut must be in (0,1)");
-  return raster_fwd<true>("gsr2d_raster_fwd", rec, nullptr, sorted_ids, tile_offset, tile_order, chunk_base, C, width,
+  return raster_fwd<true>("gsr2d_raster_fwd", rec, nullptr, sorted_ids, nullptr, tile_offset, tile_order, chunk_base, C, width,
                           height, eps_cut, bg, n_busy, stats, rgb, alpha, final_T, last, tile_end, tile_cut,
                           chunk_state, chunk_list, stream);
 }

@@ -50,7 +50,7 @@ class BinStats(ctypes.Structure):
                 ("n_sort_big", ctypes.c_int32), ("n_sort_mid", ctypes.c_int32),
                 ("isect_cap", ctypes.c_int64), ("chunk_cap", ctypes.c_int64), ("overflow", ctypes.c_int32),
                 ("chunk_entries", ctypes.c_int32), ("status", ctypes.c_void_p), ("n_sort_long", ctypes.c_int32),
-                ("reserved32", ctypes.c_int32), ("reserved", ctypes.c_int64)]
+                ("masks", ctypes.c_int32), ("reserved", ctypes.c_int64)]
 
 
 class BinCaps(ctypes.Structure):
@@ -92,17 +92,17 @@ EXPORTS = {
                                          _P, _P, _I32, _P]),
     "gsr_bin_offsets": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P, ctypes.POINTER(BinCaps), _P, _P]),
     "gsr_bin_sort_workspace": (_SZ, [_I64, _I64]),
-    "gsr_bin_emit": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I32, _P, _P, _SZ, _P]),
-    "gsr_bin_sort": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I32, _I64, _I32,
+    "gsr_bin_emit": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I32, _P, _P, _SZ, _P]),
+    "gsr_bin_sort": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I32, _I64, _I32,
                                     _I32, _I32, _I32, _I32, _P, _P, _SZ, _P, _P, _P]),
-    "gsr3d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _I32, _P, _P, _P,
+    "gsr3d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _I32, _P, _P, _P,
                                         _P, _P, _P, _P, _P, _P, _P]),
     "gsr_set_emit_staged": (ctypes.c_int, [_I32]),
     "gsr_set_split_sort": (ctypes.c_int, [_I32]),
     "gsr_lazy_workspace": (_SZ, [_I64]),
     "gsr_set_lazy_sort": (ctypes.c_int, [_I32, _I32]),
     "gsr_lazy_min_len": (ctypes.c_int, []),
-    "gsr_bin_sort_lazy": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I64, _I32, _I32,
+    "gsr_bin_sort_lazy": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I64, _I32, _I32,
                                          _I32, _I32, _I32, _P, _P, _SZ, _P, _P, _P, _P]),
     "gsr3d_raster_fwd_lazy": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _I32, _P, _P, _P,
                                              _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _P, _SZ, _P, _P]),

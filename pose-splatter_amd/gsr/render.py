@@ -44,7 +44,8 @@ from . import _lib
 from ._lib import check, lib
 
 __all__ = ["render3d", "render2d", "render2d_units", "RenderOptions3D", "last_stats", "set_capacity_mode",
-           "capacity_mode", "check_overflow", "overflow_status", "CapacityOverflowError", "set_chunk_entries"]
+           "capacity_mode", "check_overflow", "overflow_status", "CapacityOverflowError", "set_chunk_entries",
+           "set_quadrant_masks"]
 
 _TILE = _lib.TILE
 
@@ -106,6 +107,17 @@ class CapacityOverflowError(RuntimeError):
 
 
 _capacity_default = "exact"
+# 3D quadrant masks (include/gsr.h gsr_bin_emit `rec`): the emission stores which 8x8 quadrants
+# of its tile each list entry can reach, and the raster forward gathers an entry only for
+# those quadrants.  Same outputs bit for bit; off only for A/B measurements and tests.
+_quadrant_masks = True
+_MASK_MAX_ENTRIES = 1 << 28   # the masks live in bits 28..31 of the emission index
+
+
+def set_quadrant_masks(on: bool) -> None:
+    """Enable (default) or disable the 3D quadrant masks (outputs are identical either way)."""
+    global _quadrant_masks
+    _quadrant_masks = bool(on)
 # list entries per backward work unit (gsr_bin_caps.chunk_entries).  Units of several 128-entry
 # sub-chunks re-read the pixel state and write chunk records less often, but the sub-chunk
 # loop's back-edge costs the backward a wave per SIMD (127 VGPRs, 84 without the loop), which
@@ -399,6 +411,7 @@ class _Bins:
         self.post = self.chunks = None
         self.post_cap = self.chunk_cap = 0
         self.emitted = False
+        self.masks = False   # this call's emission carries quadrant masks (mask_rec)
         self.n_chunks = self.n_isect = self.max_seg = self.n_busy = self.n_lazy = 0
         self.n_sort_big = self.n_sort_mid = self.n_lazy_max = 0
         # the shape whose previous call bounds this one (band / unit grouping included: they
@@ -445,6 +458,14 @@ class _Bins:
         if self.max_seg >= 4096 and self.n_sort_big + self.n_sort_mid == 0:
             self.n_sort_mid = 1   # the 1024-thread sort shape (any shape sorts every list correctly)
         self.n_lazy_max = min(self.n_busy, int(h["big"] * 1.25) + 4)
+
+    def mask_rec(self, order):
+        """The records to pass to the emission for quadrant masks (3D depth order, masks on, an
+        emission workspace of at most 2^28 entries), else None; records the decision."""
+        use = (_quadrant_masks and order == _lib.ORDER_DEPTH and self.post is not None
+               and self.post_cap <= _MASK_MAX_ENTRIES)
+        self.masks = bool(use)
+        return self.p["rec"] if use else None
 
     def take_tile_counts(self) -> int:
         """For the projection call: 1 if the shared tile_count buffer is known to be zero."""
@@ -499,7 +520,8 @@ class _Bins:
         L = lib()
         p = self.p
         with _timed("bin_emit"):
-          check(L.gsr_bin_emit(p["depth"] if order == _lib.ORDER_DEPTH else None, p["rect"], p["isect_off"],
+          check(L.gsr_bin_emit(p["depth"] if order == _lib.ORDER_DEPTH else None, self.mask_rec(order), p["rect"],
+                               p["isect_off"],
                                p["tile_off"], p["tile_cnt"], self.C, self.N, self.W, self.H, order, p["stats_dev"],
                                p["sort_ws"], self.post.off["sort_ws"][1], stream), "gsr_bin_emit")
         self.emitted = True
@@ -550,7 +572,9 @@ class _Bins:
         L = lib()
         p = self.p
         with _timed("bin_sort"):
-          check(L.gsr_bin_sort(p["depth"] if order == _lib.ORDER_DEPTH else None, p["rect"], p["isect_off"], p["tile_off"], p["tile_cnt"], p["busy"],
+          rec = self.mask_rec(order) if not self.emitted else (p["rec"] if self.masks else None)
+          check(L.gsr_bin_sort(p["depth"] if order == _lib.ORDER_DEPTH else None, rec, p["rect"], p["isect_off"],
+                               p["tile_off"], p["tile_cnt"], p["busy"],
                              self.C, self.N,
                              self.W, self.H, order, self.n_isect, self.max_seg, self.n_busy, self.n_sort_big,
                              self.n_sort_mid, int(self.emitted), p["stats_dev"], p["sort_ws"],
@@ -572,7 +596,8 @@ class _Bins:
         L = lib()
         p = self.p
         with _timed("bin_sort"):
-          check(L.gsr_bin_sort_lazy(p["depth"], p["rect"], p["isect_off"], p["tile_off"], p["tile_cnt"], p["busy"],
+          rec = self.mask_rec(_lib.ORDER_DEPTH) if not self.emitted else (p["rec"] if self.masks else None)
+          check(L.gsr_bin_sort_lazy(p["depth"], rec, p["rect"], p["isect_off"], p["tile_off"], p["tile_cnt"], p["busy"],
                                   self.C, self.N, self.W, self.H, self.n_isect, self.max_seg, self.n_busy,
                                   self.n_sort_big, self.n_sort_mid, int(self.emitted), p["stats_dev"], p["sort_ws"],
                                   self.post.off["sort_ws"][1], p["sorted_ids"], p["k_of_s"], p["lazy"], stream),
@@ -689,7 +714,8 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts, need_bwd=True):
                                       q["sort_ws"], b.post.off["sort_ws"][1], q["k_of_s"], stream),
               "gsr3d_raster_fwd_lazy")
       else:
-        check(L.gsr3d_raster_fwd(q["rec"], q["depth"], q["sorted_ids"], q["tile_off"], q["busy"], q["chunk_base"],
+        check(L.gsr3d_raster_fwd(q["rec"], q["depth"], q["sorted_ids"], q["k_of_s"], q["tile_off"],
+                                 q["busy"], q["chunk_base"],
                                  C, width, height, _ptr(bgc), b.n_busy, q["stats_dev"], _ptr(rgb), _ptr(alpha),
                                  q["final_T"], q["last"], q["tile_end"], q["tile_cut"], cs, cl, stream),
               "gsr3d_raster_fwd")

@@ -80,8 +80,8 @@ def test_invalid_arguments_are_reported_not_launched():
     assert rc == -1 and b"need set_begin" in lib.gsr_last_error()
     rc = lib.gsr2d_project_bwd(None, 10, 9, 0, None, 1, 0, 64, 64, None, None, None, None, None, None, None, None)
     assert rc == -1 and b"bad C" in lib.gsr_last_error()
-    rc = lib.gsr_bin_sort(None, None, None, None, None, None, 1, 10, 64, 64, 5, 0, 0, 0, 0, 0, 0, None, None, 0, None, None,
-                          None)
+    rc = lib.gsr_bin_sort(None, None, None, None, None, None, None, 1, 10, 64, 64, 5, 0, 0, 0, 0, 0, 0, None, None, 0, None,
+                          None, None)
     assert rc == -1 and b"bad order" in lib.gsr_last_error()
     with pytest.raises(ValueError, match="bad order"):
         _lib.check(rc, "gsr_bin_sort")

@@ -91,7 +91,8 @@ def _check_lists_vs_torch_sort(p, V, K, W, H, C, dev):
     else:
         keep = torch.ones(I, dtype=torch.bool, device=dev)
     assert torch.equal(b.sorted_ids[:I].to(torch.int64)[keep], owner[order][keep])
-    assert torch.equal(b.k_of_s[:I].to(torch.int64)[keep], kemit[order][keep])
+    # (bits 28..31 of k_of_s: the quadrant masks, tests/test_quadrant_masks_gpu.py)
+    assert torch.equal(b.k_of_s[:I].to(torch.int64)[keep] & 0x0FFFFFFF, kemit[order][keep])
     return I, int(b.max_seg)
 
 

@@ -68,7 +68,7 @@ def _run(p, V, K, W, H, vr, va):
     r = b.rect.view(-1, 2).to(torch.int64)[cn] & 0xFFFFFFFF
     x0, x1, y0 = r[:, 0] & 0xFFFF, r[:, 0] >> 16, r[:, 1] & 0xFFFF
     kexp = b.isect_off.to(torch.int64)[cn] + (t // b.tw - y0) * (x1 - x0) + (t % b.tw - x0)
-    assert torch.equal(b.k_of_s[:n].long()[consumed], kexp), "k_of_s is not the emission index"
+    assert torch.equal(b.k_of_s[:n].long()[consumed] & 0x0FFFFFFF, kexp), "k_of_s is not the emission index"
     flagged = int(b.lazy[3 * CT]) if getattr(b, "n_lazy", 0) else 0
     return (rgb.detach(), alpha.detach(), pg.grad.detach(), te.clone(), ids, b.tile_cut.clone()), flagged, b
 

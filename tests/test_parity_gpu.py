@@ -215,7 +215,7 @@ def _check_binning_exact(p, V, K, W, H, C, cuda):
     # k_of_s: the emission entry of each sorted entry (a permutation).  The (c,n) ranges
     # [isect_offset, +count) tile [0, I) (workgroup arrival order), and emission entry
     # k = isect_offset[cn] + j belongs to Gaussian cn and to tile j (row-major) of its rect
-    ks = b.k_of_s.cpu()[:I].to(torch.int64)
+    ks = b.k_of_s.cpu()[:I].to(torch.int64) & 0x0FFFFFFF   # bits 28..31: quadrant masks
     assert torch.equal(torch.sort(ks).values, torch.arange(I))
     off = b.isect_off.cpu()[:C * N].to(torch.int64)
     nz = cnt > 0
