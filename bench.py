@@ -118,10 +118,10 @@ def parse(argv=None):
     ap.add_argument("--lazy", type=str, default="",
                     help="MIN_LEN,PREFIX: lazy depth order for 3D lists longer than MIN_LEN, sorted prefix "
                          ">= PREFIX entries (gsr_set_lazy_sort; default 16384,4096; MIN_LEN 0 disables)")
-    ap.add_argument("--masks", type=int, default=1, choices=[0, 1],
+    ap.add_argument("--masks", type=int, default=0, choices=[0, 1],
                     help="3D quadrant masks (gsr.render.set_quadrant_masks): the emission records which 8x8 "
                          "quadrants each list entry reaches and the raster forward gathers only those (same "
-                         "outputs bit for bit); 0 for A/B measurements")
+                         "outputs bit for bit; off by default: slower end to end, DESIGN.md §4)")
     ap.add_argument("--pmc-dir", default=PROFILES, help="where the per-config rocprofv3 PMC passes live")
     ap.add_argument("--chunk-entries", type=str, default="",
                     help="3D,2D backward work-unit lengths (gsr.render.set_chunk_entries; default 128,512)")

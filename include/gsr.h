@@ -143,7 +143,10 @@ int gsr_version(void);
  * gsr_rows_scatter_add, GSR_OVF_EXCHANGE); quadrant masks: gsr_bin_emit / gsr_bin_sort /
  * gsr_bin_sort_lazy take `rec` after `depth`, gsr3d_raster_fwd takes `k_of_s` after
  * `sorted_ids`, gsr_bin_stats.masks (the former reserved32) says whether they were stored. */
-#define GSR_ABI_VERSION 5
+/* Revision 6: 2D chunk records are T anchors (one float per pixel per chunk: T at the chunk's
+ * start, written by gsr2d_raster_fwd), the 2D chunk list holds one unit per tile and
+ * gsr2d_raster_bwd's n_chunks bounds the busy tiles (k_raster2d_bwd_tile). */
+#define GSR_ABI_VERSION 6
 int gsr_abi_version(void);
 const char* gsr_last_error(void);
 
@@ -358,8 +361,11 @@ int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t*
                      const int32_t* k_of_s, float* partial, void* stream);
 
 /* 2D index-order compositor (src/gaussian_renderer.py:416-425), integer pixel centres, on
- * the 3D kernels' structure (C cameras of gsr2d_project_fwd, index-order keys, the forward's chunk records feed a
- * chunk-parallel backward).  rgb = canvas + (1-A)*bg, alpha = A.  Arithmetic in
+ * the 3D kernels' structure (C cameras of gsr2d_project_fwd, index-order keys).  Since ABI 6
+ * chunk_state holds T anchors: float [chunks][256], row chunk_base[t] + k = the T of each pixel
+ * of tile t at the start of its k-th chunk of chunk_entries entries (k >= 1; written only while
+ * the pixel is live), and chunk_list gets ONE unit {start, tile_end - start, chunk_base, tile} per
+ * tile with a consumed entry (the per-tile backward).  rgb = canvas + (1-A)*bg, alpha = A.  Arithmetic in
  * transmittance form; a pixel stops after the entry that takes T to <= 2^-25 (the
  * reference's A == 1.0f).  Pairs with alpha < eps_cut (the binning's extent cut) are left
  * out.  bg [C,3]; rgb [C,H,W,3], alpha [C,H,W]; final_T [C,H,W,2] = (T_final, T before the
@@ -371,7 +377,9 @@ int gsr2d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t*
                      uint64_t* tile_cut, float* chunk_state, int32_t* chunk_list, void* stream);
 
 /* Backward of gsr2d_raster_fwd (the reference's autograd of the recursion), same contract
- * as gsr3d_raster_bwd. */
+ * as gsr3d_raster_bwd except that the units are whole tiles: n_chunks bounds the BUSY TILES
+ * (the grid; stats->n_active is the device count), one workgroup walks its tile's list back to
+ * front, re-anchoring T from chunk_state at every chunk_entries boundary. */
 int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_end, const int32_t* chunk_base, const float* chunk_state,
                      const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,

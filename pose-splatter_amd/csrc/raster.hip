@@ -27,6 +27,18 @@ constexpr int kFwdLdsPad = GSR_FWD_PAD_3D;
 #endif
 constexpr int kFwdLdsPad2D = GSR_FWD_PAD_2D;
 static int g_fwd_lanes = 0;   // gsr_set_fwd_lanes: 0 automatic, 1 / 4 / 16 forced
+// box forward (k_raster_fwd_box) build knobs, for A/B measurements: lanes grouped by box along
+// the ds_read_b128 lane groups, and the 2D walk's records packed into 2 x b128 + b32
+#ifndef GSR_BOX_LANES
+#define GSR_BOX_LANES 1
+#endif
+#ifndef GSR_BOX_PACK
+#define GSR_BOX_PACK 1
+#endif
+#ifndef GSR_BOX_K4
+#define GSR_BOX_K4 0   // 2D walk: survivor slots read four per b32 (1; measured slower at config 4: 9.55 vs 9.05 ms)
+#endif
+constexpr int kBoxStride = 132;   // survivor-list row of one 4x4 box (128 + a read-ahead word)
 
 
 __device__ __forceinline__ void tile_coords(int ct, int tw, int th, int& c, int& ty, int& tx) {
@@ -45,7 +57,34 @@ __device__ __forceinline__ void tile_coords(int ct, int tw, int th, int& c, int&
 // four boxes (box b at (qx + 4 (b & 1), qy + 4 (b >> 1))); box b's survivors are appended in
 // list order to boxl[b * stride + ..].  n[b]: the four counts (wave-uniform).  (A lane per
 // (survivor, box) pair read every record four times and walked 16 survivors per round trip.)
-template <bool IS2D>
+// Record parts as the 2D box forward stages them in LDS (PACKED): q0 = (x, y, opacity, r),
+// q1 = (a, b, c, g), q2 = (b_colour, L, -b/2c, -b/2a) -- the walk's nine values in two b128
+// reads and one b32 instead of three b128; unpack_rec restores the Splat parts for the culls.
+__device__ __forceinline__ void pack_rec(float4& p0, float4& p1, float4& p2) {
+  const float4 q0 = make_float4(p0.x, p0.y, p0.z, p2.x);
+  const float4 q1 = make_float4(p1.x, p1.y, p1.z, p2.y);
+  const float4 q2 = make_float4(p2.z, p0.w, p1.w, p2.w);
+  p0 = q0;
+  p1 = q1;
+  p2 = q2;
+}
+template <bool PACKED>
+__device__ __forceinline__ void unpack_rec(float4& p0, float4& p1, float4& p2) {
+  if constexpr (PACKED) {
+    const float4 s0 = make_float4(p0.x, p0.y, p0.z, p2.y);
+    const float4 s1 = make_float4(p1.x, p1.y, p1.z, p2.z);
+    const float4 s2 = make_float4(p0.w, p1.w, p2.x, p2.w);
+    p0 = s0;
+    p1 = s1;
+    p2 = s2;
+  }
+}
+
+// Survivor-list slot of list position p when the backward reads its groups of 7 as one 8-byte
+// word: a pad byte after every 7 (p + p / 7; the multiply-shift is exact for p < 400).
+__device__ __forceinline__ int grouped_slot(int p) { return p + ((p * 293) >> 11); }
+
+template <bool IS2D, bool PACKED = false, bool GROUPED = false>
 __device__ __forceinline__ void box4_cull(const unsigned char* __restrict__ list, int nsurv, const float4* r0,
                                           const float4* r1, const float4* r2, float qx, float qy,
                                           unsigned char* boxl, int stride, int (&n)[4]) {
@@ -56,13 +95,17 @@ __device__ __forceinline__ void box4_cull(const unsigned char* __restrict__ list
     const int s = s0 + lane;
     const bool in = s < nsurv;
     const int k = list[in ? s : 0];
-    const float4 a = r0[k], b = r1[k], c = r2[k];
+    float4 a = r0[k], b = r1[k], c = r2[k];
+    unpack_rec<PACKED>(a, b, c);
 #pragma unroll
     for (int bx = 0; bx < 4; ++bx) {
       const float x0 = qx + (float)((bx & 1) * 4), y0 = qy + (float)((bx >> 1) * 4);
       const bool keep = in && cull_keep<IS2D>(a, b, c, x0, x0 + 3.f, y0, y0 + 3.f);
       const unsigned long long m = __ballot(keep);
-      if (keep) boxl[bx * stride + n[bx] + __popcll(m & below)] = (unsigned char)k;
+      if (keep) {
+        const int p = n[bx] + __popcll(m & below);
+        boxl[bx * stride + (GROUPED ? grouped_slot(p) : p)] = (unsigned char)k;
+      }
       n[bx] += __popcll(m);
     }
   }
@@ -587,7 +630,9 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
     if (__ballot(!done) == 0ull) return false;
     if (b0 > start && ((b0 - start) & umask) == 0) {   // entering chunk kcur+1
       const float Dr = quad_sum(dr), Dg = quad_sum(dg), Db = quad_sum(db);
-      if (q == 0 && ckpt) ckpt[(int64_t)(cbase + kcur) * kRasterThreads + bwd_pixel_slot(il, jl)] = make_float4(Ts, Dr, Dg, Db);
+      // 2D: the pixel's T anchor at the chunk start (k_raster2d_bwd_tile)
+      if (q == 0 && ckpt)
+        reinterpret_cast<float*>(ckpt)[(int64_t)(cbase + kcur + 1) * kRasterThreads + bwd_pixel_slot(il, jl)] = T;
       cr += Dr;
       cg += Dg;
       cb += Db;
@@ -674,7 +719,8 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
   } else {
     last = PG::max_i(last);
   }
-  if (end > start && ckpt) {   // (no chunk records: a forward with no backward to follow)
+  // (no chunk records: a forward with no backward to follow; 2D: the T anchors are final)
+  if (!IS2D && end > start && ckpt) {
     // Turn this pixel's chunk records {T at chunk start, chunk colour sum} into what the
     // backward needs at each chunk's END: {T_end, suffix colour sum of the later chunks}
     // (positive terms, summed back to front).  The pixel's LPP lanes split the chunks into
@@ -778,8 +824,12 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
     const int32_t* __restrict__ chunk_base, int n_busy, int64_t CT,
     uint64_t* __restrict__ tile_cut, float cut2d, const FwdLazy lz, const gsr_bin_stats* __restrict__ stats) {
   (void)kos;   // one workgroup per tile: the waves' own quadrant culls decide
+  constexpr bool PACK = IS2D && GSR_BOX_PACK;   // 2D walk: records staged packed (pack_rec)
   __shared__ float4 s_r[2][3][256];              // round records, part j of slot i at s_r[buf][j][i]
-  __shared__ unsigned char s_box[4][4][129];     // ... and each box's, in list order (+1: read-ahead)
+  // ... and each box's survivors, in list order; 2D reads them four at a time (one b32 per four
+  // steps, the next word read ahead: +4), the row stride (132 B = 33 banks) puts the two boxes
+  // of a 32-lane half in different banks
+  __shared__ __attribute__((aligned(16))) unsigned char s_box[4][4][kBoxStride];
   __shared__ int s_max;
   static_assert(kChunk3 == 128, "a round half is one chunk");
   const int busy_blocks = (n_busy + 7) & ~7;   // n_busy: the grid's bound (see k_raster_fwd)
@@ -809,7 +859,16 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
   int c, ty, tx;
   tile_coords(ct, tw, th, c, ty, tx);
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#if GSR_BOX_LANES
+  // box = the lane's ds_read_b128 group ((bit 5, bit 4 ^ bit 3 ^ bit 2), MI355X_MICROARCH.md
+  // §LDS): every b128 record read of the walk is one address per lane group, a broadcast, so
+  // the four boxes' different entries never meet on a bank (with box = lane & 3 every group
+  // held all four boxes: +32 % LDS cycles in bank conflicts at config 4, r03 PMC)
+  const int box = ((lane >> 4) & 2) | (((lane >> 4) ^ (lane >> 3) ^ (lane >> 2)) & 1);
+  const int pos = (lane & 3) | ((lane >> 1) & 12);
+#else
   const int box = lane & 3, pos = lane >> 2;
+#endif
   const float off = IS2D ? 0.f : 0.5f;   // 2D: integer centres (src/gaussian_renderer.py:355-358)
   const int qx0 = tx * kTile + (wv & 1) * 8, qy0 = ty * kTile + (wv >> 1) * 8;   // quadrant origin
   const int bx0i = qx0 + (box & 1) * 4, by0i = qy0 + (box >> 1) * 4;             // box origin
@@ -840,6 +899,7 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
   }
   int buf = 0;
   for (int rb = start; rb < end; rb += 256, buf ^= 1) {
+    if constexpr (PACK) pack_rec(c0, c1, c2);
     s_r[buf][0][threadIdx.x] = c0;
     s_r[buf][1][threadIdx.x] = c1;
     s_r[buf][2][threadIdx.x] = c2;
@@ -859,7 +919,12 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
       const int hb = rb + 128 * h;
       if (hb >= end || __ballot(!done) == 0ull) break;
       if (hb > start && ((hb - start) & umask) == 0) {   // entering chunk kcur+1 (every few halves)
-        if (ckpt) ckpt[(int64_t)(cbase + kcur) * kRasterThreads + ckpt_slot_of(wv, box, pos)] = make_float4(Ts, dr, dg, db);
+        if (IS2D) {   // 2D: the pixel's T anchor at the chunk start (k_raster2d_bwd_tile)
+          if (ckpt)
+            reinterpret_cast<float*>(ckpt)[(int64_t)(cbase + kcur + 1) * kRasterThreads + ckpt_slot_of(wv, box, pos)] = T;
+        } else {
+          if (ckpt) ckpt[(int64_t)(cbase + kcur) * kRasterThreads + ckpt_slot_of(wv, box, pos)] = make_float4(Ts, dr, dg, db);
+        }
         cr += dr;
         cg += dg;
         cb += db;
@@ -876,8 +941,9 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
         for (int q = 0; q < 2; ++q) {
           const int k = q * 64 + lane;
           const int sl = 128 * h + k;
-          const bool keep = k < nh && cull_keep<IS2D>(s_r[buf][0][sl], s_r[buf][1][sl], s_r[buf][2][sl], x0,
-                                                     x0 + 7.f, y0, y0 + 7.f);
+          float4 r0 = s_r[buf][0][sl], r1 = s_r[buf][1][sl], r2 = s_r[buf][2][sl];
+          unpack_rec<PACK>(r0, r1, r2);
+          const bool keep = k < nh && cull_keep<IS2D>(r0, r1, r2, x0, x0 + 7.f, y0, y0 + 7.f);
           const unsigned long long m = __ballot(keep);
           if (keep)
             s_list_w[nsurv + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
@@ -889,8 +955,8 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
       __builtin_amdgcn_wave_barrier();
       // ... and the quadrant's survivors against each 4x4 box
       int nbx[4];
-      box4_cull<IS2D>(s_list_w, nsurv, &s_r[buf][0][128 * h], &s_r[buf][1][128 * h], &s_r[buf][2][128 * h],
-                      (float)qx0 + off, (float)qy0 + off, &s_box[wv][0][0], 129, nbx);
+      box4_cull<IS2D, PACK>(s_list_w, nsurv, &s_r[buf][0][128 * h], &s_r[buf][1][128 * h], &s_r[buf][2][128 * h],
+                            (float)qx0 + off, (float)qy0 + off, &s_box[wv][0][0], kBoxStride, nbx);
       const int nb = box == 0 ? nbx[0] : box == 1 ? nbx[1] : box == 2 ? nbx[2] : nbx[3];
       __builtin_amdgcn_wave_barrier();
       // steps walked by the wave: max over its boxes
@@ -902,31 +968,60 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
         // many scalar as vector instructions on exec masks): a box's list is padded to the
         // wave's step count with a real quadrant survivor (finite record), which a step past
         // nb reads and leaves out by select -- the same sums, bit for bit.
-        for (int s = nb + pos; s < nmax; s += 16) s_box[wv][box][s] = s_list_w[0];
+        // Steps go four at a time (one b32 read of four survivor slots, the next word read one
+        // iteration ahead), so the list is padded to whole fours.
+        const int nmax4 = (nmax + 3) & ~3;
+        unsigned char* const lst = s_box[wv][box];
+        for (int s = nb + pos; s < nmax4; s += 16) lst[s] = s_list_w[0];
         __builtin_amdgcn_wave_barrier();
-        int k_next = s_box[wv][box][0];
+        const uint32_t* const lst4 = reinterpret_cast<const uint32_t*>(lst);
+        uint32_t k4 = 0, k4_next = GSR_BOX_K4 ? lst4[0] : lst[0];
+        int lk = -1;
+#pragma nounroll
         for (int t = 0; t < nmax; ++t) {
-          const int k = k_next;
-          k_next = s_box[wv][box][t + 1];   // past the padded list: read, never used
-          __builtin_assume((unsigned)k < 128u);
-          const float4* rk = rh + k;   // the half's records: part j at rk[256 j]
-          const float4 p0 = rk[0];
-          const float4 p1 = rk[256];
-          const float4 p2 = rk[512];
-          const float dx = p0.x - px, dy = p0.y - py;
-          const float sg = conic_sigma(p1, dx, dy);
-          const float alpha = p0.z * __expf(-sg);
-          const bool valid = t < nb && !done && alpha >= cut2d;
-          const float vis = valid ? alpha * T : 0.f;
-          dr += p2.x * vis;
-          dg += p2.y * vis;
-          db += p2.z * vis;
-          Tl = valid ? T : Tl;
-          T = valid ? T * (1.f - alpha) : T;
-          last = valid ? hb + k : last;
-          done = done || (valid && T <= kT2DMin);   // the reference's A == 1.0f, after this entry
+          int k;
+          if constexpr (GSR_BOX_K4) {
+            if ((t & 3) == 0) {   // (wave-uniform)
+              k4 = k4_next;
+              k4_next = lst4[(t >> 2) + 1];   // past the padded list: read, never used
+            }
+            k = (int)(k4 & 0xFFu);
+            k4 >>= 8;
+          } else {
+            k = (int)k4_next;
+            k4_next = lst[t + 1];
+          }
+          {
+            const float4* rk = rh + k;   // the half's records: part j at rk[256 j]
+            float4 p0 = rk[0], p1 = rk[256];
+            float cb_;
+            if constexpr (PACK) {
+              cb_ = reinterpret_cast<const float*>(rk + 512)[0];   // q2.x: the blue channel (b32)
+            } else {
+              const float4 p2 = rk[512];
+              p0.w = p2.x;
+              p1.w = p2.y;
+              cb_ = p2.z;
+            }
+            const float dx = p0.x - px, dy = p0.y - py;
+            const float sg = conic_sigma(p1, dx, dy);
+            const float alpha = p0.z * __expf(-sg);
+            const bool valid = t < nb && !done && alpha >= cut2d;
+            // an invalid step enters with alpha 0: vis = 0 and T * (1 - 0) = T exactly (one
+            // select instead of three); the entry slot of the latest composite is kept per half
+            const float av = valid ? alpha : 0.f;
+            const float vis = av * T;
+            dr += p0.w * vis;
+            dg += p1.w * vis;
+            db += cb_ * vis;
+            Tl = valid ? T : Tl;
+            T = T * (1.f - av);
+            lk = valid ? k : lk;
+            done = done || (valid && T <= kT2DMin);   // the reference's A == 1.0f, after this entry
+          }
           if ((t & 31) == 31 && __ballot(!done) == 0ull) break;
         }
+        if (lk >= 0) last = hb + lk;
         __builtin_amdgcn_wave_barrier();
         continue;
       }
@@ -978,7 +1073,7 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
   cr += dr;
   cg += dg;
   cb += db;
-  if (end > start && ckpt) {
+  if (!IS2D && end > start && ckpt) {   // (2D: the T anchors are final as written)
     // chunk records {T at chunk start, chunk colour} -> what the backward needs at each chunk's
     // END: {T_end, suffix colour sum of the later chunks}, back to front (records re-read 8 at a time)
     float4* ck = ckpt + (int64_t)cbase * kRasterThreads + ckpt_slot_of(wv, box, pos);
@@ -1032,7 +1127,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_finalize(
     const float* __restrict__ depth, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ order, int n_busy, const int32_t* __restrict__ chunk_base,
     int32_t* __restrict__ tile_end, uint64_t* __restrict__ tile_cut, gsr_bin_stats* __restrict__ stats,
-    int32_t* __restrict__ chunk_list, int key_order) {
+    int32_t* __restrict__ chunk_list, int key_order, int tile_units) {
   const int ovf = stats->overflow;
   if (ovf) {   // bounded call over its bounds: report to the caller's sticky status, nothing else
     if (blockIdx.x == 0 && threadIdx.x == 0 && stats->status != nullptr) atomicOr(stats->status, ovf);
@@ -1052,7 +1147,8 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_finalize(
     tile_end[ct] = te;
     tile_cut[ct] = te < end ? sort_key(depth, ids[te], key_order) : ~0ull;
   }
-  const int U = stats->chunk_entries;
+  // tile_units (2D): one backward unit per tile, its whole consumed list [start, te)
+  const int U = tile_units ? max(te - start, 1) : stats->chunk_entries;
   const int nact = (te - start + U - 1) / U;
   // one atomic per wave on the active-chunk counter (one per tile serialised ~700 atomics on
   // one address at config 3)
@@ -1420,7 +1516,9 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
     }
     // the next (earlier) sub-chunk's ids, sort positions and records, gathered while this
     // one's rows are summed and stored (not during the walk: registers)
+    // (assigned on every path: a conditional assignment keeps the old values live across the walk)
     int kos_next = 0;
+    if (MULTI) sp0 = sp1 = sp2 = make_float4(0.f, 0.f, 0.f, 0.f);
     if (sub > 0 && threadIdx.x < kChunk3) {
       const int id_next = ids[sb0 - kChunk3 + threadIdx.x];
       kos_next = k_of_s[sb0 - kChunk3 + threadIdx.x];
@@ -1461,6 +1559,297 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
   }
 #endif
 }
+// ---------------------------------------------------------------- 2D backward, per tile
+// The 2D (index-order) lists never terminate early (I_eff = I), so every tile is long and busy:
+// config 4 has 55 296 tiles of ~2 090 entries, far more tiles than the chip's workgroup slots,
+// and the chunk-parallel backward's price -- per 128-entry chunk a 16-B {T_end, suffix colour}
+// record per pixel (written, read back and rewritten by the forward's epilogue, read by the
+// backward) and the pixel's 28-B state re-read -- bought no parallelism the tiles did not
+// already give.  Here ONE workgroup walks a tile's whole consumed list [start, tile_end) back to
+// front in 128-entry sub-chunks (same layout, culls, transposed box reduction and staged LDS sums
+// as k_raster_bwd).  The pixel state is read once per tile; mu (mu form: the value of everything
+// after the entry over T) carries from one sub-chunk into the previous one -- no suffix colour
+// sums; T is re-anchored at every unit boundary (stats->chunk_entries entries) from the
+// forward's T record (4 B per pixel per unit, written once), and inside a unit recovered as
+// T_{i+1} / (1 - a_i) exactly as in the chunk-parallel kernel.  Partial rows as there.
+#ifndef GSR_BWD2D_MINB
+#define GSR_BWD2D_MINB 5
+#endif
+#ifndef GSR_BWD2D_LDS
+#define GSR_BWD2D_LDS 1
+#endif
+#ifndef GSR_BWD2D_EARLY
+#define GSR_BWD2D_EARLY 0
+#endif
+#ifndef GSR_BWD2D_ROWS2
+#define GSR_BWD2D_ROWS2 1
+#endif
+__global__ __launch_bounds__(kRasterThreads, GSR_BWD2D_MINB) void k_raster2d_bwd_tile(
+    const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const float* __restrict__ anchors, int W, int H,
+    int tw, int th, const float* __restrict__ bg, const float* __restrict__ final_T,
+    const int32_t* __restrict__ last_in, const float* __restrict__ v_rgb, const float* __restrict__ v_alpha,
+    float* __restrict__ partial, const int32_t* __restrict__ units, gsr_bin_stats* __restrict__ stats,
+    const int32_t* __restrict__ k_of_s, float cut2d) {
+  constexpr int kNull = kChunk3;
+  constexpr int kGroup = GSR_BWD_GROUP;
+  constexpr int kLen = kChunk3 + kGroup;
+  // PK: records staged packed (pack_rec: the walk's nine values in 2 x b128 + b32) and each box's
+  // survivor list with a pad byte after every 7 (grouped_slot), so a group's seven slots are ONE
+  // 8-byte read instead of seven byte reads
+  constexpr bool PK = GSR_BWD2D_LDS;
+  constexpr bool EARLY = GSR_BWD2D_EARLY;
+  constexpr bool ROWS2 = GSR_BWD2D_ROWS2;
+  constexpr int kLenB = PK ? 8 * ((kLen + kGroup - 1) / kGroup) : kLen;
+  __shared__ float4 s_p[3][kChunk3 + 1];
+  __shared__ __attribute__((aligned(16))) float L[kPartial][4][kChunk3 + 1];
+  __shared__ unsigned char s_list[4][kLen];
+  __shared__ __attribute__((aligned(16))) unsigned char s_box[4][4][kLenB];
+  __shared__ float s_stage[4][64][4];
+#ifdef GSR_BWD_TRACE
+  // timing build (tools/bwd2d_trace.py): {start, end, nsub | cu << 32, wave 0's summed phases:
+  // top barrier + staging, culls, groups, pre-rows barrier, rows}
+  unsigned long long tr_t = wall_clock64(), tr_acc[5] = {0, 0, 0, 0, 0};
+  const unsigned long long tr_start = tr_t;
+#define BWD2_P(i)                                     \
+  if (threadIdx.x == 0) {                              \
+    const unsigned long long now_ = wall_clock64();    \
+    tr_acc[i] += now_ - tr_t;                          \
+    tr_t = now_;                                       \
+  }
+#else
+#define BWD2_P(i)
+#endif
+  // the unit {first entry, entries, first record row, tile}, the stats words: one round trip
+  const int4 cd = reinterpret_cast<const int4*>(units)[blockIdx.x];
+  const int n_act = stats->n_active, ovf = stats->overflow, U = stats->chunk_entries;
+  if ((ovf != 0) | ((int)blockIdx.x >= n_act) | (cd.y <= 0)) return;
+  const int start = cd.x, n = cd.y, cbase = cd.z, ct = cd.w;
+  int c, ty, tx;
+  tile_coords(ct, tw, th, c, ty, tx);
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int box = lane & 3, pos = lane >> 2;
+  const int qx0 = tx * kTile + (wv & 1) * 8, qy0 = ty * kTile + (wv >> 1) * 8;   // quadrant origin
+  const int pi = qy0 + (box >> 1) * 4 + (pos >> 2), pj = qx0 + (box & 1) * 4 + (pos & 3);
+  const bool inside = pi < H && pj < W;
+  const float px = (float)pj, py = (float)pi;   // 2D: integer centres (src/gaussian_renderer.py:355-358)
+  const int slot = ckpt_slot_of(wv, box, pos);
+  // the last sub-chunk [sb0, sb0 + sn): its ids, emission indices and records first
+  const int nsub = (n + kChunk3 - 1) / kChunk3;
+  int sb0 = start + (nsub - 1) * kChunk3;
+  int sn = start + n - sb0;
+  int id_mine = threadIdx.x < sn ? ids[sb0 + threadIdx.x] : 0;
+  // the rows' emission index: entry threadIdx.x (ROWS2: entry threadIdx.x / 2, two threads per row)
+  const int rsel = ROWS2 ? (int)threadIdx.x >> 1 : (int)threadIdx.x;
+  int kos_mine = rsel < sn ? k_of_s[sb0 + rsel] : 0;
+  float Tf = 1.f, Tl = 1.f, vr = 0.f, vg = 0.f, vb = 0.f, va = 0.f;
+  int last = -1;
+  if (inside) {
+    const int64_t pix = ((int64_t)c * H + pi) * W + pj;
+    last = last_in[pix];
+    const float2 t2 = reinterpret_cast<const float2*>(final_T)[pix];
+    Tf = t2.x;
+    Tl = t2.y;
+    vr = v_rgb[pix * 3 + 0];
+    vg = v_rgb[pix * 3 + 1];
+    vb = v_rgb[pix * 3 + 2];
+    va = v_alpha[pix];
+  }
+  const float4* const rec4 = reinterpret_cast<const float4*>(rec);
+  float4 sp0 = make_float4(0.f, 0.f, 0.f, 0.f), sp1 = sp0, sp2 = sp0;
+  if (threadIdx.x < sn) {
+    sp0 = rec4[3 * (int64_t)id_mine + 0];
+    sp1 = rec4[3 * (int64_t)id_mine + 1];
+    sp2 = rec4[3 * (int64_t)id_mine + 2];
+  }
+  const float* bgc = bg + c * 3;
+  // mu after the pixel's last entry; T at the list's end is the final T (tile_end - 1 is the
+  // tile's last composited entry, so no pixel has a valid entry after it)
+  float mu = bgc[0] * vr + bgc[1] * vg + bgc[2] * vb - va;
+  float T = Tf;
+  const int wlast = wave_max_i(last);
+  const int fg = lane / kPartial, fq = lane - kPartial * (lane / kPartial);
+  const bool fown = lane < kGroup * kPartial;
+  float* const Lw = &L[fq][wv][0];
+  const float* const stage_rd = &s_stage[wv][0][0] + 4 * (4 * (lane >> 2)) + (lane & 3);   // + 4*box
+  const unsigned char* my_list = s_box[wv][box];
+  for (int sub = nsub - 1; sub >= 0; --sub) {
+    if (sub != nsub - 1) {
+      // re-anchor T where this sub-chunk ends on a unit boundary (the forward wrote the pixel's T
+      // there if the pixel was still live, i.e. its last entry lies beyond; else T is Tf)
+      const int ue = sb0 + sn - start;
+      if ((ue & (U - 1)) == 0) T = last >= sb0 + sn ? anchors[(int64_t)(cbase + ue / U) * kRasterThreads + slot] : Tf;
+      __syncthreads();   // the previous sub-chunk's LDS is consumed
+    }
+    if (PK) pack_rec(sp0, sp1, sp2);
+    if (threadIdx.x < sn) {
+      s_p[0][threadIdx.x] = sp0;
+      s_p[1][threadIdx.x] = sp1;
+      s_p[2][threadIdx.x] = sp2;
+    }
+    for (int i = threadIdx.x; i < kPartial * (kChunk3 + 1); i += kRasterThreads)   // b128 stores
+      reinterpret_cast<float4*>(&L[0][0][0])[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (threadIdx.x == 0) {
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      s_p[0][kNull] = z;
+      s_p[1][kNull] = z;
+      s_p[2][kNull] = z;
+    }
+    __syncthreads();
+    BWD2_P(0);
+    const int lastk = min(last - sb0, kChunk3 - 1);   // < 0: the pixel stopped before this sub-chunk
+    const int lastq = last - sb0 < kChunk3 ? last - sb0 : -1;
+    int nsurv = 0;
+    {
+      const float x0 = (float)qx0, y0 = (float)qy0;
+#pragma unroll
+      for (int q = kChunk3 / 64 - 1; q >= 0; --q) {
+        const int k = q * 64 + lane;
+        float4 r0 = s_p[0][k], r1 = s_p[1][k], r2 = s_p[2][k];
+        unpack_rec<PK>(r0, r1, r2);
+        const bool keep = k < sn && (sb0 + k) <= wlast && cull_keep<true>(r0, r1, r2, x0, x0 + 7.f, y0, y0 + 7.f);
+        const unsigned long long mk = __ballot(keep);
+        if (keep) {
+          const unsigned long long above = lane == 63 ? 0ull : (mk >> (lane + 1));
+          s_list[wv][nsurv + __popcll(above)] = (unsigned char)k;
+        }
+        nsurv += __popcll(mk);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    int nbx[4];
+    box4_cull<true, PK, PK>(s_list[wv], nsurv, s_p[0], s_p[1], s_p[2], (float)qx0, (float)qy0, &s_box[wv][0][0],
+                            kLenB, nbx);
+    const int nb = box == 0 ? nbx[0] : box == 1 ? nbx[1] : box == 2 ? nbx[2] : nbx[3];
+    const int ngrp = max(max(nbx[0], nbx[1]), max(nbx[2], nbx[3]));
+    const int npad = (ngrp + kGroup - 1) / kGroup * kGroup;
+    for (int s = nb + pos; s < npad; s += 16) s_box[wv][box][PK ? grouped_slot(s) : s] = (unsigned char)kNull;
+    __builtin_amdgcn_wave_barrier();
+    BWD2_P(1);
+    // EARLY: the previous sub-chunk's ids / records issued before the walk (in flight during it)
+    int kos_next = 0;
+    if (EARLY) {
+      sp0 = sp1 = sp2 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (sub > 0 && threadIdx.x < kChunk3) {
+        const int id_next = ids[sb0 - kChunk3 + threadIdx.x];
+        if (!ROWS2) kos_next = k_of_s[sb0 - kChunk3 + threadIdx.x];
+        sp0 = rec4[3 * (int64_t)id_next + 0];
+        sp1 = rec4[3 * (int64_t)id_next + 1];
+        sp2 = rec4[3 * (int64_t)id_next + 2];
+      }
+    }
+    // the walk (as k_raster_bwd, IS2D): invalid pairs enter with alpha 0 (ra = 1, no change)
+    for (int g0 = 0, gb = 0; g0 < ngrp; g0 += kGroup, gb += 8) {
+      float acc[64];
+      acc[63] = 0.f;
+      const uint2 w8 = PK ? *reinterpret_cast<const uint2*>(my_list + gb) : make_uint2(0u, 0u);
+#pragma unroll
+      for (int g = 0; g < kGroup; ++g) {
+        const int k = PK ? (int)(((g < 4 ? w8.x : w8.y) >> (8 * (g & 3))) & 0xFFu) : my_list[g0 + g];
+        float4 p0 = s_p[0][k];
+        float4 p1 = s_p[1][k];
+        float4 p2;
+        if (PK) {
+          p2 = make_float4(p0.w, p1.w, reinterpret_cast<const float*>(&s_p[2][k])[0], 0.f);   // the colour
+        } else {
+          p2 = s_p[2][k];
+        }
+        const float dx = p0.x - px, dy = p0.y - py;
+        const float sigma = conic_sigma(p1, dx, dy);
+        const float alpha = p0.z * __expf(-sigma);
+        const bool valid = k <= lastk && alpha >= cut2d;
+        const float alpha_v = valid ? alpha : 0.f;
+        const float ra = __builtin_amdgcn_rcpf(1.f - alpha_v);
+        T = k == lastq ? Tl : T * ra;
+        const float fac = alpha_v * T;
+        acc[g * kPartial + 6] = fac * vr;
+        acc[g * kPartial + 7] = fac * vg;
+        acc[g * kPartial + 8] = fac * vb;
+        const float cv = p2.x * vr + p2.y * vg + p2.z * vb;
+        const float dmu = cv - mu;
+        const float v_sig = -alpha_v * (T * dmu);
+        mu = mu + alpha_v * dmu;
+        const float tx_ = v_sig * dx, ty_ = v_sig * dy;
+        acc[g * kPartial + 0] = tx_;
+        acc[g * kPartial + 1] = ty_;
+        acc[g * kPartial + 2] = tx_ * dx;
+        acc[g * kPartial + 3] = tx_ * dy;
+        acc[g * kPartial + 4] = ty_ * dy;
+        acc[g * kPartial + 5] = v_sig;
+      }
+      float sum[4];
+      reduce_box16(acc, sum);
+      reinterpret_cast<float4*>(&s_stage[wv][0][0])[lane] = make_float4(sum[0], sum[1], sum[2], sum[3]);
+      __builtin_amdgcn_wave_barrier();
+      if (fown) {
+#pragma unroll
+        for (int bx = 0; bx < 4; ++bx) {
+          const int k = s_box[wv][bx][PK ? gb + fg : g0 + fg];
+          Lw[k] += stage_rd[4 * bx];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    // the previous sub-chunk's ids, emission indices and records, gathered while this one's rows
+    // are summed and stored
+    // (assigned on every path: a conditional assignment would keep the old values -- 14 VGPRs --
+    // live across the walk)
+    BWD2_P(2);
+    if (!EARLY) sp0 = sp1 = sp2 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ROWS2 && sub > 0) kos_next = k_of_s[sb0 - kChunk3 + rsel];
+    if (!EARLY && sub > 0 && threadIdx.x < kChunk3) {
+      const int id_next = ids[sb0 - kChunk3 + threadIdx.x];
+      if (!ROWS2) kos_next = k_of_s[sb0 - kChunk3 + threadIdx.x];
+      sp0 = rec4[3 * (int64_t)id_next + 0];
+      sp1 = rec4[3 * (int64_t)id_next + 1];
+      sp2 = rec4[3 * (int64_t)id_next + 2];
+    }
+    __syncthreads();
+    BWD2_P(3);
+    if (ROWS2) {
+      // two threads per row: the even one the mean / conic moments and v8, the odd one v4..v7
+      // (the same sums, the same row layout as store_partial_row)
+      const int k = rsel;
+      if (k < sn) {
+        float4* dst = reinterpret_cast<float4*>(partial + (int64_t)(kos_mine & kEmitIndexMask) * kPartialStride);
+        auto sum4 = [&](int q) { return (L[q][0][k] + L[q][1][k]) + (L[q][2][k] + L[q][3][k]); };
+        if ((threadIdx.x & 1) == 0) {
+          const float4 p1 = s_p[1][k];
+          const float mx = sum4(0), my = sum4(1);
+          dst[0] = make_float4(2.f * p1.x * mx + p1.y * my, p1.y * mx + 2.f * p1.z * my, sum4(2), sum4(3));
+          dst[2] = make_float4(sum4(8), 0.f, 0.f, 0.f);
+        } else {
+          dst[1] = make_float4(sum4(4), -sum4(5) / s_p[0][k].z, sum4(6), sum4(7));
+        }
+      }
+    } else if (threadIdx.x < sn) {
+      const int k = threadIdx.x;
+      float v[kPartial];
+#pragma unroll
+      for (int q = 0; q < kPartial; ++q) v[q] = (L[q][0][k] + L[q][1][k]) + (L[q][2][k] + L[q][3][k]);
+      const float4 p1 = s_p[1][k];
+      const float mx = v[0], my = v[1];
+      v[0] = 2.f * p1.x * mx + p1.y * my;
+      v[1] = p1.y * mx + 2.f * p1.z * my;
+      v[5] = -v[5] / s_p[0][k].z;
+      store_partial_row(partial, kos_mine & kEmitIndexMask, v);
+    }
+    BWD2_P(4);
+    sb0 -= kChunk3;
+    sn = kChunk3;
+    kos_mine = kos_next;
+  }
+#ifdef GSR_BWD_TRACE
+  if (threadIdx.x == 0 && g_bwd_trace != nullptr) {
+    unsigned long long* dst = g_bwd_trace + (int64_t)blockIdx.x * 16;
+    dst[0] = tr_start;
+    dst[1] = wall_clock64();
+    dst[2] = ((unsigned long long)__smid() << 32) | (unsigned)nsub;
+    for (int i = 0; i < 5; ++i) dst[3 + i] = tr_acc[i];
+  }
+#endif
+}
+#undef BWD2_P
+
 #ifdef GSR_BWD_TRACE
 extern "C" int gsr_debug_bwd_trace(void* buf) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_bwd_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
@@ -1581,7 +1970,7 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
   if (finalize && n_busy > 0 && chunk_list != nullptr) {
     hipLaunchKernelGGL(k_raster_finalize, dim3(ceil_div(n_busy, kRasterThreads)), dim3(kRasterThreads), 0, s,
                        depth, sorted_ids, tile_offset, tile_order, (int)n_busy, chunk_base, tile_end,
-                       tile_cut, stats, chunk_list, IS2D ? GSR_ORDER_INDEX : GSR_ORDER_DEPTH);
+                       tile_cut, stats, chunk_list, IS2D ? GSR_ORDER_INDEX : GSR_ORDER_DEPTH, IS2D ? 1 : 0);
   }
   GSR_LAUNCH_CHECK("k_raster_finalize");
   return GSR_OK;
@@ -1601,7 +1990,15 @@ static int raster_bwd(const char* who, const float* rec, const int32_t* sorted_i
   if (n_chunks == 0) return GSR_OK;
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   // n_chunks bounds the forward's active-chunk count (stats->n_active, device-side)
-  if (chunk_entries > kChunk3)
+  if constexpr (IS2D) {   // 2D: one unit per tile (n_chunks bounds the busy tiles)
+    (void)tile_offset;
+    (void)tile_end;
+    (void)chunk_base;
+    (void)lt;
+    hipLaunchKernelGGL(k_raster2d_bwd_tile, dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
+                       (const Splat*)rec, sorted_ids, chunk_state, width, height, tw, th, bg, final_T, last, v_rgb,
+                       v_alpha, partial, chunk_list, stats, k_of_s, cut2d);
+  } else if (chunk_entries > kChunk3)
     hipLaunchKernelGGL((k_raster_bwd<LOSS, IS2D, true>), dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
                        (const Splat*)rec, sorted_ids, tile_offset, tile_end, chunk_base,
                        (const float4*)chunk_state, width, height, tw, th, bg, final_T, last, v_rgb, v_alpha, partial,
@@ -1660,7 +2057,7 @@ int gsr3d_raster_fwd_lazy(const float* rec, const float* depth, int32_t* sorted_
   if (n_busy > 0 && chunk_list != nullptr) {
     hipLaunchKernelGGL(k_raster_finalize, dim3(ceil_div(n_busy, kRasterThreads)), dim3(kRasterThreads), 0,
                        (hipStream_t)stream, depth, sorted_ids, tile_offset, tile_order, (int)n_busy, chunk_base,
-                       tile_end, tile_cut, stats, chunk_list, GSR_ORDER_DEPTH);
+                       tile_end, tile_cut, stats, chunk_list, GSR_ORDER_DEPTH, 0);
     GSR_LAUNCH_CHECK("k_raster_finalize");
   }
   return GSR_OK;

@@ -109,13 +109,17 @@ class CapacityOverflowError(RuntimeError):
 _capacity_default = "exact"
 # 3D quadrant masks (include/gsr.h gsr_bin_emit `rec`): the emission stores which 8x8 quadrants
 # of its tile each list entry can reach, and the raster forward gathers an entry only for
-# those quadrants.  Same outputs bit for bit; off only for A/B measurements and tests.
-_quadrant_masks = True
+# those quadrants.  Same outputs bit for bit.  OFF by default: measured on MI355X (round 4,
+# profiles/r04_masks_ab.txt) the emission's four quadrant tests cost more than the gathers they
+# save -- config 3 emit 29 -> 45 us for raster fwd 106 -> 105 us (step 0.395 -> 0.403 ms),
+# config 5 emit 236 -> 366 us (2.25 -> 2.35 ms); the forward's span is its heavy tiles' serial
+# walks, not its gather traffic.
+_quadrant_masks = False
 _MASK_MAX_ENTRIES = 1 << 28   # the masks live in bits 28..31 of the emission index
 
 
 def set_quadrant_masks(on: bool) -> None:
-    """Enable (default) or disable the 3D quadrant masks (outputs are identical either way)."""
+    """Enable or disable (default) the 3D quadrant masks (outputs are identical either way)."""
     global _quadrant_masks
     _quadrant_masks = bool(on)
 # list entries per backward work unit (gsr_bin_caps.chunk_entries).  Units of several 128-entry
@@ -922,7 +926,8 @@ class _Render2D(torch.autograd.Function):
             with _timed("raster2d_bwd"):
               check(L.gsr2d_raster_bwd(q["rec"], q["sorted_ids"], q["tile_off"], q["tile_end"], q["chunk_base"],
                                      q["chunk_state"], q["chunk_list"], q["stats_dev"],
-                                     b.n_chunks, b.chunk_entries, C, width, height, eps_cut, _ptr(bgc), q["final_T"],
+                                     # 2D backward units are whole tiles (ABI 6): the grid bounds the busy tiles
+                                     b.n_busy, b.chunk_entries, C, width, height, eps_cut, _ptr(bgc), q["final_T"],
                                      q["last"],
                                      _ptr(v_rgb), _ptr(v_alpha), q["k_of_s"], _ptr(partial), stream),
                   "gsr2d_raster_bwd")
