@@ -146,7 +146,12 @@ int gsr_version(void);
 /* Revision 6: 2D chunk records are T anchors (one float per pixel per chunk: T at the chunk's
  * start, written by gsr2d_raster_fwd), the 2D chunk list holds one unit per tile and
  * gsr2d_raster_bwd's n_chunks bounds the busy tiles (k_raster2d_bwd_tile). */
-#define GSR_ABI_VERSION 6
+/* Revision 7: 2D records are stored once per parameter set (gsr2d_project_fwd writes the copy of
+ * each set's first camera only); gsr2d_raster_fwd / gsr2d_raster_bwd take N, set_begin, F (the
+ * same set CSR as gsr2d_project_fwd) to read it, visit the tiles in an XCD-aware sweep (the
+ * cameras of a set render a tile back to back on one XCD), and the 2D chunk list holds one
+ * unit per sweep slot: chunk_list needs >= C * tiles + 8 entries. */
+#define GSR_ABI_VERSION 7
 int gsr_abi_version(void);
 const char* gsr_last_error(void);
 
@@ -369,23 +374,29 @@ int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t*
  * transmittance form; a pixel stops after the entry that takes T to <= 2^-25 (the
  * reference's A == 1.0f).  Pairs with alpha < eps_cut (the binning's extent cut) are left
  * out.  bg [C,3]; rgb [C,H,W,3], alpha [C,H,W]; final_T [C,H,W,2] = (T_final, T before the
- * pixel's last composited entry). */
+ * pixel's last composited entry).  N, set_begin, F: the parameter sets of the cameras as given to
+ * gsr2d_project_fwd (the record of entry c*N+n is read from the copy of the first camera of
+ * c's set).  The tiles are visited in an XCD-aware sweep (tile_order is not used by the default
+ * one-lane-per-pixel layout). */
 int gsr2d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_order, const int32_t* chunk_base, int C, int width, int height,
                      float eps_cut, const float* bg, int32_t n_busy, gsr_bin_stats* stats,
                      float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
-                     uint64_t* tile_cut, float* chunk_state, int32_t* chunk_list, void* stream);
+                     uint64_t* tile_cut, float* chunk_state, int32_t* chunk_list, int64_t N,
+                     const int32_t* set_begin, int F, void* stream);
 
 /* Backward of gsr2d_raster_fwd (the reference's autograd of the recursion), same contract
- * as gsr3d_raster_bwd except that the units are whole tiles: n_chunks bounds the BUSY TILES
- * (the grid; stats->n_active is the device count), one workgroup walks its tile's list back to
- * front, re-anchoring T from chunk_state at every chunk_entries boundary. */
+ * as gsr3d_raster_bwd except that the units are whole tiles: the forward's finalize writes one
+ * unit per slot of the XCD-aware tile sweep and the backward runs one workgroup per slot
+ * (n_chunks is not used); each walks its tile's list back to front, re-anchoring T from
+ * chunk_state at every chunk_entries boundary.  N, set_begin, F: as gsr2d_raster_fwd. */
 int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_end, const int32_t* chunk_base, const float* chunk_state,
                      const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
                      int32_t chunk_entries, int C, int width, int height, float eps_cut, const float* bg,
                      const float* final_T, const int32_t* last, const float* v_rgb,
-                     const float* v_alpha, const int32_t* k_of_s, float* partial, void* stream);
+                     const float* v_alpha, const int32_t* k_of_s, float* partial, int64_t N,
+                     const int32_t* set_begin, int F, void* stream);
 
 /* ---------------------------------------------------------------- projection backward */
 

@@ -301,4 +301,46 @@ __device__ __forceinline__ int quad_mask(const float4 p0, const float4 p1, const
   return m;
 }
 
+// Parameter set of camera c: cameras are grouped by set, set f owning cameras
+// [set_begin[f], set_begin[f+1]) (null: one set).  Uniform per workgroup (scalar loads).
+__device__ __forceinline__ int set_of_camera(const int32_t* __restrict__ set_begin, int F, int c) {
+  if (set_begin == nullptr) return 0;
+  int f = 0;
+  while (f + 1 < F && set_begin[f + 1] <= c) ++f;
+  return f;
+}
+__device__ __forceinline__ int set_first_camera(const int32_t* __restrict__ set_begin, int F, int c) {
+  return set_begin == nullptr ? 0 : set_begin[set_of_camera(set_begin, F, c)];
+}
+
+// 2D: the record of entry id = c*N + n lives in the copy of camera c's set's first camera
+// (k_project2d_fwd writes one copy per set): rec[id + rec_offset2d(c)].
+__device__ __forceinline__ int64_t rec_offset2d(const int32_t* __restrict__ set_begin, int F, int c, int64_t N) {
+  return (int64_t)(set_first_camera(set_begin, F, c) - c) * N;
+}
+
+// 2D visit order, XCD-aware.  A grid of 8*S workgroups (S = ceil(CT/8)) is dealt to the 8 XCDs
+// round-robin by id, so workgroup b runs on XCD b % 8; it takes position (b % 8) * S + b / 8 of
+// the sweep (set, tile row, tile column, camera of the set).  Each XCD thus walks its eighth of
+// the sweep in order: the cameras of a set (identical lists over one shared record copy) render
+// a tile back to back, and tile rows follow each other, so each record comes from HBM into the
+// XCD's L2 about once per set instead of once per (camera, tile).  -1 past the end.
+__device__ __forceinline__ int sweep_tile2d(int b, int64_t CT, int T, const int32_t* __restrict__ set_begin, int F) {
+  const int64_t S = (CT + 7) / 8;
+  const int64_t p = (int64_t)(b & 7) * S + (b >> 3);
+  if (p >= CT) return -1;
+  int c0 = 0, c1 = (int)(CT / T);
+  if (set_begin != nullptr) {
+    int f = 0;
+    while (f + 1 < F && (int64_t)set_begin[f + 1] * T <= p) ++f;
+    c0 = set_begin[f];
+    c1 = set_begin[f + 1];
+  }
+  const int V = c1 - c0;
+  const int q = (int)(p - (int64_t)c0 * T);
+  const int t = q / V, v = q - t * V;
+  return (c0 + v) * T + t;
+}
+__host__ __device__ __forceinline__ int sweep_grid2d(int64_t CT) { return (int)(8 * ((CT + 7) / 8)); }
+
 }  // namespace gsr

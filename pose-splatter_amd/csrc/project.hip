@@ -195,14 +195,7 @@ __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
   alloc_offsets<ITEMS>(s_cnt, (int)(n1 - n0), (int64_t)c * N + n0, counter, isect_offset);
 }
 
-// Parameter set of camera c: cameras are grouped by set, set f owning cameras
-// [set_begin[f], set_begin[f+1]) (null: one set).  Uniform per workgroup (scalar loads).
-__device__ __forceinline__ int set_of_camera(const int32_t* __restrict__ set_begin, int F, int c) {
-  if (set_begin == nullptr) return 0;
-  int f = 0;
-  while (f + 1 < F && set_begin[f + 1] <= c) ++f;
-  return f;
-}
+// (set_of_camera / set_first_camera: gsr_common.h)
 
 // Camera c = blockIdx.y renders parameter set set_of_camera(c) (multi-frame batches: every
 // (frame, view) unit is one camera; the 2D renderer ignores the camera itself,
@@ -219,6 +212,7 @@ __global__ __launch_bounds__(kProjThreads) void k_project2d_fwd(
   int32_t* gcount = tile_count + (int64_t)c * T;
   int32_t* counter = tile_count + (int64_t)C * T;
   const float* pset = params + (int64_t)set_of_camera(set_begin, F, c) * set_stride;
+  const bool rec_owner = set_first_camera(set_begin, F, c) == c;
   if (use_lds) {
     for (int t = threadIdx.x; t < T; t += blockDim.x) hist[t] = 0;
     __syncthreads();
@@ -263,7 +257,10 @@ __global__ __launch_bounds__(kProjThreads) void k_project2d_fwd(
       s.p0 = make_float4(g.u, g.v, g.op, logf(g.op / eps_cut));
       s.p1 = make_float4(g.a, g.b, g.c, -g.b / (2.f * g.c));
       s.p2 = make_float4(g.col[0], g.col[1], g.col[2], -g.b / (2.f * g.a));
-      rec[cn] = s;
+      // one record per parameter set: its cameras render identical lists (the camera is ignored,
+      // src/gaussian_renderer.py:280-281), so they all read the set's first camera's copy
+      // (raster.hip rec_offset2d) -- one copy to write, and shared by the views in the XCDs' L2
+      if (rec_owner) rec[cn] = s;
       hist_add(hist, gcount, use_lds, x0, x1, y0, y1, tw);
     }
     rect[cn] = make_uint2(pack_rect_lo(x0, x1), pack_rect_lo(y0, y1));

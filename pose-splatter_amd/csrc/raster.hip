@@ -345,6 +345,14 @@ constexpr float kT2DMin = 2.98023224e-8f;   // 2^-25
 // live, or one whose last composited entry is the prefix's last (the cut key of the next
 // entry must come from a sorted list).  rerun: the second pass over the flagged tiles
 // (list[0..count), sorted whole by then), from scratch.
+// 2D parameter sets of the cameras (gsr2d_*: one record copy per set, rec_offset2d; the XCD-aware
+// sweep, sweep_tile2d).  3D: {0, nullptr, 1}, unused.
+struct Sets2D {
+  int64_t N;
+  const int32_t* begin;
+  int F;
+};
+
 struct FwdLazy {
   const int32_t* tile_sorted;
   int32_t* flag;
@@ -392,7 +400,8 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
     float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
     int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end, float4* __restrict__ ckpt,
     const int32_t* __restrict__ chunk_base, int n_busy, int64_t CT,
-    uint64_t* __restrict__ tile_cut, float cut2d, const FwdLazy lz, const gsr_bin_stats* __restrict__ stats) {
+    uint64_t* __restrict__ tile_cut, float cut2d, const FwdLazy lz, const gsr_bin_stats* __restrict__ stats,
+    const Sets2D sets) {
   static_assert(!IS2D || LPP == 4, "2D walks per wave with quads");
   using PG = PixGroup<LPP>;
   using FS = FwdShape<LPP>;
@@ -438,6 +447,7 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
   if (u >= n_busy) return;
   int c, ty, tx;
   tile_coords(ct, tw, th, c, ty, tx);
+  if constexpr (IS2D) rec += rec_offset2d(sets.begin, sets.F, c, sets.N);   // the set's record copy
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int q = lane & (LPP - 1), p = lane / LPP;
   const int sx = (sub % (kTile / FS::WB)) * FS::WB, sy = (sub / (kTile / FS::WB)) * FS::WB;
@@ -822,7 +832,8 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
     float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
     int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end, float4* __restrict__ ckpt,
     const int32_t* __restrict__ chunk_base, int n_busy, int64_t CT,
-    uint64_t* __restrict__ tile_cut, float cut2d, const FwdLazy lz, const gsr_bin_stats* __restrict__ stats) {
+    uint64_t* __restrict__ tile_cut, float cut2d, const FwdLazy lz, const gsr_bin_stats* __restrict__ stats,
+    const Sets2D sets) {
   (void)kos;   // one workgroup per tile: the waves' own quadrant culls decide
   constexpr bool PACK = IS2D && GSR_BOX_PACK;   // 2D walk: records staged packed (pack_rec)
   __shared__ float4 s_r[2][3][256];              // round records, part j of slot i at s_r[buf][j][i]
@@ -833,19 +844,22 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
   __shared__ int s_max;
   static_assert(kChunk3 == 128, "a round half is one chunk");
   const int busy_blocks = (n_busy + 7) & ~7;   // n_busy: the grid's bound (see k_raster_fwd)
-  // device counts and this workgroup's tile in one round trip (see k_raster_fwd)
+  // device counts and this workgroup's tile in one round trip (see k_raster_fwd); 2D: every tile,
+  // busy or empty, in the XCD-aware sweep (sweep_tile2d; an empty list just writes the background)
   if (lz.rerun) order = lz.list;
-  const int ct = order[min((int)blockIdx.x, (int)CT - 1)];
+  const int ct = IS2D ? sweep_tile2d(blockIdx.x, CT, tw * th, sets.begin, sets.F) : order[min((int)blockIdx.x, (int)CT - 1)];
   const int ovf = stats->overflow;
   const int nb_dev = lz.rerun ? *lz.count : stats->n_busy;
   // (a lazy re-render's list holds only *lz.count tiles: slots past it are stale, never a fault)
-  if (ovf | ((ct < 0) & ((int)blockIdx.x < nb_dev))) {
+  if (ovf | (!IS2D & (ct < 0) & ((int)blockIdx.x < nb_dev))) {
     // (the sticky status is also set here: a forward with no backward skips the finalize)
     if (blockIdx.x == 0 && threadIdx.x == 0 && stats->status != nullptr) atomicOr(stats->status, ovf);
     nan_fill(CT, W, H, tw, th, out_rgb, out_alpha);
     return;
   }
-  if (lz.rerun) {
+  if (IS2D) {
+    if (ct < 0) return;
+  } else if (lz.rerun) {
     n_busy = min(n_busy, nb_dev);
   } else {
     n_busy = nb_dev;
@@ -855,9 +869,10 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
       return;
     }
   }
-  if ((int)blockIdx.x >= n_busy) return;
+  if (!IS2D && (int)blockIdx.x >= n_busy) return;
   int c, ty, tx;
   tile_coords(ct, tw, th, c, ty, tx);
+  if constexpr (IS2D) rec += rec_offset2d(sets.begin, sets.F, c, sets.N);   // the set's record copy
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #if GSR_BOX_LANES
   // box = the lane's ds_read_b128 group ((bit 5, bit 4 ^ bit 3 ^ bit 2), MI355X_MICROARCH.md
@@ -1127,7 +1142,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_finalize(
     const float* __restrict__ depth, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ order, int n_busy, const int32_t* __restrict__ chunk_base,
     int32_t* __restrict__ tile_end, uint64_t* __restrict__ tile_cut, gsr_bin_stats* __restrict__ stats,
-    int32_t* __restrict__ chunk_list, int key_order, int tile_units) {
+    int32_t* __restrict__ chunk_list, int key_order, int tile_units, int64_t CT, int T, const Sets2D sets) {
   const int ovf = stats->overflow;
   if (ovf) {   // bounded call over its bounds: report to the caller's sticky status, nothing else
     if (blockIdx.x == 0 && threadIdx.x == 0 && stats->status != nullptr) atomicOr(stats->status, ovf);
@@ -1136,8 +1151,10 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_finalize(
   (void)n_busy;   // the grid's bound; the tiles are the device count's
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
-  const bool in = b < stats->n_busy;
-  const int ct = in ? order[b] : 0;
+  // tile_units (2D): slot b of the XCD-aware sweep (every tile, busy or empty), one unit each
+  const int sct = tile_units && b < sweep_grid2d(CT) ? sweep_tile2d(b, CT, T, sets.begin, sets.F) : -1;
+  const bool in = tile_units ? sct >= 0 : b < stats->n_busy;
+  const int ct = tile_units ? max(sct, 0) : in ? order[b] : 0;
   int start = 0, end = 0, te = 0;
   if (in) {
     start = tile_offset[ct];
@@ -1147,8 +1164,15 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_finalize(
     tile_end[ct] = te;
     tile_cut[ct] = te < end ? sort_key(depth, ids[te], key_order) : ~0ull;
   }
-  // tile_units (2D): one backward unit per tile, its whole consumed list [start, te)
-  const int U = tile_units ? max(te - start, 1) : stats->chunk_entries;
+  if (tile_units) {
+    // the unit of sweep slot b: the tile's whole consumed list [start, te) (empty: a unit of 0
+    // entries, which the backward skips); the backward's grid is the sweep's
+    if (b == 0) stats->n_active = sweep_grid2d(CT);
+    if (b < sweep_grid2d(CT))
+      reinterpret_cast<int4*>(chunk_list)[b] = in ? make_int4(start, te - start, chunk_base[ct], ct) : make_int4(0, 0, 0, 0);
+    return;
+  }
+  const int U = stats->chunk_entries;
   const int nact = (te - start + U - 1) / U;
   // one atomic per wave on the active-chunk counter (one per tile serialised ~700 atomics on
   // one address at config 3)
@@ -1246,6 +1270,9 @@ __device__ __forceinline__ void loss_cotangent(const gsr_loss_terms& lt, int C, 
 #ifndef GSR_BWD_MINB
 #define GSR_BWD_MINB 1
 #endif
+#ifndef GSR_BWD_LDS
+#define GSR_BWD_LDS 0   // 1: packed LDS records + grouped survivor slots (PK below); measured slower in 3D (config 5 raster bwd 0.60 -> 0.67 ms)
+#endif
 #ifndef GSR_BWD_MULTI_MINB
 #define GSR_BWD_MULTI_MINB 1
 #endif
@@ -1273,12 +1300,17 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
 #endif
   constexpr int kGroup = GSR_BWD_GROUP;
   constexpr int kLen = kChunk3 + kGroup;   // survivor list capacity (padded to whole groups)
+  // PK: records staged packed (pack_rec: the walk's nine values in 2 x b128 + b32) and each box's
+  // survivor list with a pad byte after every 7 (grouped_slot): a group's seven slots are ONE
+  // 8-byte read instead of seven byte reads
+  constexpr bool PK = GSR_BWD_LDS;
+  constexpr int kLenB = PK ? 8 * ((kLen + kGroup - 1) / kGroup) : kLen;
   __shared__ float4 s_p[3][kChunk3 + 1];   // the chunk's records, part j of entry k at s_p[j][k]
   // gradient sums per entry, one slot per wave (index kNull absorbs the padding's zeros)
   __shared__ __attribute__((aligned(16))) float L[kPartial][4][kChunk3 + 1];
   static_assert((kPartial * 4 * (kChunk3 + 1)) % 4 == 0, "L is zeroed in float4 stores");
   __shared__ unsigned char s_list[4][kLen];     // quadrant survivors, back to front
-  __shared__ unsigned char s_box[4][4][kLen];   // per (wave, box) survivors, back to front
+  __shared__ __attribute__((aligned(16))) unsigned char s_box[4][4][kLenB];   // per (wave, box) survivors, back to front
   __shared__ float s_stage[4][64][4];     // per wave: the group's reduced sums, by lane
   __shared__ unsigned char s_mask[kChunk3];   // 3D: each entry's quadrant mask (k_of_s bits 28..31)
   // one workgroup per grid slot; slots past the forward's active-chunk count exit at once
@@ -1386,6 +1418,7 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
   const unsigned char* my_list = s_box[wv][box];
   for (int sub = nsub - 1; sub >= 0; --sub) {
     if (sub != nsub - 1) __syncthreads();   // the previous sub-chunk's LDS is consumed
+    if (PK) pack_rec(sp0, sp1, sp2);
     if (threadIdx.x < sn) {
       s_p[0][threadIdx.x] = sp0;
       s_p[1][threadIdx.x] = sp1;
@@ -1416,9 +1449,15 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
         const int k = q * 64 + lane;
         // the quadrant test: the emission's mask bit where it stored masks (the same cull_keep on
         // the same bounds, no record reads), else the test itself
-        const bool keep = k < sn && (sb0 + k) <= wlast &&
-                          (use_masks ? ((s_mask[k] >> wv) & 1) != 0
-                                     : cull_keep<IS2D>(s_p[0][k], s_p[1][k], s_p[2][k], x0, x0 + 7.f, y0, y0 + 7.f));
+        bool in_q;
+        if (use_masks) {
+          in_q = ((s_mask[k] >> wv) & 1) != 0;
+        } else {
+          float4 r0 = s_p[0][k], r1 = s_p[1][k], r2 = s_p[2][k];
+          unpack_rec<PK>(r0, r1, r2);
+          in_q = cull_keep<IS2D>(r0, r1, r2, x0, x0 + 7.f, y0, y0 + 7.f);
+        }
+        const bool keep = k < sn && (sb0 + k) <= wlast && in_q;
         const unsigned long long mk = __ballot(keep);
         if (keep) {
           const unsigned long long above = lane == 63 ? 0ull : (mk >> (lane + 1));
@@ -1431,13 +1470,13 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
     // ... and the quadrant's survivors against each 4x4 box (one survivor per lane, all four
     // boxes; box4_cull keeps the list order)
     int nbx[4];
-    box4_cull<IS2D>(s_list[wv], nsurv, s_p[0], s_p[1], s_p[2], (float)qx0 + off, (float)qy0 + off,
-                    &s_box[wv][0][0], kLen, nbx);
+    box4_cull<IS2D, PK, PK>(s_list[wv], nsurv, s_p[0], s_p[1], s_p[2], (float)qx0 + off, (float)qy0 + off,
+                            &s_box[wv][0][0], kLenB, nbx);
     const int nb = box == 0 ? nbx[0] : box == 1 ? nbx[1] : box == 2 ? nbx[2] : nbx[3];   // this lane's box
     // groups walked by the wave: max over its boxes
     const int ngrp = max(max(nbx[0], nbx[1]), max(nbx[2], nbx[3]));
     const int npad = (ngrp + kGroup - 1) / kGroup * kGroup;
-    for (int s = nb + pos; s < npad; s += 16) s_box[wv][box][s] = (unsigned char)kNull;
+    for (int s = nb + pos; s < npad; s += 16) s_box[wv][box][PK ? grouped_slot(s) : s] = (unsigned char)kNull;
     __builtin_amdgcn_wave_barrier();
 #ifdef GSR_BWD_TRACE
     if (pos == 0) tr_nb[wv * 4 + box] = nb;
@@ -1451,15 +1490,21 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
     // deterministic -- no LDS atomics.
     // Branch-free groups of 7 survivors: an invalid (entry, pixel) pair contributes zeros and
     // leaves T and S unchanged (ra = 1, fac = 0), so every group is straight-line code.
-    for (int g0 = 0; g0 < ngrp; g0 += kGroup) {
+    for (int g0 = 0, gb = 0; g0 < ngrp; g0 += kGroup, gb += 8) {
       float acc[64];
       acc[63] = 0.f;
+      const uint2 w8 = PK ? *reinterpret_cast<const uint2*>(my_list + gb) : make_uint2(0u, 0u);
 #pragma unroll
       for (int g = 0; g < kGroup; ++g) {
-        const int k = my_list[g0 + g];
+        const int k = PK ? (int)(((g < 4 ? w8.x : w8.y) >> (8 * (g & 3))) & 0xFFu) : my_list[g0 + g];
         const float4 p0 = s_p[0][k];
         const float4 p1 = s_p[1][k];
-        const float4 p2 = s_p[2][k];
+        float4 p2;
+        if (PK) {
+          p2 = make_float4(p0.w, p1.w, reinterpret_cast<const float*>(&s_p[2][k])[0], 0.f);   // the colour
+        } else {
+          p2 = s_p[2][k];
+        }
         const float dx = p0.x - px, dy = p0.y - py;
         const float sigma = conic_sigma(p1, dx, dy);
         const float vis = __expf(-sigma);
@@ -1508,7 +1553,7 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
       if (fown) {
 #pragma unroll
         for (int bx = 0; bx < 4; ++bx) {
-          const int k = s_box[wv][bx][g0 + fg];
+          const int k = s_box[wv][bx][PK ? gb + fg : g0 + fg];
           Lw[k] += stage_rd[4 * bx];
         }
       }
@@ -1582,14 +1627,14 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
 #define GSR_BWD2D_EARLY 0
 #endif
 #ifndef GSR_BWD2D_ROWS2
-#define GSR_BWD2D_ROWS2 1
+#define GSR_BWD2D_ROWS2 0   // 1: two threads per row (measured slower: config 4 bwd 18.7 -> 22.4 ms)
 #endif
 __global__ __launch_bounds__(kRasterThreads, GSR_BWD2D_MINB) void k_raster2d_bwd_tile(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const float* __restrict__ anchors, int W, int H,
     int tw, int th, const float* __restrict__ bg, const float* __restrict__ final_T,
     const int32_t* __restrict__ last_in, const float* __restrict__ v_rgb, const float* __restrict__ v_alpha,
     float* __restrict__ partial, const int32_t* __restrict__ units, gsr_bin_stats* __restrict__ stats,
-    const int32_t* __restrict__ k_of_s, float cut2d) {
+    const int32_t* __restrict__ k_of_s, float cut2d, const Sets2D sets) {
   constexpr int kNull = kChunk3;
   constexpr int kGroup = GSR_BWD_GROUP;
   constexpr int kLen = kChunk3 + kGroup;
@@ -1626,6 +1671,7 @@ __global__ __launch_bounds__(kRasterThreads, GSR_BWD2D_MINB) void k_raster2d_bwd
   const int start = cd.x, n = cd.y, cbase = cd.z, ct = cd.w;
   int c, ty, tx;
   tile_coords(ct, tw, th, c, ty, tx);
+  rec += rec_offset2d(sets.begin, sets.F, c, sets.N);   // the set's record copy
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int box = lane & 3, pos = lane >> 2;
   const int qx0 = tx * kTile + (wv & 1) * 8, qy0 = ty * kTile + (wv >> 1) * 8;   // quadrant origin
@@ -1930,7 +1976,8 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
                       int width, int height, float cut2d, const float* bg, int32_t n_busy, gsr_bin_stats* stats,
                       float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
                       uint64_t* tile_cut, float* chunk_state, int32_t* chunk_list,
-                      void* stream, const FwdLazy& lz = FwdLazy{}, int lanes = 0, bool finalize = true) {
+                      void* stream, const FwdLazy& lz = FwdLazy{}, int lanes = 0, bool finalize = true,
+                      const Sets2D sets = Sets2D{0, nullptr, 1}) {
   GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "%s: bad C=%d or image %dx%d", who, C, width, height);
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   const int64_t CT = (int64_t)C * tw * th;
@@ -1953,24 +2000,29 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
     hipLaunchKernelGGL((k_raster_fwd<false, 16>), dim3((unsigned)(busy_grid<16>(n_busy) + n_fill)),
                        dim3(kRasterThreads), kFwdLdsPad, s, (const Splat*)rec, sorted_ids, kos, tile_offset, tile_order,
                        width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state,
-                       chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz, stats);
+                       chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz, stats, sets);
   } else if (lanes == 4) {
     hipLaunchKernelGGL((k_raster_fwd<IS2D, 4>), dim3((unsigned)(busy_grid<4>(n_busy) + n_fill)),
                        dim3(kRasterThreads), IS2D ? kFwdLdsPad2D : kFwdLdsPad, s, (const Splat*)rec, sorted_ids, kos,
                        tile_offset, tile_order, width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end,
-                       (float4*)chunk_state, chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz, stats);
+                       (float4*)chunk_state, chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz, stats, sets);
   } else {
-    hipLaunchKernelGGL((k_raster_fwd_box<IS2D>), dim3((unsigned)(((n_busy + 7) & ~7) + n_fill)),
+    // 2D: every tile in the XCD-aware sweep (no separate empty-tile fill)
+    const int64_t grid = IS2D ? (int64_t)sweep_grid2d(CT) : ((n_busy + 7) & ~7) + n_fill;
+    hipLaunchKernelGGL((k_raster_fwd_box<IS2D>), dim3((unsigned)grid),
                        dim3(kRasterThreads), 0, s, (const Splat*)rec, sorted_ids, kos, tile_offset, tile_order, width,
                        height, tw, th, bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state, chunk_base,
-                       (int)n_busy, CT, tile_cut, cut2d, lz, stats);
+                       (int)n_busy, CT, tile_cut, cut2d, lz, stats, sets);
   }
   GSR_LAUNCH_CHECK(who);
-  // no chunk list: a forward with no backward to follow (no records, no finalize)
-  if (finalize && n_busy > 0 && chunk_list != nullptr) {
-    hipLaunchKernelGGL(k_raster_finalize, dim3(ceil_div(n_busy, kRasterThreads)), dim3(kRasterThreads), 0, s,
+  // no chunk list: a forward with no backward to follow (no records, no finalize).  2D: one unit
+  // per sweep slot, written even with no busy tile (the backward's grid is the sweep's)
+  if (finalize && (n_busy > 0 || IS2D) && chunk_list != nullptr) {
+    const int64_t fgrid = IS2D ? (int64_t)sweep_grid2d(CT) : (int64_t)n_busy;
+    hipLaunchKernelGGL(k_raster_finalize, dim3((unsigned)ceil_div(fgrid, (int64_t)kRasterThreads)), dim3(kRasterThreads), 0, s,
                        depth, sorted_ids, tile_offset, tile_order, (int)n_busy, chunk_base, tile_end,
-                       tile_cut, stats, chunk_list, IS2D ? GSR_ORDER_INDEX : GSR_ORDER_DEPTH, IS2D ? 1 : 0);
+                       tile_cut, stats, chunk_list, IS2D ? GSR_ORDER_INDEX : GSR_ORDER_DEPTH, IS2D ? 1 : 0, CT,
+                       tw * th, sets);
   }
   GSR_LAUNCH_CHECK("k_raster_finalize");
   return GSR_OK;
@@ -1982,22 +2034,24 @@ static int raster_bwd(const char* who, const float* rec, const int32_t* sorted_i
                       const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
                       int32_t chunk_entries, int C, int width, int height, float cut2d, const float* bg,
                       const float* final_T, const int32_t* last, const float* v_rgb, const float* v_alpha,
-                      const gsr_loss_terms& lt, const int32_t* k_of_s, float* partial, void* stream) {
+                      const gsr_loss_terms& lt, const int32_t* k_of_s, float* partial, void* stream,
+                      const Sets2D sets = Sets2D{0, nullptr, 1}) {
   GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "%s: bad C=%d or image %dx%d", who, C, width, height);
   GSR_REQUIRE(n_chunks >= 0, "%s: bad n_chunks", who);
   GSR_REQUIRE(chunk_entries == 0 || (chunk_entries >= kChunk3 && (chunk_entries & (chunk_entries - 1)) == 0),
               "%s: chunk_entries %d is not 0 or a power of two >= %d", who, chunk_entries, kChunk3);
-  if (n_chunks == 0) return GSR_OK;
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
+  if (n_chunks == 0 && !IS2D) return GSR_OK;
   // n_chunks bounds the forward's active-chunk count (stats->n_active, device-side)
-  if constexpr (IS2D) {   // 2D: one unit per tile (n_chunks bounds the busy tiles)
+  if constexpr (IS2D) {   // 2D: one unit per slot of the sweep (k_raster_finalize), n_chunks unused
     (void)tile_offset;
     (void)tile_end;
     (void)chunk_base;
     (void)lt;
-    hipLaunchKernelGGL(k_raster2d_bwd_tile, dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
-                       (const Splat*)rec, sorted_ids, chunk_state, width, height, tw, th, bg, final_T, last, v_rgb,
-                       v_alpha, partial, chunk_list, stats, k_of_s, cut2d);
+    const int64_t CT = (int64_t)C * tw * th;
+    hipLaunchKernelGGL(k_raster2d_bwd_tile, dim3((unsigned)sweep_grid2d(CT)), dim3(kRasterThreads), 0,
+                       (hipStream_t)stream, (const Splat*)rec, sorted_ids, chunk_state, width, height, tw, th, bg,
+                       final_T, last, v_rgb, v_alpha, partial, chunk_list, stats, k_of_s, cut2d, sets);
   } else if (chunk_entries > kChunk3)
     hipLaunchKernelGGL((k_raster_bwd<LOSS, IS2D, true>), dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
                        (const Splat*)rec, sorted_ids, tile_offset, tile_end, chunk_base,
@@ -2057,7 +2111,7 @@ int gsr3d_raster_fwd_lazy(const float* rec, const float* depth, int32_t* sorted_
   if (n_busy > 0 && chunk_list != nullptr) {
     hipLaunchKernelGGL(k_raster_finalize, dim3(ceil_div(n_busy, kRasterThreads)), dim3(kRasterThreads), 0,
                        (hipStream_t)stream, depth, sorted_ids, tile_offset, tile_order, (int)n_busy, chunk_base,
-                       tile_end, tile_cut, stats, chunk_list, GSR_ORDER_DEPTH, 0);
+                       tile_end, tile_cut, stats, chunk_list, GSR_ORDER_DEPTH, 0, CT, 0, Sets2D{0, nullptr, 1});
     GSR_LAUNCH_CHECK("k_raster_finalize");
   }
   return GSR_OK;
@@ -2092,11 +2146,13 @@ int gsr2d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t*
                      const int32_t* tile_order, const int32_t* chunk_base, int C, int width, int height, float eps_cut,
                      const float* bg, int32_t n_busy, gsr_bin_stats* stats, float* rgb, float* alpha,
                      float* final_T, int32_t* last, int32_t* tile_end, uint64_t* tile_cut, float* chunk_state,
-                     int32_t* chunk_list, void* stream) {
+                     int32_t* chunk_list, int64_t N, const int32_t* set_begin, int F, void* stream) {
   GSR_REQUIRE(eps_cut > 0.f && eps_cut < 1.f, "gsr2d_raster_fwd: eps_cut must be in (0,1)");
+  GSR_REQUIRE(N >= 0 && F >= 1 && (set_begin != nullptr || F == 1), "gsr2d_raster_fwd: bad N=%lld / F=%d",
+              (long long)N, F);
   return raster_fwd<true>("gsr2d_raster_fwd", rec, nullptr, sorted_ids, nullptr, tile_offset, tile_order, chunk_base, C, width,
                           height, eps_cut, bg, n_busy, stats, rgb, alpha, final_T, last, tile_end, tile_cut,
-                          chunk_state, chunk_list, stream);
+                          chunk_state, chunk_list, stream, FwdLazy{}, 0, true, Sets2D{N, set_begin, F});
 }
 
 int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
@@ -2104,12 +2160,15 @@ int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t*
                      const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
                      int32_t chunk_entries, int C, int width, int height, float eps_cut, const float* bg,
                      const float* final_T, const int32_t* last, const float* v_rgb, const float* v_alpha,
-                     const int32_t* k_of_s, float* partial, void* stream) {
+                     const int32_t* k_of_s, float* partial, int64_t N, const int32_t* set_begin, int F,
+                     void* stream) {
   GSR_REQUIRE(eps_cut > 0.f && eps_cut < 1.f, "gsr2d_raster_bwd: eps_cut must be in (0,1)");
+  GSR_REQUIRE(N >= 0 && F >= 1 && (set_begin != nullptr || F == 1), "gsr2d_raster_bwd: bad N=%lld / F=%d",
+              (long long)N, F);
   const gsr_loss_terms none{};
   return raster_bwd<false, true>("gsr2d_raster_bwd", rec, sorted_ids, tile_offset, tile_end, chunk_base,
                                  chunk_state, chunk_list, stats, n_chunks, chunk_entries, C, width, height, eps_cut, bg,
-                                 final_T, last, v_rgb, v_alpha, none, k_of_s, partial, stream);
+                                 final_T, last, v_rgb, v_alpha, none, k_of_s, partial, stream, Sets2D{N, set_begin, F});
 }
 
 }  // extern "C"

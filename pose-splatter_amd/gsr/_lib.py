@@ -26,7 +26,7 @@ ORDER_INDEX = 1
 INPUT_ADAPTER = 0
 INPUT_GSPLAT = 1
 
-ABI_VERSION = 6   # include/gsr.h GSR_ABI_VERSION this binding is written for
+ABI_VERSION = 7   # include/gsr.h GSR_ABI_VERSION this binding is written for
 
 # stats->overflow bits of a capacity-bounded call (include/gsr.h GSR_OVF_*)
 OVF_BITS = {1: "intersections > isect cap", 2: "chunks > chunk cap", 4: "busy tiles > n_busy bound",
@@ -109,9 +109,9 @@ EXPORTS = {
     "gsr3d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _P,
                                         _P, _P, _P, _P, _P, _P, _P]),
     "gsr2d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _I32, _P, _P, _P, _P, _P,
-                                        _P, _P, _P, _P, _P]),
+                                        _P, _P, _P, _P, _I64, _P, _I32, _P]),
     "gsr2d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _F, _P, _P,
-                                        _P, _P, _P, _P, _P, _P]),
+                                        _P, _P, _P, _P, _P, _I64, _P, _I32, _P]),
     "gsr3d_project_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _I32, _I32, _I32, _F, _I32, _P, _P,
                                          _P, _P, _P, _P, _I64, _I64, _P, _P, _P]),
     "gsr3d_touched_rows": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I64, _I64, _P, _P, _P]),

@@ -421,6 +421,8 @@ class _Bins:
         # the shape whose previous call bounds this one (band / unit grouping included: they
         # change the lists as much as the shape does)
         self.key = (str(device), C, N, width, height, key_extra)
+        # 2D: the chunk list holds one backward unit per slot of the tile sweep (include/gsr.h ABI 7)
+        self.min_units = self.CT + 8 if key_extra and key_extra[0] == "2d" else 0
         self.need_bwd = need_bwd   # False: no chunk records, no finalize (tile_end left raw)
         mode = capacity or _capacity_default
         if mode not in _MODES:
@@ -553,7 +555,7 @@ class _Bins:
 
     def alloc_chunks(self, n_chunks: int):
         K = max(n_chunks, 1)
-        self.chunks = _Arena(self.device, {"chunk_state": K * 256 * 16, "chunk_list": K * 16})
+        self.chunks = _Arena(self.device, {"chunk_state": K * 256 * 16, "chunk_list": max(K, self.min_units) * 16})
         self.chunk_cap = K
         self.p.update(self.chunks.ptr)
 
@@ -792,7 +794,8 @@ def _forward2d(params, bg, width, height, eps_cut, unit_sets=(0,), capacity=None
     with _timed("raster2d_fwd"):
       check(L.gsr2d_raster_fwd(q["rec"], q["sorted_ids"], q["tile_off"], q["busy"], q["chunk_base"], C, width, height,
                              eps_cut, _ptr(bgc), b.n_busy, q["stats_dev"], _ptr(rgb), _ptr(alpha), q["final_T"],
-                             q["last"], q["tile_end"], q["tile_cut"], cs, cl, stream), "gsr2d_raster_fwd")
+                             q["last"], q["tile_end"], q["tile_cut"], cs, cl, N, _ptr(sb), F, stream),
+          "gsr2d_raster_fwd")
     _record_stats(b)
     return rgb, alpha, b, (p, F, stride, set_stride, sb, bgc, width, height, eps_cut)
 
@@ -926,10 +929,11 @@ class _Render2D(torch.autograd.Function):
             with _timed("raster2d_bwd"):
               check(L.gsr2d_raster_bwd(q["rec"], q["sorted_ids"], q["tile_off"], q["tile_end"], q["chunk_base"],
                                      q["chunk_state"], q["chunk_list"], q["stats_dev"],
-                                     # 2D backward units are whole tiles (ABI 6): the grid bounds the busy tiles
+                                     # (2D backward units: one per slot of the tile sweep; n_chunks unused)
                                      b.n_busy, b.chunk_entries, C, width, height, eps_cut, _ptr(bgc), q["final_T"],
                                      q["last"],
-                                     _ptr(v_rgb), _ptr(v_alpha), q["k_of_s"], _ptr(partial), stream),
+                                     _ptr(v_rgb), _ptr(v_alpha), q["k_of_s"], _ptr(partial), N, _ptr(sb), F,
+                                     stream),
                   "gsr2d_raster_bwd")
             with _timed("project2d_bwd"):
               check(L.gsr2d_project_bwd(_ptr(p), N, stride, set_stride, _ptr(sb), F, C, width, height, q["rect"],
