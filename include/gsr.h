@@ -45,6 +45,9 @@
  *     [8..10]=rgb (activated colour)                [11]=-b/(2a)
  *   ([3], [7], [11] are the per-Gaussian constants of the rasterizer's sub-tile cull:
  *    L = ln(255*opacity) in 3D (gsplat's 1/255 skip), ln(opacity/eps_cut) in 2D.)
+ *   2D records (gsr2d_project_fwd, since ABI 8) are stored PACKED for the compositing walks:
+ *     [0]=x [1]=y [2]=opacity [3]=r   [4]=a [5]=b [6]=c [7]=g   [8]=b(blue) [9]=L [10]=-b/(2c)
+ *     [11]=-b/(2a); and only for the first camera of each parameter set (ABI 7).
  *   depth: 1 float per (c,n) (3D camera-space z; the sort key's high word).
  *   rect: 2 uint32 per (c,n): {x0 | x1<<16, y0 | y1<<16}, tiles [x0,x1) x [y0,y1).
  *
@@ -151,7 +154,9 @@ int gsr_version(void);
  * same set CSR as gsr2d_project_fwd) to read it, visit the tiles in an XCD-aware sweep (the
  * cameras of a set render a tile back to back on one XCD), and the 2D chunk list holds one
  * unit per sweep slot: chunk_list needs >= C * tiles + 8 entries. */
-#define GSR_ABI_VERSION 7
+/* Revision 8: 2D records are stored packed (layout above): the 2D walks read them as 2 x b128 +
+ * b32 from LDS as staged (or gathered straight into LDS). */
+#define GSR_ABI_VERSION 8
 int gsr_abi_version(void);
 const char* gsr_last_error(void);
 

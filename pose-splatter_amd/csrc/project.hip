@@ -254,9 +254,11 @@ __global__ __launch_bounds__(kProjThreads) void k_project2d_fwd(
       Splat s;
       // the raster's sub-tile cull constants (raster.hip cull_keep): L = ln(op / eps_cut)
       // (the level set this extent bounds) and the edge slopes -b/2c, -b/2a
-      s.p0 = make_float4(g.u, g.v, g.op, logf(g.op / eps_cut));
-      s.p1 = make_float4(g.a, g.b, g.c, -g.b / (2.f * g.c));
-      s.p2 = make_float4(g.col[0], g.col[1], g.col[2], -g.b / (2.f * g.a));
+      // stored packed (raster.hip pack_rec: the 2D walks read x, y, o, conic and colour as
+      // 2 x b128 + b32 straight from the staged copy)
+      s.p0 = make_float4(g.u, g.v, g.op, g.col[0]);
+      s.p1 = make_float4(g.a, g.b, g.c, g.col[1]);
+      s.p2 = make_float4(g.col[2], logf(g.op / eps_cut), -g.b / (2.f * g.c), -g.b / (2.f * g.a));
       // one record per parameter set: its cameras render identical lists (the camera is ignored,
       // src/gaussian_renderer.py:280-281), so they all read the set's first camera's copy
       // (raster.hip rec_offset2d) -- one copy to write, and shared by the views in the XCDs' L2

@@ -57,9 +57,10 @@ __device__ __forceinline__ void tile_coords(int ct, int tw, int th, int& c, int&
 // four boxes (box b at (qx + 4 (b & 1), qy + 4 (b >> 1))); box b's survivors are appended in
 // list order to boxl[b * stride + ..].  n[b]: the four counts (wave-uniform).  (A lane per
 // (survivor, box) pair read every record four times and walked 16 survivors per round trip.)
-// Record parts as the 2D box forward stages them in LDS (PACKED): q0 = (x, y, opacity, r),
-// q1 = (a, b, c, g), q2 = (b_colour, L, -b/2c, -b/2a) -- the walk's nine values in two b128
-// reads and one b32 instead of three b128; unpack_rec restores the Splat parts for the culls.
+// Packed record parts (PACKED): q0 = (x, y, opacity, r), q1 = (a, b, c, g), q2 = (b_colour, L,
+// -b/2c, -b/2a) -- the walk's nine values in two b128 reads and one b32 instead of three b128;
+// unpack_rec restores the Splat parts for the culls.  2D records are STORED packed
+// (k_project2d_fwd, ABI 8), so the 2D kernels stage them as they come.
 __device__ __forceinline__ void pack_rec(float4& p0, float4& p1, float4& p2) {
   const float4 q0 = make_float4(p0.x, p0.y, p0.z, p2.x);
   const float4 q1 = make_float4(p1.x, p1.y, p1.z, p2.y);
@@ -632,6 +633,8 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
     const Splat sb = rec[idb];
     x0 = sa.p0; x1 = sa.p1; x2 = sa.p2;
     y0 = sb.p0; y1 = sb.p1; y2 = sb.p2;
+    unpack_rec<IS2D>(x0, x1, x2);   // (2D records are stored packed: pack_rec)
+    unpack_rec<IS2D>(y0, y1, y2);
   }
   // One batch: cull + compact c (batch b0), refill c with batch b0+128 (id_use), load the ids
   // of batch b0+192 into id_new (issued BEFORE the record loads, so waiting for an id never
@@ -662,6 +665,7 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
     id_new = ids[min(b0 + 192 + lane, e_last)];
     const Splat sc = rec[id_use];
     c0 = sc.p0; c1 = sc.p1; c2 = sc.p2;
+    unpack_rec<IS2D>(c0, c1, c2);
     __builtin_amdgcn_wave_barrier();
     for (int k0 = 0; k0 < n; k0 += 4) {
       const int k = k0 + q;
@@ -914,7 +918,7 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
   }
   int buf = 0;
   for (int rb = start; rb < end; rb += 256, buf ^= 1) {
-    if constexpr (PACK) pack_rec(c0, c1, c2);
+    if constexpr (IS2D && !PACK) unpack_rec<true>(c0, c1, c2);   // (2D records are stored packed)
     s_r[buf][0][threadIdx.x] = c0;
     s_r[buf][1][threadIdx.x] = c1;
     s_r[buf][2][threadIdx.x] = c2;
@@ -1617,17 +1621,16 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
 // sums; T is re-anchored at every unit boundary (stats->chunk_entries entries) from the
 // forward's T record (4 B per pixel per unit, written once), and inside a unit recovered as
 // T_{i+1} / (1 - a_i) exactly as in the chunk-parallel kernel.  Partial rows as there.
+// 4 workgroups per CU: 128 VGPRs, no spills (at 5: 96 VGPRs and ~110 B of spills per lane outside
+// the walk -- config 4 bwd 18.9 vs 18.1 ms, profiles/r04_c4_glds_ab2.txt)
 #ifndef GSR_BWD2D_MINB
-#define GSR_BWD2D_MINB 5
+#define GSR_BWD2D_MINB 4
 #endif
-#ifndef GSR_BWD2D_LDS
-#define GSR_BWD2D_LDS 1
-#endif
-#ifndef GSR_BWD2D_EARLY
-#define GSR_BWD2D_EARLY 0
-#endif
-#ifndef GSR_BWD2D_ROWS2
-#define GSR_BWD2D_ROWS2 0   // 1: two threads per row (measured slower: config 4 bwd 18.7 -> 22.4 ms)
+// 1: the previous sub-chunk's records gathered straight into a second LDS buffer with
+// global_load_lds during the walk (no registers; LDS 38 KB) -- measured 18.5 vs 18.1 ms for the
+// register staging after the walk, kept as an option
+#ifndef GSR_BWD2D_GLDS
+#define GSR_BWD2D_GLDS 0
 #endif
 __global__ __launch_bounds__(kRasterThreads, GSR_BWD2D_MINB) void k_raster2d_bwd_tile(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const float* __restrict__ anchors, int W, int H,
@@ -1638,14 +1641,15 @@ __global__ __launch_bounds__(kRasterThreads, GSR_BWD2D_MINB) void k_raster2d_bwd
   constexpr int kNull = kChunk3;
   constexpr int kGroup = GSR_BWD_GROUP;
   constexpr int kLen = kChunk3 + kGroup;
-  // PK: records staged packed (pack_rec: the walk's nine values in 2 x b128 + b32) and each box's
-  // survivor list with a pad byte after every 7 (grouped_slot), so a group's seven slots are ONE
-  // 8-byte read instead of seven byte reads
-  constexpr bool PK = GSR_BWD2D_LDS;
-  constexpr bool EARLY = GSR_BWD2D_EARLY;
-  constexpr bool ROWS2 = GSR_BWD2D_ROWS2;
-  constexpr int kLenB = PK ? 8 * ((kLen + kGroup - 1) / kGroup) : kLen;
-  __shared__ float4 s_p[3][kChunk3 + 1];
+  // Records are stored packed (pack_rec: the walk's nine values in 2 x b128 + b32) and each box's
+  // survivor list has a pad byte after every 7 (grouped_slot), so a group's seven slots are ONE
+  // 8-byte read instead of seven byte reads (19.07 -> 18.64 ms at config 4).
+  // GL: the previous sub-chunk's records are gathered straight into the other half of a
+  // double-buffered LDS image (global_load_lds, 16 B per lane: no registers, in flight during the
+  // walk; the ids are read one sub-chunk earlier); else gathered into registers after the walk.
+  constexpr bool GL = GSR_BWD2D_GLDS;
+  constexpr int kLenB = 8 * ((kLen + kGroup - 1) / kGroup);
+  __shared__ float4 s_p[GL ? 2 : 1][3][kChunk3 + 1];
   __shared__ __attribute__((aligned(16))) float L[kPartial][4][kChunk3 + 1];
   __shared__ unsigned char s_list[4][kLen];
   __shared__ __attribute__((aligned(16))) unsigned char s_box[4][4][kLenB];
@@ -1679,14 +1683,15 @@ __global__ __launch_bounds__(kRasterThreads, GSR_BWD2D_MINB) void k_raster2d_bwd
   const bool inside = pi < H && pj < W;
   const float px = (float)pj, py = (float)pi;   // 2D: integer centres (src/gaussian_renderer.py:355-358)
   const int slot = ckpt_slot_of(wv, box, pos);
-  // the last sub-chunk [sb0, sb0 + sn): its ids, emission indices and records first
+  // the last sub-chunk [sb0, sb0 + sn) first: its ids, emission indices and records
   const int nsub = (n + kChunk3 - 1) / kChunk3;
   int sb0 = start + (nsub - 1) * kChunk3;
   int sn = start + n - sb0;
-  int id_mine = threadIdx.x < sn ? ids[sb0 + threadIdx.x] : 0;
-  // the rows' emission index: entry threadIdx.x (ROWS2: entry threadIdx.x / 2, two threads per row)
-  const int rsel = ROWS2 ? (int)threadIdx.x >> 1 : (int)threadIdx.x;
-  int kos_mine = rsel < sn ? k_of_s[sb0 + rsel] : 0;
+  const bool loader = threadIdx.x < kChunk3;   // waves 0 and 1 stage a sub-chunk's 128 entries
+  const int id_mine = threadIdx.x < sn ? ids[sb0 + threadIdx.x] : 0;
+  int kos_mine = threadIdx.x < sn ? k_of_s[sb0 + threadIdx.x] : 0;
+  // GL: the ids of the sub-chunk before the last (gathered at the start of the last one's walk)
+  int id_pf = GL && nsub > 1 && loader ? ids[sb0 - kChunk3 + threadIdx.x] : 0;
   float Tf = 1.f, Tl = 1.f, vr = 0.f, vg = 0.f, vb = 0.f, va = 0.f;
   int last = -1;
   if (inside) {
@@ -1711,36 +1716,43 @@ __global__ __launch_bounds__(kRasterThreads, GSR_BWD2D_MINB) void k_raster2d_bwd
   // mu after the pixel's last entry; T at the list's end is the final T (tile_end - 1 is the
   // tile's last composited entry, so no pixel has a valid entry after it)
   float mu = bgc[0] * vr + bgc[1] * vg + bgc[2] * vb - va;
-  float T = Tf;
+  float T = Tf, T_next = Tf;
   const int wlast = wave_max_i(last);
   const int fg = lane / kPartial, fq = lane - kPartial * (lane / kPartial);
   const bool fown = lane < kGroup * kPartial;
   float* const Lw = &L[fq][wv][0];
   const float* const stage_rd = &s_stage[wv][0][0] + 4 * (4 * (lane >> 2)) + (lane & 3);   // + 4*box
   const unsigned char* my_list = s_box[wv][box];
+  if (threadIdx.x < 3 * (GL ? 2 : 1)) s_p[threadIdx.x / 3][threadIdx.x % 3][kNull] = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int sub = nsub - 1; sub >= 0; --sub) {
+    const int buf = GL ? (nsub - 1 - sub) & 1 : 0;
+    float4 (*const sp)[kChunk3 + 1] = s_p[buf];
     if (sub != nsub - 1) {
-      // re-anchor T where this sub-chunk ends on a unit boundary (the forward wrote the pixel's T
-      // there if the pixel was still live, i.e. its last entry lies beyond; else T is Tf)
-      const int ue = sb0 + sn - start;
-      if ((ue & (U - 1)) == 0) T = last >= sb0 + sn ? anchors[(int64_t)(cbase + ue / U) * kRasterThreads + slot] : Tf;
-      __syncthreads();   // the previous sub-chunk's LDS is consumed
+      __syncthreads();   // the previous sub-chunk's LDS is consumed (and, GL, this one's gathers landed)
+      // re-anchor T where this sub-chunk ends on a unit boundary (T_next: read during the
+      // previous sub-chunk's rows)
+      if (((sb0 + sn - start) & (U - 1)) == 0) T = T_next;
     }
-    if (PK) pack_rec(sp0, sp1, sp2);
-    if (threadIdx.x < sn) {
-      s_p[0][threadIdx.x] = sp0;
-      s_p[1][threadIdx.x] = sp1;
-      s_p[2][threadIdx.x] = sp2;
+    if (!GL || sub == nsub - 1) {
+      if (threadIdx.x < sn) {
+        sp[0][threadIdx.x] = sp0;
+        sp[1][threadIdx.x] = sp1;
+        sp[2][threadIdx.x] = sp2;
+      }
     }
     for (int i = threadIdx.x; i < kPartial * (kChunk3 + 1); i += kRasterThreads)   // b128 stores
       reinterpret_cast<float4*>(&L[0][0][0])[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (threadIdx.x == 0) {
-      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-      s_p[0][kNull] = z;
-      s_p[1][kNull] = z;
-      s_p[2][kNull] = z;
-    }
     __syncthreads();
+    if (GL && sub > 0 && loader) {
+      // the previous sub-chunk's records into the other buffer (in flight during the walk), then
+      // the ids of the one before it
+      const float4* src = rec4 + 3 * (int64_t)id_pf;
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        __builtin_amdgcn_global_load_lds(src + j, (__attribute__((address_space(3))) void*)&s_p[buf ^ 1][j][64 * wv],
+                                         16, 0, 0);
+      if (sub > 1) id_pf = ids[sb0 - 2 * kChunk3 + threadIdx.x];
+    }
     BWD2_P(0);
     const int lastk = min(last - sb0, kChunk3 - 1);   // < 0: the pixel stopped before this sub-chunk
     const int lastq = last - sb0 < kChunk3 ? last - sb0 : -1;
@@ -1750,8 +1762,8 @@ __global__ __launch_bounds__(kRasterThreads, GSR_BWD2D_MINB) void k_raster2d_bwd
 #pragma unroll
       for (int q = kChunk3 / 64 - 1; q >= 0; --q) {
         const int k = q * 64 + lane;
-        float4 r0 = s_p[0][k], r1 = s_p[1][k], r2 = s_p[2][k];
-        unpack_rec<PK>(r0, r1, r2);
+        float4 r0 = sp[0][k], r1 = sp[1][k], r2 = sp[2][k];
+        unpack_rec<true>(r0, r1, r2);
         const bool keep = k < sn && (sb0 + k) <= wlast && cull_keep<true>(r0, r1, r2, x0, x0 + 7.f, y0, y0 + 7.f);
         const unsigned long long mk = __ballot(keep);
         if (keep) {
@@ -1763,42 +1775,25 @@ __global__ __launch_bounds__(kRasterThreads, GSR_BWD2D_MINB) void k_raster2d_bwd
     }
     __builtin_amdgcn_wave_barrier();
     int nbx[4];
-    box4_cull<true, PK, PK>(s_list[wv], nsurv, s_p[0], s_p[1], s_p[2], (float)qx0, (float)qy0, &s_box[wv][0][0],
-                            kLenB, nbx);
+    box4_cull<true, true, true>(s_list[wv], nsurv, sp[0], sp[1], sp[2], (float)qx0, (float)qy0, &s_box[wv][0][0],
+                                kLenB, nbx);
     const int nb = box == 0 ? nbx[0] : box == 1 ? nbx[1] : box == 2 ? nbx[2] : nbx[3];
     const int ngrp = max(max(nbx[0], nbx[1]), max(nbx[2], nbx[3]));
     const int npad = (ngrp + kGroup - 1) / kGroup * kGroup;
-    for (int s = nb + pos; s < npad; s += 16) s_box[wv][box][PK ? grouped_slot(s) : s] = (unsigned char)kNull;
+    for (int s = nb + pos; s < npad; s += 16) s_box[wv][box][grouped_slot(s)] = (unsigned char)kNull;
     __builtin_amdgcn_wave_barrier();
     BWD2_P(1);
-    // EARLY: the previous sub-chunk's ids / records issued before the walk (in flight during it)
-    int kos_next = 0;
-    if (EARLY) {
-      sp0 = sp1 = sp2 = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (sub > 0 && threadIdx.x < kChunk3) {
-        const int id_next = ids[sb0 - kChunk3 + threadIdx.x];
-        if (!ROWS2) kos_next = k_of_s[sb0 - kChunk3 + threadIdx.x];
-        sp0 = rec4[3 * (int64_t)id_next + 0];
-        sp1 = rec4[3 * (int64_t)id_next + 1];
-        sp2 = rec4[3 * (int64_t)id_next + 2];
-      }
-    }
     // the walk (as k_raster_bwd, IS2D): invalid pairs enter with alpha 0 (ra = 1, no change)
     for (int g0 = 0, gb = 0; g0 < ngrp; g0 += kGroup, gb += 8) {
       float acc[64];
       acc[63] = 0.f;
-      const uint2 w8 = PK ? *reinterpret_cast<const uint2*>(my_list + gb) : make_uint2(0u, 0u);
+      const uint2 w8 = *reinterpret_cast<const uint2*>(my_list + gb);
 #pragma unroll
       for (int g = 0; g < kGroup; ++g) {
-        const int k = PK ? (int)(((g < 4 ? w8.x : w8.y) >> (8 * (g & 3))) & 0xFFu) : my_list[g0 + g];
-        float4 p0 = s_p[0][k];
-        float4 p1 = s_p[1][k];
-        float4 p2;
-        if (PK) {
-          p2 = make_float4(p0.w, p1.w, reinterpret_cast<const float*>(&s_p[2][k])[0], 0.f);   // the colour
-        } else {
-          p2 = s_p[2][k];
-        }
+        const int k = (int)(((g < 4 ? w8.x : w8.y) >> (8 * (g & 3))) & 0xFFu);
+        const float4 p0 = sp[0][k];   // x, y, o, r
+        const float4 p1 = sp[1][k];   // a, b, c, g
+        const float cbl = reinterpret_cast<const float*>(&sp[2][k])[0];   // blue
         const float dx = p0.x - px, dy = p0.y - py;
         const float sigma = conic_sigma(p1, dx, dy);
         const float alpha = p0.z * __expf(-sigma);
@@ -1810,7 +1805,7 @@ __global__ __launch_bounds__(kRasterThreads, GSR_BWD2D_MINB) void k_raster2d_bwd
         acc[g * kPartial + 6] = fac * vr;
         acc[g * kPartial + 7] = fac * vg;
         acc[g * kPartial + 8] = fac * vb;
-        const float cv = p2.x * vr + p2.y * vg + p2.z * vb;
+        const float cv = p0.w * vr + p1.w * vg + cbl * vb;
         const float dmu = cv - mu;
         const float v_sig = -alpha_v * (T * dmu);
         mu = mu + alpha_v * dmu;
@@ -1829,54 +1824,43 @@ __global__ __launch_bounds__(kRasterThreads, GSR_BWD2D_MINB) void k_raster2d_bwd
       if (fown) {
 #pragma unroll
         for (int bx = 0; bx < 4; ++bx) {
-          const int k = s_box[wv][bx][PK ? gb + fg : g0 + fg];
+          const int k = s_box[wv][bx][gb + fg];
           Lw[k] += stage_rd[4 * bx];
         }
       }
       __builtin_amdgcn_wave_barrier();
     }
-    // the previous sub-chunk's ids, emission indices and records, gathered while this one's rows
-    // are summed and stored
-    // (assigned on every path: a conditional assignment would keep the old values -- 14 VGPRs --
-    // live across the walk)
     BWD2_P(2);
-    if (!EARLY) sp0 = sp1 = sp2 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (ROWS2 && sub > 0) kos_next = k_of_s[sb0 - kChunk3 + rsel];
-    if (!EARLY && sub > 0 && threadIdx.x < kChunk3) {
-      const int id_next = ids[sb0 - kChunk3 + threadIdx.x];
-      if (!ROWS2) kos_next = k_of_s[sb0 - kChunk3 + threadIdx.x];
-      sp0 = rec4[3 * (int64_t)id_next + 0];
-      sp1 = rec4[3 * (int64_t)id_next + 1];
-      sp2 = rec4[3 * (int64_t)id_next + 2];
+    // the previous sub-chunk's emission indices (and, !GL, records), read while this one's rows
+    // are summed and stored (assigned on every path: a conditional assignment would keep the old
+    // values live across the walk)
+    const int kos_next = sub > 0 && loader ? k_of_s[sb0 - kChunk3 + threadIdx.x] : 0;
+    // T at the previous sub-chunk's end when that is a unit boundary: the forward wrote the
+    // pixel's T there if the pixel was still live (its last entry lies beyond), else it is Tf
+    // (consumed after the next top barrier, which waits for every load anyway)
+    const int ue = sb0 - start;
+    T_next = sub > 0 && (ue & (U - 1)) == 0 && last >= sb0 ? anchors[(int64_t)(cbase + ue / U) * kRasterThreads + slot] : Tf;
+    if (!GL) {
+      sp0 = sp1 = sp2 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (sub > 0 && loader) {
+        const int id_next = ids[sb0 - kChunk3 + threadIdx.x];
+        sp0 = rec4[3 * (int64_t)id_next + 0];
+        sp1 = rec4[3 * (int64_t)id_next + 1];
+        sp2 = rec4[3 * (int64_t)id_next + 2];
+      }
     }
     __syncthreads();
     BWD2_P(3);
-    if (ROWS2) {
-      // two threads per row: the even one the mean / conic moments and v8, the odd one v4..v7
-      // (the same sums, the same row layout as store_partial_row)
-      const int k = rsel;
-      if (k < sn) {
-        float4* dst = reinterpret_cast<float4*>(partial + (int64_t)(kos_mine & kEmitIndexMask) * kPartialStride);
-        auto sum4 = [&](int q) { return (L[q][0][k] + L[q][1][k]) + (L[q][2][k] + L[q][3][k]); };
-        if ((threadIdx.x & 1) == 0) {
-          const float4 p1 = s_p[1][k];
-          const float mx = sum4(0), my = sum4(1);
-          dst[0] = make_float4(2.f * p1.x * mx + p1.y * my, p1.y * mx + 2.f * p1.z * my, sum4(2), sum4(3));
-          dst[2] = make_float4(sum4(8), 0.f, 0.f, 0.f);
-        } else {
-          dst[1] = make_float4(sum4(4), -sum4(5) / s_p[0][k].z, sum4(6), sum4(7));
-        }
-      }
-    } else if (threadIdx.x < sn) {
+    if (threadIdx.x < sn) {
       const int k = threadIdx.x;
       float v[kPartial];
 #pragma unroll
       for (int q = 0; q < kPartial; ++q) v[q] = (L[q][0][k] + L[q][1][k]) + (L[q][2][k] + L[q][3][k]);
-      const float4 p1 = s_p[1][k];
+      const float4 p1 = sp[1][k];
       const float mx = v[0], my = v[1];
       v[0] = 2.f * p1.x * mx + p1.y * my;
       v[1] = p1.y * mx + 2.f * p1.z * my;
-      v[5] = -v[5] / s_p[0][k].z;
+      v[5] = -v[5] / sp[0][k].z;
       store_partial_row(partial, kos_mine & kEmitIndexMask, v);
     }
     BWD2_P(4);
