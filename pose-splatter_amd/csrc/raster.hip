@@ -840,7 +840,10 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
     const Sets2D sets) {
   (void)kos;   // one workgroup per tile: the waves' own quadrant culls decide
   constexpr bool PACK = IS2D && GSR_BOX_PACK;   // 2D walk: records staged packed (pack_rec)
-  __shared__ float4 s_r[2][3][256];              // round records, part j of slot i at s_r[buf][j][i]
+  // round records, part j of entry k of half h at s_r[buf][j][129 h + k]; slot 129 h + 128 of every
+  // part is a zero record (opacity 0: never valid), the 2D walk's pad entry
+  constexpr int kHS = 129, kRS = 2 * kHS;
+  __shared__ float4 s_r[2][3][kRS];
   // ... and each box's survivors, in list order; 2D reads them four at a time (one b32 per four
   // steps, the next word read ahead: +4), the row stride (132 B = 33 banks) puts the two boxes
   // of a 32-lane half in different banks
@@ -916,12 +919,16 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
     c1 = rec[id0].p1;
     c2 = rec[id0].p2;
   }
+  if (threadIdx.x < 12) s_r[threadIdx.x / 6][(threadIdx.x / 2) % 3][kHS * (threadIdx.x & 1) + 128] = make_float4(0.f, 0.f, 0.f, 0.f);
   int buf = 0;
   for (int rb = start; rb < end; rb += 256, buf ^= 1) {
     if constexpr (IS2D && !PACK) unpack_rec<true>(c0, c1, c2);   // (2D records are stored packed)
-    s_r[buf][0][threadIdx.x] = c0;
-    s_r[buf][1][threadIdx.x] = c1;
-    s_r[buf][2][threadIdx.x] = c2;
+    {
+      const int si = (int)(threadIdx.x >> 7) * kHS + (int)(threadIdx.x & 127);
+      s_r[buf][0][si] = c0;
+      s_r[buf][1][si] = c1;
+      s_r[buf][2][si] = c2;
+    }
     {
       const int id_use = idn;
       idn = ids[min(rb + 512 + (int)threadIdx.x, e_last)];
@@ -933,7 +940,8 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
     // a half's quadrant survivors (slot in the half), kept in this wave's own slots of the other
     // round buffer: dead since the round barrier, and rewritten only by this wave at the next
     // round's start (LDS 27.2 -> 26.6 KB: 6 workgroups per CU)
-    unsigned char* const s_list_w = reinterpret_cast<unsigned char*>(&s_r[buf ^ 1][0][64 * wv]);
+    // (wave regions of 64 records skip the zero slot at 128)
+    unsigned char* const s_list_w = reinterpret_cast<unsigned char*>(&s_r[buf ^ 1][0][64 * wv + (wv >> 1)]);
     for (int h = 0; h < 2; ++h) {
       const int hb = rb + 128 * h;
       if (hb >= end || __ballot(!done) == 0ull) break;
@@ -959,7 +967,7 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           const int k = q * 64 + lane;
-          const int sl = 128 * h + k;
+          const int sl = kHS * h + k;
           float4 r0 = s_r[buf][0][sl], r1 = s_r[buf][1][sl], r2 = s_r[buf][2][sl];
           unpack_rec<PACK>(r0, r1, r2);
           const bool keep = k < nh && cull_keep<IS2D>(r0, r1, r2, x0, x0 + 7.f, y0, y0 + 7.f);
@@ -974,14 +982,14 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
       __builtin_amdgcn_wave_barrier();
       // ... and the quadrant's survivors against each 4x4 box
       int nbx[4];
-      box4_cull<IS2D, PACK>(s_list_w, nsurv, &s_r[buf][0][128 * h], &s_r[buf][1][128 * h], &s_r[buf][2][128 * h],
+      box4_cull<IS2D, PACK>(s_list_w, nsurv, &s_r[buf][0][kHS * h], &s_r[buf][1][kHS * h], &s_r[buf][2][kHS * h],
                             (float)qx0 + off, (float)qy0 + off, &s_box[wv][0][0], kBoxStride, nbx);
       const int nb = box == 0 ? nbx[0] : box == 1 ? nbx[1] : box == 2 ? nbx[2] : nbx[3];
       __builtin_amdgcn_wave_barrier();
       // steps walked by the wave: max over its boxes
       const int nmax = max(max(nbx[0], nbx[1]), max(nbx[2], nbx[3]));
       // the sequential walk of the box's survivors (entry index read one step ahead)
-      const float4* const rh = &s_r[buf][0][128 * h];
+      const float4* const rh = &s_r[buf][0][kHS * h];
       if constexpr (IS2D) {
         // 2D walks branch-free (lists are long and rarely saturate; the branchy walk spent as
         // many scalar as vector instructions on exec masks): a box's list is padded to the
@@ -991,7 +999,7 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
         // iteration ahead), so the list is padded to whole fours.
         const int nmax4 = (nmax + 3) & ~3;
         unsigned char* const lst = s_box[wv][box];
-        for (int s = nb + pos; s < nmax4; s += 16) lst[s] = s_list_w[0];
+        for (int s = nb + pos; s < nmax4; s += 16) lst[s] = (unsigned char)128;   // the zero record
         __builtin_amdgcn_wave_barrier();
         const uint32_t* const lst4 = reinterpret_cast<const uint32_t*>(lst);
         uint32_t k4 = 0, k4_next = GSR_BOX_K4 ? lst4[0] : lst[0];
@@ -1011,13 +1019,13 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
             k4_next = lst[t + 1];
           }
           {
-            const float4* rk = rh + k;   // the half's records: part j at rk[256 j]
-            float4 p0 = rk[0], p1 = rk[256];
+            const float4* rk = rh + k;   // the half's records: part j at rk[kRS j]
+            float4 p0 = rk[0], p1 = rk[kRS];
             float cb_;
             if constexpr (PACK) {
-              cb_ = reinterpret_cast<const float*>(rk + 512)[0];   // q2.x: the blue channel (b32)
+              cb_ = reinterpret_cast<const float*>(rk + 2 * kRS)[0];   // q2.x: the blue channel (b32)
             } else {
-              const float4 p2 = rk[512];
+              const float4 p2 = rk[2 * kRS];
               p0.w = p2.x;
               p1.w = p2.y;
               cb_ = p2.z;
@@ -1025,7 +1033,8 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
             const float dx = p0.x - px, dy = p0.y - py;
             const float sg = conic_sigma(p1, dx, dy);
             const float alpha = p0.z * __expf(-sg);
-            const bool valid = t < nb && !done && alpha >= cut2d;
+            // (steps past the box's list read the zero record: alpha 0 < cut2d, never valid)
+            const bool valid = !done && alpha >= cut2d;
             // an invalid step enters with alpha 0: vis = 0 and T * (1 - 0) = T exactly (one
             // select instead of three); the entry slot of the latest composite is kept per half
             const float av = valid ? alpha : 0.f;
@@ -1036,7 +1045,7 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
             Tl = valid ? T : Tl;
             T = T * (1.f - av);
             lk = valid ? k : lk;
-            done = done || (valid && T <= kT2DMin);   // the reference's A == 1.0f, after this entry
+            done = done || T <= kT2DMin;   // the reference's A == 1.0f, after this entry
           }
           if ((t & 31) == 31 && __ballot(!done) == 0ull) break;
         }
@@ -1050,10 +1059,10 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
         k_next = s_box[wv][box][t + 1];   // past the list: read, never used
         if (t < nb && !done) {
           __builtin_assume((unsigned)k < 256u);   // a byte: the address is one shift-add
-          const float4* rk = rh + k;   // the half's records: part j at rk[256 j]
+          const float4* rk = rh + k;   // the half's records: part j at rk[kRS j]
           const float4 p0 = rk[0];
-          const float4 p1 = rk[256];
-          const float4 p2 = rk[512];
+          const float4 p1 = rk[kRS];
+          const float4 p2 = rk[2 * kRS];
           const float dx = p0.x - px, dy = p0.y - py;
           const float sg = conic_sigma(p1, dx, dy);
           const float raw = p0.z * __expf(-sg);
