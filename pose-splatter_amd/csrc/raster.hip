@@ -35,9 +35,6 @@ static int g_fwd_lanes = 0;   // gsr_set_fwd_lanes: 0 automatic, 1 / 4 / 16 forc
 #ifndef GSR_BOX_PACK
 #define GSR_BOX_PACK 1
 #endif
-#ifndef GSR_BOX_K4
-#define GSR_BOX_K4 0   // 2D walk: survivor slots read four per b32 (1; measured slower at config 4: 9.55 vs 9.05 ms)
-#endif
 constexpr int kBoxStride = 132;   // survivor-list row of one 4x4 box (128 + a read-ahead word)
 
 
@@ -995,29 +992,21 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
         // many scalar as vector instructions on exec masks): a box's list is padded to the
         // wave's step count with a real quadrant survivor (finite record), which a step past
         // nb reads and leaves out by select -- the same sums, bit for bit.
-        // Steps go four at a time (one b32 read of four survivor slots, the next word read one
-        // iteration ahead), so the list is padded to whole fours.
-        const int nmax4 = (nmax + 3) & ~3;
+        // (reading the survivor slots four per b32 measured slower: 9.55 vs 9.05 ms at config 4)
         unsigned char* const lst = s_box[wv][box];
-        for (int s = nb + pos; s < nmax4; s += 16) lst[s] = (unsigned char)128;   // the zero record
+        for (int s = nb + pos; s < nmax; s += 16) lst[s] = (unsigned char)128;   // the zero record
         __builtin_amdgcn_wave_barrier();
-        const uint32_t* const lst4 = reinterpret_cast<const uint32_t*>(lst);
-        uint32_t k4 = 0, k4_next = GSR_BOX_K4 ? lst4[0] : lst[0];
+        int k_next = lst[0];
         int lk = -1;
+        // (steps in blocks of 32 between the "all pixels done" tests: one loop test per step)
+        for (int t0 = 0; t0 < nmax; t0 += 32) {
+          if (t0 > 0 && __ballot(!done) == 0ull) break;
+          const int t1 = min(t0 + 32, nmax);
 #pragma nounroll
-        for (int t = 0; t < nmax; ++t) {
-          int k;
-          if constexpr (GSR_BOX_K4) {
-            if ((t & 3) == 0) {   // (wave-uniform)
-              k4 = k4_next;
-              k4_next = lst4[(t >> 2) + 1];   // past the padded list: read, never used
-            }
-            k = (int)(k4 & 0xFFu);
-            k4 >>= 8;
-          } else {
-            k = (int)k4_next;
-            k4_next = lst[t + 1];
-          }
+        for (int t = t0; t < t1; ++t) {
+          const int k = k_next;
+          k_next = lst[t + 1];   // past the padded list: read, never used
+          __builtin_assume((unsigned)k <= 128u);   // a byte slot (128: the zero record)
           {
             const float4* rk = rh + k;   // the half's records: part j at rk[kRS j]
             float4 p0 = rk[0], p1 = rk[kRS];
@@ -1047,7 +1036,7 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
             lk = valid ? k : lk;
             done = done || T <= kT2DMin;   // the reference's A == 1.0f, after this entry
           }
-          if ((t & 31) == 31 && __ballot(!done) == 0ull) break;
+        }
         }
         if (lk >= 0) last = hb + lk;
         __builtin_amdgcn_wave_barrier();
