@@ -213,6 +213,27 @@ __device__ __forceinline__ void reduce_box16(float (&v)[64], float (&out)[4]) {
   }
 }
 
+// reduce_box8(v, out): the 8 lanes with equal lane bits 0-2 (a "box" of the 2D pair backward,
+// k_raster2d_bwd_pair) sum each of the 64 registers; afterwards out[i] of lane l is the box sum
+// of register 8*(l>>3) + i.  The halving butterfly of reduce_box16 over lane bits 5 and 4
+// (permlane swaps) and 3 (row_ror:8), stopping there: 96 VALU ops for 8 x 8-lane sums of 64.
+__device__ __forceinline__ void reduce_box8(float (&v)[64], float (&out)[8]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) swap32x8(&v[8 * g], &v[32 + 8 * g]);
+  float a[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) a[i] = v[i] + v[i + 32];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) swap16x8(&a[8 * g], &a[16 + 8 * g]);
+  float b[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) b[i] = a[i] + a[i + 16];
+  const bool b3 = (lane & 8) != 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) out[i] = pair_level<0x128>(b[i], b[i + 8], b3);   // row_ror:8
+}
+
 __device__ __forceinline__ unsigned long long wave_ballot(bool p) { return __ballot(p); }
 
 // Block-wide exclusive scan of one int per thread (NT threads, multiple of 64).

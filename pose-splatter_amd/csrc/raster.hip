@@ -1878,6 +1878,505 @@ __global__ __launch_bounds__(kRasterThreads, GSR_BWD2D_MINB) void k_raster2d_bwd
 }
 #undef BWD2_P
 
+// ---------------------------------------------------------------- 2D backward, per tile, pixel pairs
+// k_raster2d_bwd_tile's walk with TWO pixels per lane (the same column, rows r and r + 2 of a
+// 4x4 box): every record read, list decode and transposed reduction serves two pixels, and
+// their contributions are summed in registers before the reduction.  One workgroup of 2 waves
+// per tile; wave w owns the 16x8 half-tile of rows 8w..8w+7 (eight 4x4 boxes); lane l serves
+// box l & 7 (bits 0-2), pixel pair l >> 3.  The reduction runs over lane bits 5-3 (reduce_box8:
+// two permlane-swap levels and one DPP level), so each lane holds 8 of its box's 63 sums.  Same
+// sub-chunk walk, T anchors, mu carry and partial rows as k_raster2d_bwd_tile; the per-entry
+// sums are two waves' slots (L[q][0][k] + L[q][1][k]).
+#ifndef GSR_BWD2D_PAIR
+#define GSR_BWD2D_PAIR 1
+#endif
+#ifndef GSR_BWD2P_MINB
+#define GSR_BWD2P_MINB 3   // waves per SIMD the compiler aims at: 3 -> 168 VGPRs, ~no spills (4: 128 VGPRs + 120 B of spills, 18.7 vs 17.5 ms)
+#endif
+__global__ __launch_bounds__(128, GSR_BWD2P_MINB) void k_raster2d_bwd_pair(
+    const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const float* __restrict__ anchors, int W, int H,
+    int tw, int th, const float* __restrict__ bg, const float* __restrict__ final_T,
+    const int32_t* __restrict__ last_in, const float* __restrict__ v_rgb, const float* __restrict__ v_alpha,
+    float* __restrict__ partial, const int32_t* __restrict__ units, gsr_bin_stats* __restrict__ stats,
+    const int32_t* __restrict__ k_of_s, float cut2d, const Sets2D sets) {
+  constexpr int kNull = kChunk3;
+  constexpr int kGroup = GSR_BWD_GROUP;
+  static_assert(kGroup == 7 && kPartial == 9, "reduce_box8 sums 7 entries x 9 values in 64 registers");
+  constexpr int kLen = kChunk3 + kGroup;
+  constexpr int kLenB = 8 * ((kLen + kGroup - 1) / kGroup);
+  __shared__ float4 s_p[3][kChunk3 + 1];   // packed records of the sub-chunk (pack_rec layout)
+  __shared__ __attribute__((aligned(16))) float L[kPartial][2][kChunk3 + 1];
+  __shared__ unsigned char s_list[2][kLen];
+  __shared__ __attribute__((aligned(16))) unsigned char s_box[2][8][kLenB];
+  __shared__ __attribute__((aligned(16))) float s_stage[2][64][8];
+  const int4 cd = reinterpret_cast<const int4*>(units)[blockIdx.x];
+  const int n_act = stats->n_active, ovf = stats->overflow, U = stats->chunk_entries;
+  if ((ovf != 0) | ((int)blockIdx.x >= n_act) | (cd.y <= 0)) return;
+  const int start = cd.x, n = cd.y, cbase = cd.z, ct = cd.w;
+  int c, ty, tx;
+  tile_coords(ct, tw, th, c, ty, tx);
+  rec += rec_offset2d(sets.begin, sets.F, c, sets.N);   // the set's record copy
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int box = lane & 7, pp = lane >> 3;
+  const int hx0 = tx * kTile, hy0 = ty * kTile + 8 * wv;   // the wave's 16x8 half-tile
+  const int bjl = 4 * (box & 3), bil = 8 * wv + 4 * (box >> 2);   // box origin in the tile
+  const int jl = bjl + (pp & 3), ilA = bil + (pp >> 2), ilB = ilA + 2;
+  const int pj = tx * kTile + jl, piA = ty * kTile + ilA, piB = ty * kTile + ilB;
+  const bool inA = piA < H && pj < W, inB = piB < H && pj < W;
+  const float px = (float)pj, pyA = (float)piA, pyB = (float)piB;   // 2D: integer centres
+  const int slotA = bwd_pixel_slot(ilA, jl), slotB = bwd_pixel_slot(ilB, jl);
+  const int nsub = (n + kChunk3 - 1) / kChunk3;
+  int sb0 = start + (nsub - 1) * kChunk3;
+  int sn = start + n - sb0;
+  const int id_mine = (int)threadIdx.x < sn ? ids[sb0 + threadIdx.x] : 0;
+  int kos_mine = (int)threadIdx.x < sn ? k_of_s[sb0 + threadIdx.x] : 0;
+  float TfA = 1.f, TlA = 1.f, vrA = 0.f, vgA = 0.f, vbA = 0.f, vaA = 0.f;
+  float TfB = 1.f, TlB = 1.f, vrB = 0.f, vgB = 0.f, vbB = 0.f, vaB = 0.f;
+  int lastA = -1, lastB = -1;
+  if (inA) {
+    const int64_t pix = ((int64_t)c * H + piA) * W + pj;
+    lastA = last_in[pix];
+    const float2 t2 = reinterpret_cast<const float2*>(final_T)[pix];
+    TfA = t2.x;
+    TlA = t2.y;
+    vrA = v_rgb[pix * 3 + 0];
+    vgA = v_rgb[pix * 3 + 1];
+    vbA = v_rgb[pix * 3 + 2];
+    vaA = v_alpha[pix];
+  }
+  if (inB) {
+    const int64_t pix = ((int64_t)c * H + piB) * W + pj;
+    lastB = last_in[pix];
+    const float2 t2 = reinterpret_cast<const float2*>(final_T)[pix];
+    TfB = t2.x;
+    TlB = t2.y;
+    vrB = v_rgb[pix * 3 + 0];
+    vgB = v_rgb[pix * 3 + 1];
+    vbB = v_rgb[pix * 3 + 2];
+    vaB = v_alpha[pix];
+  }
+  const float4* const rec4 = reinterpret_cast<const float4*>(rec);
+  float4 sp0 = make_float4(0.f, 0.f, 0.f, 0.f), sp1 = sp0, sp2 = sp0;
+  if ((int)threadIdx.x < sn) {
+    sp0 = rec4[3 * (int64_t)id_mine + 0];
+    sp1 = rec4[3 * (int64_t)id_mine + 1];
+    sp2 = rec4[3 * (int64_t)id_mine + 2];
+  }
+  const float* bgc = bg + c * 3;
+  float muA = bgc[0] * vrA + bgc[1] * vgA + bgc[2] * vbA - vaA;
+  float muB = bgc[0] * vrB + bgc[1] * vgB + bgc[2] * vbB - vaB;
+  float TA = TfA, TB = TfB, TnA = TfA, TnB = TfB;
+  const int wlast = wave_max_i(max(lastA, lastB));
+  // the L update: lane f < 63 owns flat sum index f = 9 g + q of every box
+  const int fg = lane / kPartial, fq = lane - kPartial * (lane / kPartial);
+  const bool fown = lane < kGroup * kPartial;
+  float* const Lw = &L[fq][wv][0];
+  const float* const stage_rd = &s_stage[wv][(lane >> 3) << 3][lane & 7];   // + 8 * box
+  const unsigned char* my_list = s_box[wv][box];
+  if (threadIdx.x < 3) s_p[threadIdx.x][kNull] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int sub = nsub - 1; sub >= 0; --sub) {
+    if (sub != nsub - 1) {
+      __syncthreads();   // the previous sub-chunk's LDS is consumed
+      if (((sb0 + sn - start) & (U - 1)) == 0) {   // re-anchor T at a unit boundary
+        TA = TnA;
+        TB = TnB;
+      }
+    }
+    if ((int)threadIdx.x < sn) {
+      s_p[0][threadIdx.x] = sp0;
+      s_p[1][threadIdx.x] = sp1;
+      s_p[2][threadIdx.x] = sp2;
+    }
+    for (int i = threadIdx.x; i < kPartial * 2 * (kChunk3 + 1) / 4; i += 128)   // b128 stores
+      reinterpret_cast<float4*>(&L[0][0][0])[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (threadIdx.x == 0 && (kPartial * 2 * (kChunk3 + 1)) % 4 != 0)
+      for (int i = kPartial * 2 * (kChunk3 + 1) / 4 * 4; i < kPartial * 2 * (kChunk3 + 1); ++i) (&L[0][0][0])[i] = 0.f;
+    __syncthreads();
+    const int lastqA = lastA - sb0 < kChunk3 ? lastA - sb0 : -1, lastqB = lastB - sb0 < kChunk3 ? lastB - sb0 : -1;
+    // cull the sub-chunk against the wave's 16x8 half-tile (exact test), survivors back to front
+    int nsurv = 0;
+    {
+      const float x0 = (float)hx0, y0 = (float)hy0;
+#pragma unroll
+      for (int q = kChunk3 / 64 - 1; q >= 0; --q) {
+        const int k = q * 64 + lane;
+        float4 r0 = s_p[0][k], r1 = s_p[1][k], r2 = s_p[2][k];
+        unpack_rec<true>(r0, r1, r2);
+        const bool keep = k < sn && (sb0 + k) <= wlast && cull_keep<true>(r0, r1, r2, x0, x0 + 15.f, y0, y0 + 7.f);
+        const unsigned long long mk = __ballot(keep);
+        if (keep) {
+          const unsigned long long above = lane == 63 ? 0ull : (mk >> (lane + 1));
+          s_list[wv][nsurv + __popcll(above)] = (unsigned char)k;
+        }
+        nsurv += __popcll(mk);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ... and against the eight 4x4 boxes (one survivor per lane, its record read once)
+    int nbx[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) nbx[b] = 0;
+    {
+      const unsigned long long below = (1ull << lane) - 1ull;
+      for (int s0 = 0; s0 < nsurv; s0 += 64) {
+        const int si = s0 + lane;
+        const bool in = si < nsurv;
+        const int k = s_list[wv][in ? si : 0];
+        float4 r0 = s_p[0][k], r1 = s_p[1][k], r2 = s_p[2][k];
+        unpack_rec<true>(r0, r1, r2);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          const float x0 = (float)(hx0 + 4 * (b & 3)), y0 = (float)(hy0 + 4 * (b >> 2));
+          const bool keep = in && cull_keep<true>(r0, r1, r2, x0, x0 + 3.f, y0, y0 + 3.f);
+          const unsigned long long m = __ballot(keep);
+          if (keep) s_box[wv][b][grouped_slot(nbx[b] + __popcll(m & below))] = (unsigned char)k;
+          nbx[b] += __popcll(m);
+        }
+      }
+    }
+    int nb = nbx[0], ngrp = nbx[0];
+#pragma unroll
+    for (int b = 1; b < 8; ++b) {
+      nb = box == b ? nbx[b] : nb;
+      ngrp = max(ngrp, nbx[b]);
+    }
+    const int npad = (ngrp + kGroup - 1) / kGroup * kGroup;
+    for (int s = nb + pp; s < npad; s += 8) s_box[wv][box][grouped_slot(s)] = (unsigned char)kNull;
+    __builtin_amdgcn_wave_barrier();
+    // the walk: both pixels of the lane per entry, their contributions summed in registers
+    for (int g0 = 0, gb = 0; g0 < ngrp; g0 += kGroup, gb += 8) {
+      float acc[64];
+      acc[63] = 0.f;
+      const uint2 w8 = *reinterpret_cast<const uint2*>(my_list + gb);
+#pragma unroll
+      for (int g = 0; g < kGroup; ++g) {
+        const int k = (int)(((g < 4 ? w8.x : w8.y) >> (8 * (g & 3))) & 0xFFu);
+        const float4 p0 = s_p[0][k];   // x, y, o, r
+        const float4 p1 = s_p[1][k];   // a, b, c, g
+        const float cbl = reinterpret_cast<const float*>(&s_p[2][k])[0];   // blue
+        const float dx = p0.x - px, dyA = p0.y - pyA;
+        const int ks = sb0 + k;   // the entry's list position (the zero pad slot is never valid: alpha 0)
+        float a6 = 0.f, a7 = 0.f, a8 = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, a4 = 0.f, a5 = 0.f;
+        auto pixel = [&](float dy, int last, int lastq, float Tl, float vr, float vg, float vb, float& T,
+                         float& mu) {
+          const float sigma = conic_sigma(p1, dx, dy);
+          const float alpha = p0.z * __expf(-sigma);
+          const bool valid = ks <= last && alpha >= cut2d;
+          const float alpha_v = valid ? alpha : 0.f;
+          const float ra = __builtin_amdgcn_rcpf(1.f - alpha_v);
+          T = k == lastq ? Tl : T * ra;
+          const float fac = alpha_v * T;
+          a6 += fac * vr;
+          a7 += fac * vg;
+          a8 += fac * vb;
+          const float cv = p0.w * vr + p1.w * vg + cbl * vb;
+          const float dmu = cv - mu;
+          const float v_sig = -alpha_v * (T * dmu);
+          mu = mu + alpha_v * dmu;
+          const float tx_ = v_sig * dx, ty_ = v_sig * dy;
+          a0 += tx_;
+          a1 += ty_;
+          a2 += tx_ * dx;
+          a3 += tx_ * dy;
+          a4 += ty_ * dy;
+          a5 += v_sig;
+        };
+        pixel(dyA, lastA, lastqA, TlA, vrA, vgA, vbA, TA, muA);
+        pixel(p0.y - pyB, lastB, lastqB, TlB, vrB, vgB, vbB, TB, muB);   // (dy as the forward forms it)
+        acc[g * kPartial + 0] = a0;
+        acc[g * kPartial + 1] = a1;
+        acc[g * kPartial + 2] = a2;
+        acc[g * kPartial + 3] = a3;
+        acc[g * kPartial + 4] = a4;
+        acc[g * kPartial + 5] = a5;
+        acc[g * kPartial + 6] = a6;
+        acc[g * kPartial + 7] = a7;
+        acc[g * kPartial + 8] = a8;
+      }
+      float sum[8];
+      reduce_box8(acc, sum);
+      float4* st = reinterpret_cast<float4*>(&s_stage[wv][lane][0]);
+      st[0] = make_float4(sum[0], sum[1], sum[2], sum[3]);
+      st[1] = make_float4(sum[4], sum[5], sum[6], sum[7]);
+      __builtin_amdgcn_wave_barrier();
+      if (fown) {
+#pragma unroll
+        for (int bx = 0; bx < 8; ++bx) {
+          const int k = s_box[wv][bx][gb + fg];
+          Lw[k] += stage_rd[8 * bx];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    // the previous sub-chunk's ids, emission indices, records and T anchors, read while this
+    // one's rows are summed and stored (assigned on every path)
+    const bool more = sub > 0 && (int)threadIdx.x < kChunk3;
+    const int kos_next = more ? k_of_s[sb0 - kChunk3 + threadIdx.x] : 0;
+    sp0 = sp1 = sp2 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (more) {
+      const int id_next = ids[sb0 - kChunk3 + threadIdx.x];
+      sp0 = rec4[3 * (int64_t)id_next + 0];
+      sp1 = rec4[3 * (int64_t)id_next + 1];
+      sp2 = rec4[3 * (int64_t)id_next + 2];
+    }
+    {
+      const int ue = sb0 - start;
+      const bool anch = sub > 0 && (ue & (U - 1)) == 0;
+      const int64_t arow = (int64_t)(cbase + ue / U) * kRasterThreads;
+      TnA = anch && lastA >= sb0 ? anchors[arow + slotA] : TfA;
+      TnB = anch && lastB >= sb0 ? anchors[arow + slotB] : TfB;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < sn) {
+      const int k = threadIdx.x;
+      float v[kPartial];
+#pragma unroll
+      for (int q = 0; q < kPartial; ++q) v[q] = L[q][0][k] + L[q][1][k];
+      const float4 p1 = s_p[1][k];
+      const float mx = v[0], my = v[1];
+      v[0] = 2.f * p1.x * mx + p1.y * my;
+      v[1] = p1.y * mx + 2.f * p1.z * my;
+      v[5] = -v[5] / s_p[0][k].z;
+      store_partial_row(partial, kos_mine & kEmitIndexMask, v);
+    }
+    sb0 -= kChunk3;
+    sn = kChunk3;
+    kos_mine = kos_next;
+  }
+}
+
+// ---------------------------------------------------------------- 3D backward, pixel pairs
+// k_raster_bwd (3D, one 128-entry chunk per workgroup, no fused loss, one sub-chunk) with the
+// layout of k_raster2d_bwd_pair: TWO waves per chunk, wave w the 16x8 half-tile of rows
+// 8w..8w+7, lane l box l & 7 and pixel pair l >> 3 (rows r and r + 2 of the box), both pixels'
+// contributions summed in registers before reduce_box8.  A chunk holds half the waves of the
+// 4-wave kernel, so more chunks are in flight per CU for the same number of waves.
+#ifndef GSR_BWD3D_PAIR
+#define GSR_BWD3D_PAIR 0
+#endif
+#ifndef GSR_BWD3P_MINB
+#define GSR_BWD3P_MINB 3   // waves per SIMD the compiler aims at
+#endif
+__global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
+    const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const float4* __restrict__ ckpt, int W, int H,
+    int tw, int th, const float* __restrict__ bg, const float* __restrict__ final_T,
+    const int32_t* __restrict__ last_in, const float* __restrict__ v_rgb, const float* __restrict__ v_alpha,
+    float* __restrict__ partial, const int32_t* __restrict__ chunk_list, gsr_bin_stats* __restrict__ stats,
+    const int32_t* __restrict__ k_of_s) {
+  constexpr int kNull = kChunk3;
+  constexpr int kGroup = GSR_BWD_GROUP;
+  static_assert(kGroup == 7 && kPartial == 9, "reduce_box8 sums 7 entries x 9 values in 64 registers");
+  constexpr int kLen = kChunk3 + kGroup;
+  constexpr int kLenB = 8 * ((kLen + kGroup - 1) / kGroup);
+  __shared__ float4 s_p[3][kChunk3 + 1];   // the chunk's records (Splat parts)
+  __shared__ __attribute__((aligned(16))) float L[kPartial][2][kChunk3 + 1];
+  __shared__ unsigned char s_list[2][kLen];
+  __shared__ __attribute__((aligned(16))) unsigned char s_box[2][8][kLenB];
+  __shared__ __attribute__((aligned(16))) float s_stage[2][64][8];
+  const int4 cd = reinterpret_cast<const int4*>(chunk_list)[blockIdx.x];
+  const int n_act = stats->n_active, ovf = stats->overflow, ce = stats->chunk_entries;
+  const bool unit_bad = ce != kChunk3;
+  if ((ovf != 0) | ((int)blockIdx.x >= n_act) | unit_bad | (cd.y <= 0)) {
+    if (unit_bad && blockIdx.x == 0 && threadIdx.x == 0) {
+      atomicOr(&stats->overflow, GSR_OVF_UNIT);
+      if (stats->status != nullptr) atomicOr(stats->status, GSR_OVF_UNIT);
+    }
+    return;
+  }
+  const int b0 = cd.x, sn = cd.y, chunk = cd.z, ct = cd.w;
+  int c, ty, tx;
+  tile_coords(ct, tw, th, c, ty, tx);
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int box = lane & 7, pp = lane >> 3;
+  const int hx0 = tx * kTile, hy0 = ty * kTile + 8 * wv;   // the wave's 16x8 half-tile
+  const int bjl = 4 * (box & 3), bil = 8 * wv + 4 * (box >> 2);
+  const int jl = bjl + (pp & 3), ilA = bil + (pp >> 2), ilB = ilA + 2;
+  const int pj = tx * kTile + jl, piA = ty * kTile + ilA, piB = ty * kTile + ilB;
+  const bool inA = piA < H && pj < W, inB = piB < H && pj < W;
+  const float px = (float)pj + 0.5f, pyA = (float)piA + 0.5f, pyB = (float)piB + 0.5f;
+  // every load up front (see k_raster_bwd): the two pixels' chunk records and state, ids, records
+  const float4 rckA = ckpt[(int64_t)chunk * kRasterThreads + bwd_pixel_slot(ilA, jl)];
+  const float4 rckB = ckpt[(int64_t)chunk * kRasterThreads + bwd_pixel_slot(ilB, jl)];
+  const int id_mine = (int)threadIdx.x < sn ? ids[b0 + threadIdx.x] : 0;
+  const int kos_mine = (int)threadIdx.x < sn ? k_of_s[b0 + threadIdx.x] : 0;
+  float TfA = 1.f, vrA = 0.f, vgA = 0.f, vbA = 0.f, vaA = 0.f;
+  float TfB = 1.f, vrB = 0.f, vgB = 0.f, vbB = 0.f, vaB = 0.f;
+  int lastA = -1, lastB = -1;
+  if (inA) {
+    const int64_t pix = ((int64_t)c * H + piA) * W + pj;
+    lastA = last_in[pix];
+    TfA = final_T[pix];
+    vrA = v_rgb[pix * 3 + 0];
+    vgA = v_rgb[pix * 3 + 1];
+    vbA = v_rgb[pix * 3 + 2];
+    vaA = v_alpha[pix];
+  }
+  if (inB) {
+    const int64_t pix = ((int64_t)c * H + piB) * W + pj;
+    lastB = last_in[pix];
+    TfB = final_T[pix];
+    vrB = v_rgb[pix * 3 + 0];
+    vgB = v_rgb[pix * 3 + 1];
+    vbB = v_rgb[pix * 3 + 2];
+    vaB = v_alpha[pix];
+  }
+  const float4* const rec4 = reinterpret_cast<const float4*>(rec);
+  if ((int)threadIdx.x < sn) {
+    s_p[0][threadIdx.x] = rec4[3 * (int64_t)id_mine + 0];
+    s_p[1][threadIdx.x] = rec4[3 * (int64_t)id_mine + 1];
+    s_p[2][threadIdx.x] = rec4[3 * (int64_t)id_mine + 2];
+  }
+  for (int i = threadIdx.x; i < kPartial * 2 * (kChunk3 + 1) / 4; i += 128)   // b128 stores
+    reinterpret_cast<float4*>(&L[0][0][0])[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (threadIdx.x == 0 && (kPartial * 2 * (kChunk3 + 1)) % 4 != 0)
+    for (int i = kPartial * 2 * (kChunk3 + 1) / 4 * 4; i < kPartial * 2 * (kChunk3 + 1); ++i) (&L[0][0][0])[i] = 0.f;
+  if (threadIdx.x < 3) s_p[threadIdx.x][kNull] = make_float4(0.f, 0.f, 0.f, 0.f);
+  // the pixels' state at the chunk's end: {T_end, suffix colour sum} (forward epilogue); a pixel
+  // that stopped before the chunk contributes nothing
+  const bool liveA = lastA >= b0, liveB = lastB >= b0;
+  if (!liveA) { TfA = 1.f; vrA = vgA = vbA = vaA = 0.f; }
+  if (!liveB) { TfB = 1.f; vrB = vgB = vbB = vaB = 0.f; }
+  const float* bgc = bg + c * 3;
+  float TA = liveA ? rckA.x : TfA, TB = liveB ? rckB.x : TfB;
+  const float vTaA = TfA * (vaA - (bgc[0] * vrA + bgc[1] * vgA + bgc[2] * vbA));
+  const float vTaB = TfB * (vaB - (bgc[0] * vrB + bgc[1] * vgB + bgc[2] * vbB));
+  float SvA = liveA ? rckA.y * vrA + rckA.z * vgA + rckA.w * vbA : 0.f;
+  float SvB = liveB ? rckB.y * vrB + rckB.z * vgB + rckB.w * vbB : 0.f;
+  const int wlast = wave_max_i(max(lastA, lastB));
+  const int lastkA = min(lastA - b0, kChunk3 - 1), lastkB = min(lastB - b0, kChunk3 - 1);
+  const int fg = lane / kPartial, fq = lane - kPartial * (lane / kPartial);
+  const bool fown = lane < kGroup * kPartial;
+  float* const Lw = &L[fq][wv][0];
+  const float* const stage_rd = &s_stage[wv][(lane >> 3) << 3][lane & 7];   // + 8 * box
+  const unsigned char* my_list = s_box[wv][box];
+  __syncthreads();
+  // cull the chunk against the wave's 16x8 half-tile (exact test), survivors back to front
+  int nsurv = 0;
+  {
+    const float x0 = (float)hx0 + 0.5f, y0 = (float)hy0 + 0.5f;
+#pragma unroll
+    for (int q = kChunk3 / 64 - 1; q >= 0; --q) {
+      const int k = q * 64 + lane;
+      const bool keep = k < sn && (b0 + k) <= wlast &&
+                        cull_keep<false>(s_p[0][k], s_p[1][k], s_p[2][k], x0, x0 + 15.f, y0, y0 + 7.f);
+      const unsigned long long mk = __ballot(keep);
+      if (keep) {
+        const unsigned long long above = lane == 63 ? 0ull : (mk >> (lane + 1));
+        s_list[wv][nsurv + __popcll(above)] = (unsigned char)k;
+      }
+      nsurv += __popcll(mk);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  int nbx[8];
+#pragma unroll
+  for (int b = 0; b < 8; ++b) nbx[b] = 0;
+  {
+    const unsigned long long below = (1ull << lane) - 1ull;
+    for (int s0 = 0; s0 < nsurv; s0 += 64) {
+      const int si = s0 + lane;
+      const bool in = si < nsurv;
+      const int k = s_list[wv][in ? si : 0];
+      const float4 r0 = s_p[0][k], r1 = s_p[1][k], r2 = s_p[2][k];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const float x0 = (float)(hx0 + 4 * (b & 3)) + 0.5f, y0 = (float)(hy0 + 4 * (b >> 2)) + 0.5f;
+        const bool keep = in && cull_keep<false>(r0, r1, r2, x0, x0 + 3.f, y0, y0 + 3.f);
+        const unsigned long long m = __ballot(keep);
+        if (keep) s_box[wv][b][grouped_slot(nbx[b] + __popcll(m & below))] = (unsigned char)k;
+        nbx[b] += __popcll(m);
+      }
+    }
+  }
+  int nb = nbx[0], ngrp = nbx[0];
+#pragma unroll
+  for (int b = 1; b < 8; ++b) {
+    nb = box == b ? nbx[b] : nb;
+    ngrp = max(ngrp, nbx[b]);
+  }
+  const int npad = (ngrp + kGroup - 1) / kGroup * kGroup;
+  for (int s = nb + pp; s < npad; s += 8) s_box[wv][box][grouped_slot(s)] = (unsigned char)kNull;
+  __builtin_amdgcn_wave_barrier();
+  for (int g0 = 0, gb = 0; g0 < ngrp; g0 += kGroup, gb += 8) {
+    float acc[64];
+    acc[63] = 0.f;
+    const uint2 w8 = *reinterpret_cast<const uint2*>(my_list + gb);
+#pragma unroll
+    for (int g = 0; g < kGroup; ++g) {
+      const int k = (int)(((g < 4 ? w8.x : w8.y) >> (8 * (g & 3))) & 0xFFu);
+      const float4 p0 = s_p[0][k];
+      const float4 p1 = s_p[1][k];
+      const float4 p2 = s_p[2][k];
+      const float dx = p0.x - px;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, a4 = 0.f, a5 = 0.f, a6 = 0.f, a7 = 0.f, a8 = 0.f;
+      auto pixel = [&](float dy, int lastk, float vr, float vg, float vb, float vTa, float& T, float& Sv) {
+        const float sigma = conic_sigma(p1, dx, dy);
+        const float vis = __expf(-sigma);
+        const float raw = p0.z * vis;
+        const float alpha = fminf(kAlphaMax, raw);
+        const bool valid = k <= lastk && sigma >= 0.f && alpha >= kAlphaThreshold;
+        const float alpha_v = valid ? alpha : 0.f;
+        const float ra = __builtin_amdgcn_rcpf(1.f - alpha_v);
+        T *= ra;
+        const float fac = alpha_v * T;
+        a6 += fac * vr;
+        a7 += fac * vg;
+        a8 += fac * vb;
+        const float cv = p2.x * vr + p2.y * vg + p2.z * vb;
+        const float v_al = T * cv + ra * (vTa - Sv);
+        const bool unclamped = valid && raw <= kAlphaMax;
+        const float v_sig = unclamped ? -raw * v_al : 0.f;
+        const float tx_ = v_sig * dx, ty_ = v_sig * dy;
+        a0 += tx_;
+        a1 += ty_;
+        a2 += tx_ * dx;
+        a3 += tx_ * dy;
+        a4 += ty_ * dy;
+        a5 += v_sig;
+        Sv += fac * cv;
+      };
+      pixel(p0.y - pyA, lastkA, vrA, vgA, vbA, vTaA, TA, SvA);
+      pixel(p0.y - pyB, lastkB, vrB, vgB, vbB, vTaB, TB, SvB);
+      acc[g * kPartial + 0] = a0;
+      acc[g * kPartial + 1] = a1;
+      acc[g * kPartial + 2] = a2;
+      acc[g * kPartial + 3] = a3;
+      acc[g * kPartial + 4] = a4;
+      acc[g * kPartial + 5] = a5;
+      acc[g * kPartial + 6] = a6;
+      acc[g * kPartial + 7] = a7;
+      acc[g * kPartial + 8] = a8;
+    }
+    float sum[8];
+    reduce_box8(acc, sum);
+    float4* st = reinterpret_cast<float4*>(&s_stage[wv][lane][0]);
+    st[0] = make_float4(sum[0], sum[1], sum[2], sum[3]);
+    st[1] = make_float4(sum[4], sum[5], sum[6], sum[7]);
+    __builtin_amdgcn_wave_barrier();
+    if (fown) {
+#pragma unroll
+      for (int bx = 0; bx < 8; ++bx) {
+        const int k = s_box[wv][bx][gb + fg];
+        Lw[k] += stage_rd[8 * bx];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < sn) {
+    const int k = threadIdx.x;
+    float v[kPartial];
+#pragma unroll
+    for (int q = 0; q < kPartial; ++q) v[q] = L[q][0][k] + L[q][1][k];
+    const float4 p1 = s_p[1][k];
+    const float mx = v[0], my = v[1];
+    v[0] = 2.f * p1.x * mx + p1.y * my;
+    v[1] = p1.y * mx + 2.f * p1.z * my;
+    v[5] = -v[5] / s_p[0][k].z;
+    store_partial_row(partial, kos_mine & kEmitIndexMask, v);
+  }
+}
+
 #ifdef GSR_BWD_TRACE
 extern "C" int gsr_debug_bwd_trace(void* buf) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_bwd_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
@@ -2031,9 +2530,18 @@ static int raster_bwd(const char* who, const float* rec, const int32_t* sorted_i
     (void)chunk_base;
     (void)lt;
     const int64_t CT = (int64_t)C * tw * th;
-    hipLaunchKernelGGL(k_raster2d_bwd_tile, dim3((unsigned)sweep_grid2d(CT)), dim3(kRasterThreads), 0,
-                       (hipStream_t)stream, (const Splat*)rec, sorted_ids, chunk_state, width, height, tw, th, bg,
-                       final_T, last, v_rgb, v_alpha, partial, chunk_list, stats, k_of_s, cut2d, sets);
+    if (GSR_BWD2D_PAIR)
+      hipLaunchKernelGGL(k_raster2d_bwd_pair, dim3((unsigned)sweep_grid2d(CT)), dim3(128), 0,
+                         (hipStream_t)stream, (const Splat*)rec, sorted_ids, chunk_state, width, height, tw, th, bg,
+                         final_T, last, v_rgb, v_alpha, partial, chunk_list, stats, k_of_s, cut2d, sets);
+    else
+      hipLaunchKernelGGL(k_raster2d_bwd_tile, dim3((unsigned)sweep_grid2d(CT)), dim3(kRasterThreads), 0,
+                         (hipStream_t)stream, (const Splat*)rec, sorted_ids, chunk_state, width, height, tw, th, bg,
+                         final_T, last, v_rgb, v_alpha, partial, chunk_list, stats, k_of_s, cut2d, sets);
+  } else if (!LOSS && GSR_BWD3D_PAIR && chunk_entries <= kChunk3) {
+    hipLaunchKernelGGL(k_raster_bwd_pair3d, dim3(n_chunks), dim3(128), 0, (hipStream_t)stream, (const Splat*)rec,
+                       sorted_ids, (const float4*)chunk_state, width, height, tw, th, bg, final_T, last, v_rgb,
+                       v_alpha, partial, chunk_list, stats, k_of_s);
   } else if (chunk_entries > kChunk3)
     hipLaunchKernelGGL((k_raster_bwd<LOSS, IS2D, true>), dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
                        (const Splat*)rec, sorted_ids, tile_offset, tile_end, chunk_base,
