@@ -112,6 +112,8 @@ def parse(argv=None):
                          "(train_script.py:127-133) fused into libgsr kernels, or as plain torch ops")
     ap.add_argument("--fwd-lanes", type=int, default=0, choices=[0, 4, 16],
                     help="3D raster forward layout: 0 automatic, 4 or 16 lanes per pixel (gsr_set_fwd_lanes)")
+    ap.add_argument("--bwd-layout", type=int, default=0, choices=[0, 1, 2],
+                    help="3D raster backward layout: 0 automatic, 1 one pixel per lane, 2 two (gsr_set_bwd_layout)")
     ap.add_argument("--emit-staged", type=int, default=-1, choices=[-1, 0, 1],
                     help="emission layout (gsr_set_emit_staged): 1 LDS-staged per-tile runs, 0 direct "
                          "scatter, -1 library default")
@@ -171,7 +173,7 @@ def step_bytes(C: int, N: int, P: int, I: int, I_eff: int, p: int, backward: boo
 
 
 # libgsr call name (render.py timing brackets) -> substring of its dominant kernel's symbol
-KERNEL_SYMBOL = {"raster3d_bwd": "k_raster_bwd<false, false,", "raster3d_fwd": "k_raster_fwd<false,",
+KERNEL_SYMBOL = {"raster3d_bwd": "k_raster_bwd", "raster3d_fwd": "k_raster_fwd<false,",
                  "raster2d_bwd": "k_raster2d_bwd_pair", "raster2d_fwd": "k_raster_fwd_box<true>",
                  "bin_sort": "k_segsort", "project3d_fwd": "k_project3d_fwd", "project3d_bwd": "k_project3d_bwd",
                  "project2d_fwd": "k_project2d_fwd", "project2d_bwd": "k_project2d_bwd", "bin_emit": "k_emit"}
@@ -1043,6 +1045,7 @@ def main(argv=None):
     if args.graph and args.capacity != "bounded":
         raise SystemExit("--graph 1 needs --capacity bounded (an exact step waits on the host)")
     _lib.check(_lib.lib().gsr_set_fwd_lanes(args.fwd_lanes), "gsr_set_fwd_lanes")
+    _lib.check(_lib.lib().gsr_set_bwd_layout(args.bwd_layout), "gsr_set_bwd_layout")
     if args.emit_staged >= 0:
         _lib.check(_lib.lib().gsr_set_emit_staged(args.emit_staged), "gsr_set_emit_staged")
     if args.lazy:

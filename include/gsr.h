@@ -156,7 +156,8 @@ int gsr_version(void);
  * unit per sweep slot: chunk_list needs >= C * tiles + 8 entries. */
 /* Revision 8: 2D records are stored packed (layout above): the 2D walks read them as 2 x b128 +
  * b32 from LDS as staged (or gathered straight into LDS). */
-#define GSR_ABI_VERSION 8
+/* Revision 9: gsr_set_bwd_layout (the 3D raster backward's layout, process-wide). */
+#define GSR_ABI_VERSION 9
 int gsr_abi_version(void);
 const char* gsr_last_error(void);
 
@@ -173,6 +174,13 @@ int gsr_selftest_reduce_box16(float* out, void* stream);
  * tile; 2D: 1 lane per pixel, one workgroup per tile), or 1, 4 or 16 (3D only) to force one.
  * All give the same result up to fp32 regrouping of the transmittance products. */
 int gsr_set_fwd_lanes(int lanes);
+
+/* Layout of the 3D raster backward (process-wide): 0 = automatic (two pixels per lane in 2-wave
+ * workgroups when the call has at least 64 tiles (cameras x tiles) per compute unit, else one
+ * pixel per lane in 4-wave workgroups), 1 = one pixel per lane, 2 = two pixels per lane.  Calls
+ * with a fused loss or multi-chunk units always run one pixel per lane.  The layouts sum the
+ * pixels' terms in different orders (fp32 regrouping); each is deterministic. */
+int gsr_set_bwd_layout(int layout);
 
 /* Self-test of the lane-ordered LDS atomics the tile sort's ranking relies on: writes the
  * number of violations (0 expected) to the device int *violations. */

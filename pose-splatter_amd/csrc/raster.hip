@@ -27,6 +27,7 @@ constexpr int kFwdLdsPad = GSR_FWD_PAD_3D;
 #endif
 constexpr int kFwdLdsPad2D = GSR_FWD_PAD_2D;
 static int g_fwd_lanes = 0;   // gsr_set_fwd_lanes: 0 automatic, 1 / 4 / 16 forced
+static int g_bwd_layout = 0;  // gsr_set_bwd_layout: 0 automatic, 1 chunk kernel, 2 pixel pairs (3D)
 // box forward (k_raster_fwd_box) build knobs, for A/B measurements: lanes grouped by box along
 // the ds_read_b128 lane groups, and the 2D walk's records packed into 2 x b128 + b32
 #ifndef GSR_BOX_LANES
@@ -1135,6 +1136,219 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
   if (threadIdx.x == 0 && s_max >= 0) tile_end[ct] = s_max;   // one workgroup per tile; finalised by k_raster_finalize
 }
 
+// ---------------------------------------------------------------- 2D forward, pixel pairs
+// The 2D box forward with TWO pixels per lane: one 2-wave workgroup per tile, wave w the 16x8
+// half-tile of rows 8w..8w+7, eight 4x4 boxes per wave.  A lane's pixels are (r, j) and
+// (r + 2, j) of its box, so every record read from LDS (2 x b128 + b32) and the step's slot read
+// serve two pixels.  Lanes: box = 2 x (the lane's ds_read_b128 group) + (lane bit 4), so a b128
+// read of the walk has two addresses per lane group (the box forward's broadcast trick, halved).
+// The list is walked in 128-entry rounds (one chunk each; records double-buffered in 12 KB of
+// LDS), so 11 workgroups (22 waves) fit a CU.  Per pixel the arithmetic is the box forward's,
+// operation for operation (dx = x - px, dy = y - py, conic_sigma, alpha >= cut2d, T <- T (1 - a),
+// stop after T <= 2^-25), so k_raster2d_bwd_pair's validity tests agree with it exactly.
+#ifndef GSR_FWD2D_PAIR
+#define GSR_FWD2D_PAIR 0
+#endif
+#ifndef GSR_FWD2P_MINB
+#define GSR_FWD2P_MINB 5   // waves per SIMD the compiler aims at
+#endif
+__global__ __launch_bounds__(128, GSR_FWD2P_MINB) void k_raster2d_fwd_pair(
+    const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ tile_offset, int W,
+    int H, int tw, int th, const float* __restrict__ bg, float* __restrict__ out_rgb, float* __restrict__ out_alpha,
+    float* __restrict__ out_T, int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end,
+    float* __restrict__ anchors, const int32_t* __restrict__ chunk_base, int64_t CT, float cut2d,
+    const gsr_bin_stats* __restrict__ stats, const Sets2D sets) {
+  constexpr int kHS = kChunk3 + 1;   // part j of round entry k at s_r[buf][j][k]; slot 128 a zero record
+  __shared__ float4 s_r[2][3][kHS];
+  __shared__ __attribute__((aligned(16))) unsigned char s_box[2][8][kBoxStride];
+  __shared__ int s_max;
+  const int ct = sweep_tile2d(blockIdx.x, CT, tw * th, sets.begin, sets.F);
+  const int ovf = stats->overflow;
+  if (ovf) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && stats->status != nullptr) atomicOr(stats->status, ovf);
+    nan_fill(CT, W, H, tw, th, out_rgb, out_alpha);
+    return;
+  }
+  if (ct < 0) return;
+  int c, ty, tx;
+  tile_coords(ct, tw, th, c, ty, tx);
+  rec += rec_offset2d(sets.begin, sets.F, c, sets.N);   // the set's record copy
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int grp = ((lane >> 4) & 2) | (((lane >> 4) ^ (lane >> 3) ^ (lane >> 2)) & 1);   // b128 lane group
+  const int box = 2 * grp + ((lane >> 4) & 1);
+  const int pp = (lane & 3) | ((lane >> 1) & 4);   // pixel pair in the box (lane bits 0, 1, 3)
+  const int jl = 4 * (box & 3) + (pp & 3), ilA = 8 * wv + 4 * (box >> 2) + (pp >> 2), ilB = ilA + 2;
+  const int pj = tx * kTile + jl, piA = ty * kTile + ilA, piB = ty * kTile + ilB;
+  const bool inA = piA < H && pj < W, inB = piB < H && pj < W;
+  const float px = (float)pj, pyA = (float)piA, pyB = (float)piB;   // integer centres
+  const int slotA = bwd_pixel_slot(ilA, jl), slotB = bwd_pixel_slot(ilB, jl);
+  const int hx0 = tx * kTile, hy0 = ty * kTile + 8 * wv;   // the wave's half-tile origin
+  const int start = tile_offset[ct], end = tile_offset[ct + 1];
+  if (tid == 0) s_max = -1;
+  float TA = 1.f, TlA = 1.f, crA = 0.f, cgA = 0.f, cbA = 0.f, drA = 0.f, dgA = 0.f, dbA = 0.f;
+  float TB = 1.f, TlB = 1.f, crB = 0.f, cgB = 0.f, cbB = 0.f, drB = 0.f, dgB = 0.f, dbB = 0.f;
+  int lastA = -1, lastB = -1;
+  bool doneA = !inA, doneB = !inB;
+  const int cbase = chunk_base[ct];
+  const int umask = stats->chunk_entries - 1;
+  int kcur = 0;
+  const int e_last = max(end - 1, start);
+  float4 c0 = make_float4(0.f, 0.f, 0.f, 0.f), c1 = c0, c2 = c0;
+  int idn = 0;
+  if (end > start) {
+    const int id0 = ids[min(start + tid, e_last)];
+    idn = ids[min(start + kChunk3 + tid, e_last)];
+    c0 = rec[id0].p0;
+    c1 = rec[id0].p1;
+    c2 = rec[id0].p2;
+  }
+  if (tid < 6) s_r[tid / 3][tid % 3][kChunk3] = make_float4(0.f, 0.f, 0.f, 0.f);
+  int buf = 0;
+  for (int rb = start; rb < end; rb += kChunk3, buf ^= 1) {
+    s_r[buf][0][tid] = c0;
+    s_r[buf][1][tid] = c1;
+    s_r[buf][2][tid] = c2;
+    {
+      const int id_use = idn;
+      idn = ids[min(rb + 2 * kChunk3 + tid, e_last)];
+      c0 = rec[id_use].p0;
+      c1 = rec[id_use].p1;
+      c2 = rec[id_use].p2;
+    }
+    if (__syncthreads_count(!(doneA && doneB)) == 0) break;
+    if (rb > start && ((rb - start) & umask) == 0) {   // entering unit kcur+1: the pixels' T anchors
+      if (anchors) {
+        const int64_t arow = (int64_t)(cbase + kcur + 1) * kRasterThreads;
+        anchors[arow + slotA] = TA;
+        anchors[arow + slotB] = TB;
+      }
+      crA += drA;
+      cgA += dgA;
+      cbA += dbA;
+      crB += drB;
+      cgB += dgB;
+      cbB += dbB;
+      drA = dgA = dbA = drB = dgB = dbB = 0.f;
+      ++kcur;
+    }
+    const int nh = min(kChunk3, end - rb);
+    // the round's survivors of the half-tile cull, in this wave's own slots of the idle buffer
+    // (dead since the round barrier; rewritten only by this wave's threads at the next round)
+    unsigned char* const s_list_w = reinterpret_cast<unsigned char*>(&s_r[buf ^ 1][0][64 * wv]);
+    const float4* const r0 = s_r[buf][0];
+    const float4* const r1 = s_r[buf][1];
+    const float4* const r2 = s_r[buf][2];
+    int nsurv = 0;
+#pragma unroll
+    for (int q = 0; q < kChunk3 / 64; ++q) {
+      const int k = q * 64 + lane;
+      float4 a = r0[k], b = r1[k], d = r2[k];
+      unpack_rec<true>(a, b, d);
+      const bool keep = k < nh && cull_keep<true>(a, b, d, (float)hx0, (float)hx0 + 15.f, (float)hy0, (float)hy0 + 7.f);
+      const unsigned long long m = __ballot(keep);
+      if (keep)
+        s_list_w[nsurv + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] =
+            (unsigned char)k;
+      nsurv += __popcll(m);
+    }
+    __builtin_amdgcn_wave_barrier();
+    int nbx[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) nbx[b] = 0;
+    {
+      const unsigned long long below = (1ull << lane) - 1ull;
+      for (int s0 = 0; s0 < nsurv; s0 += 64) {
+        const int si = s0 + lane;
+        const bool in = si < nsurv;
+        const int k = s_list_w[in ? si : 0];
+        float4 a = r0[k], b = r1[k], d = r2[k];
+        unpack_rec<true>(a, b, d);
+#pragma unroll
+        for (int bx = 0; bx < 8; ++bx) {
+          const float x0 = (float)(hx0 + 4 * (bx & 3)), y0 = (float)(hy0 + 4 * (bx >> 2));
+          const bool keep = in && cull_keep<true>(a, b, d, x0, x0 + 3.f, y0, y0 + 3.f);
+          const unsigned long long m = __ballot(keep);
+          if (keep) s_box[wv][bx][nbx[bx] + __popcll(m & below)] = (unsigned char)k;
+          nbx[bx] += __popcll(m);
+        }
+      }
+    }
+    int nb = nbx[0], nmax = nbx[0];
+#pragma unroll
+    for (int b = 1; b < 8; ++b) {
+      nb = box == b ? nbx[b] : nb;
+      nmax = max(nmax, nbx[b]);
+    }
+    unsigned char* const lst = s_box[wv][box];
+    for (int s = nb + pp; s < nmax; s += 8) lst[s] = (unsigned char)kChunk3;   // the zero record
+    __builtin_amdgcn_wave_barrier();
+    int k_next = lst[0];
+    int lkA = -1, lkB = -1;
+    for (int t0 = 0; t0 < nmax; t0 += 32) {
+      if (t0 > 0 && __ballot(!(doneA && doneB)) == 0ull) break;
+      const int t1 = min(t0 + 32, nmax);
+#pragma nounroll
+      for (int t = t0; t < t1; ++t) {
+        const int k = k_next;
+        k_next = lst[t + 1];   // past the padded list: read, never used
+        __builtin_assume((unsigned)k <= (unsigned)kChunk3);
+        const float4* rk = r0 + k;   // part j at rk[kHS j]
+        const float4 p0 = rk[0], p1 = rk[kHS];   // (x, y, o, r), (a, b, c, g)
+        const float cbl = reinterpret_cast<const float*>(rk + 2 * kHS)[0];   // blue
+        const float dx = p0.x - px;
+        {
+          const float dy = p0.y - pyA;
+          const float alpha = p0.z * __expf(-conic_sigma(p1, dx, dy));
+          const bool valid = !doneA && alpha >= cut2d;
+          const float av = valid ? alpha : 0.f;
+          const float vis = av * TA;
+          drA += p0.w * vis;
+          dgA += p1.w * vis;
+          dbA += cbl * vis;
+          TlA = valid ? TA : TlA;
+          TA = TA * (1.f - av);
+          lkA = valid ? k : lkA;
+          doneA = doneA || TA <= kT2DMin;
+        }
+        {
+          const float dy = p0.y - pyB;
+          const float alpha = p0.z * __expf(-conic_sigma(p1, dx, dy));
+          const bool valid = !doneB && alpha >= cut2d;
+          const float av = valid ? alpha : 0.f;
+          const float vis = av * TB;
+          drB += p0.w * vis;
+          dgB += p1.w * vis;
+          dbB += cbl * vis;
+          TlB = valid ? TB : TlB;
+          TB = TB * (1.f - av);
+          lkB = valid ? k : lkB;
+          doneB = doneB || TB <= kT2DMin;
+        }
+      }
+    }
+    if (lkA >= 0) lastA = rb + lkA;
+    if (lkB >= 0) lastB = rb + lkB;
+    __builtin_amdgcn_wave_barrier();
+  }
+  const float* bgc = bg + c * 3;
+  auto store = [&](bool in, int pi, float T, float Tl, float cr, float cg, float cb, int last) {
+    if (!in) return;
+    const int64_t pix = ((int64_t)c * H + pi) * W + pj;
+    out_rgb[pix * 3 + 0] = cr + T * bgc[0];
+    out_rgb[pix * 3 + 1] = cg + T * bgc[1];
+    out_rgb[pix * 3 + 2] = cb + T * bgc[2];
+    out_alpha[pix] = 1.f - T;
+    reinterpret_cast<float2*>(out_T)[pix] = make_float2(T, Tl);
+    out_last[pix] = last;
+  };
+  store(inA, piA, TA, TlA, crA + drA, cgA + dgA, cbA + dbA, lastA);
+  store(inB, piB, TB, TlB, crB + drB, cgB + dgB, cbB + dbB, lastB);
+  const int lmax = max(lastA, lastB);
+  if (lmax >= 0) atomicMax(&s_max, lmax);
+  __syncthreads();
+  if (tid == 0 && s_max >= 0) tile_end[ct] = s_max;   // one workgroup per tile; finalised by k_raster_finalize
+}
+
 // Per busy tile: tile_end = 1 + max last over the tile's four quadrant workgroups (or the
 // tile's start), the cut key, and the tile's active chunks appended to the backward's list.
 // (A separate launch: finishing it inside the forward by the last-arriving quadrant
@@ -2151,9 +2365,13 @@ __global__ __launch_bounds__(128, GSR_BWD2P_MINB) void k_raster2d_bwd_pair(
 // 8w..8w+7, lane l box l & 7 and pixel pair l >> 3 (rows r and r + 2 of the box), both pixels'
 // contributions summed in registers before reduce_box8.  A chunk holds half the waves of the
 // 4-wave kernel, so more chunks are in flight per CU for the same number of waves.
-#ifndef GSR_BWD3D_PAIR
-#define GSR_BWD3D_PAIR 0
-#endif
+// The pair layout is the throughput choice: it keeps 7 chunks per CU in flight (the 4-wave
+// kernel 5) at a longer chunk latency, so the automatic choice (gsr_set_bwd_layout 0) takes it
+// only for calls with many tiles per CU -- config 5 (27 648 tiles, ~35k chunks): raster bwd
+// 0.60 -> 0.56 ms; config 3 (6 912 tiles, ~7.4k chunks): 0.136 -> 0.140 ms
+// (r04_c35_pair3d_ab.txt).  The rule reads the call's shape (cameras x tiles), not its chunk
+// count, so a bounded call and an exact one of the same shape take the same kernel (bitwise).
+constexpr int kBwdPairTilesPerCU = 64;
 #ifndef GSR_BWD3P_MINB
 #define GSR_BWD3P_MINB 3   // waves per SIMD the compiler aims at
 #endif
@@ -2425,6 +2643,12 @@ int gsr_set_fwd_lanes(int lanes) {
   return GSR_OK;
 }
 
+int gsr_set_bwd_layout(int layout) {
+  GSR_REQUIRE(layout >= 0 && layout <= 2, "gsr_set_bwd_layout: layout must be 0 (auto), 1 or 2, got %d", layout);
+  gsr::g_bwd_layout = layout;
+  return GSR_OK;
+}
+
 int gsr_selftest_reduce_box16(float* out, void* stream) {
   hipLaunchKernelGGL(k_selftest_reduce_box16, dim3(1), dim3(64), 0, (hipStream_t)stream, out);
   GSR_LAUNCH_CHECK("k_selftest_reduce_box16");
@@ -2487,6 +2711,11 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
                        dim3(kRasterThreads), IS2D ? kFwdLdsPad2D : kFwdLdsPad, s, (const Splat*)rec, sorted_ids, kos,
                        tile_offset, tile_order, width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end,
                        (float4*)chunk_state, chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz, stats, sets);
+  } else if (IS2D && GSR_FWD2D_PAIR) {
+    // 2D: every tile in the XCD-aware sweep, two pixels per lane
+    hipLaunchKernelGGL(k_raster2d_fwd_pair, dim3((unsigned)sweep_grid2d(CT)), dim3(128), 0, s, (const Splat*)rec,
+                       sorted_ids, tile_offset, width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end,
+                       (float*)chunk_state, chunk_base, CT, cut2d, stats, sets);
   } else {
     // 2D: every tile in the XCD-aware sweep (no separate empty-tile fill)
     const int64_t grid = IS2D ? (int64_t)sweep_grid2d(CT) : ((n_busy + 7) & ~7) + n_fill;
@@ -2507,6 +2736,26 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
   }
   GSR_LAUNCH_CHECK("k_raster_finalize");
   return GSR_OK;
+}
+
+// compute units of the current device (cached per process: one device type per box)
+static int device_cus() {
+  static int n = 0;
+  if (n <= 0) {
+    int d = 0, v = 0;
+    if (hipGetDevice(&d) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && v > 0)
+      n = v;
+    else
+      n = 256;
+  }
+  return n;
+}
+
+// 3D chunk backward layout (gsr_set_bwd_layout): 1 = k_raster_bwd (4 waves, one pixel per
+// lane), 2 = k_raster_bwd_pair3d, 0 = automatic by the call's tile count (above)
+static bool bwd3d_pair(int64_t tiles) {
+  if (g_bwd_layout != 0) return g_bwd_layout == 2;
+  return tiles >= (int64_t)kBwdPairTilesPerCU * device_cus();
 }
 
 template <bool LOSS, bool IS2D>
@@ -2538,7 +2787,7 @@ static int raster_bwd(const char* who, const float* rec, const int32_t* sorted_i
       hipLaunchKernelGGL(k_raster2d_bwd_tile, dim3((unsigned)sweep_grid2d(CT)), dim3(kRasterThreads), 0,
                          (hipStream_t)stream, (const Splat*)rec, sorted_ids, chunk_state, width, height, tw, th, bg,
                          final_T, last, v_rgb, v_alpha, partial, chunk_list, stats, k_of_s, cut2d, sets);
-  } else if (!LOSS && GSR_BWD3D_PAIR && chunk_entries <= kChunk3) {
+  } else if (!LOSS && chunk_entries <= kChunk3 && bwd3d_pair((int64_t)C * tw * th)) {
     hipLaunchKernelGGL(k_raster_bwd_pair3d, dim3(n_chunks), dim3(128), 0, (hipStream_t)stream, (const Splat*)rec,
                        sorted_ids, (const float4*)chunk_state, width, height, tw, th, bg, final_T, last, v_rgb,
                        v_alpha, partial, chunk_list, stats, k_of_s);

@@ -26,7 +26,7 @@ ORDER_INDEX = 1
 INPUT_ADAPTER = 0
 INPUT_GSPLAT = 1
 
-ABI_VERSION = 8   # include/gsr.h GSR_ABI_VERSION this binding is written for
+ABI_VERSION = 9   # include/gsr.h GSR_ABI_VERSION this binding is written for
 
 # stats->overflow bits of a capacity-bounded call (include/gsr.h GSR_OVF_*)
 OVF_BITS = {1: "intersections > isect cap", 2: "chunks > chunk cap", 4: "busy tiles > n_busy bound",
@@ -85,6 +85,7 @@ EXPORTS = {
     "gsr_selftest_reduce64": (ctypes.c_int, [_P, _P]),
     "gsr_selftest_reduce_box16": (ctypes.c_int, [_P, _P]),
     "gsr_set_fwd_lanes": (ctypes.c_int, [_I32]),
+    "gsr_set_bwd_layout": (ctypes.c_int, [_I32]),
     "gsr_selftest_lds_order": (ctypes.c_int, [_P, _P]),
     "gsr3d_project_fwd": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _I32, _I32, _I32, _F, _F, _F, _F,
                                          _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _I32, _P]),

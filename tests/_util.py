@@ -99,3 +99,21 @@ class forced_fwd_lanes:
         from gsr import _lib
         _lib.check(_lib.lib().gsr_set_fwd_lanes(0), "gsr_set_fwd_lanes")
         return False
+
+
+class forced_bwd_layout:
+    """Force the 3D raster backward's layout (gsr_set_bwd_layout: 1 one pixel per lane, 2 two)
+    inside a with-block; automatic afterwards."""
+
+    def __init__(self, layout: int):
+        self.layout = layout
+
+    def __enter__(self):
+        from gsr import _lib
+        _lib.check(_lib.lib().gsr_set_bwd_layout(self.layout), "gsr_set_bwd_layout")
+        return self
+
+    def __exit__(self, *exc):
+        from gsr import _lib
+        _lib.check(_lib.lib().gsr_set_bwd_layout(0), "gsr_set_bwd_layout")
+        return False

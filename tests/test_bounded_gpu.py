@@ -17,7 +17,7 @@ import math
 import pytest
 import torch
 
-from _util import forced_fwd_lanes
+from _util import forced_bwd_layout, forced_fwd_lanes
 
 pytestmark = pytest.mark.gpu
 
@@ -69,6 +69,21 @@ def test_bounded_equals_exact_3d(cuda, lanes):
     with forced_fwd_lanes(lanes):
         ex = _step3d(*sc, capacity="exact")
         for _ in range(2):   # the first bounded call uses the exact call's bounds, the second its own
+            _poison(cuda)
+            bd = _step3d(*sc, capacity="bounded")
+            torch.cuda.synchronize()
+            assert _same(ex, bd)
+    R.check_overflow(cuda)
+
+
+def test_bounded_equals_exact_3d_pair_backward(cuda):
+    """The two-pixels-per-lane backward (k_raster_bwd_pair3d) over a bounded grid: workgroups
+    past the device's active-chunk count leave before reading anything (poisoned arenas)."""
+    from gsr import render as R
+    sc = _scene3d(cuda)
+    with forced_bwd_layout(2):
+        ex = _step3d(*sc, capacity="exact")
+        for _ in range(2):
             _poison(cuda)
             bd = _step3d(*sc, capacity="bounded")
             torch.cuda.synchronize()

@@ -70,6 +70,17 @@ def fwd_lanes(request, cuda):
     _lib.check(_lib.lib().gsr_set_fwd_lanes(0), "gsr_set_fwd_lanes")
 
 
+@pytest.fixture(params=[1, 2], ids=["bwd1", "bwd2"])
+def bwd_layout(request, cuda):
+    """Run a 3D test under each raster-backward layout (1: one pixel per lane, 4-wave chunk
+    workgroups; 2: two pixels per lane, 2-wave workgroups), forced through gsr_set_bwd_layout
+    (the automatic choice takes 2 only for calls with >= 64 tiles per CU); automatic afterwards."""
+    from gsr import _lib
+    _lib.check(_lib.lib().gsr_set_bwd_layout(request.param), "gsr_set_bwd_layout")
+    yield request.param
+    _lib.check(_lib.lib().gsr_set_bwd_layout(0), "gsr_set_bwd_layout")
+
+
 def _oracle3d():
     from oracle import oracle3d
     return oracle3d
@@ -120,7 +131,7 @@ def _cot(C, H, W, seed):
     (200, 48, 40, 2, 3, 1.0),
     (2000, 96, 80, 3, 4, 0.0),
 ])
-def test_3d_small_vs_oracle(cuda, fwd_lanes, N, W, H, C, seed, shift):
+def test_3d_small_vs_oracle(cuda, fwd_lanes, bwd_layout, N, W, H, C, seed, shift):
     p, V, K = _scene3d(N, W, H, C, seed, extent=0.05, scale_shift=shift)
     bg = torch.tensor([0.1, 0.5, 0.9])
     vr, va = _cot(C, H, W, seed + 100)
@@ -141,7 +152,7 @@ def test_3d_multiview_equals_single_views(cuda):
         assert torch.equal(rgb_b[c], rgb_c[0]) and torch.equal(a_b[c], a_c[0])
 
 
-def test_3d_deterministic(cuda, fwd_lanes):
+def test_3d_deterministic(cuda, fwd_lanes, bwd_layout):
     W, H, C = 96, 80, 2
     p, V, K = _scene3d(20000, W, H, C, 8)
     bg = torch.ones(3)
@@ -266,7 +277,7 @@ def test_3d_isotropic_radius_mode(cuda):
     grad_close(g_g, g_o, what="grad")
 
 
-def test_3d_edge_cases(cuda, fwd_lanes):
+def test_3d_edge_cases(cuda, fwd_lanes, bwd_layout):
     W, H = 48, 40
     p, V, K = _scene3d(64, W, H, 1, 31, extent=0.05, scale_shift=1.5)
     bg = torch.tensor([0.2, 0.3, 0.4])
@@ -311,7 +322,7 @@ def test_3d_speculative_arena_regrow(cuda):
     assert torch.equal(rgb1, rgb3) and torch.equal(a1, a3) and torch.equal(g1, g3)
 
 
-def test_3d_long_tile_lists(cuda, fwd_lanes):
+def test_3d_long_tile_lists(cuda, fwd_lanes, bwd_layout):
     """> 16384 entries in one tile list: exercises the run-sort + global merge path."""
     W, H = 32, 32
     N = 40000
