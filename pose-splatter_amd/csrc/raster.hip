@@ -546,7 +546,9 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
       if (hb >= end || __ballot(!done) == 0ull) break;
       if (hb > start && ((hb - start) & umask) == 0) {   // entering chunk kcur+1
         const float Dr = PG::sum(dr), Dg = PG::sum(dg), Db = PG::sum(db);
+#ifndef GSR_EXP_NOCKPT   // (timing experiment: no chunk-record stores inside the walk; results wrong)
         if (q == 0 && ckpt) ckpt[(int64_t)(cbase + kcur) * kRasterThreads + bwd_pixel_slot(il, jl)] = make_float4(Ts, Dr, Dg, Db);
+#endif
         cr += Dr;
         cg += Dg;
         cb += Db;

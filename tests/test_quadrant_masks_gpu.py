@@ -91,7 +91,9 @@ def test_masks_match_the_cull(cuda):
     restatement keeps with a margin must have its bit set, one it culls with a margin must not
     (decisions within 1e-4 of the threshold may differ by fp32 contraction)."""
     p, V, K, W, H, vr, va = _scene(cuda)
-    _, _, _, b = _step(p, V, K, W, H, vr, va)
+    with _masks(True):   # (off by default since round 4)
+        _, _, _, b = _step(p, V, K, W, H, vr, va)
+    assert b.masks
     I = b.n_isect
     off = b.tile_off.long()
     CT = off.numel() - 1

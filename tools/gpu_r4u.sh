@@ -29,3 +29,11 @@ for cfg in 3 5; do
     show gpurun_out/r4u_c${cfg}_$v.json "c$cfg layout$v"
   done
 done
+# timing experiment: the 3D quad forward without its chunk-record stores (build_var nockpt; results wrong)
+for v in new nockpt new nockpt; do
+  case $v in
+    new) timeout -k 10 300 python bench.py --config 3 --cpu-baseline 0 --psnr 0 > gpurun_out/r4u_c3x_$v.json 2>/dev/null || exit 1 ;;
+    *) GSR_LIBRARY=$PWD/build_var/libgsr_$v.so timeout -k 10 300 python bench.py --config 3 --cpu-baseline 0 --psnr 0 > gpurun_out/r4u_c3x_$v.json 2>/dev/null || exit 1 ;;
+  esac
+  show gpurun_out/r4u_c3x_$v.json "c3 $v"
+done
