@@ -179,13 +179,15 @@ __device__ void nan_fill(int64_t CT, int W, int H, int tw, int th, float* __rest
   for (int64_t t = blockIdx.x; t < CT; t += gridDim.x) {
     int c, ty, tx;
     tile_coords((int)t, tw, th, c, ty, tx);
-    const int i = ty * kTile + (threadIdx.x >> 4), j = tx * kTile + (threadIdx.x & 15);
-    if (i < H && j < W) {
-      const int64_t pix = ((int64_t)c * H + i) * W + j;
-      out_rgb[pix * 3 + 0] = nan;
-      out_rgb[pix * 3 + 1] = nan;
-      out_rgb[pix * 3 + 2] = nan;
-      out_alpha[pix] = nan;
+    for (int p = threadIdx.x; p < kTile * kTile; p += blockDim.x) {   // (128- and 256-thread kernels)
+      const int i = ty * kTile + (p >> 4), j = tx * kTile + (p & 15);
+      if (i < H && j < W) {
+        const int64_t pix = ((int64_t)c * H + i) * W + j;
+        out_rgb[pix * 3 + 0] = nan;
+        out_rgb[pix * 3 + 1] = nan;
+        out_rgb[pix * 3 + 2] = nan;
+        out_alpha[pix] = nan;
+      }
     }
   }
 }
@@ -2277,7 +2279,12 @@ __global__ __launch_bounds__(128, GSR_BWD2P_MINB) void k_raster2d_bwd_pair(
                          float& mu) {
           const float sigma = conic_sigma(p1, dx, dy);
           const float alpha = p0.z * __expf(-sigma);
+          // (& not &&: with a short-circuit the compiler wrapped each pixel's exp in a branch)
+#ifdef GSR_EXP_SHORTCIRCUIT   // (timing experiment: the previous form)
           const bool valid = ks <= last && alpha >= cut2d;
+#else
+          const bool valid = (ks <= last) & (alpha >= cut2d);
+#endif
           const float alpha_v = valid ? alpha : 0.f;
           const float ra = __builtin_amdgcn_rcpf(1.f - alpha_v);
           T = k == lastq ? Tl : T * ra;

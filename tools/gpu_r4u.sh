@@ -1,7 +1,8 @@
 #!/bin/bash
 # round 4: the 2D pixel-pair forward (k_raster2d_fwd_pair) and the 3D backward layout knob
 # (ABI 9) -- the whole GPU suite (box forward), the 2D suites with the pair forward (build_var
-# f2p), then config 4 box vs pair forward, configs 3
+# f2p), then config 4: shipped / previous 2D pair-backward validity form (sc) / pair forward
+# (f2p), configs 3
 # and 5 with the 3D backward layout automatic / forced
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -16,7 +17,7 @@ GSR_LIBRARY=$PWD/build_var/libgsr_f2p.so timeout -k 10 500 python -u -m pytest -
   || { grep -E "FAIL|Error|error" gpurun_out/r4u_tests_f2p.txt | head -20; tail -30 gpurun_out/r4u_tests_f2p.txt; exit 1; }
 tail -1 gpurun_out/r4u_tests_f2p.txt
 show() { python -c "import json,sys; d=json.loads(open('$1').read().strip().splitlines()[-1]); k=d['kernels_ms']; print('$2', round(d['ms_per_step'],4), {x: k[x] for x in k if 'raster' in x})"; }
-for v in new f2p new f2p; do
+for v in new sc f2p new sc f2p; do
   case $v in
     new) timeout -k 10 300 python bench.py --config 4 --cpu-baseline 0 --psnr 0 --steps 5 --warmup 2 > gpurun_out/r4u_c4_$v.json 2>/dev/null || exit 1 ;;
     *) GSR_LIBRARY=$PWD/build_var/libgsr_$v.so timeout -k 10 300 python bench.py --config 4 --cpu-baseline 0 --psnr 0 --steps 5 --warmup 2 > gpurun_out/r4u_c4_$v.json 2>/dev/null || exit 1 ;;
