@@ -174,7 +174,7 @@ def step_bytes(C: int, N: int, P: int, I: int, I_eff: int, p: int, backward: boo
 
 # libgsr call name (render.py timing brackets) -> substring of its dominant kernel's symbol
 KERNEL_SYMBOL = {"raster3d_bwd": "k_raster_bwd", "raster3d_fwd": "k_raster_fwd<false,",
-                 "raster2d_bwd": "k_raster2d_bwd_pair", "raster2d_fwd": "k_raster_fwd_box<true>",
+                 "raster2d_bwd": "k_raster2d_bwd_pair", "raster2d_fwd": "k_raster2d_fwd_pair",
                  "bin_sort": "k_segsort", "project3d_fwd": "k_project3d_fwd", "project3d_bwd": "k_project3d_bwd",
                  "project2d_fwd": "k_project2d_fwd", "project2d_bwd": "k_project2d_bwd", "bin_emit": "k_emit"}
 

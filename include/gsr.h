@@ -171,7 +171,7 @@ int gsr_selftest_reduce_box16(float* out, void* stream);
 
 /* Layout of the raster forward (process-wide): 0 = automatic (3D: 16 lanes per pixel and 16
  * workgroups per tile with at most 160 busy tiles, else 4 lanes per pixel and 4 workgroups per
- * tile; 2D: 1 lane per pixel, one workgroup per tile), or 1, 4 or 16 (3D only) to force one.
+ * tile; 2D: one 2-wave workgroup per tile, two pixels per lane), or 1, 4 or 16 (3D only) to force one.
  * All give the same result up to fp32 regrouping of the transmittance products. */
 int gsr_set_fwd_lanes(int lanes);
 

@@ -548,9 +548,7 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
       if (hb >= end || __ballot(!done) == 0ull) break;
       if (hb > start && ((hb - start) & umask) == 0) {   // entering chunk kcur+1
         const float Dr = PG::sum(dr), Dg = PG::sum(dg), Db = PG::sum(db);
-#ifndef GSR_EXP_NOCKPT   // (timing experiment: no chunk-record stores inside the walk; results wrong)
         if (q == 0 && ckpt) ckpt[(int64_t)(cbase + kcur) * kRasterThreads + bwd_pixel_slot(il, jl)] = make_float4(Ts, Dr, Dg, Db);
-#endif
         cr += Dr;
         cg += Dg;
         cb += Db;
@@ -1151,7 +1149,7 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
 // operation for operation (dx = x - px, dy = y - py, conic_sigma, alpha >= cut2d, T <- T (1 - a),
 // stop after T <= 2^-25), so k_raster2d_bwd_pair's validity tests agree with it exactly.
 #ifndef GSR_FWD2D_PAIR
-#define GSR_FWD2D_PAIR 0
+#define GSR_FWD2D_PAIR 1
 #endif
 #ifndef GSR_FWD2P_MINB
 #define GSR_FWD2P_MINB 5   // waves per SIMD the compiler aims at
@@ -2280,11 +2278,7 @@ __global__ __launch_bounds__(128, GSR_BWD2P_MINB) void k_raster2d_bwd_pair(
           const float sigma = conic_sigma(p1, dx, dy);
           const float alpha = p0.z * __expf(-sigma);
           // (& not &&: with a short-circuit the compiler wrapped each pixel's exp in a branch)
-#ifdef GSR_EXP_SHORTCIRCUIT   // (timing experiment: the previous form)
-          const bool valid = ks <= last && alpha >= cut2d;
-#else
           const bool valid = (ks <= last) & (alpha >= cut2d);
-#endif
           const float alpha_v = valid ? alpha : 0.f;
           const float ra = __builtin_amdgcn_rcpf(1.f - alpha_v);
           T = k == lastq ? Tl : T * ra;
