@@ -54,7 +54,7 @@
  * Per-entry gradient partials (written by *_raster_bwd, reduced by *_project_bwd):
  *   one row of GSR_PARTIAL_STRIDE floats per intersection, in EMISSION order (row
  *   k = isect_offset[c*N+n] + j, j = row-major index of the tile in the Gaussian's rect):
- *   d/dx, d/dy, d/da, d/db, d/dc, d/dopacity, d/drgb[3], 0, 0, 0 (summed over the 16x16
+ *   d/dx, d/dy, d/da, d/db, d/dc, d/dopacity, d/drgb[3] (36 B, summed over the 16x16
  *   tile's pixels) — a deterministic replacement for float atomics.  Only entries before
  *   their tile's cut (see tile_cut) are written; the others are never read.
  */
@@ -86,7 +86,7 @@ extern "C" {
                                           ("chunk", gsr_bin_caps.chunk_entries) is a power-of-two
                                           multiple of it (default GSR_CHUNK) */
 #endif
-#define GSR_PARTIAL_STRIDE 12          /* floats per partial row (9 used, 16 B aligned) */
+#define GSR_PARTIAL_STRIDE 9           /* floats per partial row (36 B, 4 B aligned; 12 before ABI 10) */
 
 /* stats->overflow bits (capacity-bounded calls; 0 = every bound held) */
 #define GSR_OVF_ISECT 1      /* I > caps->isect: intersection buffers too small              */
@@ -157,7 +157,9 @@ int gsr_version(void);
 /* Revision 8: 2D records are stored packed (layout above): the 2D walks read them as 2 x b128 +
  * b32 from LDS as staged (or gathered straight into LDS). */
 /* Revision 9: gsr_set_bwd_layout (the 3D raster backward's layout, process-wide). */
-#define GSR_ABI_VERSION 9
+/* Revision 10: partial rows are 9 floats (GSR_PARTIAL_STRIDE 9, was 12: the 3 padding floats cost
+ * 25 % of the rows' HBM writes and reads). */
+#define GSR_ABI_VERSION 10
 int gsr_abi_version(void);
 const char* gsr_last_error(void);
 

@@ -16,7 +16,7 @@ constexpr float kAlphaMax = 0.999f;              // gsplat alpha clamp
 constexpr float kTMin = 1e-4f;                   // gsplat transmittance stop
 constexpr float kExtendMax = 3.33f;              // gsplat >=1.5 max sigma extent
 constexpr int kPartial = 9;                      // per-entry gradient partial width
-constexpr int kPartialStride = GSR_PARTIAL_STRIDE;   // floats per partial row (3 x float4)
+constexpr int kPartialStride = GSR_PARTIAL_STRIDE;   // floats per partial row (the 9 partials, 36 B)
 
 // Splat record: 3 x float4 (48 B) per (camera, Gaussian).  See include/gsr.h.
 struct __align__(16) Splat {

@@ -29,7 +29,7 @@ __device__ __forceinline__ void gather_partials(const uint2 r, int tw, int64_t c
                                                 const float* __restrict__ partial, float (&acc)[kPartial]) {
   const int x0 = r.x & 0xffff, x1 = r.x >> 16, y0 = r.y & 0xffff, y1 = r.y >> 16;
   const int cnt = (x1 - x0) * (y1 - y0);
-  const float4* rows = reinterpret_cast<const float4*>(partial + (int64_t)off * kPartialStride);
+  const float* rows = partial + (int64_t)off * kPartialStride;
   // four tiles per round: their cut keys first, then the rows that exist (two dependent
   // memory round trips per four tiles instead of two per tile)
   int tx = x0, ty = y0;   // tile of entry j0 (row-major over the rect)
@@ -46,12 +46,9 @@ __device__ __forceinline__ void gather_partials(const uint2 r, int tw, int64_t c
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (has[u]) {
-        const float4* row = rows + 3 * (j0 + u);
-        const float4 a = row[0], b = row[1];
-        const float c = row[2].x;
-        acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
-        acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
-        acc[8] += c;
+        const float* row = rows + kPartialStride * (j0 + u);
+#pragma unroll
+        for (int q = 0; q < kPartial; ++q) acc[q] += row[q];
       }
     }
   }
@@ -417,14 +414,14 @@ __device__ __forceinline__ void chain2d(const float* __restrict__ prm, const flo
 // Gaussian gathers of the 48-B rows at scattered addresses took 2.10 ms at config 4, the
 // staged reads 1.54 ms.  Correct for any layout: [lo, hi) is the hull of the workgroup's
 // rows, whatever else lies inside it.
-constexpr int kStageRows = 512;   // rows per LDS round (24 KB)
+constexpr int kStageRows = 512;   // rows per LDS round (18 KB)
 __global__ __launch_bounds__(kBwdThreads) void k_project2d_bwd_staged(
     const float* __restrict__ params, int64_t N, int64_t stride, int64_t set_stride,
     const int32_t* __restrict__ set_begin, int F, int n_cam, int tw, int th, const uint2* __restrict__ rect,
     const int32_t* __restrict__ isect_offset, const int32_t* __restrict__ isect_count,
     const uint64_t* __restrict__ tile_cut, const float* __restrict__ partial, const gsr_bin_stats* __restrict__ stats,
     float* __restrict__ v_params) {
-  __shared__ float4 s_rows[3 * kStageRows];
+  __shared__ float s_rows[kPartialStride * kStageRows];
   __shared__ int s_lo, s_hi;
   const int f = blockIdx.y;
   const int64_t n = (int64_t)blockIdx.x * kBwdThreads + threadIdx.x;
@@ -433,8 +430,7 @@ __global__ __launch_bounds__(kBwdThreads) void k_project2d_bwd_staged(
   // gathers, tested in the camera loop: no round trip of its own)
   const bool ovf = stats != nullptr && stats->overflow != 0;
   const int c0 = set_begin ? set_begin[f] : 0, c1 = set_begin ? set_begin[f + 1] : n_cam;
-  const float4* rows4 = reinterpret_cast<const float4*>(partial);
-  static_assert(kPartialStride == 12, "a partial row is 3 float4");
+  static_assert(kPartialStride * kStageRows % kBwdThreads == 0, "whole rounds of floats per thread");
   float acc[kPartial];
 #pragma unroll
   for (int v = 0; v < kPartial; ++v) acc[v] = 0.f;
@@ -468,14 +464,16 @@ __global__ __launch_bounds__(kBwdThreads) void k_project2d_bwd_staged(
       const int nr = min(kStageRows, hi - r0);
       __syncthreads();   // the previous round's rows are consumed
       {
-        float4 v[3 * kStageRows / kBwdThreads];
+        constexpr int kPer = kPartialStride * kStageRows / kBwdThreads;   // floats per thread (coalesced)
+        float v[kPer];
+        const float* src = partial + (int64_t)kPartialStride * r0;
 #pragma unroll
-        for (int u = 0; u < 3 * kStageRows / kBwdThreads; ++u) {
+        for (int u = 0; u < kPer; ++u) {
           const int i = u * kBwdThreads + threadIdx.x;
-          v[u] = i < 3 * nr ? rows4[3 * (int64_t)r0 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+          v[u] = i < kPartialStride * nr ? src[i] : 0.f;
         }
 #pragma unroll
-        for (int u = 0; u < 3 * kStageRows / kBwdThreads; ++u) s_rows[u * kBwdThreads + threadIdx.x] = v[u];
+        for (int u = 0; u < kPer; ++u) s_rows[u * kBwdThreads + threadIdx.x] = v[u];
       }
       __syncthreads();
       if (cnt > 0) {
@@ -484,12 +482,9 @@ __global__ __launch_bounds__(kBwdThreads) void k_project2d_bwd_staged(
         int ty = y0 + ja / w, tx = x0 + ja % w;
         for (int j = ja; j < jb; ++j) {
           if (key < tile_cut[ct_base + ty * tw + tx]) {
-            const int sr = 3 * (off + j - r0);
-            const float4 a = s_rows[sr], b = s_rows[sr + 1];
-            const float cz = s_rows[sr + 2].x;
-            acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
-            acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
-            acc[8] += cz;
+            const float* sr = s_rows + kPartialStride * (off + j - r0);
+#pragma unroll
+            for (int q = 0; q < kPartial; ++q) acc[q] += sr[q];
           }
           if (++tx == x1) {
             tx = x0;

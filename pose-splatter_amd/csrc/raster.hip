@@ -1409,13 +1409,13 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_finalize(
   }
 }
 
-// Partial rows are stored in EMISSION order (row k_of_s[s] for sorted entry s), 12 floats
-// (3 x float4) per row, so *_project_bwd reads each Gaussian's rows contiguously.
+// Partial rows are stored in EMISSION order (row k_of_s[s] for sorted entry s), 9 floats
+// (36 B, no padding) per row, so *_project_bwd reads each Gaussian's rows contiguously.
+static_assert(kPartialStride == kPartial, "a partial row is its 9 partials");
 __device__ __forceinline__ void store_partial_row(float* __restrict__ partial, int k, const float (&v)[kPartial]) {
-  float4* dst = reinterpret_cast<float4*>(partial + (int64_t)k * kPartialStride);
-  dst[0] = make_float4(v[0], v[1], v[2], v[3]);
-  dst[1] = make_float4(v[4], v[5], v[6], v[7]);
-  dst[2] = make_float4(v[8], 0.f, 0.f, 0.f);
+  float* dst = partial + (int64_t)k * kPartialStride;
+#pragma unroll
+  for (int q = 0; q < kPartial; ++q) dst[q] = v[q];
 }
 
 // Cotangent of  g_iou * iou_loss + g_img * img_loss  (+ extra cotangents) at one pixel
