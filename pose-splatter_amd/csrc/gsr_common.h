@@ -286,6 +286,21 @@ __device__ __forceinline__ float conic_sigma(const float4 p1, float dx, float dy
   return p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
 }
 
+// exp(-sigma) of a record's conic.  2D records store the conic and L scaled by log2(e)
+// (k_project2d_fwd, ABI 11): sigma' = sigma log2(e), so exp(-sigma) = 2^(-sigma') is ONE
+// v_exp_f32 (__expf is a multiply by -log2(e) and the same v_exp_f32).  The gradients that
+// sum v_sig * dx^2 ... stay derivatives by the unscaled conic (v_sig is dL/dsigma either way);
+// only the mean's chain through the conic needs the unscaled a, b, c (kLn2 * stored).
+constexpr float kLog2e = 1.44269504088896341f;
+constexpr float kLn2 = 0.693147180559945309f;
+template <bool IS2D>
+__device__ __forceinline__ float gauss_exp(float sigma) {
+  if constexpr (IS2D)
+    return __builtin_amdgcn_exp2f(-sigma);
+  else
+    return __expf(-sigma);
+}
+
 template <bool IS2D>
 __device__ __forceinline__ bool cull_keep(const float4 p0, const float4 p1, const float4 p2, float bx0, float bx1,
                                           float by0, float by1) {

@@ -256,9 +256,11 @@ __global__ __launch_bounds__(kProjThreads) void k_project2d_fwd(
       // (the level set this extent bounds) and the edge slopes -b/2c, -b/2a
       // stored packed (raster.hip pack_rec: the 2D walks read x, y, o, conic and colour as
       // 2 x b128 + b32 straight from the staged copy)
+      // conic and L times log2(e) (ABI 11): the raster's alpha is o 2^(-sigma'), one v_exp_f32
+      // (gsr_common.h gauss_exp); the edge slopes are ratios, unscaled
       s.p0 = make_float4(g.u, g.v, g.op, g.col[0]);
-      s.p1 = make_float4(g.a, g.b, g.c, g.col[1]);
-      s.p2 = make_float4(g.col[2], logf(g.op / eps_cut), -g.b / (2.f * g.c), -g.b / (2.f * g.a));
+      s.p1 = make_float4(g.a * kLog2e, g.b * kLog2e, g.c * kLog2e, g.col[1]);
+      s.p2 = make_float4(g.col[2], logf(g.op / eps_cut) * kLog2e, -g.b / (2.f * g.c), -g.b / (2.f * g.a));
       // one record per parameter set: its cameras render identical lists (the camera is ignored,
       // src/gaussian_renderer.py:280-281), so they all read the set's first camera's copy
       // (raster.hip rec_offset2d) -- one copy to write, and shared by the views in the XCDs' L2

@@ -586,7 +586,7 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
         const float4 p2 = s_q[buf][2][idx];
         const float dx = p0.x - px, dy = p0.y - py;
         const float sg = conic_sigma(p1, dx, dy);
-        const float raw = p0.z * __expf(-sg);
+        const float raw = p0.z * gauss_exp<IS2D>(sg);
         const float alpha = IS2D ? raw : fminf(kAlphaMax, raw);
         const bool valid = IS2D ? (k < n && !done && alpha >= cut2d)
                                 : (k < n && !done && sg >= 0.f && alpha >= kAlphaThreshold);
@@ -675,7 +675,7 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
       const float4 p2 = s_pw[wv][2][kk];
       const float dx = p0.x - px, dy = p0.y - py;
       const float sg = conic_sigma(p1, dx, dy);
-      const float raw = p0.z * __expf(-sg);
+      const float raw = p0.z * gauss_exp<IS2D>(sg);
       const float alpha = IS2D ? raw : fminf(kAlphaMax, raw);
       const bool valid = IS2D ? (k < n && !done && alpha >= cut2d)
                               : (k < n && !done && sg >= 0.f && alpha >= kAlphaThreshold);
@@ -1024,7 +1024,7 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
             }
             const float dx = p0.x - px, dy = p0.y - py;
             const float sg = conic_sigma(p1, dx, dy);
-            const float alpha = p0.z * __expf(-sg);
+            const float alpha = p0.z * gauss_exp<true>(sg);
             // (steps past the box's list read the zero record: alpha 0 < cut2d, never valid)
             const bool valid = !done && alpha >= cut2d;
             // an invalid step enters with alpha 0: vis = 0 and T * (1 - 0) = T exactly (one
@@ -1057,7 +1057,7 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
           const float4 p2 = rk[2 * kRS];
           const float dx = p0.x - px, dy = p0.y - py;
           const float sg = conic_sigma(p1, dx, dy);
-          const float raw = p0.z * __expf(-sg);
+          const float raw = p0.z * gauss_exp<IS2D>(sg);
           const float alpha = IS2D ? raw : fminf(kAlphaMax, raw);
           const bool valid = IS2D ? alpha >= cut2d : (sg >= 0.f && alpha >= kAlphaThreshold);
           if (valid) {
@@ -1300,7 +1300,7 @@ __global__ __launch_bounds__(128, GSR_FWD2P_MINB) void k_raster2d_fwd_pair(
         const float dx = p0.x - px;
         {
           const float dy = p0.y - pyA;
-          const float alpha = p0.z * __expf(-conic_sigma(p1, dx, dy));
+          const float alpha = p0.z * gauss_exp<true>(conic_sigma(p1, dx, dy));
           const bool valid = !doneA && alpha >= cut2d;
           const float av = valid ? alpha : 0.f;
           const float vis = av * TA;
@@ -1308,13 +1308,13 @@ __global__ __launch_bounds__(128, GSR_FWD2P_MINB) void k_raster2d_fwd_pair(
           dgA += p1.w * vis;
           dbA += cbl * vis;
           TlA = valid ? TA : TlA;
-          TA = TA * (1.f - av);
+          TA = fmaf(-TA, av, TA);   // T (1 - a) in one rounding
           lkA = valid ? k : lkA;
           doneA = doneA || TA <= kT2DMin;
         }
         {
           const float dy = p0.y - pyB;
-          const float alpha = p0.z * __expf(-conic_sigma(p1, dx, dy));
+          const float alpha = p0.z * gauss_exp<true>(conic_sigma(p1, dx, dy));
           const bool valid = !doneB && alpha >= cut2d;
           const float av = valid ? alpha : 0.f;
           const float vis = av * TB;
@@ -1322,7 +1322,7 @@ __global__ __launch_bounds__(128, GSR_FWD2P_MINB) void k_raster2d_fwd_pair(
           dgB += p1.w * vis;
           dbB += cbl * vis;
           TlB = valid ? TB : TlB;
-          TB = TB * (1.f - av);
+          TB = fmaf(-TB, av, TB);
           lkB = valid ? k : lkB;
           doneB = doneB || TB <= kT2DMin;
         }
@@ -1725,7 +1725,7 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
         }
         const float dx = p0.x - px, dy = p0.y - py;
         const float sigma = conic_sigma(p1, dx, dy);
-        const float vis = __expf(-sigma);
+        const float vis = gauss_exp<IS2D>(sigma);
         const float raw = p0.z * vis;
         const float alpha = IS2D ? raw : fminf(kAlphaMax, raw);
         // an invalid pair enters with alpha 0: ra = rcp(1) = 1, fac = 0 and (2D) v_sig = -0,
@@ -1799,8 +1799,10 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
       for (int q = 0; q < kPartial; ++q) v[q] = (L[q][0][k] + L[q][1][k]) + (L[q][2][k] + L[q][3][k]);
       const float4 p1 = s_p[1][k];
       const float mx = v[0], my = v[1];
-      v[0] = 2.f * p1.x * mx + p1.y * my;
-      v[1] = p1.y * mx + 2.f * p1.z * my;
+      // (2D records hold the conic times log2(e): the mean's chain takes the unscaled one)
+      const float cs = IS2D ? kLn2 : 1.f;
+      v[0] = (2.f * p1.x * mx + p1.y * my) * cs;
+      v[1] = (p1.y * mx + 2.f * p1.z * my) * cs;
       v[5] = -v[5] / s_p[0][k].z;
       store_partial_row(partial, kos_mine & kEmitIndexMask, v);   // (bits 28..31: the 3D quadrant mask)
     }
@@ -2010,7 +2012,7 @@ __global__ __launch_bounds__(kRasterThreads, GSR_BWD2D_MINB) void k_raster2d_bwd
         const float cbl = reinterpret_cast<const float*>(&sp[2][k])[0];   // blue
         const float dx = p0.x - px, dy = p0.y - py;
         const float sigma = conic_sigma(p1, dx, dy);
-        const float alpha = p0.z * __expf(-sigma);
+        const float alpha = p0.z * gauss_exp<true>(sigma);
         const bool valid = k <= lastk && alpha >= cut2d;
         const float alpha_v = valid ? alpha : 0.f;
         const float ra = __builtin_amdgcn_rcpf(1.f - alpha_v);
@@ -2072,8 +2074,9 @@ __global__ __launch_bounds__(kRasterThreads, GSR_BWD2D_MINB) void k_raster2d_bwd
       for (int q = 0; q < kPartial; ++q) v[q] = (L[q][0][k] + L[q][1][k]) + (L[q][2][k] + L[q][3][k]);
       const float4 p1 = sp[1][k];
       const float mx = v[0], my = v[1];
-      v[0] = 2.f * p1.x * mx + p1.y * my;
-      v[1] = p1.y * mx + 2.f * p1.z * my;
+      // (2D records hold the conic times log2(e): the mean's chain takes the unscaled one)
+      v[0] = (2.f * p1.x * mx + p1.y * my) * kLn2;
+      v[1] = (p1.y * mx + 2.f * p1.z * my) * kLn2;
       v[5] = -v[5] / sp[0][k].z;
       store_partial_row(partial, kos_mine & kEmitIndexMask, v);
     }
@@ -2276,7 +2279,7 @@ __global__ __launch_bounds__(128, GSR_BWD2P_MINB) void k_raster2d_bwd_pair(
         auto pixel = [&](float dy, int last, int lastq, float Tl, float vr, float vg, float vb, float& T,
                          float& mu) {
           const float sigma = conic_sigma(p1, dx, dy);
-          const float alpha = p0.z * __expf(-sigma);
+          const float alpha = p0.z * gauss_exp<true>(sigma);
           // (& not &&: with a short-circuit the compiler wrapped each pixel's exp in a branch)
           const bool valid = (ks <= last) & (alpha >= cut2d);
           const float alpha_v = valid ? alpha : 0.f;
@@ -2351,8 +2354,9 @@ __global__ __launch_bounds__(128, GSR_BWD2P_MINB) void k_raster2d_bwd_pair(
       for (int q = 0; q < kPartial; ++q) v[q] = L[q][0][k] + L[q][1][k];
       const float4 p1 = s_p[1][k];
       const float mx = v[0], my = v[1];
-      v[0] = 2.f * p1.x * mx + p1.y * my;
-      v[1] = p1.y * mx + 2.f * p1.z * my;
+      // (2D records hold the conic times log2(e): the mean's chain takes the unscaled one)
+      v[0] = (2.f * p1.x * mx + p1.y * my) * kLn2;
+      v[1] = (p1.y * mx + 2.f * p1.z * my) * kLn2;
       v[5] = -v[5] / s_p[0][k].z;
       store_partial_row(partial, kos_mine & kEmitIndexMask, v);
     }
