@@ -1182,7 +1182,9 @@ __global__ __launch_bounds__(128, GSR_FWD2P_MINB) void k_raster2d_fwd_pair(
   const int jl = 4 * (box & 3) + (pp & 3), ilA = 8 * wv + 4 * (box >> 2) + (pp >> 2), ilB = ilA + 2;
   const int pj = tx * kTile + jl, piA = ty * kTile + ilA, piB = ty * kTile + ilB;
   const bool inA = piA < H && pj < W, inB = piB < H && pj < W;
-  const float px = (float)pj, pyA = (float)piA, pyB = (float)piB;   // integer centres
+  float px = (float)pj, pyA = (float)piA, pyB = (float)piB;   // integer centres
+  // (opaque to the compiler: it re-derived pyB from the int with a v_cvt in every walk step)
+  asm volatile("" : "+v"(px), "+v"(pyA), "+v"(pyB));
   const int slotA = bwd_pixel_slot(ilA, jl), slotB = bwd_pixel_slot(ilB, jl);
   const int hx0 = tx * kTile, hy0 = ty * kTile + 8 * wv;   // the wave's half-tile origin
   const int start = tile_offset[ct], end = tile_offset[ct + 1];
@@ -2275,9 +2277,12 @@ __global__ __launch_bounds__(128, GSR_BWD2P_MINB) void k_raster2d_bwd_pair(
         const float cbl = reinterpret_cast<const float*>(&s_p[2][k])[0];   // blue
         const float dx = p0.x - px, dyA = p0.y - pyA;
         const int ks = sb0 + k;   // the entry's list position (the zero pad slot is never valid: alpha 0)
-        float a6 = 0.f, a7 = 0.f, a8 = 0.f, a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, a4 = 0.f, a5 = 0.f;
-        auto pixel = [&](float dy, int last, int lastq, float Tl, float vr, float vg, float vb, float& T,
-                         float& mu) {
+        // the entry's 9 sums over the lane's two pixels: pixel A sets them, pixel B adds (a
+        // zero start cost 63 "0 + x" adds per group: IEEE keeps them, -0 + 0 = +0)
+        float a6, a7, a8, a0, a1, a2, a3, a4, a5;
+        auto pixel = [&](const bool first, float dy, int last, int lastq, float Tl, float vr, float vg, float vb,
+                         float& T, float& mu) {
+          auto add = [first](float& a, float x) { a = first ? x : a + x; };
           const float sigma = conic_sigma(p1, dx, dy);
           const float alpha = p0.z * gauss_exp<true>(sigma);
           // (& not &&: with a short-circuit the compiler wrapped each pixel's exp in a branch)
@@ -2286,23 +2291,23 @@ __global__ __launch_bounds__(128, GSR_BWD2P_MINB) void k_raster2d_bwd_pair(
           const float ra = __builtin_amdgcn_rcpf(1.f - alpha_v);
           T = k == lastq ? Tl : T * ra;
           const float fac = alpha_v * T;
-          a6 += fac * vr;
-          a7 += fac * vg;
-          a8 += fac * vb;
+          add(a6, fac * vr);
+          add(a7, fac * vg);
+          add(a8, fac * vb);
           const float cv = p0.w * vr + p1.w * vg + cbl * vb;
           const float dmu = cv - mu;
           const float v_sig = -alpha_v * (T * dmu);
           mu = mu + alpha_v * dmu;
           const float tx_ = v_sig * dx, ty_ = v_sig * dy;
-          a0 += tx_;
-          a1 += ty_;
-          a2 += tx_ * dx;
-          a3 += tx_ * dy;
-          a4 += ty_ * dy;
-          a5 += v_sig;
+          add(a0, tx_);
+          add(a1, ty_);
+          add(a2, tx_ * dx);
+          add(a3, tx_ * dy);
+          add(a4, ty_ * dy);
+          add(a5, v_sig);
         };
-        pixel(dyA, lastA, lastqA, TlA, vrA, vgA, vbA, TA, muA);
-        pixel(p0.y - pyB, lastB, lastqB, TlB, vrB, vgB, vbB, TB, muB);   // (dy as the forward forms it)
+        pixel(true, dyA, lastA, lastqA, TlA, vrA, vgA, vbA, TA, muA);
+        pixel(false, p0.y - pyB, lastB, lastqB, TlB, vrB, vgB, vbB, TB, muB);   // (dy as the forward forms it)
         acc[g * kPartial + 0] = a0;
         acc[g * kPartial + 1] = a1;
         acc[g * kPartial + 2] = a2;
@@ -2533,35 +2538,38 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
       const float4 p1 = s_p[1][k];
       const float4 p2 = s_p[2][k];
       const float dx = p0.x - px;
-      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, a4 = 0.f, a5 = 0.f, a6 = 0.f, a7 = 0.f, a8 = 0.f;
-      auto pixel = [&](float dy, int lastk, float vr, float vg, float vb, float vTa, float& T, float& Sv) {
+      // pixel A sets the entry's 9 sums, pixel B adds (no "0 + x" adds: k_raster2d_bwd_pair)
+      float a0, a1, a2, a3, a4, a5, a6, a7, a8;
+      auto pixel = [&](const bool first, float dy, int lastk, float vr, float vg, float vb, float vTa, float& T,
+                       float& Sv) {
+        auto add = [first](float& a, float x) { a = first ? x : a + x; };
         const float sigma = conic_sigma(p1, dx, dy);
         const float vis = __expf(-sigma);
         const float raw = p0.z * vis;
         const float alpha = fminf(kAlphaMax, raw);
-        const bool valid = k <= lastk && sigma >= 0.f && alpha >= kAlphaThreshold;
+        const bool valid = (k <= lastk) & (sigma >= 0.f) & (alpha >= kAlphaThreshold);
         const float alpha_v = valid ? alpha : 0.f;
         const float ra = __builtin_amdgcn_rcpf(1.f - alpha_v);
         T *= ra;
         const float fac = alpha_v * T;
-        a6 += fac * vr;
-        a7 += fac * vg;
-        a8 += fac * vb;
+        add(a6, fac * vr);
+        add(a7, fac * vg);
+        add(a8, fac * vb);
         const float cv = p2.x * vr + p2.y * vg + p2.z * vb;
         const float v_al = T * cv + ra * (vTa - Sv);
-        const bool unclamped = valid && raw <= kAlphaMax;
+        const bool unclamped = valid & (raw <= kAlphaMax);
         const float v_sig = unclamped ? -raw * v_al : 0.f;
         const float tx_ = v_sig * dx, ty_ = v_sig * dy;
-        a0 += tx_;
-        a1 += ty_;
-        a2 += tx_ * dx;
-        a3 += tx_ * dy;
-        a4 += ty_ * dy;
-        a5 += v_sig;
+        add(a0, tx_);
+        add(a1, ty_);
+        add(a2, tx_ * dx);
+        add(a3, tx_ * dy);
+        add(a4, ty_ * dy);
+        add(a5, v_sig);
         Sv += fac * cv;
       };
-      pixel(p0.y - pyA, lastkA, vrA, vgA, vbA, vTaA, TA, SvA);
-      pixel(p0.y - pyB, lastkB, vrB, vgB, vbB, vTaB, TB, SvB);
+      pixel(true, p0.y - pyA, lastkA, vrA, vgA, vbA, vTaA, TA, SvA);
+      pixel(false, p0.y - pyB, lastkB, vrB, vgB, vbB, vTaB, TB, SvB);
       acc[g * kPartial + 0] = a0;
       acc[g * kPartial + 1] = a1;
       acc[g * kPartial + 2] = a2;
