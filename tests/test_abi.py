@@ -87,6 +87,23 @@ def test_invalid_arguments_are_reported_not_launched():
         _lib.check(rc, "gsr_bin_sort")
 
 
+def test_layout_switches_validate():
+    """The process-wide layout switches accept their documented values only (include/gsr.h:
+    gsr_set_fwd_lanes 0/1/4/16, gsr_set_bwd_layout 0/1/2) and leave the setting unchanged on a
+    bad value; no GPU call is made."""
+    from gsr import _lib
+    lib = _lib.lib()
+    for v in (0, 1, 2):
+        assert lib.gsr_set_bwd_layout(v) == 0
+    for v in (-1, 3, 16):
+        assert lib.gsr_set_bwd_layout(v) == -1 and b"gsr_set_bwd_layout" in lib.gsr_last_error()
+    for v in (0, 1, 4, 16):
+        assert lib.gsr_set_fwd_lanes(v) == 0
+    for v in (2, 8, -4):
+        assert lib.gsr_set_fwd_lanes(v) == -1 and b"gsr_set_fwd_lanes" in lib.gsr_last_error()
+    assert lib.gsr_set_bwd_layout(0) == 0 and lib.gsr_set_fwd_lanes(0) == 0
+
+
 def test_workspace_queries():
     from gsr import _lib
     lib = _lib.lib()
