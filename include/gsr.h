@@ -47,9 +47,9 @@
  *    L = ln(255*opacity) in 3D (gsplat's 1/255 skip), ln(opacity/eps_cut) in 2D.)
  *   2D records (gsr2d_project_fwd, since ABI 8) are stored PACKED for the compositing walks:
  *     [0]=x [1]=y [2]=opacity [3]=r   [4]=a [5]=b [6]=c [7]=g   [8]=b(blue) [9]=L [10]=-b/(2c)
- *     [11]=-b/(2a); and only for the first camera of each parameter set (ABI 7).  Since ABI 11
- *     the 2D a, b, c and L are stored times log2(e) (alpha = opacity * 2^-(a dx^2 + ...), one
- *     v_exp_f32 in the walks); the slopes [10], [11] are unchanged.
+ *     [11]=-b/(2a); and only for the first camera of each parameter set (ABI 7).
+ *   Since ABI 11 (2D) / 12 (3D) a, b, c and L are stored times log2(e) (alpha = opacity *
+ *   2^-(a dx^2 + ...), one v_exp_f32 in the walks); the slopes are unchanged.
  *   depth: 1 float per (c,n) (3D camera-space z; the sort key's high word).
  *   rect: 2 uint32 per (c,n): {x0 | x1<<16, y0 | y1<<16}, tiles [x0,x1) x [y0,y1).
  *
@@ -162,7 +162,8 @@ int gsr_version(void);
 /* Revision 10: partial rows are 9 floats (GSR_PARTIAL_STRIDE 9, was 12: the 3 padding floats cost
  * 25 % of the rows' HBM writes and reads). */
 /* Revision 11: 2D records hold the conic and L times log2(e) (layout above). */
-#define GSR_ABI_VERSION 11
+/* Revision 12: 3D records too hold the conic and L times log2(e). */
+#define GSR_ABI_VERSION 12
 int gsr_abi_version(void);
 const char* gsr_last_error(void);
 

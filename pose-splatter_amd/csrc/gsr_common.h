@@ -286,19 +286,28 @@ __device__ __forceinline__ float conic_sigma(const float4 p1, float dx, float dy
   return p1.x * dx * dx + p1.z * dy * dy + p1.y * dx * dy;
 }
 
-// exp(-sigma) of a record's conic.  2D records store the conic and L scaled by log2(e)
-// (k_project2d_fwd, ABI 11): sigma' = sigma log2(e), so exp(-sigma) = 2^(-sigma') is ONE
-// v_exp_f32 (__expf is a multiply by -log2(e) and the same v_exp_f32).  The gradients that
-// sum v_sig * dx^2 ... stay derivatives by the unscaled conic (v_sig is dL/dsigma either way);
-// only the mean's chain through the conic needs the unscaled a, b, c (kLn2 * stored).
+// exp(-sigma) of a record's conic.  Records store the conic and L scaled by log2(e)
+// (k_project2d_fwd since ABI 11, k_project3d_fwd since ABI 12): sigma' = sigma log2(e), so
+// exp(-sigma) = 2^(-sigma') is ONE v_exp_f32 (__expf is a multiply by -log2(e) and the same
+// v_exp_f32); sigma' >= 0 iff sigma >= 0.  The gradients that sum v_sig * dx^2 ... stay
+// derivatives by the unscaled conic (v_sig is dL/dsigma either way); only the mean's chain
+// through the conic needs the unscaled a, b, c (kLn2 * stored).
 constexpr float kLog2e = 1.44269504088896341f;
 constexpr float kLn2 = 0.693147180559945309f;
+#ifndef GSR_CONIC3D_LOG2E
+#define GSR_CONIC3D_LOG2E 1   // 0: 3D records unscaled (the ABI-11 form; a build knob for A/B runs)
+#endif
 template <bool IS2D>
 __device__ __forceinline__ float gauss_exp(float sigma) {
-  if constexpr (IS2D)
+  if constexpr (IS2D || GSR_CONIC3D_LOG2E)
     return __builtin_amdgcn_exp2f(-sigma);
   else
     return __expf(-sigma);
+}
+// factor from a stored conic to the true one (the rows phases' mean chain)
+template <bool IS2D>
+__device__ __forceinline__ constexpr float conic_unscale() {
+  return (IS2D || GSR_CONIC3D_LOG2E) ? kLn2 : 1.f;
 }
 
 template <bool IS2D>

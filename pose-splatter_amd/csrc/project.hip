@@ -179,10 +179,13 @@ __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
       if (x1 < x0) x1 = x0;
       if (y1 < y0) y1 = y0;
       // record: the compositing inputs plus the per-Gaussian constants of the exact sub-tile
-      // cull (raster.hip cull_keep): L = ln(opacity * 255) and the edge slopes -B/C, -B/A
+      // cull (raster.hip cull_keep): L = ln(opacity * 255) and the edge slopes -B/C, -B/A.
+      // Conic and L times log2(e) (ABI 12): alpha = o 2^(-sigma'), one v_exp_f32
+      // (gsr_common.h gauss_exp); the slopes are ratios, unscaled.
       Splat s;
-      s.p0 = make_float4(g.u, g.v, a.op, logf(a.op * 255.f));
-      s.p1 = make_float4(0.5f * g.A, g.B, 0.5f * g.C, -g.B / g.C);
+      constexpr float ks = GSR_CONIC3D_LOG2E ? kLog2e : 1.f;
+      s.p0 = make_float4(g.u, g.v, a.op, logf(a.op * 255.f) * ks);
+      s.p1 = make_float4(0.5f * g.A * ks, g.B * ks, 0.5f * g.C * ks, -g.B / g.C);
       s.p2 = make_float4(a.col[0], a.col[1], a.col[2], -g.B / g.A);
       rec[cn] = s;
       depth[cn] = g.mc[2];

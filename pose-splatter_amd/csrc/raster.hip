@@ -1801,10 +1801,9 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
       for (int q = 0; q < kPartial; ++q) v[q] = (L[q][0][k] + L[q][1][k]) + (L[q][2][k] + L[q][3][k]);
       const float4 p1 = s_p[1][k];
       const float mx = v[0], my = v[1];
-      // (2D records hold the conic times log2(e): the mean's chain takes the unscaled one)
-      const float cs = IS2D ? kLn2 : 1.f;
-      v[0] = (2.f * p1.x * mx + p1.y * my) * cs;
-      v[1] = (p1.y * mx + 2.f * p1.z * my) * cs;
+      // (records hold the conic times log2(e): the mean's chain takes the unscaled one)
+      v[0] = (2.f * p1.x * mx + p1.y * my) * conic_unscale<IS2D>();
+      v[1] = (p1.y * mx + 2.f * p1.z * my) * conic_unscale<IS2D>();
       v[5] = -v[5] / s_p[0][k].z;
       store_partial_row(partial, kos_mine & kEmitIndexMask, v);   // (bits 28..31: the 3D quadrant mask)
     }
@@ -2544,7 +2543,7 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
                        float& Sv) {
         auto add = [first](float& a, float x) { a = first ? x : a + x; };
         const float sigma = conic_sigma(p1, dx, dy);
-        const float vis = __expf(-sigma);
+        const float vis = gauss_exp<false>(sigma);
         const float raw = p0.z * vis;
         const float alpha = fminf(kAlphaMax, raw);
         const bool valid = (k <= lastk) & (sigma >= 0.f) & (alpha >= kAlphaThreshold);
@@ -2603,8 +2602,8 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
     for (int q = 0; q < kPartial; ++q) v[q] = L[q][0][k] + L[q][1][k];
     const float4 p1 = s_p[1][k];
     const float mx = v[0], my = v[1];
-    v[0] = 2.f * p1.x * mx + p1.y * my;
-    v[1] = p1.y * mx + 2.f * p1.z * my;
+    v[0] = (2.f * p1.x * mx + p1.y * my) * conic_unscale<false>();   // (records: conic times log2(e))
+    v[1] = (p1.y * mx + 2.f * p1.z * my) * conic_unscale<false>();
     v[5] = -v[5] / s_p[0][k].z;
     store_partial_row(partial, kos_mine & kEmitIndexMask, v);
   }
