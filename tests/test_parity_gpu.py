@@ -393,7 +393,8 @@ def _oracle2d(p, W, H, bg, vr, va):
     return rgb.detach(), alpha.detach(), pc.grad.detach()
 
 
-@pytest.mark.parametrize("N,W,H,seed,mu", [(3000, 128, 96, 51, 0.4), (1500, 64, 64, 52, 1.8)])
+# (70 x 45: ragged edge tiles -- the pair kernels' per-pixel image masks, rows r and r + 2)
+@pytest.mark.parametrize("N,W,H,seed,mu", [(3000, 128, 96, 51, 0.4), (1500, 64, 64, 52, 1.8), (1200, 70, 45, 53, 0.8)])
 def test_2d_vs_oracle_dense(cuda, fwd_lanes, N, W, H, seed, mu):
     from gsr.scenes import gaussians2d
     p = gaussians2d(N, W, H, seed)
