@@ -2386,6 +2386,9 @@ constexpr int kBwdPairTilesPerCU = 64;
 #ifndef GSR_BWD3P_MINB
 #define GSR_BWD3P_MINB 3   // waves per SIMD the compiler aims at
 #endif
+#ifndef GSR_BWD3P_HALFSTAGE
+#define GSR_BWD3P_HALFSTAGE 1
+#endif
 __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const float4* __restrict__ ckpt, int W, int H,
     int tw, int th, const float* __restrict__ bg, const float* __restrict__ final_T,
@@ -2401,7 +2404,8 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
   __shared__ __attribute__((aligned(16))) float L[kPartial][2][kChunk3 + 1];
   __shared__ unsigned char s_list[2][kLen];
   __shared__ __attribute__((aligned(16))) unsigned char s_box[2][8][kLenB];
-  __shared__ __attribute__((aligned(16))) float s_stage[2][64][8];
+  // GSR_BWD3P_HALFSTAGE: stage the reduced sums in two halves (2 KB less LDS: 8 workgroups per CU)
+  __shared__ __attribute__((aligned(16))) float s_stage[2][64][GSR_BWD3P_HALFSTAGE ? 4 : 8];
   const int4 cd = reinterpret_cast<const int4*>(chunk_list)[blockIdx.x];
   const int n_act = stats->n_active, ovf = stats->overflow, ce = stats->chunk_entries;
   const bool unit_bad = ce != kChunk3;
@@ -2476,7 +2480,7 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
   const int fg = lane / kPartial, fq = lane - kPartial * (lane / kPartial);
   const bool fown = lane < kGroup * kPartial;
   float* const Lw = &L[fq][wv][0];
-  const float* const stage_rd = &s_stage[wv][(lane >> 3) << 3][lane & 7];   // + 8 * box
+  const float* const stage_rd = &s_stage[wv][(lane >> 3) << 3][lane & (GSR_BWD3P_HALFSTAGE ? 3 : 7)];   // + 8 * box
   const unsigned char* my_list = s_box[wv][box];
   __syncthreads();
   // cull the chunk against the wave's 16x8 half-tile (exact test), survivors back to front
@@ -2582,6 +2586,21 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
     float sum[8];
     reduce_box8(acc, sum);
     float4* st = reinterpret_cast<float4*>(&s_stage[wv][lane][0]);
+#if GSR_BWD3P_HALFSTAGE
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      st[0] = h == 0 ? make_float4(sum[0], sum[1], sum[2], sum[3]) : make_float4(sum[4], sum[5], sum[6], sum[7]);
+      __builtin_amdgcn_wave_barrier();
+      if (fown && ((lane >> 2) & 1) == h) {
+#pragma unroll
+        for (int bx = 0; bx < 8; ++bx) {
+          const int k = s_box[wv][bx][gb + fg];
+          Lw[k] += stage_rd[4 * bx];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+#else
     st[0] = make_float4(sum[0], sum[1], sum[2], sum[3]);
     st[1] = make_float4(sum[4], sum[5], sum[6], sum[7]);
     __builtin_amdgcn_wave_barrier();
@@ -2593,6 +2612,7 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
       }
     }
     __builtin_amdgcn_wave_barrier();
+#endif
   }
   __syncthreads();
   if ((int)threadIdx.x < sn) {
