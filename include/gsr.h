@@ -175,6 +175,13 @@ int gsr_selftest_reduce64(float* out, void* stream);
  * out[4*l + i] = sum over the 16 lanes L with L % 4 == l % 4 of v_L[4*(l/4) + i].  out: 256 floats. */
 int gsr_selftest_reduce_box16(float* out, void* stream);
 
+/* Self-test of the b128-group-aligned per-box reductions of the raster backward (one 64-lane
+ * wave, same pattern; additive to revision 12).  box_lanes 16 (G = 4 sums per lane) or 8 (G = 8):
+ * out[G*l + i] = sum over the lanes L whose walk box equals lane l's output box of
+ * v_L[G*slot(l) + i]; then out[64*G + 4*l + {0,1,2,3}] = {walk box, position in it, output box,
+ * slot} of lane l as floats.  out: 64 * (G + 4) floats. */
+int gsr_selftest_reduce_grp(float* out, int box_lanes, void* stream);
+
 /* Layout of the raster forward (process-wide): 0 = automatic (3D: 16 lanes per pixel and 16
  * workgroups per tile with at most 160 busy tiles, else 4 lanes per pixel and 4 workgroups per
  * tile; 2D: one 2-wave workgroup per tile, two pixels per lane), or 1, 4 or 16 (3D only) to force one.
@@ -451,13 +458,16 @@ int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride,
  * own a list entry before their tile's cut in any of the call's busy tiles (tile_order, the
  * device busy count in stats; n_busy bounds it) -- exactly those the raster backward gives a
  * partial row.  header count := their number, rows 1 + i := {n, 0, 0...} for the first cap.
+ * stats->overflow set (the forward's bounds did not hold): header count := cap + 1, so the
+ * exchange (gsr_rows_scatter_add) NaN-fills and reports GSR_OVF_EXCHANGE.
  * flags: caller workspace of N bytes (rounded up to 4).  N == 0 or n_busy == 0: the header only. */
 int gsr3d_touched_rows(const int32_t* sorted_ids, const int32_t* tile_offset, const int32_t* tile_end,
                        const int32_t* tile_order, const gsr_bin_stats* stats, int32_t n_busy, int64_t N,
                        int64_t cap, uint8_t* flags, float* block, void* stream);
 
 /* gsr3d_project_bwd for the Gaussians listed in `block` (gsr3d_touched_rows): their 14
- * gradients go to words 2..15 of their rows (deterministic per row; stats->overflow set: NaN). */
+ * gradients go to words 2..15 of their rows (deterministic per row; stats->overflow set: NaN
+ * rows, and the header gsr3d_touched_rows left past the cap poisons the exchange). */
 int gsr3d_project_bwd_rows(const float* params, int64_t N, int64_t row_stride,
                            const float* viewmats, const float* Ks, int C, int width, int height,
                            float eps2d, int input_mode, const float* depth, const uint32_t* rect,

@@ -298,7 +298,7 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__
         const int t = ty * tw + tx;
         const int slot = use_lds ? atomicAdd(&hist[t], 1) : toff[t] + atomicSub(&gcnt[t], 1) - 1;
         // 3D: the entry's quadrant mask in the top bits (gsr_common.h quad_mask)
-        const int mk = rec != nullptr ? quad_mask<false>(sp.p0, sp.p1, sp.p2, tx, ty) << kMaskShift : 0;
+        const int mk = rec != nullptr ? (int)((unsigned)quad_mask<false>(sp.p0, sp.p1, sp.p2, tx, ty) << kMaskShift) : 0;
         keys[slot] = key;
         k_of_slot[slot] = k++ | mk;
       }
@@ -420,7 +420,7 @@ __global__ __launch_bounds__(kStageThreads) void k_emit_staged(
       for (int tx = x0; tx < x1; ++tx) {
         const int t = ty * tw + tx;
         const int p = atomicAdd(&cur[t], 1);
-        const int kk = k | (rec != nullptr ? quad_mask<false>(sp.p0, sp.p1, sp.p2, tx, ty) << kMaskShift : 0);
+        const int kk = (int)((unsigned)k | (rec != nullptr ? (unsigned)quad_mask<false>(sp.p0, sp.p1, sp.p2, tx, ty) << kMaskShift : 0u));
         if (staged) {
           s_key[p] = key[j];
           s_kos[p] = kk;

@@ -91,6 +91,9 @@ __global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
     const int64_t count = min((int64_t)reinterpret_cast<const int32_t*>(block)[0], cap);
     listed = i_row < count;
     n = listed ? reinterpret_cast<const int32_t*>(block)[(1 + i_row) * GSR_ROW_FLOATS] : 0;
+    // (after a forward overflow the header is past the cap and the rows hold no indices: kept
+    // in range; those rows are written NaN below, and gsr_rows_scatter_add NaN-fills anyway)
+    n = min(max(n, (int64_t)0), max(N - 1, (int64_t)0));
   } else {
     n = n_begin + i_row;
     listed = n < n_end;
@@ -323,9 +326,18 @@ __global__ __launch_bounds__(kBwdThreads) void k_mark_touched(const int32_t* __r
 }
 
 // One returning atomic per wave claims the wave's rows (positions follow arrival order; the
-// exchange's sum is per row, so the order does not change a bit of the result).
+// exchange's sum is per row, so the order does not change a bit of the result).  A forward
+// whose bounds did not hold (stats->overflow; k_mark_touched flagged nothing) sets the header
+// past the cap instead, so the exchange reports GSR_OVF_EXCHANGE and NaN-fills the gradient
+// rather than summing a share that silently lacks this rank's rows.
 __global__ __launch_bounds__(kBwdThreads) void k_touched_rows(const uint8_t* __restrict__ flag, int64_t N, int64_t cap,
-                                                              float* __restrict__ block) {
+                                                              float* __restrict__ block,
+                                                              const gsr_bin_stats* __restrict__ stats) {
+  if (stats->overflow) {
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+      reinterpret_cast<int32_t*>(block)[0] = (int32_t)min<int64_t>(cap + 1, INT32_MAX);
+    return;
+  }
   const int64_t n = (int64_t)blockIdx.x * kBwdThreads + threadIdx.x;
   const bool any = n < N && flag[n] != 0;
   const unsigned long long m = __ballot(any);
@@ -558,7 +570,8 @@ int gsr3d_touched_rows(const int32_t* sorted_ids, const int32_t* tile_offset, co
   hipLaunchKernelGGL(k_mark_touched, dim3(n_busy), dim3(kBwdThreads), 0, s, sorted_ids, tile_offset, tile_end,
                      tile_order, stats, N, flags);
   GSR_LAUNCH_CHECK("k_mark_touched");
-  hipLaunchKernelGGL(k_touched_rows, dim3(ceil_div(N, kBwdThreads)), dim3(kBwdThreads), 0, s, flags, N, cap, block);
+  hipLaunchKernelGGL(k_touched_rows, dim3(ceil_div(N, kBwdThreads)), dim3(kBwdThreads), 0, s, flags, N, cap, block,
+                     stats);
   GSR_LAUNCH_CHECK("k_touched_rows");
   return GSR_OK;
 }

@@ -1420,6 +1420,47 @@ __device__ __forceinline__ void store_partial_row(float* __restrict__ partial, i
   for (int q = 0; q < kPartial; ++q) dst[q] = v[q];
 }
 
+// The per-entry sum update of the backward kernels: lane f adds the staged value v[b] of box b
+// to its wave's slot Lw[k[b]], for NB boxes.  A box lists an entry once, but two boxes may list
+// the same entry, so adds to one address follow in box order.  GSR_BWD_LWPAR: the NB reads are
+// issued together and the aliased boxes chained in registers (n_b = n_c + v_b for the latest
+// earlier box c with k_c == k_b -- the sequential read-add-write's order of additions, so the
+// sums are bitwise those of the serial form), then NB writes in box order (the last write of an
+// address holds its full sum): one LDS round trip per batch instead of NB dependent ones.
+#ifndef GSR_BWD_LWPAR
+#define GSR_BWD_LWPAR 1
+#endif
+template <int NB>
+__device__ __forceinline__ void lw_add(float* __restrict__ Lw, const int (&k)[NB], const float (&v)[NB]) {
+#if GSR_BWD_LWPAR
+  float n[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) n[b] = Lw[k[b]];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    n[b] += v[b];
+#pragma unroll
+    for (int c = 0; c < b; ++c) n[b] = k[c] == k[b] ? n[c] + v[b] : n[b];
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) Lw[k[b]] = n[b];
+#else
+#pragma unroll
+  for (int b = 0; b < NB; ++b) Lw[k[b]] += v[b];
+#endif
+}
+// GSR_BWD_PF: the walk reads entry g+1's record from LDS before it evaluates entry g (a
+// scheduling fence keeps the reads there: left to itself the compiler issued each entry's reads
+// at its use, two exposed LDS round trips per entry, 14 per group)
+#ifndef GSR_BWD_PF
+#define GSR_BWD_PF 1
+#endif
+__device__ __forceinline__ void walk_fence() {
+#if GSR_BWD_PF
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+
 // Cotangent of  g_iou * iou_loss + g_img * img_loss  (+ extra cotangents) at one pixel
 // (scripts/training/train_script.py:30-36, 128-130), from the sums of gsr_loss_iou_l1_fwd:
 //   d iou_loss / d a = -(1/C) [ m / (U+e) - (I+e) / (U+e)^2 (1 - m) ]       (e = 1e-6)
@@ -1526,12 +1567,17 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
   constexpr bool PK = GSR_BWD_LDS;
   constexpr int kLenB = PK ? 8 * ((kLen + kGroup - 1) / kGroup) : kLen;
   __shared__ float4 s_p[3][kChunk3 + 1];   // the chunk's records, part j of entry k at s_p[j][k]
-  // gradient sums per entry, one slot per wave (index kNull absorbs the padding's zeros)
-  __shared__ __attribute__((aligned(16))) float L[kPartial][4][kChunk3 + 1];
-  static_assert((kPartial * 4 * (kChunk3 + 1)) % 4 == 0, "L is zeroed in float4 stores");
+  // gradient sums per entry, one slot per wave (index kNull absorbs the padding's zeros):
+  // sum q of entry k in wave w's slot at L[q * kLq + w * (kChunk3 + 1) + k].  The odd q stride
+  // (517 = 5 mod 32 banks) keeps the nine q of one entry on nine banks in the read-add-writes
+  // below (516 put q = 0 and q = 8 on one bank: a 2-way conflict in every instruction)
+  constexpr int kLq = 4 * (kChunk3 + 1) + 1;
+  constexpr int kLn = kPartial * kLq;
+  __shared__ __attribute__((aligned(16))) float L[(kLn + 3) & ~3];
   __shared__ unsigned char s_list[4][kLen];     // quadrant survivors, back to front
   __shared__ __attribute__((aligned(16))) unsigned char s_box[4][4][kLenB];   // per (wave, box) survivors, back to front
-  __shared__ float s_stage[4][64][4];     // per wave: the group's reduced sums, by lane
+  // per wave: the group's reduced sums, box-major rows of 64 (reduce_grp16's swizzled staging)
+  __shared__ __attribute__((aligned(16))) float s_stage[4][4][64];
   __shared__ unsigned char s_mask[kChunk3];   // 3D: each entry's quadrant mask (k_of_s bits 28..31)
   // one workgroup per grid slot; slots past the forward's active-chunk count exit at once
   // the chunk's descriptor {first entry, entries (>= 1), chunk record row, tile} -- one load
@@ -1562,7 +1608,8 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
   int c, ty, tx;
   tile_coords(ct, tw, th, c, ty, tx);
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int box = lane & 3, pos = lane >> 2;
+  // box = the lane's ds_read_b128 group (reduce_grp16): a walk read is one address per group
+  const int box = b128_group(lane), pos = grp16_pos(lane);
   const float off = IS2D ? 0.f : 0.5f;   // 2D: integer centres (src/gaussian_renderer.py:355-358)
   const int qx0 = tx * kTile + (wv & 1) * 8, qy0 = ty * kTile + (wv >> 1) * 8;   // quadrant origin
   const int bx0i = qx0 + (box & 1) * 4, by0i = qy0 + (box >> 1) * 4;             // box origin
@@ -1633,8 +1680,13 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
   }
   const int fg = lane / kPartial, fq = lane - kPartial * (lane / kPartial);
   const bool fown = lane < kGroup * kPartial;
-  float* const Lw = &L[fq][wv][0];
-  const float* const stage_rd = &s_stage[wv][0][0] + 4 * (4 * (lane >> 2)) + (lane & 3);   // + 4*box
+  float* const Lw = &L[fq * kLq + wv * (kChunk3 + 1)];
+  // lane f reads flat sum f of box bx at s_stage[wv][bx][f ^ grp16_swz(bx)]; lane l stages its
+  // four sums (box grp16_out_box(l), flat 4 grp16_slot(l) + i) as one b128 store
+  const float* const stage_rd0 = &s_stage[wv][0][lane];
+  const float* const stage_rd1 = &s_stage[wv][0][lane ^ 16];
+  float4* const stage_wr = reinterpret_cast<float4*>(
+      &s_stage[wv][grp16_out_box(lane)][(4 * grp16_slot(lane)) ^ grp16_swz(grp16_out_box(lane))]);
   const unsigned char* my_list = s_box[wv][box];
   for (int sub = nsub - 1; sub >= 0; --sub) {
     if (sub != nsub - 1) __syncthreads();   // the previous sub-chunk's LDS is consumed
@@ -1645,8 +1697,8 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
       s_p[2][threadIdx.x] = sp2;
       s_mask[threadIdx.x] = (unsigned char)((unsigned)kos_mine >> kMaskShift);
     }
-    for (int i = threadIdx.x; i < kPartial * (kChunk3 + 1); i += kRasterThreads)   // b128 stores
-      reinterpret_cast<float4*>(&L[0][0][0])[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = threadIdx.x; i < ((kLn + 3) >> 2); i += kRasterThreads)   // b128 stores
+      reinterpret_cast<float4*>(L)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (threadIdx.x == 0) {
       const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
       s_p[0][kNull] = z;
@@ -1702,8 +1754,9 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
     if (pos == 0) tr_nb[wv * 4 + box] = nb;
 #endif
     BWD_T(3);
-    // after reduce_box16 lane l holds 4 of its box's sums, flat indices 4*(l>>2) + i = 9*g + q.
-    // They are staged in LDS (one b128 store per group), and lane f < 63 then adds flat index
+    // after reduce_grp16 lane l holds 4 sums of box grp16_out_box(l), flat indices
+    // 4 grp16_slot(l) + i = 9*g + q.  They are staged in LDS (one b128 store per group, box-major
+    // and swizzled: conflict-free stores and reads), and lane f < 63 then adds flat index
     // f = 9g + q of every box, box by box, into the wave's slot L[q][wv][entry]: inside one
     // instruction the 63 (q, entry) addresses are distinct (a box lists an entry once), and
     // the boxes follow in program order, so the plain read-add-write is race-free and
@@ -1714,17 +1767,29 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
       float acc[64];
       acc[63] = 0.f;
       const uint2 w8 = PK ? *reinterpret_cast<const uint2*>(my_list + gb) : make_uint2(0u, 0u);
+      int kk[kGroup];
+#pragma unroll
+      for (int g = 0; g < kGroup; ++g)
+        kk[g] = PK ? (int)(((g < 4 ? w8.x : w8.y) >> (8 * (g & 3))) & 0xFFu) : my_list[g0 + g];
+      // entry g+1's record is read before entry g is evaluated (GSR_BWD_PF)
+      float4 n0 = s_p[0][kk[0]], n1 = s_p[1][kk[0]], n2 = s_p[2][kk[0]];
 #pragma unroll
       for (int g = 0; g < kGroup; ++g) {
-        const int k = PK ? (int)(((g < 4 ? w8.x : w8.y) >> (8 * (g & 3))) & 0xFFu) : my_list[g0 + g];
-        const float4 p0 = s_p[0][k];
-        const float4 p1 = s_p[1][k];
+        const int k = kk[g];
+        const float4 p0 = n0;
+        const float4 p1 = n1;
         float4 p2;
         if (PK) {
-          p2 = make_float4(p0.w, p1.w, reinterpret_cast<const float*>(&s_p[2][k])[0], 0.f);   // the colour
+          p2 = make_float4(p0.w, p1.w, n2.x, 0.f);   // the colour (packed: b32 in part 2)
         } else {
-          p2 = s_p[2][k];
+          p2 = n2;
         }
+        if (g + 1 < kGroup) {
+          n0 = s_p[0][kk[g + 1]];
+          n1 = s_p[1][kk[g + 1]];
+          n2 = s_p[2][kk[g + 1]];
+        }
+        walk_fence();
         const float dx = p0.x - px, dy = p0.y - py;
         const float sigma = conic_sigma(p1, dx, dy);
         const float vis = gauss_exp<IS2D>(sigma);
@@ -1767,15 +1832,18 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
         if (!IS2D) Sv += fac * cv;
       }
       float sum[4];
-      reduce_box16(acc, sum);
-      reinterpret_cast<float4*>(&s_stage[wv][0][0])[lane] = make_float4(sum[0], sum[1], sum[2], sum[3]);
+      reduce_grp16(acc, sum);
+      *stage_wr = make_float4(sum[0], sum[1], sum[2], sum[3]);
       __builtin_amdgcn_wave_barrier();
       if (fown) {
+        int kb[4];
+        float vb4[4];
 #pragma unroll
         for (int bx = 0; bx < 4; ++bx) {
-          const int k = s_box[wv][bx][PK ? gb + fg : g0 + fg];
-          Lw[k] += stage_rd[4 * bx];
+          kb[bx] = s_box[wv][bx][PK ? gb + fg : g0 + fg];
+          vb4[bx] = (grp16_swz(bx) ? stage_rd1 : stage_rd0)[64 * bx];
         }
+        lw_add(Lw, kb, vb4);
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -1798,14 +1866,19 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
       const int k = threadIdx.x;
       float v[kPartial];
 #pragma unroll
-      for (int q = 0; q < kPartial; ++q) v[q] = (L[q][0][k] + L[q][1][k]) + (L[q][2][k] + L[q][3][k]);
+      for (int q = 0; q < kPartial; ++q) {
+        const float* Lq = &L[q * kLq + k];
+        v[q] = (Lq[0] + Lq[kChunk3 + 1]) + (Lq[2 * (kChunk3 + 1)] + Lq[3 * (kChunk3 + 1)]);
+      }
       const float4 p1 = s_p[1][k];
       const float mx = v[0], my = v[1];
       // (records hold the conic times log2(e): the mean's chain takes the unscaled one)
       v[0] = (2.f * p1.x * mx + p1.y * my) * conic_unscale<IS2D>();
       v[1] = (p1.y * mx + 2.f * p1.z * my) * conic_unscale<IS2D>();
       v[5] = -v[5] / s_p[0][k].z;
-      store_partial_row(partial, kos_mine & kEmitIndexMask, v);   // (bits 28..31: the 3D quadrant mask)
+      // (bits 28..31 hold the 3D quadrant mask only where the emission stored masks: a call
+      // without them may have 2^28 entries or more, whose indices must not be cut)
+      store_partial_row(partial, use_masks ? kos_mine & kEmitIndexMask : kos_mine, v);
     }
     sb0 -= kChunk3;
     sn = kChunk3;
@@ -2079,7 +2152,7 @@ __global__ __launch_bounds__(kRasterThreads, GSR_BWD2D_MINB) void k_raster2d_bwd
       v[0] = (2.f * p1.x * mx + p1.y * my) * kLn2;
       v[1] = (p1.y * mx + 2.f * p1.z * my) * kLn2;
       v[5] = -v[5] / sp[0][k].z;
-      store_partial_row(partial, kos_mine & kEmitIndexMask, v);
+      store_partial_row(partial, kos_mine, v);   // (2D emissions store no masks)
     }
     BWD2_P(4);
     sb0 -= kChunk3;
@@ -2128,7 +2201,8 @@ __global__ __launch_bounds__(128, GSR_BWD2P_MINB) void k_raster2d_bwd_pair(
   __shared__ __attribute__((aligned(16))) float L[kPartial][2][kChunk3 + 1];
   __shared__ unsigned char s_list[2][kLen];
   __shared__ __attribute__((aligned(16))) unsigned char s_box[2][8][kLenB];
-  __shared__ __attribute__((aligned(16))) float s_stage[2][64][8];
+  // per wave: the group's reduced sums, box-major rows of 64 (reduce_grp8's swizzled staging)
+  __shared__ __attribute__((aligned(16))) float s_stage[2][8][64];
   const int4 cd = reinterpret_cast<const int4*>(units)[blockIdx.x];
   const int n_act = stats->n_active, ovf = stats->overflow, U = stats->chunk_entries;
   if ((ovf != 0) | ((int)blockIdx.x >= n_act) | (cd.y <= 0)) return;
@@ -2137,7 +2211,8 @@ __global__ __launch_bounds__(128, GSR_BWD2P_MINB) void k_raster2d_bwd_pair(
   tile_coords(ct, tw, th, c, ty, tx);
   rec += rec_offset2d(sets.begin, sets.F, c, sets.N);   // the set's record copy
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int box = lane & 7, pp = lane >> 3;
+  // box: two per ds_read_b128 lane group (reduce_grp8), so a walk read is two addresses per group
+  const int box = grp8_box(lane), pp = grp8_pos(lane);
   const int hx0 = tx * kTile, hy0 = ty * kTile + 8 * wv;   // the wave's 16x8 half-tile
   const int bjl = 4 * (box & 3), bil = 8 * wv + 4 * (box >> 2);   // box origin in the tile
   const int jl = bjl + (pp & 3), ilA = bil + (pp >> 2), ilB = ilA + 2;
@@ -2191,7 +2266,12 @@ __global__ __launch_bounds__(128, GSR_BWD2P_MINB) void k_raster2d_bwd_pair(
   const int fg = lane / kPartial, fq = lane - kPartial * (lane / kPartial);
   const bool fown = lane < kGroup * kPartial;
   float* const Lw = &L[fq][wv][0];
-  const float* const stage_rd = &s_stage[wv][(lane >> 3) << 3][lane & 7];   // + 8 * box
+  // lane f reads flat sum f of box bx at s_stage[wv][bx][f ^ grp8_swz(bx)]; lane l stages its 8
+  // sums (box grp8_out_box(l), flat 8 grp8_slot(l) + i) as two b128 stores
+  const float* const stage_rd = &s_stage[wv][0][0];
+  const int obox = grp8_out_box(lane);
+  float* const stage_wr = &s_stage[wv][obox][0];
+  const int wr0 = (8 * grp8_slot(lane)) ^ grp8_swz(obox), wr1 = (8 * grp8_slot(lane) + 4) ^ grp8_swz(obox);
   const unsigned char* my_list = s_box[wv][box];
   if (threadIdx.x < 3) s_p[threadIdx.x][kNull] = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int sub = nsub - 1; sub >= 0; --sub) {
@@ -2268,12 +2348,23 @@ __global__ __launch_bounds__(128, GSR_BWD2P_MINB) void k_raster2d_bwd_pair(
       float acc[64];
       acc[63] = 0.f;
       const uint2 w8 = *reinterpret_cast<const uint2*>(my_list + gb);
+      int kk[kGroup];
+#pragma unroll
+      for (int g = 0; g < kGroup; ++g) kk[g] = (int)(((g < 4 ? w8.x : w8.y) >> (8 * (g & 3))) & 0xFFu);
+      float4 n0 = s_p[0][kk[0]], n1 = s_p[1][kk[0]];
+      float n2 = reinterpret_cast<const float*>(&s_p[2][kk[0]])[0];
 #pragma unroll
       for (int g = 0; g < kGroup; ++g) {
-        const int k = (int)(((g < 4 ? w8.x : w8.y) >> (8 * (g & 3))) & 0xFFu);
-        const float4 p0 = s_p[0][k];   // x, y, o, r
-        const float4 p1 = s_p[1][k];   // a, b, c, g
-        const float cbl = reinterpret_cast<const float*>(&s_p[2][k])[0];   // blue
+        const int k = kk[g];
+        const float4 p0 = n0;   // x, y, o, r
+        const float4 p1 = n1;   // a, b, c, g
+        const float cbl = n2;   // blue
+        if (g + 1 < kGroup) {   // entry g+1's record read before entry g is evaluated (GSR_BWD_PF)
+          n0 = s_p[0][kk[g + 1]];
+          n1 = s_p[1][kk[g + 1]];
+          n2 = reinterpret_cast<const float*>(&s_p[2][kk[g + 1]])[0];
+        }
+        walk_fence();
         const float dx = p0.x - px, dyA = p0.y - pyA;
         const int ks = sb0 + k;   // the entry's list position (the zero pad slot is never valid: alpha 0)
         // the entry's 9 sums over the lane's two pixels: pixel A sets them, pixel B adds (a
@@ -2318,16 +2409,22 @@ __global__ __launch_bounds__(128, GSR_BWD2P_MINB) void k_raster2d_bwd_pair(
         acc[g * kPartial + 8] = a8;
       }
       float sum[8];
-      reduce_box8(acc, sum);
-      float4* st = reinterpret_cast<float4*>(&s_stage[wv][lane][0]);
-      st[0] = make_float4(sum[0], sum[1], sum[2], sum[3]);
-      st[1] = make_float4(sum[4], sum[5], sum[6], sum[7]);
+      reduce_grp8(acc, sum);
+      *reinterpret_cast<float4*>(stage_wr + wr0) = make_float4(sum[0], sum[1], sum[2], sum[3]);
+      *reinterpret_cast<float4*>(stage_wr + wr1) = make_float4(sum[4], sum[5], sum[6], sum[7]);
       __builtin_amdgcn_wave_barrier();
-      if (fown) {
+      if (fown) {   // two batches of four boxes (lw_add)
 #pragma unroll
-        for (int bx = 0; bx < 8; ++bx) {
-          const int k = s_box[wv][bx][gb + fg];
-          Lw[k] += stage_rd[8 * bx];
+        for (int h = 0; h < 2; ++h) {
+          int kb[4];
+          float vb4[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int bx = 4 * h + j;
+            kb[j] = s_box[wv][bx][gb + fg];
+            vb4[j] = stage_rd[64 * bx + (lane ^ grp8_swz(bx))];
+          }
+          lw_add(Lw, kb, vb4);
         }
       }
       __builtin_amdgcn_wave_barrier();
@@ -2362,7 +2459,7 @@ __global__ __launch_bounds__(128, GSR_BWD2P_MINB) void k_raster2d_bwd_pair(
       v[0] = (2.f * p1.x * mx + p1.y * my) * kLn2;
       v[1] = (p1.y * mx + 2.f * p1.z * my) * kLn2;
       v[5] = -v[5] / s_p[0][k].z;
-      store_partial_row(partial, kos_mine & kEmitIndexMask, v);
+      store_partial_row(partial, kos_mine, v);   // (2D emissions store no masks)
     }
     sb0 -= kChunk3;
     sn = kChunk3;
@@ -2405,9 +2502,11 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
   __shared__ unsigned char s_list[2][kLen];
   __shared__ __attribute__((aligned(16))) unsigned char s_box[2][8][kLenB];
   // GSR_BWD3P_HALFSTAGE: stage the reduced sums in two halves (2 KB less LDS: 8 workgroups per CU)
-  __shared__ __attribute__((aligned(16))) float s_stage[2][64][GSR_BWD3P_HALFSTAGE ? 4 : 8];
+  // (box-major rows of 64 -- 32 in halves -- per wave: reduce_grp8's swizzled staging)
+  __shared__ __attribute__((aligned(16))) float s_stage[2][8][GSR_BWD3P_HALFSTAGE ? 32 : 64];
   const int4 cd = reinterpret_cast<const int4*>(chunk_list)[blockIdx.x];
   const int n_act = stats->n_active, ovf = stats->overflow, ce = stats->chunk_entries;
+  const bool use_masks = stats->masks != 0;   // k_of_s bits 28..31 hold quadrant masks
   const bool unit_bad = ce != kChunk3;
   if ((ovf != 0) | ((int)blockIdx.x >= n_act) | unit_bad | (cd.y <= 0)) {
     if (unit_bad && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -2420,7 +2519,7 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
   int c, ty, tx;
   tile_coords(ct, tw, th, c, ty, tx);
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int box = lane & 7, pp = lane >> 3;
+  const int box = grp8_box(lane), pp = grp8_pos(lane);   // (two boxes per b128 lane group)
   const int hx0 = tx * kTile, hy0 = ty * kTile + 8 * wv;   // the wave's 16x8 half-tile
   const int bjl = 4 * (box & 3), bil = 8 * wv + 4 * (box >> 2);
   const int jl = bjl + (pp & 3), ilA = bil + (pp >> 2), ilB = ilA + 2;
@@ -2480,7 +2579,16 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
   const int fg = lane / kPartial, fq = lane - kPartial * (lane / kPartial);
   const bool fown = lane < kGroup * kPartial;
   float* const Lw = &L[fq][wv][0];
-  const float* const stage_rd = &s_stage[wv][(lane >> 3) << 3][lane & (GSR_BWD3P_HALFSTAGE ? 3 : 7)];   // + 8 * box
+  const float* const stage_rd = &s_stage[wv][0][0];
+  const int obox = grp8_out_box(lane);
+  float* const stage_wr = &s_stage[wv][obox][0];
+#if GSR_BWD3P_HALFSTAGE
+  // half h: sums 4h..4h+3 of every lane, compressed index 4 grp8_slot(l) + i (flat f -> ((f >> 3) << 2) | (f & 3))
+  const int wr0 = (4 * grp8_slot(lane)) ^ grp8h_swz(obox);
+  const int rdc = ((lane >> 3) << 2) | (lane & 3);
+#else
+  const int wr0 = (8 * grp8_slot(lane)) ^ grp8_swz(obox), wr1 = (8 * grp8_slot(lane) + 4) ^ grp8_swz(obox);
+#endif
   const unsigned char* my_list = s_box[wv][box];
   __syncthreads();
   // cull the chunk against the wave's 16x8 half-tile (exact test), survivors back to front
@@ -2534,12 +2642,22 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
     float acc[64];
     acc[63] = 0.f;
     const uint2 w8 = *reinterpret_cast<const uint2*>(my_list + gb);
+    int kk[kGroup];
+#pragma unroll
+    for (int g = 0; g < kGroup; ++g) kk[g] = (int)(((g < 4 ? w8.x : w8.y) >> (8 * (g & 3))) & 0xFFu);
+    float4 n0 = s_p[0][kk[0]], n1 = s_p[1][kk[0]], n2 = s_p[2][kk[0]];
 #pragma unroll
     for (int g = 0; g < kGroup; ++g) {
-      const int k = (int)(((g < 4 ? w8.x : w8.y) >> (8 * (g & 3))) & 0xFFu);
-      const float4 p0 = s_p[0][k];
-      const float4 p1 = s_p[1][k];
-      const float4 p2 = s_p[2][k];
+      const int k = kk[g];
+      const float4 p0 = n0;
+      const float4 p1 = n1;
+      const float4 p2 = n2;
+      if (g + 1 < kGroup) {   // entry g+1's record read before entry g is evaluated (GSR_BWD_PF)
+        n0 = s_p[0][kk[g + 1]];
+        n1 = s_p[1][kk[g + 1]];
+        n2 = s_p[2][kk[g + 1]];
+      }
+      walk_fence();
       const float dx = p0.x - px;
       // pixel A sets the entry's 9 sums, pixel B adds (no "0 + x" adds: k_raster2d_bwd_pair)
       float a0, a1, a2, a3, a4, a5, a6, a7, a8;
@@ -2584,31 +2702,45 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
       acc[g * kPartial + 8] = a8;
     }
     float sum[8];
-    reduce_box8(acc, sum);
-    float4* st = reinterpret_cast<float4*>(&s_stage[wv][lane][0]);
+    reduce_grp8(acc, sum);
 #if GSR_BWD3P_HALFSTAGE
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      st[0] = h == 0 ? make_float4(sum[0], sum[1], sum[2], sum[3]) : make_float4(sum[4], sum[5], sum[6], sum[7]);
+      *reinterpret_cast<float4*>(stage_wr + wr0) =
+          h == 0 ? make_float4(sum[0], sum[1], sum[2], sum[3]) : make_float4(sum[4], sum[5], sum[6], sum[7]);
       __builtin_amdgcn_wave_barrier();
-      if (fown && ((lane >> 2) & 1) == h) {
+      if (fown && ((lane >> 2) & 1) == h) {   // two batches of four boxes (lw_add)
 #pragma unroll
-        for (int bx = 0; bx < 8; ++bx) {
-          const int k = s_box[wv][bx][gb + fg];
-          Lw[k] += stage_rd[4 * bx];
+        for (int hb = 0; hb < 2; ++hb) {
+          int kb[4];
+          float vb4[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int bx = 4 * hb + j;
+            kb[j] = s_box[wv][bx][gb + fg];
+            vb4[j] = stage_rd[32 * bx + (rdc ^ grp8h_swz(bx))];
+          }
+          lw_add(Lw, kb, vb4);
         }
       }
       __builtin_amdgcn_wave_barrier();
     }
 #else
-    st[0] = make_float4(sum[0], sum[1], sum[2], sum[3]);
-    st[1] = make_float4(sum[4], sum[5], sum[6], sum[7]);
+    *reinterpret_cast<float4*>(stage_wr + wr0) = make_float4(sum[0], sum[1], sum[2], sum[3]);
+    *reinterpret_cast<float4*>(stage_wr + wr1) = make_float4(sum[4], sum[5], sum[6], sum[7]);
     __builtin_amdgcn_wave_barrier();
     if (fown) {
 #pragma unroll
-      for (int bx = 0; bx < 8; ++bx) {
-        const int k = s_box[wv][bx][gb + fg];
-        Lw[k] += stage_rd[8 * bx];
+      for (int hb = 0; hb < 2; ++hb) {
+        int kb[4];
+        float vb4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int bx = 4 * hb + j;
+          kb[j] = s_box[wv][bx][gb + fg];
+          vb4[j] = stage_rd[64 * bx + (lane ^ grp8_swz(bx))];
+        }
+        lw_add(Lw, kb, vb4);
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -2625,7 +2757,7 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
     v[0] = (2.f * p1.x * mx + p1.y * my) * conic_unscale<false>();   // (records: conic times log2(e))
     v[1] = (p1.y * mx + 2.f * p1.z * my) * conic_unscale<false>();
     v[5] = -v[5] / s_p[0][k].z;
-    store_partial_row(partial, kos_mine & kEmitIndexMask, v);
+    store_partial_row(partial, use_masks ? kos_mine & kEmitIndexMask : kos_mine, v);
   }
 }
 
@@ -2653,11 +2785,46 @@ __global__ void k_selftest_reduce_box16(float* out) {
   for (int i = 0; i < 4; ++i) out[4 * threadIdx.x + i] = s[i];
 }
 
+// reduce_grp16 / reduce_grp8 on the same pattern: out[G*l + i] = lane l's i-th sum (G = 4 / 8),
+// then per lane {walk box, position in it, output box, output slot} as floats at out[64 G + 4 l]
+template <int G>
+__global__ void k_selftest_reduce_grp(float* out) {
+  float v[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) v[i] = (float)((threadIdx.x * 7 + i * 13) % 97) + 0.25f * (float)i;
+  float s[G];
+  const int l = threadIdx.x;
+  int meta[4];
+  if constexpr (G == 4) {
+    reduce_grp16(v, s);
+    meta[0] = b128_group(l); meta[1] = grp16_pos(l); meta[2] = grp16_out_box(l); meta[3] = grp16_slot(l);
+  } else {
+    reduce_grp8(v, s);
+    meta[0] = grp8_box(l); meta[1] = grp8_pos(l); meta[2] = grp8_out_box(l); meta[3] = grp8_slot(l);
+  }
+#pragma unroll
+  for (int i = 0; i < G; ++i) out[G * l + i] = s[i];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) out[64 * G + 4 * l + i] = (float)meta[i];
+}
+
 }  // namespace gsr
 
 using namespace gsr;
 
 extern "C" {
+
+// Self-test of the b128-group-aligned box reductions (reduce_grp16 / reduce_grp8): see gsr.h.
+int gsr_selftest_reduce_grp(float* out, int box_lanes, void* stream) {
+  GSR_REQUIRE(box_lanes == 16 || box_lanes == 8, "gsr_selftest_reduce_grp: box_lanes must be 16 or 8, got %d",
+              box_lanes);
+  if (box_lanes == 16)
+    hipLaunchKernelGGL(k_selftest_reduce_grp<4>, dim3(1), dim3(64), 0, (hipStream_t)stream, out);
+  else
+    hipLaunchKernelGGL(k_selftest_reduce_grp<8>, dim3(1), dim3(64), 0, (hipStream_t)stream, out);
+  GSR_LAUNCH_CHECK("k_selftest_reduce_grp");
+  return GSR_OK;
+}
 
 
 // Self-test of the transposed wave reduction: out[l] = sum over lanes of v_lane[l] for the

@@ -84,6 +84,7 @@ EXPORTS = {
     "gsr_last_error": (ctypes.c_char_p, []),
     "gsr_selftest_reduce64": (ctypes.c_int, [_P, _P]),
     "gsr_selftest_reduce_box16": (ctypes.c_int, [_P, _P]),
+    "gsr_selftest_reduce_grp": (ctypes.c_int, [_P, ctypes.c_int, _P]),
     "gsr_set_fwd_lanes": (ctypes.c_int, [_I32]),
     "gsr_set_bwd_layout": (ctypes.c_int, [_I32]),
     "gsr_selftest_lds_order": (ctypes.c_int, [_P, _P]),

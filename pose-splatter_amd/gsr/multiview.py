@@ -278,6 +278,21 @@ class GradRows:
         from . import _lib
         self.cap = int(cap)
         self.block = torch.zeros(self.cap + 1, _lib.ROW_FLOATS, device=device, dtype=torch.float32)
+        # the exchange's buffers, kept across steps (stable addresses for a captured step, and no
+        # per-step allocation of world blocks + a dense [N,14]): see buffers()
+        self._gathered = None
+        self._out = None
+
+    def buffers(self, world: int, N: int):
+        """(gathered [world, cap+1, ROW_FLOATS], out [N, 14]) owned by this block, allocated on
+        first use and whenever world or N change; `out` is zeroed here on every call."""
+        dev = self.block.device
+        if self._gathered is None or self._gathered.shape[0] != world:
+            self._gathered = torch.empty((world,) + tuple(self.block.shape), device=dev, dtype=self.block.dtype)
+        if self._out is None or self._out.shape[0] != N:
+            self._out = torch.empty(N, 14, device=dev, dtype=torch.float32)
+        self._out.zero_()
+        return self._gathered, self._out
 
     def count(self) -> int:
         """Rows the last backward listed (a host read: diagnostics and capacity sizing only)."""
@@ -321,15 +336,16 @@ def rows_backward_units(render_band_rows: Callable, params: torch.Tensor, viewma
         _lib.check(L.gsr3d_touched_rows(None, None, None, None, None, 0, 0, grad_rows.cap, None,
                                         grad_rows.block.data_ptr(), stream), "gsr3d_touched_rows")
     blk = grad_rows.block
+    # the gathered blocks and the dense result live in grad_rows (reused every step: the returned
+    # tensor is overwritten by the next call -- clone it to keep it)
+    gathered, out = grad_rows.buffers(world, params.shape[0])
     if world > 1:
-        gathered = torch.empty((world,) + tuple(blk.shape), device=dev, dtype=blk.dtype)
         if dist.get_backend(group) == "nccl":
             dist.all_gather_into_tensor(gathered, blk, group=group)
         else:
             dist.all_gather(list(gathered.unbind(0)), blk, group=group)
     else:
         gathered = blk[None]
-    out = torch.zeros(params.shape[0], 14, device=dev, dtype=torch.float32)
     _lib.check(L.gsr_rows_scatter_add(gathered.data_ptr(), world, grad_rows.cap, out.data_ptr(), params.shape[0],
                                       None if status is None else status.data_ptr(), stream), "gsr_rows_scatter_add")
     return out

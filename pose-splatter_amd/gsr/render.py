@@ -27,12 +27,16 @@ Two capacity modes ("Threading / streams"):
   left bounds; exact otherwise (the first call of a shape, forward-only calls).  An eager
   ``model``-style training step then has no mid-forward host wait; the backward's check
   waits only for a forward that finished long before (the loss kernels run meanwhile).
+  The shape key of this mode leaves the Gaussian count out: pose-splatter's N changes on
+  almost every step (src/model.py:190-204), so the bounds come from the shape's previous
+  call at whatever N, its per-Gaussian counts scaled by N / N_prev (``_rescaled``).
 
 Intermediates live in two arenas per forward (see ``_Arena``).
 """
 from __future__ import annotations
 
 import collections
+import math
 import contextlib
 from dataclasses import dataclass, field
 
@@ -290,10 +294,28 @@ def _pinned_stats(device) -> torch.Tensor:
     return t
 
 
-def _hint_from(st) -> dict:
-    """Hint dict from the int32 words of a gsr_bin_stats (first 8 words)."""
+def _hint_from(st, N: int) -> dict:
+    """Hint dict from the int32 words of a gsr_bin_stats (first 8 words), observed at N Gaussians."""
     return {"I": (st[0] & 0xFFFFFFFF) | (st[1] << 32), "max_seg": st[2], "busy": st[3], "chunks": st[4],
-            "big": st[6], "mid": st[7]}
+            "big": st[6], "mid": st[7], "N": int(N)}
+
+
+# the hint quantities that grow with the Gaussian count (busy tiles and the sort-class counts are
+# capped by the call's tile count where they are used)
+_PER_N = ("I", "chunks", "max_seg", "busy", "big", "mid")
+
+
+def _rescaled(h: dict, N: int) -> dict:
+    """A hint observed at h["N"] Gaussians, restated for N (the "auto" mode's shape key leaves N
+    out: pose-splatter's Gaussian count changes on almost every step, src/model.py:190-204).
+    The per-Gaussian quantities scale by N / h["N"]; the device still checks every bound."""
+    n0 = int(h.get("N") or 0)
+    if n0 <= 0 or n0 == N:
+        return h
+    r = N / n0
+    out = {k: (int(math.ceil(v * r)) if k in _PER_N else v) for k, v in h.items()}
+    out["N"] = int(N)
+    return out
 
 
 def _capturing() -> bool:
@@ -302,10 +324,10 @@ def _capturing() -> bool:
 
 class _Monitor:
     """One bounded eager forward's stats, copied to pinned memory behind its kernels."""
-    __slots__ = ("key", "host", "event", "done")
+    __slots__ = ("key", "host", "event", "done", "N")
 
-    def __init__(self, key, host, event):
-        self.key, self.host, self.event, self.done = key, host, event, False
+    def __init__(self, key, host, event, N=0):
+        self.key, self.host, self.event, self.done, self.N = key, host, event, False, int(N)
 
 
 def _monitor_process(m: _Monitor) -> None:
@@ -322,10 +344,11 @@ def _monitor_process(m: _Monitor) -> None:
         raise CapacityOverflowError(f"gsr: a capacity-bounded render of this shape exceeded its bounds "
                                     f"({_lib.describe_overflow(ovf)}); its outputs and gradients were NaN -- the "
                                     "bounds are reset (the next call sizes exactly), re-run the step")
-    h = _hint_from(st)
+    h = _hint_from(st, m.N)
     old = _size_hint.get(m.key)
     if old is not None:   # keep bounds monotone over a window: shrink slowly, grow at once
-        h = {k: max(v, int(0.9 * old[k])) for k, v in h.items()}
+        old = _rescaled(old, m.N)   # (auto mode: the shape's previous observation at another N)
+        h = {k: (max(v, int(0.9 * old[k])) if k in _PER_N else v) for k, v in h.items()}
     _size_hint[m.key] = h
 
 
@@ -357,7 +380,7 @@ def _monitor_enqueue(b) -> None:
     host.copy_(b.pre.view("stats_dev", _I32), non_blocking=True)
     ev = torch.cuda.Event()
     ev.record()
-    b.monitor = _Monitor(b.key, host, ev)
+    b.monitor = _Monitor(b.key, host, ev, b.N)
     dq.append(b.monitor)
 
 
@@ -421,10 +444,15 @@ class _Bins:
         # the shape whose previous call bounds this one (band / unit grouping included: they
         # change the lists as much as the shape does)
         self.key = (str(device), C, N, width, height, key_extra)
+        mode = capacity or _capacity_default
+        if mode == "auto":
+            # the drop-in's mode: bounds from the previous call of the shape WHATEVER its N,
+            # rescaled to this N (_rescaled) -- the real caller's N changes on
+            # almost every step (src/model.py:190-204)
+            self.key = (str(device), C, "N*", width, height, key_extra)
         # 2D: the chunk list holds one backward unit per slot of the tile sweep (include/gsr.h ABI 7)
         self.min_units = self.CT + 8 if key_extra and key_extra[0] == "2d" else 0
         self.need_bwd = need_bwd   # False: no chunk records, no finalize (tile_end left raw)
-        mode = capacity or _capacity_default
         if mode not in _MODES:
             raise ValueError(f"capacity mode must be one of {_MODES}, got {mode!r}")
         self.bounded = False
@@ -439,7 +467,7 @@ class _Bins:
                 _monitor_check(self.key)
             hint = _size_hint.get(self.key)
             if hint is not None:
-                self._set_bounds(hint)
+                self._set_bounds(_rescaled(hint, N) if N > int(hint.get("N") or 0) else hint)
             elif _capturing():
                 raise RuntimeError("gsr: a bounded render captured in a graph needs bounds from an earlier call "
                                    "of the same shape (run one step before capturing)")
@@ -486,6 +514,7 @@ class _Bins:
             return
         hint = _size_hint.get(self.key)
         if hint is not None:
+            hint = _rescaled(hint, self.N)
             self.alloc_post(int(hint["I"] * 1.25) + 1024)
             if with_chunks:
                 self.alloc_chunks(int(hint["chunks"] * 1.25) + 16)
@@ -572,7 +601,7 @@ class _Bins:
         elif self.chunks is None:
             self.alloc_chunks(1)
         _size_hint[self.key] = {"I": self.n_isect, "chunks": self.n_chunks, "max_seg": self.max_seg,
-                                "busy": self.n_busy, "big": self.n_sort_big, "mid": self.n_sort_mid}
+                                "busy": self.n_busy, "big": self.n_sort_big, "mid": self.n_sort_mid, "N": self.N}
 
     def sort(self, order, stream):
         L = lib()
@@ -627,7 +656,7 @@ def last_stats() -> dict:
     call's are read from the device here, which synchronises)."""
     if _last_stats.pop("_lazy", False):
         b = _last_stats["_bins"]
-        h = _hint_from(b.pre.view("stats_dev", _I32)[:8].tolist())
+        h = _hint_from(b.pre.view("stats_dev", _I32)[:8].tolist(), b.N)
         _last_stats.update(n_isect=h["I"], max_seg=h["max_seg"], n_busy=h["busy"])
     return dict(_last_stats)
 

@@ -88,6 +88,87 @@ def test_graph_bounded_equals_exact_fullsize(cuda, idx):
     del graph
 
 
+def test_graph_bounded_equals_exact_cfg4_units(cuda):
+    """Config 4's timed mode at full size: render2d_units over F = 8 frames
+    x 6 views = 48 units of 500k Gaussians each (~115 M list entries), capacity-bounded and
+    captured in one HIP graph as bench.py times it, replayed twice (the second time after the
+    parameters moved in place) == the exact eager step, bitwise: rgb, alpha and the [8,N,9]
+    gradient.  Two units are also checked against the single-frame render2d of their frame
+    (rgb / alpha bitwise: the reference ignores the camera, src/gaussian_renderer.py:280-281),
+    and their frame's gradient against the sum of its six single-frame backward passes."""
+    from gsr import render as R
+    from gsr.scenes import CONFIGS, gaussians2d
+    c = CONFIGS[4]
+    F, C, W, H = 8, c.views, c.width, c.height
+    p0 = torch.stack([gaussians2d(c.N, W, H, c.seed + f) for f in range(F)]).to(cuda)
+    sets = [f for f in range(F) for _ in range(C)]
+    g = torch.Generator().manual_seed(c.seed + 1)
+    vr = torch.randn(F * C, H, W, 3, generator=g).to(cuda)
+    va = torch.randn(F * C, H, W, generator=g).to(cuda)
+    bg = torch.ones(3, device=cuda)
+
+    def eager(p, capacity):
+        pg = p.detach().clone().requires_grad_(True)
+        rgb, alpha = R.render2d_units(pg, sets, W, H, bg, capacity=capacity)
+        torch.autograd.backward([rgb, alpha], [vr, va])
+        return rgb.detach(), alpha.detach(), pg.grad
+
+    ref = eager(p0, "exact")
+    n_isect = R.last_stats()["n_isect"]
+    assert n_isect > 100_000_000, n_isect
+    params = p0.clone().requires_grad_(True)
+
+    def step():
+        params.grad = None
+        rgb, alpha = R.render2d_units(params, sets, W, H, bg, capacity="bounded")
+        torch.autograd.backward([rgb, alpha], [vr, va])
+        return rgb, alpha
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        g_rgb, g_alpha = step()
+    g_grad = params.grad
+    for k in range(2):
+        if k:
+            with torch.no_grad():
+                params.copy_(p0)
+                params[:, :, 0:2] += 0.05   # means (pixels) move in place between replays
+            ref = eager(params, "exact")
+        graph.replay()
+        torch.cuda.synchronize()
+        R.check_overflow(cuda)
+        assert torch.equal(ref[0], g_rgb), ("rgb", k)
+        assert torch.equal(ref[1], g_alpha), ("alpha", k)
+        assert torch.equal(ref[2], g_grad), ("v_params [8,N,9]", k)
+        print(f"[cfg4] replay {k}: 48 units, {n_isect} intersections: rgb/alpha/[8,N,9] gradient bitwise "
+              "equal to the exact eager step")
+    del graph
+    # units against the single-frame render of their frame (the last exact step's parameters)
+    p_last = params.detach()
+    for u in (0, 29):
+        f = sets[u]
+        with torch.no_grad():
+            rgb1, a1 = R.render2d(p_last[f].contiguous(), W, H, bg)
+        assert torch.equal(rgb1, ref[0][u]) and torch.equal(a1, ref[1][u]), u
+        gsum = torch.zeros_like(p_last[f])
+        for v in range(f * C, (f + 1) * C):
+            pg = p_last[f].clone().requires_grad_(True)
+            rgb1, a1 = R.render2d(pg, W, H, bg)
+            torch.autograd.backward([rgb1, a1], [vr[v], va[v]])
+            gsum += pg.grad
+        e = ref[2][f]
+        err = float((gsum - e).abs().max())
+        assert err <= 1e-5 * float(e.abs().max()) + 1e-7, (u, err, float(e.abs().max()))
+        print(f"[cfg4] unit {u} (frame {f}): rgb/alpha bitwise = render2d; frame gradient vs the sum of "
+              f"its {C} single-frame passes: max abs err {err:.3g} of max {float(e.abs().max()):.3g}")
+
+
 def _dropin_step(r, p, V, K, vr, va):
     pg = p.detach().clone().requires_grad_(True)
     rgb, alpha = r.render(pg, V, K)
@@ -161,6 +242,55 @@ def test_dropin_auto_overflow_raises_in_backward(cuda):
     torch.cuda.synchronize()
     assert torch.equal(got[0], ref[0]) and torch.equal(got[2].grad, ref[2].grad)
     assert torch.isfinite(got[2].grad).all()
+
+
+def test_dropin_auto_varying_n(cuda):
+    """pose-splatter's Gaussian count changes on almost every step (the threshold loops of
+    src/model.py:190-204 leave N anywhere in (min_n, max_n]).  The auto mode keys its bounds on
+    the shape WITHOUT N and rescales the previous call's counts to this N: over 10 steps with N
+    drawn from [1 024, 16 000] every call after the first is bounded, each result is bitwise
+    the exact-mode renderer's, and a forced overflow still raises inside backward() with .grad
+    untouched."""
+    from gsr import render as R
+    from src.gaussian_renderer import create_renderer
+    from gsr.scenes import gaussians3d, ring_cameras
+    W, H, C = 192, 170, 3
+    r = create_renderer("3d", W, H, device="cuda")
+    ex = create_renderer("3d", W, H, device="cuda", capacity="exact")
+    for rr in (r, ex):
+        rr.set_background_color(torch.ones(3, device=cuda))
+    pool = gaussians3d(16000, 51).to(cuda)
+    V, K = ring_cameras(C, W, H)
+    V, K = V.to(cuda), K.to(cuda)
+    g = torch.Generator().manual_seed(52)
+    vr = torch.randn(C, H, W, 3, generator=g).to(cuda)
+    va = torch.randn(C, H, W, generator=g).to(cuda)
+    ns = torch.randint(1024, 16001, (10,), generator=g).tolist()
+    for k, n in enumerate(ns):
+        got = _dropin_step(r, pool[:n], V, K, vr, va)
+        assert R.last_stats()["_bins"].bounded == (k > 0), (k, n)
+        ref = _dropin_step(ex, pool[:n], V, K, vr, va)
+        torch.cuda.synchronize()
+        assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]), (k, n)
+        assert torch.equal(got[2].grad, ref[2].grad), (k, n)
+    R.check_overflow(cuda)
+    print(f"[auto] N sequence {ns}: bounded after the first call, bitwise equal to exact")
+    (key,) = [k for k in R._size_hint if k[2] == "N*"]
+    h = dict(R._size_hint[key])
+    R._size_hint[key] = dict(h, I=max(1, h["I"] // 16), N=16000)
+    pg = pool.clone().requires_grad_(True)
+    rgb, alpha = r.render(pg, V, K)
+    assert R.last_stats()["_bins"].bounded
+    loss = (rgb * vr).sum() + (alpha * va).sum()
+    with pytest.raises(R.CapacityOverflowError):
+        loss.backward()
+    assert pg.grad is None
+    R.overflow_status(cuda, reset=True)
+    got = _dropin_step(r, pool, V, K, vr, va)   # bounds dropped: exact, and correct
+    assert not R.last_stats()["_bins"].bounded
+    ref = _dropin_step(ex, pool, V, K, vr, va)
+    torch.cuda.synchronize()
+    assert torch.equal(got[0], ref[0]) and torch.equal(got[2].grad, ref[2].grad)
 
 
 def test_kernel_timing_during_capture(cuda):

@@ -10,7 +10,9 @@ itself is exercised by tools/gpu_dist.sh and the driver's multi-GPU runs):
 * the rank-ordered scatter-add of the blocks equals ((0 + g_0) + g_1) + ... of the dense
   partial gradients, bitwise -- the sum a rank-ordered dense reduction gives, on every rank;
 * with one share covering everything, rows_backward_units equals the dense gradient bitwise;
-* a block too small for its share: NaN gradient and GSR_OVF_EXCHANGE in the sticky status.
+* a block too small for its share: NaN gradient and GSR_OVF_EXCHANGE in the sticky status;
+* a share whose bounded forward overflowed poisons the exchange the same way (its header is
+  set past the cap), so a captured step cannot sum a share that silently lacks its rows.
 """
 import pytest
 import torch
@@ -124,3 +126,44 @@ def test_rows_capacity_overflow_is_nan(cuda):
     assert torch.isnan(out).all()
     assert int(status.item()) & 64, _lib.describe_overflow(int(status.item()))
     R.overflow_status(cuda, reset=True)
+
+
+def test_rows_forward_overflow_poisons_exchange(cuda):
+    """A bounded band share whose forward overflowed: the raster backward skips its
+    rows, so gsr3d_touched_rows sets the block's header past the cap; the exchange then
+    NaN-fills and reports GSR_OVF_EXCHANGE -- the only signal a captured step has, where no
+    host check runs -- instead of a finite gradient without this rank's share."""
+    from gsr import _lib, render as R
+    from gsr.multiview import GradRows, unit_shard
+    p, V, K, W, H, vr, va = _scene(cuda)
+    N, C, th = p.shape[0], V.shape[0], (H + 15) // 16
+    v0, v1, band = unit_shard(C, th, 2, 1)
+    gr = GradRows(N, cuda)
+    bg = torch.ones(3, device=cuda)
+
+    def share(capacity):
+        pg = p.detach().clone().requires_grad_(True)
+        opts = R.RenderOptions3D(band=band, grad_rows=gr, capacity=capacity)
+        rgb, alpha = R.render3d(pg, V[v0:v1], K[v0:v1], W, H, bg, opts)
+        torch.autograd.backward([rgb, alpha], [vr[v0:v1], va[v0:v1]])
+        torch.cuda.synchronize()
+
+    share("exact")
+    good = gr.count()
+    assert 0 < good <= gr.cap
+    key = R.last_stats()["_bins"].key
+    h = dict(R._size_hint[key])
+    R._size_hint[key] = dict(h, I=h["I"] // 4)
+    try:
+        with pytest.raises(R.CapacityOverflowError):
+            share("bounded")   # eager: the backward's host check raises after enqueueing
+    finally:
+        R._size_hint[key] = h
+    assert gr.count() > gr.cap, (gr.count(), gr.cap)
+    status = torch.zeros(1, dtype=torch.int32, device=cuda)
+    out = _scatter(torch.stack([gr.block]), gr.cap, N, status)
+    assert torch.isnan(out).all()
+    assert int(status.item()) & 64, _lib.describe_overflow(int(status.item()))
+    R.overflow_status(cuda, reset=True)
+    share("exact")   # the next call is sized exactly and lists the rows again
+    assert gr.count() == good
