@@ -826,6 +826,45 @@ def time_steps(w: Workload, steps: int, warmup: int, dist=None, graph: bool = Fa
     return elapsed, breakdown, dom_name, ktimes.get(dom_name, (0.0, 0)) if dom_name else (0.0, 0)
 
 
+def time_eager(w, steps: int, dist=None) -> float:
+    """`steps` eager steps of the already warmed-up workload between barrier + synchronize
+    brackets (the slowest rank's time, via the caller's max over ranks)."""
+    dev = getattr(w, "dev", "cpu")
+    if dist is not None:
+        dist.barrier()
+    _sync(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        w.step()
+    _sync(dev)
+    if dist is not None:
+        dist.barrier()
+    _sync(dev)
+    return time.perf_counter() - t0
+
+
+def headline_timing(w, args, dist, dev, world: int, timer=None, eager_timer=None):
+    """The headline line's timing: `args.steps` steps in the run's launch mode (one HIP graph
+    of the timed steps at N=1 by default, eager launches at N>1, where the step's collectives
+    are not captured), max over ranks.  A graph-timed line ALSO times the same number of eager
+    steps right after, so the 1 -> N scaling curve can be read eager to eager (`value_eager`;
+    VERDICT r4 item 5): every line states its `launch_mode`."""
+    timer = timer or time_steps
+    eager_timer = eager_timer or time_eager
+    graph = bool(args.graph)
+    elapsed, breakdown, dom_name, dom = timer(w, args.steps, args.warmup, dist, graph=graph)
+    el_eager = eager_timer(w, args.steps, dist) if graph else elapsed
+    if world > 1:
+        t = torch.tensor([elapsed, el_eager], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, el_eager = (float(x) for x in t)
+    units = w.units_total * args.steps
+    timing = {"value": units / elapsed, "ms_per_step": 1000.0 * elapsed / args.steps,
+              "launch_mode": "graph" if graph else "eager",
+              "value_eager": units / el_eager, "ms_per_step_eager": 1000.0 * el_eager / args.steps}
+    return timing, elapsed, breakdown, dom_name, dom
+
+
 def allreduce_ms(nbytes: int, world: int) -> float:
     """Ring all-reduce cost model over xGMI: 2(n-1)/n * S per GPU at one link's bandwidth
     (a conservative bound: RCCL spreads rings over the 7 links of each MI355X)."""
@@ -921,7 +960,7 @@ def measure_layout(cfg, args, dev, world, rank, shard, dist, make_workload=None,
     out = {"value": w.units_total * args.steps / elapsed, "unit": "frames/s",
            "ms_per_step": 1000.0 * elapsed / args.steps, "scaling": w.scaling, "shard": shard,
            "units_per_step": w.units_total, "parallelism": w.layout,
-           "launch": "eager launches", "allreduce_ms": measure_allreduce_ms(w, dist, dev)}
+           "launch": "eager launches", "launch_mode": "eager", "allreduce_ms": measure_allreduce_ms(w, dist, dev)}
     del w
     if torch.device(dev).type == "cuda":
         torch.cuda.empty_cache()
@@ -1076,15 +1115,11 @@ def main(argv=None):
         if world > 1 or cfg.mode != "3d" or not cfg.backward or args.loss != "none":
             raise SystemExit("--split: 3D fwd+bwd configs on one GPU, loss none")
         w.split = args.split
-    elapsed, breakdown, dom_name, dom = time_steps(w, args.steps, args.warmup, dist, graph=bool(args.graph))
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+    timing, elapsed, breakdown, dom_name, dom = headline_timing(w, args, dist, dev, world)
 
     ar_ms = measure_allreduce_ms(w, dist, dev) if world > 1 else None
-    value = w.units_total * args.steps / elapsed
-    ms_per_step = 1000.0 * elapsed / args.steps
+    value = timing["value"]
+    ms_per_step = timing["ms_per_step"]
     roof, (C, P, I, I_eff) = roofline(w, dom_name, dom, args)
     sb = step_bytes(C, cfg.N, P, I, I_eff, w.p_dim, cfg.backward)
     launches_per_step = max(1, math.ceil(w.views_here / C)) if C else 1
@@ -1111,6 +1146,11 @@ def main(argv=None):
                    "split": w.split,
                    "parallelism": w.layout + (f"; backend {backend}" + (" (RCCL)" if backend == "nccl" else "")
                                               if backend else "")},
+        # the launch mode of this line and, for a graph-timed one, the same steps eager (the
+        # mode of the N > 1 lines): a 1 -> N curve compares value_eager with value_eager
+        "launch_mode": timing["launch_mode"],
+        "value_eager": timing["value_eager"],
+        "ms_per_step_eager": timing["ms_per_step_eager"],
         "roofline": roof,
         "kernels_ms": {k: round(v[0], 4) for k, v in sorted(breakdown.items())},
         "allreduce_ms": ar_ms,

@@ -141,6 +141,10 @@ def _layout_worker(rank, world, port, q):
             for sh in bench.other_layouts(cfg, shard):
                 res[(idx, bench.LAYOUT_KEY[sh])] = bench.measure_layout(cfg, args, "cpu", world, rank, sh, dist,
                                                                         make_workload=FakeWorkload, timer=timer)
+        # the headline line's timing at N > 1: eager (graph off by default there), value_eager = value
+        hargs = bench.parse(["--steps", "3", "--warmup", "1", "--graph", "0"])
+        w = FakeWorkload(CONFIGS[3], "cpu", world, rank, "views", 1, "none", True, 0.3, "dense")
+        res["headline"] = bench.headline_timing(w, hargs, dist, "cpu", world, timer=timer)[0]
         if rank == 0:
             q.put(res)
     finally:
@@ -175,4 +179,32 @@ def test_other_layouts_reported_gloo_world2():
     assert strong["units_per_step"] == CONFIGS[3].views
     owners = res[(4, "frame_owners")]
     assert owners["value"] > 0 and owners["allreduce_ms"] is None   # no Gaussian-gradient collective
-    assert set(strong) >= {"value", "ms_per_step", "allreduce_ms", "parallelism", "scaling"}
+    assert set(strong) >= {"value", "ms_per_step", "allreduce_ms", "parallelism", "scaling", "launch_mode"}
+    assert strong["launch_mode"] == owners["launch_mode"] == "eager"
+    head = res["headline"]   # every line states its launch mode
+    assert head["launch_mode"] == "eager" and head["value_eager"] == head["value"] > 0
+    assert head["ms_per_step_eager"] == head["ms_per_step"]
+
+
+def test_headline_graph_line_reports_eager_too():
+    """A graph-timed N = 1 line also reports the same steps eager (value_eager), so the driver's
+    1 -> N curve can divide eager by eager."""
+    class W:
+        units_total = 6
+
+    calls = []
+
+    def timer(w, steps, warmup, dist_, graph=False):
+        calls.append(("timer", graph))
+        return 0.010 * steps, {}, None, (0.0, 0)
+
+    def eager_timer(w, steps, dist_):
+        calls.append(("eager", steps))
+        return 0.012 * steps
+
+    args = bench.parse(["--steps", "4", "--warmup", "1", "--graph", "1"])
+    t = bench.headline_timing(W(), args, None, "cpu", 1, timer=timer, eager_timer=eager_timer)[0]
+    assert calls == [("timer", True), ("eager", 4)]
+    assert t["launch_mode"] == "graph"
+    assert abs(t["ms_per_step"] - 10.0) < 1e-9 and abs(t["ms_per_step_eager"] - 12.0) < 1e-9
+    assert abs(t["value"] - 600.0) < 1e-6 and abs(t["value_eager"] - 500.0) < 1e-6
