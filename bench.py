@@ -164,12 +164,18 @@ def algorithmic_bytes(kernel: str, C: int, N: int, P: int, I: int, I_eff: int, p
     return 0.0
 
 
-def step_bytes(C: int, N: int, P: int, I: int, I_eff: int, p: int, backward: bool = True) -> float:
+def step_bytes(C: int, N: int, P: int, I: int, I_eff: int, p: int, backward: bool = True, sets: int | None = None) -> float:
     """Whole launch sequence, SURVEY.md §8(d) (P = all pixels of the C units):
-    fwd+bwd C*N*(12p+136) + 36*I + 80*I_eff + 44*P; fwd-only C*N*(4p+32) + 36*I + 40*I_eff + 20*P."""
+    fwd+bwd C*N*(12p+136) + 36*I + 80*I_eff + 44*P; fwd-only C*N*(4p+32) + 36*I + 40*I_eff + 20*P.
+    sets: the projections the sequence runs when fewer than C (2D: one per parameter set, the
+    frames of the units -- VERDICT r4: config 4 charged its 8 frames' projection 48 times).  The
+    per-projection part (params read, record written, params read again, gradient written:
+    N*(12p+64)) is then charged `sets` times; the per-(unit, Gaussian) reduced rows (72 B: written
+    by the raster backward, read by the projection backward) still C times."""
+    S = C if sets is None else sets
     if not backward:
-        return C * N * (4.0 * p + 32.0) + 36.0 * I + 40.0 * I_eff + 20.0 * P
-    return C * N * (12.0 * p + 136.0) + 36.0 * I + 80.0 * I_eff + 44.0 * P
+        return S * N * (4.0 * p + 32.0) + 36.0 * I + 40.0 * I_eff + 20.0 * P
+    return S * N * (12.0 * p + 64.0) + C * N * 72.0 + 36.0 * I + 80.0 * I_eff + 44.0 * P
 
 
 # libgsr call name (render.py timing brackets) -> substring of its dominant kernel's symbol
@@ -745,6 +751,15 @@ class Workload:
             ls = ssim_lambda * (1 - _torch_ssim(self.timg, rgb.permute(0, 3, 1, 2)))
         (li + lm + ls).backward()
 
+    def sets_per_launch(self, C: int):
+        """Projections one launch sequence runs: 3D one per camera (C); 2D one per parameter set
+        (the frames among this rank's units, split over its buckets)."""
+        if self.cfg.mode != "2d":
+            return C
+        frames = len({f for f, _ in self.units})
+        nb = self.buckets if self.comm else 1
+        return max(1, math.ceil(frames / max(nb, 1)))
+
     def launch_shape(self):
         """(C, P) of the dominant launch sequence: cameras and pixels one launch covers."""
         cfg = self.cfg
@@ -1121,7 +1136,7 @@ def main(argv=None):
     value = timing["value"]
     ms_per_step = timing["ms_per_step"]
     roof, (C, P, I, I_eff) = roofline(w, dom_name, dom, args)
-    sb = step_bytes(C, cfg.N, P, I, I_eff, w.p_dim, cfg.backward)
+    sb = step_bytes(C, cfg.N, P, I, I_eff, w.p_dim, cfg.backward, sets=w.sets_per_launch(C))
     launches_per_step = max(1, math.ceil(w.views_here / C)) if C else 1
     out = {
         "metric": "rendered frames/sec (%s) at N_gauss x H x W" % ("fwd+bwd" if cfg.backward else "fwd"),
@@ -1159,7 +1174,8 @@ def main(argv=None):
         "step_roofline": {"algorithmic_bytes": sb * launches_per_step,
                           "achieved": sb * launches_per_step / (ms_per_step * 1e-3) / 1e9,
                           "unit": "GB/s", "frac": sb * launches_per_step / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                          "formula": ("SURVEY.md 8(d): C*N*(12p+136) + 36*I + 80*I_eff + 44*P per rank" if cfg.backward
+                          "formula": ("SURVEY.md 8(d): S*N*(12p+64) + C*N*72 + 36*I + 80*I_eff + 44*P per rank "
+                                      "(S = projections: C in 3D, the frames in 2D)" if cfg.backward
                                       else "SURVEY.md 8(d) fwd-only: C*N*(4p+32) + 36*I + 40*I_eff + 20*P per rank")},
         "binning": {"I": I, "I_eff": I_eff, "max_list": R.last_stats().get("max_seg"),
                     "busy_tiles": R.last_stats().get("n_busy"), "tiles": R.last_stats().get("tiles")},

@@ -61,6 +61,10 @@ def test_linear_fit_and_psnr():
 def test_byte_formulas_and_allreduce_model():
     # §8(d): fwd+bwd per view N(12p+136) + 36 I + 80 I_eff + 44 P
     assert bench.step_bytes(1, 10, 100, 7, 5, 14) == 10 * (12 * 14 + 136) + 36 * 7 + 80 * 5 + 44 * 100
+    # 2D: the projection charged once per parameter set (frame), the rows per unit
+    assert bench.step_bytes(48, 10, 100, 7, 5, 9, sets=8) == (8 * 10 * (12 * 9 + 64) + 48 * 10 * 72 + 36 * 7
+                                                              + 80 * 5 + 44 * 100)
+    assert bench.step_bytes(6, 10, 100, 7, 5, 14, sets=6) == bench.step_bytes(6, 10, 100, 7, 5, 14)
     assert bench.step_bytes(1, 10, 100, 7, 5, 14, backward=False) == 10 * (4 * 14 + 32) + 36 * 7 + 40 * 5 + 20 * 100
     assert bench.algorithmic_bytes("raster3d_bwd", 6, 10, 100, 7, 5, 14) == 24 * 100 + 40 * 5 + 36 * 6 * 10
     assert bench.allreduce_ms(1000, 1) == 0.0
