@@ -115,7 +115,9 @@ typedef struct gsr_bin_stats {
   int32_t* status;     /* copy of caps->status (device; may be NULL)                  */
   int32_t n_sort_long; /* tiles with lists >= 1024 entries (the sort's one-workgroup lists) */
   int32_t masks;       /* 1: the emission stored 3D quadrant masks in k_of_s (gsr_bin_emit rec) */
-  int64_t reserved;
+  int32_t n_heavy;     /* busy tiles with lists >= 2^k entries, k = gsr_set_fwd_heavy (0 if off): the
+                          first of the busy order, rendered by the 3D forward's heavy-tile layout */
+  int32_t reserved;
 } gsr_bin_stats;       /* 80 bytes; written by gsr_bin_offsets                         */
 
 /* Upper bounds for a call that does not read stats back (gsr_bin_offsets).  The caller sizes
@@ -194,6 +196,15 @@ int gsr_set_fwd_lanes(int lanes);
  * with a fused loss or multi-chunk units always run one pixel per lane.  The layouts sum the
  * pixels' terms in different orders (fp32 regrouping); each is deterministic. */
 int gsr_set_bwd_layout(int layout);
+
+/* Heavy-tile split of the 3D raster forward (process-wide; additive to revision 12): busy tiles
+ * whose lists have at least 2^log2_min_len entries (at most 64 of them, the first of the busy
+ * order) are rendered in an 8-wave, 8-lanes-per-pixel layout with 512-entry rounds on a side
+ * stream, forked from and joined into the call's stream, while the quad layout renders the
+ * others.  log2_min_len 0 turns it off; 6..30 sets the threshold (default 12: 4096 entries).
+ * Takes effect at the next gsr_bin_offsets (which counts the tiles, gsr_bin_stats.n_heavy).
+ * Same results as the quad layout up to fp32 regrouping of the transmittance products. */
+int gsr_set_fwd_heavy(int log2_min_len);
 
 /* Self-test of the lane-ordered LDS atomics the tile sort's ranking relies on: writes the
  * number of violations (0 expected) to the device int *violations. */

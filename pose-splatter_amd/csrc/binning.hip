@@ -81,7 +81,7 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(int32_t* __restrict__
                                                           int32_t* __restrict__ tile_end,
                                                           uint64_t* __restrict__ tile_cut,
                                                           const gsr_bin_caps caps,
-                                                          gsr_bin_stats* __restrict__ stats) {
+                                                          gsr_bin_stats* __restrict__ stats, int heavy_log2) {
   constexpr int NW = kTopThreads / 64;
   __shared__ int s_w[3][NW];
   __shared__ int s_max;
@@ -160,6 +160,9 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(int32_t* __restrict__
     // lists >= 1024 (kWaveSortKeys, buckets >= 10: lanes < 22) take one workgroup each
     const int n_big = __builtin_amdgcn_readlane(ex, 19), n_mid = __builtin_amdgcn_readlane(bk, 19),
               n_long = __builtin_amdgcn_readlane(ex, 22);
+    // heavy tiles of the 3D forward (gsr_set_fwd_heavy): lists >= 2^k, i.e. buckets >= k, whose
+    // count is the start of bucket k - 1 (lane 32 - k)
+    const int n_heavy = heavy_log2 > 0 ? __builtin_amdgcn_readlane(ex, 32 - heavy_log2) : 0;
     if (l == 0) {
       const int n_busy = (int)CT - te;
       s_n_busy = n_busy;
@@ -174,6 +177,8 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(int32_t* __restrict__
       stats->n_chunks = tk;
       stats->n_active = 0;
       stats->masks = 0;   // set by an emission that stores quadrant masks
+      stats->n_heavy = n_heavy;
+      stats->reserved = 0;
       // bounded call: the caller sized the intersection / chunk buffers without reading I back
       int ovf = 0;
       if (caps.isect > 0 && (int64_t)tc > caps.isect) ovf |= GSR_OVF_ISECT;
@@ -1403,7 +1408,7 @@ int gsr_bin_offsets(int32_t* tile_count, int64_t CT, int32_t* tile_offset, int32
               "gsr_bin_offsets: chunk_entries %d is not 0 or a power of two in [%d, 2^20]", ce, kChunkEntries);
   const size_t lds = CT <= kScanLdsTiles ? (size_t)CT * sizeof(int) : 0;
   hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kTopThreads), lds, (hipStream_t)stream, tile_count, CT, tile_offset,
-                     chunk_base, busy_tiles, tile_end, tile_cut, cp, stats);
+                     chunk_base, busy_tiles, tile_end, tile_cut, cp, stats, g_fwd_heavy_log2);
   GSR_LAUNCH_CHECK("k_tile_scan");
   return GSR_OK;
 }

@@ -335,6 +335,10 @@ __device__ __forceinline__ int grp8h_swz(int box) { return (box & 3) << 3; }
 
 __device__ __forceinline__ unsigned long long wave_ballot(bool p) { return __ballot(p); }
 
+// gsr_set_fwd_heavy (raster.hip): the 3D forward's heavy-tile threshold, log2 of the list length
+// (0: off); the tile scan (binning.hip) counts those tiles into gsr_bin_stats.n_heavy
+extern int g_fwd_heavy_log2;
+
 // Block-wide exclusive scan of one int per thread (NT threads, multiple of 64).
 // s_tmp must hold NT/64 + 1 ints.  Returns the exclusive prefix; *total = block sum.
 template <int NT>

@@ -12,6 +12,8 @@
 // gradients are bitwise deterministic.
 #include "gsr_common.h"
 
+#include <type_traits>
+
 namespace gsr {
 
 
@@ -27,6 +29,10 @@ constexpr int kFwdLdsPad = GSR_FWD_PAD_3D;
 #endif
 constexpr int kFwdLdsPad2D = GSR_FWD_PAD_2D;
 static int g_fwd_lanes = 0;   // gsr_set_fwd_lanes: 0 automatic, 1 / 4 / 16 forced
+#ifndef GSR_FWD_HEAVY_LOG2
+#define GSR_FWD_HEAVY_LOG2 12   // default heavy-tile threshold: lists of >= 4096 entries; 0 = off
+#endif
+int g_fwd_heavy_log2 = GSR_FWD_HEAVY_LOG2;   // gsr_set_fwd_heavy (gsr_common.h)
 static int g_bwd_layout = 0;  // gsr_set_bwd_layout: 0 automatic, 1 chunk kernel, 2 pixel pairs (3D)
 // box forward (k_raster_fwd_box) build knobs, for A/B measurements: lanes grouped by box along
 // the ds_read_b128 lane groups, and the 2D walk's records packed into 2 x b128 + b32
@@ -302,19 +308,72 @@ struct PixGroup<16> {
   static __device__ __forceinline__ float next(float v) { return dpp_mov<0x101>(v); }
 };
 
-// Forward geometry per lanes-per-pixel: LPP 4 -> 4 workgroups per tile (8x8 quadrants), waves
-// of 4x4 pixels; LPP 16 -> 16 workgroups per tile (4x4 boxes), waves of 2x2 pixels (the
-// latency mode: a quarter of the serial chain, for scenes with few busy tiles).
-template <int LPP>
+// 8 lanes per pixel (the heavy-tile forward, k_raster_fwd<false, 8, 8>): a half row of DPP
+template <>
+struct PixGroup<8> {
+  static __device__ __forceinline__ int min_i(int v) {
+    v = quad_min_i(v);
+    return min(v, dpp_i<0x141>(v));   // row_half_mirror: lane i <-> 7 - i of its half row
+  }
+  static __device__ __forceinline__ int max_i(int v) {
+    v = quad_max_i(v);
+    return max(v, dpp_i<0x141>(v));
+  }
+  static __device__ __forceinline__ float sum(float v) {
+    v = quad_sum(v);
+    return v + dpp_mov<0x141>(v);
+  }
+  static __device__ __forceinline__ void prefix(float x, int q, float& Q, float& P) {
+    float y = x, d;
+    d = dpp_mov<0x111>(y); y *= (q >= 1 ? d : 1.f);   // row_shr:1 (lane - 1)
+    d = dpp_mov<0x112>(y); y *= (q >= 2 ? d : 1.f);
+    d = dpp_mov<0x114>(y); y *= (q >= 4 ? d : 1.f);
+    Q = y;
+    d = dpp_mov<0x111>(y);
+    P = q >= 1 ? d : 1.f;
+  }
+  static __device__ __forceinline__ float suffix_excl(float v, int q) {
+    float y = v, d;
+    d = dpp_mov<0x101>(y); y += (q < 7 ? d : 0.f);   // row_shl:1 (lane + 1)
+    d = dpp_mov<0x102>(y); y += (q < 6 ? d : 0.f);
+    d = dpp_mov<0x104>(y); y += (q < 4 ? d : 0.f);
+    d = dpp_mov<0x101>(y);
+    return q < 7 ? d : 0.f;
+  }
+  static __device__ __forceinline__ float next(float v) { return dpp_mov<0x101>(v); }
+};
+
+// Forward geometry per lanes-per-pixel and waves per workgroup: LPP 4 -> 4 workgroups per tile
+// (8x8 quadrants), waves of 4x4 pixels; LPP 16 -> 16 workgroups per tile (4x4 boxes), waves of
+// 2x2 pixels (the latency mode: a quarter of the serial chain, for scenes with few busy tiles);
+// LPP 8 with 8 waves (the heavy-tile forward) -> 4 workgroups per tile (8x8 quadrants), waves
+// of 4x2 pixels and rounds of 512 list entries (half the rounds of the quad layout).
+template <int LPP, int NW = 4>
 struct FwdShape {
-  static constexpr int G = LPP == 4 ? 4 : 16;   // workgroups per tile
-  static constexpr int WB = LPP == 4 ? 8 : 4;   // workgroup box side
-  static constexpr int VB = WB / 2;             // wave box side
-  static_assert(VB * VB * LPP == 64, "a wave is VB x VB pixels x LPP lanes");
+  static constexpr int G = LPP == 16 ? 16 : 4;         // workgroups per tile
+  static constexpr int WB = LPP == 16 ? 4 : 8;         // workgroup box side
+  static constexpr int VBX = LPP == 16 ? 2 : 4;        // wave box width
+  static constexpr int VBY = 64 / LPP / VBX;           // wave box height
+  static constexpr int WPR = WB / VBX;                 // wave boxes per row of the workgroup box
+  static_assert(VBX * VBY * LPP == 64, "a wave is VBX x VBY pixels x LPP lanes");
+  static_assert(NW * VBX * VBY == WB * WB, "the waves tile the workgroup box");
 };
 // workgroups for the busy tiles: G per tile, rounded up to whole groups of 8 tiles
-template <int LPP>
-__host__ __device__ __forceinline__ int busy_grid(int n_busy) { return 8 * FwdShape<LPP>::G * ((n_busy + 7) / 8); }
+template <int LPP, int NW = 4>
+__host__ __device__ __forceinline__ int busy_grid(int n_busy) { return 8 * FwdShape<LPP, NW>::G * ((n_busy + 7) / 8); }
+// Heavy tiles (GSR_FWD_HEAVY): the first busy tiles of the visit order whose lists have at least
+// 2^kFwdHeavyLog2 entries, at most kFwdHeavyMax of them, run the 8-wave forward on a side stream
+// (forked and joined inside gsr3d_raster_fwd) while the quad forward takes the others.  Their
+// walks set the quad forward's span (r04_fwd_phase_trace_cfg3.txt: ~12-17 workgroups of 20-22
+// rounds from t ~ 0 to the end); 512-entry rounds halve the rounds, each gathered and culled by 8
+// waves in parallel.
+#ifndef GSR_FWD_HEAVY_MAX
+#define GSR_FWD_HEAVY_MAX 64
+#endif
+constexpr int kFwdHeavyMax = GSR_FWD_HEAVY_MAX;
+__device__ __forceinline__ int fwd_heavy_count(const gsr_bin_stats* stats) {
+  return min(min(stats->n_heavy, stats->n_busy), kFwdHeavyMax);
+}
 
 // slot of tile pixel (il, jl) in a chunk record: box-major inside the 8x8 quadrant wv,
 // 64 * wv + 16 * box + pos (pos = pixel within its 4x4 box).  The quad forward writes one 4x4
@@ -393,8 +452,10 @@ extern "C" int gsr_debug_fwd_trace(void* buf) {
 #ifndef GSR_FWD_MINB
 #define GSR_FWD_MINB 6
 #endif
-template <bool IS2D, int LPP>
-__global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MINB) void k_raster_fwd(
+// NW: waves per workgroup (4; 8 for the heavy-tile variant, LPP 8).  part: 0 every busy tile,
+// 1 the busy tiles past the heavy ones (fwd_heavy_count), 2 the heavy ones only.
+template <bool IS2D, int LPP, int NW = 4>
+__global__ __launch_bounds__(NW * 64, (IS2D || LPP != 4) ? 1 : GSR_FWD_MINB) void k_raster_fwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ kos,
     const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ order, int W, int H, int tw, int th, const float* __restrict__ bg,
@@ -402,10 +463,12 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
     int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end, float4* __restrict__ ckpt,
     const int32_t* __restrict__ chunk_base, int n_busy, int64_t CT,
     uint64_t* __restrict__ tile_cut, float cut2d, const FwdLazy lz, const gsr_bin_stats* __restrict__ stats,
-    const Sets2D sets) {
+    const Sets2D sets, int part = 0) {
   static_assert(!IS2D || LPP == 4, "2D walks per wave with quads");
+  static_assert(NW == 4 || (NW == 8 && !IS2D && LPP == 8), "8 waves: the 3D heavy-tile layout");
   using PG = PixGroup<LPP>;
-  using FS = FwdShape<LPP>;
+  using FS = FwdShape<LPP, NW>;
+  constexpr int NT = NW * 64;   // threads; a 3D round gathers NT list entries
   __shared__ int s_max;
 #ifdef GSR_FWD_TRACE
   __shared__ unsigned long long s_ftr[4];
@@ -416,7 +479,7 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
 #endif
   // n_busy sizes the grid (the read-back busy count or a bound); the tiles come from the device
   // count, which the sort has checked against that bound (GSR_OVF_BUSY)
-  const int busy_blocks = busy_grid<LPP>(n_busy);
+  const int busy_blocks = busy_grid<LPP, NW>(n_busy);
   // XCD-aware mapping: workgroups are dealt to the 8 XCDs round-robin by id, so the G
   // workgroups of a tile get ids 8G*k + 8*sub + x (same id mod 8): they share one XCD's L2
   // for the tile's records.  Busy tile u = 8k + x, in longest-first order.
@@ -439,27 +502,33 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
     n_busy = min(n_busy, nb_dev);
   } else {
     n_busy = nb_dev;
-    if ((int)blockIdx.x >= busy_blocks) {
-      fill_empty<IS2D>(order, tile_offset, n_busy, busy_blocks, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
-                       out_last, tile_end, tile_cut);
-      return;
+    if constexpr (NW == 4) {
+      if ((int)blockIdx.x >= busy_blocks) {
+        fill_empty<IS2D>(order, tile_offset, n_busy, busy_blocks, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
+                         out_last, tile_end, tile_cut);
+        return;
+      }
     }
   }
   if (u >= n_busy) return;
+  if (part != 0) {   // the heavy / light split of one forward (never in a lazy re-render)
+    const int nh = fwd_heavy_count(stats);
+    if (part == 1 ? u < nh : u >= nh) return;
+  }
   int c, ty, tx;
   tile_coords(ct, tw, th, c, ty, tx);
   if constexpr (IS2D) rec += rec_offset2d(sets.begin, sets.F, c, sets.N);   // the set's record copy
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int q = lane & (LPP - 1), p = lane / LPP;
   const int sx = (sub % (kTile / FS::WB)) * FS::WB, sy = (sub / (kTile / FS::WB)) * FS::WB;
-  const int ox = sx + (wv & 1) * FS::VB, oy = sy + (wv >> 1) * FS::VB;
-  const int il = oy + p / FS::VB, jl = ox + p % FS::VB;
+  const int ox = sx + (wv % FS::WPR) * FS::VBX, oy = sy + (wv / FS::WPR) * FS::VBY;
+  const int il = oy + p / FS::VBX, jl = ox + p % FS::VBX;
   const int i = ty * kTile + il, j = tx * kTile + jl;
   const bool inside = i < H && j < W;
   const float off = IS2D ? 0.f : 0.5f;   // 2D: integer centres (src/gaussian_renderer.py:355-358)
   const float px = (float)j + off, py = (float)i + off;
-  const float bx0 = (float)(tx * kTile + ox) + off, bx1 = bx0 + (float)(FS::VB - 1);
-  const float by0 = (float)(ty * kTile + oy) + off, by1 = by0 + (float)(FS::VB - 1);
+  const float bx0 = (float)(tx * kTile + ox) + off, bx1 = bx0 + (float)(FS::VBX - 1);
+  const float by0 = (float)(ty * kTile + oy) + off, by1 = by0 + (float)(FS::VBY - 1);
   const int start = tile_offset[ct], list_end = tile_offset[ct + 1];
   const int end = lz.tile_sorted && !lz.rerun ? lz.tile_sorted[ct] : list_end;
   if (threadIdx.x == 0) s_max = -1;
@@ -476,10 +545,11 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
   float Ts = 1.f, dr = 0.f, dg = 0.f, db = 0.f;   // dr..: this lane's share of the chunk's colour
   if constexpr (!IS2D) {
   // one array (records of slot i at s_q[buf][0..2][i]): one address, immediate offsets
-  __shared__ float4 s_q[2][3][256];
-  __shared__ unsigned char s_qe[2][256];   // entry - round base (LDS: 6 workgroups per CU)
-  __shared__ int s_qn[2][4];
-  __shared__ unsigned char s_l[4][128];
+  using QIdx = typename std::conditional<(NT > 256), unsigned short, unsigned char>::type;
+  __shared__ float4 s_q[2][3][NT];
+  __shared__ QIdx s_qe[2][NT];   // entry - round base (LDS: 6 workgroups per CU at 4 waves)
+  __shared__ int s_qn[2][NW];
+  __shared__ QIdx s_l[NW][128];
   // 3D -- shared rounds: the quadrant workgroup walks the list in 256-entry rounds; wave w gathers
   // entries 64w..64w+63 of the round (one round ahead), culls them against the 8x8 quadrant
   // and writes its survivors to segment w of a double-buffered LDS queue; after ONE barrier
@@ -499,7 +569,7 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
   int idn = 0;
   bool ucur = false, un = false;
   if (end > start) {
-    const int e0 = min(start + 64 * wv + lane, e_last), e1 = min(start + 256 + 64 * wv + lane, e_last);
+    const int e0 = min(start + 64 * wv + lane, e_last), e1 = min(start + NT + 64 * wv + lane, e_last);
     const int id0 = ids[e0];
     idn = ids[e1];
     ucur = kos == nullptr || ((kos[e0] >> qbit) & 1);
@@ -510,7 +580,7 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
     }
   }
   int buf = 0;
-  for (int rb = start; rb < end; rb += 256, buf ^= 1) {
+  for (int rb = start; rb < end; rb += NT, buf ^= 1) {
 #ifdef GSR_FWD_TRACE
     if (threadIdx.x == 0) f_t = wall_clock64();
 #endif
@@ -524,12 +594,12 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
         s_q[buf][0][slot] = c0;
         s_q[buf][1][slot] = c1;
         s_q[buf][2][slot] = c2;
-        s_qe[buf][slot] = (unsigned char)(64 * wv + lane);   // e - rb
+        s_qe[buf][slot] = (QIdx)(64 * wv + lane);   // e - rb
       }
       if (lane == 0) s_qn[buf][wv] = __popcll(m);
       const int id_use = idn;
       ucur = un;
-      const int e2 = min(rb + 512 + 64 * wv + lane, e_last);
+      const int e2 = min(rb + 2 * NT + 64 * wv + lane, e_last);
       idn = ids[e2];
       un = kos == nullptr || ((kos[e2] >> qbit) & 1);
       if (ucur) {
@@ -543,7 +613,7 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
 #ifdef GSR_FWD_TRACE
     if (n_rounds++ == 0) FWD_T(1);
 #endif
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < NT / 128; ++h) {
       const int hb = rb + 128 * h;
       if (hb >= end || __ballot(!done) == 0ull) break;
       if (hb > start && ((hb - start) & umask) == 0) {   // entering chunk kcur+1
@@ -565,7 +635,7 @@ __global__ __launch_bounds__(kRasterThreads, (IS2D || LPP != 4) ? 1 : GSR_FWD_MI
         const unsigned long long m = __ballot(keep);
         if (keep)
           s_l[wv][n + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] =
-              (unsigned char)idx;
+              (QIdx)idx;
         n += __popcll(m);
       }
       __builtin_amdgcn_wave_barrier();
@@ -2844,6 +2914,13 @@ int gsr_set_fwd_lanes(int lanes) {
   return GSR_OK;
 }
 
+int gsr_set_fwd_heavy(int log2_min_len) {
+  GSR_REQUIRE(log2_min_len == 0 || (log2_min_len >= 6 && log2_min_len <= 30),
+              "gsr_set_fwd_heavy: log2_min_len must be 0 (off) or 6..30, got %d", log2_min_len);
+  gsr::g_fwd_heavy_log2 = log2_min_len;
+  return GSR_OK;
+}
+
 int gsr_set_bwd_layout(int layout) {
   GSR_REQUIRE(layout >= 0 && layout <= 2, "gsr_set_bwd_layout: layout must be 0 (auto), 1 or 2, got %d", layout);
   gsr::g_bwd_layout = layout;
@@ -2873,6 +2950,34 @@ static int fwd_lanes(bool is2d, int n_busy) {
   if (g_fwd_lanes == 1 || g_fwd_lanes == 4 || (g_fwd_lanes == 16 && !is2d)) return g_fwd_lanes;
   if (is2d) return 1;
   return n_busy <= kFwd16MaxBusy ? 16 : 4;
+}
+
+// The heavy-tile forward's side stream and its fork / join events, one set per (host thread,
+// device): created on first use (before any graph capture: a bounded call, the only kind that
+// is captured, always follows an eager call of its shape), at the device's highest stream
+// priority so the heavy workgroups are dispatched ahead of the quad forward's.  The fork / join
+// are stream-ordered event waits, so a captured forward holds the two launches as parallel
+// branches of its graph.
+struct FwdSide {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  bool ok = false, tried = false;
+};
+static FwdSide* fwd_side() {
+  static thread_local FwdSide sides[16];
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 16) return nullptr;
+  FwdSide& x = sides[d];
+  if (!x.tried) {
+    x.tried = true;
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+    x.ok = hipStreamCreateWithPriority(&x.s, hipStreamNonBlocking, greatest) == hipSuccess &&
+           hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&x.join, hipEventDisableTiming) == hipSuccess;
+    if (!x.ok) (void)hipGetLastError();
+  }
+  return x.ok ? &x : nullptr;
 }
 
 // Shared by the 3D and 2D entry points (2D: C = 1, index-order keys, final_T [H,W,2]).
@@ -2908,10 +3013,28 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
                        width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state,
                        chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz, stats, sets);
   } else if (lanes == 4) {
+    // 3D: the heavy tiles (fwd_heavy_count) on the side stream in the 8-wave layout, the rest here
+    FwdSide* side = !IS2D && g_fwd_heavy_log2 > 0 && !lz.rerun && n_busy > 0 ? fwd_side() : nullptr;
+    int part = 0;
+    if (side != nullptr && hipEventRecord(side->fork, s) == hipSuccess &&
+        hipStreamWaitEvent(side->s, side->fork, 0) == hipSuccess) {
+      const int nh = std::min<int>(n_busy, kFwdHeavyMax);
+      hipLaunchKernelGGL((k_raster_fwd<false, 8, 8>), dim3((unsigned)busy_grid<8, 8>(nh)), dim3(512), 0, side->s,
+                         (const Splat*)rec, sorted_ids, kos, tile_offset, tile_order, width, height, tw, th, bg, rgb,
+                         alpha, final_T, last, tile_end, (float4*)chunk_state, chunk_base, nh, CT, tile_cut, cut2d,
+                         lz, stats, sets, 2);
+      GSR_LAUNCH_CHECK("k_raster_fwd<heavy>");
+      part = 1;
+    }
     hipLaunchKernelGGL((k_raster_fwd<IS2D, 4>), dim3((unsigned)(busy_grid<4>(n_busy) + n_fill)),
                        dim3(kRasterThreads), IS2D ? kFwdLdsPad2D : kFwdLdsPad, s, (const Splat*)rec, sorted_ids, kos,
                        tile_offset, tile_order, width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end,
-                       (float4*)chunk_state, chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz, stats, sets);
+                       (float4*)chunk_state, chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz, stats, sets, part);
+    if (part) {
+      GSR_LAUNCH_CHECK(who);
+      GSR_REQUIRE(hipEventRecord(side->join, side->s) == hipSuccess && hipStreamWaitEvent(s, side->join, 0) == hipSuccess,
+                  "%s: joining the heavy-tile stream failed", who);
+    }
   } else if (IS2D && GSR_FWD2D_PAIR) {
     // 2D: every tile in the XCD-aware sweep, two pixels per lane
     hipLaunchKernelGGL(k_raster2d_fwd_pair, dim3((unsigned)sweep_grid2d(CT)), dim3(128), 0, s, (const Splat*)rec,

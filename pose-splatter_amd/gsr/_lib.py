@@ -50,7 +50,7 @@ class BinStats(ctypes.Structure):
                 ("n_sort_big", ctypes.c_int32), ("n_sort_mid", ctypes.c_int32),
                 ("isect_cap", ctypes.c_int64), ("chunk_cap", ctypes.c_int64), ("overflow", ctypes.c_int32),
                 ("chunk_entries", ctypes.c_int32), ("status", ctypes.c_void_p), ("n_sort_long", ctypes.c_int32),
-                ("masks", ctypes.c_int32), ("reserved", ctypes.c_int64)]
+                ("masks", ctypes.c_int32), ("n_heavy", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class BinCaps(ctypes.Structure):
@@ -85,6 +85,7 @@ EXPORTS = {
     "gsr_selftest_reduce64": (ctypes.c_int, [_P, _P]),
     "gsr_selftest_reduce_box16": (ctypes.c_int, [_P, _P]),
     "gsr_selftest_reduce_grp": (ctypes.c_int, [_P, ctypes.c_int, _P]),
+    "gsr_set_fwd_heavy": (ctypes.c_int, [ctypes.c_int]),
     "gsr_set_fwd_lanes": (ctypes.c_int, [_I32]),
     "gsr_set_bwd_layout": (ctypes.c_int, [_I32]),
     "gsr_selftest_lds_order": (ctypes.c_int, [_P, _P]),

@@ -122,6 +122,17 @@ def bwd_layout(request, cuda):
     _lib.check(_lib.lib().gsr_set_bwd_layout(0), "gsr_set_bwd_layout")
 
 
+@pytest.fixture(params=[12, 6], ids=["heavy12", "heavy6"])
+def fwd_heavy(request, cuda):
+    """Run a 3D test with the forward's heavy-tile split at its default threshold (lists of
+    >= 4096 entries: none in the small scenes) and at 64 entries (most busy tiles of a small
+    scene take the 8-wave layout on the side stream), through gsr_set_fwd_heavy; default after."""
+    from gsr import _lib
+    _lib.check(_lib.lib().gsr_set_fwd_heavy(request.param), "gsr_set_fwd_heavy")
+    yield request.param
+    _lib.check(_lib.lib().gsr_set_fwd_heavy(12), "gsr_set_fwd_heavy")
+
+
 def _oracle3d():
     from oracle import oracle3d
     return oracle3d
@@ -172,7 +183,7 @@ def _cot(C, H, W, seed):
     (200, 48, 40, 2, 3, 1.0),
     (2000, 96, 80, 3, 4, 0.0),
 ])
-def test_3d_small_vs_oracle(cuda, fwd_lanes, bwd_layout, N, W, H, C, seed, shift):
+def test_3d_small_vs_oracle(cuda, fwd_lanes, bwd_layout, fwd_heavy, N, W, H, C, seed, shift):
     p, V, K = _scene3d(N, W, H, C, seed, extent=0.05, scale_shift=shift)
     bg = torch.tensor([0.1, 0.5, 0.9])
     vr, va = _cot(C, H, W, seed + 100)
@@ -193,7 +204,7 @@ def test_3d_multiview_equals_single_views(cuda):
         assert torch.equal(rgb_b[c], rgb_c[0]) and torch.equal(a_b[c], a_c[0])
 
 
-def test_3d_deterministic(cuda, fwd_lanes, bwd_layout):
+def test_3d_deterministic(cuda, fwd_lanes, bwd_layout, fwd_heavy):
     W, H, C = 96, 80, 2
     p, V, K = _scene3d(20000, W, H, C, 8)
     bg = torch.ones(3)
@@ -202,6 +213,39 @@ def test_3d_deterministic(cuda, fwd_lanes, bwd_layout):
     r2 = _run_gpu3d(p, V, K, W, H, bg, cuda, vr, va)
     for a, b in zip(r1, r2):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("heavy", [0, 6, 10, 12])
+def test_3d_heavy_tiles_vs_oracle(cuda, heavy):
+    """Long lists whose pixels never saturate (low opacity, a dense cluster: the walks that set
+    the quad forward's span).  With the heavy-tile split on (lists >= 2^heavy entries, up to 64
+    tiles in the 8-wave layout on the side stream) the render and gradient match the oracle, and
+    the split's tile count is the device's (gsr_bin_stats.n_heavy)."""
+    from gsr import _lib, render as R
+    _lib.check(_lib.lib().gsr_set_fwd_heavy(heavy), "gsr_set_fwd_heavy")
+    try:
+        W, H, C = 64, 48, 1
+        p, V, K = _scene3d(12000, W, H, C, 31, extent=0.02)
+        p[:, 13] = -3.5   # opacity ~0.03: the pixels stay live through lists of thousands of entries
+        bg = torch.tensor([0.2, 0.4, 0.6])
+        vr, va = _cot(C, H, W, 32)
+        rgb_g, a_g, g_g = _run_gpu3d(p, V, K, W, H, bg, cuda, vr, va)
+        b = R.last_stats()["_bins"]
+        st = b.pre.view("stats_dev", torch.int32)[:20].cpu()
+        n_heavy, max_seg = int(st[18]), int(st[2])
+        assert max_seg > 2048, max_seg
+        if heavy:
+            lens = (b.tile_off[1:] - b.tile_off[:-1]).cpu()
+            assert n_heavy == int((lens >= 2 ** heavy).sum()), (n_heavy, heavy)
+        else:
+            assert n_heavy == 0
+        rgb_o, a_o, g_o = _run_oracle3d(p, V, K, W, H, bg, vr, va)
+        assert_close(rgb_g, rgb_o, what="rgb")
+        assert_close(a_g, a_o, what="alpha")
+        grad_close(g_g, g_o, what="grad")
+        print(f"[heavy {heavy}] max list {max_seg}, {n_heavy} heavy tiles")
+    finally:
+        _lib.check(_lib.lib().gsr_set_fwd_heavy(12), "gsr_set_fwd_heavy")
 
 
 def test_3d_binning_exact(cuda):
