@@ -1491,33 +1491,16 @@ __device__ __forceinline__ void store_partial_row(float* __restrict__ partial, i
 }
 
 // The per-entry sum update of the backward kernels: lane f adds the staged value v[b] of box b
-// to its wave's slot Lw[k[b]], for NB boxes.  A box lists an entry once, but two boxes may list
-// the same entry, so adds to one address follow in box order.  GSR_BWD_LWPAR: the NB reads are
-// issued together and the aliased boxes chained in registers (n_b = n_c + v_b for the latest
-// earlier box c with k_c == k_b -- the sequential read-add-write's order of additions, so the
-// sums are bitwise those of the serial form), then NB writes in box order (the last write of an
-// address holds its full sum): one LDS round trip per batch instead of NB dependent ones.
-#ifndef GSR_BWD_LWPAR
-#define GSR_BWD_LWPAR 1
-#endif
+// to its wave's slot Lw[k[b]], for NB boxes, box by box.  A box lists an entry once, but two
+// boxes may list the same entry at DIFFERENT group positions, i.e. from different lanes (lane
+// (g, q) of box 0 and lane (g', q) of box 1), so the boxes' read-add-writes must stay in box
+// order: each box's reads see the previous box's writes.  (Issuing all NB reads first and
+// chaining only a lane's own aliased boxes lost those cross-lane updates: measured wrong in the
+// fit test, round 5.)
 template <int NB>
-__device__ __forceinline__ void lw_add(float* __restrict__ Lw, const int (&k)[NB], const float (&v)[NB]) {
-#if GSR_BWD_LWPAR
-  float n[NB];
-#pragma unroll
-  for (int b = 0; b < NB; ++b) n[b] = Lw[k[b]];
-#pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    n[b] += v[b];
-#pragma unroll
-    for (int c = 0; c < b; ++c) n[b] = k[c] == k[b] ? n[c] + v[b] : n[b];
-  }
-#pragma unroll
-  for (int b = 0; b < NB; ++b) Lw[k[b]] = n[b];
-#else
+__device__ __forceinline__ void lw_add(float* Lw, const int (&k)[NB], const float (&v)[NB]) {
 #pragma unroll
   for (int b = 0; b < NB; ++b) Lw[k[b]] += v[b];
-#endif
 }
 // GSR_BWD_PF: the walk reads entry g+1's record from LDS before it evaluates entry g (a
 // scheduling fence keeps the reads there: left to itself the compiler issued each entry's reads
