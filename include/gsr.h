@@ -115,9 +115,10 @@ typedef struct gsr_bin_stats {
   int32_t* status;     /* copy of caps->status (device; may be NULL)                  */
   int32_t n_sort_long; /* tiles with lists >= 1024 entries (the sort's one-workgroup lists) */
   int32_t masks;       /* 1: the emission stored 3D quadrant masks in k_of_s (gsr_bin_emit rec) */
-  int32_t n_heavy;     /* busy tiles with lists >= 2^k entries, k = gsr_set_fwd_heavy (0 if off): the
-                          first of the busy order, rendered by the 3D forward's heavy-tile layout */
-  int32_t reserved;
+  int32_t n_heavy;     /* busy tiles with lists >= heavy_min_len entries (gsr_set_fwd_heavy; 0 if
+                          off): the first of the busy order, rendered by the 3D forward's
+                          heavy-tile layout */
+  int32_t heavy_min_len; /* their list-length threshold, a power of two (INT32_MAX: none) */
 } gsr_bin_stats;       /* 80 bytes; written by gsr_bin_offsets                         */
 
 /* Upper bounds for a call that does not read stats back (gsr_bin_offsets).  The caller sizes
@@ -185,7 +186,7 @@ int gsr_selftest_reduce_box16(float* out, void* stream);
 int gsr_selftest_reduce_grp(float* out, int box_lanes, void* stream);
 
 /* Layout of the raster forward (process-wide): 0 = automatic (3D: 16 lanes per pixel and 16
- * workgroups per tile with at most 160 busy tiles, else 4 lanes per pixel and 4 workgroups per
+ * workgroups per tile for calls of at most 320 tiles (cameras x tiles), else 4 lanes per pixel and 4 workgroups per
  * tile; 2D: one 2-wave workgroup per tile, two pixels per lane), or 1, 4 or 16 (3D only) to force one.
  * All give the same result up to fp32 regrouping of the transmittance products. */
 int gsr_set_fwd_lanes(int lanes);
@@ -201,7 +202,9 @@ int gsr_set_bwd_layout(int layout);
  * whose lists have at least 2^log2_min_len entries (at most 64 of them, the first of the busy
  * order) are rendered in an 8-wave, 8-lanes-per-pixel layout with 512-entry rounds on a side
  * stream, forked from and joined into the call's stream, while the quad layout renders the
- * others.  log2_min_len 0 turns it off; 6..30 sets the threshold (default 12: 4096 entries).
+ * others.  log2_min_len 0 turns it off (the default); 6..30 sets the threshold, raised
+ * to the next power of two while more than 64 tiles reach it (a set fixed by the list lengths).
+ * Only with the automatic forward layout (gsr_set_fwd_lanes(0)): a forced layout is every tile's.
  * Takes effect at the next gsr_bin_offsets (which counts the tiles, gsr_bin_stats.n_heavy).
  * Same results as the quad layout up to fp32 regrouping of the transmittance products. */
 int gsr_set_fwd_heavy(int log2_min_len);

@@ -160,9 +160,14 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(int32_t* __restrict__
     // lists >= 1024 (kWaveSortKeys, buckets >= 10: lanes < 22) take one workgroup each
     const int n_big = __builtin_amdgcn_readlane(ex, 19), n_mid = __builtin_amdgcn_readlane(bk, 19),
               n_long = __builtin_amdgcn_readlane(ex, 22);
-    // heavy tiles of the 3D forward (gsr_set_fwd_heavy): lists >= 2^k, i.e. buckets >= k, whose
-    // count is the start of bucket k - 1 (lane 32 - k)
-    const int n_heavy = heavy_log2 > 0 ? __builtin_amdgcn_readlane(ex, 32 - heavy_log2) : 0;
+    // heavy tiles of the 3D forward (gsr_set_fwd_heavy): lists >= 2^b, i.e. buckets >= b, whose
+    // count is the start of bucket b - 1 (lane 32 - b; non-decreasing in the lane), for the
+    // smallest b >= k that leaves at most kFwdHeavyMax tiles (gsr_common.h): a set fixed by the
+    // list lengths alone
+    const unsigned long long hm = __ballot(l <= 32 - heavy_log2 && l < 32 && ex <= kFwdHeavyMax);
+    const int hl = hm ? 63 - __clzll(hm) : 0;   // (lane 0: ex = 0, no heavy tile)
+    const int n_heavy = heavy_log2 > 0 ? __builtin_amdgcn_readlane(ex, hl) : 0;
+    const int heavy_min = n_heavy > 0 ? (1 << (32 - hl)) : 0x7fffffff;
     if (l == 0) {
       const int n_busy = (int)CT - te;
       s_n_busy = n_busy;
@@ -178,7 +183,7 @@ __global__ __launch_bounds__(kTopThreads) void k_tile_scan(int32_t* __restrict__
       stats->n_active = 0;
       stats->masks = 0;   // set by an emission that stores quadrant masks
       stats->n_heavy = n_heavy;
-      stats->reserved = 0;
+      stats->heavy_min_len = heavy_min;
       // bounded call: the caller sized the intersection / chunk buffers without reading I back
       int ovf = 0;
       if (caps.isect > 0 && (int64_t)tc > caps.isect) ovf |= GSR_OVF_ISECT;

@@ -336,8 +336,16 @@ __device__ __forceinline__ int grp8h_swz(int box) { return (box & 3) << 3; }
 __device__ __forceinline__ unsigned long long wave_ballot(bool p) { return __ballot(p); }
 
 // gsr_set_fwd_heavy (raster.hip): the 3D forward's heavy-tile threshold, log2 of the list length
-// (0: off); the tile scan (binning.hip) counts those tiles into gsr_bin_stats.n_heavy
+// (0: off); the tile scan (binning.hip) counts those tiles into gsr_bin_stats.n_heavy -- at most
+// kFwdHeavyMax of them: the threshold is raised to the smallest power of two (>= 2^k) that leaves
+// at most that many, so the heavy set depends only on the list lengths (the busy order inside a
+// log2 bucket is the tile scan's arrival order: a cap taken from the order's head would make the
+// layout, and with it the fp32 rounding, vary from run to run)
 extern int g_fwd_heavy_log2;
+#ifndef GSR_FWD_HEAVY_MAX
+#define GSR_FWD_HEAVY_MAX 64
+#endif
+constexpr int kFwdHeavyMax = GSR_FWD_HEAVY_MAX;
 
 // Block-wide exclusive scan of one int per thread (NT threads, multiple of 64).
 // s_tmp must hold NT/64 + 1 ints.  Returns the exclusive prefix; *total = block sum.

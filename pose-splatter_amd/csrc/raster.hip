@@ -30,7 +30,7 @@ constexpr int kFwdLdsPad = GSR_FWD_PAD_3D;
 constexpr int kFwdLdsPad2D = GSR_FWD_PAD_2D;
 static int g_fwd_lanes = 0;   // gsr_set_fwd_lanes: 0 automatic, 1 / 4 / 16 forced
 #ifndef GSR_FWD_HEAVY_LOG2
-#define GSR_FWD_HEAVY_LOG2 12   // default heavy-tile threshold: lists of >= 4096 entries; 0 = off
+#define GSR_FWD_HEAVY_LOG2 0   // default heavy-tile threshold (0 = off; 12: lists of >= 4096 entries)
 #endif
 int g_fwd_heavy_log2 = GSR_FWD_HEAVY_LOG2;   // gsr_set_fwd_heavy (gsr_common.h)
 static int g_bwd_layout = 0;  // gsr_set_bwd_layout: 0 automatic, 1 chunk kernel, 2 pixel pairs (3D)
@@ -367,13 +367,7 @@ __host__ __device__ __forceinline__ int busy_grid(int n_busy) { return 8 * FwdSh
 // walks set the quad forward's span (r04_fwd_phase_trace_cfg3.txt: ~12-17 workgroups of 20-22
 // rounds from t ~ 0 to the end); 512-entry rounds halve the rounds, each gathered and culled by 8
 // waves in parallel.
-#ifndef GSR_FWD_HEAVY_MAX
-#define GSR_FWD_HEAVY_MAX 64
-#endif
-constexpr int kFwdHeavyMax = GSR_FWD_HEAVY_MAX;
-__device__ __forceinline__ int fwd_heavy_count(const gsr_bin_stats* stats) {
-  return min(min(stats->n_heavy, stats->n_busy), kFwdHeavyMax);
-}
+
 
 // slot of tile pixel (il, jl) in a chunk record: box-major inside the 8x8 quadrant wv,
 // 64 * wv + 16 * box + pos (pos = pixel within its 4x4 box).  The quad forward writes one 4x4
@@ -453,7 +447,8 @@ extern "C" int gsr_debug_fwd_trace(void* buf) {
 #define GSR_FWD_MINB 6
 #endif
 // NW: waves per workgroup (4; 8 for the heavy-tile variant, LPP 8).  part: 0 every busy tile,
-// 1 the busy tiles past the heavy ones (fwd_heavy_count), 2 the heavy ones only.
+// 1 the tiles with lists shorter than stats->heavy_min_len, 2 the others (the heavy tiles: a
+// first-pass forward finds them at the head of the busy order, a lazy re-render anywhere in its list).
 template <bool IS2D, int LPP, int NW = 4>
 __global__ __launch_bounds__(NW * 64, (IS2D || LPP != 4) ? 1 : GSR_FWD_MINB) void k_raster_fwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ kos,
@@ -511,10 +506,7 @@ __global__ __launch_bounds__(NW * 64, (IS2D || LPP != 4) ? 1 : GSR_FWD_MINB) voi
     }
   }
   if (u >= n_busy) return;
-  if (part != 0) {   // the heavy / light split of one forward (never in a lazy re-render)
-    const int nh = fwd_heavy_count(stats);
-    if (part == 1 ? u < nh : u >= nh) return;
-  }
+
   int c, ty, tx;
   tile_coords(ct, tw, th, c, ty, tx);
   if constexpr (IS2D) rec += rec_offset2d(sets.begin, sets.F, c, sets.N);   // the set's record copy
@@ -530,6 +522,7 @@ __global__ __launch_bounds__(NW * 64, (IS2D || LPP != 4) ? 1 : GSR_FWD_MINB) voi
   const float bx0 = (float)(tx * kTile + ox) + off, bx1 = bx0 + (float)(FS::VBX - 1);
   const float by0 = (float)(ty * kTile + oy) + off, by1 = by0 + (float)(FS::VBY - 1);
   const int start = tile_offset[ct], list_end = tile_offset[ct + 1];
+  if (part != 0 && (part == 2) != (list_end - start >= stats->heavy_min_len)) return;   // heavy / light split
   const int end = lz.tile_sorted && !lz.rerun ? lz.tile_sorted[ct] : list_end;
   if (threadIdx.x == 0) s_max = -1;
   __syncthreads();
@@ -2920,19 +2913,23 @@ int gsr_selftest_reduce_box16(float* out, void* stream) {
 
 namespace gsr {
 
-// Layout of the raster forward.  3D: 16 lanes per pixel and 16 workgroups per tile with at
-// most kFwd16MaxBusy busy tiles (the quad layout would fill under half of the chip's ~1 280
-// workgroup slots, so latency rules), else 4 lanes per pixel, 4 workgroups per tile (the heavy
+// Layout of the raster forward.  3D: 16 lanes per pixel and 16 workgroups per tile for calls of
+// at most kFwd16MaxTiles tiles (cameras x tiles: few busy tiles, the quad layout would fill
+// under half of the chip's ~1 280 workgroup slots, so latency rules; config 2: 288 tiles, 36
+// busy), else 4 lanes per pixel, 4 workgroups per tile (the heavy
 // tiles' serial walks are a quarter as long as with one lane per pixel: config 3 raster fwd
 // 112 us against 287 us for the box layout).  2D (every tile busy, no early termination, so
 // throughput rules): the box layout, one lane per pixel (config 4 raster fwd 12.5 ms against
 // 15.2 ms with quads).  gsr_set_fwd_lanes forces one (tests run every layout on the same
-// scenes).
-constexpr int kFwd16MaxBusy = 160;
-static int fwd_lanes(bool is2d, int n_busy) {
+// scenes).  The rule reads the call's shape, not its busy-tile count: a capacity-bounded call
+// knows only a bound on that count, and must run the layout an exact call of the same inputs
+// runs (bitwise-equal results; round 4 chose by the count, which a varying Gaussian count moved
+// across the threshold in one call and not in the other, tests/test_headline_mode_gpu.py).
+constexpr int64_t kFwd16MaxTiles = 320;
+static int fwd_lanes(bool is2d, int64_t CT) {
   if (g_fwd_lanes == 1 || g_fwd_lanes == 4 || (g_fwd_lanes == 16 && !is2d)) return g_fwd_lanes;
   if (is2d) return 1;
-  return n_busy <= kFwd16MaxBusy ? 16 : 4;
+  return CT <= kFwd16MaxTiles ? 16 : 4;
 }
 
 // The heavy-tile forward's side stream and its fork / join events, one set per (host thread,
@@ -2988,7 +2985,7 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
   // 3D with few busy tiles (a single small view, a multi-GPU rank's share): 16 lanes per pixel,
   // 16 workgroups per tile -- a quarter of the serial walk per wave, for a chip the quad layout
   // would leave mostly idle
-  if (lanes == 0) lanes = fwd_lanes(IS2D, n_busy);
+  if (lanes == 0) lanes = fwd_lanes(IS2D, CT);
   if (lz.rerun && n_busy == 0) return GSR_OK;
   if (!IS2D && lanes == 16) {
     hipLaunchKernelGGL((k_raster_fwd<false, 16>), dim3((unsigned)(busy_grid<16>(n_busy) + n_fill)),
@@ -2996,13 +2993,22 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
                        width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end, (float4*)chunk_state,
                        chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz, stats, sets);
   } else if (lanes == 4) {
-    // 3D: the heavy tiles (fwd_heavy_count) on the side stream in the 8-wave layout, the rest here
-    FwdSide* side = !IS2D && g_fwd_heavy_log2 > 0 && !lz.rerun && n_busy > 0 ? fwd_side() : nullptr;
+    // 3D: the heavy tiles (lists >= stats->heavy_min_len) on the side stream in the 8-wave layout,
+    // the rest here -- with the automatic layout only (a layout forced by gsr_set_fwd_lanes is every
+    // tile's).  A first pass finds them among the first kFwdHeavyMax busy tiles; a lazy re-render
+    // (lz.rerun) anywhere in its list of n_busy tiles, the same tiles as the pass over a full sort.
+    FwdSide* side = !IS2D && g_fwd_lanes == 0 && g_fwd_heavy_log2 > 0 && n_busy > 0 ? fwd_side() : nullptr;
     int part = 0;
+#ifdef GSR_FWD_HEAVY_SAMESTREAM   // (experiment: the heavy launch on the call's stream, before the quad one)
+    if (side != nullptr) {
+      hipStream_t hs = s;
+#else
     if (side != nullptr && hipEventRecord(side->fork, s) == hipSuccess &&
         hipStreamWaitEvent(side->s, side->fork, 0) == hipSuccess) {
-      const int nh = std::min<int>(n_busy, kFwdHeavyMax);
-      hipLaunchKernelGGL((k_raster_fwd<false, 8, 8>), dim3((unsigned)busy_grid<8, 8>(nh)), dim3(512), 0, side->s,
+      hipStream_t hs = side->s;
+#endif
+      const int nh = lz.rerun ? (int)n_busy : std::min<int>(n_busy, kFwdHeavyMax);
+      hipLaunchKernelGGL((k_raster_fwd<false, 8, 8>), dim3((unsigned)busy_grid<8, 8>(nh)), dim3(512), 0, hs,
                          (const Splat*)rec, sorted_ids, kos, tile_offset, tile_order, width, height, tw, th, bg, rgb,
                          alpha, final_T, last, tile_end, (float4*)chunk_state, chunk_base, nh, CT, tile_cut, cut2d,
                          lz, stats, sets, 2);
@@ -3013,11 +3019,13 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
                        dim3(kRasterThreads), IS2D ? kFwdLdsPad2D : kFwdLdsPad, s, (const Splat*)rec, sorted_ids, kos,
                        tile_offset, tile_order, width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end,
                        (float4*)chunk_state, chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz, stats, sets, part);
+#ifndef GSR_FWD_HEAVY_SAMESTREAM
     if (part) {
       GSR_LAUNCH_CHECK(who);
       GSR_REQUIRE(hipEventRecord(side->join, side->s) == hipSuccess && hipStreamWaitEvent(s, side->join, 0) == hipSuccess,
                   "%s: joining the heavy-tile stream failed", who);
     }
+#endif
   } else if (IS2D && GSR_FWD2D_PAIR) {
     // 2D: every tile in the XCD-aware sweep, two pixels per lane
     hipLaunchKernelGGL(k_raster2d_fwd_pair, dim3((unsigned)sweep_grid2d(CT)), dim3(128), 0, s, (const Splat*)rec,
@@ -3136,7 +3144,7 @@ int gsr3d_raster_fwd_lazy(const float* rec, const float* depth, int32_t* sorted_
   GSR_REQUIRE(lazy != nullptr && sort_workspace != nullptr, "gsr3d_raster_fwd_lazy: missing workspace");
   GSR_REQUIRE(n_lazy_max >= 0 && n_lazy_max <= n_busy, "gsr3d_raster_fwd_lazy: bad n_lazy_max %d", n_lazy_max);
   const int64_t CT = (int64_t)C * ceil_div(width, kTile) * ceil_div(height, kTile);
-  const int lanes = fwd_lanes(false, n_busy);
+  const int lanes = fwd_lanes(false, CT);
   // pass 1: every tile walks its sorted prefix; tiles that reach its end are listed
   const FwdLazy l1{lazy, lazy + CT, lazy + 2 * CT, lazy + 3 * CT, 0};
   int rc = raster_fwd<false>("gsr3d_raster_fwd_lazy", rec, depth, sorted_ids, k_of_s,

@@ -50,7 +50,8 @@ class BinStats(ctypes.Structure):
                 ("n_sort_big", ctypes.c_int32), ("n_sort_mid", ctypes.c_int32),
                 ("isect_cap", ctypes.c_int64), ("chunk_cap", ctypes.c_int64), ("overflow", ctypes.c_int32),
                 ("chunk_entries", ctypes.c_int32), ("status", ctypes.c_void_p), ("n_sort_long", ctypes.c_int32),
-                ("masks", ctypes.c_int32), ("n_heavy", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("masks", ctypes.c_int32), ("n_heavy", ctypes.c_int32),
+                ("heavy_min_len", ctypes.c_int32)]
 
 
 class BinCaps(ctypes.Structure):

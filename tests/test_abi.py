@@ -101,6 +101,11 @@ def test_layout_switches_validate():
         assert lib.gsr_set_fwd_lanes(v) == 0
     for v in (2, 8, -4):
         assert lib.gsr_set_fwd_lanes(v) == -1 and b"gsr_set_fwd_lanes" in lib.gsr_last_error()
+    for v in (0, 6, 12, 30):   # gsr_set_fwd_heavy: 0 (off) or a log2 list length in 6..30
+        assert lib.gsr_set_fwd_heavy(v) == 0
+    for v in (-1, 1, 5, 31):
+        assert lib.gsr_set_fwd_heavy(v) == -1 and b"gsr_set_fwd_heavy" in lib.gsr_last_error()
+    assert lib.gsr_set_fwd_heavy(0) == 0
     assert lib.gsr_set_bwd_layout(0) == 0 and lib.gsr_set_fwd_lanes(0) == 0
 
 
