@@ -116,33 +116,6 @@ __device__ __forceinline__ void box4_cull(const unsigned char* __restrict__ list
   }
 }
 
-struct SubTile {
-  int c, ty, tx, wv, lane, i, j;
-  float px, py, bx0, bx1, by0, by1;
-  bool inside;
-};
-
-template <bool IS2D>
-__device__ __forceinline__ SubTile sub_tile(int ct, int tw, int th, int W, int H) {
-  SubTile t;
-  tile_coords(ct, tw, th, t.c, t.ty, t.tx);
-  t.wv = threadIdx.x >> 6;
-  t.lane = threadIdx.x & 63;
-  const int sx0 = t.tx * kTile + (t.wv & 1) * 8;
-  const int sy0 = t.ty * kTile + (t.wv >> 1) * 8;
-  t.i = sy0 + (t.lane >> 3);
-  t.j = sx0 + (t.lane & 7);
-  t.inside = (t.i < H) && (t.j < W);
-  const float off = IS2D ? 0.f : 0.5f;   // 2D: integer centres (src/gaussian_renderer.py:355-358)
-  t.px = (float)t.j + off;
-  t.py = (float)t.i + off;
-  t.bx0 = (float)sx0 + off;
-  t.bx1 = (float)(sx0 + 7) + off;
-  t.by0 = (float)sy0 + off;
-  t.by1 = (float)(sy0 + 7) + off;
-  return t;
-}
-
 // ---------------------------------------------------------------- empty tiles
 // Tiles with an empty list only need the background.  The forward launches them as extra
 // workgroups (after the busy tiles' ones) that stride over order[n_busy..CT): cheap stores that
@@ -156,10 +129,13 @@ __device__ void fill_empty(const int32_t* __restrict__ order, const int32_t* __r
   const int G = gridDim.x - busy_blocks;
   for (int64_t t = n_busy + (blockIdx.x - busy_blocks); t < CT; t += G) {
     const int ct = order[t];
-    const SubTile st = sub_tile<IS2D>(ct, tw, th, W, H);
-    if (st.inside) {
-      const int64_t pix = ((int64_t)st.c * H + st.i) * W + st.j;
-      const float* bgc = bg + st.c * 3;
+    int c, ty, tx;
+    tile_coords(ct, tw, th, c, ty, tx);
+    for (int p = threadIdx.x; p < kTilePix; p += blockDim.x) {   // (256- and 512-thread forwards)
+      const int i = ty * kTile + (p >> 4), j = tx * kTile + (p & 15);
+      if (i >= H || j >= W) continue;
+      const int64_t pix = ((int64_t)c * H + i) * W + j;
+      const float* bgc = bg + c * 3;
       out_rgb[pix * 3 + 0] = bgc[0];
       out_rgb[pix * 3 + 1] = bgc[1];
       out_rgb[pix * 3 + 2] = bgc[2];
@@ -361,12 +337,16 @@ struct FwdShape {
 // workgroups for the busy tiles: G per tile, rounded up to whole groups of 8 tiles
 template <int LPP, int NW = 4>
 __host__ __device__ __forceinline__ int busy_grid(int n_busy) { return 8 * FwdShape<LPP, NW>::G * ((n_busy + 7) / 8); }
-// Heavy tiles (GSR_FWD_HEAVY): the first busy tiles of the visit order whose lists have at least
-// 2^kFwdHeavyLog2 entries, at most kFwdHeavyMax of them, run the 8-wave forward on a side stream
-// (forked and joined inside gsr3d_raster_fwd) while the quad forward takes the others.  Their
-// walks set the quad forward's span (r04_fwd_phase_trace_cfg3.txt: ~12-17 workgroups of 20-22
-// rounds from t ~ 0 to the end); 512-entry rounds halve the rounds, each gathered and culled by 8
-// waves in parallel.
+// Heavy tiles (gsr_set_fwd_heavy, OFF by default): busy tiles whose lists have at least
+// stats->heavy_min_len entries (at most kFwdHeavyMax of them) run the 8-wave forward on a side
+// stream (forked and joined inside gsr3d_raster_fwd) while the quad forward takes the others.
+// 512-entry rounds halve a walk's rounds, each gathered and culled by 8 waves in parallel.
+// Measured (round 5, config 3): serialised, the 8-wave kernel renders the lists >= 4096 in 42 us
+// (their walks set the quad forward's ~100 us span), but the quad forward over the rest still
+// takes 84 us; run concurrently the two kernels contend for the CUs (quad 105 -> 131 us, step
+// 0.383 -> 0.405 ms; with the side stream at the highest priority a captured step took 0.60 ms),
+// and every tile in the 8-wave layout is slower (raster fwd 107 -> 120 us, config 5 389 -> 516 us)
+// -- the forward is throughput-bound beyond its heaviest walks.
 
 
 // slot of tile pixel (il, jl) in a chunk record: box-major inside the 8x8 quadrant wv,
@@ -450,7 +430,7 @@ extern "C" int gsr_debug_fwd_trace(void* buf) {
 // 1 the tiles with lists shorter than stats->heavy_min_len, 2 the others (the heavy tiles: a
 // first-pass forward finds them at the head of the busy order, a lazy re-render anywhere in its list).
 template <bool IS2D, int LPP, int NW = 4>
-__global__ __launch_bounds__(NW * 64, (IS2D || LPP != 4) ? 1 : GSR_FWD_MINB) void k_raster_fwd(
+__global__ __launch_bounds__(NW * 64, NW == 8 ? 6 : (IS2D || LPP != 4) ? 1 : GSR_FWD_MINB) void k_raster_fwd(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const int32_t* __restrict__ kos,
     const int32_t* __restrict__ tile_offset,
     const int32_t* __restrict__ order, int W, int H, int tw, int th, const float* __restrict__ bg,
@@ -497,12 +477,10 @@ __global__ __launch_bounds__(NW * 64, (IS2D || LPP != 4) ? 1 : GSR_FWD_MINB) voi
     n_busy = min(n_busy, nb_dev);
   } else {
     n_busy = nb_dev;
-    if constexpr (NW == 4) {
-      if ((int)blockIdx.x >= busy_blocks) {
-        fill_empty<IS2D>(order, tile_offset, n_busy, busy_blocks, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
-                         out_last, tile_end, tile_cut);
-        return;
-      }
+    if ((int)blockIdx.x >= busy_blocks) {
+      fill_empty<IS2D>(order, tile_offset, n_busy, busy_blocks, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
+                       out_last, tile_end, tile_cut);
+      return;
     }
   }
   if (u >= n_busy) return;
@@ -2934,8 +2912,7 @@ static int fwd_lanes(bool is2d, int64_t CT) {
 
 // The heavy-tile forward's side stream and its fork / join events, one set per (host thread,
 // device): created on first use (before any graph capture: a bounded call, the only kind that
-// is captured, always follows an eager call of its shape), at the device's highest stream
-// priority so the heavy workgroups are dispatched ahead of the quad forward's.  The fork / join
+// is captured, always follows an eager call of its shape).  The fork / join
 // are stream-ordered event waits, so a captured forward holds the two launches as parallel
 // branches of its graph.
 struct FwdSide {
@@ -2950,9 +2927,9 @@ static FwdSide* fwd_side() {
   FwdSide& x = sides[d];
   if (!x.tried) {
     x.tried = true;
-    int least = 0, greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
-    x.ok = hipStreamCreateWithPriority(&x.s, hipStreamNonBlocking, greatest) == hipSuccess &&
+    // default priority: at the device's highest one a captured step's branches ran pathologically
+    // (config 3 step 0.38 -> 0.60 ms; 0.41 ms at the default priority, r05 A/B)
+    x.ok = hipStreamCreateWithPriority(&x.s, hipStreamNonBlocking, 0) == hipSuccess &&
            hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&x.join, hipEventDisableTiming) == hipSuccess;
     if (!x.ok) (void)hipGetLastError();
@@ -2999,14 +2976,9 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
     // (lz.rerun) anywhere in its list of n_busy tiles, the same tiles as the pass over a full sort.
     FwdSide* side = !IS2D && g_fwd_lanes == 0 && g_fwd_heavy_log2 > 0 && n_busy > 0 ? fwd_side() : nullptr;
     int part = 0;
-#ifdef GSR_FWD_HEAVY_SAMESTREAM   // (experiment: the heavy launch on the call's stream, before the quad one)
-    if (side != nullptr) {
-      hipStream_t hs = s;
-#else
     if (side != nullptr && hipEventRecord(side->fork, s) == hipSuccess &&
         hipStreamWaitEvent(side->s, side->fork, 0) == hipSuccess) {
       hipStream_t hs = side->s;
-#endif
       const int nh = lz.rerun ? (int)n_busy : std::min<int>(n_busy, kFwdHeavyMax);
       hipLaunchKernelGGL((k_raster_fwd<false, 8, 8>), dim3((unsigned)busy_grid<8, 8>(nh)), dim3(512), 0, hs,
                          (const Splat*)rec, sorted_ids, kos, tile_offset, tile_order, width, height, tw, th, bg, rgb,
@@ -3019,13 +2991,11 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
                        dim3(kRasterThreads), IS2D ? kFwdLdsPad2D : kFwdLdsPad, s, (const Splat*)rec, sorted_ids, kos,
                        tile_offset, tile_order, width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end,
                        (float4*)chunk_state, chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz, stats, sets, part);
-#ifndef GSR_FWD_HEAVY_SAMESTREAM
     if (part) {
       GSR_LAUNCH_CHECK(who);
       GSR_REQUIRE(hipEventRecord(side->join, side->s) == hipSuccess && hipStreamWaitEvent(s, side->join, 0) == hipSuccess,
                   "%s: joining the heavy-tile stream failed", who);
     }
-#endif
   } else if (IS2D && GSR_FWD2D_PAIR) {
     // 2D: every tile in the XCD-aware sweep, two pixels per lane
     hipLaunchKernelGGL(k_raster2d_fwd_pair, dim3((unsigned)sweep_grid2d(CT)), dim3(128), 0, s, (const Splat*)rec,
