@@ -116,11 +116,17 @@ __global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
     Geo3D g;
     for (int c = slot; c < C; c += CPB) {
       const int64_t cn = (int64_t)c * N + n;
-      // the (c,n) scalars load together (no dependent round trip before the rect / key)
+      // the (c,n) scalars load together (no dependent round trip before the rect / key).  Pinned
+      // by the empty asm: the compiler sank the rect / offset / depth loads below the cnt test,
+      // three more dependent round trips per camera (config 3 55 -> 53.5 us, config 5 453 -> 438
+      // us).  (Issuing all four cut keys and rows of a round unconditionally -- an entry without
+      // a row reading another one -- was slower: 55 -> 81 us.  This kernel is bound by its memory
+      // instructions, not only by their latency, so masked-off loads are worth their branches.)
       const int cnt = isect_count[cn];
       const uint2 rc = rect[cn];
       const int off = isect_offset[cn];
       const uint64_t key = sort_key(depth, cn, GSR_ORDER_DEPTH);
+      asm volatile("" ::"v"(cnt), "v"(rc.x), "v"(rc.y), "v"(off), "v"((uint32_t)(key >> 32)));
       if (cnt <= 0 || ovf) continue;
       float acc[kPartial];
 #pragma unroll

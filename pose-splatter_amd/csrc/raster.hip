@@ -215,6 +215,22 @@ __device__ __forceinline__ int quad_max_i(int v) {
   v = max(v, dpp_i<kQuadXor1>(v));
   return max(v, dpp_i<kQuadXor2>(v));
 }
+// A workgroup barrier that also tells whether any thread passed `live` (the forward round loops'
+// exit test).  __syncthreads_count took three barriers around an LDS atomic; here each wave posts
+// its ballot to its own word of `flags` and ONE barrier follows.  The caller double-buffers
+// `flags` by round parity: a fast wave writes round r+2's words only after the barrier of round
+// r+1, which every wave reaches after reading round r's.
+template <int NW>
+__device__ __forceinline__ bool sync_any(bool live, int* flags) {
+  const bool w = __ballot(live) != 0ull;
+  if ((threadIdx.x & 63) == 0) flags[threadIdx.x >> 6] = w ? 1 : 0;
+  __syncthreads();
+  int a = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) a |= flags[i];
+  return a != 0;
+}
+
 // Operations over the LPP lanes that serve one pixel in the forward: a DPP quad (LPP 4) or a
 // DPP row (LPP 16); q = the lane's slot in its group.  prefix: inclusive (Q) and exclusive (P)
 // products over the slots in order; suffix_excl: sum over the slots after q; next: slot q+1's
@@ -520,6 +536,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 6 : (IS2D || LPP != 4) ? 1 : GSR
   __shared__ float4 s_q[2][3][NT];
   __shared__ QIdx s_qe[2][NT];   // entry - round base (LDS: 6 workgroups per CU at 4 waves)
   __shared__ int s_qn[2][NW];
+  __shared__ __attribute__((aligned(16))) int s_live[2][NW];
   __shared__ QIdx s_l[NW][128];
   // 3D -- shared rounds: the quadrant workgroup walks the list in 256-entry rounds; wave w gathers
   // entries 64w..64w+63 of the round (one round ahead), culls them against the 8x8 quadrant
@@ -537,14 +554,18 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 6 : (IS2D || LPP != 4) ? 1 : GSR
   // 1.27 of its tile's 4 quadrants at config 3).  Kept entries still take the exact cull.
   const int qbit = kMaskShift + ((sy >> 3) << 1) + (sx >> 3);
   if (!stats->masks) kos = nullptr;   // this call's emission stored no masks
-  int idn = 0;
-  bool ucur = false, un = false;
+  // kn: the raw emission word of the entry two rounds ahead (all bits set without masks), tested
+  // only when its record is gathered a round later.  (Testing it at its load made every round
+  // wait out that load's full latency: the mask is an SGPR lane mask, so the compiler placed a
+  // vmcnt(0) right behind the two loads.)
+  int idn = 0, kn = -1;
+  bool ucur = false;
   if (end > start) {
     const int e0 = min(start + 64 * wv + lane, e_last), e1 = min(start + NT + 64 * wv + lane, e_last);
     const int id0 = ids[e0];
     idn = ids[e1];
     ucur = kos == nullptr || ((kos[e0] >> qbit) & 1);
-    un = kos == nullptr || ((kos[e1] >> qbit) & 1);
+    if (kos != nullptr) kn = kos[e1];
     if (ucur) {
       const Splat s0 = rec[id0];
       c0 = s0.p0; c1 = s0.p1; c2 = s0.p2;
@@ -569,17 +590,17 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 6 : (IS2D || LPP != 4) ? 1 : GSR
       }
       if (lane == 0) s_qn[buf][wv] = __popcll(m);
       const int id_use = idn;
-      ucur = un;
+      ucur = ((kn >> qbit) & 1) != 0;
       const int e2 = min(rb + 2 * NT + 64 * wv + lane, e_last);
       idn = ids[e2];
-      un = kos == nullptr || ((kos[e2] >> qbit) & 1);
+      if (kos != nullptr) kn = kos[e2];
       if (ucur) {
         const Splat sn = rec[id_use];
         c0 = sn.p0; c1 = sn.p1; c2 = sn.p2;
       }
     }
     FWD_P(0);
-    if (__syncthreads_count(!done) == 0) break;
+    if (!sync_any<NW>(!done, s_live[buf])) break;
     FWD_P(1);
 #ifdef GSR_FWD_TRACE
     if (n_rounds++ == 0) FWD_T(1);
@@ -890,6 +911,7 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
   // of a 32-lane half in different banks
   __shared__ __attribute__((aligned(16))) unsigned char s_box[4][4][kBoxStride];
   __shared__ int s_max;
+  __shared__ __attribute__((aligned(16))) int s_live[2][4];
   static_assert(kChunk3 == 128, "a round half is one chunk");
   const int busy_blocks = (n_busy + 7) & ~7;   // n_busy: the grid's bound (see k_raster_fwd)
   // device counts and this workgroup's tile in one round trip (see k_raster_fwd); 2D: every tile,
@@ -977,7 +999,7 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
       c1 = rec[id_use].p1;
       c2 = rec[id_use].p2;
     }
-    if (__syncthreads_count(!done) == 0) break;
+    if (!sync_any<4>(!done, s_live[buf])) break;
     // a half's quadrant survivors (slot in the half), kept in this wave's own slots of the other
     // round buffer: dead since the round barrier, and rewritten only by this wave at the next
     // round's start (LDS 27.2 -> 26.6 KB: 6 workgroups per CU)
@@ -1205,6 +1227,7 @@ __global__ __launch_bounds__(128, GSR_FWD2P_MINB) void k_raster2d_fwd_pair(
   __shared__ float4 s_r[2][3][kHS];
   __shared__ __attribute__((aligned(16))) unsigned char s_box[2][8][kBoxStride];
   __shared__ int s_max;
+  __shared__ __attribute__((aligned(8))) int s_live[2][2];
   const int ct = sweep_tile2d(blockIdx.x, CT, tw * th, sets.begin, sets.F);
   const int ovf = stats->overflow;
   if (ovf) {
@@ -1260,7 +1283,7 @@ __global__ __launch_bounds__(128, GSR_FWD2P_MINB) void k_raster2d_fwd_pair(
       c1 = rec[id_use].p1;
       c2 = rec[id_use].p2;
     }
-    if (__syncthreads_count(!(doneA && doneB)) == 0) break;
+    if (!sync_any<2>(!(doneA && doneB), s_live[buf])) break;
     if (rb > start && ((rb - start) & umask) == 0) {   // entering unit kcur+1: the pixels' T anchors
       if (anchors) {
         const int64_t arow = (int64_t)(cbase + kcur + 1) * kRasterThreads;
@@ -1653,6 +1676,17 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
   const float4 rck = ckpt[(int64_t)chunk * kRasterThreads + ckpt_slot_of(wv, box, pos)];
   int id_mine = threadIdx.x < sn ? ids[sb0 + threadIdx.x] : 0;
   int kos_mine = threadIdx.x < sn ? k_of_s[sb0 + threadIdx.x] : 0;
+  // the records as three float4 registers (a Splat variable assigned under a branch and in the
+  // sub-chunk loop went through 48 B of scratch per lane: a store + reload on the load chain),
+  // gathered right behind the ids: issued after the pixel-state loads, they waited for `last`
+  // as well (one more memory latency on every workgroup's load chain)
+  const float4* const rec4 = reinterpret_cast<const float4*>(rec);
+  float4 sp0 = make_float4(0.f, 0.f, 0.f, 0.f), sp1 = sp0, sp2 = sp0;
+  if (threadIdx.x < sn) {
+    sp0 = rec4[3 * (int64_t)id_mine + 0];
+    sp1 = rec4[3 * (int64_t)id_mine + 1];
+    sp2 = rec4[3 * (int64_t)id_mine + 2];
+  }
   float Tf = 1.f, Tl = 1.f, vr = 0.f, vg = 0.f, vb = 0.f, va = 0.f;
   int last = -1;
   if (inside) {
@@ -1693,15 +1727,6 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
     mu = last < b0 + n ? mu_last : (Sv + Tf * mu_last) / T;
   }
   const int wlast = wave_max_i(last);   // wave-uniform (an SGPR across the sub-chunk loop)
-  // the records as three float4 registers (a Splat variable assigned under a branch and in the
-  // sub-chunk loop went through 48 B of scratch per lane: a store + reload on the load chain)
-  const float4* const rec4 = reinterpret_cast<const float4*>(rec);
-  float4 sp0 = make_float4(0.f, 0.f, 0.f, 0.f), sp1 = sp0, sp2 = sp0;
-  if (threadIdx.x < sn) {
-    sp0 = rec4[3 * (int64_t)id_mine + 0];
-    sp1 = rec4[3 * (int64_t)id_mine + 1];
-    sp2 = rec4[3 * (int64_t)id_mine + 2];
-  }
   const int fg = lane / kPartial, fq = lane - kPartial * (lane / kPartial);
   const bool fown = lane < kGroup * kPartial;
   float* const Lw = &L[fq * kLq + wv * (kChunk3 + 1)];
