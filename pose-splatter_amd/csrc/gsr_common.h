@@ -469,6 +469,17 @@ __device__ __forceinline__ int set_first_camera(const int32_t* __restrict__ set_
   return set_begin == nullptr ? 0 : set_begin[set_of_camera(set_begin, F, c)];
 }
 
+// 2D: with several cameras per parameter set (views ignored: identical renders), the raster
+// backward walks each (set, tile) once for all the set's cameras (k_raster2d_bwd_frame) and
+// writes their summed partial rows at the set's first camera's emission indices only;
+// gsr2d_project_bwd then reads only those.  Both sides decide by this one rule.
+#ifndef GSR_BWD2D_FRAME
+#define GSR_BWD2D_FRAME 1
+#endif
+inline bool rows2d_per_set(const int32_t* set_begin, int F, int C) {
+  return GSR_BWD2D_FRAME && set_begin != nullptr && C > F;
+}
+
 // 2D: the record of entry id = c*N + n lives in the copy of camera c's set's first camera
 // (k_project2d_fwd writes one copy per set): rec[id + rec_offset2d(c)].
 __device__ __forceinline__ int64_t rec_offset2d(const int32_t* __restrict__ set_begin, int F, int c, int64_t N) {

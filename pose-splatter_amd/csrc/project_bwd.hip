@@ -438,7 +438,7 @@ __global__ __launch_bounds__(kBwdThreads) void k_project2d_bwd_staged(
     const int32_t* __restrict__ set_begin, int F, int n_cam, int tw, int th, const uint2* __restrict__ rect,
     const int32_t* __restrict__ isect_offset, const int32_t* __restrict__ isect_count,
     const uint64_t* __restrict__ tile_cut, const float* __restrict__ partial, const gsr_bin_stats* __restrict__ stats,
-    float* __restrict__ v_params) {
+    float* __restrict__ v_params, int first_only) {
   __shared__ float s_rows[kPartialStride * kStageRows];
   __shared__ int s_lo, s_hi;
   const int f = blockIdx.y;
@@ -447,7 +447,9 @@ __global__ __launch_bounds__(kBwdThreads) void k_project2d_bwd_staged(
   // the forward's bounds did not hold: NaN rows, no partial row read (loaded with the first
   // gathers, tested in the camera loop: no round trip of its own)
   const bool ovf = stats != nullptr && stats->overflow != 0;
-  const int c0 = set_begin ? set_begin[f] : 0, c1 = set_begin ? set_begin[f + 1] : n_cam;
+  const int c0 = set_begin ? set_begin[f] : 0;
+  // (rows2d_per_set: the set's summed rows are its first camera's)
+  const int c1 = first_only ? min(set_begin[f + 1], c0 + 1) : set_begin ? set_begin[f + 1] : n_cam;
   static_assert(kPartialStride * kStageRows % kBwdThreads == 0, "whole rounds of floats per thread");
   float acc[kPartial];
 #pragma unroll
@@ -634,7 +636,8 @@ int gsr2d_project_bwd(const float* params, int64_t N, int64_t row_stride, int64_
   GSR_REQUIRE(F <= 65535, "gsr2d_project_bwd: F=%d > 65535 parameter sets", F);
   hipLaunchKernelGGL(k_project2d_bwd_staged, dim3(ceil_div(N, kBwdThreads), F), dim3(kBwdThreads), 0,
                      (hipStream_t)stream, params, N, row_stride, set_stride, set_begin, F, C, tw, th,
-                     (const uint2*)rect, isect_offset, isect_count, tile_cut, partial, stats, v_params);
+                     (const uint2*)rect, isect_offset, isect_count, tile_cut, partial, stats, v_params,
+                     rows2d_per_set(set_begin, F, C) ? 1 : 0);
   GSR_LAUNCH_CHECK("k_project2d_bwd_staged");
   return GSR_OK;
 }

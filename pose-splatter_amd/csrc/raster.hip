@@ -2516,6 +2516,330 @@ __global__ __launch_bounds__(128, GSR_BWD2P_MINB) void k_raster2d_bwd_pair(
   }
 }
 
+// ---------------------------------------------------------------- 2D backward, a frame's units per tile
+// pose-splatter's 2D renderer ignores the view (src/gaussian_renderer.py:280-281): every camera
+// of a parameter set renders the same image, from the same list over the same record copy, and
+// only its cotangent differs.  k_raster2d_bwd_frame runs ONE workgroup per (set, tile) -- the
+// set's first camera's sweep slot; the other cameras' slots exit -- and walks the tile's list
+// once for all the set's cameras: the per-(entry, pixel) forward state (sigma, alpha, the
+// validity test, T recovered by division, alpha T) is computed once, then every camera's pixel
+// is walked with ITS OWN cotangent (its colour dot product, its own mu recursion, its colour
+// partials), and the cameras' contributions are summed in registers before the one cross-lane
+// reduction per group.  The entry's partial row -- the sum over the set's cameras -- is written
+// once, at the set's first camera's emission index, and gsr2d_project_bwd reads only those rows
+// (the rows of a set's cameras used to be written per camera and summed there).
+//   Same layout, culls, sub-chunk walk, T anchors and reduction as k_raster2d_bwd_pair; the forward
+// state read is the first camera's (bitwise equal to every camera's of the set:
+// tests/test_multiframe_gpu.py checks it).  GB cameras are walked per pass (registers: 8 per
+// camera and lane); a set with more walks its tile again per further GB cameras, adding to its
+// rows.  A set of one camera (GB = 1) is k_raster2d_bwd_pair's arithmetic exactly.
+#ifndef GSR_BWD2F_MINB
+#define GSR_BWD2F_MINB 2   // waves per SIMD the compiler aims at (the per-camera state: 8 x GB VGPRs)
+#endif
+template <int GB>
+__global__ __launch_bounds__(128, GSR_BWD2F_MINB) void k_raster2d_bwd_frame(
+    const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const float* __restrict__ anchors, int W, int H,
+    int tw, int th, const float* __restrict__ bg, const float* __restrict__ final_T,
+    const int32_t* __restrict__ last_in, const float* __restrict__ v_rgb, const float* __restrict__ v_alpha,
+    float* __restrict__ partial, const int32_t* __restrict__ units, gsr_bin_stats* __restrict__ stats,
+    const int32_t* __restrict__ k_of_s, float cut2d, const Sets2D sets) {
+  constexpr int kNull = kChunk3;
+  constexpr int kGroup = GSR_BWD_GROUP;
+  static_assert(kGroup == 7 && kPartial == 9, "reduce_grp8 sums 7 entries x 9 values in 64 registers");
+  constexpr int kLen = kChunk3 + kGroup;
+  constexpr int kLenB = 8 * ((kLen + kGroup - 1) / kGroup);
+  __shared__ float4 s_p[3][kChunk3 + 1];
+  __shared__ __attribute__((aligned(16))) float L[kPartial][2][kChunk3 + 1];
+  __shared__ unsigned char s_list[2][kLen];
+  __shared__ __attribute__((aligned(16))) unsigned char s_box[2][8][kLenB];
+  __shared__ __attribute__((aligned(16))) float s_stage[2][8][64];
+  const int4 cd = reinterpret_cast<const int4*>(units)[blockIdx.x];
+  const int n_act = stats->n_active, ovf = stats->overflow, U = stats->chunk_entries;
+  if ((ovf != 0) | ((int)blockIdx.x >= n_act) | (cd.y <= 0)) return;
+  const int start = cd.x, n = cd.y, cbase = cd.z, ct = cd.w;
+  int c, ty, tx;
+  tile_coords(ct, tw, th, c, ty, tx);
+  // the set of camera c: its first camera's workgroup walks the tile for all of its cameras
+  const int f = set_of_camera(sets.begin, sets.F, c);
+  const int cf = sets.begin != nullptr ? sets.begin[f] : 0;
+  const int G = sets.begin != nullptr ? sets.begin[f + 1] - cf : 1;
+  if (c != cf) return;   // (rec_offset2d(c) = 0 below: c is the copy's camera)
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int box = grp8_box(lane), pp = grp8_pos(lane);
+  const int hx0 = tx * kTile, hy0 = ty * kTile + 8 * wv;
+  const int bjl = 4 * (box & 3), bil = 8 * wv + 4 * (box >> 2);
+  const int jl = bjl + (pp & 3), ilA = bil + (pp >> 2), ilB = ilA + 2;
+  const int pj = tx * kTile + jl, piA = ty * kTile + ilA, piB = ty * kTile + ilB;
+  const bool inA = piA < H && pj < W, inB = piB < H && pj < W;
+  const float px = (float)pj, pyA = (float)piA, pyB = (float)piB;
+  const int slotA = bwd_pixel_slot(ilA, jl), slotB = bwd_pixel_slot(ilB, jl);
+  const int64_t HW = (int64_t)H * W;
+  const int64_t pvA = (int64_t)piA * W + pj, pvB = (int64_t)piB * W + pj;   // pixel within a camera's image
+  // the shared forward state (camera cf's; every camera of the set has the same)
+  float TfA = 1.f, TlA = 1.f, TfB = 1.f, TlB = 1.f;
+  int lastA = -1, lastB = -1;
+  if (inA) {
+    lastA = last_in[(int64_t)c * HW + pvA];
+    const float2 t2 = reinterpret_cast<const float2*>(final_T)[(int64_t)c * HW + pvA];
+    TfA = t2.x;
+    TlA = t2.y;
+  }
+  if (inB) {
+    lastB = last_in[(int64_t)c * HW + pvB];
+    const float2 t2 = reinterpret_cast<const float2*>(final_T)[(int64_t)c * HW + pvB];
+    TfB = t2.x;
+    TlB = t2.y;
+  }
+  const int wlast = wave_max_i(max(lastA, lastB));
+  const int fg = lane / kPartial, fq = lane - kPartial * (lane / kPartial);
+  const bool fown = lane < kGroup * kPartial;
+  float* const Lw = &L[fq][wv][0];
+  const float* const stage_rd = &s_stage[wv][0][0];
+  const int obox = grp8_out_box(lane);
+  float* const stage_wr = &s_stage[wv][obox][0];
+  const int wr0 = (8 * grp8_slot(lane)) ^ grp8_swz(obox), wr1 = (8 * grp8_slot(lane) + 4) ^ grp8_swz(obox);
+  const unsigned char* my_list = s_box[wv][box];
+  const float4* const rec4 = reinterpret_cast<const float4*>(rec);
+  const int nsub = (n + kChunk3 - 1) / kChunk3;
+  if (threadIdx.x < 3) s_p[threadIdx.x][kNull] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int u0 = 0; u0 < G; u0 += GB) {
+    // this pass's cameras' cotangents and mu (zero past the set's cameras: exact zero terms)
+    float vrA[GB], vgA[GB], vbA[GB], muA[GB], vrB[GB], vgB[GB], vbB[GB], muB[GB];
+#pragma unroll
+    for (int u = 0; u < GB; ++u) {
+      vrA[u] = vgA[u] = vbA[u] = muA[u] = vrB[u] = vgB[u] = vbB[u] = muB[u] = 0.f;
+      const int cam = cf + u0 + u;
+      if (u0 + u < G) {
+        const float* bgc = bg + cam * 3;
+        if (inA) {
+          const int64_t pix = (int64_t)cam * HW + pvA;
+          vrA[u] = v_rgb[pix * 3 + 0];
+          vgA[u] = v_rgb[pix * 3 + 1];
+          vbA[u] = v_rgb[pix * 3 + 2];
+          muA[u] = bgc[0] * vrA[u] + bgc[1] * vgA[u] + bgc[2] * vbA[u] - v_alpha[pix];
+        }
+        if (inB) {
+          const int64_t pix = (int64_t)cam * HW + pvB;
+          vrB[u] = v_rgb[pix * 3 + 0];
+          vgB[u] = v_rgb[pix * 3 + 1];
+          vbB[u] = v_rgb[pix * 3 + 2];
+          muB[u] = bgc[0] * vrB[u] + bgc[1] * vgB[u] + bgc[2] * vbB[u] - v_alpha[pix];
+        }
+      }
+    }
+    int sb0 = start + (nsub - 1) * kChunk3;
+    int sn = start + n - sb0;
+    const int id_mine = (int)threadIdx.x < sn ? ids[sb0 + threadIdx.x] : 0;
+    int kos_mine = (int)threadIdx.x < sn ? k_of_s[sb0 + threadIdx.x] : 0;
+    float4 sp0 = make_float4(0.f, 0.f, 0.f, 0.f), sp1 = sp0, sp2 = sp0;
+    if ((int)threadIdx.x < sn) {
+      sp0 = rec4[3 * (int64_t)id_mine + 0];
+      sp1 = rec4[3 * (int64_t)id_mine + 1];
+      sp2 = rec4[3 * (int64_t)id_mine + 2];
+    }
+    float TA = TfA, TB = TfB, TnA = TfA, TnB = TfB;
+    for (int sub = nsub - 1; sub >= 0; --sub) {
+      if (sub != nsub - 1 || u0 > 0) __syncthreads();   // the previous sub-chunk's (pass's) LDS is consumed
+      if (sub != nsub - 1 && ((sb0 + sn - start) & (U - 1)) == 0) {   // re-anchor T at a unit boundary
+        TA = TnA;
+        TB = TnB;
+      }
+      if ((int)threadIdx.x < sn) {
+        s_p[0][threadIdx.x] = sp0;
+        s_p[1][threadIdx.x] = sp1;
+        s_p[2][threadIdx.x] = sp2;
+      }
+      for (int i = threadIdx.x; i < kPartial * 2 * (kChunk3 + 1) / 4; i += 128)
+        reinterpret_cast<float4*>(&L[0][0][0])[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (threadIdx.x == 0 && (kPartial * 2 * (kChunk3 + 1)) % 4 != 0)
+        for (int i = kPartial * 2 * (kChunk3 + 1) / 4 * 4; i < kPartial * 2 * (kChunk3 + 1); ++i) (&L[0][0][0])[i] = 0.f;
+      __syncthreads();
+      const int lastqA = lastA - sb0 < kChunk3 ? lastA - sb0 : -1, lastqB = lastB - sb0 < kChunk3 ? lastB - sb0 : -1;
+      int nsurv = 0;
+      {
+        const float x0 = (float)hx0, y0 = (float)hy0;
+#pragma unroll
+        for (int q = kChunk3 / 64 - 1; q >= 0; --q) {
+          const int k = q * 64 + lane;
+          float4 r0 = s_p[0][k], r1 = s_p[1][k], r2 = s_p[2][k];
+          unpack_rec<true>(r0, r1, r2);
+          const bool keep = k < sn && (sb0 + k) <= wlast && cull_keep<true>(r0, r1, r2, x0, x0 + 15.f, y0, y0 + 7.f);
+          const unsigned long long mk = __ballot(keep);
+          if (keep) {
+            const unsigned long long above = lane == 63 ? 0ull : (mk >> (lane + 1));
+            s_list[wv][nsurv + __popcll(above)] = (unsigned char)k;
+          }
+          nsurv += __popcll(mk);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      int nbx[8];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) nbx[b] = 0;
+      {
+        const unsigned long long below = (1ull << lane) - 1ull;
+        for (int s0 = 0; s0 < nsurv; s0 += 64) {
+          const int si = s0 + lane;
+          const bool in = si < nsurv;
+          const int k = s_list[wv][in ? si : 0];
+          float4 r0 = s_p[0][k], r1 = s_p[1][k], r2 = s_p[2][k];
+          unpack_rec<true>(r0, r1, r2);
+#pragma unroll
+          for (int b = 0; b < 8; ++b) {
+            const float x0 = (float)(hx0 + 4 * (b & 3)), y0 = (float)(hy0 + 4 * (b >> 2));
+            const bool keep = in && cull_keep<true>(r0, r1, r2, x0, x0 + 3.f, y0, y0 + 3.f);
+            const unsigned long long m = __ballot(keep);
+            if (keep) s_box[wv][b][grouped_slot(nbx[b] + __popcll(m & below))] = (unsigned char)k;
+            nbx[b] += __popcll(m);
+          }
+        }
+      }
+      int nb = nbx[0], ngrp = nbx[0];
+#pragma unroll
+      for (int b = 1; b < 8; ++b) {
+        nb = box == b ? nbx[b] : nb;
+        ngrp = max(ngrp, nbx[b]);
+      }
+      const int npad = (ngrp + kGroup - 1) / kGroup * kGroup;
+      for (int s = nb + pp; s < npad; s += 8) s_box[wv][box][grouped_slot(s)] = (unsigned char)kNull;
+      __builtin_amdgcn_wave_barrier();
+      for (int g0 = 0, gb = 0; g0 < ngrp; g0 += kGroup, gb += 8) {
+        float acc[64];
+        acc[63] = 0.f;
+        const uint2 w8 = *reinterpret_cast<const uint2*>(my_list + gb);
+        int kk[kGroup];
+#pragma unroll
+        for (int g = 0; g < kGroup; ++g) kk[g] = (int)(((g < 4 ? w8.x : w8.y) >> (8 * (g & 3))) & 0xFFu);
+        float4 n0 = s_p[0][kk[0]], n1 = s_p[1][kk[0]];
+        float n2 = reinterpret_cast<const float*>(&s_p[2][kk[0]])[0];
+#pragma unroll
+        for (int g = 0; g < kGroup; ++g) {
+          const int k = kk[g];
+          const float4 p0 = n0;   // x, y, o, r
+          const float4 p1 = n1;   // a, b, c, g
+          const float cbl = n2;   // blue
+          if (g + 1 < kGroup) {
+            n0 = s_p[0][kk[g + 1]];
+            n1 = s_p[1][kk[g + 1]];
+            n2 = reinterpret_cast<const float*>(&s_p[2][kk[g + 1]])[0];
+          }
+          walk_fence();
+          const float dx = p0.x - px, dyA = p0.y - pyA;
+          const int ks = sb0 + k;
+          float a6, a7, a8, a0, a1, a2, a3, a4, a5;
+          auto pixel = [&](const bool first, float dy, int last, int lastq, float Tl, const float (&vr)[GB],
+                           const float (&vg)[GB], const float (&vb)[GB], float (&mu)[GB], float& T) {
+            auto add = [first](float& a, float x) { a = first ? x : a + x; };
+            // the forward state, once for the set's cameras
+            const float sigma = conic_sigma(p1, dx, dy);
+            const float alpha = p0.z * gauss_exp<true>(sigma);
+            const bool valid = (ks <= last) & (alpha >= cut2d);
+            const float alpha_v = valid ? alpha : 0.f;
+            const float ra = __builtin_amdgcn_rcpf(1.f - alpha_v);
+            T = k == lastq ? Tl : T * ra;
+            const float fac = alpha_v * T;
+            // each camera with its own cotangent: colour partials, dL/d(mu) term, mu recursion
+            float cr = fac * vr[0], cg = fac * vg[0], cb = fac * vb[0];
+            const float cv0 = p0.w * vr[0] + p1.w * vg[0] + cbl * vb[0];
+            float sdmu = cv0 - mu[0];
+            mu[0] = mu[0] + alpha_v * sdmu;
+#pragma unroll
+            for (int u = 1; u < GB; ++u) {
+              cr += fac * vr[u];
+              cg += fac * vg[u];
+              cb += fac * vb[u];
+              const float cv = p0.w * vr[u] + p1.w * vg[u] + cbl * vb[u];
+              const float dmu = cv - mu[u];
+              mu[u] = mu[u] + alpha_v * dmu;
+              sdmu += dmu;
+            }
+            add(a6, cr);
+            add(a7, cg);
+            add(a8, cb);
+            const float v_sig = -alpha_v * (T * sdmu);   // sum over the cameras of -alpha T (c.v - mu)
+            const float tx_ = v_sig * dx, ty_ = v_sig * dy;
+            add(a0, tx_);
+            add(a1, ty_);
+            add(a2, tx_ * dx);
+            add(a3, tx_ * dy);
+            add(a4, ty_ * dy);
+            add(a5, v_sig);
+          };
+          pixel(true, dyA, lastA, lastqA, TlA, vrA, vgA, vbA, muA, TA);
+          pixel(false, p0.y - pyB, lastB, lastqB, TlB, vrB, vgB, vbB, muB, TB);
+          acc[g * kPartial + 0] = a0;
+          acc[g * kPartial + 1] = a1;
+          acc[g * kPartial + 2] = a2;
+          acc[g * kPartial + 3] = a3;
+          acc[g * kPartial + 4] = a4;
+          acc[g * kPartial + 5] = a5;
+          acc[g * kPartial + 6] = a6;
+          acc[g * kPartial + 7] = a7;
+          acc[g * kPartial + 8] = a8;
+        }
+        float sum[8];
+        reduce_grp8(acc, sum);
+        *reinterpret_cast<float4*>(stage_wr + wr0) = make_float4(sum[0], sum[1], sum[2], sum[3]);
+        *reinterpret_cast<float4*>(stage_wr + wr1) = make_float4(sum[4], sum[5], sum[6], sum[7]);
+        __builtin_amdgcn_wave_barrier();
+        if (fown) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            int kb[4];
+            float vb4[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int bx = 4 * h + j;
+              kb[j] = s_box[wv][bx][gb + fg];
+              vb4[j] = stage_rd[64 * bx + (lane ^ grp8_swz(bx))];
+            }
+            lw_add(Lw, kb, vb4);
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      const bool more = sub > 0 && (int)threadIdx.x < kChunk3;
+      const int kos_next = more ? k_of_s[sb0 - kChunk3 + threadIdx.x] : 0;
+      sp0 = sp1 = sp2 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (more) {
+        const int id_next = ids[sb0 - kChunk3 + threadIdx.x];
+        sp0 = rec4[3 * (int64_t)id_next + 0];
+        sp1 = rec4[3 * (int64_t)id_next + 1];
+        sp2 = rec4[3 * (int64_t)id_next + 2];
+      }
+      {
+        const int ue = sb0 - start;
+        const bool anch = sub > 0 && (ue & (U - 1)) == 0;
+        const int64_t arow = (int64_t)(cbase + ue / U) * kRasterThreads;
+        TnA = anch && lastA >= sb0 ? anchors[arow + slotA] : TfA;
+        TnB = anch && lastB >= sb0 ? anchors[arow + slotB] : TfB;
+      }
+      __syncthreads();
+      if ((int)threadIdx.x < sn) {
+        const int k = threadIdx.x;
+        float v[kPartial];
+#pragma unroll
+        for (int q = 0; q < kPartial; ++q) v[q] = L[q][0][k] + L[q][1][k];
+        const float4 p1 = s_p[1][k];
+        const float mx = v[0], my = v[1];
+        v[0] = (2.f * p1.x * mx + p1.y * my) * kLn2;
+        v[1] = (p1.y * mx + 2.f * p1.z * my) * kLn2;
+        v[5] = -v[5] / s_p[0][k].z;
+        if (u0 == 0) {
+          store_partial_row(partial, kos_mine, v);
+        } else {   // a further pass over the set's cameras: this thread wrote the row in the first
+          float* dst = partial + (int64_t)kos_mine * kPartialStride;
+#pragma unroll
+          for (int q = 0; q < kPartial; ++q) dst[q] += v[q];
+        }
+      }
+      sb0 -= kChunk3;
+      sn = kChunk3;
+      kos_mine = kos_next;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- 3D backward, pixel pairs
 // k_raster_bwd (3D, one 128-entry chunk per workgroup, no fused loss, one sub-chunk) with the
 // layout of k_raster2d_bwd_pair: TWO waves per chunk, wave w the 16x8 half-tile of rows
@@ -3089,7 +3413,23 @@ static int raster_bwd(const char* who, const float* rec, const int32_t* sorted_i
     (void)chunk_base;
     (void)lt;
     const int64_t CT = (int64_t)C * tw * th;
-    if (GSR_BWD2D_PAIR)
+    if (rows2d_per_set(sets.begin, sets.F, C)) {
+      // cameras per pass: the set size (its mean over the call's sets), rounded up to 2, 4, 6, 8
+      const int g = (C + sets.F - 1) / sets.F;
+#define GSR_LAUNCH_FRAME(GBV)                                                                                     \
+  hipLaunchKernelGGL(k_raster2d_bwd_frame<GBV>, dim3((unsigned)sweep_grid2d(CT)), dim3(128), 0, (hipStream_t)stream, \
+                     (const Splat*)rec, sorted_ids, chunk_state, width, height, tw, th, bg, final_T, last, v_rgb,      \
+                     v_alpha, partial, chunk_list, stats, k_of_s, cut2d, sets)
+      if (g <= 2)
+        GSR_LAUNCH_FRAME(2);
+      else if (g <= 4)
+        GSR_LAUNCH_FRAME(4);
+      else if (g <= 6)
+        GSR_LAUNCH_FRAME(6);
+      else
+        GSR_LAUNCH_FRAME(8);
+#undef GSR_LAUNCH_FRAME
+    } else if (GSR_BWD2D_PAIR)
       hipLaunchKernelGGL(k_raster2d_bwd_pair, dim3((unsigned)sweep_grid2d(CT)), dim3(128), 0,
                          (hipStream_t)stream, (const Splat*)rec, sorted_ids, chunk_state, width, height, tw, th, bg,
                          final_T, last, v_rgb, v_alpha, partial, chunk_list, stats, k_of_s, cut2d, sets);
