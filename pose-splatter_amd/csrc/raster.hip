@@ -2533,6 +2533,15 @@ __global__ __launch_bounds__(128, GSR_BWD2P_MINB) void k_raster2d_bwd_pair(
 // tests/test_multiframe_gpu.py checks it).  GB cameras are walked per pass (registers: 8 per
 // camera and lane); a set with more walks its tile again per further GB cameras, adding to its
 // rows.  A set of one camera (GB = 1) is k_raster2d_bwd_pair's arithmetic exactly.
+// pairwise sum of K values (a tree of independent adds; K = 1: the value itself)
+template <int K>
+__device__ __forceinline__ float pair_sum(const float* v) {
+  if constexpr (K == 1) {
+    return v[0];
+  } else {
+    return pair_sum<K / 2>(v) + pair_sum<K - K / 2>(v + K / 2);
+  }
+}
 #ifndef GSR_BWD2F_MINB
 #define GSR_BWD2F_MINB 2   // waves per SIMD the compiler aims at (the per-camera state: 8 x GB VGPRs)
 #endif
@@ -2627,6 +2636,8 @@ __global__ __launch_bounds__(128, GSR_BWD2F_MINB) void k_raster2d_bwd_frame(
         }
       }
     }
+    const float VrA = pair_sum<GB>(vrA), VgA = pair_sum<GB>(vgA), VbA = pair_sum<GB>(vbA);
+    const float VrB = pair_sum<GB>(vrB), VgB = pair_sum<GB>(vgB), VbB = pair_sum<GB>(vbB);
     int sb0 = start + (nsub - 1) * kChunk3;
     int sn = start + n - sb0;
     const int id_mine = (int)threadIdx.x < sn ? ids[sb0 + threadIdx.x] : 0;
@@ -2728,7 +2739,8 @@ __global__ __launch_bounds__(128, GSR_BWD2F_MINB) void k_raster2d_bwd_frame(
           const int ks = sb0 + k;
           float a6, a7, a8, a0, a1, a2, a3, a4, a5;
           auto pixel = [&](const bool first, float dy, int last, int lastq, float Tl, const float (&vr)[GB],
-                           const float (&vg)[GB], const float (&vb)[GB], float (&mu)[GB], float& T) {
+                           const float (&vg)[GB], const float (&vb)[GB], float (&mu)[GB], float& T, float Vr,
+                           float Vg, float Vb) {
             auto add = [first](float& a, float x) { a = first ? x : a + x; };
             // the forward state, once for the set's cameras
             const float sigma = conic_sigma(p1, dx, dy);
@@ -2738,24 +2750,20 @@ __global__ __launch_bounds__(128, GSR_BWD2F_MINB) void k_raster2d_bwd_frame(
             const float ra = __builtin_amdgcn_rcpf(1.f - alpha_v);
             T = k == lastq ? Tl : T * ra;
             const float fac = alpha_v * T;
-            // each camera with its own cotangent: colour partials, dL/d(mu) term, mu recursion
-            float cr = fac * vr[0], cg = fac * vg[0], cb = fac * vb[0];
-            const float cv0 = p0.w * vr[0] + p1.w * vg[0] + cbl * vb[0];
-            float sdmu = cv0 - mu[0];
-            mu[0] = mu[0] + alpha_v * sdmu;
+            // each camera with its own cotangent: its colour dot product, dL/d(mu) term and mu
+            // recursion; the terms summed pairwise (independent chains, not one serial sum)
+            float dmu[GB];
 #pragma unroll
-            for (int u = 1; u < GB; ++u) {
-              cr += fac * vr[u];
-              cg += fac * vg[u];
-              cb += fac * vb[u];
+            for (int u = 0; u < GB; ++u) {
               const float cv = p0.w * vr[u] + p1.w * vg[u] + cbl * vb[u];
-              const float dmu = cv - mu[u];
-              mu[u] = mu[u] + alpha_v * dmu;
-              sdmu += dmu;
+              dmu[u] = cv - mu[u];
+              mu[u] = mu[u] + alpha_v * dmu[u];
             }
-            add(a6, cr);
-            add(a7, cg);
-            add(a8, cb);
+            const float sdmu = pair_sum<GB>(dmu);
+            // colour partials: alpha T times the cameras' summed colour cotangent
+            add(a6, fac * Vr);
+            add(a7, fac * Vg);
+            add(a8, fac * Vb);
             const float v_sig = -alpha_v * (T * sdmu);   // sum over the cameras of -alpha T (c.v - mu)
             const float tx_ = v_sig * dx, ty_ = v_sig * dy;
             add(a0, tx_);
@@ -2765,8 +2773,8 @@ __global__ __launch_bounds__(128, GSR_BWD2F_MINB) void k_raster2d_bwd_frame(
             add(a4, ty_ * dy);
             add(a5, v_sig);
           };
-          pixel(true, dyA, lastA, lastqA, TlA, vrA, vgA, vbA, muA, TA);
-          pixel(false, p0.y - pyB, lastB, lastqB, TlB, vrB, vgB, vbB, muB, TB);
+          pixel(true, dyA, lastA, lastqA, TlA, vrA, vgA, vbA, muA, TA, VrA, VgA, VbA);
+          pixel(false, p0.y - pyB, lastB, lastqB, TlB, vrB, vgB, vbB, muB, TB, VrB, VgB, VbB);
           acc[g * kPartial + 0] = a0;
           acc[g * kPartial + 1] = a1;
           acc[g * kPartial + 2] = a2;
