@@ -2550,8 +2550,9 @@ __global__ __launch_bounds__(128, GSR_BWD2F_MINB) void k_raster2d_bwd_frame(
     const Splat* __restrict__ rec, const int32_t* __restrict__ ids, const float* __restrict__ anchors, int W, int H,
     int tw, int th, const float* __restrict__ bg, const float* __restrict__ final_T,
     const int32_t* __restrict__ last_in, const float* __restrict__ v_rgb, const float* __restrict__ v_alpha,
-    float* __restrict__ partial, const int32_t* __restrict__ units, gsr_bin_stats* __restrict__ stats,
-    const int32_t* __restrict__ k_of_s, float cut2d, const Sets2D sets) {
+    float* __restrict__ partial, const int32_t* __restrict__ tile_offset, const int32_t* __restrict__ tile_end,
+    const int32_t* __restrict__ chunk_base, gsr_bin_stats* __restrict__ stats, const int32_t* __restrict__ k_of_s,
+    float cut2d, const Sets2D sets) {
   constexpr int kNull = kChunk3;
   constexpr int kGroup = GSR_BWD_GROUP;
   static_assert(kGroup == 7 && kPartial == 9, "reduce_grp8 sums 7 entries x 9 values in 64 registers");
@@ -2562,17 +2563,27 @@ __global__ __launch_bounds__(128, GSR_BWD2F_MINB) void k_raster2d_bwd_frame(
   __shared__ unsigned char s_list[2][kLen];
   __shared__ __attribute__((aligned(16))) unsigned char s_box[2][8][kLenB];
   __shared__ __attribute__((aligned(16))) float s_stage[2][8][64];
-  const int4 cd = reinterpret_cast<const int4*>(units)[blockIdx.x];
-  const int n_act = stats->n_active, ovf = stats->overflow, U = stats->chunk_entries;
-  if ((ovf != 0) | ((int)blockIdx.x >= n_act) | (cd.y <= 0)) return;
-  const int start = cd.x, n = cd.y, cbase = cd.z, ct = cd.w;
-  int c, ty, tx;
-  tile_coords(ct, tw, th, c, ty, tx);
-  // the set of camera c: its first camera's workgroup walks the tile for all of its cameras
-  const int f = set_of_camera(sets.begin, sets.F, c);
+  // One workgroup per (set, tile), XCD-aware: workgroup b runs on XCD b % 8 and takes position
+  // (b % 8) * S + b / 8 of the (set, tile row, tile column) order, so each XCD walks its eighth
+  // of it in order and a set's records come into its L2 about once.  (A grid of every camera's
+  // tile slot with the other cameras' workgroups exiting put all the working ones on every
+  // other CU -- the slots are dealt to an XCD's CUs in turn: half the chip idle.)
+  const int T = tw * th;
+  const int64_t FT = (int64_t)sets.F * T;
+  const int64_t S = (FT + 7) / 8;
+  const int64_t pos = (int64_t)(blockIdx.x & 7) * S + (blockIdx.x >> 3);
+  const int ovf = stats->overflow, U = stats->chunk_entries;
+  if ((ovf != 0) | (pos >= FT)) return;
+  const int f = (int)(pos / T), t = (int)(pos - (int64_t)f * T);
   const int cf = sets.begin != nullptr ? sets.begin[f] : 0;
   const int G = sets.begin != nullptr ? sets.begin[f + 1] - cf : 1;
-  if (c != cf) return;   // (rec_offset2d(c) = 0 below: c is the copy's camera)
+  if (G <= 0) return;   // a set no camera renders
+  const int ct = cf * T + t;
+  const int start = tile_offset[ct], te = tile_end[ct], cbase = chunk_base[ct];
+  const int n = te - start;   // the consumed list [start, tile_end) (k_raster_finalize)
+  if (n <= 0) return;
+  int c, ty, tx;
+  tile_coords(ct, tw, th, c, ty, tx);   // (c = cf: the set's record copy, rec_offset2d = 0)
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int box = grp8_box(lane), pp = grp8_pos(lane);
   const int hx0 = tx * kTile, hy0 = ty * kTile + 8 * wv;
@@ -3424,10 +3435,12 @@ static int raster_bwd(const char* who, const float* rec, const int32_t* sorted_i
     if (rows2d_per_set(sets.begin, sets.F, C)) {
       // cameras per pass: the set size (its mean over the call's sets), rounded up to 2, 4, 6, 8
       const int g = (C + sets.F - 1) / sets.F;
-#define GSR_LAUNCH_FRAME(GBV)                                                                                     \
-  hipLaunchKernelGGL(k_raster2d_bwd_frame<GBV>, dim3((unsigned)sweep_grid2d(CT)), dim3(128), 0, (hipStream_t)stream, \
-                     (const Splat*)rec, sorted_ids, chunk_state, width, height, tw, th, bg, final_T, last, v_rgb,      \
-                     v_alpha, partial, chunk_list, stats, k_of_s, cut2d, sets)
+      const int64_t FT = (int64_t)sets.F * tw * th;
+#define GSR_LAUNCH_FRAME(GBV)                                                                                       \
+  hipLaunchKernelGGL(k_raster2d_bwd_frame<GBV>, dim3((unsigned)(8 * ((FT + 7) / 8))), dim3(128), 0,                   \
+                     (hipStream_t)stream, (const Splat*)rec, sorted_ids, chunk_state, width, height, tw, th, bg,      \
+                     final_T, last, v_rgb, v_alpha, partial, tile_offset, tile_end, chunk_base, stats, k_of_s, cut2d, \
+                     sets)
       if (g <= 2)
         GSR_LAUNCH_FRAME(2);
       else if (g <= 4)

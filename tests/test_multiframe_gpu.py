@@ -22,7 +22,11 @@ def _frames(F, N, W, H, seed):
     return torch.stack([gaussians2d(N, W, H, seed + f) for f in range(F)])
 
 
-@pytest.mark.parametrize("sets", [(0, 0, 1, 2, 2, 2), (0, 2, 2), (1,)])
+# (0, 0, 1, 2, 2, 2): 6 cameras over 3 sets -> the per-set backward (k_raster2d_bwd_frame, two
+# cameras per pass: set 2 takes a second pass, set 1 a padded one); (0, 0, 2, 2, 2): the same
+# with a set no camera renders; (0, 2, 2) and (1,): one camera per set on average -> the
+# per-camera backward (k_raster2d_bwd_pair)
+@pytest.mark.parametrize("sets", [(0, 0, 1, 2, 2, 2), (0, 0, 2, 2, 2), (0, 2, 2), (1,)])
 def test_units_match_single_renders(cuda, sets):
     from gsr import render as R
     F, N, W, H = 3, 1200, 96, 80
