@@ -147,40 +147,46 @@ def parse(argv=None):
 
 # ------------------------------------------------------------------ algorithmic bytes (§8(d))
 
-def algorithmic_bytes(kernel: str, C: int, N: int, P: int, I: int, I_eff: int, p: int) -> float:
+def algorithmic_bytes(kernel: str, C: int, N: int, P: int, I: int, I_eff: int, p: int, rows: int | None = None) -> float:
     """Per-launch algorithmic bytes, SURVEY.md §8(d) per-unit figures x the units one launch
     processes: C cameras (units) x N Gaussians projected, P pixels, I intersections, I_eff
-    list entries read by the raster."""
+    list entries read by the raster.  rows: the (unit, Gaussian) reduced gradient rows the
+    backward passes on when fewer than C (2D with several units per parameter set: one row per
+    (set, Gaussian), k_raster2d_bwd_frame)."""
+    R = C if rows is None else rows
     if kernel.startswith("raster") and kernel.endswith("_fwd"):
         return 40.0 * I_eff + 20.0 * P                 # read id+xy+conic+opac+colour; write rgb+alpha+last
     if kernel.startswith("raster") and kernel.endswith("_bwd"):
-        return 24.0 * P + 40.0 * I_eff + 36.0 * C * N  # cotangents+alpha+last; list; reduced grads
+        return 24.0 * P + 40.0 * I_eff + 36.0 * R * N  # cotangents+alpha+last; list; reduced grads
     if kernel.startswith("project") and kernel.endswith("_fwd"):
         return C * N * (4.0 * p + 32.0)
     if kernel.startswith("project") and kernel.endswith("_bwd"):
-        return N * (36.0 + 32.0 + 8.0 * p) * C
+        return N * (36.0 * R + (32.0 + 8.0 * p) * C)
     if kernel == "bin_sort":
         return 36.0 * I
     return 0.0
 
 
-def step_bytes(C: int, N: int, P: int, I: int, I_eff: int, p: int, backward: bool = True, sets: int | None = None) -> float:
+def step_bytes(C: int, N: int, P: int, I: int, I_eff: int, p: int, backward: bool = True, sets: int | None = None,
+               rows: int | None = None) -> float:
     """Whole launch sequence, SURVEY.md §8(d) (P = all pixels of the C units):
     fwd+bwd C*N*(12p+136) + 36*I + 80*I_eff + 44*P; fwd-only C*N*(4p+32) + 36*I + 40*I_eff + 20*P.
     sets: the projections the sequence runs when fewer than C (2D: one per parameter set, the
     frames of the units -- VERDICT r4: config 4 charged its 8 frames' projection 48 times).  The
     per-projection part (params read, record written, params read again, gradient written:
-    N*(12p+64)) is then charged `sets` times; the per-(unit, Gaussian) reduced rows (72 B: written
-    by the raster backward, read by the projection backward) still C times."""
+    N*(12p+64)) is then charged `sets` times; the reduced rows (72 B per (unit, Gaussian): written
+    by the raster backward, read by the projection backward) `rows` times (default C; 2D with
+    several units per set: one per (set, Gaussian), the rows k_raster2d_bwd_frame passes on)."""
     S = C if sets is None else sets
+    R = C if rows is None else rows
     if not backward:
         return S * N * (4.0 * p + 32.0) + 36.0 * I + 40.0 * I_eff + 20.0 * P
-    return S * N * (12.0 * p + 64.0) + C * N * 72.0 + 36.0 * I + 80.0 * I_eff + 44.0 * P
+    return S * N * (12.0 * p + 64.0) + R * N * 72.0 + 36.0 * I + 80.0 * I_eff + 44.0 * P
 
 
 # libgsr call name (render.py timing brackets) -> substring of its dominant kernel's symbol
 KERNEL_SYMBOL = {"raster3d_bwd": "k_raster_bwd", "raster3d_fwd": "k_raster_fwd<false,",
-                 "raster2d_bwd": "k_raster2d_bwd_pair", "raster2d_fwd": "k_raster2d_fwd_pair",
+                 "raster2d_bwd": "k_raster2d_bwd_", "raster2d_fwd": "k_raster2d_fwd_pair",
                  "bin_sort": "k_segsort", "project3d_fwd": "k_project3d_fwd", "project3d_bwd": "k_project3d_bwd",
                  "project2d_fwd": "k_project2d_fwd", "project2d_bwd": "k_project2d_bwd", "bin_emit": "k_emit"}
 
@@ -760,6 +766,15 @@ class Workload:
         nb = self.buckets if self.comm else 1
         return max(1, math.ceil(frames / max(nb, 1)))
 
+    def rows_per_launch(self, C: int):
+        """Reduced gradient rows one launch's backward passes on: one per (unit, Gaussian), except
+        2D with more units than parameter sets in the launch, whose backward walks each set once
+        for all its units and writes one row per (set, Gaussian) (libgsr rows2d_per_set)."""
+        if self.cfg.mode != "2d":
+            return C
+        F = int(self.params_cpu.shape[0])
+        return self.sets_per_launch(C) if C > F else C
+
     def launch_shape(self):
         """(C, P) of the dominant launch sequence: cameras and pixels one launch covers."""
         cfg = self.cfg
@@ -894,7 +909,7 @@ def roofline(w: Workload, dom_name, dom, args):
     I, I_eff = st.get("n_isect", 0), R.effective_isect()
     C, P = w.launch_shape()
     dom_ms, dom_n = dom
-    alg = algorithmic_bytes(dom_name or "", C, cfg.N, P, I, I_eff, w.p_dim)
+    alg = algorithmic_bytes(dom_name or "", C, cfg.N, P, I, I_eff, w.p_dim, rows=w.rows_per_launch(C))
     achieved = alg / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     sym = KERNEL_SYMBOL.get(dom_name, "k_" + str(dom_name))
     tfile = pmc_files(cfg.index, "traffic", args.pmc_dir) if dom_name else None
@@ -1136,7 +1151,8 @@ def main(argv=None):
     value = timing["value"]
     ms_per_step = timing["ms_per_step"]
     roof, (C, P, I, I_eff) = roofline(w, dom_name, dom, args)
-    sb = step_bytes(C, cfg.N, P, I, I_eff, w.p_dim, cfg.backward, sets=w.sets_per_launch(C))
+    sb = step_bytes(C, cfg.N, P, I, I_eff, w.p_dim, cfg.backward, sets=w.sets_per_launch(C),
+                    rows=w.rows_per_launch(C))
     launches_per_step = max(1, math.ceil(w.views_here / C)) if C else 1
     out = {
         "metric": "rendered frames/sec (%s) at N_gauss x H x W" % ("fwd+bwd" if cfg.backward else "fwd"),
