@@ -59,6 +59,12 @@
  *   d/dx, d/dy, d/da, d/db, d/dc, d/dopacity, d/drgb[3] (36 B, summed over the 16x16
  *   tile's pixels) — a deterministic replacement for float atomics.  Only entries before
  *   their tile's cut (see tile_cut) are written; the others are never read.
+ *   2D with more cameras than parameter sets (C > F, set_begin given; round 5, revision 12
+ *   kept): the cameras of a set render the same image (views are ignored), so
+ *   gsr2d_raster_bwd walks each (set, tile) once for all the set's cameras, each with its own
+ *   cotangent, and writes the set's SUMMED row at its first camera's emission index only;
+ *   gsr2d_project_bwd, called with the same C / F / set_begin, reads only those rows.  The
+ *   other cameras' rows are left unwritten.  A caller that pairs the two calls sees no change.
  */
 #ifndef GSR_H
 #define GSR_H
