@@ -1190,8 +1190,9 @@ def main(argv=None):
         "step_roofline": {"algorithmic_bytes": sb * launches_per_step,
                           "achieved": sb * launches_per_step / (ms_per_step * 1e-3) / 1e9,
                           "unit": "GB/s", "frac": sb * launches_per_step / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                          "formula": ("SURVEY.md 8(d): S*N*(12p+64) + C*N*72 + 36*I + 80*I_eff + 44*P per rank "
-                                      "(S = projections: C in 3D, the frames in 2D)" if cfg.backward
+                          "formula": ("SURVEY.md 8(d): S*N*(12p+64) + R*N*72 + 36*I + 80*I_eff + 44*P per rank "
+                                      "(S = projections: C in 3D, the frames in 2D; R = reduced gradient rows: C, or "
+                                      "the frames in 2D when a frame's units share one backward walk)" if cfg.backward
                                       else "SURVEY.md 8(d) fwd-only: C*N*(4p+32) + 36*I + 40*I_eff + 20*P per rank")},
         "binning": {"I": I, "I_eff": I_eff, "max_list": R.last_stats().get("max_seg"),
                     "busy_tiles": R.last_stats().get("n_busy"), "tiles": R.last_stats().get("tiles")},
