@@ -147,15 +147,18 @@ def parse(argv=None):
 
 # ------------------------------------------------------------------ algorithmic bytes (§8(d))
 
-def algorithmic_bytes(kernel: str, C: int, N: int, P: int, I: int, I_eff: int, p: int, rows: int | None = None) -> float:
+def algorithmic_bytes(kernel: str, C: int, N: int, P: int, I: int, I_eff: int, p: int, rows: int | None = None,
+                      fwd_walks: float = 1.0) -> float:
     """Per-launch algorithmic bytes, SURVEY.md §8(d) per-unit figures x the units one launch
     processes: C cameras (units) x N Gaussians projected, P pixels, I intersections, I_eff
     list entries read by the raster.  rows: the (unit, Gaussian) reduced gradient rows the
     backward passes on when fewer than C (2D with several units per parameter set: one row per
-    (set, Gaussian), k_raster2d_bwd_frame)."""
+    (set, Gaussian), k_raster2d_bwd_frame).  fwd_walks: how many units walk each list in the
+    forward (2D shared lists: a set's units all render its first unit's list, while I_eff counts
+    that list once)."""
     R = C if rows is None else rows
     if kernel.startswith("raster") and kernel.endswith("_fwd"):
-        return 40.0 * I_eff + 20.0 * P                 # read id+xy+conic+opac+colour; write rgb+alpha+last
+        return 40.0 * I_eff * fwd_walks + 20.0 * P     # read id+xy+conic+opac+colour; write rgb+alpha+last
     if kernel.startswith("raster") and kernel.endswith("_bwd"):
         return 24.0 * P + 40.0 * I_eff + 36.0 * R * N  # cotangents+alpha+last; list; reduced grads
     if kernel.startswith("project") and kernel.endswith("_fwd"):
@@ -168,7 +171,7 @@ def algorithmic_bytes(kernel: str, C: int, N: int, P: int, I: int, I_eff: int, p
 
 
 def step_bytes(C: int, N: int, P: int, I: int, I_eff: int, p: int, backward: bool = True, sets: int | None = None,
-               rows: int | None = None) -> float:
+               rows: int | None = None, fwd_walks: float = 1.0) -> float:
     """Whole launch sequence, SURVEY.md §8(d) (P = all pixels of the C units):
     fwd+bwd C*N*(12p+136) + 36*I + 80*I_eff + 44*P; fwd-only C*N*(4p+32) + 36*I + 40*I_eff + 20*P.
     sets: the projections the sequence runs when fewer than C (2D: one per parameter set, the
@@ -180,8 +183,8 @@ def step_bytes(C: int, N: int, P: int, I: int, I_eff: int, p: int, backward: boo
     S = C if sets is None else sets
     R = C if rows is None else rows
     if not backward:
-        return S * N * (4.0 * p + 32.0) + 36.0 * I + 40.0 * I_eff + 20.0 * P
-    return S * N * (12.0 * p + 64.0) + R * N * 72.0 + 36.0 * I + 80.0 * I_eff + 44.0 * P
+        return S * N * (4.0 * p + 32.0) + 36.0 * I + 40.0 * I_eff * fwd_walks + 20.0 * P
+    return S * N * (12.0 * p + 64.0) + R * N * 72.0 + 36.0 * I + 40.0 * I_eff * (fwd_walks + 1.0) + 44.0 * P
 
 
 # libgsr call name (render.py timing brackets) -> substring of its dominant kernel's symbol
@@ -775,6 +778,13 @@ class Workload:
         F = int(self.params_cpu.shape[0])
         return self.sets_per_launch(C) if C > F else C
 
+    def fwd_walks(self, C: int) -> float:
+        """Units walking each list in the forward: 2D with more units than sets binds only each
+        set's first unit and all its units render that list (libgsr lists2d_per_set), so the
+        list entries I_eff counts are walked units / sets times; else 1."""
+        r = self.rows_per_launch(C)
+        return C / r if r < C else 1.0
+
     def launch_shape(self):
         """(C, P) of the dominant launch sequence: cameras and pixels one launch covers."""
         cfg = self.cfg
@@ -909,7 +919,8 @@ def roofline(w: Workload, dom_name, dom, args):
     I, I_eff = st.get("n_isect", 0), R.effective_isect()
     C, P = w.launch_shape()
     dom_ms, dom_n = dom
-    alg = algorithmic_bytes(dom_name or "", C, cfg.N, P, I, I_eff, w.p_dim, rows=w.rows_per_launch(C))
+    alg = algorithmic_bytes(dom_name or "", C, cfg.N, P, I, I_eff, w.p_dim, rows=w.rows_per_launch(C),
+                            fwd_walks=w.fwd_walks(C))
     achieved = alg / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     sym = KERNEL_SYMBOL.get(dom_name, "k_" + str(dom_name))
     tfile = pmc_files(cfg.index, "traffic", args.pmc_dir) if dom_name else None
@@ -1152,7 +1163,7 @@ def main(argv=None):
     ms_per_step = timing["ms_per_step"]
     roof, (C, P, I, I_eff) = roofline(w, dom_name, dom, args)
     sb = step_bytes(C, cfg.N, P, I, I_eff, w.p_dim, cfg.backward, sets=w.sets_per_launch(C),
-                    rows=w.rows_per_launch(C))
+                    rows=w.rows_per_launch(C), fwd_walks=w.fwd_walks(C))
     launches_per_step = max(1, math.ceil(w.views_here / C)) if C else 1
     out = {
         "metric": "rendered frames/sec (%s) at N_gauss x H x W" % ("fwd+bwd" if cfg.backward else "fwd"),

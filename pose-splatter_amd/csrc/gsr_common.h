@@ -479,6 +479,11 @@ __device__ __forceinline__ int set_first_camera(const int32_t* __restrict__ set_
 inline bool rows2d_per_set(const int32_t* set_begin, int F, int C) {
   return GSR_BWD2D_FRAME && set_begin != nullptr && C > F;
 }
+// ... and, under the same rule with the automatic 2D forward layout (raster.hip), the binning
+// emits only each set's first camera's lists (its cameras' lists would be identical copies): the
+// projection gives the other cameras no tiles, and their forwards render the first camera's
+// list (k_raster2d_fwd_pair).  Host-side: it reads the forward-layout setting.
+bool lists2d_per_set(const int32_t* set_begin, int F, int C);
 
 // 2D: the record of entry id = c*N + n lives in the copy of camera c's set's first camera
 // (k_project2d_fwd writes one copy per set): rec[id + rec_offset2d(c)].

@@ -207,7 +207,8 @@ __global__ __launch_bounds__(kProjThreads) void k_project2d_fwd(
     const float* __restrict__ params, int64_t N, int64_t stride, int64_t set_stride,
     const int32_t* __restrict__ set_begin, int F, int C, int W, int H, float eps_cut,
     int tw, int th, int use_lds, Splat* __restrict__ rec, uint2* __restrict__ rect,
-    int32_t* __restrict__ cnt, int32_t* __restrict__ tile_count, int32_t* __restrict__ isect_offset) {
+    int32_t* __restrict__ cnt, int32_t* __restrict__ tile_count, int32_t* __restrict__ isect_offset,
+    int share_lists) {
   extern __shared__ int hist[];
   __shared__ int s_cnt[kProjPerBlock];
   const int c = blockIdx.y;
@@ -216,6 +217,8 @@ __global__ __launch_bounds__(kProjThreads) void k_project2d_fwd(
   int32_t* counter = tile_count + (int64_t)C * T;
   const float* pset = params + (int64_t)set_of_camera(set_begin, F, c) * set_stride;
   const bool rec_owner = set_first_camera(set_begin, F, c) == c;
+  // lists2d_per_set: only the set's first camera gets tiles (the others render its lists)
+  const bool binned = rec_owner || !share_lists;
   if (use_lds) {
     for (int t = threadIdx.x; t < T; t += blockDim.x) hist[t] = 0;
     __syncthreads();
@@ -226,7 +229,7 @@ __global__ __launch_bounds__(kProjThreads) void k_project2d_fwd(
     const int64_t cn = (int64_t)c * N + n;
     const Geo2D g = geo2d(pset + n * stride);
     int x0 = 0, x1 = 0, y0 = 0, y1 = 0;
-    bool ok = g.op > eps_cut && isfinite(g.u) && isfinite(g.v);
+    bool ok = binned && g.op > eps_cut && isfinite(g.u) && isfinite(g.v);
     if (ok) {
       // q <= L = ln(op/eps) ellipse; its AABB half-extents: sqrt(L * (Minv)_xx), Minv =
       // R^T diag(1/ia, 1/ib) R.  Slightly inflated so the cut never drops g >= eps_cut.
@@ -363,7 +366,8 @@ int gsr2d_project_fwd(const float* params, int64_t N, int64_t row_stride, int64_
   const size_t lds = use_lds ? (size_t)T * sizeof(int) : 0;
   hipLaunchKernelGGL(k_project2d_fwd, dim3(ceil_div(N, kProjPerBlock), C), dim3(kProjThreads), lds,
                      (hipStream_t)stream, params, N, row_stride, set_stride, set_begin, F, C, width, height,
-                     eps_cut, tw, th, use_lds, (Splat*)rec, (uint2*)rect, isect_count, tile_count, isect_offset);
+                     eps_cut, tw, th, use_lds, (Splat*)rec, (uint2*)rect, isect_count, tile_count, isect_offset,
+                     lists2d_per_set(set_begin, F, C) ? 1 : 0);
   GSR_LAUNCH_CHECK("k_project2d_fwd");
   return GSR_OK;
 }

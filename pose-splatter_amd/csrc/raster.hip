@@ -1222,7 +1222,7 @@ __global__ __launch_bounds__(128, GSR_FWD2P_MINB) void k_raster2d_fwd_pair(
     int H, int tw, int th, const float* __restrict__ bg, float* __restrict__ out_rgb, float* __restrict__ out_alpha,
     float* __restrict__ out_T, int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end,
     float* __restrict__ anchors, const int32_t* __restrict__ chunk_base, int64_t CT, float cut2d,
-    const gsr_bin_stats* __restrict__ stats, const Sets2D sets) {
+    const gsr_bin_stats* __restrict__ stats, const Sets2D sets, int share_lists) {
   constexpr int kHS = kChunk3 + 1;   // part j of round entry k at s_r[buf][j][k]; slot 128 a zero record
   __shared__ float4 s_r[2][3][kHS];
   __shared__ __attribute__((aligned(16))) unsigned char s_box[2][8][kBoxStride];
@@ -1238,7 +1238,9 @@ __global__ __launch_bounds__(128, GSR_FWD2P_MINB) void k_raster2d_fwd_pair(
   if (ct < 0) return;
   int c, ty, tx;
   tile_coords(ct, tw, th, c, ty, tx);
-  rec += rec_offset2d(sets.begin, sets.F, c, sets.N);   // the set's record copy
+  // the set's record copy: entry ids of camera c's own list are c*N + n, of a shared list (the
+  // set's first camera's, lists2d_per_set) already cf*N + n
+  if (!share_lists) rec += rec_offset2d(sets.begin, sets.F, c, sets.N);
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int grp = ((lane >> 4) & 2) | (((lane >> 4) ^ (lane >> 3) ^ (lane >> 2)) & 1);   // b128 lane group
   const int box = 2 * grp + ((lane >> 4) & 1);
@@ -1251,7 +1253,15 @@ __global__ __launch_bounds__(128, GSR_FWD2P_MINB) void k_raster2d_fwd_pair(
   asm volatile("" : "+v"(px), "+v"(pyA), "+v"(pyB));
   const int slotA = bwd_pixel_slot(ilA, jl), slotB = bwd_pixel_slot(ilB, jl);
   const int hx0 = tx * kTile, hy0 = ty * kTile + 8 * wv;   // the wave's half-tile origin
-  const int start = tile_offset[ct], end = tile_offset[ct + 1];
+  // lists2d_per_set: every camera of the set renders its first camera's list of this tile; only
+  // that camera writes the T anchors and tile_end (the others have no chunk rows; theirs would
+  // be the same values), and the backward reads that camera's state (k_raster2d_bwd_frame)
+  const int T = tw * th;
+  const int cfirst = share_lists ? set_first_camera(sets.begin, sets.F, c) : c;
+  const int ctl = cfirst * T + (ct - c * T);
+  const bool lead = cfirst == c;
+  if (!lead) anchors = nullptr;
+  const int start = tile_offset[ctl], end = tile_offset[ctl + 1];
   if (tid == 0) s_max = -1;
   float TA = 1.f, TlA = 1.f, crA = 0.f, cgA = 0.f, cbA = 0.f, drA = 0.f, dgA = 0.f, dbA = 0.f;
   float TB = 1.f, TlB = 1.f, crB = 0.f, cgB = 0.f, cbB = 0.f, drB = 0.f, dgB = 0.f, dbB = 0.f;
@@ -1414,7 +1424,8 @@ __global__ __launch_bounds__(128, GSR_FWD2P_MINB) void k_raster2d_fwd_pair(
   const int lmax = max(lastA, lastB);
   if (lmax >= 0) atomicMax(&s_max, lmax);
   __syncthreads();
-  if (tid == 0 && s_max >= 0) tile_end[ct] = s_max;   // one workgroup per tile; finalised by k_raster_finalize
+  // one workgroup per tile; finalised by k_raster_finalize
+  if (tid == 0 && s_max >= 0 && lead) tile_end[ct] = s_max;
 }
 
 // Per busy tile: tile_end = 1 + max last over the tile's four quadrant workgroups (or the
@@ -3272,6 +3283,9 @@ namespace gsr {
 // runs (bitwise-equal results; round 4 chose by the count, which a varying Gaussian count moved
 // across the threshold in one call and not in the other, tests/test_headline_mode_gpu.py).
 constexpr int64_t kFwd16MaxTiles = 320;
+bool lists2d_per_set(const int32_t* set_begin, int F, int C) {
+  return GSR_FWD2D_PAIR && g_fwd_lanes == 0 && rows2d_per_set(set_begin, F, C);
+}
 static int fwd_lanes(bool is2d, int64_t CT) {
   if (g_fwd_lanes == 1 || g_fwd_lanes == 4 || (g_fwd_lanes == 16 && !is2d)) return g_fwd_lanes;
   if (is2d) return 1;
@@ -3368,7 +3382,8 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
     // 2D: every tile in the XCD-aware sweep, two pixels per lane
     hipLaunchKernelGGL(k_raster2d_fwd_pair, dim3((unsigned)sweep_grid2d(CT)), dim3(128), 0, s, (const Splat*)rec,
                        sorted_ids, tile_offset, width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end,
-                       (float*)chunk_state, chunk_base, CT, cut2d, stats, sets);
+                       (float*)chunk_state, chunk_base, CT, cut2d, stats, sets,
+                       lists2d_per_set(sets.begin, sets.F, C) ? 1 : 0);
   } else {
     // 2D: every tile in the XCD-aware sweep (no separate empty-tile fill)
     const int64_t grid = IS2D ? (int64_t)sweep_grid2d(CT) : ((n_busy + 7) & ~7) + n_fill;

@@ -69,6 +69,10 @@ def test_byte_formulas_and_allreduce_model():
     assert bench.step_bytes(48, 10, 100, 7, 5, 9, sets=8, rows=8) == (8 * 10 * (12 * 9 + 64) + 8 * 10 * 72 + 36 * 7
                                                                       + 80 * 5 + 44 * 100)
     assert bench.algorithmic_bytes("raster2d_bwd", 48, 10, 100, 7, 5, 9, rows=8) == 24 * 100 + 40 * 5 + 36 * 8 * 10
+    # ... and its lists walked by all six units of a set in the forward (shared lists)
+    assert bench.step_bytes(48, 10, 100, 7, 5, 9, sets=8, rows=8, fwd_walks=6.0) == (
+        8 * 10 * (12 * 9 + 64) + 8 * 10 * 72 + 36 * 7 + 40 * 5 * 7 + 44 * 100)
+    assert bench.algorithmic_bytes("raster2d_fwd", 48, 10, 100, 7, 5, 9, rows=8, fwd_walks=6.0) == 40 * 5 * 6 + 20 * 100
     assert bench.algorithmic_bytes("project2d_bwd", 48, 10, 100, 7, 5, 9, rows=8) == 10 * (36 * 8 + (32 + 72) * 48)
     assert bench.step_bytes(1, 10, 100, 7, 5, 14, backward=False) == 10 * (4 * 14 + 32) + 36 * 7 + 40 * 5 + 20 * 100
     assert bench.algorithmic_bytes("raster3d_bwd", 6, 10, 100, 7, 5, 14) == 24 * 100 + 40 * 5 + 36 * 6 * 10

@@ -115,7 +115,8 @@ def test_graph_bounded_equals_exact_cfg4_units(cuda):
 
     ref = eager(p0, "exact")
     n_isect = R.last_stats()["n_isect"]
-    assert n_isect > 100_000_000, n_isect
+    # the 8 frames' lists (each frame's six views render its first view's: lists2d_per_set)
+    assert n_isect > 15_000_000, n_isect
     params = p0.clone().requires_grad_(True)
 
     def step():
@@ -146,7 +147,7 @@ def test_graph_bounded_equals_exact_cfg4_units(cuda):
         assert torch.equal(ref[0], g_rgb), ("rgb", k)
         assert torch.equal(ref[1], g_alpha), ("alpha", k)
         assert torch.equal(ref[2], g_grad), ("v_params [8,N,9]", k)
-        print(f"[cfg4] replay {k}: 48 units, {n_isect} intersections: rgb/alpha/[8,N,9] gradient bitwise "
+        print(f"[cfg4] replay {k}: 48 units, {n_isect} list entries: rgb/alpha/[8,N,9] gradient bitwise "
               "equal to the exact eager step")
     del graph
     # units against the single-frame render of their frame (the last exact step's parameters)
