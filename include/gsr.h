@@ -65,6 +65,9 @@
  *   cotangent, and writes the set's SUMMED row at its first camera's emission index only;
  *   gsr2d_project_bwd, called with the same C / F / set_begin, reads only those rows.  The
  *   other cameras' rows are left unwritten.  A caller that pairs the two calls sees no change.
+ *   With the automatic forward layout (gsr_set_fwd_lanes(0)) the binning is shared the same way:
+ *   gsr2d_project_fwd gives only each set's first camera tiles (the other cameras' rect / count
+ *   are empty), and gsr2d_raster_fwd renders every camera of the set from that camera's lists.
  */
 #ifndef GSR_H
 #define GSR_H
