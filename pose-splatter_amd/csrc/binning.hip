@@ -361,6 +361,8 @@ __global__ __launch_bounds__(kStageThreads) void k_emit_staged(
   const int c = blockIdx.y;
   int32_t* gcnt = tile_count + (int64_t)c * T;
   const int32_t* toff = tile_offset + (int64_t)c * T;
+  // a camera with no entries (2D: a set's other cameras, lists2d_per_set) -- nothing to stage
+  if (toff[0] == toff[T]) return;
   const int64_t n0 = (int64_t)blockIdx.x * kStagePer;
   for (int t = threadIdx.x; t < T; t += NT) cur[t] = 0;
   uint2 rr[GPT];
