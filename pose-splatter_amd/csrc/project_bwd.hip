@@ -61,6 +61,7 @@ __device__ __forceinline__ void gather_partials(const uint2 r, int tw, int64_t c
 // fixed order (deterministic) and one thread per Gaussian applies the camera-independent
 // chain (rotation / scale / quaternion normalisation / adapter activations).
 constexpr int kContrib = 16;   // v_m[3], V_M[9], v_col[3], v_op
+constexpr int kCamLds = 16;    // cameras staged in LDS per workgroup (calls of more read them from global)
 
 // 5 workgroups of 256 threads per CU (96 VGPRs, 16 B/lane spilled): the kernel waits on its
 // gathers (tile cut keys, then the partial rows) most of the time, so occupancy pays --
@@ -82,6 +83,22 @@ __global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
     float* __restrict__ v_params, float* __restrict__ block, int64_t cap) {
   __shared__ float s_con[kBwdThreads][kContrib + 1];
   __shared__ int s_any[kBwdThreads];
+  // the cameras, staged once per workgroup (four b128 LDS reads per camera instead of ~6 global
+  // loads per (camera, Gaussian) thread: this kernel is bound by its memory instructions)
+  __shared__ float4 s_cam[kCamLds][4];
+  const bool cam_lds = C <= kCamLds;
+  if (cam_lds && (int)threadIdx.x < 4 * C) {
+    const int cc = threadIdx.x >> 2, part = threadIdx.x & 3;
+    const float* V = viewmats + cc * 16;
+    const float* Kc = Ks + cc * 9;
+    float4 v;
+    if (part == 0) v = make_float4(V[0], V[1], V[2], V[4]);
+    else if (part == 1) v = make_float4(V[5], V[6], V[8], V[9]);
+    else if (part == 2) v = make_float4(V[10], V[3], V[7], V[11]);
+    else v = make_float4(Kc[0], Kc[4], Kc[2], Kc[5]);
+    s_cam[cc][part] = v;
+  }
+  __syncthreads();
   const int g_loc = threadIdx.x % G;
   const int slot = threadIdx.x / G;
   const int64_t i_row = (int64_t)blockIdx.x * G + g_loc;   // ROWS: the row of this Gaussian
@@ -132,7 +149,16 @@ __global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
 #pragma unroll
       for (int v = 0; v < kPartial; ++v) acc[v] = 0.f;
       gather_partials(rc, tw, (int64_t)c * T, key, off, tile_cut, partial, acc);
-      const Cam cam = load_cam(viewmats + c * 16, Ks + c * 9);
+      Cam cam;
+      if (cam_lds) {
+        const float4 a = s_cam[c][0], b = s_cam[c][1], d = s_cam[c][2], k = s_cam[c][3];
+        cam.R[0] = a.x; cam.R[1] = a.y; cam.R[2] = a.z; cam.R[3] = a.w;
+        cam.R[4] = b.x; cam.R[5] = b.y; cam.R[6] = b.z; cam.R[7] = b.w;
+        cam.R[8] = d.x; cam.t[0] = d.y; cam.t[1] = d.z; cam.t[2] = d.w;
+        cam.fx = k.x; cam.fy = k.y; cam.cx = k.z; cam.cy = k.w;
+      } else {
+        cam = load_cam(viewmats + c * 16, Ks + c * 9);
+      }
       // recompute the forward geometry (not culled: it has intersections)
       geo3d(a, cam, W, H, 0.f, 3.4e38f, eps2d, g);
       any = 1;
