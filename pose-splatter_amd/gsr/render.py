@@ -1016,5 +1016,13 @@ def render2d_units(params: torch.Tensor, unit_sets, width: int, height: int, bac
     if not sets:
         raise ValueError("render2d_units: no units")
     _set_begin(sets, params.shape[0], params.device)   # validates the grouping
+    # Only the sets [sets[0], sets[-1]] are rendered: the launch sees that range (a view, no copy;
+    # autograd's slice backward gives the other sets a zero gradient).  The per-set backward and the
+    # shared lists key on C > F, so a frame owner's one frame of six views (params [8,N,9], sets
+    # (f,)*6) takes them as the full batch does (profiles/r05_rankshare_cfg4.json).
+    f0, f1 = sets[0], sets[-1] + 1
+    if (f0, f1) != (0, params.shape[0]):
+        params = params[f0:f1]
+        sets = tuple(f - f0 for f in sets)
     return _Render2D.apply(params, background, int(width), int(height), float(eps_cut), sets, capacity,
                            _needs_grad(params))

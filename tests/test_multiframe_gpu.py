@@ -25,8 +25,10 @@ def _frames(F, N, W, H, seed):
 # (0, 0, 1, 2, 2, 2): 6 cameras over 3 sets -> the per-set backward (k_raster2d_bwd_frame, two
 # cameras per pass: set 2 takes a second pass, set 1 a padded one); (0, 0, 2, 2, 2): the same
 # with a set no camera renders; (0, 2, 2) and (1,): one camera per set on average -> the
-# per-camera backward (k_raster2d_bwd_pair)
-@pytest.mark.parametrize("sets", [(0, 0, 1, 2, 2, 2), (0, 0, 2, 2, 2), (0, 2, 2), (1,)])
+# per-camera backward (k_raster2d_bwd_pair); (1, 1, 1) and (1, 1, 2, 2): the launch sees only the
+# rendered range of sets (one frame of three views: a frame owner's share), so the per-set path
+# applies and the sets outside the range get zero gradients through autograd's slice
+@pytest.mark.parametrize("sets", [(0, 0, 1, 2, 2, 2), (0, 0, 2, 2, 2), (0, 2, 2), (1,), (1, 1, 1), (1, 1, 2, 2)])
 def test_units_match_single_renders(cuda, sets):
     from gsr import render as R
     F, N, W, H = 3, 1200, 96, 80
