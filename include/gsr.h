@@ -218,6 +218,18 @@ int gsr_set_bwd_layout(int layout);
  * Same results as the quad layout up to fp32 regrouping of the transmittance products. */
 int gsr_set_fwd_heavy(int log2_min_len);
 
+/* Split 2D per-set backward (process-wide; additive to revision 12).  With several cameras per
+ * parameter set (the per-set walk, see "Per-entry gradient partials") and fewer than
+ * target_workgroups (set, tile) pairs in a call -- a frame owner's one frame of six views --
+ * gsr2d_raster_bwd splits each tile's consumed list into P = min(16, ceil(target / (F x tiles)))
+ * unit-aligned parts walked by separate workgroups, each starting from the pixels' suffix state
+ * at its end.  gsr2d_raster_fwd then also writes, per pixel, its colour sum before every unit
+ * and in total into chunk_state as three planes of n_chunks x 256 floats after the T anchors:
+ * chunk_state must then hold 4 floats per slot (n_chunks*256*4, as in 3D) instead of the one the
+ * 2D contract names.  0 (the default) is off; the Python binding sets 4 608.  Same results up to
+ * fp32 regrouping of the suffix terms; each setting is deterministic. */
+int gsr_set_bwd2d_parts(int target_workgroups);
+
 /* Self-test of the lane-ordered LDS atomics the tile sort's ranking relies on: writes the
  * number of violations (0 expected) to the device int *violations. */
 int gsr_selftest_lds_order(int32_t* violations, void* stream);

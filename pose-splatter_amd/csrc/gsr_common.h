@@ -484,6 +484,12 @@ inline bool rows2d_per_set(const int32_t* set_begin, int F, int C) {
 // projection gives the other cameras no tiles, and their forwards render the first camera's
 // list (k_raster2d_fwd_pair).  Host-side: it reads the forward-layout setting.
 bool lists2d_per_set(const int32_t* set_begin, int F, int C);
+// ... and when the call has few (set, tile) pairs for the chip (a frame owner's one frame), the
+// per-set backward splits each tile's consumed list into frame_parts2d(...) unit-aligned parts
+// walked by separate workgroups; the forward then also stores, per pixel, its colour sum before
+// every unit and in total (three planes after the T anchors, colour_plane2d floats apart), so a
+// part starts from the suffix state at its end.  1: no split.  Host-side (raster.hip).
+int frame_parts2d(const int32_t* set_begin, int F, int C, int T);
 
 // 2D: the record of entry id = c*N + n lives in the copy of camera c's set's first camera
 // (k_project2d_fwd writes one copy per set): rec[id + rec_offset2d(c)].
@@ -514,5 +520,10 @@ __device__ __forceinline__ int sweep_tile2d(int b, int64_t CT, int T, const int3
   return (c0 + v) * T + t;
 }
 __host__ __device__ __forceinline__ int sweep_grid2d(int64_t CT) { return (int)(8 * ((CT + 7) / 8)); }
+// floats between the 2D T anchors and each colour plane (frame_parts2d): one plane per colour
+// channel, as many rows as the call's units (the chunk-state buffer holds 4 floats per row slot)
+__device__ __forceinline__ int64_t colour_plane2d(const gsr_bin_stats* __restrict__ stats) {
+  return (int64_t)stats->n_chunks * 256;
+}
 
 }  // namespace gsr

@@ -33,6 +33,10 @@ static int g_fwd_lanes = 0;   // gsr_set_fwd_lanes: 0 automatic, 1 / 4 / 16 forc
 #define GSR_FWD_HEAVY_LOG2 0   // default heavy-tile threshold (0 = off; 12: lists of >= 4096 entries)
 #endif
 int g_fwd_heavy_log2 = GSR_FWD_HEAVY_LOG2;   // gsr_set_fwd_heavy (gsr_common.h)
+// gsr_set_bwd2d_parts (frame_parts2d): 0, the default, is off -- a caller that sized chunk_state by
+// the 2D contract of revision 12 (one float per slot) keeps it; the Python binding, which
+// allocates four floats per slot, turns it on
+int g_bwd2d_part_wgs = 0;
 static int g_bwd_layout = 0;  // gsr_set_bwd_layout: 0 automatic, 1 chunk kernel, 2 pixel pairs (3D)
 // box forward (k_raster_fwd_box) build knobs, for A/B measurements: lanes grouped by box along
 // the ds_read_b128 lane groups, and the 2D walk's records packed into 2 x b128 + b32
@@ -1222,7 +1226,7 @@ __global__ __launch_bounds__(128, GSR_FWD2P_MINB) void k_raster2d_fwd_pair(
     int H, int tw, int th, const float* __restrict__ bg, float* __restrict__ out_rgb, float* __restrict__ out_alpha,
     float* __restrict__ out_T, int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end,
     float* __restrict__ anchors, const int32_t* __restrict__ chunk_base, int64_t CT, float cut2d,
-    const gsr_bin_stats* __restrict__ stats, const Sets2D sets, int share_lists) {
+    const gsr_bin_stats* __restrict__ stats, const Sets2D sets, int share_lists, int part_colour) {
   constexpr int kHS = kChunk3 + 1;   // part j of round entry k at s_r[buf][j][k]; slot 128 a zero record
   __shared__ float4 s_r[2][3][kHS];
   __shared__ __attribute__((aligned(16))) unsigned char s_box[2][8][kBoxStride];
@@ -1295,11 +1299,6 @@ __global__ __launch_bounds__(128, GSR_FWD2P_MINB) void k_raster2d_fwd_pair(
     }
     if (!sync_any<2>(!(doneA && doneB), s_live[buf])) break;
     if (rb > start && ((rb - start) & umask) == 0) {   // entering unit kcur+1: the pixels' T anchors
-      if (anchors) {
-        const int64_t arow = (int64_t)(cbase + kcur + 1) * kRasterThreads;
-        anchors[arow + slotA] = TA;
-        anchors[arow + slotB] = TB;
-      }
       crA += drA;
       cgA += dgA;
       cbA += dbA;
@@ -1307,6 +1306,21 @@ __global__ __launch_bounds__(128, GSR_FWD2P_MINB) void k_raster2d_fwd_pair(
       cgB += dgB;
       cbB += dbB;
       drA = dgA = dbA = drB = dgB = dbB = 0.f;
+      if (anchors) {
+        const int64_t arow = (int64_t)(cbase + kcur + 1) * kRasterThreads;
+        anchors[arow + slotA] = TA;
+        anchors[arow + slotB] = TB;
+        if (part_colour) {   // the colour before the unit (k_raster2d_bwd_frame's parts)
+          float* const cp = anchors + arow;
+          const int64_t pl = colour_plane2d(stats);
+          cp[pl + slotA] = crA;
+          cp[2 * pl + slotA] = cgA;
+          cp[3 * pl + slotA] = cbA;
+          cp[pl + slotB] = crB;
+          cp[2 * pl + slotB] = cgB;
+          cp[3 * pl + slotB] = cbB;
+        }
+      }
       ++kcur;
     }
     const int nh = min(kChunk3, end - rb);
@@ -1421,6 +1435,16 @@ __global__ __launch_bounds__(128, GSR_FWD2P_MINB) void k_raster2d_fwd_pair(
   };
   store(inA, piA, TA, TlA, crA + drA, cgA + dgA, cbA + dbA, lastA);
   store(inB, piB, TB, TlB, crB + drB, cgB + dgB, cbB + dbB, lastB);
+  if (anchors && part_colour && end > start) {   // row 0 (no anchor there) holds the totals
+    float* const cp = anchors + (int64_t)cbase * kRasterThreads;
+    const int64_t pl = colour_plane2d(stats);
+    cp[pl + slotA] = crA + drA;
+    cp[2 * pl + slotA] = cgA + dgA;
+    cp[3 * pl + slotA] = cbA + dbA;
+    cp[pl + slotB] = crB + drB;
+    cp[2 * pl + slotB] = cgB + dgB;
+    cp[3 * pl + slotB] = cbB + dbB;
+  }
   const int lmax = max(lastA, lastB);
   if (lmax >= 0) atomicMax(&s_max, lmax);
   __syncthreads();
@@ -2563,7 +2587,7 @@ __global__ __launch_bounds__(128, GSR_BWD2F_MINB) void k_raster2d_bwd_frame(
     const int32_t* __restrict__ last_in, const float* __restrict__ v_rgb, const float* __restrict__ v_alpha,
     float* __restrict__ partial, const int32_t* __restrict__ tile_offset, const int32_t* __restrict__ tile_end,
     const int32_t* __restrict__ chunk_base, gsr_bin_stats* __restrict__ stats, const int32_t* __restrict__ k_of_s,
-    float cut2d, const Sets2D sets) {
+    float cut2d, const Sets2D sets, int parts) {
   constexpr int kNull = kChunk3;
   constexpr int kGroup = GSR_BWD_GROUP;
   static_assert(kGroup == 7 && kPartial == 9, "reduce_grp8 sums 7 entries x 9 values in 64 registers");
@@ -2580,12 +2604,14 @@ __global__ __launch_bounds__(128, GSR_BWD2F_MINB) void k_raster2d_bwd_frame(
   // tile slot with the other cameras' workgroups exiting put all the working ones on every
   // other CU -- the slots are dealt to an XCD's CUs in turn: half the chip idle.)
   const int T = tw * th;
-  const int64_t FT = (int64_t)sets.F * T;
-  const int64_t S = (FT + 7) / 8;
+  const int64_t FTP = (int64_t)sets.F * T * parts;   // (set, tile, part) slots, parts of a tile adjacent
+  const int64_t S = (FTP + 7) / 8;
   const int64_t pos = (int64_t)(blockIdx.x & 7) * S + (blockIdx.x >> 3);
   const int ovf = stats->overflow, U = stats->chunk_entries;
-  if ((ovf != 0) | (pos >= FT)) return;
-  const int f = (int)(pos / T), t = (int)(pos - (int64_t)f * T);
+  if ((ovf != 0) | (pos >= FTP)) return;
+  const int64_t tpos = pos / parts;
+  const int part = (int)(pos - tpos * parts);
+  const int f = (int)(tpos / T), t = (int)(tpos - (int64_t)f * T);
   const int cf = sets.begin != nullptr ? sets.begin[f] : 0;
   const int G = sets.begin != nullptr ? sets.begin[f + 1] - cf : 1;
   if (G <= 0) return;   // a set no camera renders
@@ -2593,6 +2619,15 @@ __global__ __launch_bounds__(128, GSR_BWD2F_MINB) void k_raster2d_bwd_frame(
   const int start = tile_offset[ct], te = tile_end[ct], cbase = chunk_base[ct];
   const int n = te - start;   // the consumed list [start, tile_end) (k_raster_finalize)
   if (n <= 0) return;
+  // this workgroup's part [pbeg, pend) of it: whole units, `parts` about equal ranges
+  int pbeg = start, pend = te;
+  if (parts > 1) {   // units [nu p / parts, nu (p + 1) / parts): none empty while nu >= parts
+    const int nu = (n + U - 1) / U, u_lo = (int)((int64_t)nu * part / parts),
+              u_hi = (int)((int64_t)nu * (part + 1) / parts);
+    if (u_lo >= u_hi) return;
+    pbeg = start + u_lo * U;
+    pend = min(start + u_hi * U, te);
+  }
   int c, ty, tx;
   tile_coords(ct, tw, th, c, ty, tx);   // (c = cf: the set's record copy, rec_offset2d = 0)
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -2621,6 +2656,28 @@ __global__ __launch_bounds__(128, GSR_BWD2F_MINB) void k_raster2d_bwd_frame(
     TfB = t2.x;
     TlB = t2.y;
   }
+  // a part before the list's end starts from each live pixel's state there: T from the anchor at
+  // pend, and (per camera, below) mu = (S.v + T_f mu_last) / T with S the colour after pend -- the
+  // total minus the colour before pend (the forward's colour planes)
+  const bool contA = pend < te && lastA >= pend, contB = pend < te && lastB >= pend;
+  float T0A = TfA, T0B = TfB, SrA = 0.f, SgA = 0.f, SbA = 0.f, SrB = 0.f, SgB = 0.f, SbB = 0.f;
+  if (contA | contB) {
+    const int64_t pl = colour_plane2d(stats);
+    const float* const ae = anchors + (int64_t)(cbase + (pend - start) / U) * kRasterThreads;
+    const float* const a0 = anchors + (int64_t)cbase * kRasterThreads;
+    if (contA) {
+      T0A = ae[slotA];
+      SrA = a0[pl + slotA] - ae[pl + slotA];
+      SgA = a0[2 * pl + slotA] - ae[2 * pl + slotA];
+      SbA = a0[3 * pl + slotA] - ae[3 * pl + slotA];
+    }
+    if (contB) {
+      T0B = ae[slotB];
+      SrB = a0[pl + slotB] - ae[pl + slotB];
+      SgB = a0[2 * pl + slotB] - ae[2 * pl + slotB];
+      SbB = a0[3 * pl + slotB] - ae[3 * pl + slotB];
+    }
+  }
   const int wlast = wave_max_i(max(lastA, lastB));
   const int fg = lane / kPartial, fq = lane - kPartial * (lane / kPartial);
   const bool fown = lane < kGroup * kPartial;
@@ -2631,7 +2688,7 @@ __global__ __launch_bounds__(128, GSR_BWD2F_MINB) void k_raster2d_bwd_frame(
   const int wr0 = (8 * grp8_slot(lane)) ^ grp8_swz(obox), wr1 = (8 * grp8_slot(lane) + 4) ^ grp8_swz(obox);
   const unsigned char* my_list = s_box[wv][box];
   const float4* const rec4 = reinterpret_cast<const float4*>(rec);
-  const int nsub = (n + kChunk3 - 1) / kChunk3;
+  const int nsub = (pend - pbeg + kChunk3 - 1) / kChunk3;
   if (threadIdx.x < 3) s_p[threadIdx.x][kNull] = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int u0 = 0; u0 < G; u0 += GB) {
     // this pass's cameras' cotangents and mu (zero past the set's cameras: exact zero terms)
@@ -2657,11 +2714,13 @@ __global__ __launch_bounds__(128, GSR_BWD2F_MINB) void k_raster2d_bwd_frame(
           muB[u] = bgc[0] * vrB[u] + bgc[1] * vgB[u] + bgc[2] * vbB[u] - v_alpha[pix];
         }
       }
+      if (contA) muA[u] = (SrA * vrA[u] + SgA * vgA[u] + SbA * vbA[u] + TfA * muA[u]) / T0A;
+      if (contB) muB[u] = (SrB * vrB[u] + SgB * vgB[u] + SbB * vbB[u] + TfB * muB[u]) / T0B;
     }
     const float VrA = pair_sum<GB>(vrA), VgA = pair_sum<GB>(vgA), VbA = pair_sum<GB>(vbA);
     const float VrB = pair_sum<GB>(vrB), VgB = pair_sum<GB>(vgB), VbB = pair_sum<GB>(vbB);
-    int sb0 = start + (nsub - 1) * kChunk3;
-    int sn = start + n - sb0;
+    int sb0 = pbeg + (nsub - 1) * kChunk3;
+    int sn = pend - sb0;
     const int id_mine = (int)threadIdx.x < sn ? ids[sb0 + threadIdx.x] : 0;
     int kos_mine = (int)threadIdx.x < sn ? k_of_s[sb0 + threadIdx.x] : 0;
     float4 sp0 = make_float4(0.f, 0.f, 0.f, 0.f), sp1 = sp0, sp2 = sp0;
@@ -2670,7 +2729,7 @@ __global__ __launch_bounds__(128, GSR_BWD2F_MINB) void k_raster2d_bwd_frame(
       sp1 = rec4[3 * (int64_t)id_mine + 1];
       sp2 = rec4[3 * (int64_t)id_mine + 2];
     }
-    float TA = TfA, TB = TfB, TnA = TfA, TnB = TfB;
+    float TA = T0A, TB = T0B, TnA = TfA, TnB = TfB;
     for (int sub = nsub - 1; sub >= 0; --sub) {
       if (sub != nsub - 1 || u0 > 0) __syncthreads();   // the previous sub-chunk's (pass's) LDS is consumed
       if (sub != nsub - 1 && ((sb0 + sn - start) & (U - 1)) == 0) {   // re-anchor T at a unit boundary
@@ -3254,6 +3313,13 @@ int gsr_set_fwd_heavy(int log2_min_len) {
   return GSR_OK;
 }
 
+int gsr_set_bwd2d_parts(int target_workgroups) {
+  GSR_REQUIRE(target_workgroups >= 0 && target_workgroups <= (1 << 24),
+              "gsr_set_bwd2d_parts: target_workgroups must be in [0, 2^24], got %d", target_workgroups);
+  gsr::g_bwd2d_part_wgs = target_workgroups;
+  return GSR_OK;
+}
+
 int gsr_set_bwd_layout(int layout) {
   GSR_REQUIRE(layout >= 0 && layout <= 2, "gsr_set_bwd_layout: layout must be 0 (auto), 1 or 2, got %d", layout);
   gsr::g_bwd_layout = layout;
@@ -3285,6 +3351,16 @@ namespace gsr {
 constexpr int64_t kFwd16MaxTiles = 320;
 bool lists2d_per_set(const int32_t* set_begin, int F, int C) {
   return GSR_FWD2D_PAIR && g_fwd_lanes == 0 && rows2d_per_set(set_begin, F, C);
+}
+// frame_parts2d: parts per tile so that the per-set backward has about gsr_set_bwd2d_parts'
+// target workgroups (at most 16 parts; 1 -- the whole list per workgroup -- from that many (set,
+// tile) pairs on, e.g. config 4's eight frames at the binding's 4 608).  Only with the pair
+// forward's shared lists, whose lead camera writes the colour planes.
+int frame_parts2d(const int32_t* set_begin, int F, int C, int T) {
+  const int target = g_bwd2d_part_wgs;
+  if (target <= 0 || !lists2d_per_set(set_begin, F, C)) return 1;
+  const int64_t ft = std::max<int64_t>(1, (int64_t)F * T);
+  return (int)std::min<int64_t>(16, std::max<int64_t>(1, (target + ft - 1) / ft));
 }
 static int fwd_lanes(bool is2d, int64_t CT) {
   if (g_fwd_lanes == 1 || g_fwd_lanes == 4 || (g_fwd_lanes == 16 && !is2d)) return g_fwd_lanes;
@@ -3383,7 +3459,8 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
     hipLaunchKernelGGL(k_raster2d_fwd_pair, dim3((unsigned)sweep_grid2d(CT)), dim3(128), 0, s, (const Splat*)rec,
                        sorted_ids, tile_offset, width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end,
                        (float*)chunk_state, chunk_base, CT, cut2d, stats, sets,
-                       lists2d_per_set(sets.begin, sets.F, C) ? 1 : 0);
+                       lists2d_per_set(sets.begin, sets.F, C) ? 1 : 0,
+                       frame_parts2d(sets.begin, sets.F, C, tw * th) > 1 ? 1 : 0);
   } else {
     // 2D: every tile in the XCD-aware sweep (no separate empty-tile fill)
     const int64_t grid = IS2D ? (int64_t)sweep_grid2d(CT) : ((n_busy + 7) & ~7) + n_fill;
@@ -3450,12 +3527,14 @@ static int raster_bwd(const char* who, const float* rec, const int32_t* sorted_i
     if (rows2d_per_set(sets.begin, sets.F, C)) {
       // cameras per pass: the set size (its mean over the call's sets), rounded up to 2, 4, 6, 8
       const int g = (C + sets.F - 1) / sets.F;
-      const int64_t FT = (int64_t)sets.F * tw * th;
+      const int parts = frame_parts2d(sets.begin, sets.F, C, tw * th);   // (the forward's rule: its colour planes)
+      const int64_t FTP = (int64_t)sets.F * tw * th * parts;
+      GSR_REQUIRE(8 * ((FTP + 7) / 8) < (1ll << 31), "%s: too many (set, tile, part) workgroups", who);
 #define GSR_LAUNCH_FRAME(GBV)                                                                                       \
-  hipLaunchKernelGGL(k_raster2d_bwd_frame<GBV>, dim3((unsigned)(8 * ((FT + 7) / 8))), dim3(128), 0,                   \
+  hipLaunchKernelGGL(k_raster2d_bwd_frame<GBV>, dim3((unsigned)(8 * ((FTP + 7) / 8))), dim3(128), 0,                  \
                      (hipStream_t)stream, (const Splat*)rec, sorted_ids, chunk_state, width, height, tw, th, bg,      \
                      final_T, last, v_rgb, v_alpha, partial, tile_offset, tile_end, chunk_base, stats, k_of_s, cut2d, \
-                     sets)
+                     sets, parts)
       if (g <= 2)
         GSR_LAUNCH_FRAME(2);
       else if (g <= 4)

@@ -27,6 +27,9 @@ INPUT_ADAPTER = 0
 INPUT_GSPLAT = 1
 
 ABI_VERSION = 12   # include/gsr.h GSR_ABI_VERSION this binding is written for
+# gsr_set_bwd2d_parts at load (profiles/r05_ab5_bwd2d_parts_sweep.txt; GSR_BWD2D_PART_WGS overrides it
+# for measurements, tools/parts_sweep.sh)
+BWD2D_PART_WORKGROUPS = int(os.environ.get("GSR_BWD2D_PART_WGS", "4608"))
 
 # stats->overflow bits of a capacity-bounded call (include/gsr.h GSR_OVF_*)
 OVF_BITS = {1: "intersections > isect cap", 2: "chunks > chunk cap", 4: "busy tiles > n_busy bound",
@@ -87,6 +90,7 @@ EXPORTS = {
     "gsr_selftest_reduce_box16": (ctypes.c_int, [_P, _P]),
     "gsr_selftest_reduce_grp": (ctypes.c_int, [_P, ctypes.c_int, _P]),
     "gsr_set_fwd_heavy": (ctypes.c_int, [ctypes.c_int]),
+    "gsr_set_bwd2d_parts": (ctypes.c_int, [ctypes.c_int]),
     "gsr_set_fwd_lanes": (ctypes.c_int, [_I32]),
     "gsr_set_bwd_layout": (ctypes.c_int, [_I32]),
     "gsr_selftest_lds_order": (ctypes.c_int, [_P, _P]),
@@ -178,6 +182,9 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
+        # the split 2D per-set backward for few (set, tile) pairs: render.py allocates chunk_state
+        # with 4 floats per slot, which its colour planes need (include/gsr.h)
+        handle.gsr_set_bwd2d_parts(BWD2D_PART_WORKGROUPS)
         _lib = handle
         return _lib
 

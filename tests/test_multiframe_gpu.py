@@ -77,3 +77,43 @@ def test_unit_vs_oracle(cuda):
     assert_close(alpha[1].detach(), a_o.detach(), what="unit 1 alpha")
     grad_close(pb.grad[1], po.grad, what="frame 1 grad")
     assert torch.count_nonzero(pb.grad[0]) == 0
+
+
+@pytest.mark.parametrize("target", [160, 4608])
+def test_split_set_backward_matches_whole_walks(cuda, target):
+    """The split per-set backward (gsr_set_bwd2d_parts: each tile's list in unit-aligned parts,
+    every part starting from the forward's suffix state at its end -- T anchor and colour planes)
+    against the same call with whole-list walks (target 0), and both against the sum of the
+    views' single-camera backward passes.  One frame of four views at 160x128 (80 tiles: 2 parts
+    per tile at target 160, the cap of 16 at 4 608) over lists of ~10 128-entry units."""
+    from gsr import render as R
+    from gsr import _lib
+    F, N, W, H = 2, 20000, 160, 128
+    P = _frames(F, N, W, H, 91)
+    bg = torch.tensor([0.2, 0.4, 0.9])
+    sets = (1, 1, 1, 1)
+    g = torch.Generator().manual_seed(92)
+    vr, va = torch.randn(4, H, W, 3, generator=g), torch.randn(4, H, W, generator=g)
+    L = _lib.lib()
+    grads, imgs = [], []
+    try:
+        for t in (target, 0):
+            assert L.gsr_set_bwd2d_parts(t) == 0
+            pb = P.to(cuda).requires_grad_(True)
+            rgb, alpha = R.render2d_units(pb, sets, W, H, bg.to(cuda))
+            torch.autograd.backward([rgb, alpha], [vr.to(cuda), va.to(cuda)])
+            grads.append(pb.grad.detach().cpu())
+            imgs.append((rgb.detach().cpu(), alpha.detach().cpu()))
+    finally:
+        L.gsr_set_bwd2d_parts(_lib.BWD2D_PART_WORKGROUPS)
+    assert R.last_stats().get("n_isect", 0) > 80 * 128 * 4, "lists too short to split"
+    assert torch.equal(imgs[0][0], imgs[1][0]) and torch.equal(imgs[0][1], imgs[1][1])   # forward unchanged
+    assert torch.count_nonzero(grads[0][0]) == 0
+    grad_close(grads[0][1], grads[1][1].double(), rtol=1e-5, rel_floor=1e-6, what="split vs whole walks")
+    ref = torch.zeros(N, 9, dtype=torch.float64)
+    for c in range(4):
+        ps = P[1].to(cuda).requires_grad_(True)
+        r1, a1 = R.render2d(ps, W, H, bg.to(cuda))
+        torch.autograd.backward([r1, a1], [vr[c].to(cuda), va[c].to(cuda)])
+        ref += ps.grad.double().cpu()
+    grad_close(grads[0][1], ref, rtol=1e-5, rel_floor=1e-6, what="split vs single-camera passes")
