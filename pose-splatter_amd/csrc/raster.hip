@@ -1212,9 +1212,11 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
 // serve two pixels.  Lanes: box = 2 x (the lane's ds_read_b128 group) + (lane bit 4), so a b128
 // read of the walk has two addresses per lane group (the box forward's broadcast trick, halved).
 // The list is walked in 128-entry rounds (one chunk each; records double-buffered in 12 KB of
-// LDS), so 11 workgroups (22 waves) fit a CU.  Per pixel the arithmetic is the box forward's,
-// operation for operation (dx = x - px, dy = y - py, conic_sigma, alpha >= cut2d, T <- T (1 - a),
-// stop after T <= 2^-25), so k_raster2d_bwd_pair's validity tests agree with it exactly.
+// LDS), so 11 workgroups (22 waves) fit a CU.  Per pixel the arithmetic is the box forward's
+// (dx = x - px, dy = y - py, conic_sigma, alpha >= cut2d, stop after T <= 2^-25), so
+// k_raster2d_bwd_pair's validity tests agree with it exactly -- except that T <- T (1 - a) is one
+// fmaf (one rounding, the box forward rounds 1 - a first): the images are not bitwise the box
+// layout's (EXPERIMENTS.md §F).
 #ifndef GSR_FWD2D_PAIR
 #define GSR_FWD2D_PAIR 1
 #endif
