@@ -42,7 +42,7 @@ import torch
 
 __all__ = [
     "Ref3D", "activations3d", "quat_to_rotmat", "project3d", "isect_tiles",
-    "raster3d_fwd", "raster3d_bwd", "render3d", "render3d_pixelloop",
+    "raster3d_fwd", "raster3d_bwd", "render3d", "render3d_pixelloop", "tie_flags",
 ]
 
 
@@ -447,6 +447,120 @@ def render3d(params, viewmats, Ks, width, height, background, *,
     if return_meta:
         return rgb, alpha, dict(proj=proj, offsets=offsets, ids=ids, last=last)
     return rgb, alpha
+
+
+def tie_flags(params, viewmats, Ks, width, height, *, margin=1e-4, radius_mode=Ref3D.RADIUS_OPACITY_AABB,
+              activated=False, band=None, tile=Ref3D.TILE):
+    """Where two correct fp32 implementations of A.3 may resolve a discrete decision differently.
+
+    Walks the same lists as ``raster3d_fwd`` (same ``done`` state) and flags a pixel when any
+    entry it evaluates sits within ``margin`` (relative) of a decision threshold:
+      * the skip test α ≥ 1/255 (|α − 1/255| ≤ margin/255),
+      * the stop test T(1 − α) ≤ 1e-4 for an entry that passes the skip (|nT − 1e-4| ≤ margin·1e-4),
+      * the clamp α = min(0.999, o e^{−σ}) that switches the σ / opacity gradients off
+        (|o e^{−σ} − 0.999| ≤ margin),
+      * the test σ ≥ 0 (|σ| ≤ margin·(|A dx²| + |C dy²| + |2B dx dy|)/2: a pixel at the centre).
+    The GPU evaluates the same formulas from its own projection (different fp32 roundings,
+    exp2 with a log2(e)-scaled conic).  The fp32 oracle's own alpha near 1/255 is off its float64
+    value by up to 2.9e-5 (relative) at config 1 (conic cancellation, sigma ~5.5 in the
+    exponent); two fp32 implementations differ by up to twice that, hence 1e-4.
+
+    Returns (pixels [C,H,W] bool, gaussians [N] bool, n_pixels): ``gaussians`` marks every
+    Gaussian with α ≥ (1 − margin)/255 at a flagged pixel -- the entries whose gradient a flipped
+    decision there can change (a skip flip moves that entry and, through T and the suffix
+    colour, every other entry of the pixel; a stop flip adds or drops the entries after it).
+    Tests allow an out-of-tolerance value ONLY at a flagged pixel / a marked Gaussian's row.
+    """
+    C, N = viewmats.shape[0], params.shape[0]
+    with torch.no_grad():
+        p = params.detach()
+        if activated:
+            means, scales, quats = p[:, 0:3], p[:, 3:6], p[:, 6:10]
+            opac = p[:, 13]
+        else:
+            means, quats, scales, _, opac = activations3d(p)
+        proj = project3d(means, quats, scales, opac, viewmats, Ks, width, height, radius_mode=radius_mode)
+        offsets, ids = isect_tiles(proj.means2d, proj.radii, proj.depths, width, height, band=band)
+        dt = proj.means2d.dtype
+        xy = proj.means2d.reshape(C * N, 2)
+        con = proj.conics.reshape(C * N, 3)
+        op = opac[None].expand(C, N).reshape(C * N).to(dt)
+        tw = (width + tile - 1) // tile
+        th = (height + tile - 1) // tile
+        T_ = tw * th
+        pix = torch.zeros(C, height, width, dtype=torch.bool)
+        gau = torch.zeros(N, dtype=torch.bool)
+        counts = offsets[1:] - offsets[:-1]
+        busy = torch.nonzero(counts > 0).flatten()
+        if busy.numel() == 0:
+            return pix, gau, 0
+        cams, tloc = busy // T_, busy % T_
+        j, i, inside = _tile_pixels(width, height, tile, tloc, tw, 0.5)
+        px, py = j.to(dt) + 0.5, i.to(dt) + 0.5
+        starts, lens = offsets[busy], counts[busy]
+        Tn, P = busy.numel(), tile * tile
+        thr = Ref3D.ALPHA_THRESHOLD
+
+        def step(k):
+            act = k < lens
+            e = torch.where(act, starts + k, starts)
+            g = ids[e]
+            A, B, Cc = con[g, 0][:, None], con[g, 1][:, None], con[g, 2][:, None]
+            dx, dy = xy[g, 0][:, None] - px, xy[g, 1][:, None] - py
+            sigma = 0.5 * (A * dx * dx + Cc * dy * dy) + B * dx * dy
+            mag = 0.5 * ((A * dx * dx).abs() + (Cc * dy * dy).abs()) + (B * dx * dy).abs()
+            raw = op[g][:, None] * torch.exp(-sigma)
+            return act, g, sigma, mag, raw, torch.clamp(raw, max=Ref3D.ALPHA_MAX)
+
+        Tcur = torch.ones(Tn, P, dtype=dt)
+        done = ~inside
+        flag = torch.zeros(Tn, P, dtype=torch.bool)
+        Lmax = int(lens.max())
+        for k in range(Lmax):
+            act, g, sigma, mag, raw, al = step(k)
+            live = act[:, None] & ~done
+            if not bool(live.any()):
+                break
+            near = ((al - thr).abs() <= margin * thr) | (sigma.abs() <= margin * mag)
+            ok = live & (sigma >= 0) & (al >= thr)
+            nT = Tcur * (1.0 - al)
+            near = near | (ok & (((nT - Ref3D.T_MIN).abs() <= margin * Ref3D.T_MIN) |
+                                 ((raw - Ref3D.ALPHA_MAX).abs() <= margin)))
+            flag |= live & near
+            stop = ok & (nT <= Ref3D.T_MIN)
+            done = done | stop
+            Tcur = torch.where(ok & ~stop, nT, Tcur)
+        flag &= inside
+        if bool(flag.any()):
+            # the flagged pixels' walks again: every entry at or above the skip threshold (minus
+            # the margin) up to the pixel's stop, and the next `extra` after it (a stop flip: the
+            # other implementation stops at one of the next passing entries, T being at 1e-4)
+            rows = torch.nonzero(flag.any(1)).flatten()
+            fl = flag[rows]
+            Tr = torch.ones(rows.numel(), P, dtype=dt)
+            dn = ~inside[rows]
+            after = torch.zeros(rows.numel(), P, dtype=torch.int64)
+            extra = 2
+            for k in range(Lmax):
+                act, g, sigma, mag, raw, al = step(k)
+                a_r, g_r, s_r, al_r = act[rows][:, None], g[rows], sigma[rows], al[rows]
+                passing = a_r & (al_r >= (1.0 - margin) * thr)
+                hit = fl & passing & (after < extra)
+                sel = hit.any(1)
+                if bool(sel.any()):
+                    gau[(g_r[sel] % N)] = True
+                after = after + (fl & passing & dn).to(torch.int64)
+                ok = a_r & ~dn & (s_r >= 0) & (al_r >= thr)
+                nT = Tr * (1.0 - al_r)
+                stop = ok & (nT <= Ref3D.T_MIN)
+                dn = dn | stop
+                Tr = torch.where(ok & ~stop, nT, Tr)
+                if not bool((a_r & fl & (after < extra)).any()):
+                    break
+            for n_ in rows.tolist():
+                m = flag[n_]
+                pix[int(cams[n_]), i[n_][m], j[n_][m]] = True
+        return pix, gau, int(pix.sum())
 
 
 def render3d_pixelloop(params, viewmats, Ks, width, height, background, **kw):

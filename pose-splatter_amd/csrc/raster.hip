@@ -446,6 +446,12 @@ extern "C" int gsr_debug_fwd_trace(void* buf) {
 #ifndef GSR_FWD_MINB
 #define GSR_FWD_MINB 6
 #endif
+#ifndef GSR_FWD_PRIO
+#define GSR_FWD_PRIO 3       // s_setprio of the waves of long-list tiles (0: off; 3: +0.7 % at config 3, r06 A/B)
+#endif
+#ifndef GSR_FWD_PRIO_LEN
+#define GSR_FWD_PRIO_LEN 2048
+#endif
 // NW: waves per workgroup (4; 8 for the heavy-tile variant, LPP 8).  part: 0 every busy tile,
 // 1 the tiles with lists shorter than stats->heavy_min_len, 2 the others (the heavy tiles: a
 // first-pass forward finds them at the head of the busy order, a lazy re-render anywhere in its list).
@@ -522,6 +528,10 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 6 : (IS2D || LPP != 4) ? 1 : GSR
   const int start = tile_offset[ct], list_end = tile_offset[ct + 1];
   if (part != 0 && (part == 2) != (list_end - start >= stats->heavy_min_len)) return;   // heavy / light split
   const int end = lz.tile_sorted && !lz.rerun ? lz.tile_sorted[ct] : list_end;
+#if GSR_FWD_PRIO
+  // long lists: the serial round chains that set the forward's span win the CU's issue arbitration
+  if (!IS2D && list_end - start >= GSR_FWD_PRIO_LEN) __builtin_amdgcn_s_setprio(GSR_FWD_PRIO);
+#endif
   if (threadIdx.x == 0) s_max = -1;
   __syncthreads();
   float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f;
@@ -1528,10 +1538,29 @@ __device__ __forceinline__ void store_partial_row(float* __restrict__ partial, i
 // order: each box's reads see the previous box's writes.  (Issuing all NB reads first and
 // chaining only a lane's own aliased boxes lost those cross-lane updates: measured wrong in the
 // fit test, round 5.)
+// GSR_BWD_LWPAR=1 rebuilds exactly that broken form (commit 3ec9d20) as the NEGATIVE CONTROL of
+// tests/test_race_gpu.py (tools/race_control.sh builds it into build_var/; never the product).
+#ifndef GSR_BWD_LWPAR
+#define GSR_BWD_LWPAR 0
+#endif
 template <int NB>
 __device__ __forceinline__ void lw_add(float* Lw, const int (&k)[NB], const float (&v)[NB]) {
+#if GSR_BWD_LWPAR
+  float n[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) n[b] = Lw[k[b]];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    n[b] += v[b];
+#pragma unroll
+    for (int c = 0; c < b; ++c) n[b] = k[c] == k[b] ? n[c] + v[b] : n[b];
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) Lw[k[b]] = n[b];
+#else
 #pragma unroll
   for (int b = 0; b < NB; ++b) Lw[k[b]] += v[b];
+#endif
 }
 // GSR_BWD_PF: the walk reads entry g+1's record from LDS before it evaluates entry g (a
 // scheduling fence keeps the reads there: left to itself the compiler issued each entry's reads
@@ -1620,6 +1649,9 @@ __device__ __forceinline__ void loss_cotangent(const gsr_loss_terms& lt, int C, 
 #endif
 #ifndef GSR_BWD_MULTI_MINB
 #define GSR_BWD_MULTI_MINB 1
+#endif
+#ifndef GSR_BWD_PRIO
+#define GSR_BWD_PRIO 0   // 1: s_setprio by the wave's walk length (timing experiment)
 #endif
 #ifdef GSR_BWD_TRACE
 // timing build only (tools/bwd_trace.py): per workgroup {wall clock at 7 points, hw id, groups}
@@ -1836,6 +1868,12 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
     const int npad = (ngrp + kGroup - 1) / kGroup * kGroup;
     for (int s = nb + pos; s < npad; s += 16) s_box[wv][box][PK ? grouped_slot(s) : s] = (unsigned char)kNull;
     __builtin_amdgcn_wave_barrier();
+#if GSR_BWD_PRIO
+    // the chunk's long walks (its slowest waves, which the others wait for at the rows barrier)
+    // win the CU's issue arbitration
+    if (ngrp > 3 * kGroup) __builtin_amdgcn_s_setprio(2);
+    else if (ngrp > 2 * kGroup) __builtin_amdgcn_s_setprio(1);
+#endif
 #ifdef GSR_BWD_TRACE
     if (pos == 0) tr_nb[wv * 4 + box] = nb;
 #endif

@@ -183,8 +183,14 @@ def lib():
             fn.restype = res
             fn.argtypes = args
         # the split 2D per-set backward for few (set, tile) pairs: render.py allocates chunk_state
-        # with 4 floats per slot, which its colour planes need (include/gsr.h)
-        handle.gsr_set_bwd2d_parts(BWD2D_PART_WORKGROUPS)
+        # with 4 floats per slot, which its colour planes need (include/gsr.h).  A process-wide
+        # library setting: another C-ABI caller in this process that sizes chunk_state by the
+        # one-float contract must turn it off (gsr_set_bwd2d_parts(0)); the backward refuses to
+        # split a walk whose forward wrote no colour planes (GSR_OVF_LAYOUT)
+        rc = handle.gsr_set_bwd2d_parts(BWD2D_PART_WORKGROUPS)
+        if rc != 0:
+            raise GsrLibraryError(f"gsr_set_bwd2d_parts({BWD2D_PART_WORKGROUPS}) failed (code {rc}): "
+                                  f"{handle.gsr_last_error().decode(errors='replace')}")
         _lib = handle
         return _lib
 

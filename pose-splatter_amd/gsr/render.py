@@ -177,6 +177,17 @@ def _status_buf(device) -> torch.Tensor:
     return t
 
 
+_scratch = {}   # device -> int32 [1]: the status word of auto-mode calls that verify themselves
+
+
+def _scratch_status(device) -> torch.Tensor:
+    key = str(device)
+    t = _scratch.get(key)
+    if t is None:
+        t = _scratch[key] = torch.zeros(1, device=device, dtype=torch.int32)
+    return t
+
+
 def overflow_status(device=None, reset: bool = False) -> int:
     """The sticky GSR_OVF_* bits of every call on ``device`` since the last reset (synchronises)."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -419,7 +430,7 @@ class _Bins:
     buffers).  A bounded call sizes both before any kernel runs and never reads back."""
 
     def __init__(self, device, C, N, width, height, capacity=None, key_extra=None, chunk_entries=128,
-                 need_bwd=True):
+                 need_bwd=True, retry=False):
         self.device = device
         self.C, self.N, self.W, self.H = C, N, width, height
         self.tw = (width + _TILE - 1) // _TILE
@@ -457,11 +468,21 @@ class _Bins:
             raise ValueError(f"capacity mode must be one of {_MODES}, got {mode!r}")
         self.bounded = False
         self.monitor = None
+        # auto mode, eager: the forward checks its own bounds (verify_launch / verify_overflow) and
+        # renders again, sized exactly, if they failed -- the caller never sees an overflow
+        self.verify = False
+        status = _status_buf(device)
         if mode == "auto":
-            # bounded only where a backward follows to check it, and where bounds exist
+            # bounded only where a backward follows, and where bounds exist; `retry`: the exact
+            # re-render of a call whose bounds failed (same key, so it re-seeds the bounds)
             if need_bwd and not _capturing():
                 _monitor_check(self.key)
-            mode = "bounded" if need_bwd and (self.key in _size_hint or _capturing()) else "exact"
+            mode = "bounded" if need_bwd and not retry and (self.key in _size_hint or _capturing()) else "exact"
+            if mode == "bounded" and not _capturing():
+                self.verify = True
+                # the failed call's kernels report to a word nobody reads: the re-render replaces
+                # it, so the sticky status (check_overflow) must not see its bits
+                status = _scratch_status(device)
         if mode == "bounded":
             if not _capturing():
                 _monitor_check(self.key)
@@ -475,7 +496,7 @@ class _Bins:
         # (a forward with no backward writes no chunk records: no chunk bound to check)
         self.caps = _lib.BinCaps(self.post_cap if self.bounded else 0,
                                  self.chunk_cap if self.bounded and need_bwd else 0,
-                                 _status_buf(device).data_ptr(), self.chunk_entries, 0)
+                                 status.data_ptr(), self.chunk_entries, 0)
 
     def _set_bounds(self, h: dict) -> None:
         """Bounded call: every buffer and grid from the shape's hint plus margins (the device
@@ -500,6 +521,29 @@ class _Bins:
                and self.post_cap <= _MASK_MAX_ENTRIES)
         self.masks = bool(use)
         return self.p["rec"] if use else None
+
+    def verify_launch(self) -> None:
+        """Auto mode, eager: copy the stats to pinned memory behind the last kernel of the forward
+        that can set an overflow bit (the sort; the lazy forward's own re-sort), no wait."""
+        if not self.verify:
+            return
+        self._vhost = _monitor_pool.pop() if _monitor_pool else torch.empty(_STATS_I32, dtype=torch.int32,
+                                                                            pin_memory=True)
+        self._vhost.copy_(self.pre.view("stats_dev", _I32), non_blocking=True)
+        self._vev = torch.cuda.Event()
+        self._vev.record()
+
+    def verify_overflow(self) -> int:
+        """The GSR_OVF_* bits of this call's forward (waits for verify_launch's copy, which the
+        GPU reaches while the raster forward enqueued behind it still has to run); 0 unless
+        verifying.  (the drop-in's default mode must not raise on a caller whose
+        footprints grow past the previous step's bounds.)"""
+        if not self.verify:
+            return 0
+        self._vev.synchronize()
+        st = self._vhost.tolist()
+        _monitor_pool.append(self._vhost)
+        return int(st[12])
 
     def take_tile_counts(self) -> int:
         """For the projection call: 1 if the shared tile_count buffer is known to be zero."""
@@ -706,9 +750,10 @@ def _background(bg: torch.Tensor, C: int, dev) -> torch.Tensor:
     return hit[1]
 
 
-def _forward3d(params, viewmats, Ks, bg, width, height, opts, need_bwd=True):
+def _forward3d(params, viewmats, Ks, bg, width, height, opts, need_bwd=True, retry=False):
     """Projection → binning → raster fwd.  Returns (rgb, alpha, bins, meta).  need_bwd False: no
-    backward will follow (no grad needed), so no chunk records and no finalize."""
+    backward will follow (no grad needed), so no chunk records and no finalize.  An auto-mode
+    call whose bounds fail renders again, sized exactly (retry)."""
     L = lib()
     dev = params.device
     stream = _stream(dev)
@@ -719,7 +764,7 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts, need_bwd=True):
     Kc = Ks.detach().to(device=dev, dtype=torch.float32).contiguous()
     bgc = _background(bg, C, dev)
     b = _Bins(dev, C, N, width, height, opts.capacity, ("3d", opts.band, opts.input_mode, opts.radius_mode, opts.tag),
-              _chunk_entries["3d"], need_bwd)
+              _chunk_entries["3d"], need_bwd, retry)
     q = b.p
     with _timed("project3d_fwd"):
       check(L.gsr3d_project_fwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height,
@@ -738,6 +783,7 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts, need_bwd=True):
         b.sort_lazy(stream)
     else:
         b.sort(_lib.ORDER_DEPTH, stream)
+        b.verify_launch()
     rgb = torch.empty(C, height, width, 3, device=dev, dtype=torch.float32)
     alpha = torch.empty(C, height, width, device=dev, dtype=torch.float32)
     with _timed("raster3d_fwd"):
@@ -754,6 +800,10 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts, need_bwd=True):
                                  C, width, height, _ptr(bgc), b.n_busy, q["stats_dev"], _ptr(rgb), _ptr(alpha),
                                  q["final_T"], q["last"], q["tile_end"], q["tile_cut"], cs, cl, stream),
               "gsr3d_raster_fwd")
+    if n_lazy:
+        b.verify_launch()   # (the lazy forward's re-sort can still flag GSR_OVF_LAZY)
+    if b.verify_overflow():
+        return _forward3d(params, viewmats, Ks, bg, width, height, opts, need_bwd, retry=True)
     _record_stats(b)
     return rgb, alpha, b, (p, stride, V, Kc, bgc, width, height, opts)
 
@@ -796,7 +846,7 @@ def _sets2d(params: torch.Tensor):
     return p, F, N, int(p.stride(1)) if N > 0 else 9, int(p.stride(0))
 
 
-def _forward2d(params, bg, width, height, eps_cut, unit_sets=(0,), capacity=None, need_bwd=True):
+def _forward2d(params, bg, width, height, eps_cut, unit_sets=(0,), capacity=None, need_bwd=True, retry=False):
     """unit_sets[c] = parameter set rendered by camera (unit) c (non-decreasing)."""
     L = lib()
     dev = params.device
@@ -805,7 +855,8 @@ def _forward2d(params, bg, width, height, eps_cut, unit_sets=(0,), capacity=None
     C = len(unit_sets)
     sb = _set_begin(tuple(unit_sets), F, dev)
     bgc = _background(bg, C, dev)
-    b = _Bins(dev, C, N, width, height, capacity, ("2d", tuple(unit_sets), F), _chunk_entries["2d"], need_bwd)
+    b = _Bins(dev, C, N, width, height, capacity, ("2d", tuple(unit_sets), F), _chunk_entries["2d"], need_bwd,
+              retry)
     q = b.p
     with _timed("project2d_fwd"):
       check(L.gsr2d_project_fwd(_ptr(p), N, stride, set_stride, _ptr(sb), F, C, width, height, eps_cut, q["rec"],
@@ -817,6 +868,7 @@ def _forward2d(params, bg, width, height, eps_cut, unit_sets=(0,), capacity=None
     b.offsets_wait()
     b.ensure_post(with_chunks=need_bwd)
     b.sort(_lib.ORDER_INDEX, stream)
+    b.verify_launch()
     cs, cl = (q["chunk_state"], q["chunk_list"]) if need_bwd else (None, None)
     rgb = torch.empty(C, height, width, 3, device=dev, dtype=torch.float32)
     alpha = torch.empty(C, height, width, device=dev, dtype=torch.float32)
@@ -825,6 +877,8 @@ def _forward2d(params, bg, width, height, eps_cut, unit_sets=(0,), capacity=None
                              eps_cut, _ptr(bgc), b.n_busy, q["stats_dev"], _ptr(rgb), _ptr(alpha), q["final_T"],
                              q["last"], q["tile_end"], q["tile_cut"], cs, cl, N, _ptr(sb), F, stream),
           "gsr2d_raster_fwd")
+    if b.verify_overflow():
+        return _forward2d(params, bg, width, height, eps_cut, unit_sets, capacity, need_bwd, retry=True)
     _record_stats(b)
     return rgb, alpha, b, (p, F, stride, set_stride, sb, bgc, width, height, eps_cut)
 

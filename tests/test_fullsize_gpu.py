@@ -3,7 +3,13 @@ tests of test_parity_gpu.py cannot reach.
 
 * config 3 (3D, 200k, 576x512, 6 views): one whole view fwd+bwd against the CPU oracle
   (oracle/oracle3d.py, ~10 s on 16 host threads), same tolerances as config 1 in
-  test_parity_gpu.py plus the 0.05 dB PSNR bar of BASELINE.json's north_star.
+  test_parity_gpu.py plus the 0.05 dB PSNR bar of BASELINE.json's north_star.  No fraction
+  of outliers is allowed: oracle3d.tie_flags marks the pixels where a discrete
+  decision sits within 1e-4 (relative) of its threshold (an alpha at 1/255, a T at 1e-4 at a
+  stop, the 0.999 clamp, sigma at 0) -- the only places two correct fp32 implementations may
+  differ.  The forward may leave the tolerance only there, and the cotangent is zero there, so
+  the GRADIENT is compared with no exemption at all (a flipped decision at pixel p moves only
+  the terms pixel p contributes).  Counts are printed.
 * config 5 (3D, 2M, 1152x1024, 6 views): the oracle restricted to three central tile rows
   (oracle3d.isect_tiles' ``band``; the rest of the image is the same computation at other
   tiles), fwd in those rows and the gradient of a cotangent supported on them.
@@ -24,9 +30,19 @@ tests of test_parity_gpu.py cannot reach.
 import pytest
 import torch
 
-from _util import assert_close, forced_fwd_lanes, grad_close
+from _util import assert_close, close_at_ties, forced_fwd_lanes, grad_close, untie_cotangent as _untie
 
 pytestmark = pytest.mark.gpu
+
+# Gradient floor at full size: |a-e| <= 1e-4 |e| + FULL_FLOOR * max|e[:, col]|, every element (no
+# outlier fraction).  A Gaussian's mean gradient is a sum over up to ~10^4 pixel terms that
+# cancel around its centre, so two fp32 summation orders (GPU box reductions vs the oracle's
+# tile sums) differ by ~eps * sum|terms|: the worst such element measured 1.4e-5 (config 3) and
+# 3.95e-5 (config 5 band) of its column's largest gradient on the r06 tree, with the ties'
+# cotangent removed.  (The round-5 tests allowed 0.2 % of the elements up to 2e-3; the racy
+# round-5 update rebuilt as a negative control is off by 0.3-1.9 column scales,
+# tests/test_race_gpu.py.)
+FULL_FLOOR = 5e-5
 
 
 def _scene(idx):
@@ -122,16 +138,17 @@ def test_cfg3_view_vs_oracle(cuda):
     c, p, V, K = _scene(3)
     W, H = c.width, c.height
     vr, va = _cot(1, H, W, 5, "cpu")
+    tie_pix, vr, va = _untie(p, V[:1], K[:1], W, H, vr, va)
     rgb_g, a_g, g_g = _gpu3d(p, V[:1], K[:1], W, H, cuda, vr.to(cuda), va.to(cuda))
     po = p.clone().requires_grad_(True)
     rgb_o, a_o, = render3d(po, V[:1], K[:1], W, H, torch.ones(3))
     torch.autograd.backward([rgb_o, a_o], [vr, va])
-    r = assert_close(rgb_g.cpu(), rgb_o.detach(), max_frac=2e-4, max_outlier=0.02, what="rgb")
-    assert_close(a_g.cpu(), a_o.detach(), max_frac=2e-4, max_outlier=0.02, what="alpha")
-    grad_close(g_g.cpu(), po.grad, max_frac=2e-3, outlier_rel=2e-3, what="grad")
+    close_at_ties(rgb_g.cpu(), rgb_o.detach(), tie_pix, what="cfg3 rgb")
+    close_at_ties(a_g.cpu(), a_o.detach(), tie_pix, what="cfg3 alpha")
+    grad_close(g_g.cpu(), po.grad, rel_floor=FULL_FLOOR, what="cfg3 grad")
     tgt = (rgb_o.detach() + 0.05 * torch.randn(rgb_o.shape, generator=torch.Generator().manual_seed(1))).clamp(0, 1)
     psnr = lambda x: float(10 * torch.log10(1.0 / ((x - tgt) ** 2).mean()))
-    assert abs(psnr(rgb_g.cpu()) - psnr(rgb_o.detach())) < 0.05, r
+    assert abs(psnr(rgb_g.cpu()) - psnr(rgb_o.detach())) < 0.05
 
 
 def test_cfg3_lists_and_properties(cuda):
@@ -153,17 +170,18 @@ def test_cfg2_view_vs_oracle(cuda):
     rgb_f, a_f, _ = _gpu3d(p, V, K, W, H, cuda)
     assert R.last_stats()["n_isect"] > 50_000
     vr, va = _cot(1, H, W, 8, "cpu")
+    tie_pix, vr, va = _untie(p, V, K, W, H, vr, va)
     rgb_g, a_g, g_g = _gpu3d(p, V, K, W, H, cuda, vr.to(cuda), va.to(cuda))
     assert torch.equal(rgb_f, rgb_g) and torch.equal(a_f, a_g)
     po = p.clone().requires_grad_(True)
     rgb_o, a_o = render3d(po, V, K, W, H, torch.ones(3))
     torch.autograd.backward([rgb_o, a_o], [vr, va])
-    r = assert_close(rgb_g.cpu(), rgb_o.detach(), max_frac=2e-4, max_outlier=0.02, what="cfg2 rgb")
-    assert_close(a_g.cpu(), a_o.detach(), max_frac=2e-4, max_outlier=0.02, what="cfg2 alpha")
-    grad_close(g_g.cpu(), po.grad, max_frac=2e-3, outlier_rel=2e-3, what="cfg2 grad")
+    close_at_ties(rgb_g.cpu(), rgb_o.detach(), tie_pix, what="cfg2 rgb")
+    close_at_ties(a_g.cpu(), a_o.detach(), tie_pix, what="cfg2 alpha")
+    grad_close(g_g.cpu(), po.grad, rel_floor=FULL_FLOOR, what="cfg2 grad")
     tgt = (rgb_o.detach() + 0.05 * torch.randn(rgb_o.shape, generator=torch.Generator().manual_seed(1))).clamp(0, 1)
     psnr = lambda x: float(10 * torch.log10(1.0 / ((x - tgt) ** 2).mean()))
-    assert abs(psnr(rgb_g.cpu()) - psnr(rgb_o.detach())) < 0.05, r
+    assert abs(psnr(rgb_g.cpu()) - psnr(rgb_o.detach())) < 0.05
     # the tile lists (36 busy tiles: the split block sort + rank merge) against a stable sort
     I, max_seg = _check_lists_vs_torch_sort(p, V, K, W, H, c.views, cuda)
     assert max_seg > 2048
@@ -180,13 +198,14 @@ def test_cfg5_band_vs_oracle(cuda):
     band = torch.zeros(1, H, W)
     band[:, y0:y1] = 1.0
     vr, va = vr * band[..., None], va * band
+    tie_pix, vr, va = _untie(p, V[:1], K[:1], W, H, vr, va, band=(row, row + 3))
     rgb_g, a_g, g_g = _gpu3d(p, V[:1], K[:1], W, H, cuda, vr.to(cuda), va.to(cuda))
     po = p.clone().requires_grad_(True)
     rgb_o, a_o = render3d(po, V[:1], K[:1], W, H, torch.ones(3), band=(row, row + 3))
     torch.autograd.backward([rgb_o, a_o], [vr, va])
-    assert_close(rgb_g.cpu()[:, y0:y1], rgb_o.detach()[:, y0:y1], max_frac=2e-4, max_outlier=0.02, what="rgb")
-    assert_close(a_g.cpu()[:, y0:y1], a_o.detach()[:, y0:y1], max_frac=2e-4, max_outlier=0.02, what="alpha")
-    grad_close(g_g.cpu(), po.grad, max_frac=2e-3, outlier_rel=2e-3, what="grad")
+    close_at_ties(rgb_g.cpu()[:, y0:y1], rgb_o.detach()[:, y0:y1], tie_pix[:, y0:y1], what="cfg5 band rgb")
+    close_at_ties(a_g.cpu()[:, y0:y1], a_o.detach()[:, y0:y1], tie_pix[:, y0:y1], what="cfg5 band alpha")
+    grad_close(g_g.cpu(), po.grad, rel_floor=FULL_FLOOR, what="cfg5 band grad")
     assert float(po.grad.abs().max()) > 0
 
 

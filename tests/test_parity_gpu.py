@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 import torch
 
-from _util import assert_close, grad_close
+from _util import assert_close, close_at_ties, grad_close, untie_cotangent
 
 pytestmark = pytest.mark.gpu
 
@@ -341,15 +341,18 @@ def test_3d_cfg1_vs_oracle(cuda, fwd_lanes):
     V, K = ring_cameras(c.views, c.width, c.height)
     bg = torch.ones(3)
     vr, va = _cot(1, c.height, c.width, 5)
+    # no outlier fraction: the forward may differ only at the oracle's discrete-
+    # decision ties, which carry no cotangent, so the gradient compares with no exemption
+    tie_pix, vr, va = untie_cotangent(p, V, K, c.width, c.height, vr, va)
     rgb_g, a_g, g_g = _run_gpu3d(p, V, K, c.width, c.height, bg, cuda, vr, va)
     rgb_o, a_o, g_o = _run_oracle3d(p, V, K, c.width, c.height, bg, vr, va)
-    r = assert_close(rgb_g, rgb_o, max_frac=2e-4, max_outlier=0.02, what="rgb")
-    assert_close(a_g, a_o, max_frac=2e-4, max_outlier=0.02, what="alpha")
-    grad_close(g_g, g_o, max_frac=2e-3, outlier_rel=2e-3, what="grad")
+    close_at_ties(rgb_g, rgb_o, tie_pix, what="rgb")
+    close_at_ties(a_g, a_o, tie_pix, what="alpha")
+    grad_close(g_g, g_o, what="grad")
     # PSNR of the rendering against the oracle render must agree to 0.05 dB vs any target
     tgt = (rgb_o + 0.05 * torch.randn(rgb_o.shape, generator=torch.Generator().manual_seed(1))).clamp(0, 1)
     psnr = lambda x: float(10 * torch.log10(1.0 / ((x - tgt) ** 2).mean()))
-    assert abs(psnr(rgb_g) - psnr(rgb_o)) < 0.05, r
+    assert abs(psnr(rgb_g) - psnr(rgb_o)) < 0.05
 
 
 def test_3d_isotropic_radius_mode(cuda):
@@ -420,13 +423,14 @@ def test_3d_long_tile_lists(cuda, fwd_lanes, bwd_layout):
     p[:, 13] = -3.5                       # faint, so pixels terminate late
     bg = torch.zeros(3)
     vr, va = _cot(1, H, W, 42)
+    tie_pix, vr, va = untie_cotangent(p, V, K, W, H, vr, va)
     from gsr import render as R
     rgb_g, a_g, g_g = _run_gpu3d(p, V, K, W, H, bg, cuda, vr, va)
     st = R.last_stats()
     assert st["max_seg"] > 16384, st
     rgb_o, a_o, g_o = _run_oracle3d(p, V, K, W, H, bg, vr, va)
-    assert_close(rgb_g, rgb_o, max_frac=1e-3, max_outlier=0.02, what="rgb")
-    grad_close(g_g, g_o, max_frac=2e-3, outlier_rel=2e-3, what="grad")
+    close_at_ties(rgb_g, rgb_o, tie_pix, what="rgb")
+    grad_close(g_g, g_o, what="grad")
 
 
 # ------------------------------------------------------------------------------------ 2D
