@@ -12,14 +12,16 @@ over the whole job.
 Multi-GPU (torchrun, one process per GPU, RCCL over xGMI), SURVEY.md §8(e).  At N > 1 the
 line reports the default layout as `value` AND the config's other layout next to it (keys
 "weak" / "strong" / "frame_owners", each with its own value, ms_per_step and allreduce_ms):
-  * 3D, --shard views (default, "weak"): a multi-camera batch -- every rank renders C views of
-    its own (ring offset per rank) of the same Gaussians, and the [N,14] gradient is
-    all-reduced in Gaussian-range buckets that overlap the projection backward.
-  * 3D, --shard units ("strong", reported under "strong"): ONE C-view job per step; the C*th
-    (view, tile row) units are cut into `world` contiguous ranges balanced by list entries
-    read plus a per-view cost (gsr.multiview.unit_shard); each rank projects only the views
-    it touches, bins only its rows, and all-reduces its partial v_params in buckets
-    (latency- and exchange-bound at configs 3 and 5: DESIGN.md §5, --rank-share).
+  * 3D, --shard units (default since round 6, "strong"): ONE C-view job per step -- the same
+    job at every N; the C*th (view, tile row) units are cut into `world` contiguous ranges
+    balanced by list entries read plus a per-view cost (gsr.multiview.unit_shard); each rank
+    projects only the views it touches, bins only its rows, and all-reduces its partial
+    v_params in buckets (latency- and exchange-bound at configs 3 and 5: DESIGN.md §5,
+    --rank-share).
+  * 3D, --shard views ("weak", reported under "weak"): a multi-camera batch -- every rank
+    renders C views of its own (ring offset per rank) of the same Gaussians, and the [N,14]
+    gradient is all-reduced in Gaussian-range buckets that overlap the projection backward
+    (N times the work at N ranks: the data-parallel shape, not the 1 -> N curve of one job).
   * 2D (config 4), --shard units (default, "strong"): 8 frames x 6 views = 48 (frame, view)
     units, round-robin over ranks; each rank renders its units batched per frame bucket and
     all-reduces the [8,N,9] gradient per bucket (async, overlapping the next bucket) -- the
@@ -139,7 +141,10 @@ def parse(argv=None):
                          "launches; -1: 1 on a single GPU with bounded capacity, else 0")
     a = ap.parse_args(argv)
     if a.shard is None:
-        a.shard = "units" if a.config == 4 else "views"
+        # every config but 2 (one fwd-only view: replicas) times the SAME job at every N by default:
+        # 3D, the C-view job split into (view, tile row) units; 2D, the 48 (frame, view) units
+        # (the 1 -> N curve must not time N times the work at N ranks)
+        a.shard = "views" if a.config == 2 else "units"
     if a.shard == "frames" and a.config != 4:
         raise SystemExit("--shard frames is the 2D multi-frame layout (config 4)")
     return a
@@ -689,7 +694,8 @@ class Workload:
             self.params.grad = rows_backward_units(self._render_band_rows, self.params, self.Vd, self.Kd,
                                                    self.v_rgb_all, self.v_alpha_all, self.th, self.grad_rows,
                                                    self.weights, view_cost=self.view_cost,
-                                                   status=self.R._status_buf(self.dev))
+                                                   status=self.R._status_buf(self.dev),
+                                                   reuse_output=True)   # (consumed before the next step)
             return
         if self.v1 > self.v0:
             p = self.params.detach().requires_grad_(True)
@@ -1201,9 +1207,11 @@ def main(argv=None):
         "step_roofline": {"algorithmic_bytes": sb * launches_per_step,
                           "achieved": sb * launches_per_step / (ms_per_step * 1e-3) / 1e9,
                           "unit": "GB/s", "frac": sb * launches_per_step / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                          "formula": ("SURVEY.md 8(d): S*N*(12p+64) + R*N*72 + 36*I + 80*I_eff + 44*P per rank "
-                                      "(S = projections: C in 3D, the frames in 2D; R = reduced gradient rows: C, or "
-                                      "the frames in 2D when a frame's units share one backward walk)" if cfg.backward
+                          "formula": ("SURVEY.md 8(d): S*N*(12p+64) + R*N*72 + 36*I + 40*I_eff*(W+1) + 44*P per "
+                                      "rank (S = projections: C in 3D, the frames in 2D; R = reduced gradient rows: C, "
+                                      "or the frames in 2D when a frame's units share one backward walk; W = forward "
+                                      f"walks of each list, {w.fwd_walks(C):g} here: a 2D frame's views each walk "
+                                      "its shared list)" if cfg.backward
                                       else "SURVEY.md 8(d) fwd-only: C*N*(4p+32) + 36*I + 40*I_eff + 20*P per rank")},
         "binning": {"I": I, "I_eff": I_eff, "max_list": R.last_stats().get("max_seg"),
                     "busy_tiles": R.last_stats().get("n_busy"), "tiles": R.last_stats().get("tiles")},

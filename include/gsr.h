@@ -107,6 +107,9 @@ extern "C" {
 #define GSR_OVF_LAZY 16      /* more lazily sorted tiles than the re-render covers            */
 #define GSR_OVF_UNIT 32      /* a raster backward given another chunk_entries than gsr_bin_offsets */
 #define GSR_OVF_EXCHANGE 64  /* a rank touched more Gaussians than its gradient row block holds */
+#define GSR_OVF_LAYOUT 128   /* a 2D call's layout decisions disagree between its calls (a gsr_set_*
+                                setting changed between projection, forward and backward): the
+                                tiles / gradients concerned are NaN */
 
 typedef struct gsr_bin_stats {
   int64_t n_isect;     /* total (Gaussian, tile) intersections I                     */
@@ -123,7 +126,9 @@ typedef struct gsr_bin_stats {
   int32_t chunk_entries; /* list entries per backward work unit (copy of caps->chunk_entries) */
   int32_t* status;     /* copy of caps->status (device; may be NULL)                  */
   int32_t n_sort_long; /* tiles with lists >= 1024 entries (the sort's one-workgroup lists) */
-  int32_t masks;       /* 1: the emission stored 3D quadrant masks in k_of_s (gsr_bin_emit rec) */
+  int32_t masks;       /* bit 0: the emission stored 3D quadrant masks in k_of_s (gsr_bin_emit rec);
+                          bit 1: the 2D forward wrote the colour planes of the split per-set
+                          backward (gsr_set_bwd2d_parts), which checks it */
   int32_t n_heavy;     /* busy tiles with lists >= heavy_min_len entries (gsr_set_fwd_heavy; 0 if
                           off): the first of the busy order, rendered by the 3D forward's
                           heavy-tile layout */
@@ -175,7 +180,14 @@ int gsr_version(void);
  * 25 % of the rows' HBM writes and reads). */
 /* Revision 11: 2D records hold the conic and L times log2(e) (layout above). */
 /* Revision 12: 3D records too hold the conic and L times log2(e). */
-#define GSR_ABI_VERSION 12
+/* Revision 13 (round 6): the 2D contract changes of round 5 and round 6 made explicit -- with more
+ * cameras than parameter sets (C > F) gsr2d_project_fwd bins only each set's first camera (the
+ * other cameras get no tiles and their forwards render the first camera's lists) and
+ * gsr2d_raster_bwd / gsr2d_project_bwd write / read one summed partial row per (set, entry);
+ * gsr_bin_stats.masks became a bit field (bit 1: the 2D forward wrote the split backward's
+ * colour planes); GSR_OVF_LAYOUT (128) flags a 2D call whose calls disagree on those layout
+ * decisions (a gsr_set_* setting changed between them): NaN tiles / gradients, sticky status. */
+#define GSR_ABI_VERSION 13
 int gsr_abi_version(void);
 const char* gsr_last_error(void);
 

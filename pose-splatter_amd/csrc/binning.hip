@@ -256,7 +256,7 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__
     if (ovf) emit_skip_counts(tile_count, tw * th);
     return;
   }
-  if (rec != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) stats->masks = 1;
+  if (rec != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) stats->masks |= kStatsMasks3D;
   // Slots are claimed by counting each tile's count down to zero (slot = tile start +
   // remaining count - 1): no separate cursor array, and tile_count is left zeroed.
   extern __shared__ int hist[];
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(kStageThreads) void k_emit_staged(
     if (ovf) emit_skip_counts(tile_count, tw * th);
     return;
   }
-  if (rec != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) stats->masks = 1;
+  if (rec != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) stats->masks |= kStatsMasks3D;
   constexpr int NT = kStageThreads;
   constexpr int kStagePer = GPT * NT;   // Gaussians per workgroup
   extern __shared__ uint64_t s_key[];   // [kStageCap]

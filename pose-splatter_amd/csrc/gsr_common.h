@@ -443,6 +443,10 @@ __device__ __forceinline__ bool cull_keep(const float4 p0, const float4 p1, cons
 // pixel-centre box -- the same test on the same fp32 box bounds as the raster forward's
 // quadrant workgroups, so a workgroup may skip (not even gather) an entry whose bit is clear.
 // Stored by the emission in the top bits of the entry's emission index (k_of_s).
+// gsr_bin_stats.masks: bit 0 -- the 3D emission stored quadrant masks (k_of_s bits 28..31); bit 1 --
+// the 2D pair forward wrote the colour planes that the split per-set backward starts from
+constexpr int kStatsMasks3D = 1;
+constexpr int kStatsPlanes2D = 2;
 constexpr int kMaskShift = 28;                         // k_of_s bits 28..31
 constexpr int32_t kEmitIndexMask = (1 << kMaskShift) - 1;
 template <bool IS2D>

@@ -120,21 +120,37 @@ __device__ __forceinline__ void box4_cull(const unsigned char* __restrict__ list
   }
 }
 
+// 2D parameter sets of the cameras (gsr2d_*: one record copy per set, rec_offset2d; the XCD-aware
+// sweep, sweep_tile2d).  3D: {0, nullptr, 1}, unused.
+struct Sets2D {
+  int64_t N;
+  const int32_t* begin;
+  int F;
+};
+
 // ---------------------------------------------------------------- empty tiles
 // Tiles with an empty list only need the background.  The forward launches them as extra
 // workgroups (after the busy tiles' ones) that stride over order[n_busy..CT): cheap stores that
 // run beside the busy tiles instead of one short-lived workgroup per empty tile.
+__device__ void nan_tile(int c, int ty, int tx, int W, int H, float* __restrict__ out_rgb, float* __restrict__ out_alpha);
+__device__ __forceinline__ bool lists2d_missing(const int32_t* __restrict__ tile_offset, const Sets2D& sets, int c,
+                                                int ct, int T);
 template <bool IS2D>
 __device__ void fill_empty(const int32_t* __restrict__ order, const int32_t* __restrict__ tile_offset, int n_busy,
                            int busy_blocks, int64_t CT, int W, int H, int tw, int th, const float* __restrict__ bg,
                            float* __restrict__ out_rgb, float* __restrict__ out_alpha, float* __restrict__ out_T,
                            int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end,
-                           uint64_t* __restrict__ tile_cut) {
+                           uint64_t* __restrict__ tile_cut, const Sets2D sets, int32_t* status) {
   const int G = gridDim.x - busy_blocks;
   for (int64_t t = n_busy + (blockIdx.x - busy_blocks); t < CT; t += G) {
     const int ct = order[t];
     int c, ty, tx;
     tile_coords(ct, tw, th, c, ty, tx);
+    if (IS2D && lists2d_missing(tile_offset, sets, c, ct, tw * th)) {
+      if (threadIdx.x == 0 && status != nullptr) atomicOr(status, GSR_OVF_LAYOUT);
+      nan_tile(c, ty, tx, W, H, out_rgb, out_alpha);
+      continue;
+    }
     for (int p = threadIdx.x; p < kTilePix; p += blockDim.x) {   // (256- and 512-thread forwards)
       const int i = ty * kTile + (p >> 4), j = tx * kTile + (p & 15);
       if (i >= H || j >= W) continue;
@@ -176,6 +192,35 @@ __device__ void nan_fill(int64_t CT, int W, int H, int tw, int th, float* __rest
       }
     }
   }
+}
+
+// One tile's pixels NaN (a 2D layout mismatch, lists2d_missing below)
+__device__ void nan_tile(int c, int ty, int tx, int W, int H, float* __restrict__ out_rgb, float* __restrict__ out_alpha) {
+  const float nan = __builtin_nanf("");
+  for (int p = threadIdx.x; p < kTile * kTile; p += blockDim.x) {
+    const int i = ty * kTile + (p >> 4), j = tx * kTile + (p & 15);
+    if (i < H && j < W) {
+      const int64_t pix = ((int64_t)c * H + i) * W + j;
+      out_rgb[pix * 3 + 0] = nan;
+      out_rgb[pix * 3 + 1] = nan;
+      out_rgb[pix * 3 + 2] = nan;
+      out_alpha[pix] = nan;
+    }
+  }
+}
+
+// gsr2d_project_fwd and the 2D raster forward decide lists2d_per_set on the host each
+// (the rule reads gsr_set_fwd_lanes).  A forward that renders a camera from its OWN list after a
+// projection that binned only its set's first camera would draw it as background: its list is
+// then empty where the first camera's is not -- impossible otherwise, a set's cameras render
+// identical lists -- so such a tile is NaN and GSR_OVF_LAYOUT goes to the sticky status.
+__device__ __forceinline__ bool lists2d_missing(const int32_t* __restrict__ tile_offset, const Sets2D& sets, int c,
+                                                int ct, int T) {
+  if (sets.begin == nullptr) return false;
+  const int cf = set_first_camera(sets.begin, sets.F, c);
+  if (cf == c) return false;
+  const int ctl = cf * T + (ct - c * T);
+  return tile_offset[ctl + 1] > tile_offset[ctl];
 }
 
 // ---------------------------------------------------------------- 3D forward
@@ -399,13 +444,6 @@ constexpr float kT2DMin = 2.98023224e-8f;   // 2^-25
 // live, or one whose last composited entry is the prefix's last (the cut key of the next
 // entry must come from a sorted list).  rerun: the second pass over the flagged tiles
 // (list[0..count), sorted whole by then), from scratch.
-// 2D parameter sets of the cameras (gsr2d_*: one record copy per set, rec_offset2d; the XCD-aware
-// sweep, sweep_tile2d).  3D: {0, nullptr, 1}, unused.
-struct Sets2D {
-  int64_t N;
-  const int32_t* begin;
-  int F;
-};
 
 struct FwdLazy {
   const int32_t* tile_sorted;
@@ -505,7 +543,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 6 : (IS2D || LPP != 4) ? 1 : GSR
     n_busy = nb_dev;
     if ((int)blockIdx.x >= busy_blocks) {
       fill_empty<IS2D>(order, tile_offset, n_busy, busy_blocks, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
-                       out_last, tile_end, tile_cut);
+                       out_last, tile_end, tile_cut, sets, stats->status);
       return;
     }
   }
@@ -567,7 +605,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 6 : (IS2D || LPP != 4) ? 1 : GSR
   // 8x8 quadrant is clear cannot reach it -- its record is not even gathered (an entry reaches
   // 1.27 of its tile's 4 quadrants at config 3).  Kept entries still take the exact cull.
   const int qbit = kMaskShift + ((sy >> 3) << 1) + (sx >> 3);
-  if (!stats->masks) kos = nullptr;   // this call's emission stored no masks
+  if ((stats->masks & kStatsMasks3D) == 0) kos = nullptr;   // this call's emission stored no masks
   // kn: the raw emission word of the entry two rounds ahead (all bits set without masks), tested
   // only when its record is gathered a round later.  (Testing it at its load made every round
   // wait out that load's full latency: the mask is an SGPR lane mask, so the compiler placed a
@@ -949,7 +987,7 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
     n_busy = nb_dev;
     if ((int)blockIdx.x >= busy_blocks) {
       fill_empty<IS2D>(order, tile_offset, n_busy, busy_blocks, CT, W, H, tw, th, bg, out_rgb, out_alpha, out_T,
-                       out_last, tile_end, tile_cut);
+                       out_last, tile_end, tile_cut, sets, stats->status);
       return;
     }
   }
@@ -975,6 +1013,11 @@ __global__ __launch_bounds__(kRasterThreads, 6) void k_raster_fwd_box(
   const bool inside = i < H && j < W;
   const float px = (float)j + off, py = (float)i + off;
   const int start = tile_offset[ct], list_end = tile_offset[ct + 1];
+  if (IS2D && start == list_end && lists2d_missing(tile_offset, sets, c, ct, tw * th)) {
+    if (threadIdx.x == 0 && stats->status != nullptr) atomicOr(stats->status, GSR_OVF_LAYOUT);
+    nan_tile(c, ty, tx, W, H, out_rgb, out_alpha);
+    return;
+  }
   const int end = lz.tile_sorted && !lz.rerun ? lz.tile_sorted[ct] : list_end;
   if (threadIdx.x == 0) s_max = -1;
   float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f;
@@ -1238,7 +1281,7 @@ __global__ __launch_bounds__(128, GSR_FWD2P_MINB) void k_raster2d_fwd_pair(
     int H, int tw, int th, const float* __restrict__ bg, float* __restrict__ out_rgb, float* __restrict__ out_alpha,
     float* __restrict__ out_T, int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end,
     float* __restrict__ anchors, const int32_t* __restrict__ chunk_base, int64_t CT, float cut2d,
-    const gsr_bin_stats* __restrict__ stats, const Sets2D sets, int share_lists, int part_colour) {
+    gsr_bin_stats* __restrict__ stats, const Sets2D sets, int share_lists, int part_colour) {
   constexpr int kHS = kChunk3 + 1;   // part j of round entry k at s_r[buf][j][k]; slot 128 a zero record
   __shared__ float4 s_r[2][3][kHS];
   __shared__ __attribute__((aligned(16))) unsigned char s_box[2][8][kBoxStride];
@@ -1251,6 +1294,8 @@ __global__ __launch_bounds__(128, GSR_FWD2P_MINB) void k_raster2d_fwd_pair(
     nan_fill(CT, W, H, tw, th, out_rgb, out_alpha);
     return;
   }
+  // the backward's split walks read the colour planes only if this forward wrote them
+  if (part_colour && anchors != nullptr && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&stats->masks, kStatsPlanes2D);
   if (ct < 0) return;
   int c, ty, tx;
   tile_coords(ct, tw, th, c, ty, tx);
@@ -1278,6 +1323,11 @@ __global__ __launch_bounds__(128, GSR_FWD2P_MINB) void k_raster2d_fwd_pair(
   const bool lead = cfirst == c;
   if (!lead) anchors = nullptr;
   const int start = tile_offset[ctl], end = tile_offset[ctl + 1];
+  if (!share_lists && start == end && lists2d_missing(tile_offset, sets, c, ct, T)) {
+    if (threadIdx.x == 0 && stats->status != nullptr) atomicOr(stats->status, GSR_OVF_LAYOUT);
+    nan_tile(c, ty, tx, W, H, out_rgb, out_alpha);
+    return;
+  }
   if (tid == 0) s_max = -1;
   float TA = 1.f, TlA = 1.f, crA = 0.f, cgA = 0.f, cbA = 0.f, drA = 0.f, dgA = 0.f, dbA = 0.f;
   float TB = 1.f, TlB = 1.f, crB = 0.f, cgB = 0.f, cbB = 0.f, drB = 0.f, dgB = 0.f, dbB = 0.f;
@@ -1709,7 +1759,7 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
 #endif
   const int4 cd = reinterpret_cast<const int4*>(chunk_list)[blockIdx.x];
   const int n_act = stats->n_active, ovf = stats->overflow, ce = stats->chunk_entries;
-  const bool use_masks = !IS2D && stats->masks != 0;
+  const bool use_masks = !IS2D && (stats->masks & kStatsMasks3D) != 0;
   const bool unit_bad = !MULTI && ce != kChunk3;
   if ((ovf != 0) | ((int)blockIdx.x >= n_act) | unit_bad | (cd.y <= 0)) {
     if (unit_bad && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -2648,6 +2698,16 @@ __global__ __launch_bounds__(128, GSR_BWD2F_MINB) void k_raster2d_bwd_frame(
   const int64_t S = (FTP + 7) / 8;
   const int64_t pos = (int64_t)(blockIdx.x & 7) * S + (blockIdx.x >> 3);
   const int ovf = stats->overflow, U = stats->chunk_entries;
+  // split walks start from the colour planes: only if the forward wrote them (ADVICE r5 -- a
+  // gsr_set_bwd2d_parts / gsr_set_fwd_lanes change between the calls); else refuse, loudly
+  const bool planes_missing = parts > 1 && (stats->masks & kStatsPlanes2D) == 0;
+  if (planes_missing) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      atomicOr(&stats->overflow, GSR_OVF_LAYOUT);
+      if (stats->status != nullptr) atomicOr(stats->status, GSR_OVF_LAYOUT);
+    }
+    return;
+  }
   if ((ovf != 0) | (pos >= FTP)) return;
   const int64_t tpos = pos / parts;
   const int part = (int)(pos - tpos * parts);
@@ -3008,7 +3068,7 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
   __shared__ __attribute__((aligned(16))) float s_stage[2][8][GSR_BWD3P_HALFSTAGE ? 32 : 64];
   const int4 cd = reinterpret_cast<const int4*>(chunk_list)[blockIdx.x];
   const int n_act = stats->n_active, ovf = stats->overflow, ce = stats->chunk_entries;
-  const bool use_masks = stats->masks != 0;   // k_of_s bits 28..31 hold quadrant masks
+  const bool use_masks = (stats->masks & kStatsMasks3D) != 0;   // k_of_s bits 28..31 hold quadrant masks
   const bool unit_bad = ce != kChunk3;
   if ((ovf != 0) | ((int)blockIdx.x >= n_act) | unit_bad | (cd.y <= 0)) {
     if (unit_bad && blockIdx.x == 0 && threadIdx.x == 0) {

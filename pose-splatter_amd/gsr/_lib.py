@@ -26,7 +26,7 @@ ORDER_INDEX = 1
 INPUT_ADAPTER = 0
 INPUT_GSPLAT = 1
 
-ABI_VERSION = 12   # include/gsr.h GSR_ABI_VERSION this binding is written for
+ABI_VERSION = 13   # include/gsr.h GSR_ABI_VERSION this binding is written for
 # gsr_set_bwd2d_parts at load (profiles/r05_ab5_bwd2d_parts_sweep.txt; GSR_BWD2D_PART_WGS overrides it
 # for measurements, tools/parts_sweep.sh)
 BWD2D_PART_WORKGROUPS = int(os.environ.get("GSR_BWD2D_PART_WGS", "4608"))
@@ -35,7 +35,8 @@ BWD2D_PART_WORKGROUPS = int(os.environ.get("GSR_BWD2D_PART_WGS", "4608"))
 OVF_BITS = {1: "intersections > isect cap", 2: "chunks > chunk cap", 4: "busy tiles > n_busy bound",
             8: "list longer than the split sort's max_seg", 16: "lazily sorted tiles > n_lazy_max bound",
             32: "raster backward chunk_entries differs from the forward's",
-            64: "a rank touched more Gaussians than its gradient row block holds"}
+            64: "a rank touched more Gaussians than its gradient row block holds",
+            128: "a 2D call's layout decisions changed between its calls (gsr_set_* settings)"}
 ROW_FLOATS = 16   # GSR_ROW_FLOATS: floats per row of a sparse gradient row block
 
 GSR_EINVAL = -1

@@ -313,14 +313,16 @@ def rows_capacity(touched: int, group=None, margin: float = 1.25, slack: int = 1
 def rows_backward_units(render_band_rows: Callable, params: torch.Tensor, viewmats: torch.Tensor,
                         Ks: torch.Tensor, v_rgb: torch.Tensor, v_alpha: torch.Tensor, rows: int,
                         grad_rows: GradRows, weights=None, group=None, view_cost: float = 0.0,
-                        status: torch.Tensor | None = None) -> torch.Tensor:
+                        status: torch.Tensor | None = None, reuse_output: bool = False) -> torch.Tensor:
     """Gradient of sum(rgb*v_rgb + alpha*v_alpha) over all C views, (view, row)-unit sharded,
     with the device sparse exchange.  ``render_band_rows(p, viewmats_sub, Ks_sub, band, grad_rows)``
     renders views v0..v1-1 binned to ``band`` with ``RenderOptions3D(grad_rows=grad_rows)``;
     its backward leaves the touched rows in ``grad_rows.block``.  The blocks of all ranks are
     all-gathered and summed in rank order (``gsr_rows_scatter_add``): identical bits on every
     rank, no host synchronisation (a rank with more touched rows than the capacity makes the
-    result NaN and sets GSR_OVF_EXCHANGE in ``status``)."""
+    result NaN and sets GSR_OVF_EXCHANGE in ``status``).  The dense result is built in a buffer
+    of ``grad_rows`` that the next call overwrites: a copy is returned unless ``reuse_output``
+    (a caller that consumes the gradient before its next call, e.g. bench.py)."""
     from . import _lib
     L = _lib.lib()
     world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -336,8 +338,7 @@ def rows_backward_units(render_band_rows: Callable, params: torch.Tensor, viewma
         _lib.check(L.gsr3d_touched_rows(None, None, None, None, None, 0, 0, grad_rows.cap, None,
                                         grad_rows.block.data_ptr(), stream), "gsr3d_touched_rows")
     blk = grad_rows.block
-    # the gathered blocks and the dense result live in grad_rows (reused every step: the returned
-    # tensor is overwritten by the next call -- clone it to keep it)
+    # the gathered blocks and the dense result live in grad_rows (reused every step)
     gathered, out = grad_rows.buffers(world, params.shape[0])
     if world > 1:
         if dist.get_backend(group) == "nccl":
@@ -348,7 +349,7 @@ def rows_backward_units(render_band_rows: Callable, params: torch.Tensor, viewma
         gathered = blk[None]
     _lib.check(L.gsr_rows_scatter_add(gathered.data_ptr(), world, grad_rows.cap, out.data_ptr(), params.shape[0],
                                       None if status is None else status.data_ptr(), stream), "gsr_rows_scatter_add")
-    return out
+    return out if reuse_output else out.clone()
 
 
 def frame_view_units(F: int, V: int, world: int, rank: int) -> list:

@@ -83,7 +83,9 @@ def test_byte_formulas_and_allreduce_model():
 
 def test_bench_args_defaults():
     a = bench.parse([])
-    assert a.config == 3 and a.gpus == 1 and a.shard == "views" and a.cpu_threads == 0
+    # configs 3 and 5 time ONE job at every N (the strong layout) by default
+    assert a.config == 3 and a.gpus == 1 and a.shard == "units" and a.cpu_threads == 0
+    assert bench.parse(["--config", "5"]).shard == "units" and bench.parse(["--config", "2"]).shard == "views"
     assert a.capacity == "bounded" and a.graph == -1
     assert bench.cpu_threads(3) == 3 and bench.cpu_threads(0) >= 1
     assert a.split == 1
@@ -154,10 +156,12 @@ def _layout_worker(rank, world, port, q):
             for sh in bench.other_layouts(cfg, shard):
                 res[(idx, bench.LAYOUT_KEY[sh])] = bench.measure_layout(cfg, args, "cpu", world, rank, sh, dist,
                                                                         make_workload=FakeWorkload, timer=timer)
-        # the headline line's timing at N > 1: eager (graph off by default there), value_eager = value
+        # the headline line's timing at N > 1: eager (graph off by default there), value_eager = value;
+        # config 3's default layout is the strong one (the same job at every N)
         hargs = bench.parse(["--steps", "3", "--warmup", "1", "--graph", "0"])
-        w = FakeWorkload(CONFIGS[3], "cpu", world, rank, "views", 1, "none", True, 0.3, "dense")
+        w = FakeWorkload(CONFIGS[3], "cpu", world, rank, hargs.shard, 1, "none", True, 0.3, "dense")
         res["headline"] = bench.headline_timing(w, hargs, dist, "cpu", world, timer=timer)[0]
+        res["headline_layout"] = (bench.LAYOUT_KEY[hargs.shard], w.scaling, w.units_total)
         if rank == 0:
             q.put(res)
     finally:
@@ -165,14 +169,14 @@ def _layout_worker(rank, world, port, q):
 
 
 def test_other_layouts_reported_gloo_world2():
-    """at N > 1 one bench.py run reports config 3's weak (default) AND strong
+    """at N > 1 one bench.py run reports config 3's strong (default) AND weak
     layouts, and config 4's round-robin all-reduce layout (default) AND the frame owners, each
     with its own value and collective timing -- rehearsed with two gloo ranks on the CPU."""
     import multiprocessing as mp
     import socket
     from gsr.scenes import CONFIGS
     assert bench.parse(["--config", "4"]).shard == "units"   # the all-reduce layout is the default
-    assert bench.other_layouts(CONFIGS[3], "views") == ["units"]
+    assert bench.other_layouts(CONFIGS[3], "units") == ["views"]
     assert bench.other_layouts(CONFIGS[4], "units") == ["frames"]
     assert bench.other_layouts(CONFIGS[2], "views") == []
     with socket.socket() as so:
@@ -187,9 +191,12 @@ def test_other_layouts_reported_gloo_world2():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    strong = res[(3, "strong")]
-    assert strong["scaling"] == "strong" and strong["value"] > 0 and strong["allreduce_ms"] is not None
-    assert strong["units_per_step"] == CONFIGS[3].views
+    # config 3 at N = 2: value is the strong layout (one 6-view job), the weak one a secondary key
+    assert res["headline_layout"] == ("strong", "strong", CONFIGS[3].views), res["headline_layout"]
+    weak = res[(3, "weak")]
+    assert weak["scaling"] == "weak" and weak["value"] > 0 and weak["allreduce_ms"] is not None
+    assert weak["units_per_step"] == 2 * CONFIGS[3].views
+    strong = weak
     owners = res[(4, "frame_owners")]
     assert owners["value"] > 0 and owners["allreduce_ms"] is None   # no Gaussian-gradient collective
     assert set(strong) >= {"value", "ms_per_step", "allreduce_ms", "parallelism", "scaling", "launch_mode"}

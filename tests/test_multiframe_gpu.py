@@ -117,3 +117,72 @@ def test_split_set_backward_matches_whole_walks(cuda, target):
         torch.autograd.backward([r1, a1], [vr[c].to(cuda), va[c].to(cuda)])
         ref += ps.grad.double().cpu()
     grad_close(grads[0][1], ref, rtol=1e-5, rel_floor=1e-6, what="split vs single-camera passes")
+
+
+def test_layout_change_between_forward_and_backward_fails_loudly(cuda):
+    """the split per-set backward (gsr_set_bwd2d_parts) starts its parts from colour
+    planes the FORWARD writes only if it split too.  A setting changed between the two calls must
+    not give silently wrong gradients: the forward records the planes in gsr_bin_stats.masks, and
+    a backward that would read unwritten planes refuses -- NaN gradients, GSR_OVF_LAYOUT in the
+    sticky status."""
+    from gsr import _lib, render as R
+    F, N, W, H = 1, 400, 64, 48
+    P = _frames(F, N, W, H, 91)
+    sets = (0, 0, 0)
+    bg = torch.ones(3)
+    g = torch.Generator().manual_seed(92)
+    vr, va = torch.randn(3, H, W, 3, generator=g), torch.randn(3, H, W, generator=g)
+    L = _lib.lib()
+    R.overflow_status(cuda, reset=True)
+    try:
+        _lib.check(L.gsr_set_bwd2d_parts(0), "gsr_set_bwd2d_parts")        # forward: whole walks, no planes
+        pb = P.to(cuda).requires_grad_(True)
+        rgb, alpha = R.render2d_units(pb, sets, W, H, bg.to(cuda), capacity="exact")
+        assert torch.isfinite(rgb).all()
+        _lib.check(L.gsr_set_bwd2d_parts(_lib.BWD2D_PART_WORKGROUPS), "gsr_set_bwd2d_parts")   # backward: split
+        torch.autograd.backward([rgb, alpha], [vr.to(cuda), va.to(cuda)])
+        assert not bool(torch.isfinite(pb.grad).any()), "a split backward over unwritten planes must not compute"
+        bits = R.overflow_status(cuda, reset=True)
+        assert bits & 128, bits
+        # the consistent calls (both split) are fine
+        pb2 = P.to(cuda).requires_grad_(True)
+        rgb2, alpha2 = R.render2d_units(pb2, sets, W, H, bg.to(cuda), capacity="exact")
+        torch.autograd.backward([rgb2, alpha2], [vr.to(cuda), va.to(cuda)])
+        assert torch.isfinite(pb2.grad).all() and R.overflow_status(cuda, reset=True) == 0
+    finally:
+        _lib.check(L.gsr_set_bwd2d_parts(_lib.BWD2D_PART_WORKGROUPS), "gsr_set_bwd2d_parts")
+
+
+def test_lists_layout_change_between_projection_and_forward_fails_loudly(cuda, monkeypatch):
+    """gsr2d_project_fwd bins only each set's first camera when the forward will share
+    its lists (automatic layout).  A forward forced to another layout after that projection
+    (gsr_set_fwd_lanes changed between the two calls) would render the other cameras from their
+    own, empty, lists as background; it writes NaN there instead and flags GSR_OVF_LAYOUT."""
+    from gsr import _lib, render as R
+    F, N, W, H = 1, 400, 64, 48
+    P = _frames(F, N, W, H, 93)
+    real = _lib.lib()
+
+    class Proxy:   # flips the forward layout between the projection and the raster forward
+        def __getattr__(self, name):
+            fn = getattr(real, name)
+            if name != "gsr2d_raster_fwd":
+                return fn
+
+            def wrapped(*a):
+                _lib.check(real.gsr_set_fwd_lanes(1), "gsr_set_fwd_lanes")
+                return fn(*a)
+            return wrapped
+
+    monkeypatch.setattr(R, "lib", lambda: Proxy())
+    R.overflow_status(cuda, reset=True)
+    try:
+        with torch.no_grad():
+            rgb, alpha = R.render2d_units(P.to(cuda), (0, 0, 0), W, H, torch.ones(3, device=cuda), capacity="exact")
+    finally:
+        _lib.check(real.gsr_set_fwd_lanes(0), "gsr_set_fwd_lanes")
+    assert torch.isfinite(rgb[0]).all()                         # the set's first camera renders its list
+    bad = ~torch.isfinite(rgb[1:])
+    assert bool(bad.any())                                      # the others: NaN where it has entries,
+    assert bool((rgb[1:][~bad] == 1.0).all())                   # background only where it has none
+    assert R.overflow_status(cuda, reset=True) & 128
