@@ -68,6 +68,7 @@ import torch  # noqa: E402
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 XGMI_LINK_GBS = 153.0   # one xGMI link, per direction (ring all-reduce cost model)
 N_SIMDS = 256 * 4       # MI355X: 256 CUs x 4 SIMDs
+CLOCK_GHZ = 2.4         # MI355X maximum engine clock (MI355X_MICROARCH.md)
 PROFILES = os.path.join(ROOT, "profiles")
 FRAMES_2D = 8           # config 4: 8 frames x 6 views
 
@@ -840,6 +841,11 @@ def time_steps(w: Workload, steps: int, warmup: int, dist=None, graph: bool = Fa
             for _ in range(steps):
                 w.step()
         torch.cuda.synchronize()
+        # one untimed replay first: a graph's first launch also uploads it (its kernel nodes'
+        # arguments and resources), a fixed cost the 20-step driver run saw as graph-timed steps
+        # slower than the same steps launched eagerly
+        g.replay()
+        torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -932,6 +938,14 @@ def roofline(w: Workload, dom_name, dom, args):
     tfile = pmc_files(cfg.index, "traffic", args.pmc_dir) if dom_name else None
     sq = pmc_files(cfg.index, "sq", args.pmc_dir) if dom_name else None
     traffic = traffic_from_csv(tfile, sym) if tfile else None
+    valu = valu_from_csv(sq, sym) if sq else None
+    if valu is not None and dom_ms > 0:
+        # the kernel's VALU floor: its wave64 VALU instructions (PMC) at 2 cycles each on the
+        # 1 024 SIMDs at the 2.4 GHz maximum clock -- the bound of a VALU-issue-bound kernel
+        # (config 4's 2D forward: 67 % issue), next to the HBM fraction
+        floor_ms = 2.0 * valu["insts_per_launch"] / (N_SIMDS * CLOCK_GHZ * 1e9) * 1e3
+        valu.update(floor_ms=floor_ms, frac_of_floor=floor_ms / dom_ms,
+                    floor_model=f"SQ_INSTS_VALU x 2 cycles / ({N_SIMDS} SIMDs x {CLOCK_GHZ} GHz)")
     return {"bound": "hbm", "kernel": dom_name, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "traffic_source": os.path.relpath(tfile, ROOT) if traffic is not None else None,
@@ -939,7 +953,7 @@ def roofline(w: Workload, dom_name, dom, args):
             "timing": ("HIP events around each launch on its stream, over the timed steps" if not args.graph else
                        "HIP events around each launch on its stream, over as many eager bounded steps run right "
                        "after the graph-timed region (ROCm rejects timing events inside a captured graph)"),
-            "valu": valu_from_csv(sq, sym) if sq else None,
+            "valu": valu,
             "units_per_launch": {"C": C, "P": P, "N": cfg.N, "I": I, "I_eff": I_eff}}, (C, P, I, I_eff)
 
 

@@ -342,13 +342,6 @@ __global__ __launch_bounds__(kStageThreads) void k_emit_staged(
     int64_t N, int tw, int th, int order, const int32_t* __restrict__ tile_offset, int32_t* __restrict__ tile_count,
     uint64_t* __restrict__ keys, int32_t* __restrict__ k_of_slot, gsr_bin_stats* __restrict__ stats,
     int64_t cap) {
-  const int ovf = stats->overflow & kOvfCapacity;   // see k_emit
-  const int64_t n_isect = stats->n_isect;
-  if (ovf | (n_isect > cap)) {
-    if (ovf) emit_skip_counts(tile_count, tw * th);
-    return;
-  }
-  if (rec != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) stats->masks |= kStatsMasks3D;
   constexpr int NT = kStageThreads;
   constexpr int kStagePer = GPT * NT;   // Gaussians per workgroup
   extern __shared__ uint64_t s_key[];   // [kStageCap]
@@ -361,16 +354,33 @@ __global__ __launch_bounds__(kStageThreads) void k_emit_staged(
   const int c = blockIdx.y;
   int32_t* gcnt = tile_count + (int64_t)c * T;
   const int32_t* toff = tile_offset + (int64_t)c * T;
-  // a camera with no entries (2D: a set's other cameras, lists2d_per_set) -- nothing to stage
-  if (toff[0] == toff[T]) return;
   const int64_t n0 = (int64_t)blockIdx.x * kStagePer;
-  for (int t = threadIdx.x; t < T; t += NT) cur[t] = 0;
+  // Every load that depends on nothing is issued here, in one round trip: the stats words, the
+  // camera's list range and this thread's Gaussians' rects, sort keys and emission offsets (the
+  // tests below, then the keys' use after the claims, used to wait for each in turn: three
+  // memory latencies on every workgroup's chain, round 6)
+  const int ovf = stats->overflow & kOvfCapacity;   // see k_emit
+  const int64_t n_isect = stats->n_isect;
+  const int cam_first = toff[0], cam_end = toff[T];
   uint2 rr[GPT];
+  uint64_t key[GPT];
+  int k0[GPT];
 #pragma unroll
   for (int j = 0; j < GPT; ++j) {
     const int64_t n = n0 + threadIdx.x + j * NT;
-    rr[j] = n < N ? rect[(int64_t)c * N + n] : make_uint2(0u, 0u);
+    const int64_t cn = (int64_t)c * N + (n < N ? n : 0);
+    rr[j] = n < N ? rect[cn] : make_uint2(0u, 0u);
+    key[j] = sort_key(depth, cn, order);
+    k0[j] = isect_offset[cn];
   }
+  if (ovf | (n_isect > cap)) {
+    if (ovf) emit_skip_counts(tile_count, tw * th);
+    return;
+  }
+  if (rec != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) stats->masks |= kStatsMasks3D;
+  // a camera with no entries (2D: a set's other cameras, lists2d_per_set) -- nothing to stage
+  if (cam_first == cam_end) return;
+  for (int t = threadIdx.x; t < T; t += NT) cur[t] = 0;
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < GPT; ++j) {
@@ -412,15 +422,6 @@ __global__ __launch_bounds__(kStageThreads) void k_emit_staged(
   }
   __syncthreads();
   const bool staged = total <= kStageCap;   // uniform: else scatter directly (huge rects)
-  uint64_t key[GPT];
-  int k0[GPT];
-#pragma unroll
-  for (int j = 0; j < GPT; ++j) {
-    const int64_t n = n0 + threadIdx.x + j * NT;
-    const int64_t cn = (int64_t)c * N + (n < N ? n : 0);
-    key[j] = sort_key(depth, cn, order);
-    k0[j] = isect_offset[cn];
-  }
 #pragma unroll
   for (int j = 0; j < GPT; ++j) {
     const int x0 = rr[j].x & 0xffff, x1 = rr[j].x >> 16, y0 = rr[j].y & 0xffff, y1 = rr[j].y >> 16;
