@@ -128,7 +128,8 @@ typedef struct gsr_bin_stats {
   int32_t n_sort_long; /* tiles with lists >= 1024 entries (the sort's one-workgroup lists) */
   int32_t masks;       /* bit 0: the emission stored 3D quadrant masks in k_of_s (gsr_bin_emit rec);
                           bit 1: the 2D forward wrote the colour planes of the split per-set
-                          backward (gsr_set_bwd2d_parts), which checks it */
+                          backward (gsr_set_bwd2d_parts), which checks it;
+                          bit 2: the 3D forward wrote box survivor masks (box_masks) */
   int32_t n_heavy;     /* busy tiles with lists >= heavy_min_len entries (gsr_set_fwd_heavy; 0 if
                           off): the first of the busy order, rendered by the 3D forward's
                           heavy-tile layout */
@@ -187,7 +188,10 @@ int gsr_version(void);
  * gsr_bin_stats.masks became a bit field (bit 1: the 2D forward wrote the split backward's
  * colour planes); GSR_OVF_LAYOUT (128) flags a 2D call whose calls disagree on those layout
  * decisions (a gsr_set_* setting changed between them): NaN tiles / gradients, sticky status. */
-#define GSR_ABI_VERSION 13
+/* Revision 14 (round 6): gsr3d_raster_fwd, gsr3d_raster_fwd_lazy, gsr3d_raster_bwd and
+ * gsr3d_raster_bwd_loss take box_masks (before the stream): the forward's per-chunk box
+ * survivor masks, stats->masks bit 2. */
+#define GSR_ABI_VERSION 14
 int gsr_abi_version(void);
 const char* gsr_last_error(void);
 
@@ -405,13 +409,20 @@ int gsr_bin_sort_lazy(const float* depth, const float* rec, const uint32_t* rect
  * stats->n_active).  stats: the device gsr_bin_stats of gsr_bin_offsets.
  * k_of_s (may be NULL): the sort's emission indices; when the emission stored quadrant masks
  * in them (stats->masks, gsr_bin_emit given rec) a quadrant workgroup gathers only the entries
- * whose bit is set.  The outputs are the same bit for bit either way. */
+ * whose bit is set.  The outputs are the same bit for bit either way.
+ * box_masks (may be NULL; ABI 14): uint32 [chunk rows][16][4], chunk rows as chunk_state.  With
+ * 128-entry chunks (chunk_entries 0 or 128) the quad-layout forward writes, per chunk and 4x4
+ * pixel box b of the tile (b = 4 * quadrant + box in quadrant, row-major), the 128-bit mask of
+ * the chunk's entries that survive both culls for that box (empty once every pixel of the box
+ * is done), and sets stats->masks bit 2; gsr3d_raster_bwd given the same buffer then lists
+ * each box's entries from the masks instead of culling again.  Results are the same. */
 int gsr3d_raster_fwd(const float* rec, const float* depth, const int32_t* sorted_ids, const int32_t* k_of_s,
                      const int32_t* tile_offset,
                      const int32_t* tile_order, const int32_t* chunk_base, int C, int width,
                      int height, const float* bg, int32_t n_busy, gsr_bin_stats* stats,
                      float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
-                     uint64_t* tile_cut, float* chunk_state, int32_t* chunk_list, void* stream);
+                     uint64_t* tile_cut, float* chunk_state, int32_t* chunk_list, uint32_t* box_masks,
+                     void* stream);
 
 /* gsr3d_raster_fwd over the lists of gsr_bin_sort_lazy (same outputs, see above): the tiles
  * that read past their sorted prefix are sorted whole (sort_workspace / k_of_s / max_seg of
@@ -423,20 +434,22 @@ int gsr3d_raster_fwd_lazy(const float* rec, const float* depth, int32_t* sorted_
                           const float* bg, int32_t n_busy, gsr_bin_stats* stats, float* rgb, float* alpha,
                           float* final_T, int32_t* last, int32_t* tile_end, uint64_t* tile_cut, float* chunk_state,
                           int32_t* chunk_list, int32_t* lazy, int32_t n_lazy_max, int32_t max_seg,
-                          void* sort_workspace, size_t sort_workspace_bytes, int32_t* k_of_s, void* stream);
+                          void* sort_workspace, size_t sort_workspace_bytes, int32_t* k_of_s, uint32_t* box_masks,
+                          void* stream);
 
 /* Backward of gsr3d_raster_fwd: workgroup b takes chunk_list[b] for b < stats->n_active
  * (n_chunks bounds the grid).  chunk_entries: the caps->chunk_entries given to gsr_bin_offsets
  * (0 = GSR_CHUNK); it selects the one- or the multi-sub-chunk kernel, and a mismatch with the
  * forward is flagged GSR_OVF_UNIT (NaN gradients).  v_rgb [C,H,W,3], v_alpha [C,H,W]
  * (contiguous).  Writes the partial row k_of_s[s] of every sorted entry s in [tile start,
- * tile_end). */
+ * tile_end).  box_masks (may be NULL): the buffer given to the forward (used only when
+ * stats->masks bit 2 says it wrote it). */
 int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
                      const int32_t* tile_end, const int32_t* chunk_base, const float* chunk_state,
                      const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
                      int32_t chunk_entries, int C, int width, int height, const float* bg, const float* final_T,
                      const int32_t* last, const float* v_rgb, const float* v_alpha,
-                     const int32_t* k_of_s, float* partial, void* stream);
+                     const int32_t* k_of_s, float* partial, const uint32_t* box_masks, void* stream);
 
 /* 2D index-order compositor (src/gaussian_renderer.py:416-425), integer pixel centres, on
  * the 3D kernels' structure (C cameras of gsr2d_project_fwd, index-order keys).  Since ABI 6
@@ -574,7 +587,7 @@ int gsr3d_raster_bwd_loss(const float* rec, const int32_t* sorted_ids, const int
                           const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats,
                           int32_t n_chunks, int32_t chunk_entries, int C, int width, int height, const float* bg,
                           const float* final_T, const int32_t* last, const gsr_loss_terms* loss,
-                          const int32_t* k_of_s, float* partial, void* stream);
+                          const int32_t* k_of_s, float* partial, const uint32_t* box_masks, void* stream);
 
 /* ---- Parameter head + pose transform ----------------------------
  * Replace the post-MLP part of PoseSplatter.get_gaussian_params_from_volume_unified

@@ -1000,6 +1000,83 @@ __device__ __forceinline__ void wave_sort_list(uint64_t* a, int* hist, int n, co
   }
 }
 
+// MSD partition of a long list (> lds_keys, <= kMsdRegs NT keys) from REGISTERS: the list's
+// sort words are loaded once (every load of a thread in flight together: one memory round trip),
+// OR-ed for the varying bits, counted into per-wave digit counters, scanned digit-major /
+// wave-minor in parallel, and scattered to part[] as (word << 32 | i) with per-wave returning
+// atomics.  (The loop form read the list three times, a batch of 8 loads per thread per round
+// trip, and scanned the 256 buckets on one thread: ~61 of a long list's ~90 us at config 5,
+// profiles/r06_sort_trace_cfg5.txt.)  Order inside a bucket is free: each group of buckets is
+// then sorted whole, ties by c*N+n.  Leaves s_dstart[0..256] (bucket starts) and *s_maxb.
+#ifndef GSR_MSD_REGS
+#define GSR_MSD_REGS 1
+#endif
+constexpr int kMsdRegs = 32;
+template <int NT>
+__device__ __forceinline__ void msd_partition_regs(SortGroup<NT>& g, const uint64_t* __restrict__ seg, int len,
+                                                   int* s_hist, int* s_dstart, unsigned* s_or, int* s_maxb,
+                                                   uint64_t* __restrict__ part, int lds_keys) {
+  constexpr int W = NT / 64;
+  static_assert(W == 16, "digit totals below: 16 per-wave counters per digit = one lane quad");
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  for (int i = lane; i < 256; i += 64) s_hist[wv * 256 + i] = 0;
+  const uint32_t w0 = sort_word(seg[0]);
+  uint32_t w[kMsdRegs];
+#pragma unroll
+  for (int j = 0; j < kMsdRegs; ++j) {
+    const int i = tid + j * NT;
+    w[j] = sort_word(seg[i < len ? i : 0]);
+  }
+  uint32_t orv = 0;
+#pragma unroll
+  for (int j = 0; j < kMsdRegs; ++j) orv |= w[j] ^ w0;   // (clamped duplicates of seg[0] add nothing)
+  orv = (uint32_t)wave_or_i((int)orv);
+  __syncthreads();   // s_or / s_maxb initialised, the counters zeroed
+  if (lane == 0 && orv) atomicOr(s_or, orv);
+  __syncthreads();
+  const uint32_t varying = *s_or;
+  const int sh = varying ? max(31 - __clz(varying) - 7, 0) : 0;
+#pragma unroll
+  for (int j = 0; j < kMsdRegs; ++j)
+    if (tid + j * NT < len) atomicAdd(&s_hist[wv * 256 + ((w[j] >> sh) & 0xFFu)], 1);
+  __syncthreads();
+  int v[4], sum = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = tid * 4 + j;   // counter (wave c & 15, digit c >> 4)
+    v[j] = s_hist[(c & 15) * 256 + (c >> 4)];
+    sum += v[j];
+  }
+  // digit tid >> 2's total: the sums of the lane quad that holds its 16 counters
+  int dt = sum + dpp_row_i<0xB1>(sum);   // quad_perm [1,0,3,2]
+  dt += dpp_row_i<0x4E>(dt);             // quad_perm [2,3,0,1]
+  const int mb = wave_max_i(dt);
+  int total;
+  int run = group_exclusive_scan<NT>(g, sum, s_hist + W * 256 + 8, &total);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = tid * 4 + j;
+    s_hist[(c & 15) * 256 + (c >> 4)] = run;
+    if ((c & 15) == 0) s_dstart[c >> 4] = run;
+    run += v[j];
+  }
+  if (lane == 0) atomicMax(s_maxb, mb);
+  if (tid == 0) s_dstart[256] = len;
+  __syncthreads();
+  if (*s_maxb <= lds_keys) {
+#pragma unroll
+    for (int j = 0; j < kMsdRegs; ++j) {
+      const int i = tid + j * NT;
+      if (i < len) {
+        const int pos = atomicAdd(&s_hist[wv * 256 + ((w[j] >> sh) & 0xFFu)], 1);
+        part[pos] = ((uint64_t)w[j] << 32) | (uint64_t)(uint32_t)i;
+      }
+    }
+    __threadfence_block();
+    __syncthreads();
+  }
+}
+
 // Outputs: sorted_ids[s] = c*N+n of sorted entry s; k_of_s[s] = its emission entry index.
 #ifdef GSR_SORT_TRACE
 // timing build only (tools/sort_trace.py): per workgroup {start, end, list length, hw id}
@@ -1155,6 +1232,16 @@ __global__ __launch_bounds__(NT) void k_segsort(
       s_maxb = 0;
     }
     for (int d = threadIdx.x; d < 256; d += blockDim.x) s_dcur[d] = 0;
+    bool in_regs = false;
+#if GSR_MSD_REGS
+    if constexpr (NT == 1024) {
+      if (len <= kMsdRegs * NT) {
+        msd_partition_regs<NT>(g, seg, len, s_hist, s_dstart, &s_or, &s_maxb, tmpk + start, lds_keys);
+        in_regs = true;
+      }
+    }
+#endif
+    if (!in_regs) {
     __syncthreads();
     const uint32_t w0 = sort_word(seg[0]);
     uint32_t orv = 0;
@@ -1217,6 +1304,10 @@ __global__ __launch_bounds__(NT) void k_segsort(
       }
       __threadfence_block();
       __syncthreads();
+    }
+    }
+    if (s_maxb <= lds_keys) {
+      uint64_t* part = tmpk + start;
       int d0 = 0;
       while (d0 < 256) {
         const int g0 = s_dstart[d0];

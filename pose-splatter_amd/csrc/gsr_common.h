@@ -421,13 +421,28 @@ __device__ __forceinline__ constexpr float conic_unscale() {
   return (IS2D || GSR_CONIC3D_LOG2E) ? kLn2 : 1.f;
 }
 
+#ifndef GSR_CULL_BRANCHFREE
+#define GSR_CULL_BRANCHFREE 0
+#endif
 template <bool IS2D>
 __device__ __forceinline__ bool cull_keep(const float4 p0, const float4 p1, const float4 p2, float bx0, float bx1,
                                           float by0, float by1) {
   (void)IS2D;   // 3D: L = ln(opacity * 255); 2D: L = ln(opacity / eps_cut)
   const float L = p0.w;   // < 0: the Gaussian never reaches the cut anywhere
-  if (!(L >= 0.f)) return false;
   const float a = p1.x, b = p1.y, c = p1.z;
+#if GSR_CULL_BRANCHFREE
+  // the same decision without early exits (every term is evaluated; the selects pick as the
+  // branches did): exec-mask branches cost scalar instructions on every culled entry
+  const bool pd = a > 0.f && c > 0.f && 4.f * a * c > b * b;   // not positive definite: keep
+  const float dxe = p0.x - fminf(fmaxf(p0.x, bx0), bx1);
+  const float dye = p0.y - fminf(fmaxf(p0.y, by0), by1);
+  const float dy1 = fminf(fmaxf(p1.w * dxe, p0.y - by1), p0.y - by0);
+  const float dx2 = fminf(fmaxf(p2.w * dye, p0.x - bx1), p0.x - bx0);
+  const float s1 = a * dxe * dxe + b * dxe * dy1 + c * dy1 * dy1;
+  const float s2 = a * dx2 * dx2 + b * dx2 * dye + c * dye * dye;
+  return (L >= 0.f) & (!pd | (fminf(s1, s2) <= L * 1.001f + 1e-3f));
+#else
+  if (!(L >= 0.f)) return false;
   if (!(a > 0.f && c > 0.f && 4.f * a * c > b * b)) return true;   // not positive definite: keep
   const float dxe = p0.x - fminf(fmaxf(p0.x, bx0), bx1);
   const float dye = p0.y - fminf(fmaxf(p0.y, by0), by1);
@@ -436,6 +451,7 @@ __device__ __forceinline__ bool cull_keep(const float4 p0, const float4 p1, cons
   const float s1 = a * dxe * dxe + b * dxe * dy1 + c * dy1 * dy1;
   const float s2 = a * dx2 * dx2 + b * dx2 * dye + c * dye * dye;
   return fminf(s1, s2) <= L * 1.001f + 1e-3f;
+#endif
 }
 
 // Quadrant mask of a (record, tile) list entry: bit q (q = 2 * (quadrant row) + quadrant
@@ -447,6 +463,7 @@ __device__ __forceinline__ bool cull_keep(const float4 p0, const float4 p1, cons
 // the 2D pair forward wrote the colour planes that the split per-set backward starts from
 constexpr int kStatsMasks3D = 1;
 constexpr int kStatsPlanes2D = 2;
+constexpr int kStatsBoxMasks = 4;   // bit 2: the 3D quad forward wrote per-box survivor masks (box_masks)
 constexpr int kMaskShift = 28;                         // k_of_s bits 28..31
 constexpr int32_t kEmitIndexMask = (1 << kMaskShift) - 1;
 template <bool IS2D>

@@ -490,6 +490,23 @@ extern "C" int gsr_debug_fwd_trace(void* buf) {
 #ifndef GSR_FWD_PRIO_LEN
 #define GSR_FWD_PRIO_LEN 2048
 #endif
+#ifndef GSR_BOXM
+#define GSR_BOXM 1   // the quad forward writes each chunk's box survivor masks for the backward
+#endif
+#ifndef GSR_FWD_SLOTPF
+#define GSR_FWD_SLOTPF 1   // 0: plain slot reads (folded into one read at the use: measurement knob)
+#endif
+template <typename T>
+__device__ __forceinline__ int fwd_slot(T* p) {
+#if GSR_FWD_SLOTPF
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#else
+  return *p;
+#endif
+}
+#ifndef GSR_FWD_PF2
+#define GSR_FWD_PF2 0   // 1: 3D quad rounds gather records two rounds ahead (12 more VGPRs)
+#endif
 // NW: waves per workgroup (4; 8 for the heavy-tile variant, LPP 8).  part: 0 every busy tile,
 // 1 the tiles with lists shorter than stats->heavy_min_len, 2 the others (the heavy tiles: a
 // first-pass forward finds them at the head of the busy order, a lazy re-render anywhere in its list).
@@ -502,7 +519,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 6 : (IS2D || LPP != 4) ? 1 : GSR
     int32_t* __restrict__ out_last, int32_t* __restrict__ tile_end, float4* __restrict__ ckpt,
     const int32_t* __restrict__ chunk_base, int n_busy, int64_t CT,
     uint64_t* __restrict__ tile_cut, float cut2d, const FwdLazy lz, const gsr_bin_stats* __restrict__ stats,
-    const Sets2D sets, int part = 0) {
+    const Sets2D sets, int part = 0, uint4* __restrict__ boxm = nullptr) {
   static_assert(!IS2D || LPP == 4, "2D walks per wave with quads");
   static_assert(NW == 4 || (NW == 8 && !IS2D && LPP == 8), "8 waves: the 3D heavy-tile layout");
   using PG = PixGroup<LPP>;
@@ -590,6 +607,10 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 6 : (IS2D || LPP != 4) ? 1 : GSR
   __shared__ int s_qn[2][NW];
   __shared__ __attribute__((aligned(16))) int s_live[2][NW];
   __shared__ QIdx s_l[NW][128];
+  // box survivor masks for the backward (boxm): per wave, one flag byte per entry of the half
+  __shared__ __attribute__((aligned(4))) unsigned char s_fl[NW][128];
+  const bool wbm = boxm != nullptr && ckpt != nullptr && umask == kChunk3 - 1;
+  if (wbm && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(const_cast<int32_t*>(&stats->masks), kStatsBoxMasks);
   // 3D -- shared rounds: the quadrant workgroup walks the list in 256-entry rounds; wave w gathers
   // entries 64w..64w+63 of the round (one round ahead), culls them against the 8x8 quadrant
   // and writes its survivors to segment w of a double-buffered LDS queue; after ONE barrier
@@ -612,17 +633,45 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 6 : (IS2D || LPP != 4) ? 1 : GSR
   // vmcnt(0) right behind the two loads.)
   int idn = 0, kn = -1;
   bool ucur = false;
+#if GSR_FWD_PF2
+  // records TWO rounds ahead (d*: the next round's, in flight while this round is culled and
+  // composited), ids three ahead
+  float4 d0 = c0, d1 = c0, d2 = c0;
+  bool unext = false;
+  if (end > start) {
+    const int e0 = min(start + 64 * wv + lane, e_last), e1 = min(start + NT + 64 * wv + lane, e_last);
+    const int e2 = min(start + 2 * NT + 64 * wv + lane, e_last);
+    const int id0 = ids[e0], id1 = ids[e1];
+    idn = ids[e2];
+    ucur = kos == nullptr || ((kos[e0] >> qbit) & 1);
+    unext = kos == nullptr || ((kos[e1] >> qbit) & 1);
+    if (kos != nullptr) kn = kos[e2];
+    if (ucur) {
+      const Splat s0 = rec[id0];
+      c0 = s0.p0; c1 = s0.p1; c2 = s0.p2;
+    }
+    if (unext) {
+      const Splat s1 = rec[id1];
+      d0 = s1.p0; d1 = s1.p1; d2 = s1.p2;
+    }
+  }
+#else
+  // (without masks kn is read from ids, a word of the same line as idn, and never tested: a
+  // conditional load kept the old kn live beside the new one, and the loop's latch then copied
+  // the loaded registers -- a vmcnt(0) behind every round's record gather)
+  const int32_t* const kptr = kos != nullptr ? kos : ids;
   if (end > start) {
     const int e0 = min(start + 64 * wv + lane, e_last), e1 = min(start + NT + 64 * wv + lane, e_last);
     const int id0 = ids[e0];
     idn = ids[e1];
     ucur = kos == nullptr || ((kos[e0] >> qbit) & 1);
-    if (kos != nullptr) kn = kos[e1];
+    kn = kptr[e1];
     if (ucur) {
       const Splat s0 = rec[id0];
       c0 = s0.p0; c1 = s0.p1; c2 = s0.p2;
     }
   }
+#endif
   int buf = 0;
   for (int rb = start; rb < end; rb += NT, buf ^= 1) {
 #ifdef GSR_FWD_TRACE
@@ -642,14 +691,29 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 6 : (IS2D || LPP != 4) ? 1 : GSR
       }
       if (lane == 0) s_qn[buf][wv] = __popcll(m);
       const int id_use = idn;
-      ucur = ((kn >> qbit) & 1) != 0;
-      const int e2 = min(rb + 2 * NT + 64 * wv + lane, e_last);
-      idn = ids[e2];
-      if (kos != nullptr) kn = kos[e2];
+#if GSR_FWD_PF2
+      c0 = d0; c1 = d1; c2 = d2;
+      ucur = unext;
+      unext = ((kn >> qbit) & 1) != 0;
+      const int e3 = min(rb + 3 * NT + 64 * wv + lane, e_last);
+      idn = ids[e3];
+      if (kos != nullptr) kn = kos[e3];
+      if (unext) {
+        const Splat sn = rec[id_use];
+        d0 = sn.p0; d1 = sn.p1; d2 = sn.p2;
+      }
+#else
+      // the next round's records first, then the ids two rounds ahead into the registers the
+      // records' addresses have just freed (loaded in place: no copy at the loop's latch)
+      ucur = kos == nullptr || ((kn >> qbit) & 1) != 0;
       if (ucur) {
         const Splat sn = rec[id_use];
         c0 = sn.p0; c1 = sn.p1; c2 = sn.p2;
       }
+      const int e2 = min(rb + 2 * NT + 64 * wv + lane, e_last);
+      idn = ids[e2];
+      kn = kptr[e2];
+#endif
     }
     FWD_P(0);
     if (!sync_any<NW>(!done, s_live[buf])) break;
@@ -659,6 +723,8 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 6 : (IS2D || LPP != 4) ? 1 : GSR
 #endif
     for (int h = 0; h < NT / 128; ++h) {
       const int hb = rb + 128 * h;
+      // (a wave whose pixels are all done writes no more box masks: the backward reads a box's
+      // masks only up to the box's last composited entry)
       if (hb >= end || __ballot(!done) == 0ull) break;
       if (hb > start && ((hb - start) & umask) == 0) {   // entering chunk kcur+1
         const float Dr = PG::sum(dr), Dg = PG::sum(dg), Db = PG::sum(db);
@@ -672,17 +738,22 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 6 : (IS2D || LPP != 4) ? 1 : GSR
       }
       const int na = s_qn[buf][2 * h], nh = na + s_qn[buf][2 * h + 1];
       int n = 0, lastq = -1;
+      if (wbm && lane < 32) reinterpret_cast<uint32_t*>(s_fl[wv])[lane] = 0u;
+      __builtin_amdgcn_wave_barrier();
       for (int r0 = 0; r0 < nh; r0 += 64) {
         const int ii = r0 + lane;
         const int idx = ii < na ? 128 * h + ii : 128 * h + 64 + (ii - na);
         const bool keep = ii < nh && cull_keep<IS2D>(s_q[buf][0][idx], s_q[buf][1][idx], s_q[buf][2][idx], bx0, bx1, by0, by1);
         const unsigned long long m = __ballot(keep);
-        if (keep)
+        if (keep) {
           s_l[wv][n + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] =
               (QIdx)idx;
+          if (wbm) s_fl[wv][s_qe[buf][idx] - 128 * h] = 1;   // (entry - hb: this half's 128)
+        }
         n += __popcll(m);
       }
       __builtin_amdgcn_wave_barrier();
+
       FWD_P(2);
 #ifdef GSR_FWD_TRACE
       f_groups += (n + LPP - 1) / LPP;
@@ -690,11 +761,14 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 6 : (IS2D || LPP != 4) ? 1 : GSR
 #endif
       // the next group's queue slot is read one group ahead (one LDS round trip less on the
       // serial chain of a group)
-      int idx_next = s_l[wv][q < n ? q : max(n - 1, 0)];
+      // (relaxed atomic reads: instcombine folds a phi of two plain loads into ONE load at the
+      // use, which put the slot read back on the group's chain; atomic loads are not folded)
+      QIdx* const lq = s_l[wv];
+      int idx_next = fwd_slot(lq + (q < n ? q : max(n - 1, 0)));
       for (int k0 = 0; k0 < n; k0 += LPP) {
         const int k = k0 + q;
         const int idx = idx_next;
-        idx_next = s_l[wv][k + LPP < n ? k + LPP : n - 1];
+        idx_next = fwd_slot(lq + (k + LPP < n ? k + LPP : n - 1));
         const float4 p0 = s_q[buf][0][idx];
         const float4 p1 = s_q[buf][1][idx];
         const float4 p2 = s_q[buf][2][idx];
@@ -720,6 +794,14 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 6 : (IS2D || LPP != 4) ? 1 : GSR
         // the group minimum of non-negative transmittances, on their int32 bit patterns
         T = __int_as_float(PG::min_i(__float_as_int((IS2D ? q <= fs : q < fs) ? nT : T)));
         done = done || fs < LPP;
+      }
+      if (wbm) {
+        // the box's survivors of this 128-entry chunk as a 128-bit mask over its entries (read
+        // after the walk: off the walk's serial chain)
+        const unsigned long long blo = __ballot(s_fl[wv][lane] != 0), bhi = __ballot(s_fl[wv][64 + lane] != 0);
+        if (lane == 0)
+          boxm[(int64_t)(cbase + ((hb - start) >> 7)) * 16 + 4 * sub + wv] =
+              make_uint4((uint32_t)blo, (uint32_t)(blo >> 32), (uint32_t)bhi, (uint32_t)(bhi >> 32));
       }
       if (lastq >= 0) {   // the entry index of this lane's latest composite, once per half
         last = rb + s_qe[buf][lastq];
@@ -1718,7 +1800,8 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
     const float* __restrict__ bg, const float* __restrict__ final_T, const int32_t* __restrict__ last_in,
     const float* __restrict__ v_rgb, const float* __restrict__ v_alpha, float* __restrict__ partial,
     const int32_t* __restrict__ chunk_list, gsr_bin_stats* __restrict__ stats,
-    const int32_t* __restrict__ k_of_s, const gsr_loss_terms lt, int C, float cut2d) {
+    const int32_t* __restrict__ k_of_s, const gsr_loss_terms lt, int C, float cut2d,
+    const uint4* __restrict__ boxm = nullptr) {
   static_assert(!(LOSS && IS2D), "the fused loss is the 3D training loss");
   // slot kNull: a zero-opacity record (never valid) that pads survivor groups to 7
   constexpr int kNull = kChunk3;
@@ -1759,7 +1842,8 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
 #endif
   const int4 cd = reinterpret_cast<const int4*>(chunk_list)[blockIdx.x];
   const int n_act = stats->n_active, ovf = stats->overflow, ce = stats->chunk_entries;
-  const bool use_masks = !IS2D && (stats->masks & kStatsMasks3D) != 0;
+  const int smasks = stats->masks;
+  const bool use_masks = !IS2D && (smasks & kStatsMasks3D) != 0;
   const bool unit_bad = !MULTI && ce != kChunk3;
   if ((ovf != 0) | ((int)blockIdx.x >= n_act) | unit_bad | (cd.y <= 0)) {
     if (unit_bad && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1793,6 +1877,15 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
   // bounds this kernel's fixed part): the pixel's state, its chunk record, the last sub-chunk's
   // ids and sort positions; pixels that stopped before this unit then drop them by select.
   const float4 rck = ckpt[(int64_t)chunk * kRasterThreads + ckpt_slot_of(wv, box, pos)];
+  // the forward's survivor masks of this chunk's 4x4 boxes (the same two culls, done there):
+  // wave-uniform, scalar loads
+  const bool use_bm = !IS2D && !MULTI && boxm != nullptr && (smasks & kStatsBoxMasks) != 0;
+  uint4 bm[4] = {};
+  if (use_bm) {
+    const uint4* bmp = boxm + (int64_t)chunk * 16 + 4 * __builtin_amdgcn_readfirstlane(wv);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) bm[b] = bmp[b];
+  }
   int id_mine = threadIdx.x < sn ? ids[sb0 + threadIdx.x] : 0;
   int kos_mine = threadIdx.x < sn ? k_of_s[sb0 + threadIdx.x] : 0;
   // the records as three float4 registers (a Splat variable assigned under a branch and in the
@@ -1880,6 +1973,37 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
     // in a later sub-chunk or before this one)
     const int lastk = min(last - sb0, kChunk3 - 1);   // < 0: the pixel stopped before this sub-chunk
     const int lastq = last - sb0 < kChunk3 ? last - sb0 : -1;
+    int nbx[4];
+    if (use_bm) {
+      // each box's list from its mask, back to front, cut at the box's last composited entry
+      // (the forward writes a box's masks only while one of its pixels is live): the max of
+      // `last` over the box's 16 lanes -- quad xor 1, 2, row_mirror (xor 15), swizzle xor 24
+      int bl16 = last;
+      bl16 = max(bl16, dpp_row_i<0xB1>(bl16));   // quad_perm [1,0,3,2]
+      bl16 = max(bl16, dpp_row_i<0x4E>(bl16));   // quad_perm [2,3,0,1]
+      bl16 = max(bl16, dpp_row_i<0x140>(bl16));  // row_mirror
+      bl16 = max(bl16, __builtin_amdgcn_ds_swizzle(bl16, (0x18 << 10) | 0x1F));   // lane ^ 24 in 32
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        // box b's lanes: bit 5 = b >> 1, parity of bits 2..4 = b & 1 (b128_group); lane 32 (b >> 1) + 4 (b & 1)
+        const int lim = min(sn - 1, __builtin_amdgcn_readlane(bl16, 32 * (b >> 1) + 4 * (b & 1)) - sb0);
+        const unsigned long long mlo = lim < 0 ? 0ull : lim >= 63 ? ~0ull : (2ull << lim) - 1ull;
+        const unsigned long long mhi = lim < 64 ? 0ull : lim >= 127 ? ~0ull : (2ull << (lim - 64)) - 1ull;
+        const unsigned long long lo = (((unsigned long long)bm[b].y << 32) | bm[b].x) & mlo;
+        const unsigned long long hi = (((unsigned long long)bm[b].w << 32) | bm[b].z) & mhi;
+        const int nhi = __popcll(hi);
+        nbx[b] = nhi + __popcll(lo);
+        unsigned char* const bl = s_box[wv][b];
+        if ((hi >> lane) & 1ull) {
+          const int p = __popcll((hi >> lane) >> 1);
+          bl[PK ? grouped_slot(p) : p] = (unsigned char)(64 + lane);
+        }
+        if ((lo >> lane) & 1ull) {
+          const int p = nhi + __popcll((lo >> lane) >> 1);
+          bl[PK ? grouped_slot(p) : p] = (unsigned char)lane;
+        }
+      }
+    } else {
     // cull the sub-chunk against this wave's 8x8 quadrant; survivors are listed back to front
     int nsurv = 0;
     {
@@ -1909,9 +2033,9 @@ __global__ __launch_bounds__(kRasterThreads, MULTI ? GSR_BWD_MULTI_MINB : GSR_BW
     __builtin_amdgcn_wave_barrier();
     // ... and the quadrant's survivors against each 4x4 box (one survivor per lane, all four
     // boxes; box4_cull keeps the list order)
-    int nbx[4];
     box4_cull<IS2D, PK, PK>(s_list[wv], nsurv, s_p[0], s_p[1], s_p[2], (float)qx0 + off, (float)qy0 + off,
                             &s_box[wv][0][0], kLenB, nbx);
+    }
     const int nb = box == 0 ? nbx[0] : box == 1 ? nbx[1] : box == 2 ? nbx[2] : nbx[3];   // this lane's box
     // groups walked by the wave: max over its boxes
     const int ngrp = max(max(nbx[0], nbx[1]), max(nbx[2], nbx[3]));
@@ -3495,6 +3619,7 @@ static FwdSide* fwd_side() {
   return x.ok ? &x : nullptr;
 }
 
+static bool bwd3d_pair(int64_t tiles);
 // Shared by the 3D and 2D entry points (2D: C = 1, index-order keys, final_T [H,W,2]).
 template <bool IS2D>
 static int raster_fwd(const char* who, const float* rec, const float* depth, const int32_t* sorted_ids,
@@ -3503,7 +3628,7 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
                       float* rgb, float* alpha, float* final_T, int32_t* last, int32_t* tile_end,
                       uint64_t* tile_cut, float* chunk_state, int32_t* chunk_list,
                       void* stream, const FwdLazy& lz = FwdLazy{}, int lanes = 0, bool finalize = true,
-                      const Sets2D sets = Sets2D{0, nullptr, 1}) {
+                      const Sets2D sets = Sets2D{0, nullptr, 1}, uint32_t* box_masks = nullptr) {
   GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "%s: bad C=%d or image %dx%d", who, C, width, height);
   const int tw = ceil_div(width, kTile), th = ceil_div(height, kTile);
   const int64_t CT = (int64_t)C * tw * th;
@@ -3548,7 +3673,9 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
     hipLaunchKernelGGL((k_raster_fwd<IS2D, 4>), dim3((unsigned)(busy_grid<4>(n_busy) + n_fill)),
                        dim3(kRasterThreads), IS2D ? kFwdLdsPad2D : kFwdLdsPad, s, (const Splat*)rec, sorted_ids, kos,
                        tile_offset, tile_order, width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end,
-                       (float4*)chunk_state, chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz, stats, sets, part);
+                       (float4*)chunk_state, chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz, stats, sets, part,
+                       // (the masks serve k_raster_bwd; the pair layout culls on its own)
+                       part == 0 && GSR_BOXM && !bwd3d_pair(CT) ? reinterpret_cast<uint4*>(box_masks) : nullptr);
     if (part) {
       GSR_LAUNCH_CHECK(who);
       GSR_REQUIRE(hipEventRecord(side->join, side->s) == hipSuccess && hipStreamWaitEvent(s, side->join, 0) == hipSuccess,
@@ -3610,7 +3737,7 @@ static int raster_bwd(const char* who, const float* rec, const int32_t* sorted_i
                       int32_t chunk_entries, int C, int width, int height, float cut2d, const float* bg,
                       const float* final_T, const int32_t* last, const float* v_rgb, const float* v_alpha,
                       const gsr_loss_terms& lt, const int32_t* k_of_s, float* partial, void* stream,
-                      const Sets2D sets = Sets2D{0, nullptr, 1}) {
+                      const Sets2D sets = Sets2D{0, nullptr, 1}, const uint32_t* box_masks = nullptr) {
   GSR_REQUIRE(C >= 1 && width > 0 && height > 0, "%s: bad C=%d or image %dx%d", who, C, width, height);
   GSR_REQUIRE(n_chunks >= 0, "%s: bad n_chunks", who);
   GSR_REQUIRE(chunk_entries == 0 || (chunk_entries >= kChunk3 && (chunk_entries & (chunk_entries - 1)) == 0),
@@ -3665,7 +3792,7 @@ static int raster_bwd(const char* who, const float* rec, const int32_t* sorted_i
     hipLaunchKernelGGL((k_raster_bwd<LOSS, IS2D, false>), dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
                        (const Splat*)rec, sorted_ids, tile_offset, tile_end, chunk_base,
                        (const float4*)chunk_state, width, height, tw, th, bg, final_T, last, v_rgb, v_alpha, partial,
-                       chunk_list, stats, k_of_s, lt, C, cut2d);
+                       chunk_list, stats, k_of_s, lt, C, cut2d, reinterpret_cast<const uint4*>(box_masks));
   GSR_LAUNCH_CHECK(who);
   return GSR_OK;
 }
@@ -3679,10 +3806,10 @@ int gsr3d_raster_fwd(const float* rec, const float* depth, const int32_t* sorted
                      const int32_t* tile_order, const int32_t* chunk_base, int C, int width, int height,
                      const float* bg, int32_t n_busy, gsr_bin_stats* stats, float* rgb, float* alpha,
                      float* final_T, int32_t* last, int32_t* tile_end, uint64_t* tile_cut, float* chunk_state,
-                     int32_t* chunk_list, void* stream) {
+                     int32_t* chunk_list, uint32_t* box_masks, void* stream) {
   return raster_fwd<false>("gsr3d_raster_fwd", rec, depth, sorted_ids, k_of_s, tile_offset, tile_order, chunk_base, C, width,
                            height, 0.f, bg, n_busy, stats, rgb, alpha, final_T, last, tile_end, tile_cut,
-                           chunk_state, chunk_list, stream);
+                           chunk_state, chunk_list, stream, FwdLazy{}, 0, true, Sets2D{0, nullptr, 1}, box_masks);
 }
 
 int gsr3d_raster_fwd_lazy(const float* rec, const float* depth, int32_t* sorted_ids, const int32_t* tile_offset,
@@ -3690,7 +3817,8 @@ int gsr3d_raster_fwd_lazy(const float* rec, const float* depth, int32_t* sorted_
                           const float* bg, int32_t n_busy, gsr_bin_stats* stats, float* rgb, float* alpha,
                           float* final_T, int32_t* last, int32_t* tile_end, uint64_t* tile_cut, float* chunk_state,
                           int32_t* chunk_list, int32_t* lazy, int32_t n_lazy_max, int32_t max_seg,
-                          void* sort_workspace, size_t sort_workspace_bytes, int32_t* k_of_s, void* stream) {
+                          void* sort_workspace, size_t sort_workspace_bytes, int32_t* k_of_s, uint32_t* box_masks,
+                          void* stream) {
   GSR_REQUIRE(lazy != nullptr && sort_workspace != nullptr, "gsr3d_raster_fwd_lazy: missing workspace");
   GSR_REQUIRE(n_lazy_max >= 0 && n_lazy_max <= n_busy, "gsr3d_raster_fwd_lazy: bad n_lazy_max %d", n_lazy_max);
   const int64_t CT = (int64_t)C * ceil_div(width, kTile) * ceil_div(height, kTile);
@@ -3700,7 +3828,7 @@ int gsr3d_raster_fwd_lazy(const float* rec, const float* depth, int32_t* sorted_
   int rc = raster_fwd<false>("gsr3d_raster_fwd_lazy", rec, depth, sorted_ids, k_of_s,
                              tile_offset, tile_order, chunk_base, C,
                              width, height, 0.f, bg, n_busy, stats, rgb, alpha, final_T, last, tile_end, tile_cut,
-                             chunk_state, chunk_list, stream, l1, lanes, false);
+                             chunk_state, chunk_list, stream, l1, lanes, false, Sets2D{0, nullptr, 1}, box_masks);
   if (rc != GSR_OK) return rc;
   // the listed tiles sorted whole, then rendered again from scratch (same layout)
   rc = bin_sort_rest(tile_offset, CT, max_seg, n_lazy_max, sort_workspace, sort_workspace_bytes, lazy, tile_end,
@@ -3710,7 +3838,7 @@ int gsr3d_raster_fwd_lazy(const float* rec, const float* depth, int32_t* sorted_
   rc = raster_fwd<false>("gsr3d_raster_fwd_lazy", rec, depth, sorted_ids, k_of_s,
                          tile_offset, tile_order, chunk_base, C,
                          width, height, 0.f, bg, n_lazy_max, stats, rgb, alpha, final_T, last, tile_end, tile_cut,
-                         chunk_state, chunk_list, stream, l2, lanes, false);
+                         chunk_state, chunk_list, stream, l2, lanes, false, Sets2D{0, nullptr, 1}, box_masks);
   if (rc != GSR_OK) return rc;
   if (n_busy > 0 && chunk_list != nullptr) {
     hipLaunchKernelGGL(k_raster_finalize, dim3(ceil_div(n_busy, kRasterThreads)), dim3(kRasterThreads), 0,
@@ -3726,11 +3854,12 @@ int gsr3d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t*
                      const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats, int32_t n_chunks,
                      int32_t chunk_entries, int C, int width, int height, const float* bg, const float* final_T,
                      const int32_t* last, const float* v_rgb, const float* v_alpha, const int32_t* k_of_s,
-                     float* partial, void* stream) {
+                     float* partial, const uint32_t* box_masks, void* stream) {
   const gsr_loss_terms none{};
   return raster_bwd<false, false>("gsr3d_raster_bwd", rec, sorted_ids, tile_offset, tile_end, chunk_base,
                                   chunk_state, chunk_list, stats, n_chunks, chunk_entries, C, width, height, 0.f, bg,
-                                  final_T, last, v_rgb, v_alpha, none, k_of_s, partial, stream);
+                                  final_T, last, v_rgb, v_alpha, none, k_of_s, partial, stream, Sets2D{0, nullptr, 1},
+                                  box_masks);
 }
 
 int gsr3d_raster_bwd_loss(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,
@@ -3738,12 +3867,13 @@ int gsr3d_raster_bwd_loss(const float* rec, const int32_t* sorted_ids, const int
                           const float* chunk_state, const int32_t* chunk_list, gsr_bin_stats* stats,
                           int32_t n_chunks, int32_t chunk_entries, int C, int width, int height, const float* bg,
                           const float* final_T, const int32_t* last, const gsr_loss_terms* loss,
-                          const int32_t* k_of_s, float* partial, void* stream) {
+                          const int32_t* k_of_s, float* partial, const uint32_t* box_masks, void* stream) {
   GSR_REQUIRE(loss != nullptr && loss->rgb && loss->target_img && loss->target_mask && loss->sums && loss->grad_out,
               "gsr3d_raster_bwd_loss: incomplete loss terms");
   return raster_bwd<true, false>("gsr3d_raster_bwd_loss", rec, sorted_ids, tile_offset, tile_end, chunk_base,
                                  chunk_state, chunk_list, stats, n_chunks, chunk_entries, C, width, height, 0.f, bg,
-                                 final_T, last, nullptr, nullptr, *loss, k_of_s, partial, stream);
+                                 final_T, last, nullptr, nullptr, *loss, k_of_s, partial, stream, Sets2D{0, nullptr, 1},
+                                 box_masks);
 }
 
 int gsr2d_raster_fwd(const float* rec, const int32_t* sorted_ids, const int32_t* tile_offset,

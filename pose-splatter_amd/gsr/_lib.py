@@ -26,7 +26,7 @@ ORDER_INDEX = 1
 INPUT_ADAPTER = 0
 INPUT_GSPLAT = 1
 
-ABI_VERSION = 13   # include/gsr.h GSR_ABI_VERSION this binding is written for
+ABI_VERSION = 14   # include/gsr.h GSR_ABI_VERSION this binding is written for
 # gsr_set_bwd2d_parts at load (profiles/r05_ab5_bwd2d_parts_sweep.txt; GSR_BWD2D_PART_WGS overrides it
 # for measurements, tools/parts_sweep.sh)
 BWD2D_PART_WORKGROUPS = int(os.environ.get("GSR_BWD2D_PART_WGS", "4608"))
@@ -105,7 +105,7 @@ EXPORTS = {
     "gsr_bin_sort": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I32, _I64, _I32,
                                     _I32, _I32, _I32, _I32, _P, _P, _SZ, _P, _P, _P]),
     "gsr3d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _I32, _P, _P, _P,
-                                        _P, _P, _P, _P, _P, _P, _P]),
+                                        _P, _P, _P, _P, _P, _P, _P, _P]),
     "gsr_set_emit_staged": (ctypes.c_int, [_I32]),
     "gsr_set_split_sort": (ctypes.c_int, [_I32]),
     "gsr_lazy_workspace": (_SZ, [_I64]),
@@ -114,9 +114,9 @@ EXPORTS = {
     "gsr_bin_sort_lazy": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _I64, _I32, _I32,
                                          _I32, _I32, _I32, _P, _P, _SZ, _P, _P, _P, _P]),
     "gsr3d_raster_fwd_lazy": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _I32, _P, _P, _P,
-                                             _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _P, _SZ, _P, _P]),
+                                             _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _P, _SZ, _P, _P, _P]),
     "gsr3d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _P,
-                                        _P, _P, _P, _P, _P, _P, _P]),
+                                        _P, _P, _P, _P, _P, _P, _P, _P]),
     "gsr2d_raster_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _I32, _P, _P, _P, _P, _P,
                                         _P, _P, _P, _P, _I64, _P, _I32, _P]),
     "gsr2d_raster_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _F, _P, _P,
@@ -132,7 +132,7 @@ EXPORTS = {
     "gsr_loss_workspace": (_SZ, [_I32, _I32, _I32]),
     "gsr_loss_iou_l1_fwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _SZ, _P, _P, _P, _P]),
     "gsr3d_raster_bwd_loss": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _P,
-                                             _P, _P, ctypes.POINTER(LossTerms), _P, _P, _P]),
+                                             _P, _P, ctypes.POINTER(LossTerms), _P, _P, _P, _P]),
     "gsr_head_select_workspace": (_SZ, [_I64]),
     "gsr_head_select": (ctypes.c_int, [_P, _I64, _D, _F, _D, _I32, _I32, _I32, _P, _SZ, _P, _P, _P, _P]),
     "gsr_head3d_fwd": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _P, _F, _F, _F, _F, _F, _I32, _D, _P, _P, _P]),

@@ -152,7 +152,7 @@ class _RenderIouL1(torch.autograd.Function):
                                           q["chunk_base"], q["chunk_state"], q["chunk_list"],
                                           q["stats_dev"], b.n_chunks, b.chunk_entries, b.C, width, height, _ptr(bgc),
                                           q["final_T"], q["last"], ctypes.byref(terms), q["k_of_s"],
-                                          _ptr(partial), stream), "gsr3d_raster_bwd_loss")
+                                          _ptr(partial), q.get("box_masks"), stream), "gsr3d_raster_bwd_loss")
         v_params = backward3d(b, ctx.meta, raster)
         return (v_params.view(ctx.params_shape),) + (None,) * 9
 

@@ -463,6 +463,8 @@ class _Bins:
             self.key = (str(device), C, "N*", width, height, key_extra)
         # 2D: the chunk list holds one backward unit per slot of the tile sweep (include/gsr.h ABI 7)
         self.min_units = self.CT + 8 if key_extra and key_extra[0] == "2d" else 0
+        # 3D: the forward's box survivor masks for the backward (include/gsr.h ABI 14), 256 B per chunk
+        self.box_masks = bool(key_extra and key_extra[0] == "3d")
         self.need_bwd = need_bwd   # False: no chunk records, no finalize (tile_end left raw)
         if mode not in _MODES:
             raise ValueError(f"capacity mode must be one of {_MODES}, got {mode!r}")
@@ -628,7 +630,10 @@ class _Bins:
 
     def alloc_chunks(self, n_chunks: int):
         K = max(n_chunks, 1)
-        self.chunks = _Arena(self.device, {"chunk_state": K * 256 * 16, "chunk_list": max(K, self.min_units) * 16})
+        spec = {"chunk_state": K * 256 * 16, "chunk_list": max(K, self.min_units) * 16}
+        if self.box_masks:
+            spec["box_masks"] = K * 256
+        self.chunks = _Arena(self.device, spec)
         self.chunk_cap = K
         self.p.update(self.chunks.ptr)
 
@@ -778,6 +783,7 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts, need_bwd=True, ret
     b.offsets_wait()
     b.ensure_post(with_chunks=need_bwd)
     cs, cl = (q["chunk_state"], q["chunk_list"]) if need_bwd else (None, None)
+    bm = q.get("box_masks") if need_bwd else None
     n_lazy = b.n_lazy = b.lazy_bound()
     if n_lazy:
         b.sort_lazy(stream)
@@ -792,13 +798,13 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts, need_bwd=True, ret
                                       q["chunk_base"], C, width, height, _ptr(bgc), b.n_busy, q["stats_dev"],
                                       _ptr(rgb), _ptr(alpha), q["final_T"], q["last"], q["tile_end"], q["tile_cut"],
                                       cs, cl, q["lazy"], n_lazy, b.max_seg,
-                                      q["sort_ws"], b.post.off["sort_ws"][1], q["k_of_s"], stream),
+                                      q["sort_ws"], b.post.off["sort_ws"][1], q["k_of_s"], bm, stream),
               "gsr3d_raster_fwd_lazy")
       else:
         check(L.gsr3d_raster_fwd(q["rec"], q["depth"], q["sorted_ids"], q["k_of_s"], q["tile_off"],
                                  q["busy"], q["chunk_base"],
                                  C, width, height, _ptr(bgc), b.n_busy, q["stats_dev"], _ptr(rgb), _ptr(alpha),
-                                 q["final_T"], q["last"], q["tile_end"], q["tile_cut"], cs, cl, stream),
+                                 q["final_T"], q["last"], q["tile_end"], q["tile_cut"], cs, cl, bm, stream),
               "gsr3d_raster_fwd")
     if n_lazy:
         b.verify_launch()   # (the lazy forward's re-sort can still flag GSR_OVF_LAZY)
@@ -918,7 +924,8 @@ class _Render3D(torch.autograd.Function):
             check(L.gsr3d_raster_bwd(q["rec"], q["sorted_ids"], q["tile_off"], q["tile_end"], q["chunk_base"],
                                      q["chunk_state"], q["chunk_list"], q["stats_dev"],
                                      b.n_chunks, b.chunk_entries, C, width, height, _ptr(bgc), q["final_T"], q["last"],
-                                     _ptr(v_rgb), _ptr(v_alpha), q["k_of_s"], _ptr(partial), stream),
+                                     _ptr(v_rgb), _ptr(v_alpha), q["k_of_s"], _ptr(partial), q.get("box_masks"),
+                                     stream),
                   "gsr3d_raster_bwd")
         v_params = backward3d(b, ctx.meta, raster)
         _backward_check(b)   # a bounded forward that overflowed raises here, before .grad

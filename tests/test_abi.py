@@ -170,5 +170,5 @@ def test_loss_entry_points_validate():
     assert lib.gsr_loss_workspace(6, 576, 512) >= 6 * 16
     rc = lib.gsr_loss_iou_l1_fwd(None, None, None, None, 0, 64, 64, 1.0, None, 0, None, None, None, None)
     assert rc == -1 and b"bad C" in lib.gsr_last_error()
-    rc = lib.gsr3d_raster_bwd_loss(*([None] * 8), 1, 0, 1, 64, 64, None, None, None, None, None, None, None)
+    rc = lib.gsr3d_raster_bwd_loss(*([None] * 8), 1, 0, 1, 64, 64, None, None, None, None, None, None, None, None)
     assert rc == -1 and b"loss terms" in lib.gsr_last_error()

@@ -103,7 +103,7 @@ def test_unit_mismatch_is_flagged(cuda):
         _lib.check(L.gsr3d_raster_bwd(q["rec"], q["sorted_ids"], q["tile_off"], q["tile_end"], q["chunk_base"],
                                       q["chunk_state"], q["chunk_list"], q["stats_dev"], b.n_chunks, 128, b.C, W, H,
                                       bgc.data_ptr(), q["final_T"], q["last"], vr.data_ptr(), va.data_ptr(),
-                                      q["k_of_s"], partial.data_ptr(), stream), "gsr3d_raster_bwd")
+                                      q["k_of_s"], partial.data_ptr(), None, stream), "gsr3d_raster_bwd")
     v = R.backward3d(b, meta, raster)
     torch.cuda.synchronize()
     assert torch.isnan(v).all()
