@@ -422,7 +422,7 @@ __device__ __forceinline__ constexpr float conic_unscale() {
 }
 
 #ifndef GSR_CULL_BRANCHFREE
-#define GSR_CULL_BRANCHFREE 0
+#define GSR_CULL_BRANCHFREE 1
 #endif
 template <bool IS2D>
 __device__ __forceinline__ bool cull_keep(const float4 p0, const float4 p1, const float4 p2, float bx0, float bx1,

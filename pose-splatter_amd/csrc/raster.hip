@@ -608,8 +608,9 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 6 : (IS2D || LPP != 4) ? 1 : GSR
   __shared__ __attribute__((aligned(16))) int s_live[2][NW];
   __shared__ QIdx s_l[NW][128];
   // box survivor masks for the backward (boxm): per wave, one flag byte per entry of the half
-  __shared__ __attribute__((aligned(4))) unsigned char s_fl[NW][128];
-  const bool wbm = boxm != nullptr && ckpt != nullptr && umask == kChunk3 - 1;
+  constexpr bool kBoxMasks = LPP == 4 && NW == 4;   // the quad layout's waves are the 4x4 boxes
+  __shared__ __attribute__((aligned(4))) unsigned char s_fl[kBoxMasks ? NW : 1][128];
+  const bool wbm = kBoxMasks && boxm != nullptr && ckpt != nullptr && umask == kChunk3 - 1;
   if (wbm && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(const_cast<int32_t*>(&stats->masks), kStatsBoxMasks);
   // 3D -- shared rounds: the quadrant workgroup walks the list in 256-entry rounds; wave w gathers
   // entries 64w..64w+63 of the round (one round ahead), culls them against the 8x8 quadrant
@@ -633,90 +634,75 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 6 : (IS2D || LPP != 4) ? 1 : GSR
   // vmcnt(0) right behind the two loads.)
   int idn = 0, kn = -1;
   bool ucur = false;
-#if GSR_FWD_PF2
-  // records TWO rounds ahead (d*: the next round's, in flight while this round is culled and
-  // composited), ids three ahead
-  float4 d0 = c0, d1 = c0, d2 = c0;
-  bool unext = false;
-  if (end > start) {
-    const int e0 = min(start + 64 * wv + lane, e_last), e1 = min(start + NT + 64 * wv + lane, e_last);
-    const int e2 = min(start + 2 * NT + 64 * wv + lane, e_last);
-    const int id0 = ids[e0], id1 = ids[e1];
-    idn = ids[e2];
-    ucur = kos == nullptr || ((kos[e0] >> qbit) & 1);
-    unext = kos == nullptr || ((kos[e1] >> qbit) & 1);
-    if (kos != nullptr) kn = kos[e2];
-    if (ucur) {
-      const Splat s0 = rec[id0];
-      c0 = s0.p0; c1 = s0.p1; c2 = s0.p2;
-    }
-    if (unext) {
-      const Splat s1 = rec[id1];
-      d0 = s1.p0; d1 = s1.p1; d2 = s1.p2;
-    }
-  }
-#else
   // (without masks kn is read from ids, a word of the same line as idn, and never tested: a
   // conditional load kept the old kn live beside the new one, and the loop's latch then copied
   // the loaded registers -- a vmcnt(0) behind every round's record gather)
   const int32_t* const kptr = kos != nullptr ? kos : ids;
+  // rounds of records in flight: 1, or (GSR_FWD_PF2) 2 in two register sets that the rounds use
+  // in turn (no copies: a copy of a set waits for its load)
+  constexpr int kAhead = GSR_FWD_PF2 ? 2 : 1;
+#if GSR_FWD_PF2
+  float4 d0 = c0, d1 = c0, d2 = c0;
+  bool unext = false;
+#endif
   if (end > start) {
     const int e0 = min(start + 64 * wv + lane, e_last), e1 = min(start + NT + 64 * wv + lane, e_last);
     const int id0 = ids[e0];
-    idn = ids[e1];
     ucur = kos == nullptr || ((kos[e0] >> qbit) & 1);
+#if GSR_FWD_PF2
+    const int e2 = min(start + 2 * NT + 64 * wv + lane, e_last);
+    const int id1 = ids[e1];
+    unext = kos == nullptr || ((kos[e1] >> qbit) & 1);
+    idn = ids[e2];
+    kn = kptr[e2];
+#else
+    idn = ids[e1];
     kn = kptr[e1];
+#endif
     if (ucur) {
       const Splat s0 = rec[id0];
       c0 = s0.p0; c1 = s0.p1; c2 = s0.p2;
     }
-  }
+#if GSR_FWD_PF2
+    if (unext) {
+      const Splat s1 = rec[id1];
+      d0 = s1.p0; d1 = s1.p1; d2 = s1.p2;
+    }
 #endif
-  int buf = 0;
-  for (int rb = start; rb < end; rb += NT, buf ^= 1) {
+  }
+  // one round: cull the set x (this round's records) into the queue, gather into x the records
+  // kAhead rounds on and the ids one round further, then the round's walk.  false: every pixel
+  // of the workgroup is done.
+  auto round = [&](int rb, int buf, float4& x0, float4& x1, float4& x2, bool& ux) -> bool {
 #ifdef GSR_FWD_TRACE
     if (threadIdx.x == 0) f_t = wall_clock64();
 #endif
     {
       const int e = rb + 64 * wv + lane;
-      const bool keep = e < end && ucur && cull_keep<IS2D>(c0, c1, c2, qx0, qx1, qy0, qy1);
+      const bool keep = e < end && ux && cull_keep<IS2D>(x0, x1, x2, qx0, qx1, qy0, qy1);
       const unsigned long long m = __ballot(keep);
       if (keep) {
         const int slot = 64 * wv +
                          __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-        s_q[buf][0][slot] = c0;
-        s_q[buf][1][slot] = c1;
-        s_q[buf][2][slot] = c2;
+        s_q[buf][0][slot] = x0;
+        s_q[buf][1][slot] = x1;
+        s_q[buf][2][slot] = x2;
         s_qe[buf][slot] = (QIdx)(64 * wv + lane);   // e - rb
       }
       if (lane == 0) s_qn[buf][wv] = __popcll(m);
-      const int id_use = idn;
-#if GSR_FWD_PF2
-      c0 = d0; c1 = d1; c2 = d2;
-      ucur = unext;
-      unext = ((kn >> qbit) & 1) != 0;
-      const int e3 = min(rb + 3 * NT + 64 * wv + lane, e_last);
-      idn = ids[e3];
-      if (kos != nullptr) kn = kos[e3];
-      if (unext) {
-        const Splat sn = rec[id_use];
-        d0 = sn.p0; d1 = sn.p1; d2 = sn.p2;
-      }
-#else
-      // the next round's records first, then the ids two rounds ahead into the registers the
+      // the records kAhead rounds on first, then the ids one round further into the registers the
       // records' addresses have just freed (loaded in place: no copy at the loop's latch)
-      ucur = kos == nullptr || ((kn >> qbit) & 1) != 0;
-      if (ucur) {
-        const Splat sn = rec[id_use];
-        c0 = sn.p0; c1 = sn.p1; c2 = sn.p2;
+      ux = kos == nullptr || ((kn >> qbit) & 1) != 0;
+      if (ux) {
+        const Splat sn = rec[idn];
+        x0 = sn.p0; x1 = sn.p1; x2 = sn.p2;
       }
-      const int e2 = min(rb + 2 * NT + 64 * wv + lane, e_last);
-      idn = ids[e2];
-      kn = kptr[e2];
-#endif
+      const int en = min(rb + (kAhead + 1) * NT + 64 * wv + lane, e_last);
+      idn = ids[en];
+      kn = kptr[en];
     }
     FWD_P(0);
-    if (!sync_any<NW>(!done, s_live[buf])) break;
+    if (!sync_any<NW>(!done, s_live[buf])) return false;
     FWD_P(1);
 #ifdef GSR_FWD_TRACE
     if (n_rounds++ == 0) FWD_T(1);
@@ -810,7 +796,17 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 6 : (IS2D || LPP != 4) ? 1 : GSR
       __builtin_amdgcn_wave_barrier();
       FWD_P(3);
     }
+    return true;
+  };
+#if GSR_FWD_PF2
+  for (int rb = start; rb < end; rb += 2 * NT) {
+    if (!round(rb, 0, c0, c1, c2, ucur)) break;
+    if (rb + NT >= end || !round(rb + NT, 1, d0, d1, d2, unext)) break;
   }
+#else
+  for (int rb = start, buf = 0; rb < end; rb += NT, buf ^= 1)
+    if (!round(rb, buf, c0, c1, c2, ucur)) break;
+#endif
   } else {
   // 2D (every tile busy and long; the per-wave walk measured faster there): each wave walks
   // the list on its own in 64-entry batches.
@@ -1606,18 +1602,20 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_finalize(
     const int32_t* __restrict__ order, int n_busy, const int32_t* __restrict__ chunk_base,
     int32_t* __restrict__ tile_end, uint64_t* __restrict__ tile_cut, gsr_bin_stats* __restrict__ stats,
     int32_t* __restrict__ chunk_list, int key_order, int tile_units, int64_t CT, int T, const Sets2D sets) {
-  const int ovf = stats->overflow;
+  // the stats words and this thread's tile load together (the tile slot is clamped into the
+  // grid's bound; used only when real): one round trip, then the tile's words, then the atomic
+  const int ovf = stats->overflow, nb_dev = stats->n_busy;
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ct_busy = tile_units ? 0 : order[min(b, max(n_busy - 1, 0))];
   if (ovf) {   // bounded call over its bounds: report to the caller's sticky status, nothing else
     if (blockIdx.x == 0 && threadIdx.x == 0 && stats->status != nullptr) atomicOr(stats->status, ovf);
     return;
   }
-  (void)n_busy;   // the grid's bound; the tiles are the device count's
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
   // tile_units (2D): slot b of the XCD-aware sweep (every tile, busy or empty), one unit each
   const int sct = tile_units && b < sweep_grid2d(CT) ? sweep_tile2d(b, CT, T, sets.begin, sets.F) : -1;
-  const bool in = tile_units ? sct >= 0 : b < stats->n_busy;
-  const int ct = tile_units ? max(sct, 0) : in ? order[b] : 0;
+  const bool in = tile_units ? sct >= 0 : b < nb_dev;
+  const int ct = tile_units ? max(sct, 0) : in ? ct_busy : 0;
   int start = 0, end = 0, te = 0;
   if (in) {
     start = tile_offset[ct];
@@ -1625,7 +1623,6 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_finalize(
     const int m = tile_end[ct];
     te = m >= 0 ? m + 1 : start;
     tile_end[ct] = te;
-    tile_cut[ct] = te < end ? sort_key(depth, ids[te], key_order) : ~0ull;
   }
   if (tile_units) {
     // the unit of sweep slot b: the tile's whole consumed list [start, te) (empty: a unit of 0
@@ -1633,6 +1630,7 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_finalize(
     if (b == 0) stats->n_active = sweep_grid2d(CT);
     if (b < sweep_grid2d(CT))
       reinterpret_cast<int4*>(chunk_list)[b] = in ? make_int4(start, te - start, chunk_base[ct], ct) : make_int4(0, 0, 0, 0);
+    if (in) tile_cut[ct] = te < end ? sort_key(depth, ids[te], key_order) : ~0ull;
     return;
   }
   const int U = stats->chunk_entries;
@@ -1652,6 +1650,8 @@ __global__ __launch_bounds__(kRasterThreads) void k_raster_finalize(
       desc[pos + k] = make_int4(b0, min(U, te - b0), cbase + k, ct);
     }
   }
+  // the cut key (two more dependent loads) after the chunk list: off its chain
+  if (in) tile_cut[ct] = te < end ? sort_key(depth, ids[te], key_order) : ~0ull;
 }
 
 // Partial rows are stored in EMISSION order (row k_of_s[s] for sorted entry s), 9 floats
