@@ -2,7 +2,7 @@
 §8(d)): the same scene is fitted for 200 Adam steps once through the HIP path and once through
 the oracle (the CPU restatement of the reference semantics), from the same start toward the
 same target image, and the final PSNRs (get_psnr, scripts/utils/evaluate_model.py:240-243)
-must agree within 0.05 dB.
+must agree within 0.03 dB (the north star's bar is 0.05 dB; VERDICT r5 asked for 0.03).
 
 The oracle costs ~0.3 s per fwd+bwd even on a small image (it walks every tile list position
 by position), so the fitted scene is a small one: 300 Gaussians of the config-1 distribution
@@ -53,8 +53,8 @@ SEEDS = (5, 6, 7)
 @pytest.mark.timeout(1200)
 def test_adam_fit_200_steps_dpsnr(cuda):
     """Three starts (perturbation seeds) of the same fit (one seed's dPSNR was decided
-    by how the compiler fused one rounding): each final PSNR within 0.05 dB of the oracle's (the
-    north-star bar), the largest printed -- 0.022 dB on the round-6 tree, 0.029 dB with the
+    by how the compiler fused one rounding): each final PSNR within 0.03 dB of the oracle's (the
+    north-star bar is 0.05), the largest printed -- 0.022 dB on the round-6 tree, 0.029 dB with the
     projection backward built without fp contraction (GSR_PBWD_CONTRACT=0), so contraction is not
     what decides it (profiles/r06_fit_contract.txt)."""
     from gsr import render as R
@@ -84,5 +84,5 @@ def test_adam_fit_200_steps_dpsnr(cuda):
               f"max |param difference| {float((p_g - p_o).abs().max()):.3e}", flush=True)
         assert rec_g[0] == pytest.approx(rec_o[0], abs=1e-3)
         assert rec_g[STEPS] > rec_g[0] + 3.0, "the fit did not converge"   # a real optimisation, not a no-op
-        assert d <= 0.05, (seed, rec_g, rec_o)
-    print(f"[fit] max dPSNR over seeds {SEEDS}: {worst:.4f} dB (bar 0.05)")
+        assert d <= 0.03, (seed, rec_g, rec_o)
+    print(f"[fit] max dPSNR over seeds {SEEDS}: {worst:.4f} dB (bar 0.03)")
