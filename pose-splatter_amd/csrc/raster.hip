@@ -3177,7 +3177,7 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
     int tw, int th, const float* __restrict__ bg, const float* __restrict__ final_T,
     const int32_t* __restrict__ last_in, const float* __restrict__ v_rgb, const float* __restrict__ v_alpha,
     float* __restrict__ partial, const int32_t* __restrict__ chunk_list, gsr_bin_stats* __restrict__ stats,
-    const int32_t* __restrict__ k_of_s) {
+    const int32_t* __restrict__ k_of_s, const uint4* __restrict__ boxm = nullptr) {
   constexpr int kNull = kChunk3;
   constexpr int kGroup = GSR_BWD_GROUP;
   static_assert(kGroup == 7 && kPartial == 9, "reduce_box8 sums 7 entries x 9 values in 64 registers");
@@ -3192,7 +3192,8 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
   __shared__ __attribute__((aligned(16))) float s_stage[2][8][GSR_BWD3P_HALFSTAGE ? 32 : 64];
   const int4 cd = reinterpret_cast<const int4*>(chunk_list)[blockIdx.x];
   const int n_act = stats->n_active, ovf = stats->overflow, ce = stats->chunk_entries;
-  const bool use_masks = (stats->masks & kStatsMasks3D) != 0;   // k_of_s bits 28..31 hold quadrant masks
+  const int smasks = stats->masks;
+  const bool use_masks = (smasks & kStatsMasks3D) != 0;   // k_of_s bits 28..31 hold quadrant masks
   const bool unit_bad = ce != kChunk3;
   if ((ovf != 0) | ((int)blockIdx.x >= n_act) | unit_bad | (cd.y <= 0)) {
     if (unit_bad && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -3215,6 +3216,15 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
   // every load up front (see k_raster_bwd): the two pixels' chunk records and state, ids, records
   const float4 rckA = ckpt[(int64_t)chunk * kRasterThreads + bwd_pixel_slot(ilA, jl)];
   const float4 rckB = ckpt[(int64_t)chunk * kRasterThreads + bwd_pixel_slot(ilB, jl)];
+  // the forward's box survivor masks (as k_raster_bwd): this wave's 8 boxes are tile boxes
+  // (bx, by) = (b & 3, 2 wv + (b >> 2)), mask slots 4 quadrant + box in quadrant = 8 wv + ..
+  const bool use_bm = boxm != nullptr && (smasks & kStatsBoxMasks) != 0;
+  uint4 bm[8] = {};
+  if (use_bm) {
+    const uint4* bmp = boxm + (int64_t)chunk * 16 + 8 * __builtin_amdgcn_readfirstlane(wv);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) bm[b] = bmp[4 * ((b & 3) >> 1) + 2 * (b >> 2) + (b & 1)];
+  }
   const int id_mine = (int)threadIdx.x < sn ? ids[b0 + threadIdx.x] : 0;
   const int kos_mine = (int)threadIdx.x < sn ? k_of_s[b0 + threadIdx.x] : 0;
   float TfA = 1.f, vrA = 0.f, vgA = 0.f, vbA = 0.f, vaA = 0.f;
@@ -3277,6 +3287,29 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
 #endif
   const unsigned char* my_list = s_box[wv][box];
   __syncthreads();
+  int nbx[8];
+  if (use_bm) {
+    // each box's list from its mask, back to front, cut at the box's last composited entry: the
+    // max over its 8 lanes (quad xor 1, row_mirror = xor 15, swizzle xor 24 keep grp8_box)
+    int bl8 = max(lastA, lastB);
+    bl8 = max(bl8, dpp_row_i<0xB1>(bl8));   // quad_perm [1,0,3,2]
+    bl8 = max(bl8, dpp_row_i<0x140>(bl8));  // row_mirror
+    bl8 = max(bl8, __builtin_amdgcn_ds_swizzle(bl8, (0x18 << 10) | 0x1F));   // lane ^ 24 in 32
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      // box b's lanes: bit 5 = b >> 2, parity(bits 2,3,4) = (b >> 1) & 1, parity(bits 1,3,4) = b & 1
+      const int lim = min(sn - 1, __builtin_amdgcn_readlane(bl8, 32 * (b >> 2) + 4 * ((b >> 1) & 1) + 2 * (b & 1)) - b0);
+      const unsigned long long mlo = lim < 0 ? 0ull : lim >= 63 ? ~0ull : (2ull << lim) - 1ull;
+      const unsigned long long mhi = lim < 64 ? 0ull : lim >= 127 ? ~0ull : (2ull << (lim - 64)) - 1ull;
+      const unsigned long long lo = (((unsigned long long)bm[b].y << 32) | bm[b].x) & mlo;
+      const unsigned long long hi = (((unsigned long long)bm[b].w << 32) | bm[b].z) & mhi;
+      const int nhi = __popcll(hi);
+      nbx[b] = nhi + __popcll(lo);
+      unsigned char* const bl = s_box[wv][b];
+      if ((hi >> lane) & 1ull) bl[grouped_slot(__popcll((hi >> lane) >> 1))] = (unsigned char)(64 + lane);
+      if ((lo >> lane) & 1ull) bl[grouped_slot(nhi + __popcll((lo >> lane) >> 1))] = (unsigned char)lane;
+    }
+  } else {
   // cull the chunk against the wave's 16x8 half-tile (exact test), survivors back to front
   int nsurv = 0;
   {
@@ -3295,7 +3328,6 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
     }
   }
   __builtin_amdgcn_wave_barrier();
-  int nbx[8];
 #pragma unroll
   for (int b = 0; b < 8; ++b) nbx[b] = 0;
   {
@@ -3314,6 +3346,7 @@ __global__ __launch_bounds__(128, GSR_BWD3P_MINB) void k_raster_bwd_pair3d(
         nbx[b] += __popcll(m);
       }
     }
+  }
   }
   int nb = nbx[0], ngrp = nbx[0];
 #pragma unroll
@@ -3619,7 +3652,6 @@ static FwdSide* fwd_side() {
   return x.ok ? &x : nullptr;
 }
 
-static bool bwd3d_pair(int64_t tiles);
 // Shared by the 3D and 2D entry points (2D: C = 1, index-order keys, final_T [H,W,2]).
 template <bool IS2D>
 static int raster_fwd(const char* who, const float* rec, const float* depth, const int32_t* sorted_ids,
@@ -3674,8 +3706,7 @@ static int raster_fwd(const char* who, const float* rec, const float* depth, con
                        dim3(kRasterThreads), IS2D ? kFwdLdsPad2D : kFwdLdsPad, s, (const Splat*)rec, sorted_ids, kos,
                        tile_offset, tile_order, width, height, tw, th, bg, rgb, alpha, final_T, last, tile_end,
                        (float4*)chunk_state, chunk_base, (int)n_busy, CT, tile_cut, cut2d, lz, stats, sets, part,
-                       // (the masks serve k_raster_bwd; the pair layout culls on its own)
-                       part == 0 && GSR_BOXM && !bwd3d_pair(CT) ? reinterpret_cast<uint4*>(box_masks) : nullptr);
+                       part == 0 && GSR_BOXM ? reinterpret_cast<uint4*>(box_masks) : nullptr);
     if (part) {
       GSR_LAUNCH_CHECK(who);
       GSR_REQUIRE(hipEventRecord(side->join, side->s) == hipSuccess && hipStreamWaitEvent(s, side->join, 0) == hipSuccess,
@@ -3782,7 +3813,7 @@ static int raster_bwd(const char* who, const float* rec, const int32_t* sorted_i
   } else if (!LOSS && chunk_entries <= kChunk3 && bwd3d_pair((int64_t)C * tw * th)) {
     hipLaunchKernelGGL(k_raster_bwd_pair3d, dim3(n_chunks), dim3(128), 0, (hipStream_t)stream, (const Splat*)rec,
                        sorted_ids, (const float4*)chunk_state, width, height, tw, th, bg, final_T, last, v_rgb,
-                       v_alpha, partial, chunk_list, stats, k_of_s);
+                       v_alpha, partial, chunk_list, stats, k_of_s, reinterpret_cast<const uint4*>(box_masks));
   } else if (chunk_entries > kChunk3)
     hipLaunchKernelGGL((k_raster_bwd<LOSS, IS2D, true>), dim3(n_chunks), dim3(kRasterThreads), 0, (hipStream_t)stream,
                        (const Splat*)rec, sorted_ids, tile_offset, tile_end, chunk_base,

@@ -52,12 +52,13 @@ def _bwd(b, meta, vr, va, W, H, masks):
     return v.cpu()
 
 
+@pytest.mark.parametrize("layout", [1, 2], ids=["k_raster_bwd", "k_raster_bwd_pair3d"])
 @pytest.mark.parametrize("scene", ["units", "clusters"])
-def test_box_masks_match_culls(cuda, scene):
+def test_box_masks_match_culls(cuda, scene, layout):
     from gsr import render as R
     p, V, K, W, H = _scene_units(cuda) if scene == "units" else _scene_clusters(cuda)
-    # the quad forward (the masks' writer) and the 4-wave backward (their reader) at any shape
-    with forced_bwd_layout(1), forced_fwd_lanes(4):
+    # the quad forward (the masks' writer) and a chunk backward (their reader) at any shape
+    with forced_bwd_layout(layout), forced_fwd_lanes(4):
         rgb, alpha, b, meta = R.debug_forward3d(p, V, K, torch.ones(3, device=cuda), W, H)
         st = b.pre.view("stats_dev", torch.int32).tolist()
         assert st[_masks_word()] & 4, "the forward wrote no box masks"
@@ -72,21 +73,23 @@ def test_box_masks_match_culls(cuda, scene):
     # up to the association of a box's lane reduction when its list starts earlier (an entry's
     # slot in its group of 7)
     ndiff = int((listed != culled).sum())
-    print(f"[box masks, {scene}] {ndiff} of {listed.numel()} gradient values differ from the culling backward")
+    print(f"[box masks, {scene}, layout {layout}] {ndiff} of {listed.numel()} gradient values differ from the culling backward")
     assert_close(listed, culled, rtol=1e-5, atol=1e-8 * float(culled.abs().max()), what="box-mask grads")
 
 
-def test_pair_layout_forward_writes_no_masks(cuda):
-    """With the pixel-pair backward chosen for the shape, the forward skips the masks (that
-    kernel culls on its own) and the stats bit stays clear; the default render is unchanged."""
+def test_masks_need_quad_forward(cuda):
+    """The 16-lane forward (small calls) writes no masks: the stats bit stays clear, and the
+    backward culls; rgb / alpha of the quad forward do not depend on whether it writes them."""
     from gsr import render as R
     p, V, K, W, H = _scene_units(cuda)
-    with forced_bwd_layout(2), forced_fwd_lanes(4):
-        rgb2, alpha2, b, meta = R.debug_forward3d(p, V, K, torch.ones(3, device=cuda), W, H)
-        st = b.pre.view("stats_dev", torch.int32).tolist()
-        assert not st[_masks_word()] & 4
-    with forced_bwd_layout(1), forced_fwd_lanes(4):
+    with forced_fwd_lanes(16):
+        _, _, b, _ = R.debug_forward3d(p, V, K, torch.ones(3, device=cuda), W, H)
+        assert not b.pre.view("stats_dev", torch.int32).tolist()[_masks_word()] & 4
+    with forced_fwd_lanes(4):
         rgb1, alpha1, b, _ = R.debug_forward3d(p, V, K, torch.ones(3, device=cuda), W, H)
         assert b.pre.view("stats_dev", torch.int32).tolist()[_masks_word()] & 4
+        opts = R.RenderOptions3D()
+        rgb2, alpha2, b2, _ = R._forward3d(p, V, K, torch.ones(3, device=cuda), W, H, opts, need_bwd=False)
+        assert not b2.pre.view("stats_dev", torch.int32).tolist()[_masks_word()] & 4
     assert torch.equal(alpha1.cpu(), alpha2.cpu())
     assert_close(rgb1.cpu(), rgb2.cpu(), rtol=0, atol=0, what="rgb")

@@ -15,8 +15,9 @@ that differ box to box.  Each is compared with the oracle with NO outlier fracti
 forward may leave the tolerance only at a discrete-decision tie the oracle flags,
 oracle3d.tie_flags, and the cotangent is zero there, so every gradient element must match; 2D has
 no such decisions), for every backward kernel that uses lw_add:
-  * 3D k_raster_bwd (one pixel per lane, 128-entry units) with and without the forward's box
-    masks, its multi-sub-chunk form (256-entry units) and k_raster_bwd_pair3d (two pixels per lane);
+  * 3D k_raster_bwd (one pixel per lane, 128-entry units) and k_raster_bwd_pair3d (two pixels
+    per lane), each with and without the forward's box masks, and the multi-sub-chunk form
+    (256-entry units);
   * 2D k_raster2d_bwd_pair (one parameter set) and k_raster2d_bwd_frame (sets of several cameras;
     whole-list walks and the split walks of gsr_set_bwd2d_parts).
 The fixture also counts, from the oracle's lists, how many (chunk, quadrant) groups hold an entry
@@ -122,8 +123,9 @@ def scene3d():
                 grad=po.grad.detach(), tie_pix=tie_pix, racy=racy)
 
 
-@pytest.mark.parametrize("layout,entries,lanes", [(1, 128, 0), (1, 128, 4), (1, 256, 0), (2, 128, 0)],
-                         ids=["k_raster_bwd", "k_raster_bwd_box_masks", "k_raster_bwd_multi", "k_raster_bwd_pair3d"])
+@pytest.mark.parametrize("layout,entries,lanes", [(1, 128, 0), (1, 128, 4), (1, 256, 0), (2, 128, 0), (2, 128, 4)],
+                         ids=["k_raster_bwd", "k_raster_bwd_box_masks", "k_raster_bwd_multi", "k_raster_bwd_pair3d",
+                              "k_raster_bwd_pair3d_box_masks"])
 def test_race_3d(cuda, scene3d, layout, entries, lanes):
     """lanes 4: the quad forward, whose box masks the backward lists its boxes from (ABI 14);
     the fixture's small views otherwise take the 16-lane forward, which writes none."""
