@@ -325,6 +325,9 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const float* __restrict__
 // 4), so 2048 of them overflow the stage and fell back to the scattered writes (2.1 ms at
 // config 4): index-order (2D) emission takes 1024 per workgroup (GPT = 1).
 constexpr int kStageThreads = 1024;
+#ifndef GSR_EMIT_GPT
+#define GSR_EMIT_GPT 3   // 3D Gaussians per thread of the staged emission (2 or 3)
+#endif
 constexpr int kStageCap = 6144;          // staged entries (16 B each)
 constexpr size_t kStageLds = (size_t)kStageCap * 16;
 // cursor + offset per tile (8 B each) in what is left of the 160 KB of LDS after the stage and
@@ -341,13 +344,13 @@ __global__ __launch_bounds__(kStageThreads) void k_emit_staged(
     const int32_t* __restrict__ isect_offset,
     int64_t N, int tw, int th, int order, const int32_t* __restrict__ tile_offset, int32_t* __restrict__ tile_count,
     uint64_t* __restrict__ keys, int32_t* __restrict__ k_of_slot, gsr_bin_stats* __restrict__ stats,
-    int64_t cap) {
+    int64_t cap, int stage_cap) {
   constexpr int NT = kStageThreads;
   constexpr int kStagePer = GPT * NT;   // Gaussians per workgroup
-  extern __shared__ uint64_t s_key[];   // [kStageCap]
-  int32_t* s_kos = (int32_t*)(s_key + kStageCap);
-  int32_t* s_slot = s_kos + kStageCap;
-  int* cur = s_slot + kStageCap;        // [T] local cursor (starts at the tile's local offset)
+  extern __shared__ uint64_t s_key[];   // [stage_cap]
+  int32_t* s_kos = (int32_t*)(s_key + stage_cap);
+  int32_t* s_slot = s_kos + stage_cap;
+  int* cur = s_slot + stage_cap;        // [T] local cursor (starts at the tile's local offset)
   const int T = tw * th;
   int* delta = cur + T;                 // [T] global slot - local position
   __shared__ int s_tmp[NT / 64 + 1];
@@ -421,7 +424,7 @@ __global__ __launch_bounds__(kStageThreads) void k_emit_staged(
     }
   }
   __syncthreads();
-  const bool staged = total <= kStageCap;   // uniform: else scatter directly (huge rects)
+  const bool staged = total <= stage_cap;   // uniform: else scatter directly (huge rects)
 #pragma unroll
   for (int j = 0; j < GPT; ++j) {
     const int x0 = rr[j].x & 0xffff, x1 = rr[j].x >> 16, y0 = rr[j].y & 0xffff, y1 = rr[j].y >> 16;
@@ -1561,18 +1564,25 @@ int gsr_bin_emit(const float* depth, const float* rec, const uint32_t* rect, con
   const int use_lds = T <= kHistMaxTiles;
   // staged when it fills the chip with its 1024-thread workgroups (config 2's 25 would leave
   // most CUs idle: 7.3 us scattered vs 9.8 us staged; config 3 30 -> 27 us, config 5 450 -> 230 us)
-  const int gpt = order == GSR_ORDER_INDEX ? 1 : 2;   // Gaussians per thread (see k_emit_staged)
+  // 3D: GSR_EMIT_GPT Gaussians per thread, the stage sized by the LDS the camera's tile counters
+  // leave (fewer, larger workgroups claim fewer (workgroup, tile) ranges with returning atomics)
+  const int gpt = order == GSR_ORDER_INDEX ? 1 : GSR_EMIT_GPT;   // Gaussians per thread (see k_emit_staged)
   const int64_t per = (int64_t)gpt * kStageThreads;
   if (T <= kStageMaxTiles && g_emit_staged && ceil_div(N, per) * C >= 256) {
-    const size_t lds = kStageLds + (size_t)2 * T * sizeof(int);
+    const int stage_cap = gpt == 3 ? (int)((kLdsBytes - kStageStaticLds - 8 * T) / 16) : kStageCap;
+    const size_t lds = (size_t)stage_cap * 16 + (size_t)2 * T * sizeof(int);
     if (gpt == 1)
       hipLaunchKernelGGL(k_emit_staged<1>, dim3(ceil_div(N, per), C), dim3(kStageThreads), lds, (hipStream_t)stream,
                          depth, (const Splat*)rec, (const uint2*)rect, isect_offset, N, tw, th, order, tile_offset, tile_count, w.keys,
-                         w.k_of_slot, stats, cap);
+                         w.k_of_slot, stats, cap, stage_cap);
+    else if (gpt == 3)
+      hipLaunchKernelGGL(k_emit_staged<3>, dim3(ceil_div(N, per), C), dim3(kStageThreads), lds, (hipStream_t)stream,
+                         depth, (const Splat*)rec, (const uint2*)rect, isect_offset, N, tw, th, order, tile_offset, tile_count, w.keys,
+                         w.k_of_slot, stats, cap, stage_cap);
     else
       hipLaunchKernelGGL(k_emit_staged<2>, dim3(ceil_div(N, per), C), dim3(kStageThreads), lds, (hipStream_t)stream,
                          depth, (const Splat*)rec, (const uint2*)rect, isect_offset, N, tw, th, order, tile_offset, tile_count, w.keys,
-                         w.k_of_slot, stats, cap);
+                         w.k_of_slot, stats, cap, stage_cap);
     GSR_LAUNCH_CHECK("k_emit_staged");
     return GSR_OK;
   }
