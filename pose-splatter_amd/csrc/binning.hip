@@ -1018,11 +1018,13 @@ constexpr int kMsdRegs = 32;
 template <int NT>
 __device__ __forceinline__ void msd_partition_regs(SortGroup<NT>& g, const uint64_t* __restrict__ seg, int len,
                                                    int* s_hist, int* s_dstart, unsigned* s_or, int* s_maxb,
-                                                   uint64_t* __restrict__ part, int lds_keys) {
+                                                   uint64_t* __restrict__ part, int lds_keys, int lazy_prefix) {
   constexpr int W = NT / 64;
   static_assert(W == 16, "digit totals below: 16 per-wave counters per digit = one lane quad");
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   for (int i = lane; i < 256; i += 64) s_hist[wv * 256 + i] = 0;
+  int* const s_cut = s_hist + W * 256 + 40;   // (a free word of the misc ints)
+  if (tid == 0) *s_cut = 256;
   const uint32_t w0 = sort_word(seg[0]);
   uint32_t w[kMsdRegs];
 #pragma unroll
@@ -1066,12 +1068,23 @@ __device__ __forceinline__ void msd_partition_regs(SortGroup<NT>& g, const uint6
   if (lane == 0) atomicMax(s_maxb, mb);
   if (tid == 0) s_dstart[256] = len;
   __syncthreads();
+  // a lazily sorted list (lazy_prefix > 0): the walk sorts only the buckets up to the one that
+  // reaches the prefix, as ONE group when they fit in LDS -- the other keys are never read, so
+  // they are not written (config 5: ~5k of a 29k-key list)
+  int dlim = 256;
+  if (lazy_prefix > 0) {
+    if (tid < 256 && s_dstart[tid] < lazy_prefix && s_dstart[tid + 1] >= lazy_prefix) *s_cut = tid + 1;
+    __syncthreads();
+    const int dn = *s_cut;
+    if (s_dstart[dn] <= lds_keys) dlim = dn;
+  }
   if (*s_maxb <= lds_keys) {
 #pragma unroll
     for (int j = 0; j < kMsdRegs; ++j) {
       const int i = tid + j * NT;
-      if (i < len) {
-        const int pos = atomicAdd(&s_hist[wv * 256 + ((w[j] >> sh) & 0xFFu)], 1);
+      const int d = (w[j] >> sh) & 0xFFu;
+      if (i < len && d < dlim) {
+        const int pos = atomicAdd(&s_hist[wv * 256 + d], 1);
         part[pos] = ((uint64_t)w[j] << 32) | (uint64_t)(uint32_t)i;
       }
     }
@@ -1239,7 +1252,8 @@ __global__ __launch_bounds__(NT) void k_segsort(
 #if GSR_MSD_REGS
     if constexpr (NT == 1024) {
       if (len <= kMsdRegs * NT) {
-        msd_partition_regs<NT>(g, seg, len, s_hist, s_dstart, &s_or, &s_maxb, tmpk + start, lds_keys);
+        msd_partition_regs<NT>(g, seg, len, s_hist, s_dstart, &s_or, &s_maxb, tmpk + start, lds_keys,
+                               lazy ? lz.prefix : 0);
         in_regs = true;
       }
     }
