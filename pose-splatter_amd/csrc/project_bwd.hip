@@ -151,11 +151,13 @@ __global__ __launch_bounds__(kBwdThreads, GSR_PBWD_MINB) void k_project3d_bwd(
       // us).  (Issuing all four cut keys and rows of a round unconditionally -- an entry without
       // a row reading another one -- was slower: 55 -> 81 us.  This kernel is bound by its memory
       // instructions, not only by their latency, so masked-off loads are worth their branches.)
-      const int cnt = isect_count[cn];
+      // (the entry count is the rect's area, as the forward wrote it: isect_count is not read,
+      // 4 B less per (c,n) -- 48 MB of the config-5 launch's traffic)
       const uint2 rc = rect[cn];
       const int off = isect_offset[cn];
       const uint64_t key = sort_key(depth, cn, GSR_ORDER_DEPTH);
-      asm volatile("" ::"v"(cnt), "v"(rc.x), "v"(rc.y), "v"(off), "v"((uint32_t)(key >> 32)));
+      asm volatile("" ::"v"(rc.x), "v"(rc.y), "v"(off), "v"((uint32_t)(key >> 32)));
+      const int cnt = (int)(((rc.x >> 16) - (rc.x & 0xffffu)) * ((rc.y >> 16) - (rc.y & 0xffffu)));
       if (cnt <= 0 || ovf) continue;
       float acc[kPartial];
 #pragma unroll
