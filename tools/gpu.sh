@@ -24,7 +24,7 @@ show() {  # file label
   python3 -c "
 import json; d = json.loads(open('$1').read().strip().splitlines()[-1])
 k = d.get('kernels_ms', {})
-print('$2', round(d['value'], 1), round(d['ms_per_step'], 4), 'ms', {x: k[x] for x in k if 'raster' in x or 'proj' in x})"
+print('$2', round(d['value'], 1), round(d['ms_per_step'], 4), 'ms', k)"
 }
 steps() { case $1 in 4) echo "--steps 8 --warmup 2";; 5) echo "--steps 20 --warmup 3";; *) echo "--steps 40 --warmup 5";; esac; }
 for step in "$@"; do
