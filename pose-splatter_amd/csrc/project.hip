@@ -21,7 +21,10 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
-constexpr int kProjThreads = 256;
+#ifndef GSR_PROJ_THREADS
+#define GSR_PROJ_THREADS 256
+#endif
+constexpr int kProjThreads = GSR_PROJ_THREADS;
 #ifndef GSR_PROJ_PER_BLOCK
 #define GSR_PROJ_PER_BLOCK 1024
 #endif
