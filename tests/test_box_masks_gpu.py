@@ -93,3 +93,29 @@ def test_masks_need_quad_forward(cuda):
         assert not b2.pre.view("stats_dev", torch.int32).tolist()[_masks_word()] & 4
     assert torch.equal(alpha1.cpu(), alpha2.cpu())
     assert_close(rgb1.cpu(), rgb2.cpu(), rtol=0, atol=0, what="rgb")
+
+
+@pytest.mark.parametrize("layout", [1, 2], ids=["k_raster_bwd", "k_raster_bwd_pair3d"])
+def test_box_masks_with_lazy_rerun(cuda, layout):
+    """A lazily sorted list whose walk reaches the end of its sorted prefix is re-sorted whole and
+    its tile rendered again (gsr3d_raster_fwd_lazy): the second walk must rewrite that tile's box
+    masks for the final order.  The sort-class scene (lists of 1 023 to 8 192 entries) with lazy
+    prefixes of 256 entries re-renders tiles; its gradients must equal the whole sort's bit for
+    bit in both chunk layouts (the lists, and so the masks, are the same)."""
+    from gsr import render as R
+    from test_sort_classes_gpu import W as SW, H as SH, _lazy, _scene, _step
+    p, V, K = (x.to(cuda) for x in _scene())
+    with forced_bwd_layout(layout), forced_fwd_lanes(4):
+        with _lazy(0, 4096):   # every list sorted whole
+            ref = _step(p, V, K)
+        with _lazy(1023, 256):
+            _, _, b, _ = R.debug_forward3d(p, V, K, torch.ones(3, device=cuda), SW, SH)
+            st = b.pre.view("stats_dev", torch.int32).tolist()
+            assert st[_masks_word()] & 4, "the forward wrote no box masks"
+            reran = int(b.pre.view("lazy", torch.int32)[3 * b.CT].item())
+            print(f"[box masks, lazy, layout {layout}] {reran} tile(s) re-rendered after a whole re-sort")
+            assert reran > 0, "no tile reached the end of its sorted prefix"
+            lz = _step(p, V, K)
+    for x, y, what in zip(ref, lz, ("rgb", "alpha", "grad")):
+        assert torch.equal(x, y), what
+    R.check_overflow(cuda)
