@@ -257,7 +257,9 @@ int gsr_selftest_lds_order(int32_t* violations, void* stream);
  * 6:10, colour 10:13, opacity 13).  input_mode GSR_INPUT_ADAPTER: raw values through the
  * adapter's activations; GSR_INPUT_GSPLAT: activated values as gsplat's rasterization()
  * takes them (no exp/sigmoid/clamp; the quaternion is only renormalised).  viewmats [C,4,4] world->cam
- * row-major; Ks [C,3,3].  Writes rec [C*N*12], depth [C*N], rect [C*N*2], isect_count [C*N],
+ * row-major; Ks [C,3,3].  Writes rec [C*N*12], depth [C*N], rect [C*N*2], isect_count [C*N]
+ * (optional: NULL writes no counts -- a count is its rect's area, (x1-x0)*(y1-y0), and no 3D
+ * kernel reads it; 4 of the 68 bytes written per (c,n)),
  * isect_offset [C*N] (the first emission entry of each (c,n): every workgroup claims one
  * contiguous range for its items with one atomic, so the (c,n) ranges tile [0, I) in
  * workgroup arrival order -- consumers only address rows through isect_offset) and
@@ -492,7 +494,8 @@ int gsr2d_raster_bwd(const float* rec, const int32_t* sorted_ids, const int32_t*
  * Gaussian ranges let a multi-GPU caller start the all-reduce of finished rows while later
  * ranges are still being computed.  depth: the projection's depth array (sort keys).
  * stats: the forward's device gsr_bin_stats (may be NULL): with stats->overflow set the rows
- * are written as NaN. */
+ * are written as NaN.  isect_count is not read (each entry count is its rect's area; may be
+ * NULL). */
 int gsr3d_project_bwd(const float* params, int64_t N, int64_t row_stride,
                       const float* viewmats, const float* Ks, int C, int width, int height,
                       float eps2d, int input_mode, const float* depth, const uint32_t* rect,

@@ -201,7 +201,9 @@ __global__ __launch_bounds__(kProjThreads) void k_project3d_fwd(
       hist_add(hist, gcount, use_lds, x0, x1, y0, y1, tw);
     }
     rect[cn] = make_uint2(pack_rect_lo(x0, x1), pack_rect_lo(y0, y1));
-    cnt[cn] = s_cnt[n - n0] = (x1 - x0) * (y1 - y0);
+    // (the count is the rect's area: an optional output, 4 of the 68 B written per pair)
+    s_cnt[n - n0] = (x1 - x0) * (y1 - y0);
+    if (cnt != nullptr) cnt[cn] = s_cnt[n - n0];
   }
   if (use_lds) hist_flush(hist, gcount, T);
   alloc_offsets<ITEMS>(s_cnt, (int)(n1 - n0), (int64_t)c * N + n0, counter, isect_offset);

@@ -567,6 +567,13 @@ class _Bins:
 
     def __getattr__(self, name):
         # typed views of arena buffers (not used on the hot path)
+        if name == "cnt" and self.__dict__.get("box_masks"):
+            # 3D: the projection does not write the counts (include/gsr.h: optional); each
+            # (camera, Gaussian)'s entry count is its tile rect's area
+            r = self.pre.view("rect", torch.int32).view(-1, 2).to(torch.int64) & 0xFFFFFFFF
+            w = (r[:, 0] >> 16) - (r[:, 0] & 0xFFFF)
+            h = (r[:, 1] >> 16) - (r[:, 1] & 0xFFFF)
+            return (w * h).to(torch.int32)
         if name in _VIEWS:
             where, dt = _VIEWS[name]
             arena = self.__dict__.get(where)
@@ -775,7 +782,8 @@ def _forward3d(params, viewmats, Ks, bg, width, height, opts, need_bwd=True, ret
       check(L.gsr3d_project_fwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height,
                               opts.near_plane, opts.far_plane, opts.radius_clip, opts.eps2d,
                               opts.radius_mode, opts.input_mode, opts.band[0], opts.band[1], q["rec"], q["depth"],
-                              q["rect"], q["cnt"], q["isect_off"], q["tile_cnt"], b.take_tile_counts(), stream),
+                              q["rect"], q["cnt"] if _counts3d else None, q["isect_off"], q["tile_cnt"],
+                              b.take_tile_counts(), stream),
           "gsr3d_project_fwd")
     b.guess_post(with_chunks=need_bwd)
     b.offsets_launch(stream)
@@ -889,6 +897,11 @@ def _forward2d(params, bg, width, height, eps_cut, unit_sets=(0,), capacity=None
     return rgb, alpha, b, (p, F, stride, set_stride, sb, bgc, width, height, eps_cut)
 
 
+# measurement hook: the 3D projection also writes isect_count (a (camera, Gaussian)'s entry count
+# is its rect's area; no 3D kernel reads the counts, so the product path passes NULL)
+_counts3d = False
+
+
 def debug_forward3d(params, viewmats, Ks, bg, width, height, opts=None):
     """Test hook: the forward plus all binning intermediates (no autograd)."""
     return _forward3d(params, viewmats, Ks, bg, width, height, opts or RenderOptions3D())
@@ -955,7 +968,7 @@ def backward3d(b, meta, raster) -> torch.Tensor:
             with _timed("project3d_bwd"):
               check(L.gsr3d_project_bwd(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height, opts.eps2d,
                                         opts.input_mode,
-                                        q["depth"], q["rect"], q["isect_off"], q["cnt"], q["tile_cut"],
+                                        q["depth"], q["rect"], q["isect_off"], None, q["tile_cut"],
                                         _ptr(partial), n0, n1, q["stats_dev"], _ptr(v_params), stream),
                     "gsr3d_project_bwd")
             if opts.grad_hook is not None:
@@ -983,7 +996,7 @@ def _backward3d_rows(L, b, meta, raster, stream) -> None:
         raster(L, q, partial, stream)
     with _timed("project3d_bwd"):
         check(L.gsr3d_project_bwd_rows(_ptr(p), N, stride, _ptr(V), _ptr(Kc), C, width, height, opts.eps2d,
-                                       opts.input_mode, q["depth"], q["rect"], q["isect_off"], q["cnt"],
+                                       opts.input_mode, q["depth"], q["rect"], q["isect_off"], None,
                                        q["tile_cut"], _ptr(partial), q["stats_dev"], rows.cap,
                                        rows.block.data_ptr(), stream), "gsr3d_project_bwd_rows")
     return None
