@@ -867,8 +867,13 @@ def time_steps(w: Workload, steps: int, warmup: int, dist=None, graph: bool = Fa
         # in rocm"): the dominant kernel is timed with HIP events around each of its launches
         # on its stream over the same number of eager bounded steps (no host sync between
         # them), right after the graph-timed region -- the same kernel on the same inputs
+        # Each step starts behind a short GPU spin (torch.cuda._sleep, ~1 ms) so that the host has
+        # queued the whole step before the GPU reaches it: without it, a launch whose Python-side
+        # preparation outlasts the GPU's queue (the backward after autograd's bookkeeping) is timed
+        # from its start event across the host gap (config 3: 124 vs 113.6 us by rocprof).
         R.enable_kernel_timing(True, only={dom_name} if dom_name else None)
         for _ in range(steps):
+            torch.cuda._sleep(KTIMING_SPIN_CYCLES)
             w.step()
         torch.cuda.synchronize()
     ktimes = R.kernel_times_ms()
@@ -876,6 +881,9 @@ def time_steps(w: Workload, steps: int, warmup: int, dist=None, graph: bool = Fa
     R.check_overflow(w.dev)   # a bounded step over its bounds would have rendered NaN: fail loudly
     del g
     return elapsed, breakdown, dom_name, ktimes.get(dom_name, (0.0, 0)) if dom_name else (0.0, 0)
+
+
+KTIMING_SPIN_CYCLES = 2_000_000   # GPU clock cycles spun before each kernel-timing step
 
 
 def time_eager(w, steps: int, dist=None) -> float:
@@ -952,7 +960,8 @@ def roofline(w: Workload, dom_name, dom, args):
             "algorithmic_bytes": alg, "avg_ms": dom_ms, "launches": dom_n,
             "timing": ("HIP events around each launch on its stream, over the timed steps" if not args.graph else
                        "HIP events around each launch on its stream, over as many eager bounded steps run right "
-                       "after the graph-timed region (ROCm rejects timing events inside a captured graph)"),
+                       "after the graph-timed region (ROCm rejects timing events inside a captured graph), each "
+                       "step queued behind a short GPU spin so no host gap falls inside a timed launch"),
             "valu": valu,
             "units_per_launch": {"C": C, "P": P, "N": cfg.N, "I": I, "I_eff": I_eff}}, (C, P, I, I_eff)
 
