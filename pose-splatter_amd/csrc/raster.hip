@@ -21,7 +21,7 @@ constexpr int kRasterThreads = 256;
 constexpr int kChunk3 = GSR_CHUNK;   // backward work unit: list entries per chunk
 constexpr int kFillBlocks = 1024;    // workgroups that fill the empty tiles
 #ifndef GSR_FWD_PAD_3D
-#define GSR_FWD_PAD_3D 0   // 3D shared rounds (~28 KB LDS): 5 per CU measured best (4 per CU: +10 us)
+#define GSR_FWD_PAD_3D 0   // 3D quad rounds (26.4 KB LDS: 6 per CU): padded to 5 per CU +2 us, to 4 per CU +12 us (round 6, profiles/r06_ab_fwd_pad.txt)
 #endif
 constexpr int kFwdLdsPad = GSR_FWD_PAD_3D;
 #ifndef GSR_FWD_PAD_2D
